@@ -1,0 +1,94 @@
+"""Loader for the sbk C-ABI shared library (HIP kernels for gfx950).
+
+The library is built in-tree by `speechbrain_amd._build.build()` (or
+`__graft_entry__.build()`) into `speechbrain_amd/libsbk.so`.  There is no CPU
+or PyTorch fallback: if the library is missing, or a tensor is not on a ROCm
+device, calls raise immediately.
+
+`import torch` must precede loading libsbk.so: torch's bundled
+libamdhip64.so (SONAME libamdhip64.so.7) is then the one that satisfies
+libsbk.so's dependency, so both share one HIP runtime, one device context
+and the same streams.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsbk.so")
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_ll = ctypes.c_longlong
+_f = ctypes.c_float
+
+# name -> argtypes (all functions return int: 0 = ok, else hipError_t / SBK_ERR_ARG)
+SIGNATURES = {
+    "sbk_fft_supported": [_i],
+    "sbk_spectrum": [_i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _i, _f, _f, _f, _i, _vp,
+                     _vp, _vp, _vp, _vp, _i, _i, _f, _f, _f, _vp, _vp, _vp],
+    "sbk_filterbank": [_vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _i, _i, _f, _f, _f, _vp, _vp, _vp],
+    "sbk_topdb_clamp": [_vp, _vp, _ll, _i, _f, _vp],
+    "sbk_magnitude": [_vp, _vp, _ll, _i, _f, _f, _i, _vp],
+    "sbk_dct": [_vp, _vp, _vp, _ll, _i, _i, _vp],
+    "sbk_deltas": [_vp, _vp, _i, _i, _i, _i, _i, _vp],
+    "sbk_context_window": [_vp, _vp, _i, _i, _i, _i, _i, _vp],
+}
+
+_lib = None
+_load_error = None
+
+
+class SbkError(RuntimeError):
+    pass
+
+
+def lib():
+    """Return the loaded ctypes library, raising loudly if it is unavailable."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SbkError(
+            f"speechbrain_amd HIP library not found at {LIB_PATH}; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950). "
+            "There is no CPU fallback.")
+    try:
+        l = ctypes.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover - depends on the box
+        _load_error = e
+        raise SbkError(f"failed to load {LIB_PATH}: {e}") from e
+    for name, argt in SIGNATURES.items():
+        fn = getattr(l, name)
+        fn.argtypes = argt
+        fn.restype = ctypes.c_int
+    _lib = l
+    return l
+
+
+def exported_symbols():
+    return list(SIGNATURES)
+
+
+def check(rc, what):
+    if rc != 0:
+        raise SbkError(f"{what} failed with code {rc}" + (" (invalid argument)" if rc == 1001 else ""))
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if t is not None and (not isinstance(t, torch.Tensor) or t.device.type != "cuda"):
+            raise SbkError("speechbrain_amd kernels need ROCm device tensors (got "
+                           f"{getattr(t, 'device', type(t))}); there is no CPU fallback")

@@ -1,0 +1,67 @@
+// Shared device helpers for the sbk (speechbrain-amd kernels) library.
+// gfx950 / CDNA4 only: wave64, 160 KiB LDS per CU, fp32 + bf16 MFMA.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define SBK_API extern "C" __attribute__((visibility("default")))
+
+#define SBK_CHECK_LAUNCH()                          \
+  do {                                              \
+    hipError_t _e = hipGetLastError();              \
+    if (_e != hipSuccess) return (int)_e;           \
+  } while (0)
+
+#define SBK_ERR_ARG 1001  // invalid argument (shape/config) detected on host
+
+namespace sbk {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// Monotone float <-> int32 key so that atomicMax on the key orders floats.
+__device__ __forceinline__ int float_to_key(float f) {
+  int i = __float_as_int(f);
+  return i >= 0 ? i : (i ^ 0x7FFFFFFF);
+}
+__device__ __forceinline__ float key_to_float(int k) {
+  return __int_as_float(k >= 0 ? k : (k ^ 0x7FFFFFFF));
+}
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) {
+  return __uint_as_float(((uint32_t)h) << 16);
+}
+// Round-to-nearest-even f32 -> bf16 (NaN handled by the hardware cvt path
+// where the compiler emits v_cvt_pk_bf16_f32).
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  __hip_bfloat16 b = __float2bfloat16(f);
+  return *reinterpret_cast<uint16_t*>(&b);
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+// Block-wide sum for blockDim.x a multiple of 64 (<= 1024). `red` >= 16 floats.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+  for (int i = 0; i < nw; ++i) s += red[i];
+  return s;
+}
+
+}  // namespace sbk

@@ -1,0 +1,275 @@
+"""Generate the golden fixtures under tests/golden/ from the REAL reference.
+
+Runs only in the build container (the reference at /root/reference never
+travels to the GPU box); the committed .npz files are what the tests read.
+
+    python tests/golden/gen_golden.py
+
+The reference imports three packages that are absent here and unused by the
+hot-path arithmetic (hyperpyyaml, torchaudio, ruamel.yaml), so
+they are replaced by inert stub modules before `import speechbrain`.  WAVs
+are read with the stdlib `wave` module and scaled by 1/32768, the same
+normalisation torchaudio.load applies (speechbrain/dataio/dataio.py:216-250).
+
+Fixture inventory (all float32 unless noted):
+  fbank_wavs.npz   Fbank(n_mels=80|40) on 3 tests/samples/ASR WAVs, single
+                   and zero-padded batch (lobes/features.py:82-147)
+  features.npz     STFT (mono + 3-channel), spectral_magnitude, Filterbank
+                   (3 shapes, log/linear, freeze=False + grads), DCT,
+                   Deltas, ContextWindow, MFCC, Fbank(deltas, context)
+                   (processing/features.py:50-937)
+  specaug.npz      SpecAugment outputs + every randint draw it made
+                   (lobes/augment.py:32-201)
+  conformer.npz    ConvolutionFrontEnd + TransformerASR.encode (Conformer,
+                   RelPosMHAXL) weights, inputs, outputs, attention maps,
+                   RelPosEncXL and rel_shift vectors
+                   (lobes/models/convolution.py, lobes/models/transformer/*,
+                   nnet/attention.py)
+The RNN-T known answer (tests/unittests/test_losses.py:109-152) needs numba
+and is pinned as a literal in tests/test_oracle_golden.py instead.
+"""
+import os
+import sys
+import types
+import wave
+
+import numpy as np
+
+sys.dont_write_bytecode = True
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _install_stubs():
+    def stub(name, **attrs):
+        m = types.ModuleType(name)
+        for k, v in attrs.items():
+            setattr(m, k, v)
+        sys.modules[name] = m
+        return m
+
+    def _raise(*a, **k):
+        raise RuntimeError("stubbed dependency")
+
+    ta = stub("torchaudio", set_audio_backend=lambda *a, **k: None,
+              load=_raise, save=_raise, info=_raise)
+    ta.transforms = stub("torchaudio.transforms")
+    ta.functional = stub("torchaudio.functional")
+    stub("hyperpyyaml", resolve_references=_raise, load_hyperpyyaml=_raise)
+    r = stub("ruamel")
+    r.yaml = stub("ruamel.yaml", YAML=_raise)
+    sys.path.insert(0, REF)
+
+
+_install_stubs()
+import torch  # noqa: E402
+
+torch.set_num_threads(8)
+
+from speechbrain.processing import features as F  # noqa: E402
+from speechbrain.lobes import features as LF  # noqa: E402
+from speechbrain.lobes.augment import SpecAugment  # noqa: E402
+from speechbrain.lobes.models.convolution import ConvolutionFrontEnd  # noqa: E402
+from speechbrain.lobes.models.transformer.TransformerASR import TransformerASR  # noqa: E402
+from speechbrain.lobes.models.transformer.Conformer import ConformerEncoder  # noqa: E402
+from speechbrain.nnet.attention import RelPosEncXL, RelPosMHAXL  # noqa: E402
+
+
+def read_wav(name):
+    w = wave.open(os.path.join(REF, "tests/samples/ASR", name + ".wav"))
+    assert w.getsampwidth() == 2 and w.getnchannels() == 1
+    pcm = np.frombuffer(w.readframes(w.getnframes()), dtype="<i2")
+    return pcm
+
+
+def t2n(x):
+    return x.detach().cpu().numpy().astype(np.float32)
+
+
+def gen_fbank_wavs():
+    names = ["spk2_snt2", "spk2_snt6", "spk2_snt3"]
+    out = {}
+    pcms = [read_wav(n) for n in names]
+    L = max(len(p) for p in pcms)
+    batch = np.zeros((len(pcms), L), np.float32)
+    for i, p in enumerate(pcms):
+        out[f"pcm{i}"] = p.astype(np.int16)
+        batch[i, : len(p)] = p.astype(np.float32) / 32768.0
+    for n_mels in (80, 40):
+        fb = LF.Fbank(n_mels=n_mels)
+        fb.eval()
+        with torch.no_grad():
+            for i, p in enumerate(pcms):
+                wav = torch.from_numpy(p.astype(np.float32) / 32768.0)[None]
+                out[f"fbank{n_mels}_single{i}"] = t2n(fb(wav))
+            out[f"fbank{n_mels}_batch"] = t2n(fb(torch.from_numpy(batch)))
+    np.savez_compressed(os.path.join(OUT, "fbank_wavs.npz"), **out)
+
+
+def gen_features():
+    out = {}
+    g = torch.Generator().manual_seed(0)
+    x = 0.1 * torch.randn(2, 16000, generator=g)
+    x3 = 0.1 * torch.randn(2, 4000, 3, generator=g)
+    out["x"] = t2n(x)
+    out["x3"] = t2n(x3)
+    stft = F.STFT(sample_rate=16000)
+    s = stft(x)
+    out["stft"] = t2n(s)
+    out["stft3"] = t2n(stft(x3))
+    # non-default STFT geometry: 20 ms window, 5 ms hop, n_fft 512, reflect pad
+    stft_b = F.STFT(sample_rate=16000, win_length=20, hop_length=5, n_fft=512,
+                    pad_mode="reflect")
+    out["stft_b"] = t2n(stft_b(x))
+    mag = F.spectral_magnitude(s)
+    out["mag_p1"] = t2n(mag)
+    out["mag_p05"] = t2n(F.spectral_magnitude(s, power=0.5))
+    out["mag_log"] = t2n(F.spectral_magnitude(s, power=1, log=True))
+    for shape in ("triangular", "rectangular", "gaussian"):
+        fbm = F.Filterbank(n_mels=40, filter_shape=shape)
+        out[f"fb_{shape}"] = t2n(fbm(mag))
+    out["fb_lin"] = t2n(F.Filterbank(n_mels=23, log_mel=False)(mag))
+    out["fb_80"] = t2n(F.Filterbank(n_mels=80)(mag))
+    out["fb_fmin_fmax"] = t2n(F.Filterbank(n_mels=40, f_min=100, f_max=7000)(mag))
+    # learnable filterbank: forward + grads of sum() wrt f_central/band
+    fbl = F.Filterbank(n_mels=40, freeze=False)
+    y = fbl(mag)
+    y.sum().backward()
+    out["fb_learn"] = t2n(y)
+    out["fb_learn_grad_fc"] = t2n(fbl.f_central.grad)
+    out["fb_learn_grad_band"] = t2n(fbl.band.grad)
+    # multichannel filterbank (B,T,F,C)
+    out["fb_multi"] = t2n(F.Filterbank(n_mels=40)(F.spectral_magnitude(stft(x3))))
+    fbank40 = out["fb_triangular"]
+    dct = F.DCT(input_size=40, n_out=20)
+    d = dct(torch.from_numpy(fbank40))
+    out["dct"] = t2n(d)
+    out["dct_noortho"] = t2n(F.DCT(input_size=40, n_out=13, ortho_norm=False)(torch.from_numpy(fbank40)))
+    deltas = F.Deltas(input_size=20)
+    d1 = deltas(d)
+    out["delta1"] = t2n(d1)
+    out["delta2"] = t2n(deltas(d1))
+    out["delta_w7"] = t2n(F.Deltas(input_size=20, window_length=7)(d))
+    for lf, rf in ((5, 5), (0, 2), (3, 1), (0, 0)):
+        cw = F.ContextWindow(left_frames=lf, right_frames=rf)
+        out[f"cw_{lf}_{rf}"] = t2n(cw(d))
+    mf = LF.MFCC()
+    out["mfcc"] = t2n(mf(x))
+    fbdc = LF.Fbank(n_mels=40, deltas=True, context=True, left_frames=2, right_frames=2)
+    out["fbank_dc"] = t2n(fbdc(x))
+    np.savez_compressed(os.path.join(OUT, "features.npz"), **out)
+
+
+def gen_specaug():
+    """Run the reference SpecAugment, recording every torch.randint draw."""
+    out = {}
+    g = torch.Generator().manual_seed(123)
+    feats = torch.randn(4, 150, 80, generator=g)
+    out["feats"] = t2n(feats)
+    real_randint = torch.randint
+    draws = []
+
+    def rec_randint(*a, **k):
+        r = real_randint(*a, **k)
+        draws.append(r.detach().cpu().numpy().reshape(-1).astype(np.int64))
+        return r
+
+    configs = {
+        # conformer_small.yaml:252-262
+        "recipe": dict(time_warp=True, time_warp_window=5, time_warp_mode="bicubic",
+                       freq_mask=True, n_freq_mask=2, time_mask=True, n_time_mask=2,
+                       replace_with_zero=False, freq_mask_width=30, time_mask_width=40),
+        "default": dict(),
+        "nowarp": dict(time_warp=False, freq_mask_width=(5, 15), time_mask_width=(10, 20),
+                       n_freq_mask=3, n_time_mask=1),
+    }
+    torch.randint = rec_randint
+    try:
+        for name, cfg in configs.items():
+            for seed in range(4):
+                aug = SpecAugment(**cfg)
+                torch.manual_seed(seed)
+                draws.clear()
+                y = aug(feats.clone())
+                out[f"{name}_s{seed}"] = t2n(y)
+                out[f"{name}_s{seed}_draws"] = np.concatenate(draws)
+    finally:
+        torch.randint = real_randint
+    # time-warp only, to pin the bicubic resample in isolation
+    aug = SpecAugment(time_warp=True, freq_mask=False, time_mask=False)
+    for seed in range(4):
+        torch.manual_seed(100 + seed)
+        out[f"warp_s{seed}"] = t2n(aug(feats.clone()))
+    np.savez_compressed(os.path.join(OUT, "specaug.npz"), **out)
+
+
+def gen_conformer():
+    out = {}
+    torch.manual_seed(0)
+    # recipe front-end (conformer_small.yaml:123-130)
+    cnn = ConvolutionFrontEnd(input_shape=(8, 10, 80), num_blocks=2, num_layers_per_block=1,
+                              out_channels=(64, 32), kernel_sizes=(3, 3), strides=(2, 2),
+                              residuals=(False, False))
+    tr = TransformerASR(tgt_vocab=10, input_size=640, d_model=64, nhead=4,
+                        num_encoder_layers=2, num_decoder_layers=0, d_ffn=128,
+                        dropout=0.0, encoder_module="conformer",
+                        attention_type="RelPosMHAXL", normalize_before=True,
+                        causal=False)
+    cnn.eval()
+    tr.eval()
+    for k, v in cnn.state_dict().items():
+        out["cnn." + k] = t2n(v)
+    for k, v in tr.state_dict().items():
+        out["tr." + k] = t2n(v)
+    g = torch.Generator().manual_seed(1)
+    feats = torch.randn(2, 101, 80, generator=g)
+    wav_len = torch.tensor([1.0, 0.8])
+    out["feats"] = t2n(feats)
+    out["wav_len"] = t2n(wav_len)
+    with torch.no_grad():
+        c = cnn(feats)
+        out["cnn_out"] = t2n(c)
+        out["enc_out"] = t2n(tr.encode(c, wav_len))
+        out["enc_out_nolen"] = t2n(tr.encode(c))
+    # ConformerEncoder directly: returns attention maps too
+    torch.manual_seed(2)
+    enc = ConformerEncoder(num_layers=2, d_model=64, d_ffn=128, nhead=4, kernel_size=31)
+    enc.eval()
+    for k, v in enc.state_dict().items():
+        out["enc." + k] = t2n(v)
+    src = torch.randn(3, 37, 64, generator=g)
+    kpm = torch.arange(37)[None, :] >= torch.tensor([37, 30, 21])[:, None]
+    pe = RelPosEncXL(64)(src)
+    out["enc_src"] = t2n(src)
+    out["enc_kpm"] = kpm.numpy()
+    out["enc_pos"] = t2n(pe)
+    with torch.no_grad():
+        y, attn = enc(src, src_key_padding_mask=kpm, pos_embs=pe)
+    out["enc_y"] = t2n(y)
+    for i, a in enumerate(attn):
+        out[f"enc_attn{i}"] = t2n(a)
+    # causal conformer (ConvolutionModule chomp; Conformer.py:62-66,108-110)
+    torch.manual_seed(3)
+    encc = ConformerEncoder(num_layers=1, d_model=64, d_ffn=96, nhead=2, kernel_size=7, causal=True)
+    encc.eval()
+    for k, v in encc.state_dict().items():
+        out["encc." + k] = t2n(v)
+    with torch.no_grad():
+        yc, _ = encc(src, pos_embs=pe)
+    out["encc_y"] = t2n(yc)
+    # rel_shift pin: out[i,j] = bd[i, T-1-i+j]
+    mha = RelPosMHAXL(embed_dim=64, num_heads=4)
+    bd = torch.randn(1, 2, 5, 9, generator=g)
+    out["relshift_in"] = t2n(bd)
+    out["relshift_out"] = t2n(mha.rel_shift(bd))
+    np.savez_compressed(os.path.join(OUT, "conformer.npz"), **out)
+
+
+if __name__ == "__main__":
+    gen_fbank_wavs()
+    gen_features()
+    gen_specaug()
+    gen_conformer()
+    for f in sorted(os.listdir(OUT)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(OUT, f)))

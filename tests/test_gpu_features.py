@@ -1,0 +1,169 @@
+"""HIP feature kernels vs the golden fixtures and the CPU oracle (parity)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import assert_close
+import oracle.features as OF
+
+pytestmark = pytest.mark.gpu
+
+
+def _mods():
+    from speechbrain_amd.processing import features as F
+    from speechbrain_amd.lobes import features as LF
+    return F, LF
+
+
+def test_stft_vs_golden(golden, dev):
+    F, _ = _mods()
+    g = golden("features")
+    x, x3 = torch.from_numpy(g["x"]).to(dev), torch.from_numpy(g["x3"]).to(dev)
+    st = F.STFT(sample_rate=16000)
+    s = st(x)
+    assert_close(s, g["stft"], name="stft")
+    assert_close(st(x3), g["stft3"], name="stft3")
+    stb = F.STFT(sample_rate=16000, win_length=20, hop_length=5, n_fft=512, pad_mode="reflect")
+    assert_close(stb(x), g["stft_b"], name="stft_b")
+    assert_close(F.spectral_magnitude(s), g["mag_p1"], name="mag")
+    assert_close(F.spectral_magnitude(s, power=0.5), g["mag_p05"], name="mag05")
+    assert_close(F.spectral_magnitude(s, power=1, log=True), g["mag_log"], rtol=2e-4, name="maglog")
+    # fused STFT→power equals the two-step path
+    assert_close(st.power_spectrum(x), g["mag_p1"], name="fused power")
+
+
+@pytest.mark.parametrize("n_fft,hop,center,pad", [(400, 160, True, "constant"), (512, 128, True, "reflect"),
+                                                    (256, 100, False, "constant"), (480, 160, True, "replicate"),
+                                                    (384, 96, True, "circular")])
+def test_stft_geometries_vs_oracle(dev, n_fft, hop, center, pad):
+    F, _ = _mods()
+    g = torch.Generator().manual_seed(n_fft)
+    x = 0.3 * torch.randn(3, 4001, generator=g)
+    ms_win, ms_hop = n_fft / 16.0, hop / 16.0
+    st = F.STFT(16000, win_length=ms_win, hop_length=ms_hop, n_fft=n_fft, center=center, pad_mode=pad)
+    ref = OF.stft(x, 16000, ms_win, ms_hop, n_fft, center=center, pad_mode=pad, compute_dtype=torch.float64)
+    out = st(x.to(dev))
+    scale = float(ref.abs().max())
+    assert_close(out / scale, ref / scale, rtol=2e-6, name=f"stft{n_fft}")
+    st2 = F.STFT(16000, win_length=ms_win, hop_length=ms_hop, n_fft=n_fft, center=center, pad_mode=pad,
+                 onesided=False, normalized_stft=True)
+    ref2 = OF.stft(x, 16000, ms_win, ms_hop, n_fft, normalized=True, center=center, pad_mode=pad, onesided=False,
+                   compute_dtype=torch.float64)
+    s2 = float(ref2.abs().max())
+    assert_close(st2(x.to(dev)) / s2, ref2 / s2, rtol=2e-6, name="twosided")
+
+
+@pytest.mark.parametrize("shape", ["triangular", "rectangular", "gaussian"])
+def test_filterbank_vs_golden(golden, dev, shape):
+    F, _ = _mods()
+    g = golden("features")
+    mag = torch.from_numpy(g["mag_p1"]).to(dev)
+    assert_close(F.Filterbank(n_mels=40, filter_shape=shape)(mag), g[f"fb_{shape}"], name=shape)
+
+
+def test_filterbank_variants_vs_golden(golden, dev):
+    F, _ = _mods()
+    g = golden("features")
+    mag = torch.from_numpy(g["mag_p1"]).to(dev)
+    assert_close(F.Filterbank(n_mels=23, log_mel=False)(mag), g["fb_lin"], name="lin")
+    assert_close(F.Filterbank(n_mels=80)(mag), g["fb_80"], name="80")
+    assert_close(F.Filterbank(n_mels=40, f_min=100, f_max=7000)(mag), g["fb_fmin_fmax"], name="fminmax")
+    x3 = torch.from_numpy(g["x3"]).to(dev)
+    st = F.STFT(sample_rate=16000)
+    assert_close(F.Filterbank(n_mels=40)(F.spectral_magnitude(st(x3))), g["fb_multi"], name="multi")
+    assert_close(F.Filterbank(n_mels=40, freeze=False)(mag), g["fb_learn"], name="learnable fwd")
+
+
+def test_filterbank_reference_unit_checks(dev):
+    """tests/unittests/test_features.py:60-88 on the HIP path."""
+    F, _ = _mods()
+    fb = F.Filterbank()
+    z = fb(torch.zeros(10, 101, 201, device=dev))
+    assert torch.equal(z, torch.full_like(z, -100.0))
+    i1 = torch.rand(1, 101, 201, device=dev) * 10
+    i2 = torch.rand(1, 101, 201, device=dev)
+    f1, f2, f3 = fb(i1), fb(i2), fb(torch.cat([i1, i2]))
+    assert torch.sum(torch.abs(f1[0] - f3[0])) < 8e-5
+    assert torch.sum(torch.abs(f2[0] - f3[1])) < 8e-5
+    assert torch.jit.trace(fb, torch.ones(10, 101, 201, device=dev))
+
+
+def test_dct_deltas_context_vs_golden(golden, dev):
+    F, _ = _mods()
+    g = golden("features")
+    fb40 = torch.from_numpy(g["fb_triangular"]).to(dev)
+    d = F.DCT(input_size=40)(fb40)
+    assert_close(d, g["dct"], name="dct")
+    assert_close(F.DCT(input_size=40, n_out=13, ortho_norm=False)(fb40), g["dct_noortho"], name="dct2")
+    deltas = F.Deltas(input_size=20)
+    d1 = deltas(d)
+    assert_close(d1, g["delta1"], name="d1")
+    assert_close(deltas(d1), g["delta2"], name="d2")
+    assert_close(F.Deltas(input_size=20, window_length=7)(d), g["delta_w7"], name="d7")
+    for lf, rf in ((5, 5), (0, 2), (3, 1), (0, 0)):
+        assert_close(F.ContextWindow(lf, rf)(d), g[f"cw_{lf}_{rf}"], rtol=0, name=f"cw{lf}{rf}")
+
+
+def test_deltas_context_reference_unit_checks(dev):
+    """tests/unittests/test_features.py:4-39."""
+    F, _ = _mods()
+    inp = torch.ones(10, 101, 20, device=dev)
+    d = F.Deltas(input_size=20)
+    assert torch.sum(d(inp) == 0) == inp.numel()
+    assert torch.jit.trace(d, inp)
+    cw = F.ContextWindow(left_frames=1, right_frames=1)
+    out = cw(torch.tensor([1.0, 2, 3], device=dev).view(1, 3, 1))
+    assert torch.equal(out, torch.tensor([[[0.0, 1, 2], [1, 2, 3], [2, 3, 0]]], device=dev))
+    inp = torch.rand(2, 10, 5, device=dev)
+    assert torch.equal(F.ContextWindow(0, 0)(inp), inp)
+    assert torch.jit.trace(F.ContextWindow(0, 0), inp)
+
+
+def test_multichannel_deltas_context(dev):
+    F, _ = _mods()
+    x = torch.randn(2, 30, 6, 3)
+    d = F.Deltas(input_size=6)(x.to(dev))
+    ref = OF.deltas(x)
+    assert_close(d, ref, name="deltas4d")
+
+
+@pytest.mark.parametrize("n_mels", [80, 40])
+def test_fbank_wavs_vs_golden(golden, dev, n_mels):
+    _, LF = _mods()
+    g = golden("fbank_wavs")
+    fb = LF.Fbank(n_mels=n_mels)
+    for i in range(3):
+        w = torch.from_numpy(g[f"pcm{i}"].astype(np.float32) / 32768.0)[None].to(dev)
+        assert_close(fb(w), g[f"fbank{n_mels}_single{i}"], name=f"wav{i}")
+    L = max(len(g[f"pcm{i}"]) for i in range(3))
+    batch = torch.zeros(3, L)
+    for i in range(3):
+        p = g[f"pcm{i}"]
+        batch[i, :len(p)] = torch.from_numpy(p.astype(np.float32) / 32768.0)
+    assert_close(fb(batch.to(dev)), g[f"fbank{n_mels}_batch"], name="batch")
+
+
+def test_mfcc_fbank_composites_vs_golden(golden, dev):
+    _, LF = _mods()
+    g = golden("features")
+    x = torch.from_numpy(g["x"]).to(dev)
+    assert_close(LF.MFCC()(x), g["mfcc"], name="mfcc")
+    fb = LF.Fbank(n_mels=40, deltas=True, context=True, left_frames=2, right_frames=2)
+    assert_close(fb(x), g["fbank_dc"], name="fbdc")
+    # state_dict key names match the reference (Fbank has buffer compute_deltas.kernel)
+    assert list(fb.state_dict()) == ["compute_deltas.kernel"]
+
+
+def test_fbank_full_size_properties(dev):
+    """BASELINE config 2 size (32 x 15 s): compare against the oracle on a
+    subset of utterances, and check batch-invariance on the full batch."""
+    _, LF = _mods()
+    g = torch.Generator().manual_seed(0)
+    wav = 0.1 * torch.randn(32, 240000, generator=g)
+    fb = LF.Fbank(n_mels=80)
+    out = fb(wav.to(dev))
+    assert out.shape == (32, 1501, 80)
+    ref = OF.fbank(wav[:2], n_mels=80)
+    assert_close(out[:2], ref, name="full")
+    one = fb(wav[5:6].to(dev))
+    assert torch.equal(one[0], out[5])  # per-utterance top_db: batch-invariant, bit-exact
