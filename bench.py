@@ -1,0 +1,254 @@
+"""Headline benchmark (BASELINE.json metric): audio-sec/sec of
+Fbank → ConvolutionFrontEnd → Conformer encoder forward on synthetic 16 kHz
+batches of 32 x 15 s per GPU (weak scaling: every rank encodes its own
+batch; no collective on the data path).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--d-model 256]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+One step = one pass of the hot path over one batch already resident in HBM:
+fused Fbank kernel (+top_db clamp) → 2 fused ConvBlocks → src Linear →
+12 Conformer layers → final LayerNorm, bf16 MFMA (torch.autocast bf16),
+captured once into a HIP graph and replayed.  Rank 0 prints ONE JSON line.
+
+Also reported (rank 0, N=1 path of the contract):
+  roofline      the dominant kernel (bf16 MFMA GEMM) timed with HIP events
+                around each of its launches during an eager pass of K steps
+                on the launch stream; achieved = algorithmic FLOPs / time.
+  cpu_baseline  the from-scratch CPU restatement (oracle/, PyTorch CPU fp32)
+                of the same path on a bounded sample, host threads stated.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+SR = 16000
+SECONDS = 15.0
+BATCH = 32
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+
+
+def build_model(d_model, dev, layers=12):
+    from speechbrain_amd.lobes.features import Fbank
+    from speechbrain_amd.lobes.models.convolution import ConvolutionFrontEnd
+    from speechbrain_amd.lobes.models.transformer.TransformerASR import TransformerASR
+    torch.manual_seed(0)
+    fbank = Fbank(sample_rate=SR, n_fft=400, n_mels=80)
+    cnn = ConvolutionFrontEnd(input_shape=(8, 10, 80), num_blocks=2, num_layers_per_block=1, out_channels=(64, 32),
+                              kernel_sizes=(3, 3), strides=(2, 2), residuals=(False, False))
+    tr = TransformerASR(tgt_vocab=5000, input_size=640, d_model=d_model, nhead=4, num_encoder_layers=layers,
+                        num_decoder_layers=0, d_ffn=1024, dropout=0.1, encoder_module="conformer",
+                        attention_type="RelPosMHAXL", normalize_before=True, causal=False)
+    return fbank.to(dev).eval(), cnn.to(dev).eval(), tr.to(dev).eval()
+
+
+def encoder_flops(B, T_e, d, dff=1024, k=31, H=4, layers=12, T1=751, F1=40, T2=376, F2=20, c1=64, c2=32,
+                  in_dim=640):
+    """Algorithmic FLOPs of one step: per layer QKV 6d², out 2d²,
+    FFN 2x4·d·dff, conv 4d²+2kd+2d², scores 2T·d + 2(2T-1)·d, AV 2T·d per token,
+    linear_pos 2(2T-1)d² per layer; plus front-end convs and the src Linear."""
+    per_tok = (6 * d * d + 2 * d * d + 2 * 4 * d * dff + 4 * d * d + 2 * k * d + 2 * d * d
+               + 2 * T_e * d + 2 * (2 * T_e - 1) * d + 2 * T_e * d)
+    enc = layers * (B * T_e * per_tok + 2 * (2 * T_e - 1) * d * d)
+    front = B * (2 * T1 * F1 * c1 * 9 + 2 * T2 * F2 * c2 * 9 * c1) + B * T_e * 2 * in_dim * d
+    return enc + front
+
+
+def gemm_flops(M, N, K):
+    return 2.0 * M * N * K
+
+
+def cpu_baseline(d_model, n_utt=16, reps=4):
+    """Oracle (PyTorch CPU fp32 restatement) on n_utt x 15 s, median of `reps`."""
+    import oracle.conformer as OC
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    fbank, cnn, tr = build_model(d_model, "cpu")
+    sd_cnn = cnn.state_dict()
+    sd_tr = tr.state_dict()
+    g = torch.Generator().manual_seed(0)
+    wav = 0.1 * torch.randn(n_utt, int(SR * SECONDS), generator=g)
+    lens = torch.ones(n_utt)
+    times = []
+    with torch.no_grad():
+        for r in range(reps + 1):
+            t0 = time.perf_counter()
+            OC.fbank_to_encoder(wav, sd_cnn, sd_tr, 12, 4, n_mels=80, wav_len=lens)
+            if r:
+                times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": round(n_utt * SECONDS / med, 2), "unit": "audio-sec/sec", "cores": threads, "kind": "port",
+            "sample": f"{n_utt} utt x 15 s synthetic, fp32, median of {reps} after 1 warm-up; CPU: {model}"}
+
+
+class _GemmProbe:
+    """Wraps speechbrain_amd._enc.gemm to time every bf16 GEMM launch with HIP
+    events on the launch stream and accumulate its algorithmic FLOPs."""
+
+    def __init__(self):
+        from speechbrain_amd import _enc
+        self._enc = _enc
+        self.orig = _enc.gemm
+        self.events = []
+        self.flops = 0.0
+
+    def __enter__(self):
+        probe = self
+
+        def wrapped(a, w, *args, **kw):
+            if a.dtype != torch.bfloat16:
+                return probe.orig(a, w, *args, **kw)
+            s = torch.cuda.current_stream(a.device)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            out = probe.orig(a, w, *args, **kw)
+            e1.record(s)
+            probe.events.append((e0, e1))
+            probe.flops += gemm_flops(a.shape[0], w.shape[0], a.shape[1])
+            return out
+        self._enc.gemm = wrapped
+        # modules hold a reference through the module object, so patching the attribute suffices
+        return self
+
+    def __exit__(self, *exc):
+        self._enc.gemm = self.orig
+
+    def result(self):
+        torch.cuda.synchronize()
+        ms = sum(e0.elapsed_time(e1) for e0, e1 in self.events)
+        n = len(self.events)
+        return ms, n, self.flops
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--d-model", type=int, default=256)
+    ap.add_argument("--batch", type=int, default=BATCH)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    fbank, cnn, tr = build_model(args.d_model, dev)
+    g = torch.Generator().manual_seed(1234 + rank)
+    wav = (0.1 * torch.randn(args.batch, int(SR * SECONDS), generator=g)).to(dev)
+    wav_len = torch.ones(args.batch, device=dev)
+
+    def step():
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            feats = fbank(wav)
+            src = cnn.run(feats, torch.bfloat16)
+            return tr.encode(src, wav_len)
+
+    out = step()
+    T_e = out.shape[1]
+    torch.cuda.synchronize()
+    graph = None
+    if not args.no_graph:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                step()
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = step()
+        torch.cuda.synchronize()
+
+    run = graph.replay if graph is not None else step
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = 1000.0 * elapsed / args.steps
+    audio = world * args.batch * SECONDS * args.steps
+    value = audio / elapsed
+
+    if rank == 0:
+        total_flops = encoder_flops(args.batch, T_e, args.d_model)
+        # dominant kernel: bf16 MFMA GEMM, HIP events around each launch over K eager steps
+        with _GemmProbe() as probe:
+            for _ in range(args.steps):
+                step()
+        gms, glaunch, gflops = probe.result()
+        achieved = gflops / (gms * 1e-3) / 1e12
+        res = {
+            "metric": "audio-sec/sec Fbank→Conformer fwd (16kHz, B=32×15s) at 1/2/4/8 GPU",
+            "value": round(value, 1),
+            "unit": "audio-sec/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (0.1·N(0,1) 16 kHz, random-init weights)",
+            "config": {"workload": f"Fbank(80)→ConvFrontEnd(64,32)→Conformer 12L d={args.d_model} H=4 ffn=1024 "
+                                   f"k=31 encode, B={args.batch}×15s per GPU",
+                       "global_batch": world * args.batch, "seq_len": T_e, "parallelism": f"replicas{world}",
+                       "hip_graph": graph is not None},
+            "roofline": {"bound": "mfma", "kernel": "gemm_kernel<bf16> (all encoder projections)",
+                         "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                         "launches_per_step": glaunch // max(1, args.steps),
+                         "avg_launch_us": round(1000.0 * gms / max(1, glaunch), 3),
+                         "step_algorithmic_tflop": round(total_flops / 1e12, 4),
+                         "step_tflops_achieved": round(total_flops / (ms_per_step * 1e-3) / 1e12, 2)},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            res["cpu_baseline"] = cpu_baseline(args.d_model)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,135 @@
+/*
+ * sbk.h — C ABI of libsbk.so, the MI355X (gfx950) kernel library behind
+ * speechbrain_amd.  Plain pointers, sizes and a hipStream_t passed as void*;
+ * no torch types.  Every entry point launches asynchronously on `stream`
+ * and returns 0, a hipError_t code, or SBK_ERR_ARG (1001) for an invalid
+ * shape/configuration detected on the host.  All pointers are device
+ * pointers unless stated otherwise.
+ *
+ * The reference (Sinica-SLAM/speechbrain 0.5.13) has no FFI: its plugin
+ * boundary is the nn.Module import path resolved by HyperPyYAML
+ * (SURVEY.md §8b).  Each entry point below names the reference operation it
+ * replaces; the Python drop-in modules in speechbrain_amd/ call these
+ * through ctypes (speechbrain_amd/_lib.py).
+ */
+#ifndef SBK_H
+#define SBK_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SBK_ERR_ARG 1001
+
+/* ---------------------------------------------------------------- features */
+
+/* 1 if n_fft (even) factors into radices {8,5,4,3,2} (the LDS FFT plan). */
+int sbk_fft_supported(int n_fft);
+
+/* STFT family, replaces torch.stft in STFT.forward
+ * (speechbrain/processing/features.py:133-188), spectral_magnitude
+ * (:327-356) and, fused, Filterbank.forward + _amplitude_to_DB before the
+ * top_db clamp (:490-560, :691-712) — Fbank.forward (lobes/features.py:130-147).
+ *   mode 0: STFT  -> out[bo*os_b + c*os_c + t*os_t + k*os_k + ri*os_ri]
+ *   mode 1: power -> out[bo*os_b + c*os_c + t*os_t + k*os_k]  (power, eps, log_mag)
+ *   mode 2: Fbank -> out (Bo, T, M) dB, per-sequence max key in maxkey (Bo,)
+ * wav: (Bo, S, C) fp32; window: n_fft fp32 (win centred, zero padded);
+ * twiddle_nc: n_fft/2 complex W_{n_fft/2}^m; twiddle_nfft: n_fft/2+1 complex W_{n_fft}^k;
+ * out_strides: HOST array of 5 int64 (modes 0/1); mel_*: per-filter CSR of the
+ * (n_fft/2+1, M) filter matrix (start bin, length, offset into mel_w). */
+int sbk_spectrum(int mode, const float* wav, int Bo, int S, int C, int n_fft, int hop, int center, int pad_mode,
+                 int T, const float* window, const float* twiddle_nc, const float* twiddle_nfft, int onesided,
+                 float norm_scale, float power, float eps, int log_mag, const long long* out_strides,
+                 const int* mel_start, const int* mel_len, const int* mel_off, const float* mel_w, int M,
+                 int log_mel, float multiplier, float db_offset, float amin, float* out, int* maxkey, void* stream);
+
+/* Filterbank.forward on a spectrogram (N, T, F) -> (N, T, M) (features.py:490-560):
+ * sparse CSR filters, or a dense (F, M) matrix when `dense` is non-null
+ * (learnable filters, freeze=False). */
+int sbk_filterbank(const float* spec, int N, int T, int F, const int* mel_start, const int* mel_len,
+                   const int* mel_off, const float* mel_w, const float* dense, int M, int log_mel, float multiplier,
+                   float db_offset, float amin, float* out, int* maxkey, void* stream);
+
+/* top_db floor of _amplitude_to_DB (features.py:706-711), in place:
+ * x[n, :] = max(x[n, :], max_n - top_db) for nseq sequences of per_seq values. */
+int sbk_topdb_clamp(float* x, const int* maxkey, long long per_seq, int nseq, float top_db, void* stream);
+
+/* spectral_magnitude (features.py:347-356): y[i] = f(sum_q x[i, q]^2), q < L. */
+int sbk_magnitude(const float* x, float* y, long long n, int L, float power, float eps, int log_mag, void* stream);
+
+/* DCT.forward (features.py:765-786): y (rows, n_out) = x (rows, n_in) @ D (n_in, n_out). */
+int sbk_dct(const float* x, const float* D, float* y, long long rows, int n_in, int n_out, void* stream);
+
+/* Deltas.forward (features.py:829-852) along time of (N, T, F); concat=1
+ * writes [x | d1 | d2] (N, T, 3F) in one pass (lobes/features.py:141-144). */
+int sbk_deltas(const float* x, float* y, int N, int T, int F, int window_length, int concat, void* stream);
+
+/* ContextWindow.forward (features.py:917-937): (N, T, F) -> (N, T, F*(l+r+1)). */
+int sbk_context_window(const float* x, float* y, int N, int T, int F, int left, int right, void* stream);
+
+/* ----------------------------------------------------------------- encoder */
+
+/* Output channels per wave tile in the GLU-paired GEMM (weights are
+ * row-permuted in groups of this size). */
+int sbk_gemm_glu_group(int dtype_bf16);
+
+/* out = res + alpha * act(A @ W^T + bias), masked rows -> 0 before the residual.
+ * A (M, K) lda, W (N, K) ldw, both bf16 (dtype_bf16=1) or fp32; act: 0 none,
+ * 1 Swish, 2 GLU (N/2 outputs, W permuted), 3 LeakyReLU(slope), 4 GELU;
+ * res fp32 (M, ldr) or null; rowmask uint8 (M) or null; out fp32 or bf16.
+ * Replaces nn.Linear / 1x1 Conv1d sites: attention.py:549-553,581,636,823-839;
+ * Conformer.py:73-79,87-92,105; TransformerASR.py:127-135. */
+int sbk_gemm(int dtype_bf16, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
+             const float* bias, int act, float slope, const float* res, int ldr, float alpha,
+             const uint8_t* rowmask, void* out, int ldc, int out_bf16, int tile, void* stream);
+
+/* LayerNorm (normalization.py:172-223; Conformer.py:178,194,340): one or two
+ * chained LayerNorms over rows of x (M, D) fp32, D <= 1024. */
+int sbk_layernorm(const float* x, int M, int D, const float* g1, const float* b1, float eps1, void* out1,
+                  int out1_bf16, const float* g2, const float* b2, float eps2, void* out2, int out2_bf16,
+                  void* stream);
+
+/* ConvolutionModule middle (Conformer.py:106-113): depthwise Conv1d(K) over
+ * time (zero pad (K-1)/2, or K-1 left when causal) + bias -> LayerNorm(C)
+ * -> Swish.  x (B*T, C) bf16/fp32 -> out (B*T, C). */
+int sbk_dwconv_ln_swish(int in_bf16, const void* x, int B, int T, int C, const float* w, const float* bias, int K,
+                        int causal, const float* g, const float* beta, float eps, void* out, int out_bf16,
+                        void* stream);
+
+/* ConvBlock (convolution.py:169-175 + CNN.py:616-657) with Cin = 1:
+ * Conv2d 3x3 stride 2 reflect pad -> LayerNorm(Fout x Cout) -> LeakyReLU.
+ * x (B, Tin, Fin) fp32 -> out (B, Tout, Fout, Cout).  x == NULL: shape query. */
+int sbk_conv_block_c1(const float* x, int B, int Tin, int Fin, int Cout, const float* w, const float* bias,
+                      const float* g, const float* beta, float eps, float slope, void* out, int out_bf16, int* Tout,
+                      int* Fout, void* stream);
+
+/* Same block for Cin % 8 == 0 as an MFMA implicit GEMM; wperm (Cout, 3 time,
+ * 3 freq, Cin) in the input dtype. */
+int sbk_conv_block_mfma(int in_bf16, const void* x, int B, int Tin, int Fin, int Cin, int Cout, const void* wperm,
+                        const float* bias, const float* g, const float* beta, float eps, float slope, void* out,
+                        int out_bf16, int* Tout, int* Fout, void* stream);
+
+/* fp32 -> bf16 cast (n elements). */
+int sbk_cast_bf16(const float* x, void* y, long long n, void* stream);
+
+/* Swish (activations.py:111-142): y = x * sigmoid(beta * x). */
+int sbk_swish(const float* x, float* y, long long n, float beta, void* stream);
+
+/* RelPosMHAXL core (attention.py:566-636 incl. rel_shift :468-483):
+ * qkv (B*T, 3d) head-interleaved in_proj output, pk (2T-1, d) linear_pos
+ * output, pbu/pbv (H*dh) fp32, kpm (B, T) uint8 or null; out (B*T, d);
+ * probs (B, H, T, T) fp32 or null.  dh <= 128. */
+int sbk_relpos_attention(int dtype_bf16, const void* qkv, const void* pk, const float* pbu, const float* pbv,
+                         const uint8_t* kpm, int B, int T, int H, int dh, float scale, void* out, float* probs,
+                         void* stream);
+
+/* LDS bytes one attention workgroup needs (host-side capacity check). */
+long long sbk_relpos_attention_lds(int dtype_bf16, int T, int dh);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SBK_H */

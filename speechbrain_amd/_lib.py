@@ -34,7 +34,21 @@ SIGNATURES = {
     "sbk_dct": [_vp, _vp, _vp, _ll, _i, _i, _vp],
     "sbk_deltas": [_vp, _vp, _i, _i, _i, _i, _i, _vp],
     "sbk_context_window": [_vp, _vp, _i, _i, _i, _i, _i, _vp],
+    # gemm.hip
+    "sbk_gemm_glu_group": [_i],
+    "sbk_gemm": [_i, _vp, _i, _vp, _i, _i, _i, _i, _vp, _i, _f, _vp, _i, _f, _vp, _vp, _i, _i, _i, _vp],
+    # conformer.hip
+    "sbk_layernorm": [_vp, _i, _i, _vp, _vp, _f, _vp, _i, _vp, _vp, _f, _vp, _i, _vp],
+    "sbk_dwconv_ln_swish": [_i, _vp, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _f, _vp, _i, _vp],
+    "sbk_conv_block_c1": [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _f, _vp, _i, _vp, _vp, _vp],
+    "sbk_conv_block_mfma": [_i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _f, _vp, _i, _vp, _vp, _vp],
+    "sbk_cast_bf16": [_vp, _vp, _ll, _vp],
+    "sbk_swish": [_vp, _vp, _ll, _f, _vp],
+    # attention.hip
+    "sbk_relpos_attention": [_i, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _vp],
+    "sbk_relpos_attention_lds": [_i, _i, _i],
 }
+RESTYPES = {"sbk_relpos_attention_lds": ctypes.c_longlong}
 
 _lib = None
 _load_error = None
@@ -62,7 +76,7 @@ def lib():
     for name, argt in SIGNATURES.items():
         fn = getattr(l, name)
         fn.argtypes = argt
-        fn.restype = ctypes.c_int
+        fn.restype = RESTYPES.get(name, ctypes.c_int)
     _lib = l
     return l
 

@@ -1,0 +1,231 @@
+// MFMA GEMM with fused epilogues for the Conformer projections.
+//
+//   C[M, N] = epilogue( A[M, K] · W[N, K]^T )
+//
+// A: activations (row-major, lda), W: nn.Linear weight layout [out][in]
+// (K contiguous) — both operands are K-contiguous, so every MFMA fragment is
+// one 16-byte LDS read for bf16 (two for f32).  Tiles: 4 waves (2x2), each
+// wave owns a (BM/2)x(BN/2) block of 16x16 MFMA tiles; K staged through a
+// double-buffered LDS ring (register prefetch of tile k+1 overlaps the MFMAs
+// of tile k, one barrier per K tile).
+//
+// Epilogues (fused so no activation makes an extra HBM round trip):
+//   bias, activation (Swish / GLU / LeakyReLU), row mask (padding frames ->
+//   0), residual  out = res + alpha * val,  fp32 or bf16 output.
+// These implement speechbrain nn.Linear / Conv1d(k=1) sites:
+//   attention.py:549-553 (in_proj), :581 (linear_pos), :636 (out_proj),
+//   :823-839 (FFN Linear-Swish-Linear), Conformer.py:73-79,105 (pointwise
+//   conv + GLU), :87-92 (after_conv Linear), :243,:259 (0.5-scaled residuals),
+//   TransformerASR.py:127-135 (custom_src_module Linear).
+#include "mfma.h"
+
+using namespace sbk;
+
+namespace {
+
+enum Act { ACT_NONE = 0, ACT_SWISH = 1, ACT_GLU = 2, ACT_LRELU = 3, ACT_GELU = 4 };
+
+struct Epi {
+  const float* bias;        // [N] (GLU: permuted like W) or null
+  int act;
+  float slope;              // LeakyReLU negative slope
+  const float* res;         // residual [M, ldr] fp32 or null
+  int ldr;
+  float alpha;              // val scale before residual add
+  const uint8_t* rowmask;   // [M]: nonzero -> val = 0
+  void* out;
+  int ldc;
+  int out_bf16;
+};
+
+template <typename T, int BM, int BN, int BK>
+__global__ void __launch_bounds__(256) gemm_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W,
+                                                   int ldw, int M, int N, int K, Epi ep) {
+  using Tr = MT<T>;
+  constexpr int VEC = Tr::VEC;
+  constexpr int LDSR = BK + Tr::PAD;     // LDS row stride (elements)
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int CPR = BK / VEC;          // 16-B chunks per row
+  constexpr int ACH = BM * CPR / 256;    // chunks per thread (A)
+  constexpr int BCH = BN * CPR / 256;    // chunks per thread (B)
+  static_assert(ACH >= 1 && BCH >= 1, "tile too small for 256 threads");
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* As = reinterpret_cast<T*>(smem);
+  T* Bs = As + 2 * BM * LDSR;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int ntn = (N + BN - 1) / BN;
+  const int m0 = (blockIdx.x / ntn) * BM;
+  const int n0 = (blockIdx.x % ntn) * BN;
+
+  uint4 ra[ACH], rb[BCH];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int c = tid + i * 256, r = c / CPR, kc = (c % CPR) * VEC;
+      const int gr = m0 + r, gk = k0 + kc;
+      ra[i] = (gr < M && gk < K) ? *reinterpret_cast<const uint4*>(A + (long long)gr * lda + gk) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int c = tid + i * 256, r = c / CPR, kc = (c % CPR) * VEC;
+      const int gr = n0 + r, gk = k0 + kc;
+      rb[i] = (gr < N && gk < K) ? *reinterpret_cast<const uint4*>(W + (long long)gr * ldw + gk) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto sstore = [&](int buf) {
+    T* as = As + buf * BM * LDSR;
+    T* bs = Bs + buf * BN * LDSR;
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int c = tid + i * 256, r = c / CPR, kc = (c % CPR) * VEC;
+      *reinterpret_cast<uint4*>(as + r * LDSR + kc) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int c = tid + i * 256, r = c / CPR, kc = (c % CPR) * VEC;
+      *reinterpret_cast<uint4*>(bs + r * LDSR + kc) = rb[i];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (K + BK - 1) / BK;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  int cur = 0;
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) gload((kt + 1) * BK);
+    const T* as = As + cur * BM * LDSR + (wm * WM + fr) * LDSR + fk;
+    const T* bs = Bs + cur * BN * LDSR + (wn * WN + fr) * LDSR + fk;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      typename Tr::frag fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = Tr::load(as + i * 16 * LDSR + ks * 32);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = Tr::load(bs + j * 16 * LDSR + ks * 32);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) Tr::mma(acc[i][j], fa[i], fb[j]);
+    }
+    if (kt + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // ---- epilogue ----
+  const int rbase = m0 + wm * WM + 4 * (lane >> 4);
+  const int cbase = n0 + wn * WN + fr;
+  if (ep.act == ACT_GLU) {
+    // wave column span [n0 + wn*WN, +WN): first half = value channels, second = gates
+    const int ocol0 = (n0 + wn * WN) / 2;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN / 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = rbase + i * 16 + r;
+          const int ca = cbase + j * 16, cb = ca + WN / 2;
+          const int oc = ocol0 + j * 16 + fr;
+          if (row >= M || cb >= N) continue;
+          float va = acc[i][j][r], vb = acc[i][j + TN / 2][r];
+          if (ep.bias) {
+            va += ep.bias[ca];
+            vb += ep.bias[cb];
+          }
+          float v = va * (1.0f / (1.0f + expf(-vb)));
+          if (ep.rowmask && ep.rowmask[row]) v = 0.f;
+          v *= ep.alpha;
+          if (ep.res) v += ep.res[(long long)row * ep.ldr + oc];
+          if (ep.out_bf16)
+            reinterpret_cast<bf16_t*>(ep.out)[(long long)row * ep.ldc + oc] = f32_to_bf16(v);
+          else
+            reinterpret_cast<float*>(ep.out)[(long long)row * ep.ldc + oc] = v;
+        }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rbase + i * 16 + r;
+        const int col = cbase + j * 16;
+        if (row >= M || col >= N) continue;
+        float v = acc[i][j][r];
+        if (ep.bias) v += ep.bias[col];
+        if (ep.act == ACT_SWISH)
+          v = v * (1.0f / (1.0f + expf(-v)));
+        else if (ep.act == ACT_LRELU)
+          v = v >= 0.f ? v : v * ep.slope;
+        else if (ep.act == ACT_GELU)
+          v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+        if (ep.rowmask && ep.rowmask[row]) v = 0.f;
+        v *= ep.alpha;
+        if (ep.res) v += ep.res[(long long)row * ep.ldr + col];
+        if (ep.out_bf16)
+          reinterpret_cast<bf16_t*>(ep.out)[(long long)row * ep.ldc + col] = f32_to_bf16(v);
+        else
+          reinterpret_cast<float*>(ep.out)[(long long)row * ep.ldc + col] = v;
+      }
+}
+
+template <typename T, int BM, int BN, int BK>
+int launch(const void* A, int lda, const void* W, int ldw, int M, int N, int K, const Epi& ep, hipStream_t s) {
+  constexpr int LDSR = BK + MT<T>::PAD;
+  const size_t lds = (size_t)2 * (BM + BN) * LDSR * sizeof(T);
+  const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, BK>), dim3(grid), dim3(256), lds, s, reinterpret_cast<const T*>(A),
+                     lda, reinterpret_cast<const T*>(W), ldw, M, N, K, ep);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace
+
+// The GLU column permutation depends on the wave tile width WN = BN/2; the
+// host asks for it here so weights are permuted consistently.
+SBK_API int sbk_gemm_glu_group(int dtype_bf16) { return 16; }  // = WN/2 of the 64x64 tile
+
+// dtype_bf16: A and W are bf16 (else fp32).  tile: 0 auto, 1 = 128x128, 2 = 64x64, 3 = 128x64.
+SBK_API int sbk_gemm(int dtype_bf16, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
+                     const float* bias, int act, float slope, const float* res, int ldr, float alpha,
+                     const uint8_t* rowmask, void* out, int ldc, int out_bf16, int tile, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return SBK_ERR_ARG;
+  const int vec = dtype_bf16 ? 8 : 4;
+  if ((K % vec) || (lda % vec) || (ldw % vec)) return SBK_ERR_ARG;
+  if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(W)) & 15) return SBK_ERR_ARG;
+  if (act == ACT_GLU && (N % 32)) return SBK_ERR_ARG;  // whole [a16|gate16] groups
+  Epi ep{bias, act, slope, res, ldr, alpha, rowmask, out, ldc, out_bf16};
+  hipStream_t s = (hipStream_t)stream;
+  if (act == ACT_GLU) tile = 2;  // GLU pairing assumes WN = 32
+  if (tile == 0) {
+    const long long t128 = (long long)((M + 127) / 128) * ((N + 127) / 128);
+    tile = t128 >= 512 ? 1 : 2;
+  }
+  if (dtype_bf16) {
+    switch (tile) {
+      case 1: return launch<bf16_t, 128, 128, 64>(A, lda, W, ldw, M, N, K, ep, s);
+      case 3: return launch<bf16_t, 128, 64, 64>(A, lda, W, ldw, M, N, K, ep, s);
+      default: return launch<bf16_t, 64, 64, 64>(A, lda, W, ldw, M, N, K, ep, s);
+    }
+  }
+  switch (tile) {
+    case 1: return launch<float, 128, 128, 32>(A, lda, W, ldw, M, N, K, ep, s);
+    case 3: return launch<float, 128, 64, 32>(A, lda, W, ldw, M, N, K, ep, s);
+    default: return launch<float, 64, 64, 32>(A, lda, W, ldw, M, N, K, ep, s);
+  }
+}

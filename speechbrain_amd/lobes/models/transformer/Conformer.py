@@ -1,0 +1,221 @@
+"""Drop-in for speechbrain.lobes.models.transformer.Conformer encoder side
+(ConvolutionModule, ConformerEncoderLayer, ConformerEncoder;
+speechbrain/lobes/models/transformer/Conformer.py:24-383).
+
+Same constructor arguments and submodule tree (so state_dict keys match the
+reference); forward runs a fused kernel schedule per layer:
+
+  LN                      → u        (bf16 | f32)
+  GEMM+bias+Swish         → h        FFN1 up
+  GEMM+bias, x += 0.5·val → x        FFN1 down (residual fused)
+  LN(norm1)               → u
+  GEMM in_proj            → qkv      ; GEMM linear_pos → p_k
+  rel-pos attention       → o        (scores, rel_shift, mask, softmax, P·V)
+  GEMM out_proj, x += val → x
+  LN(conv.layer_norm)     → u
+  GEMM pointwise + GLU    → g
+  depthwise conv+LN+Swish → v
+  GEMM after_conv, mask, x += val → x
+  LN ; FFN2 (as FFN1, 0.5 residual) → z
+  LN(norm2)[+ next layer's FFN1 LN] → x, u
+The residual stream stays fp32; GEMM/attention operands are bf16 under
+torch.autocast (bf16 MFMA) and fp32 otherwise (exact-f32 MFMA, the parity
+path).
+"""
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from .... import _enc
+from ....nnet.activations import Swish
+from ....nnet.attention import PositionalwiseFeedForward, RelPosMHAXL
+from ....nnet.normalization import LayerNorm
+
+__all__ = ["ConvolutionModule", "ConformerEncoderLayer", "ConformerEncoder"]
+
+_f32 = torch.float32
+_bf16 = torch.bfloat16
+
+
+def _check_swish(act_module):
+    if not (isinstance(act_module, Swish) or type(act_module).__name__ == "Swish"):
+        raise NotImplementedError("fused conv module supports the Swish activation only")
+    if getattr(act_module, "beta", 1) != 1:
+        raise NotImplementedError("Swish(beta != 1) is not fused")
+
+
+class ConvolutionModule(nn.Module):
+    """Conformer.py:24-115."""
+
+    def __init__(self, input_size, kernel_size=31, bias=True, activation=Swish, dropout=0.0, causal=False,
+                 dilation=1):
+        super().__init__()
+        self.causal = causal
+        if dilation != 1:
+            raise NotImplementedError("dilated depthwise conv is not on the hot path")
+        if self.causal:
+            self.padding = (kernel_size - 1) * 2 ** (dilation - 1)
+        else:
+            self.padding = (kernel_size - 1) * 2 ** (dilation - 1) // 2
+        self.layer_norm = nn.LayerNorm(input_size)
+        self.bottleneck = nn.Sequential(
+            nn.Conv1d(input_size, 2 * input_size, kernel_size=1, stride=1, bias=bias), nn.GLU(dim=1))
+        self.conv = nn.Conv1d(input_size, input_size, kernel_size=kernel_size, stride=1, padding=self.padding,
+                              dilation=dilation, groups=input_size, bias=bias)
+        self.after_conv = nn.Sequential(nn.LayerNorm(input_size), activation(), nn.Linear(input_size, input_size,
+                                                                                          bias=bias),
+                                        nn.Dropout(dropout))
+        self._wc = _enc.WeightCache()
+
+    def kernel_weights(self, dtype):
+        """(GLU-permuted pointwise weight, permuted bias, after_conv weight)."""
+        w1 = self.bottleneck[0].weight
+        b1 = self.bottleneck[0].bias
+        w2 = self.after_conv[2].weight
+
+        def make():
+            d = w2.shape[0]
+            grp = _enc.glu_group()  # output channels per wave tile of the GLU GEMM
+            perm = []
+            for q in range(d // grp):
+                perm += list(range(q * grp, (q + 1) * grp))
+                perm += list(range(d + q * grp, d + (q + 1) * grp))
+            idx = torch.tensor(perm, device=w1.device)
+            w1p = w1.detach().reshape(2 * d, d).index_select(0, idx).contiguous()
+            b1p = b1.detach().index_select(0, idx).contiguous() if b1 is not None else None
+            w2d = w2.detach().contiguous()
+            if dtype == _bf16:
+                w1p, w2d = _enc.cast_bf16(w1p), _enc.cast_bf16(w2d)
+            return w1p, b1p, w2d
+        ps = [w1, w2] + ([b1] if b1 is not None else [])
+        return self._wc.get(str(dtype), ps, make)
+
+    def run(self, x2d, B, T, dtype, pad_mask_u8=None, residual=None):
+        """x2d: (B*T, d) fp32 → residual + mask(ConvolutionModule(x)) (fp32)."""
+        d = x2d.shape[1]
+        if d % _enc.glu_group():
+            raise NotImplementedError("fused GLU needs d_model % 16 == 0")
+        _check_swish(self.after_conv[1])
+        w1p, b1p, w2 = self.kernel_weights(dtype)
+        u, _ = _enc.layernorm(x2d, self.layer_norm.weight.detach(), self.layer_norm.bias.detach(),
+                              self.layer_norm.eps, out1_dtype=dtype)
+        g = _enc.gemm(u, w1p, bias=b1p, act="glu", out_dtype=dtype)
+        ln = self.after_conv[0]
+        v = _enc.dwconv_ln_swish(g, B, T, self.conv.weight.detach(), self.conv.bias.detach() if self.conv.bias is not None
+                                 else None, self.causal, ln.weight.detach(), ln.bias.detach(), ln.eps, dtype)
+        lin = self.after_conv[2]
+        return _enc.gemm(v, w2, bias=lin.bias.detach() if lin.bias is not None else None, rowmask=pad_mask_u8,
+                         res=residual, out_dtype=_f32)
+
+    def forward(self, x, mask=None):
+        if self.training and self.after_conv[3].p > 0:
+            raise NotImplementedError("dropout in training mode is not implemented in HIP yet")
+        B, T, d = x.shape
+        m = mask.reshape(B * T).to(torch.uint8).contiguous() if mask is not None else None
+        return self.run(x.float().reshape(B * T, d).contiguous(), B, T, _enc.compute_dtype(), m).view(B, T, d)
+
+
+class ConformerEncoderLayer(nn.Module):
+    """Conformer.py:118-260."""
+
+    def __init__(self, d_model, d_ffn, nhead, kernel_size=31, kdim=None, vdim=None, activation=Swish, bias=True,
+                 dropout=0.0, causal=False, attention_type="RelPosMHAXL"):
+        super().__init__()
+        if attention_type != "RelPosMHAXL":
+            raise NotImplementedError("only RelPosMHAXL attention is on the accelerated Conformer path")
+        self.mha_layer = RelPosMHAXL(num_heads=nhead, embed_dim=d_model, dropout=dropout, mask_pos_future=causal)
+        self.convolution_module = ConvolutionModule(d_model, kernel_size, bias, activation, dropout, causal=causal)
+        self.ffn_module1 = nn.Sequential(
+            nn.LayerNorm(d_model),
+            PositionalwiseFeedForward(d_ffn=d_ffn, input_size=d_model, dropout=dropout, activation=activation),
+            nn.Dropout(dropout))
+        self.ffn_module2 = nn.Sequential(
+            nn.LayerNorm(d_model),
+            PositionalwiseFeedForward(d_ffn=d_ffn, input_size=d_model, dropout=dropout, activation=activation),
+            nn.Dropout(dropout))
+        self.norm1 = LayerNorm(d_model)
+        self.norm2 = LayerNorm(d_model)
+        self.drop = nn.Dropout(dropout)
+
+    def _ln(self, mod):
+        return mod.weight.detach(), mod.bias.detach(), mod.eps
+
+    def fused(self, x, B, T, pos, kpm_u8, dtype, need_attn, u_in=None, next_ln=None):
+        """One layer.  x: (B*T, d) fp32 residual stream; pos: (2T-1, d) in
+        dtype; u_in: LN_ffn1(x) if a previous kernel already produced it;
+        next_ln: (w, b, eps) of the NEXT consumer's LayerNorm to chain after
+        norm2.  Returns (x_out fp32, u_next or None, attn or None)."""
+        if self.training and self.drop.p > 0:
+            raise NotImplementedError("dropout in training mode is not implemented in HIP yet")
+        f1, f2 = self.ffn_module1, self.ffn_module2
+        if u_in is None:
+            u_in, _ = _enc.layernorm(x, *self._ln(f1[0]), out1_dtype=dtype)
+        x = f1[1].run(u_in, dtype, residual=x, alpha=0.5)
+        u, _ = _enc.layernorm(x, *self._ln(self.norm1.norm), out1_dtype=dtype)
+        x, attn = self.mha_layer.attend(u, B, T, pos, kpm_u8, dtype, need_attn, residual=x)
+        x = self.convolution_module.run(x, B, T, dtype, kpm_u8, residual=x)
+        u, _ = _enc.layernorm(x, *self._ln(f2[0]), out1_dtype=dtype)
+        z = f2[1].run(u, dtype, residual=x, alpha=0.5)
+        w2, b2, e2 = self._ln(self.norm2.norm)
+        if next_ln is not None:
+            x, u_next = _enc.layernorm(z, w2, b2, e2, out1_dtype=_f32, w2=next_ln[0], b2=next_ln[1],
+                                       eps2=next_ln[2], out2_dtype=dtype)
+            return x, u_next, attn
+        x, _ = _enc.layernorm(z, w2, b2, e2, out1_dtype=_f32)
+        return x, None, attn
+
+    def forward(self, x, src_mask: Optional[torch.Tensor] = None,
+                src_key_padding_mask: Optional[torch.Tensor] = None, pos_embs: Optional[torch.Tensor] = None):
+        if src_mask is not None:
+            raise NotImplementedError("src_mask is not supported by the fused attention kernel")
+        B, T, d = x.shape
+        dtype = _enc.compute_dtype()
+        kpm = src_key_padding_mask.to(torch.uint8).contiguous() if src_key_padding_mask is not None else None
+        pos = _enc.to_compute(pos_embs.reshape(-1, d), dtype)
+        y, _, attn = self.fused(x.float().reshape(B * T, d).contiguous(), B, T, pos, kpm, dtype, True)
+        return y.view(B, T, d), attn
+
+
+class ConformerEncoder(nn.Module):
+    """Conformer.py:263-383."""
+
+    def __init__(self, num_layers, d_model, d_ffn, nhead, kernel_size=31, kdim=None, vdim=None, activation=Swish,
+                 bias=True, dropout=0.0, causal=False, attention_type="RelPosMHAXL"):
+        super().__init__()
+        self.layers = torch.nn.ModuleList([
+            ConformerEncoderLayer(d_ffn=d_ffn, nhead=nhead, d_model=d_model, kdim=kdim, vdim=vdim, dropout=dropout,
+                                  activation=activation, kernel_size=kernel_size, bias=bias, causal=causal,
+                                  attention_type=attention_type) for i in range(num_layers)])
+        self.norm = LayerNorm(d_model, eps=1e-6)
+        self.attention_type = attention_type
+
+    def run(self, src2d, B, T, pos_embs, kpm_u8, dtype, need_attn):
+        """Fused stack on (B*T, d) fp32 → ((B*T, d) fp32, [attn])."""
+        d = src2d.shape[1]
+        pos = _enc.to_compute(pos_embs.reshape(-1, d), dtype)
+        x = src2d
+        u = None
+        attns = []
+        n = len(self.layers)
+        for i, layer in enumerate(self.layers):
+            nxt = self.layers[i + 1].ffn_module1[0] if i + 1 < n else None
+            next_ln = (nxt.weight.detach(), nxt.bias.detach(), nxt.eps) if nxt is not None else None
+            x, u, a = layer.fused(x, B, T, pos, kpm_u8, dtype, need_attn, u_in=u, next_ln=next_ln)
+            attns.append(a)
+        fn = self.norm.norm
+        y, _ = _enc.layernorm(x, fn.weight.detach(), fn.bias.detach(), fn.eps, out1_dtype=_f32)
+        return y, attns
+
+    def forward(self, src, src_mask: Optional[torch.Tensor] = None,
+                src_key_padding_mask: Optional[torch.Tensor] = None, pos_embs: Optional[torch.Tensor] = None):
+        if self.attention_type == "RelPosMHAXL" and pos_embs is None:
+            raise ValueError("The chosen attention type for the Conformer is RelPosMHAXL. For this attention type, "
+                             "the positional embeddings are mandatory")
+        if src_mask is not None:
+            raise NotImplementedError("src_mask is not supported by the fused attention kernel")
+        B, T, d = src.shape
+        kpm = src_key_padding_mask.to(torch.uint8).contiguous() if src_key_padding_mask is not None else None
+        y, attns = self.run(src.float().reshape(B * T, d).contiguous(), B, T, pos_embs, kpm,
+                            _enc.compute_dtype(), True)
+        return y.view(B, T, d), attns

@@ -1,0 +1,195 @@
+"""Drop-in for speechbrain.nnet.attention: RelPosEncXL, RelPosMHAXL,
+PositionalwiseFeedForward (speechbrain/nnet/attention.py:312-839).
+
+Parameter names and shapes match the reference so checkpoints load with
+strict=True.  RelPosMHAXL self-attention runs as: in_proj GEMM (MFMA) →
+linear_pos GEMM → one fused rel-pos attention kernel (scores, closed-form
+rel_shift, mask, softmax, P·V) → out_proj GEMM.
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+from .. import _enc
+from .activations import Swish
+
+__all__ = ["RelPosEncXL", "RelPosMHAXL", "PositionalwiseFeedForward"]
+
+
+class RelPosEncXL(nn.Module):
+    """attention.py:312-359.  The (1, 2T-1, d) table depends only on T and d;
+    it is built once per (T, device) on the host from the registered
+    inv_freq buffer and cached."""
+
+    def __init__(self, emb_dim):
+        super().__init__()
+        self.emb_dim = emb_dim
+        inv_freq = torch.exp(torch.arange(0, self.emb_dim, 2, dtype=torch.float32)
+                             * -(math.log(10000.0) / self.emb_dim))
+        self.register_buffer("inv_freq", inv_freq)
+        self._cache = {}
+
+    def table(self, seq_len, device, dtype=torch.float32):
+        key = (seq_len, str(device), dtype, self.inv_freq.data_ptr())
+        pe = self._cache.get(key)
+        if pe is None:
+            inv = self.inv_freq.detach().to("cpu", torch.float32)
+            pos = torch.arange(0, seq_len, dtype=torch.float32).unsqueeze(-1)
+            pe_half = torch.zeros(seq_len, self.emb_dim, dtype=torch.float32)
+            pe_half[:, 0::2] = torch.sin(pos * inv)
+            pe_half[:, 1::2] = torch.cos(pos * inv)  # cos(-x) == cos(x): past/future equal
+            pe = torch.cat([torch.flip(pe_half, (0,)), pe_half[1:]], dim=0).unsqueeze(0)
+            pe = pe.to(device=device, dtype=dtype)
+            self._cache = {key: pe}
+        return pe
+
+    def forward(self, x: torch.Tensor):
+        return self.table(x.size(1), x.device, torch.float32 if x.dtype == torch.bfloat16 else x.dtype)
+
+
+class RelPosMHAXL(nn.Module):
+    """attention.py:362-639 (self-attention path)."""
+
+    def __init__(self, embed_dim, num_heads, dropout=0.0, vbias=False, vdim=None, mask_pos_future=False):
+        super().__init__()
+        self.embed_dim = embed_dim
+        self.vdim = vdim if vdim is not None else embed_dim
+        self._qkv_same_embed_dim = self.vdim == embed_dim
+        self.mask_pos_future = mask_pos_future
+        self.vbias = vbias
+        self.num_heads = num_heads
+        self.dropout = dropout
+        self.head_dim = embed_dim // num_heads
+        self.vhead_dim = self.vdim // num_heads
+        assert self.head_dim * num_heads == self.embed_dim, "embed_dim must be divisible by num_heads"
+        assert self.vhead_dim * num_heads == self.vdim, "vdim must be divisible by num_heads"
+        if self._qkv_same_embed_dim is False:
+            self.qk_proj_weight = nn.Parameter(torch.empty(2 * embed_dim, embed_dim))
+            self.v_proj_weight = nn.Parameter(torch.empty(self.vdim, embed_dim))
+        else:
+            self.in_proj_weight = nn.Parameter(torch.empty(3 * embed_dim, embed_dim))
+        if vbias:
+            self.value_bias_weight = nn.Parameter(torch.empty(self.vdim))
+        else:
+            self.vbias = None
+        self.dropout_att = nn.Dropout(dropout)
+        self.out_proj = nn.Linear(self.vdim, embed_dim)
+        self.linear_pos = nn.Linear(embed_dim, embed_dim, bias=False)
+        self.pos_bias_u = nn.Parameter(torch.empty(self.head_dim, self.num_heads))
+        self.pos_bias_v = nn.Parameter(torch.empty(self.head_dim, self.num_heads))
+        if next(self.parameters()).dtype == torch.float16:
+            self.attn_fill_value = -65000
+        else:
+            self.attn_fill_value = -float("inf")
+        self._reset_parameters()
+        self.scale = 1 / math.sqrt(self.embed_dim)
+        self._wc = _enc.WeightCache()
+
+    def _reset_parameters(self):
+        if self._qkv_same_embed_dim:
+            torch.nn.init.xavier_uniform_(self.in_proj_weight)
+        else:
+            torch.nn.init.xavier_uniform_(self.qk_proj_weight)
+            torch.nn.init.xavier_uniform_(self.v_proj_weight)
+        if self.vbias is not None:
+            torch.nn.init.constant_(self.value_bias_weight, 0.0)
+        torch.nn.init.xavier_uniform_(self.pos_bias_u)
+        torch.nn.init.xavier_uniform_(self.pos_bias_v)
+
+    def kernel_weights(self, dtype):
+        """(in_proj, linear_pos, out_proj) weights in the compute dtype."""
+        ps = [self.in_proj_weight, self.linear_pos.weight, self.out_proj.weight]
+        if dtype == torch.float32:
+            return tuple(p.detach() for p in ps)
+        return self._wc.get("bf16", ps, lambda: tuple(_enc.cast_bf16(p.detach().contiguous()) for p in ps))
+
+    def attend(self, x2d, B, T, pos_embs, kpm_u8, dtype, need_weights, residual=None):
+        """Core used by the fused Conformer layer: x2d (B*T, d) in `dtype`.
+        Returns (out (B*T, d) fp32 [+ residual], attn or None)."""
+        if self.vbias is not None:
+            raise NotImplementedError("vbias=True is not on the RelPosMHAXL hot path")
+        w_in, w_pos, w_out = self.kernel_weights(dtype)
+        qkv = _enc.gemm(x2d, w_in, out_dtype=dtype)
+        pos = pos_embs.reshape(-1, self.embed_dim)
+        if pos.dtype != dtype:
+            pos = _enc.cast_bf16(pos.float().contiguous()) if dtype == torch.bfloat16 else pos.float()
+        pk = _enc.gemm(pos.contiguous(), w_pos, out_dtype=dtype)
+        o, probs = _enc.relpos_attention(qkv, pk, self.pos_bias_u.detach(), self.pos_bias_v.detach(), kpm_u8, B, T,
+                                         self.num_heads, self.head_dim, self.scale, need_weights)
+        out = _enc.gemm(o, w_out, bias=self.out_proj.bias.detach(), res=residual, out_dtype=torch.float32)
+        return out, probs
+
+    def forward(self, query, key, value, pos_embs, key_padding_mask=None, attn_mask=None,
+                return_attn_weights=True):
+        """attention.py:485-639.  Self-attention only (query, key and value
+        identical, as in every Conformer call site)."""
+        if not self._qkv_same_embed_dim:
+            raise NotImplementedError  # the reference raises too (attention.py:558)
+        if not ((query is key or torch.equal(query, key)) and (key is value or torch.equal(key, value))):
+            raise NotImplementedError("cross-attention RelPosMHAXL is not on the accelerated path")
+        if attn_mask is not None:
+            raise NotImplementedError("attn_mask is not supported by the fused kernel (encoder passes none)")
+        if self.training and self.dropout > 0:
+            raise NotImplementedError("attention dropout in training mode is not implemented in HIP yet")
+        B, T, d = query.shape
+        dtype = _enc.compute_dtype()
+        x2d = query.reshape(B * T, d)
+        x2d = _enc.to_compute(x2d, dtype)
+        kpm = key_padding_mask.to(torch.uint8).contiguous() if key_padding_mask is not None else None
+        out, attn = self.attend(x2d, B, T, pos_embs, kpm, dtype, return_attn_weights)
+        out = out.view(B, T, d)
+        if return_attn_weights:
+            return out, attn
+        return out
+
+
+class PositionalwiseFeedForward(nn.Module):
+    """attention.py:781-839: Linear → activation → Dropout → Linear, the
+    activation fused into the first GEMM's epilogue."""
+
+    def __init__(self, d_ffn, input_shape=None, input_size=None, dropout=0.0, activation=nn.ReLU):
+        super().__init__()
+        if input_shape is None and input_size is None:
+            raise ValueError("Expected one of input_shape or input_size")
+        if input_size is None:
+            input_size = input_shape[-1]
+        self.ffn = nn.Sequential(nn.Linear(input_size, d_ffn), activation(), nn.Dropout(dropout),
+                                 nn.Linear(d_ffn, input_size))
+        self._wc = _enc.WeightCache()
+
+    def act_name(self):
+        a = self.ffn[1]
+        if isinstance(a, Swish) or type(a).__name__ == "Swish":
+            if getattr(a, "beta", 1) != 1:
+                raise NotImplementedError("Swish(beta != 1) is not fused")
+            return "swish", 0.0
+        if isinstance(a, nn.ReLU):
+            return "relu", 0.0
+        if isinstance(a, nn.LeakyReLU):
+            return "leaky_relu", a.negative_slope
+        if isinstance(a, nn.GELU):
+            return "gelu", 0.0
+        raise NotImplementedError(f"activation {type(a).__name__} is not fused")
+
+    def kernel_weights(self, dtype):
+        ps = [self.ffn[0].weight, self.ffn[3].weight]
+        if dtype == torch.float32:
+            return tuple(p.detach() for p in ps)
+        return self._wc.get("bf16", ps, lambda: tuple(_enc.cast_bf16(p.detach().contiguous()) for p in ps))
+
+    def run(self, u2d, dtype, residual=None, alpha=1.0):
+        """u2d (M, d) in dtype → residual + alpha * FFN(u2d) (fp32)."""
+        w1, w2 = self.kernel_weights(dtype)
+        act, slope = self.act_name()
+        h = _enc.gemm(u2d, w1, bias=self.ffn[0].bias.detach(), act=act, slope=slope, out_dtype=dtype)
+        return _enc.gemm(h, w2, bias=self.ffn[3].bias.detach(), res=residual, alpha=alpha, out_dtype=torch.float32)
+
+    def forward(self, x):
+        if self.training and self.ffn[2].p > 0:
+            raise NotImplementedError("FFN dropout in training mode is not implemented in HIP yet")
+        shp = x.shape
+        dtype = _enc.compute_dtype()
+        u = x.reshape(-1, shp[-1])
+        u = _enc.to_compute(u, dtype)
+        return self.run(u, dtype).view(*shp[:-1], -1)

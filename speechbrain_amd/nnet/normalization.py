@@ -1,0 +1,26 @@
+"""Drop-in for speechbrain.nnet.normalization.LayerNorm (normalization.py:172-223)
+on the HIP LayerNorm kernel (state_dict keys: norm.weight, norm.bias)."""
+import math
+
+import torch
+
+from .. import _enc
+
+
+class LayerNorm(torch.nn.Module):
+    def __init__(self, input_size=None, input_shape=None, eps=1e-05, elementwise_affine=True):
+        super().__init__()
+        self.eps = eps
+        self.elementwise_affine = elementwise_affine
+        if input_shape is not None:
+            input_size = input_shape[2:]
+        self.norm = torch.nn.LayerNorm(input_size, eps=self.eps, elementwise_affine=self.elementwise_affine)
+
+    def forward(self, x):
+        shp = self.norm.normalized_shape
+        D = int(math.prod(shp))
+        if not self.elementwise_affine:
+            raise NotImplementedError("LayerNorm without affine parameters is not on the hot path")
+        y, _ = _enc.layernorm(x.float().reshape(-1, D).contiguous(), self.norm.weight.detach().reshape(-1),
+                              self.norm.bias.detach().reshape(-1), self.eps)
+        return y.view(x.shape)

@@ -1,0 +1,185 @@
+"""HIP encoder kernels (GEMM, LayerNorm, rel-pos attention, conv module,
+conv front-end) and the drop-in modules vs the golden fixtures / CPU oracle.
+fp32 path: within 1e-4 of the reference; bf16 path: sanity bounds."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import assert_close
+import oracle.conformer as OC
+import oracle.features as OF
+
+pytestmark = pytest.mark.gpu
+
+
+def _sub(g, prefix):
+    return {k[len(prefix):]: torch.from_numpy(g[k]) for k in g.files if k.startswith(prefix)}
+
+
+# ----------------------------------------------------------------------------- kernels
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(12032, 768, 256), (1000, 256, 1024), (77, 96, 40), (12032, 256, 640),
+                                   (300, 144, 144)])
+def test_gemm_vs_torch(dev, dtype, M, N, K):
+    from speechbrain_amd import _enc
+    g = torch.Generator().manual_seed(M + N + K)
+    a = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) / math.sqrt(K)
+    bias = torch.randn(N, generator=g)
+    res = torch.randn(M, N, generator=g)
+    ad, wd = a.to(dev, dtype), w.to(dev, dtype)
+    ref_a, ref_w = ad.float().cpu(), wd.float().cpu()  # same rounded operands
+    ref = ref_a @ ref_w.t()
+    tol = 2e-5 if dtype == torch.float32 else 2e-3
+    out = _enc.gemm(ad, wd)
+    assert_close(out, ref, rtol=tol, name="plain")
+    out = _enc.gemm(ad, wd, bias=bias.to(dev), act="swish", res=res.to(dev), alpha=0.5)
+    r2 = res + 0.5 * F.silu(ref + bias)
+    assert_close(out, r2, rtol=tol, name="swish+res")
+    mask = (torch.arange(M) % 7 == 3).to(torch.uint8)
+    out = _enc.gemm(ad, wd, bias=bias.to(dev), act="gelu", rowmask=mask.to(dev), out_dtype=dtype)
+    r3 = F.gelu(ref + bias)
+    r3[mask.bool()] = 0
+    assert_close(out.float(), r3, rtol=tol if dtype == torch.float32 else 1e-2, name="gelu+mask")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_glu_permutation(dev, dtype):
+    from speechbrain_amd.lobes.models.transformer.Conformer import ConvolutionModule
+    from speechbrain_amd import _enc
+    torch.manual_seed(0)
+    d = 128
+    cm = ConvolutionModule(d, 7).to(dev)
+    w1p, b1p, _ = cm.kernel_weights(dtype)
+    u = torch.randn(333, d).to(dev)
+    ud = u.to(dtype)
+    g = _enc.gemm(ud, w1p, bias=b1p, act="glu", out_dtype=torch.float32)
+    w1 = cm.bottleneck[0].weight.detach().reshape(2 * d, d).float()
+    ref = F.glu(ud.float() @ w1.to(dtype).float().t() + cm.bottleneck[0].bias.detach(), dim=-1)
+    assert_close(g, ref, rtol=2e-5 if dtype == torch.float32 else 3e-3, name="glu")
+
+
+def test_layernorm_chain(dev):
+    from speechbrain_amd import _enc
+    x = torch.randn(1000, 256) * 3 + 1
+    w1, b1, w2, b2 = (torch.randn(256) for _ in range(4))
+    y1, y2 = _enc.layernorm(x.to(dev), w1.to(dev), b1.to(dev), 1e-5, torch.float32, w2.to(dev), b2.to(dev), 1e-6,
+                            torch.float32)
+    r1 = F.layer_norm(x, (256,), w1, b1, 1e-5)
+    assert_close(y1, r1, rtol=1e-5)
+    assert_close(y2, F.layer_norm(r1, (256,), w2, b2, 1e-6), rtol=1e-5)
+
+
+# ----------------------------------------------------------------------------- modules vs golden
+def test_conv_frontend_vs_golden(golden, dev):
+    from speechbrain_amd.lobes.models.convolution import ConvolutionFrontEnd
+    g = golden("conformer")
+    cnn = ConvolutionFrontEnd(input_shape=(8, 10, 80), num_blocks=2, num_layers_per_block=1, out_channels=(64, 32),
+                              kernel_sizes=(3, 3), strides=(2, 2), residuals=(False, False))
+    cnn.load_state_dict(_sub(g, "cnn."), strict=True)
+    cnn = cnn.to(dev).eval()
+    with torch.no_grad():
+        out = cnn(torch.from_numpy(g["feats"]).to(dev))
+    assert_close(out, g["cnn_out"], name="cnn")
+
+
+def _tr(g, dev):
+    from speechbrain_amd.lobes.models.transformer.TransformerASR import TransformerASR
+    tr = TransformerASR(tgt_vocab=10, input_size=640, d_model=64, nhead=4, num_encoder_layers=2,
+                        num_decoder_layers=0, d_ffn=128, dropout=0.0, encoder_module="conformer",
+                        attention_type="RelPosMHAXL", normalize_before=True, causal=False)
+    tr.load_state_dict(_sub(g, "tr."), strict=True)
+    return tr.to(dev).eval()
+
+
+def test_transformer_asr_encode_vs_golden(golden, dev):
+    g = golden("conformer")
+    tr = _tr(g, dev)
+    src = torch.from_numpy(g["cnn_out"]).to(dev)
+    with torch.no_grad():
+        assert_close(tr.encode(src, torch.from_numpy(g["wav_len"]).to(dev)), g["enc_out"], name="enc")
+        assert_close(tr.encode(src), g["enc_out_nolen"], name="enc_nolen")
+
+
+def test_conformer_encoder_vs_golden(golden, dev):
+    from speechbrain_amd.lobes.models.transformer.Conformer import ConformerEncoder
+    g = golden("conformer")
+    enc = ConformerEncoder(num_layers=2, d_model=64, d_ffn=128, nhead=4, kernel_size=31)
+    enc.load_state_dict(_sub(g, "enc."), strict=True)
+    enc = enc.to(dev).eval()
+    src = torch.from_numpy(g["enc_src"]).to(dev)
+    kpm = torch.from_numpy(g["enc_kpm"]).to(dev)
+    pe = torch.from_numpy(g["enc_pos"]).to(dev)
+    with torch.no_grad():
+        y, attn = enc(src, src_key_padding_mask=kpm, pos_embs=pe)
+    assert_close(y, g["enc_y"], name="y")
+    assert_close(attn[0], g["enc_attn0"], name="attn0")
+    assert_close(attn[1], g["enc_attn1"], name="attn1")
+    encc = ConformerEncoder(num_layers=1, d_model=64, d_ffn=96, nhead=2, kernel_size=7, causal=True)
+    encc.load_state_dict(_sub(g, "encc."), strict=True)
+    encc = encc.to(dev).eval()
+    with torch.no_grad():
+        yc, _ = encc(src, pos_embs=pe)
+    assert_close(yc, g["encc_y"], name="causal")
+
+
+def test_relpos_mha_module_vs_oracle(dev):
+    """Standalone RelPosMHAXL (d=256, H=4) vs the oracle at a ragged length."""
+    from speechbrain_amd.nnet.attention import RelPosEncXL, RelPosMHAXL
+    torch.manual_seed(0)
+    mha = RelPosMHAXL(embed_dim=256, num_heads=4).eval()
+    sd = {k: v.clone() for k, v in mha.state_dict().items()}
+    x = torch.randn(3, 97, 256)
+    pe = RelPosEncXL(256)(x)
+    kpm = torch.arange(97)[None] >= torch.tensor([97, 60, 5])[:, None]
+    ref, ref_attn = OC.rel_pos_mha(x, pe, sd, "", 4, kpm)
+    mha = mha.to(dev)
+    with torch.no_grad():
+        out, attn = mha(x.to(dev), x.to(dev), x.to(dev), pe.to(dev), key_padding_mask=kpm.to(dev))
+    assert_close(out, ref, name="mha")
+    assert_close(attn, ref_attn, name="attn")
+
+
+def test_encoder_bf16_autocast_close(golden, dev):
+    g = golden("conformer")
+    tr = _tr(g, dev)
+    src = torch.from_numpy(g["cnn_out"]).to(dev)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        y = tr.encode(src, torch.from_numpy(g["wav_len"]).to(dev))
+    ref = torch.from_numpy(g["enc_out"])
+    err = (y.float().cpu() - ref).abs().max().item()
+    assert y.dtype == torch.float32 and err < 0.1, err  # LayerNorm-scale outputs, bf16 operands
+
+
+def _c3_modules(d_model, dev):
+    """BASELINE config 3: ConvolutionFrontEnd + 12-layer Conformer (conformer_small.yaml shapes)."""
+    from speechbrain_amd.lobes.models.convolution import ConvolutionFrontEnd
+    from speechbrain_amd.lobes.models.transformer.TransformerASR import TransformerASR
+    torch.manual_seed(0)
+    cnn = ConvolutionFrontEnd(input_shape=(8, 10, 80), num_blocks=2, num_layers_per_block=1, out_channels=(64, 32),
+                              kernel_sizes=(3, 3), strides=(2, 2), residuals=(False, False))
+    tr = TransformerASR(tgt_vocab=5000, input_size=640, d_model=d_model, nhead=4, num_encoder_layers=12,
+                        num_decoder_layers=0, d_ffn=1024, dropout=0.1, encoder_module="conformer",
+                        attention_type="RelPosMHAXL", normalize_before=True, causal=False)
+    return cnn.to(dev).eval(), tr.to(dev).eval()
+
+
+@pytest.mark.parametrize("d_model", [256, 144])
+def test_full_size_encoder_vs_oracle(dev, d_model):
+    """Fbank → CNN → 12-layer encoder at 15 s, fp32 path vs the CPU oracle on
+    2 utterances (rows are independent, so this checks the full-size kernels)."""
+    from speechbrain_amd.lobes.features import Fbank
+    cnn, tr = _c3_modules(d_model, dev)
+    g = torch.Generator().manual_seed(0)
+    wav = 0.1 * torch.randn(2, 240000, generator=g)
+    with torch.no_grad():
+        feats = Fbank(n_mels=80)(wav.to(dev))
+        y = tr.encode(cnn(feats), torch.ones(2, device=dev))
+    sd_cnn = {k: v.cpu() for k, v in cnn.state_dict().items()}
+    sd_tr = {k: v.cpu() for k, v in tr.state_dict().items()}
+    ref = OC.fbank_to_encoder(wav, sd_cnn, sd_tr, 12, 4, wav_len=torch.ones(2))
+    assert y.shape == (2, 376, d_model)
+    assert_close(y, ref, rtol=1e-4, name="full")
