@@ -1,0 +1,88 @@
+"""Kernel micro-benchmarks on the GPU box (not part of the product):
+per-shape GEMM TFLOP/s for each tile config, attention, dwconv, LN, Fbank.
+    python scripts/kbench.py [gemm|attn|misc|all]
+"""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from speechbrain_amd import _enc  # noqa: E402
+from speechbrain_amd._lib import lib, ptr, stream_of  # noqa: E402
+
+
+def timeit(fn, reps=50, warm=5):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1000.0  # us
+
+
+def gemm_bench():
+    dev = torch.device("cuda")
+    M = 12032
+    shapes = [("ffn_up", 1024, 256, "swish", False, torch.bfloat16), ("ffn_down", 256, 1024, None, True, torch.float32),
+              ("qkv", 768, 256, None, False, torch.bfloat16), ("out_proj", 256, 256, None, True, torch.float32),
+              ("glu", 512, 256, "glu", False, torch.bfloat16), ("src", 256, 640, None, False, torch.float32)]
+    for name, N, K, act, res, od in shapes:
+        a = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        w = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
+        b = torch.randn(N, device=dev)
+        r = torch.randn(M, N // 2 if act == "glu" else N, device=dev) if res else None
+        fl = 2.0 * M * N * K
+        line = f"{name:9s} M={M} N={N} K={K}:"
+        for tile in (1, 2, 3):
+            us = timeit(lambda: _enc.gemm(a, w, bias=b, act=act, res=r, out_dtype=od, tile=tile))
+            line += f"  tile{tile} {us:7.1f}us {fl / us / 1e6:7.1f}TF"
+        us = timeit(lambda: _enc.gemm(a, w, out_dtype=torch.float32, tile=1))
+        line += f" | plain128 {us:6.1f}us {fl / us / 1e6:6.1f}TF"
+        print(line, flush=True)
+
+
+def attn_bench():
+    dev = torch.device("cuda")
+    B, T, H, dh = 32, 376, 4, 64
+    d = H * dh
+    qkv = torch.randn(B * T, 3 * d, device=dev).to(torch.bfloat16)
+    pk = torch.randn(2 * T - 1, d, device=dev).to(torch.bfloat16)
+    u = torch.randn(H * dh, device=dev)
+    v = torch.randn(H * dh, device=dev)
+    us = timeit(lambda: _enc.relpos_attention(qkv, pk, u, v, None, B, T, H, dh, 1 / 16.0))
+    fl = B * H * (2 * T * T * dh * 2 + 2 * T * (T + 64) * dh)
+    print(f"relpos_attn bf16 B={B} T={T}: {us:.1f}us  {fl / us / 1e6:.1f} TF (algorithmic)", flush=True)
+
+
+def misc_bench():
+    dev = torch.device("cuda")
+    M, d = 12032, 256
+    x = torch.randn(M, d, device=dev)
+    w = torch.randn(d, device=dev)
+    us = timeit(lambda: _enc.layernorm(x, w, w, 1e-5, torch.bfloat16))
+    print(f"layernorm {M}x{d}: {us:.1f}us {(M * d * 6) / us / 1e3:.0f} GB/s", flush=True)
+    g = torch.randn(M, d, device=dev).to(torch.bfloat16)
+    cw = torch.randn(d, 1, 31, device=dev)
+    us = timeit(lambda: _enc.dwconv_ln_swish(g, 32, 376, cw, w, False, w, w, 1e-5, torch.bfloat16))
+    print(f"dwconv_ln_swish: {us:.1f}us {(M * d * 4) / us / 1e3:.0f} GB/s", flush=True)
+    from speechbrain_amd.lobes.features import Fbank
+    fb = Fbank(n_mels=80).to(dev)
+    wav = torch.randn(32, 240000, device=dev) * 0.1
+    us = timeit(lambda: fb(wav), reps=20)
+    print(f"fbank 32x15s: {us:.1f}us {(32 * 240000 * 4 + 32 * 1501 * 80 * 4) / us / 1e3:.0f} GB/s", flush=True)
+
+
+if __name__ == "__main__":
+    what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if what in ("gemm", "all"):
+        gemm_bench()
+    if what in ("attn", "all"):
+        attn_bench()
+    if what in ("misc", "all"):
+        misc_bench()

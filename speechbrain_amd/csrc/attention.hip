@@ -3,217 +3,304 @@
 // Reference: speechbrain/nnet/attention.py:485-639 (RelPosMHAXL.forward),
 // rel_shift :468-483.  For query i, key j (T queries = T keys):
 //   score[i,j] = ( (q_i + u)·k_j  +  (q_i + v)·p_{T-1-i+j} ) / sqrt(d_model)
-//   masked (key padding) -> -inf, softmax over j, out_i = Σ_j P[i,j] v_j
-// where p = linear_pos(RelPosEncXL) and rel_shift is applied in closed form
-// (out[i,j] = bd[i, T-1-i+j]) — the (B,H,T,2T-1) bd tensor the reference
-// materialises (145 MB at B=32, T=376) never exists here.
+//   key-padding -> -inf, softmax over j, out_i = Σ_j P[i,j] v_j
+// with p = linear_pos(RelPosEncXL) and rel_shift in closed form
+// (out[i,j] = bd[i, T-1-i+j]); the (B,H,T,2T-1) bd tensor the reference
+// materialises (145 MB at B=32, T=376) never exists.
 //
-// One workgroup = (batch b, head h, BQ=32 query rows); 4 waves.
-//  phase 1: per 64-key chunk, MFMA tiles of (q+u)Kᵀ straight into an fp32
-//           LDS score block S[32][T], and of G = (q+v) P_bandᵀ for the
-//           KC+BQ-1 positional rows the chunk needs; S += G[ii][jj+BQ-1-ii].
-//  phase 2: exact (two-pass) softmax per row in fp32 from LDS; optional fp32
-//           probability output (the reference's returned attention map).
-//  phase 3: O = P·V on MFMA with V staged transposed per chunk.
-// bf16 inputs use v_mfma_f32_16x16x32_bf16, fp32 inputs exact f32 MFMA
-// (see mfma.h); softmax and accumulation are fp32 in both.
+// Flash-style, transposed formulation (MI355X wave64 + 16x16 MFMA):
+//  * workgroup = (b, h, 64 queries), 4 waves x 16 queries; 64-key chunks of
+//    K, V^T and the 127 positional rows the chunk needs are staged in LDS
+//    with 16-B loads, shared by the 4 waves.
+//  * each wave computes S^T = K·Qu^T (4 tiles) — the query sits on the lane,
+//    so softmax statistics are per-lane (+2 xor-shuffles) — and
+//    G^T = P_band·Qv^T (5 tiles); the rel_shift gather S^T[jj][ii] +=
+//    G^T[15-ii+jj][ii] stays inside the lane's column via a 5 KB per-wave
+//    LDS scratch.
+//  * O^T = V^T·P^T accumulates with P taken straight from the S registers
+//    (permuted-k fragments: keys {4g..4g+3, 16+4g..16+4g+3} per 32-key step,
+//    V^T read in the same order) — no LDS round trip for P.
+//  * online softmax (running max / sum, rescale) when no probabilities are
+//    requested; with probabilities (the reference's returned attention map)
+//    a stats pass then an exact pass that writes P and accumulates P·V.
+// bf16 operands use v_mfma_f32_16x16x32_bf16, fp32 operands exact f32 MFMA
+// (mfma.h); softmax and accumulators are fp32.
 #include "mfma.h"
 
 using namespace sbk;
 
 namespace {
 
-constexpr int BQ = 32;
-constexpr int KC = 64;
+constexpr int QB = 64;        // queries per workgroup
+constexpr int KC = 64;        // keys per chunk
+constexpr int PBR = KC + QB;  // positional band rows staged per chunk (127 used)
+constexpr int GR = 80;        // G^T rows per wave (79 used)
+constexpr int GS = 17;        // G^T scratch row stride (floats)
 
 template <typename T, int DHP>
-struct AttnLds {
+struct FlashLds {
   static constexpr int PAD = MT<T>::PAD;
-  static constexpr int QR = DHP + PAD;      // row stride of Qu/Qv/Kc/Pc (elements)
-  static constexpr int GR = KC + BQ + 4;    // fp32 G row stride
-  static constexpr int VR = KC + PAD;       // Vt row stride
-  static size_t bytes(int Tp) {
-    const size_t q = (size_t)2 * BQ * QR * sizeof(T);
-    const size_t s = (size_t)BQ * (Tp + 4) * 4;
-    const size_t p1 = (size_t)KC * QR * sizeof(T) + (size_t)(KC + BQ) * QR * sizeof(T) + (size_t)BQ * GR * 4;
-    const size_t p3 = (size_t)BQ * (Tp + PAD) * sizeof(T) + (size_t)DHP * VR * sizeof(T);
-    auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
-    return al(q) + al(s) + al(p1 > p3 ? p1 : p3);
-  }
+  static constexpr int KR = DHP + PAD;  // Ks / Ps row stride
+  static constexpr int VR = KC + PAD;   // Vt row stride
+  static constexpr size_t ks = (size_t)KC * KR * sizeof(T);
+  static constexpr size_t vt = (size_t)DHP * VR * sizeof(T);
+  static constexpr size_t ps = (size_t)PBR * KR * sizeof(T);
+  static constexpr size_t gs = (size_t)4 * GR * GS * 4;
+  static constexpr size_t ms = (size_t)KC * 4;
+  static constexpr size_t bytes = ks + vt + ps + gs + ms;
 };
 
-template <typename T, int DHP>
-__global__ void __launch_bounds__(256) relpos_attn_kernel(const T* __restrict__ qkv, const T* __restrict__ pk,
-                                                          const float* __restrict__ pbu, const float* __restrict__ pbv,
-                                                          const uint8_t* __restrict__ kpm, int B, int Tn, int H,
-                                                          int dh, float scale, T* __restrict__ out,
-                                                          float* __restrict__ probs) {
+template <typename T, int DHP, bool PROBS>
+__global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__ qkv, const T* __restrict__ pk,
+                                                           const float* __restrict__ pbu,
+                                                           const float* __restrict__ pbv,
+                                                           const uint8_t* __restrict__ kpm, int B, int Tn, int H,
+                                                           int dh, float scale, T* __restrict__ out,
+                                                           float* __restrict__ probs, int vec_ok) {
   using Tr = MT<T>;
-  using L = AttnLds<T, DHP>;
-  constexpr int QR = L::QR, GR = L::GR, VR = L::VR, PAD = L::PAD;
-  const int Tp = (Tn + KC - 1) / KC * KC;
-  const int SR = Tp + 4;
-  const int PR = Tp + PAD;
-  const int d_model = H * dh;
-  const int qrow3 = 3 * d_model;  // qkv row length
-
+  using L = FlashLds<T, DHP>;
+  constexpr int KR = L::KR, VR = L::VR, VEC = Tr::VEC;
+  constexpr int KS = DHP / 32;   // k-steps over the head dim
+  constexpr int NDT = DHP / 16;  // O^T tiles (head-dim rows)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
-  T* Qu = reinterpret_cast<T*>(smem);
-  T* Qv = Qu + BQ * QR;
-  float* S = reinterpret_cast<float*>(smem + al((size_t)2 * BQ * QR * sizeof(T)));
-  unsigned char* r1 = reinterpret_cast<unsigned char*>(S) + al((size_t)BQ * SR * 4);
-  T* Kc = reinterpret_cast<T*>(r1);
-  T* Pc = Kc + KC * QR;
-  float* G = reinterpret_cast<float*>(r1 + (size_t)KC * QR * sizeof(T) + (size_t)(KC + BQ) * QR * sizeof(T));
-  T* Pb = reinterpret_cast<T*>(r1);
-  T* Vt = Pb + BQ * PR;
+  T* Ks = reinterpret_cast<T*>(smem);
+  T* Vt = reinterpret_cast<T*>(smem + L::ks);
+  T* Ps = reinterpret_cast<T*>(smem + L::ks + L::vt);
+  float* Gs = reinterpret_cast<float*>(smem + L::ks + L::vt + L::ps);
+  float* Ms = reinterpret_cast<float*>(smem + L::ks + L::vt + L::ps + L::gs);
 
-  const int nqt = (Tn + BQ - 1) / BQ;
-  const int qt = blockIdx.x % nqt;
-  const int bh = blockIdx.x / nqt;
+  const int d_model = H * dh;
+  const long long row3 = 3LL * d_model;
+  const int nqb = (Tn + QB - 1) / QB;
+  const int qb = blockIdx.x % nqb;
+  const int bh = blockIdx.x / nqb;
   const int h = bh % H, b = bh / H;
-  const int i0 = qt * BQ;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int fr = lane & 15, fk = 8 * (lane >> 4);
-  const T* qkv_b = qkv + (long long)b * Tn * qrow3 + h * 3 * dh;
+  const int i0 = qb * QB;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c16 = lane & 15, g = lane >> 4;
+  const int i0w = i0 + 16 * w;
+  const int my_i = i0w + c16;  // this lane's query
+  const T* qkv_b = qkv + (long long)b * Tn * row3 + h * 3 * dh;
+  const T* pk_h = pk + h * dh;
+  float* Gw = Gs + w * GR * GS;
 
-  // ---- Q + u, Q + v into LDS (zero padded rows/dims) ----
-  for (int e = tid; e < BQ * DHP; e += 256) {
-    const int ii = e / DHP, d = e - ii * DHP;
-    const int i = i0 + ii;
-    float q = 0.f, u = 0.f, v = 0.f;
-    if (i < Tn && d < dh) {
-      q = Tr::to_f32(qkv_b[(long long)i * qrow3 + d]);
-      u = pbu[h * dh + d];
-      v = pbv[h * dh + d];
+  // ---- Qu / Qv as B-operand fragments (query on the lane) ----
+  typename Tr::frag fqu[KS], fqv[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    float qu[8], qv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int d = 32 * s + 8 * g + e;
+      float q = 0.f, u = 0.f, v = 0.f;
+      if (my_i < Tn && d < dh) {
+        q = Tr::to_f32(qkv_b[(long long)my_i * row3 + d]);
+        u = pbu[h * dh + d];
+        v = pbv[h * dh + d];
+        qu[e] = q + u;
+        qv[e] = q + v;
+      } else {
+        qu[e] = 0.f;
+        qv[e] = 0.f;
+      }
     }
-    Qu[ii * QR + d] = Tr::from_f32(i < Tn && d < dh ? q + u : 0.f);
-    Qv[ii * QR + d] = Tr::from_f32(i < Tn && d < dh ? q + v : 0.f);
+    fqu[s] = Tr::from8(qu);
+    fqv[s] = Tr::from8(qv);
   }
 
-  // ---- phase 1: scores ----
-  const int ntiles_s = (BQ / 16) * (KC / 16);            // 8
-  const int ntiles_g = (BQ / 16) * ((KC + BQ) / 16);     // 12
-  for (int j0 = 0; j0 < Tp; j0 += KC) {
-    __syncthreads();  // previous chunk's readers of Kc/Pc/G are done (and Q staged)
-    for (int e = tid; e < KC * DHP; e += 256) {
-      const int jj = e / DHP, d = e - jj * DHP;
-      const int j = j0 + jj;
-      Kc[jj * QR + d] = (j < Tn && d < dh) ? qkv_b[(long long)j * qrow3 + dh + d] : Tr::from_f32(0.f);
-    }
-    const int rbase = Tn - BQ - i0 + j0;
-    for (int e = tid; e < (KC + BQ) * DHP; e += 256) {
-      const int rr = e / DHP, d = e - rr * DHP;
-      const int r = rbase + rr;
-      Pc[rr * QR + d] = (rr < KC + BQ - 1 && r >= 0 && r <= 2 * Tn - 2 && d < dh)
-                            ? pk[(long long)r * d_model + h * dh + d]
-                            : Tr::from_f32(0.f);
-    }
-    __syncthreads();
-    for (int t = wid; t < ntiles_s + ntiles_g; t += 4) {
-      const bool isg = t >= ntiles_s;
-      const int tt = isg ? t - ntiles_s : t;
-      const int ncol = isg ? (KC + BQ) / 16 : KC / 16;
-      const int tm = tt / ncol, tn = tt - tm * ncol;
-      const T* a = (isg ? Qv : Qu) + (tm * 16 + fr) * QR + fk;
-      const T* bm = (isg ? Pc : Kc) + (tn * 16 + fr) * QR + fk;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+  f32x4 acc_o[NDT];
 #pragma unroll
-      for (int ks = 0; ks < DHP / 32; ++ks) Tr::mma(acc, Tr::load(a + ks * 32), Tr::load(bm + ks * 32));
+  for (int t = 0; t < NDT; ++t) acc_o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int Tp = (Tn + KC - 1) / KC * KC;
+  constexpr int NPASS = PROBS ? 2 : 1;
+  for (int pass = 0; pass < NPASS; ++pass) {
+    const bool stats_only = PROBS && pass == 0;
+    for (int j0 = 0; j0 < Tp; j0 += KC) {
+      __syncthreads();  // previous chunk's readers done
+      // ---- stage K rows, V^T, positional band rows, key mask ----
+      const int rbase = Tn - QB - i0 + j0;
+      if (vec_ok) {
+        constexpr int CPR = DHP / VEC;
+        for (int c = tid; c < KC * CPR; c += 256) {
+          const int r = c / CPR, d = (c % CPR) * VEC;
+          const int j = j0 + r;
+          uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+          if (j < Tn && d < dh) {
+            kv = *reinterpret_cast<const uint4*>(qkv_b + (long long)j * row3 + dh + d);
+            if (!stats_only) vv = *reinterpret_cast<const uint4*>(qkv_b + (long long)j * row3 + 2 * dh + d);
+          }
+          *reinterpret_cast<uint4*>(Ks + r * KR + d) = kv;
+          if (!stats_only) {
+            const T* ve = reinterpret_cast<const T*>(&vv);
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) Vt[(d + e) * VR + r] = ve[e];
+          }
+        }
+        for (int c = tid; c < PBR * CPR; c += 256) {
+          const int rr = c / CPR, d = (c % CPR) * VEC;
+          const int r = rbase + rr;
+          uint4 pv = make_uint4(0, 0, 0, 0);
+          if (rr < PBR - 1 && r >= 0 && r <= 2 * Tn - 2 && d < dh)
+            pv = *reinterpret_cast<const uint4*>(pk_h + (long long)r * d_model + d);
+          *reinterpret_cast<uint4*>(Ps + rr * KR + d) = pv;
+        }
+      } else {
+        for (int e = tid; e < KC * DHP; e += 256) {
+          const int r = e / DHP, d = e - r * DHP;
+          const int j = j0 + r;
+          const bool ok = j < Tn && d < dh;
+          Ks[r * KR + d] = ok ? qkv_b[(long long)j * row3 + dh + d] : Tr::from_f32(0.f);
+          if (!stats_only) Vt[d * VR + r] = ok ? qkv_b[(long long)j * row3 + 2 * dh + d] : Tr::from_f32(0.f);
+        }
+        for (int e = tid; e < PBR * DHP; e += 256) {
+          const int rr = e / DHP, d = e - rr * DHP;
+          const int r = rbase + rr;
+          Ps[rr * KR + d] = (rr < PBR - 1 && r >= 0 && r <= 2 * Tn - 2 && d < dh) ? pk_h[(long long)r * d_model + d]
+                                                                                  : Tr::from_f32(0.f);
+        }
+      }
+      if (tid < KC) {
+        const int j = j0 + tid;
+        Ms[tid] = (j < Tn && !(kpm && kpm[(long long)b * Tn + j])) ? 0.f : -INFINITY;
+      }
+      __syncthreads();
+
+      // ---- S^T (keys x queries) and G^T (band rows x queries) ----
+      f32x4 acc_s[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        acc_s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const T* a = Ks + (16 * t + c16) * KR + 8 * g;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) Tr::mma(acc_s[t], Tr::load(a + 32 * s), fqu[s]);
+      }
+      const int pofs = 48 - 16 * w;
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        f32x4 acc_g = {0.f, 0.f, 0.f, 0.f};
+        const T* a = Ps + (pofs + 16 * t + c16) * KR + 8 * g;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) Tr::mma(acc_g, Tr::load(a + 32 * s), fqv[s]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Gw[(16 * t + 4 * g + r) * GS + c16] = acc_g[r];
+      }
+      __syncthreads();  // G^T scratch visible to the wave's other lanes
+
+      // ---- scores for this lane's query: keys jj = 16t + 4g + r ----
+      float sc[4][4];
+      float cmax = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int jj = 16 * t + 4 * g + r;
+          const float v = (acc_s[t][r] + Gw[(15 - c16 + jj) * GS + c16]) * scale + Ms[jj];
+          sc[t][r] = v;
+          cmax = fmaxf(cmax, v);
+        }
+      cmax = fmaxf(cmax, __shfl_xor(cmax, 16));
+      cmax = fmaxf(cmax, __shfl_xor(cmax, 32));
+
+      if (stats_only) {
+        const float m_new = fmaxf(m_run, cmax);
+        const float mref = m_new == -INFINITY ? 0.f : m_new;
+        float ls = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ls += expf(sc[t][r] - mref);
+        ls += __shfl_xor(ls, 16);
+        ls += __shfl_xor(ls, 32);
+        l_run = l_run * expf(m_run - mref) + ls;
+        m_run = m_new;
+        continue;
+      }
+
+      float p[4][4];
+      if (PROBS) {
+        // exact pass: final max / sum known
+        const float mref = m_run == -INFINITY ? 0.f : m_run;
+        const float inv = 1.0f / l_run;
+        float* prow = probs + (((long long)b * H + h) * Tn + my_i) * Tn;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int j = j0 + 16 * t + 4 * g + r;
+            p[t][r] = expf(sc[t][r] - mref) * inv;
+            if (my_i < Tn && j < Tn) prow[j] = p[t][r];
+          }
+      } else {
+        const float m_new = fmaxf(m_run, cmax);
+        const float mref = m_new == -INFINITY ? 0.f : m_new;
+        const float alpha = expf(m_run - mref);
+        float ls = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            p[t][r] = expf(sc[t][r] - mref);
+            ls += p[t][r];
+          }
+        ls += __shfl_xor(ls, 16);
+        ls += __shfl_xor(ls, 32);
+        l_run = l_run * alpha + ls;
+        m_run = m_new;
+#pragma unroll
+        for (int t = 0; t < NDT; ++t) acc_o[t] *= alpha;
+      }
+      // ---- O^T += V^T · P^T  (2 k-steps of 32 keys) ----
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        float pv[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pv[r] = p[2 * s2][r];
+          pv[4 + r] = p[2 * s2 + 1][r];
+        }
+        const typename Tr::frag fp = Tr::from8(pv);
+#pragma unroll
+        for (int t = 0; t < NDT; ++t) {
+          const T* vrow = Vt + (16 * t + c16) * VR + 32 * s2 + 4 * g;
+          Tr::mma(acc_o[t], Tr::load2x4(vrow, vrow + 16), fp);
+        }
+      }
+    }
+  }
+  // ---- write O (row = this lane's query, cols d = 16t + 4g + r) ----
+  if (my_i < Tn) {
+    const float inv = PROBS ? 1.0f : 1.0f / l_run;
+    T* orow = out + ((long long)b * Tn + my_i) * d_model + h * dh;
+#pragma unroll
+    for (int t = 0; t < NDT; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int ii = tm * 16 + 4 * (lane >> 4) + r;
-        const int jj = tn * 16 + fr;
-        if (isg)
-          G[ii * GR + jj] = acc[r];
-        else
-          S[ii * SR + j0 + jj] = acc[r];
+        const int d = 16 * t + 4 * g + r;
+        if (d < dh) orow[d] = Tr::from_f32(acc_o[t][r] * inv);
       }
-    }
-    __syncthreads();
-    for (int e = tid; e < BQ * KC; e += 256) {
-      const int ii = e / KC, jj = e - ii * KC;
-      const int j = j0 + jj;
-      float s = (S[ii * SR + j] + G[ii * GR + jj + BQ - 1 - ii]) * scale;
-      if (j >= Tn || (kpm && kpm[(long long)b * Tn + j])) s = -INFINITY;
-      S[ii * SR + j] = s;
-    }
-  }
-  __syncthreads();
-
-  // ---- phase 2: softmax rows (wave per row) ----
-  for (int ii = wid; ii < BQ; ii += 4) {
-    const int i = i0 + ii;
-    float* srow = S + ii * SR;
-    float m = -INFINITY;
-    for (int j = lane; j < Tn; j += 64) m = fmaxf(m, srow[j]);
-    m = wave_max(m);
-    float sum = 0.f;
-    for (int j = lane; j < Tn; j += 64) {
-      const float e = expf(srow[j] - m);
-      srow[j] = e;
-      sum += e;
-    }
-    sum = wave_sum(sum);
-    const float inv = 1.0f / sum;
-    float* prow = (probs && i < Tn) ? probs + (((long long)b * H + h) * Tn + i) * Tn : nullptr;
-    for (int j = lane; j < Tp; j += 64) {
-      float p = 0.f;
-      if (j < Tn && i < Tn) {
-        p = srow[j] * inv;
-        if (prow) prow[j] = p;
-      }
-      Pb[ii * PR + j] = Tr::from_f32(p);
-    }
-  }
-
-  // ---- phase 3: O = P V ----
-  constexpr int NT3 = (BQ / 16) * (DHP / 16) / 4;  // output tiles per wave
-  f32x4 acc[NT3];
-#pragma unroll
-  for (int q = 0; q < NT3; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int j0 = 0; j0 < Tp; j0 += KC) {
-    __syncthreads();  // Pb complete / previous Vt consumers done
-    for (int e = tid; e < KC * DHP; e += 256) {
-      const int jj = e / DHP, d = e - jj * DHP;
-      const int j = j0 + jj;
-      Vt[d * VR + jj] = (j < Tn && d < dh) ? qkv_b[(long long)j * qrow3 + 2 * dh + d] : Tr::from_f32(0.f);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < NT3; ++q) {
-      const int t = wid + 4 * q;
-      const int tm = t / (DHP / 16), tn = t - tm * (DHP / 16);
-      const T* a = Pb + (tm * 16 + fr) * PR + j0 + fk;
-      const T* bm = Vt + (tn * 16 + fr) * VR + fk;
-#pragma unroll
-      for (int ks = 0; ks < KC / 32; ++ks) Tr::mma(acc[q], Tr::load(a + ks * 32), Tr::load(bm + ks * 32));
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < NT3; ++q) {
-    const int t = wid + 4 * q;
-    const int tm = t / (DHP / 16), tn = t - tm * (DHP / 16);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = i0 + tm * 16 + 4 * (lane >> 4) + r;
-      const int d = tn * 16 + fr;
-      if (i < Tn && d < dh) out[((long long)b * Tn + i) * d_model + h * dh + d] = Tr::from_f32(acc[q][r]);
-    }
   }
 }
 
 template <typename T, int DHP>
 int launch(const void* qkv, const void* pk, const float* pbu, const float* pbv, const uint8_t* kpm, int B, int Tn,
            int H, int dh, float scale, void* out, float* probs, hipStream_t s) {
-  const int Tp = (Tn + KC - 1) / KC * KC;
-  const size_t lds = AttnLds<T, DHP>::bytes(Tp);
-  if (lds > 160 * 1024) return SBK_ERR_ARG;
-  const int grid = B * H * ((Tn + BQ - 1) / BQ);
-  hipLaunchKernelGGL((relpos_attn_kernel<T, DHP>), dim3(grid), dim3(256), lds, s, reinterpret_cast<const T*>(qkv),
-                     reinterpret_cast<const T*>(pk), pbu, pbv, kpm, B, Tn, H, dh, scale, reinterpret_cast<T*>(out),
-                     probs);
+  constexpr size_t lds = FlashLds<T, DHP>::bytes;
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  const int grid = B * H * ((Tn + QB - 1) / QB);
+  const int VEC = MT<T>::VEC;
+  const int d_model = H * dh;
+  const int vec_ok = (dh % VEC == 0) && (d_model % VEC == 0) &&
+                     ((reinterpret_cast<uintptr_t>(qkv) | reinterpret_cast<uintptr_t>(pk)) % 16 == 0);
+  if (probs)
+    hipLaunchKernelGGL((relpos_flash_kernel<T, DHP, true>), dim3(grid), dim3(256), lds, s,
+                       reinterpret_cast<const T*>(qkv), reinterpret_cast<const T*>(pk), pbu, pbv, kpm, B, Tn, H, dh,
+                       scale, reinterpret_cast<T*>(out), probs, vec_ok);
+  else
+    hipLaunchKernelGGL((relpos_flash_kernel<T, DHP, false>), dim3(grid), dim3(256), lds, s,
+                       reinterpret_cast<const T*>(qkv), reinterpret_cast<const T*>(pk), pbu, pbv, kpm, B, Tn, H, dh,
+                       scale, reinterpret_cast<T*>(out), probs, vec_ok);
   SBK_CHECK_LAUNCH();
   return 0;
 }
@@ -236,7 +323,7 @@ SBK_API int sbk_relpos_attention(int dtype_bf16, const void* qkv, const void* pk
 }
 
 SBK_API long long sbk_relpos_attention_lds(int dtype_bf16, int Tn, int dh) {
-  const int Tp = (Tn + KC - 1) / KC * KC;
-  if (dtype_bf16) return dh <= 64 ? (long long)AttnLds<bf16_t, 64>::bytes(Tp) : (long long)AttnLds<bf16_t, 128>::bytes(Tp);
-  return dh <= 64 ? (long long)AttnLds<float, 64>::bytes(Tp) : (long long)AttnLds<float, 128>::bytes(Tp);
+  (void)Tn;
+  if (dtype_bf16) return dh <= 64 ? (long long)FlashLds<bf16_t, 64>::bytes : (long long)FlashLds<bf16_t, 128>::bytes;
+  return dh <= 64 ? (long long)FlashLds<float, 64>::bytes : (long long)FlashLds<float, 128>::bytes;
 }

@@ -88,17 +88,76 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
 
 // Depthwise Conv1d over time (zero padding padL left / K-1-padL right)
 // + bias -> LayerNorm over channels -> Swish.  x: (B, T, C) T-typed.
-// Block = TT timesteps of one sequence; conv results staged in LDS, then one
-// wave per timestep normalises.
-template <typename T>
+// Block = TT timesteps of one sequence.  Phase 1: one thread per channel
+// keeps its K taps and its (TT + K - 1)-sample input window in registers
+// (K, TT compile-time) and writes TT conv outputs to LDS; phase 2: one wave
+// per timestep normalises across channels and applies Swish.
+template <typename T, int K, int TT>
 __global__ void __launch_bounds__(256) dwconv_ln_swish_kernel(const T* __restrict__ x, int B, int Tn, int C,
-                                                              const float* __restrict__ w, const float* __restrict__ bias,
-                                                              int K, int padL, const float* __restrict__ g,
+                                                              const float* __restrict__ w,
+                                                              const float* __restrict__ bias, int padL,
+                                                              const float* __restrict__ g,
                                                               const float* __restrict__ beta, float eps, void* out,
-                                                              int out_bf16, int TT) {
+                                                              int out_bf16) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* xin = reinterpret_cast<float*>(smem);      // (TT + K - 1) x C
-  float* cv = xin + (TT + K - 1) * C;               // TT x C
+  float* cv = reinterpret_cast<float*>(smem);  // TT x C
+  const int ntile = (Tn + TT - 1) / TT;
+  const int b = blockIdx.x / ntile;
+  const int t0 = (blockIdx.x - b * ntile) * TT;
+  const int nt = min(TT, Tn - t0);
+  const T* xb = x + (long long)b * Tn * C;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float wk[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) wk[k] = w[c * K + k];
+    float win[TT + K - 1];
+#pragma unroll
+    for (int r = 0; r < TT + K - 1; ++r) {
+      const int t = t0 - padL + r;
+      win[r] = (t >= 0 && t < Tn) ? ld(xb, (long long)t * C + c) : 0.f;
+    }
+    const float bc = bias ? bias[c] : 0.f;
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt) {
+      float acc = bc;
+#pragma unroll
+      for (int k = 0; k < K; ++k) acc = fmaf(wk[k], win[tt + k], acc);
+      cv[tt * C + c] = acc;
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int tt = wid; tt < nt; tt += 4) {
+    const float* r = cv + tt * C;
+    float s = 0.f;
+    for (int c = lane; c < C; c += 64) s += r[c];
+    const float mean = wave_sum(s) / C;
+    float q = 0.f;
+    for (int c = lane; c < C; c += 64) {
+      const float d = r[c] - mean;
+      q += d * d;
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
+    const long long ob = ((long long)b * Tn + t0 + tt) * C;
+    for (int c = lane; c < C; c += 64) {
+      float y = (r[c] - mean) * rstd * g[c] + beta[c];
+      y = y * (1.0f / (1.0f + expf(-y)));
+      st(out, ob + c, y, out_bf16);
+    }
+  }
+}
+
+// Generic-K fallback: input rows staged in LDS, taps read per channel.
+template <typename T>
+__global__ void __launch_bounds__(256) dwconv_ln_swish_generic(const T* __restrict__ x, int B, int Tn, int C,
+                                                               const float* __restrict__ w,
+                                                               const float* __restrict__ bias, int K, int padL,
+                                                               const float* __restrict__ g,
+                                                               const float* __restrict__ beta, float eps, void* out,
+                                                               int out_bf16, int TT) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* xin = reinterpret_cast<float*>(smem);  // (TT + K - 1) x C
+  float* cv = xin + (TT + K - 1) * C;          // TT x C
   const int ntile = (Tn + TT - 1) / TT;
   const int b = blockIdx.x / ntile;
   const int t0 = (blockIdx.x - b * ntile) * TT;
@@ -318,17 +377,30 @@ SBK_API int sbk_dwconv_ln_swish(int in_bf16, const void* x, int B, int Tn, int C
                                 int out_bf16, void* stream) {
   if (B <= 0 || Tn <= 0 || C <= 0 || K <= 0) return SBK_ERR_ARG;
   const int padL = causal ? K - 1 : (K - 1) / 2;
+  hipStream_t s = (hipStream_t)stream;
+  if (K == 31 && (size_t)16 * C * 4 <= 64 * 1024) {
+    constexpr int TT = 16;
+    const int grid = B * ((Tn + TT - 1) / TT);
+    const size_t lds = (size_t)TT * C * 4;
+    if (in_bf16)
+      hipLaunchKernelGGL((dwconv_ln_swish_kernel<bf16_t, 31, TT>), dim3(grid), dim3(256), lds, s,
+                         reinterpret_cast<const bf16_t*>(x), B, Tn, C, w, bias, padL, g, beta, eps, out, out_bf16);
+    else
+      hipLaunchKernelGGL((dwconv_ln_swish_kernel<float, 31, TT>), dim3(grid), dim3(256), lds, s,
+                         reinterpret_cast<const float*>(x), B, Tn, C, w, bias, padL, g, beta, eps, out, out_bf16);
+    SBK_CHECK_LAUNCH();
+    return 0;
+  }
   int TT = 16;
   auto lds = [&](int tt) { return (size_t)((tt + K - 1) + tt) * C * 4; };
   while (TT > 1 && lds(TT) > 64 * 1024) TT >>= 1;
   if (lds(TT) > 160 * 1024) return SBK_ERR_ARG;
   const int grid = B * ((Tn + TT - 1) / TT);
-  hipStream_t s = (hipStream_t)stream;
   if (in_bf16)
-    hipLaunchKernelGGL(dwconv_ln_swish_kernel<bf16_t>, dim3(grid), dim3(256), lds(TT), s,
+    hipLaunchKernelGGL(dwconv_ln_swish_generic<bf16_t>, dim3(grid), dim3(256), lds(TT), s,
                        reinterpret_cast<const bf16_t*>(x), B, Tn, C, w, bias, K, padL, g, beta, eps, out, out_bf16, TT);
   else
-    hipLaunchKernelGGL(dwconv_ln_swish_kernel<float>, dim3(grid), dim3(256), lds(TT), s,
+    hipLaunchKernelGGL(dwconv_ln_swish_generic<float>, dim3(grid), dim3(256), lds(TT), s,
                        reinterpret_cast<const float*>(x), B, Tn, C, w, bias, K, padL, g, beta, eps, out, out_bf16, TT);
   SBK_CHECK_LAUNCH();
   return 0;

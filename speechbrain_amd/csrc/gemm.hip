@@ -124,69 +124,100 @@ __global__ void __launch_bounds__(256) gemm_kernel(const T* __restrict__ A, int 
     cur ^= 1;
   }
 
-  // ---- epilogue ----
-  const int rbase = m0 + wm * WM + 4 * (lane >> 4);
-  const int cbase = n0 + wn * WN + fr;
-  if (ep.act == ACT_GLU) {
-    // wave column span [n0 + wn*WN, +WN): first half = value channels, second = gates
-    const int ocol0 = (n0 + wn * WN) / 2;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN / 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = rbase + i * 16 + r;
-          const int ca = cbase + j * 16, cb = ca + WN / 2;
-          const int oc = ocol0 + j * 16 + fr;
-          if (row >= M || cb >= N) continue;
-          float va = acc[i][j][r], vb = acc[i][j + TN / 2][r];
-          if (ep.bias) {
-            va += ep.bias[ca];
-            vb += ep.bias[cb];
-          }
-          float v = va * (1.0f / (1.0f + expf(-vb)));
-          if (ep.rowmask && ep.rowmask[row]) v = 0.f;
-          v *= ep.alpha;
-          if (ep.res) v += ep.res[(long long)row * ep.ldr + oc];
-          if (ep.out_bf16)
-            reinterpret_cast<bf16_t*>(ep.out)[(long long)row * ep.ldc + oc] = f32_to_bf16(v);
-          else
-            reinterpret_cast<float*>(ep.out)[(long long)row * ep.ldc + oc] = v;
-        }
-    return;
-  }
+  // ---- epilogue: accumulators -> LDS C tile -> coalesced vector pass ----
+  // (the staging ring is free: the last loop iteration ended with a barrier)
+  constexpr int CR = BN + 4;  // C tile row stride (floats)
+  float* Cs = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = rbase + i * 16 + r;
-        const int col = cbase + j * 16;
-        if (row >= M || col >= N) continue;
-        float v = acc[i][j][r];
-        if (ep.bias) v += ep.bias[col];
-        if (ep.act == ACT_SWISH)
-          v = v * (1.0f / (1.0f + expf(-v)));
-        else if (ep.act == ACT_LRELU)
-          v = v >= 0.f ? v : v * ep.slope;
-        else if (ep.act == ACT_GELU)
-          v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
-        if (ep.rowmask && ep.rowmask[row]) v = 0.f;
-        v *= ep.alpha;
-        if (ep.res) v += ep.res[(long long)row * ep.ldr + col];
-        if (ep.out_bf16)
-          reinterpret_cast<bf16_t*>(ep.out)[(long long)row * ep.ldc + col] = f32_to_bf16(v);
-        else
-          reinterpret_cast<float*>(ep.out)[(long long)row * ep.ldc + col] = v;
+      for (int r = 0; r < 4; ++r)
+        Cs[(wm * WM + i * 16 + 4 * (lane >> 4) + r) * CR + wn * WN + j * 16 + fr] = acc[i][j][r];
+  __syncthreads();
+  const bool glu = ep.act == ACT_GLU;
+  const int ncols = glu ? BN / 2 : BN;       // output columns of this tile
+  const int oc0 = glu ? n0 / 2 : n0;         // first output column
+  const int nout = glu ? N / 2 : N;
+  for (int c = tid; c < BM * (ncols / 4); c += 256) {
+    const int r = c / (ncols / 4), o = (c % (ncols / 4)) * 4;
+    const int row = m0 + r;
+    if (row >= M || oc0 + o >= nout) continue;
+    float v[4];
+    if (glu) {
+      const int q = o >> 4, wi = o & 15;
+      const int ca = 32 * q + wi, cg = ca + 16;  // [value16 | gate16] column groups
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float va = Cs[r * CR + ca + e], vg = Cs[r * CR + cg + e];
+        if (ep.bias) {
+          va += ep.bias[n0 + ca + e];
+          vg += ep.bias[n0 + cg + e];
+        }
+        v[e] = va * (1.0f / (1.0f + __expf(-vg)));
       }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x = Cs[r * CR + o + e];
+        if (ep.bias) x += ep.bias[n0 + o + e];
+        if (ep.act == ACT_SWISH)
+          x = x * (1.0f / (1.0f + __expf(-x)));
+        else if (ep.act == ACT_LRELU)
+          x = x >= 0.f ? x : x * ep.slope;
+        else if (ep.act == ACT_GELU)
+          x = 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+        v[e] = x;
+      }
+    }
+    const bool masked = ep.rowmask && ep.rowmask[row];
+    const long long oc = oc0 + o;
+    const bool full = oc + 3 < nout;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (masked ? 0.f : v[e]) * ep.alpha;
+    if (ep.res) {
+      const float* rp = ep.res + (long long)row * ep.ldr + oc;
+      if (full && ((reinterpret_cast<uintptr_t>(rp) & 15) == 0)) {
+        const float4 rv = *reinterpret_cast<const float4*>(rp);
+        v[0] += rv.x; v[1] += rv.y; v[2] += rv.z; v[3] += rv.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (oc + e < nout) v[e] += rp[e];
+      }
+    }
+    if (ep.out_bf16) {
+      bf16_t* op = reinterpret_cast<bf16_t*>(ep.out) + (long long)row * ep.ldc + oc;
+      if (full && ((reinterpret_cast<uintptr_t>(op) & 7) == 0)) {
+        uint2 pk;
+        pk.x = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
+        pk.y = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
+        *reinterpret_cast<uint2*>(op) = pk;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (oc + e < nout) op[e] = f32_to_bf16(v[e]);
+      }
+    } else {
+      float* op = reinterpret_cast<float*>(ep.out) + (long long)row * ep.ldc + oc;
+      if (full && ((reinterpret_cast<uintptr_t>(op) & 15) == 0)) {
+        *reinterpret_cast<float4*>(op) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (oc + e < nout) op[e] = v[e];
+      }
+    }
+  }
 }
 
 template <typename T, int BM, int BN, int BK>
 int launch(const void* A, int lda, const void* W, int ldw, int M, int N, int K, const Epi& ep, hipStream_t s) {
   constexpr int LDSR = BK + MT<T>::PAD;
-  const size_t lds = (size_t)2 * (BM + BN) * LDSR * sizeof(T);
+  size_t lds = (size_t)2 * (BM + BN) * LDSR * sizeof(T);
+  const size_t cbytes = (size_t)BM * (BN + 4) * 4;  // epilogue C tile
+  if (cbytes > lds) lds = cbytes;
   const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   hipLaunchKernelGGL((gemm_kernel<T, BM, BN, BK>), dim3(grid), dim3(256), lds, s, reinterpret_cast<const T*>(A),
                      lda, reinterpret_cast<const T*>(W), ldw, M, N, K, ep);
@@ -198,7 +229,7 @@ int launch(const void* A, int lda, const void* W, int ldw, int M, int N, int K, 
 
 // The GLU column permutation depends on the wave tile width WN = BN/2; the
 // host asks for it here so weights are permuted consistently.
-SBK_API int sbk_gemm_glu_group(int dtype_bf16) { return 16; }  // = WN/2 of the 64x64 tile
+SBK_API int sbk_gemm_glu_group(int dtype_bf16) { (void)dtype_bf16; return 16; }  // [value16 | gate16] groups
 
 // dtype_bf16: A and W are bf16 (else fp32).  tile: 0 auto, 1 = 128x128, 2 = 64x64, 3 = 128x64.
 SBK_API int sbk_gemm(int dtype_bf16, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
@@ -211,7 +242,6 @@ SBK_API int sbk_gemm(int dtype_bf16, const void* A, int lda, const void* W, int 
   if (act == ACT_GLU && (N % 32)) return SBK_ERR_ARG;  // whole [a16|gate16] groups
   Epi ep{bias, act, slope, res, ldr, alpha, rowmask, out, ldc, out_bf16};
   hipStream_t s = (hipStream_t)stream;
-  if (act == ACT_GLU) tile = 2;  // GLU pairing assumes WN = 32
   if (tile == 0) {
     const long long t128 = (long long)((M + 127) / 128) * ((N + 127) / 128);
     tile = t128 >= 512 ? 1 : 2;

@@ -32,6 +32,19 @@ struct MT<bf16_t> {
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
   }
   __device__ static __forceinline__ frag zero() { return frag{}; }
+  // elements 0..3 from p0, 4..7 from p1 (permuted-k fragments)
+  __device__ static __forceinline__ frag load2x4(const bf16_t* p0, const bf16_t* p1) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    const bf16x4 a = *reinterpret_cast<const bf16x4*>(p0);
+    const bf16x4 b = *reinterpret_cast<const bf16x4*>(p1);
+    return frag{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  }
+  __device__ static __forceinline__ frag from8(const float* v) {
+    frag f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = (__bf16)v[i];
+    return f;
+  }
   __device__ static __forceinline__ bf16_t from_f32(float v) { return f32_to_bf16(v); }
   __device__ static __forceinline__ float to_f32(bf16_t v) { return bf16_to_f32(v); }
 };
@@ -54,6 +67,20 @@ struct MT<float> {
     for (int s = 0; s < 8; ++s) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], c, 0, 0, 0);
   }
   __device__ static __forceinline__ frag zero() { return frag{}; }
+  __device__ static __forceinline__ frag load2x4(const float* p0, const float* p1) {
+    const float4 a = *reinterpret_cast<const float4*>(p0);
+    const float4 b = *reinterpret_cast<const float4*>(p1);
+    frag v;
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    return v;
+  }
+  __device__ static __forceinline__ frag from8(const float* v) {
+    frag f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = v[i];
+    return f;
+  }
   __device__ static __forceinline__ float from_f32(float v) { return v; }
   __device__ static __forceinline__ float to_f32(float v) { return v; }
 };
