@@ -69,6 +69,36 @@ int sbk_deltas(const float* x, float* y, int N, int T, int F, int window_length,
 /* ContextWindow.forward (features.py:917-937): (N, T, F) -> (N, T, F*(l+r+1)). */
 int sbk_context_window(const float* x, float* y, int N, int T, int F, int left, int right, void* stream);
 
+/* SpecAugment.forward (speechbrain/lobes/augment.py:106-201) on x (N, T, F)
+ * fp32, in place: bicubic time warp (c, w; c < 0 = none) through `tmp`,
+ * then frequency / time masks given as device int32 (N, n, 2) [len, pos]
+ * arrays drawn on the host, filled with 0 or the running means
+ * (use_mean; `partial` scratch of 2*N*ceil(T/16) floats; n_fcells = number
+ * of frequency-masked cells). */
+int sbk_specaugment(float* x, int N, int T, int F, int c, int w, float* tmp, const int* fmask, int n_fmask,
+                    const int* tmask, int n_tmask, int use_mean, float* partial, long long n_fcells, void* stream);
+
+/* ------------------------------------------------------------ RNN-T loss */
+
+/* Transducer forward (speechbrain/nnet/loss/transducer_loss.py:31-287 and
+ * losses.py:79-85): x (B, T, U1, V) logits (is_logits=1: log-softmax fused)
+ * or log-probs; labels (B, U1-1) int32; Tl, Ul (B,) int32 absolute lengths.
+ * Computes per-cell blank/label log-probs, the α and β lattices
+ * (anti-diagonal wavefront), log P, the sparse gradients and the reduced
+ * loss: loss_mode 0 = SpeechBrain semantics -(α+lp)/T, 1 = -log P;
+ * reduction 0 mean, 1 sum, 2 none (out holds B values).
+ * ws: sbk_rnnt_workspace_floats(B, T, U1) floats, kept for the backward. */
+int sbk_rnnt_forward(const float* x, const int* labels, const int* Tl, const int* Ul, int B, int T, int U1, int V,
+                     int blank, int is_logits, int loss_mode, int reduction, float* ws, float* out, void* stream);
+long long sbk_rnnt_workspace_floats(int B, int T, int U1);
+
+/* Dense gradient (B, T, U1, V) from the forward's workspace: mode 0 wrt the
+ * log-probs (Transducer.apply contract, zero except blank/label entries),
+ * mode 1 wrt the logits through the log-softmax; rows scaled by scale[b]
+ * (scale_per_b) or scale[0]. */
+int sbk_rnnt_backward(const float* x, const int* labels, int B, int T, int U1, int V, int blank, int mode,
+                      const float* ws, const float* scale, int scale_per_b, float* grad, void* stream);
+
 /* ----------------------------------------------------------------- encoder */
 
 /* Output channels per wave tile in the GLU-paired GEMM (weights are

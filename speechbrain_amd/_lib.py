@@ -44,11 +44,17 @@ SIGNATURES = {
     "sbk_conv_block_mfma": [_i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _f, _vp, _i, _vp, _vp, _vp],
     "sbk_cast_bf16": [_vp, _vp, _ll, _vp],
     "sbk_swish": [_vp, _vp, _ll, _f, _vp],
+    # augment.hip
+    "sbk_specaugment": [_vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _i, _vp, _ll, _vp],
+    # rnnt.hip
+    "sbk_rnnt_forward": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp],
+    "sbk_rnnt_workspace_floats": [_i, _i, _i],
+    "sbk_rnnt_backward": [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp],
     # attention.hip
     "sbk_relpos_attention": [_i, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _vp],
     "sbk_relpos_attention_lds": [_i, _i, _i],
 }
-RESTYPES = {"sbk_relpos_attention_lds": ctypes.c_longlong}
+RESTYPES = {"sbk_relpos_attention_lds": ctypes.c_longlong, "sbk_rnnt_workspace_floats": ctypes.c_longlong}
 
 _lib = None
 _load_error = None

@@ -1,0 +1,215 @@
+// SpecAugment kernels: bicubic time warp, frequency/time masks, mean fill.
+//
+// Reference: speechbrain/lobes/augment.py:106-201 (SpecAugment.forward,
+// time_warp, mask_along_axis).  The random draws (warp centre c and width w,
+// mask lengths/positions) are made on the host with the CPU generator in the
+// reference's order, so mask indices are bit-exact with the reference CPU
+// path; the kernels only apply them.
+//
+// Data: x (N, T, F) fp32 (N = batch, or batch*channels for 4-D input).
+//   warp kernel : y[n, t, :] = bicubic(x[n, 0:c, :] -> w rows)  for t <  w
+//                              bicubic(x[n, c:T, :] -> T-w rows) for t >= w
+//                 (align_corners=True, A=-0.75, border-clamped taps; the
+//                  frequency axis keeps its size, where bicubic is the identity)
+//                 + per-block partial sums for the mean fill.
+//   apply kernel: x = time-masked ? mean2 : freq-masked ? mean1 : y
+//                 (mean1 = mean after warp, mean2 = mean after freq masking,
+//                  reduced in a fixed order from the partials -> deterministic)
+// HBM traffic: read x, write y, read y, write x (the in-place contract needs
+// the copy because warped rows move), or read+write x once without warp.
+#include "sbk_common.h"
+
+// No FMA contraction in this file: the warp weights and the source index are
+// rounded op by op like the reference's float arithmetic (an fma of the
+// index product shifts the bicubic phase by up to 1 ulp of the index).
+#pragma clang fp contract(off)
+
+using namespace sbk;
+
+namespace {
+
+__device__ __forceinline__ float cubic1(float x) {  // |x| <= 1
+  const float A = -0.75f;
+  return ((A + 2.f) * x - (A + 3.f)) * x * x + 1.f;
+}
+__device__ __forceinline__ float cubic2(float x) {  // 1 < |x| < 2
+  const float A = -0.75f;
+  return ((A * x - 5.f * A) * x + 8.f * A) * x - 4.f * A;
+}
+
+// Is frequency bin f of sequence n covered by one of its masks?
+__device__ __forceinline__ bool in_masks(const int* m, int n, int nm, int i) {
+  for (int k = 0; k < nm; ++k) {
+    const int len = m[(n * nm + k) * 2 + 0], pos = m[(n * nm + k) * 2 + 1];
+    if (pos <= i && i < pos + len) return true;
+  }
+  return false;
+}
+
+// One block per (n, tile of TT output rows); threads over F.
+__global__ void __launch_bounds__(256) warp_kernel(const float* __restrict__ x, float* __restrict__ y, int N, int T,
+                                                   int F, int c, int w, int TT, const int* __restrict__ fmask,
+                                                   int n_fmask, float* __restrict__ partial) {
+  __shared__ float red[16];
+  const int ntile = (T + TT - 1) / TT;
+  const int n = blockIdx.x / ntile;
+  const int t0 = (blockIdx.x - n * ntile) * TT;
+  const int t1 = min(T, t0 + TT);
+  const float* xn = x + (long long)n * T * F;
+  float* yn = y + (long long)n * T * F;
+  float s_all = 0.f, s_msk = 0.f;
+  for (int t = t0; t < t1; ++t) {
+    // segment: [0, w) <- x[0, c) ; [w, T) <- x[c, T)
+    const bool left = t < w;
+    const int in_rows = left ? c : T - c;
+    const int out_rows = left ? w : T - w;
+    const int src0 = left ? 0 : c;
+    const int dst = left ? t : t - w;
+    int idx[4];
+    float wt[4];
+    if (in_rows == out_rows) {
+      idx[0] = idx[1] = idx[2] = idx[3] = dst;
+      wt[0] = 0.f; wt[1] = 1.f; wt[2] = 0.f; wt[3] = 0.f;
+    } else {
+      // correctly rounded like the reference (a float divide may be 1 ulp off on the GPU)
+      const float scale = out_rows > 1 ? (float)((double)(in_rows - 1) / (double)(out_rows - 1)) : 0.f;
+      const float real = scale * (float)dst;
+      const float fl = floorf(real);
+      const float tt = real - fl;
+      const int i0 = (int)fl;
+      wt[0] = cubic2(tt + 1.f);
+      wt[1] = cubic1(tt);
+      wt[2] = cubic1(1.f - tt);
+      wt[3] = cubic2(2.f - tt);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) idx[k] = min(max(i0 - 1 + k, 0), in_rows - 1);
+    }
+    for (int f = threadIdx.x; f < F; f += blockDim.x) {
+      float v;
+      if (in_rows == out_rows) {
+        v = xn[(long long)(src0 + dst) * F + f];
+      } else {
+        v = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v += wt[k] * xn[(long long)(src0 + idx[k]) * F + f];
+      }
+      yn[(long long)t * F + f] = v;
+      s_all += v;
+      if (n_fmask && in_masks(fmask, n, n_fmask, f)) s_msk += v;
+    }
+  }
+  if (partial) {
+    const float a = block_sum(s_all, red);
+    const float m = block_sum(s_msk, red);
+    if (threadIdx.x == 0) {
+      partial[2 * blockIdx.x] = a;
+      partial[2 * blockIdx.x + 1] = m;
+    }
+  }
+}
+
+// Partial sums without a warp (mean fill on unwarped input).
+__global__ void __launch_bounds__(256) sum_kernel(const float* __restrict__ x, int N, int T, int F, int TT,
+                                                  const int* __restrict__ fmask, int n_fmask,
+                                                  float* __restrict__ partial) {
+  __shared__ float red[16];
+  const int ntile = (T + TT - 1) / TT;
+  const int n = blockIdx.x / ntile;
+  const int t0 = (blockIdx.x - n * ntile) * TT;
+  const int t1 = min(T, t0 + TT);
+  const float* xn = x + (long long)n * T * F;
+  float s_all = 0.f, s_msk = 0.f;
+  for (int t = t0; t < t1; ++t)
+    for (int f = threadIdx.x; f < F; f += blockDim.x) {
+      const float v = xn[(long long)t * F + f];
+      s_all += v;
+      if (n_fmask && in_masks(fmask, n, n_fmask, f)) s_msk += v;
+    }
+  const float a = block_sum(s_all, red);
+  const float m = block_sum(s_msk, red);
+  if (threadIdx.x == 0) {
+    partial[2 * blockIdx.x] = a;
+    partial[2 * blockIdx.x + 1] = m;
+  }
+}
+
+// x[n,t,f] = tmask ? fill_t : fmask ? fill_f : src[n,t,f]   (src may alias x)
+__global__ void __launch_bounds__(256) apply_kernel(const float* src, float* x, int N, int T, int F, int TT,
+                                                    const int* __restrict__ fmask, int n_fmask,
+                                                    const int* __restrict__ tmask, int n_tmask,
+                                                    const float* __restrict__ partial, int nparts,
+                                                    long long n_fcells, int use_mean) {
+  __shared__ float red[16];
+  __shared__ float fills[2];
+  if (use_mean) {
+    // deterministic reduction of the per-block partial sums, same order in every block
+    float a = 0.f, m = 0.f;
+    for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
+      a += partial[2 * i];
+      m += partial[2 * i + 1];
+    }
+    a = block_sum(a, red);
+    m = block_sum(m, red);
+    if (threadIdx.x == 0) {
+      const double total = (double)N * T * F;
+      const float mean1 = (float)(a / total);
+      fills[0] = mean1;
+      fills[1] = (float)(((double)a - (double)m + (double)mean1 * (double)n_fcells) / total);
+    }
+  } else if (threadIdx.x == 0) {
+    fills[0] = fills[1] = 0.f;
+  }
+  __syncthreads();
+  const float fill_f = fills[0], fill_t = fills[1];
+  const int ntile = (T + TT - 1) / TT;
+  const int n = blockIdx.x / ntile;
+  const int t0 = (blockIdx.x - n * ntile) * TT;
+  const int t1 = min(T, t0 + TT);
+  for (int t = t0; t < t1; ++t) {
+    const bool tm = n_tmask && in_masks(tmask, n, n_tmask, t);
+    for (int f = threadIdx.x; f < F; f += blockDim.x) {
+      const long long i = ((long long)n * T + t) * F + f;
+      float v;
+      if (tm)
+        v = fill_t;
+      else if (n_fmask && in_masks(fmask, n, n_fmask, f))
+        v = fill_f;
+      else
+        v = src[i];
+      x[i] = v;
+    }
+  }
+}
+
+}  // namespace
+
+// Full SpecAugment application on x (N, T, F) fp32, in place.
+//   warp: c, w (warp skipped when c < 0); tmp: (N, T, F) scratch, required when warping;
+//   fmask (N, n_fmask, 2) / tmask (N, n_tmask, 2) int32 [len, pos] device arrays (or n_* = 0);
+//   use_mean: fill with the running means (replace_with_zero=False), else 0;
+//   partial: scratch of 2 * N * ceil(T/16) floats (when use_mean);
+//   n_fcells: number of frequency-masked cells (host-computed, for the second mean).
+SBK_API int sbk_specaugment(float* x, int N, int T, int F, int c, int w, float* tmp, const int* fmask, int n_fmask,
+                            const int* tmask, int n_tmask, int use_mean, float* partial, long long n_fcells,
+                            void* stream) {
+  if (N <= 0 || T <= 0 || F <= 0) return SBK_ERR_ARG;
+  const int TT = 16;
+  const int nblk = N * ((T + TT - 1) / TT);
+  hipStream_t s = (hipStream_t)stream;
+  const float* src = x;
+  if (c >= 0) {
+    if (!tmp || c <= 0 || c >= T || w <= 0 || w >= T) return SBK_ERR_ARG;
+    hipLaunchKernelGGL(warp_kernel, dim3(nblk), dim3(256), 0, s, x, tmp, N, T, F, c, w, TT, fmask, n_fmask,
+                       use_mean ? partial : nullptr);
+    SBK_CHECK_LAUNCH();
+    src = tmp;
+  } else if (use_mean) {
+    hipLaunchKernelGGL(sum_kernel, dim3(nblk), dim3(256), 0, s, x, N, T, F, TT, fmask, n_fmask, partial);
+    SBK_CHECK_LAUNCH();
+  }
+  if (c < 0 && n_fmask == 0 && n_tmask == 0) return 0;
+  hipLaunchKernelGGL(apply_kernel, dim3(nblk), dim3(256), 0, s, src, x, N, T, F, TT, fmask, n_fmask, tmask, n_tmask,
+                     partial, nblk, n_fcells, use_mean);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,94 @@
+"""Drop-in for speechbrain.lobes.augment.SpecAugment (augment.py:32-201).
+
+Random draws (warp centre/width, mask lengths/positions) are made on the host
+with the CPU generator in exactly the reference's order, so a given
+torch.manual_seed reproduces the reference CPU path's mask indices bit for
+bit — also for ROCm tensors, where the reference would draw masks on the
+device generator.  The warp / mask / mean-fill arithmetic runs in
+speechbrain_amd/csrc/augment.hip; the input is mutated in place and
+returned, as in the reference.
+"""
+import torch
+
+from .._lib import check, lib, ptr, require_device, stream_of
+
+__all__ = ["SpecAugment"]
+
+
+class SpecAugment(torch.nn.Module):
+    def __init__(self, time_warp=True, time_warp_window=5, time_warp_mode="bicubic", freq_mask=True,
+                 freq_mask_width=(0, 20), n_freq_mask=2, time_mask=True, time_mask_width=(0, 100), n_time_mask=2,
+                 replace_with_zero=True):
+        super().__init__()
+        assert time_warp or freq_mask or time_mask, \
+            "at least one of time_warp, time_mask, or freq_mask should be applied"
+        if time_warp and time_warp_mode != "bicubic":
+            raise NotImplementedError("only bicubic time warping is implemented (the recipe mode)")
+        self.apply_time_warp = time_warp
+        self.time_warp_window = time_warp_window
+        self.time_warp_mode = time_warp_mode
+        self.freq_mask = freq_mask
+        if isinstance(freq_mask_width, int):
+            freq_mask_width = (0, freq_mask_width)
+        self.freq_mask_width = freq_mask_width
+        self.n_freq_mask = n_freq_mask
+        self.time_mask = time_mask
+        if isinstance(time_mask_width, int):
+            time_mask_width = (0, time_mask_width)
+        self.time_mask_width = time_mask_width
+        self.n_time_mask = n_time_mask
+        self.replace_with_zero = replace_with_zero
+        self.last_draws = None
+
+    def draws(self, N, T, F):
+        """Host draws in the reference order (augment.py:131-133, :175-186)."""
+        c = w = -1
+        if self.apply_time_warp:
+            win = self.time_warp_window
+            if T - win > win:
+                c = int(torch.randint(win, T - win, (1,))[0])
+                w = int(torch.randint(c - win, c + win, (1,))[0]) + 1
+        fm = tm = None
+        if self.freq_mask:
+            ln = torch.randint(self.freq_mask_width[0], self.freq_mask_width[1], (N, self.n_freq_mask))
+            ps = torch.randint(0, max(1, F - int(ln.max())), (N, self.n_freq_mask))
+            fm = torch.stack([ln, ps], -1).to(torch.int32)
+        if self.time_mask:
+            ln = torch.randint(self.time_mask_width[0], self.time_mask_width[1], (N, self.n_time_mask))
+            ps = torch.randint(0, max(1, T - int(ln.max())), (N, self.n_time_mask))
+            tm = torch.stack([ln, ps], -1).to(torch.int32)
+        return c, w, fm, tm
+
+    def forward(self, x):
+        """Takes in input a tensor and returns an augmented one (in place)."""
+        require_device(x)
+        if x.dtype != torch.float32 or not x.is_contiguous():
+            raise TypeError("SpecAugment kernel expects a contiguous fp32 tensor")
+        if x.dim() == 3:
+            N, T, F = x.shape
+        elif x.dim() == 4:
+            N, T, F = x.shape[0] * x.shape[1], x.shape[2], x.shape[3]
+        else:
+            raise ValueError("expected (batch, time, freq) or (batch, channel, time, freq)")
+        c, w, fm, tm = self.draws(N, T, F)
+        if c == w:
+            c = w = -1  # identical segment sizes: the resize is the identity
+        self.last_draws = (c, w, fm, tm)
+        dev = x.device
+        n_f = fm.shape[1] if fm is not None else 0
+        n_t = tm.shape[1] if tm is not None else 0
+        fm_d = fm.to(dev, non_blocking=True) if fm is not None else None
+        tm_d = tm.to(dev, non_blocking=True) if tm is not None else None
+        use_mean = not self.replace_with_zero
+        n_fcells = 0
+        if fm is not None:
+            # number of masked (sequence, freq) cells x T, for the second running mean
+            ar = torch.arange(F).view(1, 1, -1)
+            cov = ((fm[..., 1:2] <= ar) & (ar < fm[..., 1:2] + fm[..., 0:1])).any(1)
+            n_fcells = int(cov.sum()) * T
+        tmp = torch.empty_like(x) if c >= 0 else None
+        partial = torch.empty(2 * N * ((T + 15) // 16), device=dev, dtype=torch.float32) if use_mean else None
+        rc = lib().sbk_specaugment(ptr(x), N, T, F, c, w, ptr(tmp), ptr(fm_d), n_f, ptr(tm_d), n_t, int(use_mean),
+                                   ptr(partial), n_fcells, stream_of(x))
+        check(rc, "sbk_specaugment")
+        return x

@@ -1,0 +1,93 @@
+"""HIP SpecAugment vs the reference's golden outputs (same seeds → same
+CPU-generator draws → bit-exact mask indices) and vs the oracle at the
+BASELINE config-2 size."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import assert_close
+import oracle.augment as OA
+
+pytestmark = pytest.mark.gpu
+
+CFGS = {
+    "recipe": dict(time_warp=True, time_warp_window=5, time_warp_mode="bicubic", freq_mask=True, n_freq_mask=2,
+                   time_mask=True, n_time_mask=2, replace_with_zero=False, freq_mask_width=30, time_mask_width=40),
+    "default": dict(),
+    "nowarp": dict(time_warp=False, freq_mask_width=(5, 15), time_mask_width=(10, 20), n_freq_mask=3,
+                   n_time_mask=1),
+}
+
+
+@pytest.mark.parametrize("cfg", list(CFGS))
+def test_specaugment_vs_golden(golden, dev, cfg):
+    from speechbrain_amd.lobes.augment import SpecAugment
+    g = golden("specaug")
+    feats = torch.from_numpy(g["feats"])
+    for s in range(4):
+        aug = SpecAugment(**CFGS[cfg])
+        torch.manual_seed(s)
+        x = feats.clone().to(dev)
+        y = aug(x)
+        assert y is x  # in place, like the reference
+        ref = g[f"{cfg}_s{s}"]
+        assert_close(y, ref, rtol=1e-5, name=f"{cfg}{s}")
+        # bit-exact indices: the fill pattern matches cell for cell
+        if cfg != "recipe":
+            yn = y.cpu().numpy()
+            assert np.array_equal(yn == 0, ref == 0)
+
+
+def test_specaugment_draw_order_matches_reference(golden, dev):
+    from speechbrain_amd.lobes.augment import SpecAugment
+    g = golden("specaug")
+    feats = torch.from_numpy(g["feats"])
+    for s in range(4):
+        aug = SpecAugment(**CFGS["recipe"])
+        torch.manual_seed(s)
+        aug(feats.clone().to(dev))
+        c, w, fm, tm = aug.last_draws
+        got = np.concatenate([[c], [w - 1], fm[..., 0].reshape(-1), fm[..., 1].reshape(-1),
+                              tm[..., 0].reshape(-1), tm[..., 1].reshape(-1)]).astype(np.int64)
+        assert np.array_equal(got, g[f"recipe_s{s}_draws"])
+
+
+def test_time_warp_only_vs_golden(golden, dev):
+    from speechbrain_amd.lobes.augment import SpecAugment
+    g = golden("specaug")
+    feats = torch.from_numpy(g["feats"])
+    aug = SpecAugment(time_warp=True, freq_mask=False, time_mask=False)
+    for s in range(4):
+        torch.manual_seed(100 + s)
+        assert_close(aug(feats.clone().to(dev)), g[f"warp_s{s}"], rtol=1e-5, name=f"warp{s}")
+
+
+def test_specaugment_full_size_vs_oracle(dev):
+    """B=32 x 1501 x 80 (BASELINE config 2), recipe parameters."""
+    from speechbrain_amd.lobes.augment import SpecAugment
+    x = torch.randn(32, 1501, 80, generator=torch.Generator().manual_seed(7)) * 10 - 40
+    for seed in (1234, 1235):
+        torch.manual_seed(seed)
+        y = SpecAugment(**CFGS["recipe"])(x.clone().to(dev))
+        torch.manual_seed(seed)
+        ref = OA.spec_augment(x.clone(), time_warp_on=True, time_warp_window=5, freq_mask=True, n_freq_mask=2,
+                              time_mask=True, n_time_mask=2, replace_with_zero=False, freq_mask_width=30,
+                              time_mask_width=40)
+        assert_close(y, ref, rtol=1e-5, name=f"full{seed}")
+
+
+def test_specaugment_4d_and_short(dev):
+    from speechbrain_amd.lobes.augment import SpecAugment
+    x = torch.randn(2, 3, 40, 20)
+    torch.manual_seed(5)
+    y = SpecAugment(freq_mask_width=(0, 5), time_mask_width=(0, 8))(x.clone().to(dev))
+    torch.manual_seed(5)
+    ref = OA.spec_augment(x.clone(), freq_mask_width=(0, 5), time_mask_width=(0, 8))
+    assert_close(y, ref, rtol=1e-5, name="4d")
+    # T - window <= window: no warp, no draws for it (augment.py:128-129)
+    x = torch.randn(2, 9, 20)
+    torch.manual_seed(6)
+    y = SpecAugment(freq_mask_width=(0, 5), time_mask_width=(0, 3))(x.clone().to(dev))
+    torch.manual_seed(6)
+    ref = OA.spec_augment(x.clone(), freq_mask_width=(0, 5), time_mask_width=(0, 3))
+    assert_close(y, ref, rtol=1e-5, name="short")
