@@ -38,12 +38,13 @@ int sbk_fft_supported(int n_fft);
  * wav: (Bo, S, C) fp32; window: n_fft fp32 (win centred, zero padded);
  * twiddle_nc: n_fft/2 complex W_{n_fft/2}^m; twiddle_nfft: n_fft/2+1 complex W_{n_fft}^k;
  * out_strides: HOST array of 5 int64 (modes 0/1); mel_*: per-filter CSR of the
- * (n_fft/2+1, M) filter matrix (start bin, length, offset into mel_w). */
+ * (n_fft/2+1, M) filter matrix (start bin, length, offset into mel_w of n_melw weights). */
 int sbk_spectrum(int mode, const float* wav, int Bo, int S, int C, int n_fft, int hop, int center, int pad_mode,
                  int T, const float* window, const float* twiddle_nc, const float* twiddle_nfft, int onesided,
                  float norm_scale, float power, float eps, int log_mag, const long long* out_strides,
-                 const int* mel_start, const int* mel_len, const int* mel_off, const float* mel_w, int M,
-                 int log_mel, float multiplier, float db_offset, float amin, float* out, int* maxkey, void* stream);
+                 const int* mel_start, const int* mel_len, const int* mel_off, const float* mel_w, int n_melw,
+                 int M, int log_mel, float multiplier, float db_offset, float amin, float* out, int* maxkey,
+                 void* stream);
 
 /* Filterbank.forward on a spectrogram (N, T, F) -> (N, T, M) (features.py:490-560):
  * sparse CSR filters, or a dense (F, M) matrix when `dense` is non-null

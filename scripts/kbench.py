@@ -39,11 +39,9 @@ def gemm_bench():
         r = torch.randn(M, N // 2 if act == "glu" else N, device=dev) if res else None
         fl = 2.0 * M * N * K
         line = f"{name:9s} M={M} N={N} K={K}:"
-        for tile in (1, 2, 3):
+        for tile in (2, 3, 8, 9, 10):
             us = timeit(lambda: _enc.gemm(a, w, bias=b, act=act, res=r, out_dtype=od, tile=tile))
-            line += f"  tile{tile} {us:7.1f}us {fl / us / 1e6:7.1f}TF"
-        us = timeit(lambda: _enc.gemm(a, w, out_dtype=torch.float32, tile=1))
-        line += f" | plain128 {us:6.1f}us {fl / us / 1e6:6.1f}TF"
+            line += f" t{tile} {us:6.1f}us {fl / us / 1e6:6.0f}TF"
         print(line, flush=True)
 
 

@@ -27,7 +27,7 @@ _f = ctypes.c_float
 SIGNATURES = {
     "sbk_fft_supported": [_i],
     "sbk_spectrum": [_i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _i, _f, _f, _f, _i, _vp,
-                     _vp, _vp, _vp, _vp, _i, _i, _f, _f, _f, _vp, _vp, _vp],
+                     _vp, _vp, _vp, _vp, _i, _i, _i, _f, _f, _f, _vp, _vp, _vp],
     "sbk_filterbank": [_vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _i, _i, _f, _f, _f, _vp, _vp, _vp],
     "sbk_topdb_clamp": [_vp, _vp, _ll, _i, _f, _vp],
     "sbk_magnitude": [_vp, _vp, _ll, _i, _f, _f, _i, _vp],

@@ -35,20 +35,40 @@ constexpr int QB = 64;        // queries per workgroup
 constexpr int KC = 64;        // keys per chunk
 constexpr int PBR = KC + QB;  // positional band rows staged per chunk (127 used)
 constexpr int GR = 80;        // G^T rows per wave (79 used)
-constexpr int GS = 17;        // G^T scratch row stride (floats)
+constexpr int GS = 20;        // G^T scratch row stride (floats): conflict-free writes and shifted reads
+
+template <typename T>
+struct VLayout {  // bf16: V row-major + ds_read_tr16 ; fp32: V^T staged transposed
+  static constexpr bool TR = sizeof(T) == 2;
+};
 
 template <typename T, int DHP>
 struct FlashLds {
   static constexpr int PAD = MT<T>::PAD;
-  static constexpr int KR = DHP + PAD;  // Ks / Ps row stride
-  static constexpr int VR = KC + PAD;   // Vt row stride
+  static constexpr int KR = DHP + PAD;  // Ks / Ps / V(row-major) row stride
+  static constexpr int VR = KC + PAD;   // Vt row stride (fp32 path)
   static constexpr size_t ks = (size_t)KC * KR * sizeof(T);
-  static constexpr size_t vt = (size_t)DHP * VR * sizeof(T);
+  static constexpr size_t vt = VLayout<T>::TR ? (size_t)KC * KR * sizeof(T) : (size_t)DHP * VR * sizeof(T);
   static constexpr size_t ps = (size_t)PBR * KR * sizeof(T);
   static constexpr size_t gs = (size_t)4 * GR * GS * 4;
   static constexpr size_t ms = (size_t)KC * 4;
   static constexpr size_t bytes = ks + vt + ps + gs + ms;
 };
+
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+
+// A-operand fragment of V^T (rows d = dbase + (lane&15)) for keys
+// {k0 + 4g .. k0 + 4g + 3} ∪ {k0 + 16 + 4g .. +3}, read from row-major V in
+// LDS with two transposing reads (ds_read_b64_tr_b16): lane 4q+p of each
+// 16-lane group addresses row (key) q, columns (d) 4p..4p+3 of the block.
+__device__ __forceinline__ bf16x8 vt_frag_tr(const bf16_t* V, int KR, int k0, int dbase, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const bf16_t* a0 = V + (k0 + 4 * g + q) * KR + dbase + 4 * p;
+  const bf16_t* a1 = a0 + 16 * KR;
+  const bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4_t*)(a0));
+  const bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4_t*)(a1));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
 
 template <typename T, int DHP, bool PROBS>
 __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__ qkv, const T* __restrict__ pk,
@@ -60,11 +80,15 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
   using Tr = MT<T>;
   using L = FlashLds<T, DHP>;
   constexpr int KR = L::KR, VR = L::VR, VEC = Tr::VEC;
+  constexpr bool TRV = VLayout<T>::TR;
   constexpr int KS = DHP / 32;   // k-steps over the head dim
   constexpr int NDT = DHP / 16;  // O^T tiles (head-dim rows)
+  constexpr int CPR = DHP / VEC; // 16-B chunks per staged row
+  constexpr int NKC = KC * CPR / 256;   // K (and V) chunks per thread
+  constexpr int NPC = PBR * CPR / 256;  // P-band chunks per thread
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* Ks = reinterpret_cast<T*>(smem);
-  T* Vt = reinterpret_cast<T*>(smem + L::ks);
+  T* Vs = reinterpret_cast<T*>(smem + L::ks);
   T* Ps = reinterpret_cast<T*>(smem + L::ks + L::vt);
   float* Gs = reinterpret_cast<float*>(smem + L::ks + L::vt + L::ps);
   float* Ms = reinterpret_cast<float*>(smem + L::ks + L::vt + L::ps + L::gs);
@@ -92,13 +116,10 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int d = 32 * s + 8 * g + e;
-      float q = 0.f, u = 0.f, v = 0.f;
       if (my_i < Tn && d < dh) {
-        q = Tr::to_f32(qkv_b[(long long)my_i * row3 + d]);
-        u = pbu[h * dh + d];
-        v = pbv[h * dh + d];
-        qu[e] = q + u;
-        qv[e] = q + v;
+        const float q = Tr::to_f32(qkv_b[(long long)my_i * row3 + d]);
+        qu[e] = q + pbu[h * dh + d];
+        qv[e] = q + pbv[h * dh + d];
       } else {
         qu[e] = 0.f;
         qv[e] = 0.f;
@@ -114,58 +135,96 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
   for (int t = 0; t < NDT; ++t) acc_o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int Tp = (Tn + KC - 1) / KC * KC;
+  const int nchunk = Tp / KC;
+
+  // ---- staging: registers (vector path) -> LDS ----
+  uint4 rk[NKC], rv[NKC], rp[NPC];
+  float rm = 0.f;
+  auto fetch = [&](int j0, bool need_v) {
+    const int rbase = Tn - QB - i0 + j0;
+#pragma unroll
+    for (int i = 0; i < NKC; ++i) {
+      const int c = tid + 256 * i, r = c / CPR, d = (c % CPR) * VEC, j = j0 + r;
+      const bool ok = j < Tn && d < dh;
+      rk[i] = ok ? *reinterpret_cast<const uint4*>(qkv_b + (long long)j * row3 + dh + d) : make_uint4(0, 0, 0, 0);
+      rv[i] = (ok && need_v) ? *reinterpret_cast<const uint4*>(qkv_b + (long long)j * row3 + 2 * dh + d)
+                             : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NPC; ++i) {
+      const int c = tid + 256 * i, rr = c / CPR, d = (c % CPR) * VEC, r = rbase + rr;
+      rp[i] = (rr < PBR - 1 && r >= 0 && r <= 2 * Tn - 2 && d < dh)
+                  ? *reinterpret_cast<const uint4*>(pk_h + (long long)r * d_model + d)
+                  : make_uint4(0, 0, 0, 0);
+    }
+    if (tid < KC) {
+      const int j = j0 + tid;
+      rm = (j < Tn && !(kpm && kpm[(long long)b * Tn + j])) ? 0.f : -INFINITY;
+    }
+  };
+  auto commit = [&](bool need_v) {
+#pragma unroll
+    for (int i = 0; i < NKC; ++i) {
+      const int c = tid + 256 * i, r = c / CPR, d = (c % CPR) * VEC;
+      *reinterpret_cast<uint4*>(Ks + r * KR + d) = rk[i];
+      if (need_v) {
+        if (TRV) {
+          *reinterpret_cast<uint4*>(Vs + r * KR + d) = rv[i];
+        } else {
+          const T* ve = reinterpret_cast<const T*>(&rv[i]);
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) Vs[(d + e) * VR + r] = ve[e];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NPC; ++i) {
+      const int c = tid + 256 * i, rr = c / CPR, d = (c % CPR) * VEC;
+      *reinterpret_cast<uint4*>(Ps + rr * KR + d) = rp[i];
+    }
+    if (tid < KC) Ms[tid] = rm;
+  };
+  auto stage_scalar = [&](int j0, bool need_v) {  // unaligned head dims (e.g. d=144, H=4)
+    const int rbase = Tn - QB - i0 + j0;
+    for (int e = tid; e < KC * DHP; e += 256) {
+      const int r = e / DHP, d = e - r * DHP, j = j0 + r;
+      const bool ok = j < Tn && d < dh;
+      Ks[r * KR + d] = ok ? qkv_b[(long long)j * row3 + dh + d] : Tr::from_f32(0.f);
+      if (need_v) {
+        const T v = ok ? qkv_b[(long long)j * row3 + 2 * dh + d] : Tr::from_f32(0.f);
+        if (TRV)
+          Vs[r * KR + d] = v;
+        else
+          Vs[d * VR + r] = v;
+      }
+    }
+    for (int e = tid; e < PBR * DHP; e += 256) {
+      const int rr = e / DHP, d = e - rr * DHP, r = rbase + rr;
+      Ps[rr * KR + d] = (rr < PBR - 1 && r >= 0 && r <= 2 * Tn - 2 && d < dh) ? pk_h[(long long)r * d_model + d]
+                                                                              : Tr::from_f32(0.f);
+    }
+    if (tid < KC) {
+      const int j = j0 + tid;
+      Ms[tid] = (j < Tn && !(kpm && kpm[(long long)b * Tn + j])) ? 0.f : -INFINITY;
+    }
+  };
+
   constexpr int NPASS = PROBS ? 2 : 1;
   for (int pass = 0; pass < NPASS; ++pass) {
     const bool stats_only = PROBS && pass == 0;
-    for (int j0 = 0; j0 < Tp; j0 += KC) {
-      __syncthreads();  // previous chunk's readers done
-      // ---- stage K rows, V^T, positional band rows, key mask ----
-      const int rbase = Tn - QB - i0 + j0;
-      if (vec_ok) {
-        constexpr int CPR = DHP / VEC;
-        for (int c = tid; c < KC * CPR; c += 256) {
-          const int r = c / CPR, d = (c % CPR) * VEC;
-          const int j = j0 + r;
-          uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-          if (j < Tn && d < dh) {
-            kv = *reinterpret_cast<const uint4*>(qkv_b + (long long)j * row3 + dh + d);
-            if (!stats_only) vv = *reinterpret_cast<const uint4*>(qkv_b + (long long)j * row3 + 2 * dh + d);
-          }
-          *reinterpret_cast<uint4*>(Ks + r * KR + d) = kv;
-          if (!stats_only) {
-            const T* ve = reinterpret_cast<const T*>(&vv);
-#pragma unroll
-            for (int e = 0; e < VEC; ++e) Vt[(d + e) * VR + r] = ve[e];
-          }
-        }
-        for (int c = tid; c < PBR * CPR; c += 256) {
-          const int rr = c / CPR, d = (c % CPR) * VEC;
-          const int r = rbase + rr;
-          uint4 pv = make_uint4(0, 0, 0, 0);
-          if (rr < PBR - 1 && r >= 0 && r <= 2 * Tn - 2 && d < dh)
-            pv = *reinterpret_cast<const uint4*>(pk_h + (long long)r * d_model + d);
-          *reinterpret_cast<uint4*>(Ps + rr * KR + d) = pv;
-        }
-      } else {
-        for (int e = tid; e < KC * DHP; e += 256) {
-          const int r = e / DHP, d = e - r * DHP;
-          const int j = j0 + r;
-          const bool ok = j < Tn && d < dh;
-          Ks[r * KR + d] = ok ? qkv_b[(long long)j * row3 + dh + d] : Tr::from_f32(0.f);
-          if (!stats_only) Vt[d * VR + r] = ok ? qkv_b[(long long)j * row3 + 2 * dh + d] : Tr::from_f32(0.f);
-        }
-        for (int e = tid; e < PBR * DHP; e += 256) {
-          const int rr = e / DHP, d = e - rr * DHP;
-          const int r = rbase + rr;
-          Ps[rr * KR + d] = (rr < PBR - 1 && r >= 0 && r <= 2 * Tn - 2 && d < dh) ? pk_h[(long long)r * d_model + d]
-                                                                                  : Tr::from_f32(0.f);
-        }
-      }
-      if (tid < KC) {
-        const int j = j0 + tid;
-        Ms[tid] = (j < Tn && !(kpm && kpm[(long long)b * Tn + j])) ? 0.f : -INFINITY;
-      }
-      __syncthreads();
+    const bool need_v = !stats_only;
+    __syncthreads();
+    if (vec_ok) {
+      fetch(0, need_v);
+      commit(need_v);
+    } else {
+      stage_scalar(0, need_v);
+    }
+    __syncthreads();
+    for (int ch = 0; ch < nchunk; ++ch) {
+      const int j0 = ch * KC;
+      const bool more = ch + 1 < nchunk;
+      if (vec_ok && more) fetch(j0 + KC, need_v);  // next chunk in flight during this chunk's math
 
       // ---- S^T (keys x queries) and G^T (band rows x queries) ----
       f32x4 acc_s[4];
@@ -210,62 +269,74 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) ls += expf(sc[t][r] - mref);
+          for (int r = 0; r < 4; ++r) ls += __expf(sc[t][r] - mref);
         ls += __shfl_xor(ls, 16);
         ls += __shfl_xor(ls, 32);
-        l_run = l_run * expf(m_run - mref) + ls;
+        l_run = l_run * __expf(m_run - mref) + ls;
         m_run = m_new;
-        continue;
-      }
-
-      float p[4][4];
-      if (PROBS) {
-        // exact pass: final max / sum known
-        const float mref = m_run == -INFINITY ? 0.f : m_run;
-        const float inv = 1.0f / l_run;
-        float* prow = probs + (((long long)b * H + h) * Tn + my_i) * Tn;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int j = j0 + 16 * t + 4 * g + r;
-            p[t][r] = expf(sc[t][r] - mref) * inv;
-            if (my_i < Tn && j < Tn) prow[j] = p[t][r];
-          }
       } else {
-        const float m_new = fmaxf(m_run, cmax);
-        const float mref = m_new == -INFINITY ? 0.f : m_new;
-        const float alpha = expf(m_run - mref);
-        float ls = 0.f;
+        float p[4][4];
+        if (PROBS) {
+          const float mref = m_run == -INFINITY ? 0.f : m_run;
+          const float inv = 1.0f / l_run;
+          float* prow = probs + (((long long)b * H + h) * Tn + my_i) * Tn;
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int j = j0 + 16 * t + 4 * g + r;
+              p[t][r] = __expf(sc[t][r] - mref) * inv;
+              if (my_i < Tn && j < Tn) prow[j] = p[t][r];
+            }
+        } else {
+          const float m_new = fmaxf(m_run, cmax);
+          const float mref = m_new == -INFINITY ? 0.f : m_new;
+          const float alpha = __expf(m_run - mref);
+          float ls = 0.f;
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              p[t][r] = __expf(sc[t][r] - mref);
+              ls += p[t][r];
+            }
+          ls += __shfl_xor(ls, 16);
+          ls += __shfl_xor(ls, 32);
+          l_run = l_run * alpha + ls;
+          m_run = m_new;
+#pragma unroll
+          for (int t = 0; t < NDT; ++t) acc_o[t] *= alpha;
+        }
+        // ---- O^T += V^T · P^T  (2 k-steps of 32 keys) ----
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          float pv[8];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            p[t][r] = expf(sc[t][r] - mref);
-            ls += p[t][r];
+            pv[r] = p[2 * s2][r];
+            pv[4 + r] = p[2 * s2 + 1][r];
           }
-        ls += __shfl_xor(ls, 16);
-        ls += __shfl_xor(ls, 32);
-        l_run = l_run * alpha + ls;
-        m_run = m_new;
+          const typename Tr::frag fp = Tr::from8(pv);
 #pragma unroll
-        for (int t = 0; t < NDT; ++t) acc_o[t] *= alpha;
+          for (int t = 0; t < NDT; ++t) {
+            typename Tr::frag fa;
+            if constexpr (TRV) {
+              fa = vt_frag_tr(reinterpret_cast<const bf16_t*>(Vs), KR, 32 * s2, 16 * t, lane);
+            } else {
+              const T* vrow = Vs + (16 * t + c16) * VR + 32 * s2 + 4 * g;
+              fa = Tr::load2x4(vrow, vrow + 16);
+            }
+            Tr::mma(acc_o[t], fa, fp);
+          }
+        }
       }
-      // ---- O^T += V^T · P^T  (2 k-steps of 32 keys) ----
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        float pv[8];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          pv[r] = p[2 * s2][r];
-          pv[4 + r] = p[2 * s2 + 1][r];
-        }
-        const typename Tr::frag fp = Tr::from8(pv);
-#pragma unroll
-        for (int t = 0; t < NDT; ++t) {
-          const T* vrow = Vt + (16 * t + c16) * VR + 32 * s2 + 4 * g;
-          Tr::mma(acc_o[t], Tr::load2x4(vrow, vrow + 16), fp);
-        }
+      __syncthreads();  // every wave done with this chunk's Ks / Vs / Ps / Gs
+      if (more) {
+        if (vec_ok)
+          commit(need_v);
+        else
+          stage_scalar(j0 + KC, need_v);
+        __syncthreads();
       }
     }
   }

@@ -202,8 +202,8 @@ struct SpecArgs {
   const int* mel_len;     // (M,)
   const int* mel_off;     // (M,) offset into mel_w
   const float* mel_w;
-  int M, log_mel;
-  float multiplier, db_offset, amin;
+  int M, log_mel, n_melw;
+  float multiplier, db_offset, amin, amin_db;
   float* out;
   int* maxkey;  // (Bfold,) per-sequence max dB key
 };
@@ -223,7 +223,25 @@ __global__ void __launch_bounds__(256) spec_kernel(SpecArgs a, FftPlan plan) {
 
   float2* bufA = reinterpret_cast<float2*>(smem);
   float2* bufB = bufA + a.fpb * nc;
-  float* smp = reinterpret_cast<float*>(bufB + a.fpb * nc);
+  float2* tw = bufB + a.fpb * nc;           // W_nc^m, staged once per block
+  float2* tw2 = tw + nc;                    // W_nfft^k, k <= nc
+  int* mstart = reinterpret_cast<int*>(tw2 + nc + 1);
+  int* mlen = mstart + a.M;
+  int* moff = mlen + a.M;
+  float* mw = reinterpret_cast<float*>(moff + a.M);
+  float* win = mw + (MODE == MODE_FBANK ? a.n_melw : 0);
+  float* smp = win + a.n_fft;
+  for (int i = threadIdx.x; i < a.n_fft; i += blockDim.x) win[i] = a.window[i];
+  for (int i = threadIdx.x; i < nc; i += blockDim.x) tw[i] = a.tw[i];
+  for (int i = threadIdx.x; i <= nc; i += blockDim.x) tw2[i] = a.tw2[i];
+  if (MODE == MODE_FBANK) {
+    for (int i = threadIdx.x; i < a.M; i += blockDim.x) {
+      mstart[i] = a.mel_start[i];
+      mlen[i] = a.mel_len[i];
+      moff[i] = a.mel_off[i];
+    }
+    for (int i = threadIdx.x; i < a.n_melw; i += blockDim.x) mw[i] = a.mel_w[i];
+  }
 
   // 1) stage the samples spanned by this block's frames
   const int pad = a.center ? a.n_fft / 2 : 0;
@@ -239,10 +257,10 @@ __global__ void __launch_bounds__(256) spec_kernel(SpecArgs a, FftPlan plan) {
   for (int i = threadIdx.x; i < nf * nc; i += blockDim.x) {
     const int f = i / nc, m = i - f * nc;
     const float* fr = smp + f * a.hop;
-    bufA[f * nc + m] = make_float2(fr[2 * m] * a.window[2 * m], fr[2 * m + 1] * a.window[2 * m + 1]);
+    bufA[f * nc + m] = make_float2(fr[2 * m] * win[2 * m], fr[2 * m + 1] * win[2 * m + 1]);
   }
   // 3) complex FFT of size nc
-  float2* Z = run_fft(bufA, bufB, plan, a.tw, nf);
+  float2* Z = run_fft(bufA, bufB, plan, tw, nf);
   float2* other = (Z == bufA) ? bufB : bufA;
 
   // 4) split into the real-input spectrum X[k], k = 0..nc
@@ -258,7 +276,7 @@ __global__ void __launch_bounds__(256) spec_kernel(SpecArgs a, FftPlan plan) {
       const float2 zc = make_float2(zr.x, -zr.y);
       const float2 E = make_float2(0.5f * (zk.x + zc.x), 0.5f * (zk.y + zc.y));
       const float2 O = mul_mi(make_float2(0.5f * (zk.x - zc.x), 0.5f * (zk.y - zc.y)));
-      float2 X = cadd(E, cmul(a.tw2[k], O));
+      float2 X = cadd(E, cmul(tw2[k], O));
       if (mirror) X.y = -X.y;
       float* o = a.out + bo * a.os_b + ch * a.os_c + (long long)(t0 + f) * a.os_t + kk * a.os_k;
       o[0] = X.x * a.norm_scale;
@@ -274,7 +292,7 @@ __global__ void __launch_bounds__(256) spec_kernel(SpecArgs a, FftPlan plan) {
     const float2 zc = make_float2(zr.x, -zr.y);
     const float2 E = make_float2(0.5f * (zk.x + zc.x), 0.5f * (zk.y + zc.y));
     const float2 O = mul_mi(make_float2(0.5f * (zk.x - zc.x), 0.5f * (zk.y - zc.y)));
-    float2 X = cadd(E, cmul(a.tw2[k], O));
+    float2 X = cadd(E, cmul(tw2[k], O));
     X.x *= a.norm_scale;
     X.y *= a.norm_scale;
     float s = X.x * X.x + X.y * X.y;
@@ -296,13 +314,14 @@ __global__ void __launch_bounds__(256) spec_kernel(SpecArgs a, FftPlan plan) {
   float* orow = a.out + ((long long)bf * a.T + t0) * a.M;
   for (int i = threadIdx.x; i < nf * a.M; i += blockDim.x) {
     const int f = i / a.M, j = i - f * a.M;
-    const float* pf = P + f * nbins + a.mel_start[j];
-    const float* w = a.mel_w + a.mel_off[j];
-    const int L = a.mel_len[j];
+    const float* pf = P + f * nbins + mstart[j];
+    const float* w = mw + moff[j];
+    const int L = mlen[j];
     float acc = 0.f;
     for (int q = 0; q < L; ++q) acc = fmaf(pf[q], w[q], acc);
     if (a.log_mel) {
-      acc = a.multiplier * (float)log10((double)fmaxf(acc, a.amin)) - a.db_offset;
+      // clamp(x, amin) -> the host-rounded dB of amin exactly (-100 for 1e-10)
+      acc = acc <= a.amin ? a.amin_db : a.multiplier * log10f(acc) - a.db_offset;
       lmax = fmaxf(lmax, acc);
     }
     orow[i] = acc;
@@ -323,7 +342,7 @@ struct FbArgs {
   const float* mel_w;
   const float* dense;  // optional dense (F, M) matrix (learnable filters); null -> sparse
   int M, log_mel, rows_per_block;
-  float multiplier, db_offset, amin;
+  float multiplier, db_offset, amin, amin_db;
   float* out;
   int* maxkey;
 };
@@ -351,7 +370,7 @@ __global__ void __launch_bounds__(256) filterbank_kernel(FbArgs a) {
       for (int q = 0; q < L; ++q) acc = fmaf(pf[q], w[q], acc);
     }
     if (a.log_mel) {
-      acc = a.multiplier * (float)log10((double)fmaxf(acc, a.amin)) - a.db_offset;
+      acc = acc <= a.amin ? a.amin_db : a.multiplier * log10f(acc) - a.db_offset;
       const int n = (int)((r0 + rr) / a.T);
       // rows of one block may straddle two sequences: flush per sequence
       if (n != cur_n) {
@@ -546,8 +565,8 @@ SBK_API int sbk_spectrum(int mode, const float* wav, int Bo, int S, int C, int n
                          int pad_mode, int T, const float* window, const float* twiddle_nc,
                          const float* twiddle_nfft, int onesided, float norm_scale, float power, float eps,
                          int log_mag, const long long* out_strides, const int* mel_start, const int* mel_len,
-                         const int* mel_off, const float* mel_w, int M, int log_mel, float multiplier,
-                         float db_offset, float amin, float* out, int* maxkey, void* stream) {
+                         const int* mel_off, const float* mel_w, int n_melw, int M, int log_mel,
+                         float multiplier, float db_offset, float amin, float* out, int* maxkey, void* stream) {
   if (Bo <= 0 || T <= 0 || S <= 0 || C <= 0) return SBK_ERR_ARG;
   FftPlan plan;
   if ((n_fft & 1) || fill_plan(&plan, n_fft / 2)) return SBK_ERR_ARG;
@@ -568,11 +587,15 @@ SBK_API int sbk_spectrum(int mode, const float* wav, int Bo, int S, int C, int n
   a.M = M; a.log_mel = log_mel; a.multiplier = multiplier; a.db_offset = db_offset; a.amin = amin;
   a.out = out; a.maxkey = maxkey;
   const int nc = n_fft / 2;
-  int fpb = 8;
+  a.n_melw = mode == MODE_FBANK ? n_melw : 0;
+  a.amin_db = multiplier * (float)log10((double)amin) - db_offset;
+  if (mode != MODE_FBANK) a.M = 0;
+  int fpb = 16;
   auto lds_bytes = [&](int f) {
-    return (size_t)2 * f * nc * sizeof(float2) + (size_t)((f - 1) * hop + n_fft) * sizeof(float);
+    return (size_t)2 * f * nc * sizeof(float2) + (size_t)(2 * nc + 1) * sizeof(float2) +
+           (size_t)(3 * a.M + a.n_melw + n_fft) * 4 + (size_t)((f - 1) * hop + n_fft) * sizeof(float);
   };
-  while (fpb > 1 && lds_bytes(fpb) > 64 * 1024) fpb >>= 1;
+  while (fpb > 1 && lds_bytes(fpb) > 72 * 1024) fpb >>= 1;
   if (lds_bytes(fpb) > 160 * 1024) return SBK_ERR_ARG;
   a.fpb = fpb;
   const int nblk = a.Bfold * ((T + fpb - 1) / fpb);
@@ -600,6 +623,7 @@ SBK_API int sbk_filterbank(const float* spec, int N, int T, int F, const int* me
   a.spec = spec; a.N = N; a.T = T; a.F = F;
   a.mel_start = mel_start; a.mel_len = mel_len; a.mel_off = mel_off; a.mel_w = mel_w; a.dense = dense;
   a.M = M; a.log_mel = log_mel; a.multiplier = multiplier; a.db_offset = db_offset; a.amin = amin;
+  a.amin_db = multiplier * (float)log10((double)amin) - db_offset;
   a.out = out; a.maxkey = maxkey;
   int rpb = 8;
   while (rpb > 1 && (size_t)rpb * F * 4 > 48 * 1024) rpb >>= 1;

@@ -38,7 +38,7 @@ struct Epi {
   int out_bf16;
 };
 
-template <typename T, int BM, int BN, int BK>
+template <typename T, int BM, int BN, int BK, int NBUF>
 __global__ void __launch_bounds__(256) gemm_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W,
                                                    int ldw, int M, int N, int K, Epi ep) {
   using Tr = MT<T>;
@@ -53,13 +53,18 @@ __global__ void __launch_bounds__(256) gemm_kernel(const T* __restrict__ A, int 
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* As = reinterpret_cast<T*>(smem);
-  T* Bs = As + 2 * BM * LDSR;
+  T* Bs = As + NBUF * BM * LDSR;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int ntn = (N + BN - 1) / BN;
-  const int m0 = (blockIdx.x / ntn) * BM;
-  const int n0 = (blockIdx.x % ntn) * BN;
+  // XCD-aware remap (bijective): workgroups dealt round-robin to the 8 XCDs get
+  // consecutive tiles per XCD, so the N-tiles of one A row-panel share an L2.
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int tile_id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int m0 = (tile_id / ntn) * BM;
+  const int n0 = (tile_id % ntn) * BN;
 
   uint4 ra[ACH], rb[BCH];
   auto gload = [&](int k0) {
@@ -119,10 +124,17 @@ __global__ void __launch_bounds__(256) gemm_kernel(const T* __restrict__ A, int 
 #pragma unroll
         for (int j = 0; j < TN; ++j) Tr::mma(acc[i][j], fa[i], fb[j]);
     }
-    if (kt + 1 < nk) sstore(cur ^ 1);
-    __syncthreads();
-    cur ^= 1;
+    if (NBUF == 2) {
+      if (kt + 1 < nk) sstore(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    } else if (kt + 1 < nk) {
+      __syncthreads();  // all waves done reading the single buffer
+      sstore(0);
+      __syncthreads();
+    }
   }
+  if (NBUF == 1) __syncthreads();
 
   // ---- epilogue: accumulators -> LDS C tile -> coalesced vector pass ----
   // (the staging ring is free: the last loop iteration ended with a barrier)
@@ -212,14 +224,14 @@ __global__ void __launch_bounds__(256) gemm_kernel(const T* __restrict__ A, int 
   }
 }
 
-template <typename T, int BM, int BN, int BK>
+template <typename T, int BM, int BN, int BK, int NBUF = 2>
 int launch(const void* A, int lda, const void* W, int ldw, int M, int N, int K, const Epi& ep, hipStream_t s) {
   constexpr int LDSR = BK + MT<T>::PAD;
-  size_t lds = (size_t)2 * (BM + BN) * LDSR * sizeof(T);
+  size_t lds = (size_t)NBUF * (BM + BN) * LDSR * sizeof(T);
   const size_t cbytes = (size_t)BM * (BN + 4) * 4;  // epilogue C tile
   if (cbytes > lds) lds = cbytes;
   const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, BK>), dim3(grid), dim3(256), lds, s, reinterpret_cast<const T*>(A),
+  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, BK, NBUF>), dim3(grid), dim3(256), lds, s, reinterpret_cast<const T*>(A),
                      lda, reinterpret_cast<const T*>(W), ldw, M, N, K, ep);
   SBK_CHECK_LAUNCH();
   return 0;
@@ -231,7 +243,9 @@ int launch(const void* A, int lda, const void* W, int ldw, int M, int N, int K, 
 // host asks for it here so weights are permuted consistently.
 SBK_API int sbk_gemm_glu_group(int dtype_bf16) { (void)dtype_bf16; return 16; }  // [value16 | gate16] groups
 
-// dtype_bf16: A and W are bf16 (else fp32).  tile: 0 auto, 1 = 128x128, 2 = 64x64, 3 = 128x64.
+// dtype_bf16: A and W are bf16 (else fp32).  tile: 0 auto, 1 = 128x128, 2 = 64x64, 3 = 128x64 (BK 64,
+// double-buffered); bf16 only: 4/5/6 = 64x64 / 64x128 / 128x64 with BK 256 single buffer,
+// 7 = 128x128 BK 128 single buffer, 8 = 64x64 BK 128 double buffer.
 SBK_API int sbk_gemm(int dtype_bf16, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
                      const float* bias, int act, float slope, const float* res, int ldr, float alpha,
                      const uint8_t* rowmask, void* out, int ldc, int out_bf16, int tile, void* stream) {
@@ -242,14 +256,18 @@ SBK_API int sbk_gemm(int dtype_bf16, const void* A, int lda, const void* W, int 
   if (act == ACT_GLU && (N % 32)) return SBK_ERR_ARG;  // whole [a16|gate16] groups
   Epi ep{bias, act, slope, res, ldr, alpha, rowmask, out, ldc, out_bf16};
   hipStream_t s = (hipStream_t)stream;
-  if (tile == 0) {
-    const long long t128 = (long long)((M + 127) / 128) * ((N + 127) / 128);
-    tile = t128 >= 512 ? 1 : 2;
-  }
+  if (tile == 0) tile = (dtype_bf16 && K <= 256 && N >= 512) ? 9 : 2;  // measured best (scripts/kbench.py)
   if (dtype_bf16) {
     switch (tile) {
       case 1: return launch<bf16_t, 128, 128, 64>(A, lda, W, ldw, M, N, K, ep, s);
       case 3: return launch<bf16_t, 128, 64, 64>(A, lda, W, ldw, M, N, K, ep, s);
+      case 4: return launch<bf16_t, 64, 64, 256, 1>(A, lda, W, ldw, M, N, K, ep, s);
+      case 5: return launch<bf16_t, 64, 128, 256, 1>(A, lda, W, ldw, M, N, K, ep, s);
+      case 6: return launch<bf16_t, 128, 64, 256, 1>(A, lda, W, ldw, M, N, K, ep, s);
+      case 7: return launch<bf16_t, 128, 128, 128, 1>(A, lda, W, ldw, M, N, K, ep, s);
+      case 8: return launch<bf16_t, 64, 64, 128, 2>(A, lda, W, ldw, M, N, K, ep, s);
+      case 9: return launch<bf16_t, 64, 64, 32, 2>(A, lda, W, ldw, M, N, K, ep, s);
+      case 10: return launch<bf16_t, 128, 64, 32, 2>(A, lda, W, ldw, M, N, K, ep, s);
       default: return launch<bf16_t, 64, 64, 64>(A, lda, W, ldw, M, N, K, ep, s);
     }
   }

@@ -55,7 +55,7 @@ def stft(x: torch.Tensor, window: torch.Tensor, tw_nc: torch.Tensor, tw_nfft: to
     scale = float(n_fft) ** -0.5 if normalized else 1.0
     rc = _lib.lib().sbk_spectrum(0, ptr(x), B, S, C, n_fft, hop, int(center), pad_mode, T, ptr(window),
                                  ptr(tw_nc), ptr(tw_nfft), int(onesided), scale, 1.0, 0.0, 0, st_p,
-                                 None, None, None, None, 0, 0, 0.0, 0.0, 0.0, ptr(out), None, stream_of(x))
+                                 None, None, None, None, 0, 0, 0, 0.0, 0.0, 0.0, ptr(out), None, stream_of(x))
     check(rc, "sbk_spectrum(stft)")
     return out
 
@@ -84,7 +84,7 @@ def power_spectrum(x: torch.Tensor, window: torch.Tensor, tw_nc: torch.Tensor, t
     scale = float(n_fft) ** -0.5 if normalized else 1.0
     rc = _lib.lib().sbk_spectrum(1, ptr(x), B, S, 1, n_fft, hop, int(center), pad_mode, T, ptr(window),
                                  ptr(tw_nc), ptr(tw_nfft), 1, scale, float(power), float(eps), int(log_mag),
-                                 st.ctypes.data_as(ctypes.c_void_p), None, None, None, None, 0, 0, 0.0, 0.0,
+                                 st.ctypes.data_as(ctypes.c_void_p), None, None, None, None, 0, 0, 0, 0.0, 0.0,
                                  0.0, ptr(out), None, stream_of(x))
     check(rc, "sbk_spectrum(power)")
     return out
@@ -112,7 +112,8 @@ def fbank(x: torch.Tensor, window: torch.Tensor, tw_nc: torch.Tensor, tw_nfft: t
     s = stream_of(x)
     rc = L.sbk_spectrum(2, ptr(x), B, S, 1, n_fft, hop, int(center), pad_mode, T, ptr(window), ptr(tw_nc),
                         ptr(tw_nfft), 1, 1.0, 1.0, 0.0, 0, None, ptr(mel_start), ptr(mel_len), ptr(mel_off),
-                        ptr(mel_w), n_mels, int(log_mel), multiplier, db_offset, amin, ptr(out), ptr(maxkey), s)
+                        ptr(mel_w), mel_w.numel(), n_mels, int(log_mel), multiplier, db_offset, amin, ptr(out),
+                        ptr(maxkey), s)
     check(rc, "sbk_spectrum(fbank)")
     if log_mel:
         check(L.sbk_topdb_clamp(ptr(out), ptr(maxkey), T * n_mels, B, top_db, s), "sbk_topdb_clamp")
