@@ -34,7 +34,8 @@ int sbk_fft_supported(int n_fft);
  * top_db clamp (:490-560, :691-712) — Fbank.forward (lobes/features.py:130-147).
  *   mode 0: STFT  -> out[bo*os_b + c*os_c + t*os_t + k*os_k + ri*os_ri]
  *   mode 1: power -> out[bo*os_b + c*os_c + t*os_t + k*os_k]  (power, eps, log_mag)
- *   mode 2: Fbank -> out (Bo, T, M) dB, per-sequence max key in maxkey (Bo,)
+ *   mode 2: Fbank -> out (Bo, T, M) dB; slot_max (Bo, sbk_spectrum_slots(..)) receives one
+ *           partial max per workgroup (input of sbk_topdb_clamp; no atomics, deterministic)
  * wav: (Bo, S, C) fp32; window: n_fft fp32 (win centred, zero padded);
  * twiddle_nc: n_fft/2 complex W_{n_fft/2}^m; twiddle_nfft: n_fft/2+1 complex W_{n_fft}^k;
  * out_strides: HOST array of 5 int64 (modes 0/1); mel_*: per-filter CSR of the
@@ -43,19 +44,27 @@ int sbk_spectrum(int mode, const float* wav, int Bo, int S, int C, int n_fft, in
                  int T, const float* window, const float* twiddle_nc, const float* twiddle_nfft, int onesided,
                  float norm_scale, float power, float eps, int log_mag, const long long* out_strides,
                  const int* mel_start, const int* mel_len, const int* mel_off, const float* mel_w, int n_melw,
-                 int M, int log_mel, float multiplier, float db_offset, float amin, float* out, int* maxkey,
+                 int M, int log_mel, float multiplier, float db_offset, float amin, float* out, float* slot_max,
                  void* stream);
+
+/* Number of per-sequence partial-max slots sbk_spectrum(mode 2) writes. */
+int sbk_spectrum_slots(int n_fft, int hop, int T, int M, int n_melw);
 
 /* Filterbank.forward on a spectrogram (N, T, F) -> (N, T, M) (features.py:490-560):
  * sparse CSR filters, or a dense (F, M) matrix when `dense` is non-null
  * (learnable filters, freeze=False). */
 int sbk_filterbank(const float* spec, int N, int T, int F, const int* mel_start, const int* mel_len,
                    const int* mel_off, const float* mel_w, const float* dense, int M, int log_mel, float multiplier,
-                   float db_offset, float amin, float* out, int* maxkey, void* stream);
+                   float db_offset, float amin, float* out, float* slot_max, void* stream);
+
+/* Number of per-sequence partial-max slots sbk_filterbank writes. */
+int sbk_filterbank_slots(int T, int F);
 
 /* top_db floor of _amplitude_to_DB (features.py:706-711), in place:
- * x[n, :] = max(x[n, :], max_n - top_db) for nseq sequences of per_seq values. */
-int sbk_topdb_clamp(float* x, const int* maxkey, long long per_seq, int nseq, float top_db, void* stream);
+ * x[n, :] = max(x[n, :], max_n - top_db) for nseq sequences of per_seq values,
+ * max_n = max of slot_max[n, 0:nslot]. */
+int sbk_topdb_clamp(float* x, const float* slot_max, int nslot, long long per_seq, int nseq, float top_db,
+                    void* stream);
 
 /* spectral_magnitude (features.py:347-356): y[i] = f(sum_q x[i, q]^2), q < L. */
 int sbk_magnitude(const float* x, float* y, long long n, int L, float power, float eps, int log_mag, void* stream);

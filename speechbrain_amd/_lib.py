@@ -29,7 +29,9 @@ SIGNATURES = {
     "sbk_spectrum": [_i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _i, _f, _f, _f, _i, _vp,
                      _vp, _vp, _vp, _vp, _i, _i, _i, _f, _f, _f, _vp, _vp, _vp],
     "sbk_filterbank": [_vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _i, _i, _f, _f, _f, _vp, _vp, _vp],
-    "sbk_topdb_clamp": [_vp, _vp, _ll, _i, _f, _vp],
+    "sbk_spectrum_slots": [_i, _i, _i, _i, _i],
+    "sbk_filterbank_slots": [_i, _i],
+    "sbk_topdb_clamp": [_vp, _vp, _i, _ll, _i, _f, _vp],
     "sbk_magnitude": [_vp, _vp, _ll, _i, _f, _f, _i, _vp],
     "sbk_dct": [_vp, _vp, _vp, _ll, _i, _i, _vp],
     "sbk_deltas": [_vp, _vp, _i, _i, _i, _i, _i, _vp],

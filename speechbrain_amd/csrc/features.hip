@@ -114,43 +114,58 @@ __device__ __forceinline__ void dft_small<8>(float2* v) {
   }
 }
 
-// One Stockham autosort stage of radix R over FPB frames held in LDS.
+// LDS layout of a frame's complex buffer: one float2 of padding every 8, so
+// the radix-8 first stage's stride-8 writes (and the later stages' strided
+// writes) hit distinct 64-bit bank pairs; frames are NCP float2 apart with
+// NCP odd so neighbouring frames do not alias either.
+__host__ __device__ constexpr int fpad(int i) { return i + (i >> 3); }
+__host__ __device__ constexpr int frame_stride(int nc) { return (fpad(nc - 1) + 1) | 1; }
+__host__ __device__ constexpr int first_radix(int n) {
+  return n % 8 == 0 ? 8 : n % 5 == 0 ? 5 : n % 4 == 0 ? 4 : n % 3 == 0 ? 3 : n % 2 == 0 ? 2 : 0;
+}
+
+template <int R>
+__device__ __forceinline__ void stockham_task(const float2* __restrict__ s, float2* __restrict__ d, int j, int nb,
+                                              int Ns, int k, int step, const float2* __restrict__ tw) {
+  float2 v[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) v[r] = s[fpad(j + r * nb)];
+#pragma unroll
+  for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw[r * k * step]);
+  dft_small<R>(v);
+  const int idxD = (j - k) * R + k;  // (j / Ns) * Ns * R + k
+#pragma unroll
+  for (int r = 0; r < R; ++r) d[fpad(idxD + r * Ns)] = v[r];
+}
+
+// One Stockham autosort stage of radix R over the block's frames (runtime size).
 template <int R>
 __device__ __forceinline__ void stockham_stage(const float2* __restrict__ src, float2* __restrict__ dst,
-                                               int nc, int Ns, const float2* __restrict__ tw, int nframes) {
+                                               int nc, int ncp, int Ns, const float2* __restrict__ tw, int nframes) {
   const int nb = nc / R;
   const int step = nc / (Ns * R);
-  for (int task = threadIdx.x; task < nframes * nb; task += blockDim.x) {
-    const int f = task / nb;
-    const int j = task - f * nb;
-    const float2* s = src + f * nc;
-    float2* d = dst + f * nc;
-    const int k = j % Ns;
-    float2 v[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) v[r] = s[j + r * nb];
-#pragma unroll
-    for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw[r * k * step]);
-    dft_small<R>(v);
-    const int idxD = (j / Ns) * Ns * R + k;
-#pragma unroll
-    for (int r = 0; r < R; ++r) d[idxD + r * Ns] = v[r];
+  int f = 0, j = threadIdx.x;
+  while (j >= nb) { j -= nb; ++f; }
+  while (f < nframes) {
+    stockham_task<R>(src + f * ncp, dst + f * ncp, j, nb, Ns, j % Ns, step, tw);
+    j += blockDim.x;
+    while (j >= nb) { j -= nb; ++f; }
   }
 }
 
-// Runs the whole complex FFT; returns the buffer holding the result.
-__device__ float2* run_fft(float2* bufA, float2* bufB, const FftPlan& plan, const float2* tw, int nframes) {
+// Runs the whole complex FFT (runtime plan); returns the buffer holding the result.
+__device__ float2* run_fft(float2* bufA, float2* bufB, const FftPlan& plan, int ncp, const float2* tw, int nframes) {
   float2* src = bufA;
   float2* dst = bufB;
   int Ns = 1;
   for (int s = 0; s < plan.nstages; ++s) {
     __syncthreads();
     switch (plan.radix[s]) {
-      case 8: stockham_stage<8>(src, dst, plan.nc, Ns, tw, nframes); break;
-      case 5: stockham_stage<5>(src, dst, plan.nc, Ns, tw, nframes); break;
-      case 4: stockham_stage<4>(src, dst, plan.nc, Ns, tw, nframes); break;
-      case 3: stockham_stage<3>(src, dst, plan.nc, Ns, tw, nframes); break;
-      default: stockham_stage<2>(src, dst, plan.nc, Ns, tw, nframes); break;
+      case 8: stockham_stage<8>(src, dst, plan.nc, ncp, Ns, tw, nframes); break;
+      case 5: stockham_stage<5>(src, dst, plan.nc, ncp, Ns, tw, nframes); break;
+      case 4: stockham_stage<4>(src, dst, plan.nc, ncp, Ns, tw, nframes); break;
+      case 3: stockham_stage<3>(src, dst, plan.nc, ncp, Ns, tw, nframes); break;
+      default: stockham_stage<2>(src, dst, plan.nc, ncp, Ns, tw, nframes); break;
     }
     Ns *= plan.radix[s];
     float2* t = src;
@@ -205,15 +220,31 @@ struct SpecArgs {
   int M, log_mel, n_melw;
   float multiplier, db_offset, amin, amin_db;
   float* out;
-  int* maxkey;  // (Bfold,) per-sequence max dB key
+  float* slot_max;  // (Bfold, ceil(T / fpb)) per-block max dB (top_db reference)
 };
 
 enum { MODE_STFT = 0, MODE_POWER = 1, MODE_FBANK = 2 };
 
+// Visits (f, j), f < nf, j < W, in the order of i = f*W + j strided by the
+// block size, without a runtime division per element.
+template <class Fn>
+__device__ __forceinline__ void for_fj(int nf, int W, Fn&& fn) {
+  int f = 0, j = threadIdx.x;
+  while (j >= W) { j -= W; ++f; }
+  while (f < nf) {
+    fn(f, j);
+    j += blockDim.x;
+    while (j >= W) { j -= W; ++f; }
+  }
+}
+
+// Runtime-plan spectrum kernel (any n_fft the radix set supports).
 template <int MODE>
 __global__ void __launch_bounds__(256) spec_kernel(SpecArgs a, FftPlan plan) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ float red[4];
   const int nc = plan.nc;
+  const int ncp = frame_stride(nc);
   const int nblk_t = (a.T + a.fpb - 1) / a.fpb;
   const int bf = blockIdx.x / nblk_t;
   const int t0 = (blockIdx.x - bf * nblk_t) * a.fpb;
@@ -222,57 +253,90 @@ __global__ void __launch_bounds__(256) spec_kernel(SpecArgs a, FftPlan plan) {
   const float* wrow = a.wav + (long long)bo * a.S * a.C + ch;
 
   float2* bufA = reinterpret_cast<float2*>(smem);
-  float2* bufB = bufA + a.fpb * nc;
-  float2* tw = bufB + a.fpb * nc;           // W_nc^m, staged once per block
-  float2* tw2 = tw + nc;                    // W_nfft^k, k <= nc
+  float2* bufB = bufA + a.fpb * ncp;
+  float* tab = reinterpret_cast<float*>(bufB + a.fpb * ncp);  // tables, staged once per block
+  float2* tw = reinterpret_cast<float2*>(tab);                // W_nc^m
+  float2* tw2 = tw + nc;                                      // W_nfft^k, k <= nc
   int* mstart = reinterpret_cast<int*>(tw2 + nc + 1);
   int* mlen = mstart + a.M;
   int* moff = mlen + a.M;
   float* mw = reinterpret_cast<float*>(moff + a.M);
-  float* win = mw + (MODE == MODE_FBANK ? a.n_melw : 0);
-  float* smp = win + a.n_fft;
-  for (int i = threadIdx.x; i < a.n_fft; i += blockDim.x) win[i] = a.window[i];
-  for (int i = threadIdx.x; i < nc; i += blockDim.x) tw[i] = a.tw[i];
-  for (int i = threadIdx.x; i <= nc; i += blockDim.x) tw2[i] = a.tw2[i];
-  if (MODE == MODE_FBANK) {
-    for (int i = threadIdx.x; i < a.M; i += blockDim.x) {
-      mstart[i] = a.mel_start[i];
-      mlen[i] = a.mel_len[i];
-      moff[i] = a.mel_off[i];
-    }
-    for (int i = threadIdx.x; i < a.n_melw; i += blockDim.x) mw[i] = a.mel_w[i];
-  }
+  // table segments: [tw | tw2 | mstart | mlen | moff | mw]
+  const int b1 = 2 * nc, b2 = b1 + 2 * nc + 2, b3 = b2 + a.M, b4 = b3 + a.M, b5 = b4 + a.M;
+  const int ntab = b5 + a.n_melw;
 
-  // 1) stage the samples spanned by this block's frames
+  // 1) prologue: every global load of a chunk (tables, frame samples, window)
+  //    is issued before the first LDS store, so the block pays one memory
+  //    latency instead of one per table / sample row.
   const int pad = a.center ? a.n_fft / 2 : 0;
   const int base = t0 * a.hop - pad;
   const int span = (nf - 1) * a.hop + a.n_fft;
-  for (int q = threadIdx.x; q < span; q += blockDim.x) {
-    bool ok;
-    int p = map_pos(base + q, a.S, a.pad_mode, &ok);
-    smp[q] = ok ? wrow[(long long)p * a.C] : 0.f;
-  }
-  __syncthreads();
-  // 2) window + pack real frame into nc complex values
-  for (int i = threadIdx.x; i < nf * nc; i += blockDim.x) {
-    const int f = i / nc, m = i - f * nc;
-    const float* fr = smp + f * a.hop;
-    bufA[f * nc + m] = make_float2(fr[2 * m] * win[2 * m], fr[2 * m + 1] * win[2 * m + 1]);
+  const bool interior = base >= 0 && base + span <= a.S;
+  const bool vec2 = interior && a.C == 1 && ((a.hop | base | a.S) & 1) == 0;
+  const int nfe = nf * nc;
+  constexpr int KT = 8, KF = 8;
+  for (int tb = 0, fb = 0; tb < ntab || fb < nfe; tb += KT * 256, fb += KF * 256) {
+    float tv[KT];
+    float2 fv[KF], wv[KF];
+#pragma unroll
+    for (int u = 0; u < KT; ++u) {
+      const int i = tb + (int)threadIdx.x + u * 256;
+      float v = 0.f;
+      if (i < b1) v = reinterpret_cast<const float*>(a.tw)[i];
+      else if (i < b2) v = reinterpret_cast<const float*>(a.tw2)[i - b1];
+      else if (i < b3) v = __int_as_float(a.mel_start[i - b2]);
+      else if (i < b4) v = __int_as_float(a.mel_len[i - b3]);
+      else if (i < b5) v = __int_as_float(a.mel_off[i - b4]);
+      else if (i < ntab) v = a.mel_w[i - b5];
+      tv[u] = v;
+    }
+#pragma unroll
+    for (int u = 0; u < KF; ++u) {
+      const int e = fb + (int)threadIdx.x + u * 256;
+      fv[u] = wv[u] = make_float2(0.f, 0.f);
+      if (e < nfe) {
+        const int f = e / nc, m = e - f * nc;
+        const int q = f * a.hop + 2 * m;
+        wv[u] = *reinterpret_cast<const float2*>(a.window + 2 * m);
+        if (vec2) {
+          fv[u] = *reinterpret_cast<const float2*>(wrow + base + q);
+        } else if (interior) {
+          fv[u] = make_float2(wrow[(long long)(base + q) * a.C], wrow[(long long)(base + q + 1) * a.C]);
+        } else {
+          bool ok0, ok1;
+          const int p0 = map_pos(base + q, a.S, a.pad_mode, &ok0);
+          const int p1 = map_pos(base + q + 1, a.S, a.pad_mode, &ok1);
+          fv[u] = make_float2(ok0 ? wrow[(long long)p0 * a.C] : 0.f, ok1 ? wrow[(long long)p1 * a.C] : 0.f);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < KT; ++u) {
+      const int i = tb + (int)threadIdx.x + u * 256;
+      if (i < ntab) tab[i] = tv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < KF; ++u) {
+      const int e = fb + (int)threadIdx.x + u * 256;
+      if (e < nfe) {
+        const int f = e / nc, m = e - f * nc;
+        bufA[f * ncp + fpad(m)] = make_float2(fv[u].x * wv[u].x, fv[u].y * wv[u].y);
+      }
+    }
   }
   // 3) complex FFT of size nc
-  float2* Z = run_fft(bufA, bufB, plan, tw, nf);
+  float2* Z = run_fft(bufA, bufB, plan, ncp, tw, nf);
   float2* other = (Z == bufA) ? bufB : bufA;
 
   // 4) split into the real-input spectrum X[k], k = 0..nc
   const int nbins = nc + 1;
   if (MODE == MODE_STFT) {
     const int nout = a.onesided ? nbins : a.n_fft;
-    for (int i = threadIdx.x; i < nf * nout; i += blockDim.x) {
-      const int f = i / nout, kk = i - f * nout;
+    for_fj(nf, nout, [&](int f, int kk) {
       const bool mirror = kk > nc;
       const int k = mirror ? a.n_fft - kk : kk;
-      const float2 zk = Z[f * nc + (k % nc)];
-      const float2 zr = Z[f * nc + ((nc - k) % nc)];
+      const float2 zk = Z[f * ncp + fpad(k == nc ? 0 : k)];
+      const float2 zr = Z[f * ncp + fpad(k == 0 ? 0 : nc - k)];
       const float2 zc = make_float2(zr.x, -zr.y);
       const float2 E = make_float2(0.5f * (zk.x + zc.x), 0.5f * (zk.y + zc.y));
       const float2 O = mul_mi(make_float2(0.5f * (zk.x - zc.x), 0.5f * (zk.y - zc.y)));
@@ -281,14 +345,13 @@ __global__ void __launch_bounds__(256) spec_kernel(SpecArgs a, FftPlan plan) {
       float* o = a.out + bo * a.os_b + ch * a.os_c + (long long)(t0 + f) * a.os_t + kk * a.os_k;
       o[0] = X.x * a.norm_scale;
       o[a.os_ri] = X.y * a.norm_scale;
-    }
+    });
     return;
   }
   float* P = reinterpret_cast<float*>(other);  // (nf, nbins) power
-  for (int i = threadIdx.x; i < nf * nbins; i += blockDim.x) {
-    const int f = i / nbins, k = i - f * nbins;
-    const float2 zk = Z[f * nc + (k % nc)];
-    const float2 zr = Z[f * nc + ((nc - k) % nc)];
+  for_fj(nf, nbins, [&](int f, int k) {
+    const float2 zk = Z[f * ncp + fpad(k == nc ? 0 : k)];
+    const float2 zr = Z[f * ncp + fpad(k == 0 ? 0 : nc - k)];
     const float2 zc = make_float2(zr.x, -zr.y);
     const float2 E = make_float2(0.5f * (zk.x + zc.x), 0.5f * (zk.y + zc.y));
     const float2 O = mul_mi(make_float2(0.5f * (zk.x - zc.x), 0.5f * (zk.y - zc.y)));
@@ -304,16 +367,15 @@ __global__ void __launch_bounds__(256) spec_kernel(SpecArgs a, FftPlan plan) {
       if (a.log_mag) s = logf(s + a.eps);
       a.out[bo * a.os_b + ch * a.os_c + (long long)(t0 + f) * a.os_t + k * a.os_k] = s;
     } else {
-      P[i] = s;
+      P[f * nbins + k] = s;
     }
-  }
+  });
   if (MODE == MODE_POWER) return;
   __syncthreads();
   // 5) sparse mel projection + dB + running max
   float lmax = -INFINITY;
   float* orow = a.out + ((long long)bf * a.T + t0) * a.M;
-  for (int i = threadIdx.x; i < nf * a.M; i += blockDim.x) {
-    const int f = i / a.M, j = i - f * a.M;
+  for_fj(nf, a.M, [&](int f, int j) {
     const float* pf = P + f * nbins + mstart[j];
     const float* w = mw + moff[j];
     const int L = mlen[j];
@@ -324,11 +386,11 @@ __global__ void __launch_bounds__(256) spec_kernel(SpecArgs a, FftPlan plan) {
       acc = acc <= a.amin ? a.amin_db : a.multiplier * log10f(acc) - a.db_offset;
       lmax = fmaxf(lmax, acc);
     }
-    orow[i] = acc;
-  }
-  if (a.log_mel) {
-    lmax = wave_max(lmax);
-    if ((threadIdx.x & 63) == 0 && lmax > -INFINITY) atomicMax(a.maxkey + bf, float_to_key(lmax));
+    orow[f * a.M + j] = acc;
+  });
+  if (a.log_mel) {  // one partial max per block, reduced by the top_db kernel (no atomics)
+    const float m = block_max(lmax, red);
+    if (threadIdx.x == 0) a.slot_max[blockIdx.x] = m;
   }
 }
 
@@ -344,21 +406,22 @@ struct FbArgs {
   int M, log_mel, rows_per_block;
   float multiplier, db_offset, amin, amin_db;
   float* out;
-  int* maxkey;
+  float* slot_max;  // (N, ceil(T / rows_per_block)) per-block max dB
 };
 
+// One block per (sequence n, tile of rows_per_block frames).
 __global__ void __launch_bounds__(256) filterbank_kernel(FbArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ float red[4];
   float* rowbuf = reinterpret_cast<float*>(smem);
-  const long long nrows = (long long)a.N * a.T;
-  const long long r0 = (long long)blockIdx.x * a.rows_per_block;
-  const int nr = (int)min((long long)a.rows_per_block, nrows - r0);
+  const int nblk_t = (a.T + a.rows_per_block - 1) / a.rows_per_block;
+  const int n = blockIdx.x / nblk_t;
+  const long long r0 = (long long)n * a.T + (long long)(blockIdx.x - n * nblk_t) * a.rows_per_block;
+  const int nr = (int)min((long long)a.rows_per_block, (long long)(n + 1) * a.T - r0);
   for (int i = threadIdx.x; i < nr * a.F; i += blockDim.x) rowbuf[i] = a.spec[r0 * a.F + i];
   __syncthreads();
   float lmax = -INFINITY;
-  int cur_n = -1;
-  for (int i = threadIdx.x; i < nr * a.M; i += blockDim.x) {
-    const int rr = i / a.M, j = i - rr * a.M;
+  for_fj(nr, a.M, [&](int rr, int j) {
     const float* pf = rowbuf + rr * a.F;
     float acc = 0.f;
     if (a.dense) {
@@ -371,41 +434,40 @@ __global__ void __launch_bounds__(256) filterbank_kernel(FbArgs a) {
     }
     if (a.log_mel) {
       acc = acc <= a.amin ? a.amin_db : a.multiplier * log10f(acc) - a.db_offset;
-      const int n = (int)((r0 + rr) / a.T);
-      // rows of one block may straddle two sequences: flush per sequence
-      if (n != cur_n) {
-        if (cur_n >= 0 && lmax > -INFINITY) atomicMax(a.maxkey + cur_n, float_to_key(lmax));
-        cur_n = n;
-        lmax = -INFINITY;
-      }
       lmax = fmaxf(lmax, acc);
     }
     a.out[(r0 + rr) * a.M + j] = acc;
+  });
+  if (a.log_mel) {
+    const float m = block_max(lmax, red);
+    if (threadIdx.x == 0) a.slot_max[blockIdx.x] = m;
   }
-  if (a.log_mel && cur_n >= 0 && lmax > -INFINITY) atomicMax(a.maxkey + cur_n, float_to_key(lmax));
 }
 
-// x[n, :] = max(x[n, :], max_n - top_db), per sequence n of `per_seq` floats.
-__global__ void topdb_clamp_kernel(float* __restrict__ x, const int* __restrict__ maxkey,
-                                   long long per_seq, int nseq, float top_db) {
-  const long long total = per_seq * nseq;
-  for (long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < total;
-       i += (long long)gridDim.x * blockDim.x * 4) {
-    if (i + 3 < total && (per_seq % 4) == 0) {
-      const int n = (int)(i / per_seq);
-      const float fl = key_to_float(maxkey[n]) - top_db;
-      float4 v = *reinterpret_cast<float4*>(x + i);
+// x[n, :] = max(x[n, :], max_n - top_db), per sequence n of `per_seq` floats;
+// max_n is the max of the sequence's nslot per-block partial maxima.
+// Grid (chunks, nseq): every block reduces its sequence's partials first.
+__global__ void __launch_bounds__(256) topdb_clamp_kernel(float* __restrict__ x, const float* __restrict__ slot_max,
+                                                          int nslot, long long per_seq, float top_db) {
+  __shared__ float red[4];
+  const int n = blockIdx.y;
+  float m = -INFINITY;
+  for (int i = threadIdx.x; i < nslot; i += blockDim.x) m = fmaxf(m, slot_max[(long long)n * nslot + i]);
+  const float fl = block_max(m, red) - top_db;
+  float* xs = x + (long long)n * per_seq;
+  const long long chunk = (long long)blockDim.x * 16;
+  const long long c0 = (long long)blockIdx.x * chunk, c1 = min(per_seq, c0 + chunk);
+  if ((per_seq & 3) == 0) {
+    for (long long i = c0 + threadIdx.x * 4; i < c1; i += blockDim.x * 4) {
+      float4 v = *reinterpret_cast<float4*>(xs + i);
       v.x = fmaxf(v.x, fl);
       v.y = fmaxf(v.y, fl);
       v.z = fmaxf(v.z, fl);
       v.w = fmaxf(v.w, fl);
-      *reinterpret_cast<float4*>(x + i) = v;
-    } else {
-      for (long long e = i; e < min(i + 4, total); ++e) {
-        const int n = (int)(e / per_seq);
-        x[e] = fmaxf(x[e], key_to_float(maxkey[n]) - top_db);
-      }
+      *reinterpret_cast<float4*>(xs + i) = v;
     }
+  } else {
+    for (long long i = c0 + threadIdx.x; i < c1; i += blockDim.x) xs[i] = fmaxf(xs[i], fl);
   }
 }
 
@@ -541,6 +603,341 @@ int fill_plan(FftPlan* p, int nc) {
   return 0;
 }
 
+
+// ---------------------------------------------------------------------------
+// Static-plan spectrum kernel for the common FFT sizes (n_fft 400/512/1024/
+// 2048).  NT threads own FPB frames; every stage's task -> thread map is a
+// compile-time constant, so the per-element index arithmetic folds away and
+// each thread runs a fixed, branch-free set of butterflies:
+//   * stage 0 reads its radix-R0 inputs straight from the waveform (window
+//     applied in registers), so the frames never pass through LDS raw;
+//   * later stages run in place (read -> barrier -> write -> barrier) on one
+//     padded LDS buffer per frame;
+//   * the real-FFT split handles bins k and nc-k in one thread.
+// For n_fft 400 (nc 200 = 8*5*5): FPB 8, NT 320 -> each radix-5 stage is
+// exactly one task per thread.
+// ---------------------------------------------------------------------------
+__host__ __device__ constexpr int plan_nstages(int nc) {
+  int n = 0;
+  while (nc > 1) { nc /= first_radix(nc); ++n; }
+  return n;
+}
+__host__ __device__ constexpr int plan_radix(int nc, int s) {
+  for (int i = 0; i < s; ++i) nc /= first_radix(nc);
+  return first_radix(nc);
+}
+__host__ __device__ constexpr int plan_ns(int nc, int s) {
+  int ns = 1;
+  for (int i = 0; i < s; ++i) { const int r = first_radix(nc); ns *= r; nc /= r; }
+  return ns;
+}
+
+template <int NC, int FPB, int NT, int S>
+__device__ __forceinline__ void static_stage(float2* __restrict__ buf, const float2* __restrict__ tw) {
+  if constexpr (S < plan_nstages(NC)) {
+    constexpr int R = plan_radix(NC, S), NS = plan_ns(NC, S), NB = NC / R;
+    constexpr int STEP = NC / (NS * R), NCP = frame_stride(NC);
+    constexpr int TASKS = FPB * NB, TPT = (TASKS + NT - 1) / NT;
+    float2 v[TPT][R];
+#pragma unroll
+    for (int u = 0; u < TPT; ++u) {
+      const int t = threadIdx.x + u * NT;
+      if (TASKS % NT == 0 || t < TASKS) {
+        const int f = t / NB, j = t - f * NB;
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[u][r] = buf[f * NCP + fpad(j + r * NB)];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < TPT; ++u) {
+      const int t = threadIdx.x + u * NT;
+      if (TASKS % NT == 0 || t < TASKS) {
+        const int f = t / NB, j = t - f * NB, k = j % NS;
+#pragma unroll
+        for (int r = 1; r < R; ++r) v[u][r] = cmul(v[u][r], tw[r * k * STEP]);
+        dft_small<R>(v[u]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) buf[f * NCP + fpad((j - k) * R + k + r * NS)] = v[u][r];
+      }
+    }
+    __syncthreads();
+    static_stage<NC, FPB, NT, S + 1>(buf, tw);
+  }
+}
+
+template <int MODE, int NC, int FPB, int NT>
+__global__ void __launch_bounds__(NT) spec_static_kernel(SpecArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ float red[NT / 64];
+  constexpr int NCP = frame_stride(NC), NBINS = NC + 1;
+  const int tid = threadIdx.x;
+  const int nblk_t = (a.T + FPB - 1) / FPB;
+  const int bf = blockIdx.x / nblk_t;
+  const int t0 = (blockIdx.x - bf * nblk_t) * FPB;
+  const int nf = min(FPB, a.T - t0);
+  const int bo = bf / a.C, ch = bf - bo * a.C;
+  const float* wrow = a.wav + (long long)bo * a.S * a.C + ch;
+
+  float2* buf = reinterpret_cast<float2*>(smem);                 // FPB x NCP complex
+  float* P = reinterpret_cast<float*>(buf + FPB * NCP);           // FPB x NBINS power (FBANK)
+  float* tab = P + (MODE == MODE_FBANK ? FPB * NBINS : 0);
+  float2* tw = reinterpret_cast<float2*>(tab);                    // W_nc^m
+  float2* tw2 = tw + NC;                                          // W_nfft^k
+  int* mstart = reinterpret_cast<int*>(tw2 + NC + 1);
+  int* mlen = mstart + a.M;
+  int* moff = mlen + a.M;
+  float* mw = reinterpret_cast<float*>(moff + a.M);
+  // ---- tables: per-segment loads issued first, stored once the frame loads
+  //      are in flight too (one memory latency for the whole prologue)
+  constexpr int KW = (NC + NT - 1) / NT, KW2 = (NC + 1 + NT - 1) / NT, KMW = 4;
+  float2 tv1[KW], tv2[KW2];
+  float mwv[KMW];
+  int ms = 0, ml = 0, mo = 0;
+#pragma unroll
+  for (int u = 0; u < KW; ++u) {
+    const int i = tid + u * NT;
+    tv1[u] = (NC % NT == 0 || i < NC) ? a.tw[i] : make_float2(0.f, 0.f);
+  }
+#pragma unroll
+  for (int u = 0; u < KW2; ++u) {
+    const int i = tid + u * NT;
+    tv2[u] = i <= NC ? a.tw2[i] : make_float2(0.f, 0.f);
+  }
+  if constexpr (MODE == MODE_FBANK) {
+    if (tid < a.M) {
+      ms = a.mel_start[tid];
+      ml = a.mel_len[tid];
+      mo = a.mel_off[tid];
+    }
+#pragma unroll
+    for (int u = 0; u < KMW; ++u) {
+      const int i = tid + u * NT;
+      mwv[u] = i < a.n_melw ? a.mel_w[i] : 0.f;
+    }
+  }
+
+  // ---- stage 0 straight from the waveform: radix-R0 butterflies, Ns = 1
+  {
+    constexpr int R = first_radix(NC), NB = NC / R;
+    constexpr int TASKS = FPB * NB, TPT = (TASKS + NT - 1) / NT;
+    const int pad = a.center ? a.n_fft / 2 : 0;
+    const int base = t0 * a.hop - pad;
+    const int span = (nf - 1) * a.hop + a.n_fft;
+    const bool interior = base >= 0 && base + span <= a.S;
+    const bool vec2 = interior && a.C == 1 && ((a.hop | base | a.S) & 1) == 0;
+    float2 v[TPT][R];
+#pragma unroll
+    for (int u = 0; u < TPT; ++u) {
+      const int t = tid + u * NT;
+      const int f = t / NB, j = t - f * NB;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int m = j + r * NB;
+        float2 x = make_float2(0.f, 0.f);
+        if ((TASKS % NT == 0 || t < TASKS) && f < nf) {
+          const int q = base + f * a.hop + 2 * m;
+          if (vec2) {  // row pointer once per task, constant offsets per r
+            x = *reinterpret_cast<const float2*>(wrow + (base + f * a.hop + 2 * j) + 2 * r * NB);
+          } else if (interior) {
+            x = make_float2(wrow[(long long)q * a.C], wrow[(long long)(q + 1) * a.C]);
+          } else {
+            bool ok0, ok1;
+            const int p0 = map_pos(q, a.S, a.pad_mode, &ok0);
+            const int p1 = map_pos(q + 1, a.S, a.pad_mode, &ok1);
+            x = make_float2(ok0 ? wrow[(long long)p0 * a.C] : 0.f, ok1 ? wrow[(long long)p1 * a.C] : 0.f);
+          }
+          const float2 w = *reinterpret_cast<const float2*>(a.window + 2 * j + 2 * r * NB);
+          x.x *= w.x;
+          x.y *= w.y;
+        }
+        v[u][r] = x;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < KW; ++u) {
+      const int i = tid + u * NT;
+      if (NC % NT == 0 || i < NC) tw[i] = tv1[u];
+    }
+#pragma unroll
+    for (int u = 0; u < KW2; ++u) {
+      const int i = tid + u * NT;
+      if (i <= NC) tw2[i] = tv2[u];
+    }
+    if constexpr (MODE == MODE_FBANK) {
+      if (tid < a.M) {
+        mstart[tid] = ms;
+        mlen[tid] = ml;
+        moff[tid] = mo;
+      }
+      for (int i = tid + NT; i < a.M; i += NT) {  // M > NT (rare)
+        mstart[i] = a.mel_start[i];
+        mlen[i] = a.mel_len[i];
+        moff[i] = a.mel_off[i];
+      }
+#pragma unroll
+      for (int u = 0; u < KMW; ++u) {
+        const int i = tid + u * NT;
+        if (i < a.n_melw) mw[i] = mwv[u];
+      }
+      for (int i = tid + KMW * NT; i < a.n_melw; i += NT) mw[i] = a.mel_w[i];
+    }
+#pragma unroll
+    for (int u = 0; u < TPT; ++u) {
+      const int t = tid + u * NT;
+      if (TASKS % NT == 0 || t < TASKS) {
+        const int f = t / NB, j = t - f * NB;
+        dft_small<R>(v[u]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) buf[f * NCP + fpad(j * R + r)] = v[u][r];
+      }
+    }
+    __syncthreads();
+  }
+  // ---- remaining stages in place
+  static_stage<NC, FPB, NT, 1>(buf, tw);
+
+  // ---- real split: bins k and NC-k per task
+  constexpr int NPAIR = NC / 2 + 1, TASKS = FPB * NPAIR, TPT = (TASKS + NT - 1) / NT;
+#pragma unroll
+  for (int u = 0; u < TPT; ++u) {
+    const int t = tid + u * NT;
+    if (!(TASKS % NT == 0 || t < TASKS)) continue;
+    const int f = t / NPAIR, k = t - f * NPAIR;
+    if (f >= nf) continue;
+    const float2 zk = buf[f * NCP + fpad(k)];
+    const float2 zr = buf[f * NCP + fpad(k == 0 ? 0 : NC - k)];
+    float2 X[2];
+    int bins[2] = {k, NC - k};
+    const int nb = (k == NC - k) ? 1 : 2;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float2 za = h ? zr : zk, zb = h ? zk : zr;
+      const float2 zc = make_float2(zb.x, -zb.y);
+      const float2 E = make_float2(0.5f * (za.x + zc.x), 0.5f * (za.y + zc.y));
+      const float2 O = mul_mi(make_float2(0.5f * (za.x - zc.x), 0.5f * (za.y - zc.y)));
+      X[h] = cadd(E, cmul(tw2[bins[h]], O));
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h >= nb) break;
+      const int kk = bins[h];
+      float2 x = X[h];
+      x.x *= a.norm_scale;
+      x.y *= a.norm_scale;
+      if (MODE == MODE_STFT) {
+        float* o = a.out + bo * a.os_b + ch * a.os_c + (long long)(t0 + f) * a.os_t + kk * a.os_k;
+        o[0] = x.x;
+        o[a.os_ri] = x.y;
+      } else {
+        float p = x.x * x.x + x.y * x.y;
+        if (a.power != 1.0f) {
+          if (a.power < 1.0f) p += a.eps;
+          p = powf(p, a.power);
+        }
+        if (MODE == MODE_POWER) {
+          if (a.log_mag) p = logf(p + a.eps);
+          a.out[bo * a.os_b + ch * a.os_c + (long long)(t0 + f) * a.os_t + kk * a.os_k] = p;
+        } else {
+          P[f * NBINS + kk] = p;
+        }
+      }
+    }
+  }
+  if constexpr (MODE == MODE_FBANK) {
+    __syncthreads();
+    float lmax = -INFINITY;
+    float* orow = a.out + ((long long)bf * a.T + t0) * a.M;
+    // lane -> (mel j = t / FPB, frame f = t % FPB): a wave covers 64/FPB
+    // neighbouring filters, whose lengths are nearly equal (little divergence)
+    for (int t = tid; t < a.M * FPB; t += NT) {
+      const int j = t / FPB, f = t - j * FPB;
+      if (f >= nf) continue;
+      const float* pf = P + f * NBINS + mstart[j];
+      const float* w = mw + moff[j];
+      const int L = mlen[j];
+      float acc = 0.f;
+      for (int q = 0; q < L; ++q) acc = fmaf(pf[q], w[q], acc);
+      if (a.log_mel) {
+        acc = acc <= a.amin ? a.amin_db : a.multiplier * log10f(acc) - a.db_offset;
+        lmax = fmaxf(lmax, acc);
+      }
+      orow[f * a.M + j] = acc;
+    }
+    if (a.log_mel) {
+      const float m = block_max(lmax, red);
+      if (tid == 0) a.slot_max[blockIdx.x] = m;
+    }
+  }
+}
+
+template <int NC> struct StaticCfg;
+template <> struct StaticCfg<200> { static constexpr int FPB = 8, NT = 320; };
+template <> struct StaticCfg<256> { static constexpr int FPB = 8, NT = 256; };
+template <> struct StaticCfg<512> { static constexpr int FPB = 4, NT = 256; };
+template <> struct StaticCfg<1024> { static constexpr int FPB = 2, NT = 256; };
+
+template <int NC>
+size_t static_lds(int mode, int M, int n_melw) {
+  constexpr int FPB = StaticCfg<NC>::FPB;
+  return (size_t)FPB * frame_stride(NC) * sizeof(float2) + (mode == MODE_FBANK ? (size_t)FPB * (NC + 1) * 4 : 0) +
+         (size_t)(4 * NC + 2 + 3 * M + n_melw) * 4;
+}
+
+template <int MODE, int NC>
+void launch_static(int nblk_rows, hipStream_t s, const SpecArgs& a) {
+  constexpr int FPB = StaticCfg<NC>::FPB, NT = StaticCfg<NC>::NT;
+  const int nblk = nblk_rows * ((a.T + FPB - 1) / FPB);
+  hipLaunchKernelGGL((spec_static_kernel<MODE, NC, FPB, NT>), dim3(nblk), dim3(NT),
+                     static_lds<NC>(MODE, a.M, a.n_melw), s, a);
+}
+
+// Static-plan FFT sizes (n_fft 400 / 512 / 1024 / 2048); 0 = runtime plan.
+int static_nc(int nc, int mode, int onesided) {
+  if (mode == MODE_STFT && !onesided) return 0;
+  return (nc == 200 || nc == 256 || nc == 512 || nc == 1024) ? nc : 0;
+}
+int static_fpb(int nc) {
+  switch (nc) {
+    case 200: return StaticCfg<200>::FPB;
+    case 256: return StaticCfg<256>::FPB;
+    case 512: return StaticCfg<512>::FPB;
+    default: return StaticCfg<1024>::FPB;
+  }
+}
+size_t static_lds_for(int nc, int mode, int M, int n_melw) {
+  switch (nc) {
+    case 200: return static_lds<200>(mode, M, n_melw);
+    case 256: return static_lds<256>(mode, M, n_melw);
+    case 512: return static_lds<512>(mode, M, n_melw);
+    default: return static_lds<1024>(mode, M, n_melw);
+  }
+}
+
+template <int MODE>
+void launch_static_m(int nc, int rows, hipStream_t s, const SpecArgs& a) {
+  switch (nc) {
+    case 200: launch_static<MODE, 200>(rows, s, a); break;
+    case 256: launch_static<MODE, 256>(rows, s, a); break;
+    case 512: launch_static<MODE, 512>(rows, s, a); break;
+    default: launch_static<MODE, 1024>(rows, s, a); break;
+  }
+}
+
+void launch_spec(int mode, int nc, int rows, size_t lds, hipStream_t s, const SpecArgs& a, const FftPlan& plan) {
+  const int snc = static_nc(nc, mode, a.onesided);
+  if (snc) {
+    if (mode == MODE_STFT) launch_static_m<MODE_STFT>(snc, rows, s, a);
+    else if (mode == MODE_POWER) launch_static_m<MODE_POWER>(snc, rows, s, a);
+    else launch_static_m<MODE_FBANK>(snc, rows, s, a);
+    return;
+  }
+  const dim3 grid(rows * ((a.T + a.fpb - 1) / a.fpb));
+  if (mode == MODE_STFT) hipLaunchKernelGGL(spec_kernel<MODE_STFT>, grid, dim3(256), lds, s, a, plan);
+  else if (mode == MODE_POWER) hipLaunchKernelGGL(spec_kernel<MODE_POWER>, grid, dim3(256), lds, s, a, plan);
+  else hipLaunchKernelGGL(spec_kernel<MODE_FBANK>, grid, dim3(256), lds, s, a, plan);
+}
+
 inline int grid_for(long long n, int block) {
   long long g = (n + block - 1) / block;
   if (g > 8192) g = 8192;
@@ -560,14 +957,51 @@ SBK_API int sbk_fft_supported(int n_fft) {
   return fill_plan(&p, n_fft / 2) == 0 ? 1 : 0;
 }
 
+namespace {
+// Frames per spectrum workgroup: as many as fit ~72 KB of LDS (<= 16).
+// LDS of a spectrum workgroup: two padded frame buffers + the tables.
+size_t spec_lds(int n_fft, int M, int n_melw, int fpb) {
+  const int nc = n_fft / 2, ncp = frame_stride(nc);
+  return (size_t)2 * fpb * ncp * sizeof(float2) + (size_t)(2 * nc + 1) * sizeof(float2) +
+         (size_t)(3 * M + n_melw) * 4;
+}
+// Frames per workgroup: up to 8 while the LDS stays under ~40 KB (4
+// workgroups per CU), fewer for long FFTs.
+int spec_fpb(int n_fft, int hop, int M, int n_melw) {
+  (void)hop;
+  int fpb = 8;
+  while (fpb > 1 && spec_lds(n_fft, M, n_melw, fpb) > 40 * 1024) fpb >>= 1;
+  return spec_lds(n_fft, M, n_melw, fpb) > 160 * 1024 ? 0 : fpb;
+}
+int fb_rows_per_block(int F) {
+  int rpb = 8;
+  while (rpb > 1 && (size_t)rpb * F * 4 > 48 * 1024) rpb >>= 1;
+  return rpb;
+}
+}  // namespace
+
+SBK_API int sbk_spectrum_slots(int n_fft, int hop, int T, int M, int n_melw) {
+  if (n_fft < 4 || (n_fft & 1) || T <= 0) return 0;
+  const int snc = static_nc(n_fft / 2, MODE_FBANK, 1);
+  const int fpb = snc ? static_fpb(snc) : spec_fpb(n_fft, hop, M, n_melw);
+  return fpb ? (T + fpb - 1) / fpb : 0;
+}
+
+SBK_API int sbk_filterbank_slots(int T, int F) {
+  if (T <= 0 || F <= 0) return 0;
+  const int rpb = fb_rows_per_block(F);
+  return (T + rpb - 1) / rpb;
+}
+
 // mode 0: STFT (complex), 1: power spectrum, 2: fused Fbank (mel + dB, pre-top_db)
 SBK_API int sbk_spectrum(int mode, const float* wav, int Bo, int S, int C, int n_fft, int hop, int center,
                          int pad_mode, int T, const float* window, const float* twiddle_nc,
                          const float* twiddle_nfft, int onesided, float norm_scale, float power, float eps,
                          int log_mag, const long long* out_strides, const int* mel_start, const int* mel_len,
                          const int* mel_off, const float* mel_w, int n_melw, int M, int log_mel,
-                         float multiplier, float db_offset, float amin, float* out, int* maxkey, void* stream) {
+                         float multiplier, float db_offset, float amin, float* out, float* slot_max, void* stream) {
   if (Bo <= 0 || T <= 0 || S <= 0 || C <= 0) return SBK_ERR_ARG;
+  if (mode < MODE_STFT || mode > MODE_FBANK) return SBK_ERR_ARG;
   FftPlan plan;
   if ((n_fft & 1) || fill_plan(&plan, n_fft / 2)) return SBK_ERR_ARG;
   SpecArgs a;
@@ -584,67 +1018,49 @@ SBK_API int sbk_spectrum(int mode, const float* wav, int Bo, int S, int C, int n
   a.os_ri = out_strides ? out_strides[4] : 0;
   a.onesided = onesided; a.norm_scale = norm_scale;
   a.mel_start = mel_start; a.mel_len = mel_len; a.mel_off = mel_off; a.mel_w = mel_w;
-  a.M = M; a.log_mel = log_mel; a.multiplier = multiplier; a.db_offset = db_offset; a.amin = amin;
-  a.out = out; a.maxkey = maxkey;
-  const int nc = n_fft / 2;
+  a.M = mode == MODE_FBANK ? M : 0;
   a.n_melw = mode == MODE_FBANK ? n_melw : 0;
+  a.log_mel = log_mel; a.multiplier = multiplier; a.db_offset = db_offset; a.amin = amin;
   a.amin_db = multiplier * (float)log10((double)amin) - db_offset;
-  if (mode != MODE_FBANK) a.M = 0;
-  int fpb = 16;
-  auto lds_bytes = [&](int f) {
-    return (size_t)2 * f * nc * sizeof(float2) + (size_t)(2 * nc + 1) * sizeof(float2) +
-           (size_t)(3 * a.M + a.n_melw + n_fft) * 4 + (size_t)((f - 1) * hop + n_fft) * sizeof(float);
-  };
-  while (fpb > 1 && lds_bytes(fpb) > 72 * 1024) fpb >>= 1;
-  if (lds_bytes(fpb) > 160 * 1024) return SBK_ERR_ARG;
+  a.out = out; a.slot_max = slot_max;
+  if (mode == MODE_FBANK && log_mel && (C != 1 || !slot_max)) return SBK_ERR_ARG;
+  const int snc = static_nc(n_fft / 2, mode, onesided);
+  const int fpb = snc ? static_fpb(snc) : spec_fpb(n_fft, hop, a.M, a.n_melw);
+  if (!fpb) return SBK_ERR_ARG;
+  if (snc && static_lds_for(snc, mode, a.M, a.n_melw) > 64 * 1024) return SBK_ERR_ARG;
   a.fpb = fpb;
-  const int nblk = a.Bfold * ((T + fpb - 1) / fpb);
-  hipStream_t s = (hipStream_t)stream;
-  if (mode == MODE_FBANK && log_mel) {
-    if (C != 1) return SBK_ERR_ARG;
-    hipError_t e = hipMemsetD32Async((hipDeviceptr_t)maxkey, (int)0x80000000, a.Bfold, s);
-    if (e != hipSuccess) return (int)e;
-  }
-  switch (mode) {
-    case MODE_STFT: hipLaunchKernelGGL(spec_kernel<MODE_STFT>, dim3(nblk), dim3(256), lds_bytes(fpb), s, a, plan); break;
-    case MODE_POWER: hipLaunchKernelGGL(spec_kernel<MODE_POWER>, dim3(nblk), dim3(256), lds_bytes(fpb), s, a, plan); break;
-    case MODE_FBANK: hipLaunchKernelGGL(spec_kernel<MODE_FBANK>, dim3(nblk), dim3(256), lds_bytes(fpb), s, a, plan); break;
-    default: return SBK_ERR_ARG;
-  }
+  launch_spec(mode, n_fft / 2, a.Bfold, spec_lds(n_fft, a.M, a.n_melw, fpb), (hipStream_t)stream, a, plan);
   SBK_CHECK_LAUNCH();
   return 0;
 }
 
 SBK_API int sbk_filterbank(const float* spec, int N, int T, int F, const int* mel_start, const int* mel_len,
                            const int* mel_off, const float* mel_w, const float* dense, int M, int log_mel,
-                           float multiplier, float db_offset, float amin, float* out, int* maxkey, void* stream) {
+                           float multiplier, float db_offset, float amin, float* out, float* slot_max,
+                           void* stream) {
   if (N <= 0 || T <= 0 || F <= 0 || M <= 0) return SBK_ERR_ARG;
+  if ((size_t)F * 4 > 160 * 1024) return SBK_ERR_ARG;
+  if (log_mel && !slot_max) return SBK_ERR_ARG;
   FbArgs a;
   a.spec = spec; a.N = N; a.T = T; a.F = F;
   a.mel_start = mel_start; a.mel_len = mel_len; a.mel_off = mel_off; a.mel_w = mel_w; a.dense = dense;
   a.M = M; a.log_mel = log_mel; a.multiplier = multiplier; a.db_offset = db_offset; a.amin = amin;
   a.amin_db = multiplier * (float)log10((double)amin) - db_offset;
-  a.out = out; a.maxkey = maxkey;
-  int rpb = 8;
-  while (rpb > 1 && (size_t)rpb * F * 4 > 48 * 1024) rpb >>= 1;
-  if ((size_t)F * 4 > 160 * 1024) return SBK_ERR_ARG;
+  a.out = out; a.slot_max = slot_max;
+  const int rpb = fb_rows_per_block(F);
   a.rows_per_block = rpb;
-  const long long nrows = (long long)N * T;
-  hipStream_t s = (hipStream_t)stream;
-  if (log_mel) {
-    hipError_t e = hipMemsetD32Async((hipDeviceptr_t)maxkey, (int)0x80000000, N, s);
-    if (e != hipSuccess) return (int)e;
-  }
-  hipLaunchKernelGGL(filterbank_kernel, dim3((unsigned)((nrows + rpb - 1) / rpb)), dim3(256),
-                     (size_t)rpb * F * 4, s, a);
+  const long long nblk = (long long)N * ((T + rpb - 1) / rpb);
+  hipLaunchKernelGGL(filterbank_kernel, dim3((unsigned)nblk), dim3(256), (size_t)rpb * F * 4, (hipStream_t)stream, a);
   SBK_CHECK_LAUNCH();
   return 0;
 }
 
-SBK_API int sbk_topdb_clamp(float* x, const int* maxkey, long long per_seq, int nseq, float top_db, void* stream) {
-  if (per_seq <= 0 || nseq <= 0) return SBK_ERR_ARG;
-  hipLaunchKernelGGL(topdb_clamp_kernel, dim3(grid_for(per_seq * nseq / 4 + 1, 256)), dim3(256), 0,
-                     (hipStream_t)stream, x, maxkey, per_seq, nseq, top_db);
+SBK_API int sbk_topdb_clamp(float* x, const float* slot_max, int nslot, long long per_seq, int nseq, float top_db,
+                            void* stream) {
+  if (per_seq <= 0 || nseq <= 0 || nslot <= 0) return SBK_ERR_ARG;
+  const long long chunk = 256 * 16;
+  hipLaunchKernelGGL(topdb_clamp_kernel, dim3((unsigned)((per_seq + chunk - 1) / chunk), nseq), dim3(256), 0,
+                     (hipStream_t)stream, x, slot_max, nslot, per_seq, top_db);
   SBK_CHECK_LAUNCH();
   return 0;
 }

@@ -53,6 +53,18 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
 // Block-wide sum for blockDim.x a multiple of 64 (<= 1024). `red` >= 16 floats.
+// Block-wide max (all threads get the result); red: >= blockDim/64 floats.
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float m = red[0];
+  for (int i = 1; i < nw; ++i) m = fmaxf(m, red[i]);
+  return m;
+}
+
 __device__ __forceinline__ float block_sum(float v, float* red) {
   v = wave_sum(v);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;

@@ -107,16 +107,17 @@ def fbank(x: torch.Tensor, window: torch.Tensor, tw_nc: torch.Tensor, tw_nfft: t
     B, S = x.shape
     T = n_frames(S, n_fft, hop, center)
     out = torch.empty(B, T, n_mels, device=x.device, dtype=_f32)
-    maxkey = torch.empty(B, device=x.device, dtype=torch.int32)
     L = _lib.lib()
+    nslot = L.sbk_spectrum_slots(n_fft, hop, T, n_mels, mel_w.numel())
+    slot_max = torch.empty(B, max(nslot, 1), device=x.device, dtype=_f32)
     s = stream_of(x)
     rc = L.sbk_spectrum(2, ptr(x), B, S, 1, n_fft, hop, int(center), pad_mode, T, ptr(window), ptr(tw_nc),
                         ptr(tw_nfft), 1, 1.0, 1.0, 0.0, 0, None, ptr(mel_start), ptr(mel_len), ptr(mel_off),
                         ptr(mel_w), mel_w.numel(), n_mels, int(log_mel), multiplier, db_offset, amin, ptr(out),
-                        ptr(maxkey), s)
+                        ptr(slot_max), s)
     check(rc, "sbk_spectrum(fbank)")
     if log_mel:
-        check(L.sbk_topdb_clamp(ptr(out), ptr(maxkey), T * n_mels, B, top_db, s), "sbk_topdb_clamp")
+        check(L.sbk_topdb_clamp(ptr(out), ptr(slot_max), nslot, T * n_mels, B, top_db, s), "sbk_topdb_clamp")
     return out
 
 
@@ -135,14 +136,15 @@ def filterbank(spec: torch.Tensor, mel_start: torch.Tensor, mel_len: torch.Tenso
     spec = _c(spec.to(_f32))
     N, T, Fd = spec.shape
     out = torch.empty(N, T, n_mels, device=spec.device, dtype=_f32)
-    maxkey = torch.empty(N, device=spec.device, dtype=torch.int32)
     L = _lib.lib()
+    nslot = L.sbk_filterbank_slots(T, Fd)
+    slot_max = torch.empty(N, max(nslot, 1), device=spec.device, dtype=_f32)
     s = stream_of(spec)
     rc = L.sbk_filterbank(ptr(spec), N, T, Fd, ptr(mel_start), ptr(mel_len), ptr(mel_off), ptr(mel_w), None,
-                          n_mels, int(log_mel), multiplier, db_offset, amin, ptr(out), ptr(maxkey), s)
+                          n_mels, int(log_mel), multiplier, db_offset, amin, ptr(out), ptr(slot_max), s)
     check(rc, "sbk_filterbank")
     if log_mel:
-        check(L.sbk_topdb_clamp(ptr(out), ptr(maxkey), T * n_mels, N, top_db, s), "sbk_topdb_clamp")
+        check(L.sbk_topdb_clamp(ptr(out), ptr(slot_max), nslot, T * n_mels, N, top_db, s), "sbk_topdb_clamp")
     return out
 
 
@@ -161,14 +163,15 @@ def filterbank_dense(spec: torch.Tensor, mat: torch.Tensor, log_mel: bool, multi
     N, T, Fd = spec.shape
     M = mat.shape[1]
     out = torch.empty(N, T, M, device=spec.device, dtype=_f32)
-    maxkey = torch.empty(N, device=spec.device, dtype=torch.int32)
     L = _lib.lib()
+    nslot = L.sbk_filterbank_slots(T, Fd)
+    slot_max = torch.empty(N, max(nslot, 1), device=spec.device, dtype=_f32)
     s = stream_of(spec)
     rc = L.sbk_filterbank(ptr(spec), N, T, Fd, None, None, None, None, ptr(mat), M, int(log_mel), multiplier,
-                          db_offset, amin, ptr(out), ptr(maxkey), s)
+                          db_offset, amin, ptr(out), ptr(slot_max), s)
     check(rc, "sbk_filterbank(dense)")
     if log_mel:
-        check(L.sbk_topdb_clamp(ptr(out), ptr(maxkey), T * M, N, top_db, s), "sbk_topdb_clamp")
+        check(L.sbk_topdb_clamp(ptr(out), ptr(slot_max), nslot, T * M, N, top_db, s), "sbk_topdb_clamp")
     return out
 
 
