@@ -125,6 +125,20 @@ int sbk_gemm(int dtype_bf16, const void* A, int lda, const void* W, int ldw, int
              const float* bias, int act, float slope, const float* res, int ldr, float alpha,
              const uint8_t* rowmask, void* out, int ldc, int out_bf16, int tile, void* stream);
 
+/* 1 if the fused FFN kernel supports d_model D and d_ffn H (D in {256, 512}, H % 256 == 0). */
+int sbk_ffn_supported(int D, int H);
+
+/* Fused macaron feed-forward block, bf16 MFMA (Conformer.py:239-260 with
+ * attention.py:823-839):
+ *   z = x + alpha * (act(LN0(x) W1^T + b1) W2^T + b2);  out = LNp(z) if gp;
+ *   u = LNn(out) if gn (bf16 when u_bf16, else fp32).
+ * x, out (M, D) fp32 (out may alias x); w1 (H, D), w2 (D, H) bf16; b1, b2 required (zeros when the
+ * Linear has no bias); act as sbk_gemm (not GLU). */
+int sbk_ffn(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0, const void* w1,
+            const float* b1, int act, float slope, const void* w2, const float* b2, float alpha, const float* gp,
+            const float* bp, float epsp, float* out, const float* gn, const float* bn, float epsn, void* u,
+            int u_bf16, void* stream);
+
 /* LayerNorm (normalization.py:172-223; Conformer.py:178,194,340): one or two
  * chained LayerNorms over rows of x (M, D) fp32, D <= 1024. */
 int sbk_layernorm(const float* x, int M, int D, const float* g1, const float* b1, float eps1, void* out1,

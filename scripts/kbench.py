@@ -76,6 +76,23 @@ def misc_bench():
     print(f"fbank 32x15s: {us:.1f}us {(32 * 240000 * 4 + 32 * 1501 * 80 * 4) / us / 1e3:.0f} GB/s", flush=True)
 
 
+def ffn_bench():
+    from speechbrain_amd.nnet.attention import PositionalwiseFeedForward
+    from speechbrain_amd.nnet.activations import Swish
+    dev = torch.device("cuda")
+    for D, H in ((256, 1024), (256, 2048)):
+        M = 12032
+        ffn = PositionalwiseFeedForward(H, input_size=D, activation=Swish).to(dev).eval()
+        x = torch.randn(M, D, device=dev)
+        ln = (torch.ones(D, device=dev), torch.zeros(D, device=dev), 1e-5)
+        with torch.no_grad():
+            us = timeit(lambda: ffn.run_fused(x, ln, 0.5, next_ln=ln))
+            u = _enc.layernorm(x, *ln, out1_dtype=torch.bfloat16)[0]
+            us2 = timeit(lambda: ffn.run(u, torch.bfloat16, residual=x, alpha=0.5))
+        fl = 4.0 * M * D * H
+        print(f"ffn D={D} H={H} M={M}: fused {us:.1f}us {fl / us / 1e6:.0f} TF/s | 2 gemms {us2:.1f}us", flush=True)
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("gemm", "all"):
@@ -84,3 +101,5 @@ if __name__ == "__main__":
         attn_bench()
     if what in ("misc", "all"):
         misc_bench()
+    if what in ("ffn", "all"):
+        ffn_bench()

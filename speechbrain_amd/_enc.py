@@ -54,6 +54,30 @@ def layernorm(x, w1, b1, eps1, out1_dtype=_f32, w2=None, b2=None, eps2=1e-5, out
     return out1, out2
 
 
+def ffn_supported(D, H):
+    return bool(lib().sbk_ffn_supported(int(D), int(H)))
+
+
+def ffn(x, ln0, w1, b1, act, slope, w2, b2, alpha, post_ln=None, next_ln=None, next_dtype=_bf16, out=None):
+    """Fused macaron FFN block (bf16 MFMA): z = x + alpha * FFN(LN0(x));
+    out = post_ln(z) if given; u = next_ln(out) (returned) if given.
+    x: (M, D) fp32; ln*: (weight, bias, eps); w1 (H, D), w2 (D, H) bf16.
+    `out` may alias x."""
+    require_device(x, w1, w2)
+    M, D = x.shape
+    H = w1.shape[0]
+    if out is None:
+        out = torch.empty_like(x)
+    u = torch.empty(M, D, device=x.device, dtype=next_dtype) if next_ln is not None else None
+    gp, bp, ep = post_ln if post_ln is not None else (None, None, 0.0)
+    gn, bn, en = next_ln if next_ln is not None else (None, None, 0.0)
+    rc = lib().sbk_ffn(ptr(x), M, D, H, ptr(ln0[0]), ptr(ln0[1]), float(ln0[2]), ptr(w1), ptr(b1), ACT[act],
+                       float(slope), ptr(w2), ptr(b2), float(alpha), ptr(gp), ptr(bp), float(ep), ptr(out),
+                       ptr(gn), ptr(bn), float(en), ptr(u), int(next_dtype == _bf16), stream_of(x))
+    check(rc, "sbk_ffn")
+    return out, u
+
+
 def dwconv_ln_swish(x, B, T, w, bias, causal, ln_w, ln_b, eps, out_dtype):
     """Depthwise Conv1d over time + LayerNorm(C) + Swish.  x: (B*T, C)."""
     C = x.shape[-1]

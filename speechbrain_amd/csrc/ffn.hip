@@ -1,0 +1,414 @@
+// Fused Conformer feed-forward block (bf16 MFMA):
+//
+//   z   = x + alpha * ( act( LN0(x) · W1^T + b1 ) · W2^T + b2 )
+//   out = LNp(z)            (optional post-LayerNorm, e.g. norm2)
+//   u   = LNn(out)          (optional, bf16/fp32 input of the next consumer)
+//
+// Reference: speechbrain/lobes/models/transformer/Conformer.py:239-260
+// (macaron FFNs: ffn_module = Sequential(LayerNorm, PositionalwiseFeedForward,
+// Dropout), 0.5-scaled residuals, norm2 after the second FFN) and
+// speechbrain/nnet/attention.py:823-839 (PositionalwiseFeedForward).
+//
+// Design (MI355X): one workgroup (16 waves) owns BM = 48 rows for
+// the whole block, so neither LN0(x) nor the (BM x H) hidden activation ever
+// leaves the CU:
+//   prologue : x rows (fp32) -> LayerNorm -> bf16 Xn, resident in LDS; b1 -> LDS;
+//   per chunk of HC = 256 hidden units (8 K-steps of 64):
+//     phase 1: Hc^T = W1[c]·Xn^T  -> +b1, act -> bf16 Hs (LDS);
+//     phase 2: acc2^T += W2[:, c]·Hs^T  (accumulators stay in VGPRs);
+//   epilogue : +b2, alpha, residual, optional post-LN and next-LN over the
+//              full rows (cross-wave reduction through LDS), float4 stores.
+// Weight tiles (256 rows x 64 k = 32 KB) stream L2 -> LDS by LDS-DMA
+// (global_load_lds_dwordx4: full 128-B lines, no VGPRs) into a 3-slot ring,
+// two tiles in flight across one raw barrier per K-step (counted vmcnt).
+// The ring image is lane-linear; bank conflicts are removed by XOR-swizzling
+// the 16-B chunk index with (row >> 1) & 7 on the global source address and
+// on the fragment reads.  Per workgroup the 2·D·H weight bytes cross L2 once;
+// HBM traffic per row: D fp32 in + D fp32 out (+ D u out).
+// Bound: every workgroup streams all 2·D·H weight bytes (1 MB at D=256,
+// H=1024) through its CU; at ~25-30 GB/s per CU of L2->LDS-DMA this per-CU
+// stream, not MFMA (~12 % busy) or HBM, sets the time.
+// Tried and slower: 8-wave register-staged ring (48 us), 4 waves (69 us),
+// fragment-shaped loads straight to VGPRs (64 us), row-owner waves with the
+// hidden chunk in registers (78 us); 16 waves here: 42 us (M = 12032).
+#include "mfma.h"
+
+using namespace sbk;
+
+namespace {
+
+enum Act { ACT_NONE = 0, ACT_SWISH = 1, ACT_GLU = 2, ACT_LRELU = 3, ACT_GELU = 4 };
+
+struct FfnArgs {
+  const float* x;  // (M, D) fp32
+  int M, H;
+  const float *g0, *b0;
+  float eps0;
+  const bf16_t* w1;  // (H, D)
+  const float* b1;
+  int act;
+  float slope;
+  const bf16_t* w2;  // (D, H)
+  const float* b2;
+  float alpha;
+  const float *gp, *bp;  // post-LN (or null)
+  float epsp;
+  float* out;  // (M, D) fp32, may alias x
+  const float *gn, *bn;  // next-LN (or null)
+  float epsn;
+  void* u;
+  int u_bf16;
+};
+
+__device__ __forceinline__ bf16x8 ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+constexpr int FFN_BM = 48, FFN_NW = 16, FFN_NT = FFN_NW * 64;
+
+__device__ __forceinline__ float act_fn(float v, int act, float slope) {
+  if (act == ACT_SWISH) return v * (1.0f / (1.0f + __expf(-v)));
+  if (act == ACT_LRELU) return v >= 0.f ? v : v * slope;
+  if (act == ACT_GELU) return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+  return v;
+}
+
+// Full-row LayerNorm of the epilogue values z (in place).  Lane (w, g, fr)
+// holds rows mt*16 + fr, units (w*T2 + j)*16 + 4g + e; row statistics are
+// reduced over g by shuffles and over the NW waves through red[NW][BM].
+template <int D, int T2, int MT, int NW>
+__device__ __forceinline__ void row_ln(float (&z)[T2][MT][4], float (*red)[FFN_BM], const float* gam,
+                                       const float* bet, float eps, int w, int g, int fr) {
+  float mean[MT], rstd[MT];
+  // pass 1: mean
+  {
+    float part[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < T2; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s += z[j][mt][e];
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      part[mt] = s;
+    }
+    __syncthreads();
+    if (g == 0) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) red[w][mt * 16 + fr] = part[mt];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < NW; ++k) t += red[k][mt * 16 + fr];
+      mean[mt] = t / D;
+    }
+  }
+  // pass 2: variance about the mean
+  {
+    float part[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < T2; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float dv = z[j][mt][e] - mean[mt];
+          s += dv * dv;
+        }
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      part[mt] = s;
+    }
+    __syncthreads();
+    if (g == 0) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) red[w][mt * 16 + fr] = part[mt];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < NW; ++k) t += red[k][mt * 16 + fr];
+      rstd[mt] = 1.0f / sqrtf(t / D + eps);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < T2; ++j) {
+    const int d = (w * T2 + j) * 16 + 4 * g;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float gm = gam[d + e], bt = bet[d + e];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) z[j][mt][e] = (z[j][mt][e] - mean[mt]) * rstd[mt] * gm + bt;
+    }
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
+  constexpr int BM = FFN_BM, HC = 256, NW = FFN_NW, NT = FFN_NT;
+  constexpr int XS = D + 16, HS = HC + 16;   // LDS row strides (elements), +32 B pad: conflict-free b128 reads
+  constexpr int MT = BM / 16;                // m-tiles (3)
+  constexpr int T = 256 / 16 / FFN_NW;       // 16-row weight tiles per wave (HC/16/NW = D/16/NW)
+  constexpr int BK = 64;                     // K per step: one 128-B line per weight row
+  constexpr int K1 = D / BK, K2 = HC / BK, SPC = K1 + K2;
+  constexpr int NB = 3;                      // ring slots (2 tiles in flight + 1 being read)
+  constexpr int TROWS = 256;                 // rows per weight tile (HC for W1, D for W2)
+  constexpr int GL = TROWS * BK * 2 / 16 / NT;  // LDS-DMA instructions per thread per tile (8)
+  constexpr int PER = D / 64;                // LN: floats per lane
+  static_assert(D == 256 && HC / 16 / NW == T && D / 16 / NW == T, "shape");
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* ring = reinterpret_cast<bf16_t*>(smem);          // NB x TROWS x BK (linear 128-B rows)
+  bf16_t* Xn = ring + NB * TROWS * BK;                      // BM x XS
+  bf16_t* Hs = Xn + BM * XS;                                // BM x HS
+  float* b1s = reinterpret_cast<float*>(Hs + BM * HS);      // H
+  float (*red)[BM] = reinterpret_cast<float (*)[BM]>(b1s + a.H);  // NW x BM
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int fr = lane & 15, g = lane >> 4, fk = 8 * g;
+  const int m0 = blockIdx.x * BM;
+  const int S = (a.H / HC) * SPC;
+
+  // ---- prologue: LayerNorm of the workgroup's rows -> Xn (bf16); b1 -> LDS
+  for (int rr = w; rr < BM; rr += NW) {
+    const int row = m0 + rr;
+    float v[PER];
+    if (row < a.M) {
+      const float* xr = a.x + (long long)row * D + lane * PER;
+#pragma unroll
+      for (int i = 0; i < PER; i += 4) {
+        const float4 t4 = *reinterpret_cast<const float4*>(xr + i);
+        v[i] = t4.x; v[i + 1] = t4.y; v[i + 2] = t4.z; v[i + 3] = t4.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < PER; ++i) v[i] = 0.f;
+    }
+    float sm = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) sm += v[i];
+    const float mean = wave_sum(sm) / D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) q += (v[i] - mean) * (v[i] - mean);
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / D + a.eps0);
+    bf16_t* xo = Xn + rr * XS + lane * PER;
+#pragma unroll
+    for (int i = 0; i < PER; i += 4) {
+      const int c = lane * PER + i;
+      uint2 pk;
+      pk.x = (uint32_t)f32_to_bf16((v[i] - mean) * rstd * a.g0[c] + a.b0[c]) |
+             ((uint32_t)f32_to_bf16((v[i + 1] - mean) * rstd * a.g0[c + 1] + a.b0[c + 1]) << 16);
+      pk.y = (uint32_t)f32_to_bf16((v[i + 2] - mean) * rstd * a.g0[c + 2] + a.b0[c + 2]) |
+             ((uint32_t)f32_to_bf16((v[i + 3] - mean) * rstd * a.g0[c + 3] + a.b0[c + 3]) << 16);
+      *reinterpret_cast<uint2*>(xo + i) = pk;
+    }
+  }
+  for (int i = tid; i < a.H; i += NT) b1s[i] = a.b1[i];
+
+  // ---- weight tile s -> ring slot (LDS-DMA, 1 KB = 8 rows per wave-instruction)
+  // lane L of instruction i writes row R0 + L/8, 16-B chunk L%8 (linear image)
+  // and fetches source chunk (L%8) ^ ((row >> 1) & 7): the read side applies
+  // the same involution.
+  const int lrow = lane >> 3, lchk = lane & 7;
+  auto issue = [&](int s, int slot) __attribute__((always_inline)) {
+    const int c = s / SPC, r = s - c * SPC;
+    const bool p1 = r < K1;
+    const bf16_t* base = p1 ? a.w1 + (long long)c * HC * D + r * BK : a.w2 + c * HC + (r - K1) * BK;
+    const int ld = p1 ? D : a.H;
+    bf16_t* dst = ring + slot * TROWS * BK;
+#pragma unroll
+    for (int i = 0; i < GL; ++i) {
+      const int r0 = (i * NW + w) * 8;
+      const int row = r0 + lrow;
+      const bf16_t* src = base + (long long)row * ld + ((lchk ^ ((row >> 1) & 7)) << 3);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(dst + r0 * BK), 16, 0, 0);
+    }
+  };
+  issue(0, 0);
+  issue(1, 1);
+
+  f32x4 acc1[T][MT], acc2[T][MT];
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      acc1[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc2[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+
+  for (int s = 0; s < S; ++s) {
+    const int c = s / SPC, r = s - c * SPC;
+    // tile s landed (tile s+1 stays in flight), LDS writes of step s-1 done
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // slot (s+2)%NB was last read in step s-1: refill (tail: a harmless reload of the last tile)
+    issue(min(s + 2, S - 1), (s + 2) % NB);
+    const bf16_t* tile = ring + (s % NB) * TROWS * BK;
+    if (r < K1) {
+#pragma unroll
+      for (int ks = 0; ks < BK / 32; ++ks) {
+        bf16x8 fw[T], fx[MT];
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          const int row = w * (T * 16) + t * 16 + fr;
+          fw[t] = ld8(tile + row * BK + (((ks * 4 + g) ^ ((row >> 1) & 7)) << 3));
+        }
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) fx[mt] = ld8(Xn + (mt * 16 + fr) * XS + r * BK + ks * 32 + fk);
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+            acc1[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[t], fx[mt], acc1[t][mt], 0, 0, 0);
+      }
+      if (r == K1 - 1) {
+        // hidden chunk -> +b1, act -> Hs (4 consecutive units per lane, one 8-B store);
+        // phase 2 reads it after the next step's barrier
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          const int n = w * (T * 16) + t * 16 + 4 * g;
+          const float4 bb = *reinterpret_cast<const float4*>(b1s + c * HC + n);
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const f32x4 v = acc1[t][mt];
+            uint2 pk;
+            pk.x = (uint32_t)f32_to_bf16(act_fn(v[0] + bb.x, a.act, a.slope)) |
+                   ((uint32_t)f32_to_bf16(act_fn(v[1] + bb.y, a.act, a.slope)) << 16);
+            pk.y = (uint32_t)f32_to_bf16(act_fn(v[2] + bb.z, a.act, a.slope)) |
+                   ((uint32_t)f32_to_bf16(act_fn(v[3] + bb.w, a.act, a.slope)) << 16);
+            *reinterpret_cast<uint2*>(Hs + (mt * 16 + fr) * HS + n) = pk;
+            acc1[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+        }
+      }
+    } else {
+      const int kk = (r - K1) * BK;
+#pragma unroll
+      for (int ks = 0; ks < BK / 32; ++ks) {
+        bf16x8 fw[T], fh[MT];
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          const int row = w * (T * 16) + t * 16 + fr;
+          fw[t] = ld8(tile + row * BK + (((ks * 4 + g) ^ ((row >> 1) & 7)) << 3));
+        }
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) fh[mt] = ld8(Hs + (mt * 16 + fr) * HS + kk + ks * 32 + fk);
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+            acc2[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[t], fh[mt], acc2[t][mt], 0, 0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the tail reloads
+
+  // ---- epilogue: lane holds rows m = mt*16 + fr, units d = (w*T + j)*16 + 4g .. +3
+  constexpr int T2 = T;
+  float z[T2][MT][4];
+#pragma unroll
+  for (int j = 0; j < T2; ++j) {
+    const int d = (w * T2 + j) * 16 + 4 * g;
+    const float4 bb = *reinterpret_cast<const float4*>(a.b2 + d);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int row = m0 + mt * 16 + fr;
+      float4 xr = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (row < a.M) xr = *reinterpret_cast<const float4*>(a.x + (long long)row * D + d);
+      z[j][mt][0] = xr.x + a.alpha * (acc2[j][mt][0] + bb.x);
+      z[j][mt][1] = xr.y + a.alpha * (acc2[j][mt][1] + bb.y);
+      z[j][mt][2] = xr.z + a.alpha * (acc2[j][mt][2] + bb.z);
+      z[j][mt][3] = xr.w + a.alpha * (acc2[j][mt][3] + bb.w);
+    }
+  }
+  if (a.gp) row_ln<D, T2, MT, NW>(z, red, a.gp, a.bp, a.epsp, w, g, fr);
+  // all residual reads of x are done before out (which may alias x) is written
+#pragma unroll
+  for (int j = 0; j < T2; ++j) {
+    const int d = (w * T2 + j) * 16 + 4 * g;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int row = m0 + mt * 16 + fr;
+      if (row < a.M)
+        *reinterpret_cast<float4*>(a.out + (long long)row * D + d) =
+            make_float4(z[j][mt][0], z[j][mt][1], z[j][mt][2], z[j][mt][3]);
+    }
+  }
+  if (a.gn) {
+    row_ln<D, T2, MT, NW>(z, red, a.gn, a.bn, a.epsn, w, g, fr);
+#pragma unroll
+    for (int j = 0; j < T2; ++j) {
+      const int d = (w * T2 + j) * 16 + 4 * g;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int row = m0 + mt * 16 + fr;
+        if (row >= a.M) continue;
+        if (a.u_bf16) {
+          uint2 pk;
+          pk.x = (uint32_t)f32_to_bf16(z[j][mt][0]) | ((uint32_t)f32_to_bf16(z[j][mt][1]) << 16);
+          pk.y = (uint32_t)f32_to_bf16(z[j][mt][2]) | ((uint32_t)f32_to_bf16(z[j][mt][3]) << 16);
+          *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(a.u) + (long long)row * D + d) = pk;
+        } else {
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.u) + (long long)row * D + d) =
+              make_float4(z[j][mt][0], z[j][mt][1], z[j][mt][2], z[j][mt][3]);
+        }
+      }
+    }
+  }
+}
+
+template <int D>
+size_t ffn_lds(int H) {
+  return ((size_t)3 * 256 * 64 + (size_t)FFN_BM * (D + 16) + (size_t)FFN_BM * (256 + 16)) * sizeof(bf16_t) +
+         (size_t)H * 4 + (size_t)FFN_NW * FFN_BM * 4;
+}
+
+template <int D>
+int launch_ffn(const FfnArgs& a, hipStream_t s) {
+  const size_t lds = ffn_lds<D>(a.H);
+  if (lds > 160 * 1024) return SBK_ERR_ARG;
+  static bool attr = false;  // > 64 KB dynamic LDS: opt in once per kernel
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ffn_kernel<D>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((ffn_kernel<D>), dim3((a.M + FFN_BM - 1) / FFN_BM), dim3(FFN_NT), lds, s, a);
+  return 0;
+}
+
+
+}  // namespace
+
+SBK_API int sbk_ffn_supported(int D, int H) { return D == 256 && H > 0 && H % 256 == 0 && H <= 2048; }
+
+SBK_API int sbk_ffn(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0,
+                    const void* w1, const float* b1, int act, float slope, const void* w2, const float* b2,
+                    float alpha, const float* gp, const float* bp, float epsp, float* out, const float* gn,
+                    const float* bn, float epsn, void* u, int u_bf16, void* stream) {
+  if (M <= 0 || !sbk_ffn_supported(D, H) || !g0 || !b0 || !w1 || !b1 || !w2 || !b2 || !out) return SBK_ERR_ARG;
+  if (act == ACT_GLU || (gn && !u)) return SBK_ERR_ARG;
+  FfnArgs a;
+  a.x = x; a.M = M; a.H = H;
+  a.g0 = g0; a.b0 = b0; a.eps0 = eps0;
+  a.w1 = reinterpret_cast<const bf16_t*>(w1); a.b1 = b1; a.act = act; a.slope = slope;
+  a.w2 = reinterpret_cast<const bf16_t*>(w2); a.b2 = b2; a.alpha = alpha;
+  a.gp = gp; a.bp = bp; a.epsp = epsp;
+  a.out = out;
+  a.gn = gn; a.bn = bn; a.epsn = epsn; a.u = u; a.u_bf16 = u_bf16;
+  hipStream_t s = (hipStream_t)stream;
+  int rc = launch_ffn<256>(a, s);
+  if (rc) return rc;
+  SBK_CHECK_LAUNCH();
+  return 0;
+}

@@ -141,14 +141,25 @@ class ConformerEncoderLayer(nn.Module):
     def _ln(self, mod):
         return mod.weight.detach(), mod.bias.detach(), mod.eps
 
-    def fused(self, x, B, T, pos, kpm_u8, dtype, need_attn, u_in=None, next_ln=None):
+    def fused(self, x, B, T, pos, kpm_u8, dtype, need_attn, u_in=None, next_ln=None, final_ln=None):
         """One layer.  x: (B*T, d) fp32 residual stream; pos: (2T-1, d) in
         dtype; u_in: LN_ffn1(x) if a previous kernel already produced it;
         next_ln: (w, b, eps) of the NEXT consumer's LayerNorm to chain after
-        norm2.  Returns (x_out fp32, u_next or None, attn or None)."""
+        norm2; final_ln: the encoder's closing LayerNorm, applied on chip by
+        the fused-FFN path.  Returns (x_out fp32, u_next or None, attn or
+        None, final_ln_applied)."""
         if self.training and self.drop.p > 0:
             raise NotImplementedError("dropout in training mode is not implemented in HIP yet")
         f1, f2 = self.ffn_module1, self.ffn_module2
+        if f1[1].fusable(dtype) and f2[1].fusable(dtype):
+            # FFN1 + norm1 in one kernel, FFN2 + norm2 in one kernel (LayerNorms
+            # computed on chip; the next layer's FFN1 normalises its own input)
+            x, u = f1[1].run_fused(x, self._ln(f1[0]), 0.5, next_ln=self._ln(self.norm1.norm), next_dtype=dtype)
+            x, attn = self.mha_layer.attend(u, B, T, pos, kpm_u8, dtype, need_attn, residual=x)
+            x = self.convolution_module.run(x, B, T, dtype, kpm_u8, residual=x)
+            x, y = f2[1].run_fused(x, self._ln(f2[0]), 0.5, post_ln=self._ln(self.norm2.norm), out=x,
+                                   next_ln=final_ln, next_dtype=_f32)
+            return (y, None, attn, True) if final_ln is not None else (x, None, attn, False)
         if u_in is None:
             u_in, _ = _enc.layernorm(x, *self._ln(f1[0]), out1_dtype=dtype)
         x = f1[1].run(u_in, dtype, residual=x, alpha=0.5)
@@ -161,9 +172,9 @@ class ConformerEncoderLayer(nn.Module):
         if next_ln is not None:
             x, u_next = _enc.layernorm(z, w2, b2, e2, out1_dtype=_f32, w2=next_ln[0], b2=next_ln[1],
                                        eps2=next_ln[2], out2_dtype=dtype)
-            return x, u_next, attn
+            return x, u_next, attn, False
         x, _ = _enc.layernorm(z, w2, b2, e2, out1_dtype=_f32)
-        return x, None, attn
+        return x, None, attn, False
 
     def forward(self, x, src_mask: Optional[torch.Tensor] = None,
                 src_key_padding_mask: Optional[torch.Tensor] = None, pos_embs: Optional[torch.Tensor] = None):
@@ -173,7 +184,7 @@ class ConformerEncoderLayer(nn.Module):
         dtype = _enc.compute_dtype()
         kpm = src_key_padding_mask.to(torch.uint8).contiguous() if src_key_padding_mask is not None else None
         pos = _enc.to_compute(pos_embs.reshape(-1, d), dtype)
-        y, _, attn = self.fused(x.float().reshape(B * T, d).contiguous(), B, T, pos, kpm, dtype, True)
+        y, _, attn, _ = self.fused(x.float().reshape(B * T, d).contiguous(), B, T, pos, kpm, dtype, True)
         return y.view(B, T, d), attn
 
 
@@ -201,8 +212,13 @@ class ConformerEncoder(nn.Module):
         for i, layer in enumerate(self.layers):
             nxt = self.layers[i + 1].ffn_module1[0] if i + 1 < n else None
             next_ln = (nxt.weight.detach(), nxt.bias.detach(), nxt.eps) if nxt is not None else None
-            x, u, a = layer.fused(x, B, T, pos, kpm_u8, dtype, need_attn, u_in=u, next_ln=next_ln)
+            fn = self.norm.norm
+            final_ln = (fn.weight.detach(), fn.bias.detach(), fn.eps) if nxt is None else None
+            x, u, a, done = layer.fused(x, B, T, pos, kpm_u8, dtype, need_attn, u_in=u, next_ln=next_ln,
+                                        final_ln=final_ln)
             attns.append(a)
+            if done:
+                return x, attns
         fn = self.norm.norm
         y, _ = _enc.layernorm(x, fn.weight.detach(), fn.bias.detach(), fn.eps, out1_dtype=_f32)
         return y, attns

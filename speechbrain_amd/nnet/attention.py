@@ -185,6 +185,21 @@ class PositionalwiseFeedForward(nn.Module):
         h = _enc.gemm(u2d, w1, bias=self.ffn[0].bias.detach(), act=act, slope=slope, out_dtype=dtype)
         return _enc.gemm(h, w2, bias=self.ffn[3].bias.detach(), res=residual, alpha=alpha, out_dtype=torch.float32)
 
+    def fusable(self, dtype):
+        """True when the whole LN→FFN→residual block can run as one kernel."""
+        return (dtype == torch.bfloat16 and self.act_name()[0] != "glu"
+                and _enc.ffn_supported(self.ffn[0].in_features, self.ffn[0].out_features))
+
+    def run_fused(self, x, ln0, alpha, post_ln=None, next_ln=None, next_dtype=torch.bfloat16, out=None):
+        """x (M, d) fp32 → (post_ln(x + alpha * FFN(LN0(x))), next_ln(...) or None),
+        one kernel (bf16 MFMA, hidden activation kept on chip)."""
+        w1, w2 = self.kernel_weights(torch.bfloat16)
+        act, slope = self.act_name()
+        b1, b2 = (lin.bias.detach() if lin.bias is not None else torch.zeros(lin.out_features, device=x.device)
+                  for lin in (self.ffn[0], self.ffn[3]))
+        return _enc.ffn(x, ln0, w1, b1, act, slope, w2, b2, alpha,
+                        post_ln=post_ln, next_ln=next_ln, next_dtype=next_dtype, out=out)
+
     def forward(self, x):
         if self.training and self.ffn[2].p > 0:
             raise NotImplementedError("FFN dropout in training mode is not implemented in HIP yet")

@@ -73,6 +73,37 @@ def test_layernorm_chain(dev):
     assert_close(y2, F.layer_norm(r1, (256,), w2, b2, 1e-6), rtol=1e-5)
 
 
+@pytest.mark.parametrize("D,H,M", [(256, 1024, 1000), (256, 2048, 333), (256, 512, 48), (256, 1024, 12032)])
+def test_fused_ffn_vs_unfused(dev, D, H, M):
+    """sbk_ffn (LN → Linear → Swish → Linear → 0.5·residual → norm2 → next LN,
+    one kernel) vs the same chain through the separate HIP kernels, both bf16
+    operands / fp32 accumulation.  Rounding points are identical; only the
+    fp32 summation order of the LayerNorm statistics and MFMA K-chunks differ,
+    which can flip single bf16 roundings: tolerance 2e-2 of LayerNorm-scale
+    values (|a-b| <= 2e-2 * max(1, |b|))."""
+    from speechbrain_amd import _enc
+    from speechbrain_amd.nnet.attention import PositionalwiseFeedForward
+    from speechbrain_amd.nnet.activations import Swish
+    torch.manual_seed(0)
+    ffn = PositionalwiseFeedForward(H, input_size=D, activation=Swish).to(dev).eval()
+    x = (torch.randn(M, D) * 2 + 0.5).to(dev)
+    lns = [(torch.randn(D, device=dev) * 0.5 + 1, torch.randn(D, device=dev) * 0.1, 1e-5) for _ in range(3)]
+    bf = torch.bfloat16
+    with torch.no_grad():
+        out, u = ffn.run_fused(x, lns[0], 0.5, post_ln=lns[1], next_ln=lns[2])
+        u0, _ = _enc.layernorm(x, *lns[0], out1_dtype=bf)
+        z = ffn.run(u0, bf, residual=x, alpha=0.5)
+        ref, uref = _enc.layernorm(z, *lns[1], out1_dtype=torch.float32, w2=lns[2][0], b2=lns[2][1],
+                                   eps2=lns[2][2], out2_dtype=bf)
+        # in-place variant (out aliases x) and no post/next LN
+        x2 = x.clone()
+        out2, none = ffn.run_fused(x2, lns[0], 0.5, out=x2)
+    assert none is None and out2.data_ptr() == x2.data_ptr()
+    assert_close(out, ref, rtol=2e-2, name="ffn out")
+    assert_close(u.float(), uref.float(), rtol=2e-2, name="ffn next-LN")
+    assert_close(out2, z, rtol=2e-2, name="ffn in-place")
+
+
 # ----------------------------------------------------------------------------- modules vs golden
 def test_conv_frontend_vs_golden(golden, dev):
     from speechbrain_amd.lobes.models.convolution import ConvolutionFrontEnd
@@ -183,3 +214,19 @@ def test_full_size_encoder_vs_oracle(dev, d_model):
     ref = OC.fbank_to_encoder(wav, sd_cnn, sd_tr, 12, 4, wav_len=torch.ones(2))
     assert y.shape == (2, 376, d_model)
     assert_close(y, ref, rtol=1e-4, name="full")
+
+
+def test_full_size_encoder_bf16_vs_fp32(dev):
+    """d=256 encoder at 15 s under bf16 autocast (fused FFN kernels, bf16
+    GEMM/attention) vs the fp32 path: LayerNorm-scale outputs within 0.1."""
+    cnn, tr = _c3_modules(256, dev)
+    g = torch.Generator().manual_seed(1)
+    feats = torch.randn(4, 1501, 80, generator=g).to(dev)
+    with torch.no_grad():
+        src = cnn(feats)
+        y32 = tr.encode(src, torch.ones(4, device=dev))
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y16 = tr.encode(src, torch.ones(4, device=dev))
+    err = (y16.float() - y32).abs()
+    assert y16.dtype == torch.float32 and torch.isfinite(y16).all()
+    assert err.max().item() < 0.1 and err.mean().item() < 0.01, (err.max().item(), err.mean().item())
