@@ -12,9 +12,11 @@ fused Fbank kernel (+top_db clamp) → 2 fused ConvBlocks → src Linear →
 captured once into a HIP graph and replayed.  Rank 0 prints ONE JSON line.
 
 Also reported (rank 0, N=1 path of the contract):
-  roofline      the dominant kernel (bf16 MFMA GEMM) timed with HIP events
-                around each of its launches during an eager pass of K steps
-                on the launch stream; achieved = algorithmic FLOPs / time.
+  roofline      the dominant kernel (the fused FFN; the projection GEMMs are
+                listed beside it) timed with HIP events around each of its
+                launches during an eager pass of K steps on the launch
+                stream; achieved = algorithmic FLOPs / time; traffic = HBM
+                bytes per launch from the committed rocprofv3 PMC pass.
   cpu_baseline  the from-scratch CPU restatement (oracle/, PyTorch CPU fp32)
                 of the same path on a bounded sample, host threads stated.
 """
@@ -101,44 +103,75 @@ def cpu_baseline(d_model, n_utt=16, reps=4):
             "sample": f"{n_utt} utt x 15 s synthetic, fp32, median of {reps} after 1 warm-up; CPU: {model}"}
 
 
-class _GemmProbe:
-    """Wraps speechbrain_amd._enc.gemm to time every bf16 GEMM launch with HIP
-    events on the launch stream and accumulate its algorithmic FLOPs."""
+class _LaunchProbe:
+    """Wraps one speechbrain_amd._enc entry point so that every bf16 launch is
+    bracketed by HIP events on the launch stream (torch's current stream, the
+    one the ctypes kernels are launched on) and its algorithmic FLOPs are
+    accumulated: `flops_of(*args, **kw)` -> FLOPs of that call."""
 
-    def __init__(self):
+    def __init__(self, name, flops_of, is_bf16):
         from speechbrain_amd import _enc
         self._enc = _enc
-        self.orig = _enc.gemm
+        self.name = name
+        self.orig = getattr(_enc, name)
+        self.flops_of = flops_of
+        self.is_bf16 = is_bf16
         self.events = []
         self.flops = 0.0
 
     def __enter__(self):
         probe = self
 
-        def wrapped(a, w, *args, **kw):
-            if a.dtype != torch.bfloat16:
-                return probe.orig(a, w, *args, **kw)
-            s = torch.cuda.current_stream(a.device)
+        def wrapped(*args, **kw):
+            if not probe.is_bf16(*args, **kw):
+                return probe.orig(*args, **kw)
+            s = torch.cuda.current_stream()
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record(s)
-            out = probe.orig(a, w, *args, **kw)
+            out = probe.orig(*args, **kw)
             e1.record(s)
             probe.events.append((e0, e1))
-            probe.flops += gemm_flops(a.shape[0], w.shape[0], a.shape[1])
+            probe.flops += probe.flops_of(*args, **kw)
             return out
-        self._enc.gemm = wrapped
-        # modules hold a reference through the module object, so patching the attribute suffices
+        setattr(self._enc, self.name, wrapped)  # callers resolve _enc.<name> at call time
         return self
 
     def __exit__(self, *exc):
-        self._enc.gemm = self.orig
+        setattr(self._enc, self.name, self.orig)
 
     def result(self):
         torch.cuda.synchronize()
         ms = sum(e0.elapsed_time(e1) for e0, e1 in self.events)
-        n = len(self.events)
-        return ms, n, self.flops
+        return ms, len(self.events), self.flops
+
+
+def _ffn_flops(x, ln0, w1, *a, **k):
+    return 4.0 * x.shape[0] * x.shape[1] * w1.shape[0]
+
+
+def _gemm_flops(a, w, *r, **k):
+    return gemm_flops(a.shape[0], w.shape[0], a.shape[1])
+
+
+def load_traffic():
+    """Per-launch HBM bytes of the profiled kernels (rocprofv3 PMC FETCH_SIZE x2
+    (gfx950 correction) + WRITE_SIZE), committed under profiles/."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
+def max_over_ranks(elapsed, world, device):
+    """The slowest rank's wall time (the job finishes when it does)."""
+    if world <= 1:
+        return elapsed
+    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def main():
@@ -200,23 +233,38 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
     ms_per_step = 1000.0 * elapsed / args.steps
     audio = world * args.batch * SECONDS * args.steps
     value = audio / elapsed
 
     if rank == 0:
         total_flops = encoder_flops(args.batch, T_e, args.d_model)
-        # dominant kernel: bf16 MFMA GEMM, HIP events around each launch over K eager steps
-        with _GemmProbe() as probe:
+        # per-kernel timing: HIP events around each launch over K eager steps
+        bf = lambda t: t.dtype == torch.bfloat16  # noqa: E731
+        probes = [_LaunchProbe("ffn", _ffn_flops, lambda x, ln0, w1, *a, **k: bf(w1)),
+                  _LaunchProbe("gemm", _gemm_flops, lambda a, w, *r, **k: bf(a))]
+        for p in probes:
+            p.__enter__()
+        try:
             for _ in range(args.steps):
+                # park the GPU while the host enqueues the step, so the events
+                # time kernels back to back, not host launch gaps
+                torch.cuda._sleep(50_000_000)
                 step()
-        gms, glaunch, gflops = probe.result()
-        achieved = gflops / (gms * 1e-3) / 1e12
+        finally:
+            for p in probes:
+                p.__exit__()
+        kern = {}
+        for p, label in zip(probes, ("ffn_kernel<256> (fused macaron FFN)", "gemm_kernel<bf16> (projections, all tiles)")):
+            ms, n, fl = p.result()
+            if n:
+                kern[p.name] = {"kernel": label, "launches_per_step": n // max(1, args.steps),
+                                "avg_launch_us": round(1000.0 * ms / n, 3),
+                                "achieved": round(fl / (ms * 1e-3) / 1e12, 2),
+                                "step_share_ms": round(ms / args.steps, 4)}
+        dom = max(kern.values(), key=lambda k: k["step_share_ms"]) if kern else None
+        traffic = load_traffic()
         res = {
             "metric": "audio-sec/sec Fbank→Conformer fwd (16kHz, B=32×15s) at 1/2/4/8 GPU",
             "value": round(value, 1),
@@ -234,13 +282,15 @@ def main():
                                    f"k=31 encode, B={args.batch}×15s per GPU",
                        "global_batch": world * args.batch, "seq_len": T_e, "parallelism": f"replicas{world}",
                        "hip_graph": graph is not None},
-            "roofline": {"bound": "mfma", "kernel": "gemm_kernel<bf16> (all encoder projections)",
-                         "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
-                         "launches_per_step": glaunch // max(1, args.steps),
-                         "avg_launch_us": round(1000.0 * gms / max(1, glaunch), 3),
-                         "step_algorithmic_tflop": round(total_flops / 1e12, 4),
-                         "step_tflops_achieved": round(total_flops / (ms_per_step * 1e-3) / 1e12, 2)},
+            "roofline": None if dom is None else {
+                "bound": "mfma", "kernel": dom["kernel"], "achieved": dom["achieved"], "peak": PEAK_BF16_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(dom["achieved"] / PEAK_BF16_TFLOPS, 4),
+                "traffic": traffic.get(dom["kernel"].split(" ")[0]),
+                "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch)",
+                "launches_per_step": dom["launches_per_step"], "avg_launch_us": dom["avg_launch_us"],
+                "step_algorithmic_tflop": round(total_flops / 1e12, 4),
+                "step_tflops_achieved": round(total_flops / (ms_per_step * 1e-3) / 1e12, 2),
+                "other_kernels": [k for k in kern.values() if k is not dom]},
         }
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(args.d_model)
