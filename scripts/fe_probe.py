@@ -1,0 +1,21 @@
+"""Front-end probe (GPU box, not part of the product): the fused two-block
+ConvolutionFrontEnd on (32, 1501, 80) bf16, timed."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import speechbrain_amd._lib as _L  # noqa: E402
+if os.environ.get("SBK_PROBE_LIB"):
+    _L.LIB_PATH = os.environ["SBK_PROBE_LIB"]  # probe builds of the kernel (not product)
+from speechbrain_amd.lobes.models.convolution import ConvolutionFrontEnd  # noqa: E402
+from scripts.kbench import timeit  # noqa: E402
+
+dev = torch.device("cuda")
+cnn = ConvolutionFrontEnd(input_shape=(8, 10, 80), num_blocks=2, num_layers_per_block=1, out_channels=(64, 32),
+                          kernel_sizes=(3, 3), strides=(2, 2), residuals=(False, False)).to(dev).eval()
+x = torch.randn(32, 1501, 80, device=dev)
+with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+    us = timeit(lambda: cnn.run(x, torch.bfloat16), reps=20)
+print(f"frontend fused: {us:.1f}us", flush=True)

@@ -117,6 +117,25 @@ def conv_block_mfma(x, wperm, bias, ln_w, ln_b, eps, slope, out_dtype):
     return out
 
 
+def conv_frontend2(x, blk1, blk2, wperm2, out_dtype):
+    """Both ConvBlocks in one kernel: x (B, T, F) fp32 → (B, T2, F2, C2).
+    blk*: (conv weight, bias, ln weight, ln bias, ln eps, leaky slope);
+    wperm2: block-2 weights (C2, 3, 3, C1) in the compute dtype."""
+    require_device(x, wperm2)
+    B, Tin, Fin = x.shape
+    w1, b1, g1, be1, e1, s1 = blk1
+    _, b2, g2, be2, e2, s2 = blk2
+    C1, C2 = w1.shape[0], wperm2.shape[0]
+    T1, F1 = (Tin - 1) // 2 + 1, (Fin - 1) // 2 + 1
+    T2, F2 = (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1
+    out = torch.empty(B, T2, F2, C2, device=x.device, dtype=out_dtype)
+    rc = lib().sbk_conv_frontend2(int(_is_bf16(wperm2)), ptr(x), B, Tin, Fin, ptr(w1), ptr(b1), ptr(g1), ptr(be1),
+                                  float(e1), float(s1), C1, ptr(wperm2), ptr(b2), ptr(g2), ptr(be2), float(e2),
+                                  float(s2), C2, ptr(out), int(out_dtype == _bf16), None, None, stream_of(x))
+    check(rc, "sbk_conv_frontend2")
+    return out
+
+
 def relpos_attention(qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale, need_probs=False):
     """Fused RelPosMHAXL core.  qkv: (B*T, 3d) head-interleaved, pk: (2T-1, d),
     both bf16 or fp32; returns (out (B*T, d) in qkv.dtype, probs or None)."""

@@ -12,6 +12,8 @@
 //                       Conv2d "same" reflect padding speechbrain/nnet/CNN.py:616-700
 #include "mfma.h"
 
+#include <algorithm>
+
 using namespace sbk;
 
 namespace {
@@ -334,6 +336,207 @@ __global__ void __launch_bounds__(256) conv_block_mfma_kernel(const T* __restric
   }
 }
 
+
+// Both ConvBlocks of the ConvolutionFrontEnd in one kernel (convolution.py
+// :12-84,169-175): conv3x3/s2 reflect (Cin=1) -> LN(F1*C1) -> LeakyReLU ->
+// conv3x3/s2 reflect (C1 -> C2, MFMA implicit GEMM) -> LN(F2*C2) -> LeakyReLU.
+// A 640-thread workgroup owns TT2 = 8 output time rows of one utterance: it
+// computes the 2*TT2+1 block-1 rows they read (reflect-padded) straight into
+// LDS (the (B, T1, F1, C1) intermediate never reaches HBM), stages the block-2
+// weights in LDS once, then waves 0..7 convolve output row t2_0 + w and
+// normalise it on their own.
+//   x (B, Tin, Fin) fp32; w1 (C1, 3, 3) fp32 in conv_block_c1's tap order;
+//   wp2 (C2, 3 time, 3 freq, C1) T; out (B, T2, F2*C2).
+// Block 1, two rows per pass: thread t owns channels 8*(t%8) .. +7 (their 72
+// taps and LN affine stay in VGPRs) at frequency (t/8) % 40 of row (t/8)/40,
+// so a row is exactly 5 waves; 9 input samples feed 72 FMAs and the 8 outputs
+// leave as one 16-B LDS store.
+template <typename T, int C1>
+__global__ void __launch_bounds__(640) frontend2_kernel(const float* __restrict__ x, int Tin, int Fin, int T1, int F1,
+                                                        int T2, int F2, const float* __restrict__ w1,
+                                                        const float* __restrict__ b1, const float* __restrict__ g1,
+                                                        const float* __restrict__ be1, float eps1, float slope1,
+                                                        const T* __restrict__ wp2, int C2,
+                                                        const float* __restrict__ b2, const float* __restrict__ g2,
+                                                        const float* __restrict__ be2, float eps2, float slope2,
+                                                        void* out, int out_bf16) {
+  using Tr = MT<T>;
+  constexpr int NT = 640, NW = NT / 64, TT2 = 8, NJ = 2 * TT2 + 1;
+  constexpr int FMAX = 40, CG = 8, WPR = FMAX * (C1 / CG) / 64;  // waves per block-1 row (5)
+  static_assert(C1 == 64 && FMAX * (C1 / CG) * 2 == NT, "block-1 thread map");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // LDS row strides padded by 16 B: the MFMA fragment reads of 16 lanes at
+  // different output frequencies (b1r rows 2 apart) / channels (wl rows)
+  // then spread over the banks instead of hitting one 16-B slot column
+  constexpr int C1P = C1 + 8;
+  const int K = 9 * C1, KP = K + 8;
+  T* wl = reinterpret_cast<T*>(smem);                                   // C2 x KP block-2 weights
+  float* yv = reinterpret_cast<float*>(wl + C2 * KP);                   // TT2 x F2*C2 (block 2)
+  float* xs = yv;                                                       // NJ x 3 x Fin (block 1, same space)
+  const int xsz = max(TT2 * F2 * C2, (NJ * 3 * Fin + 3) & ~3);
+  T* b1r = reinterpret_cast<T*>(yv + xsz);                              // NJ x F1 x C1P
+  __shared__ float red[2][NW];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nblk = (T2 + TT2 - 1) / TT2;
+  const int b = blockIdx.x / nblk, t20 = (blockIdx.x - b * nblk) * TT2;
+  const float* xb = x + (long long)b * Tin * Fin;
+
+  // stage block-2 weights (16-B vectors) and the input rows: block-1 row j is
+  // t1 = reflect(2*t20 - 1 + j) and reads x rows reflect(2*t1 - 1 + kt)
+  for (int i = tid; i < C2 * K / Tr::VEC; i += NT) {
+    const int co = (i * Tr::VEC) / K, kk = i * Tr::VEC - co * K;
+    *reinterpret_cast<uint4*>(wl + co * KP + kk) = reinterpret_cast<const uint4*>(wp2)[i];
+  }
+  for (int i = tid; i < NJ * 3 * Fin; i += NT) {
+    const int jk = i / Fin, f = i - jk * Fin;
+    const int j = jk / 3, kt = jk - 3 * j;
+    const int t1 = reflect_idx(2 * t20 - 1 + j, T1);
+    xs[i] = xb[(long long)reflect_idx(2 * t1 - 1 + kt, Tin) * Fin + f];
+  }
+  const int cg = tid % CG, q = tid / CG, rp = q / FMAX, f1 = q - rp * FMAX;
+  const bool act = f1 < F1;
+  const int f1c = act ? f1 : 0;
+  float wr[CG][9], gg[CG], bb[CG], bi[CG];
+#pragma unroll
+  for (int e = 0; e < CG; ++e) {
+    const int c = cg * CG + e;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wr[e][t] = w1[c * 9 + t];
+    bi[e] = b1 ? b1[c] : 0.f;
+    gg[e] = g1[f1c * C1 + c];
+    bb[e] = be1[f1c * C1 + c];
+  }
+  const int fi0 = reflect_idx(2 * f1c - 1, Fin), fi1 = 2 * f1c, fi2 = reflect_idx(2 * f1c + 1, Fin);
+  const float n1 = (float)(F1 * C1);
+  __syncthreads();
+
+  for (int j0 = 0; j0 < NJ; j0 += 2) {
+    const int j = j0 + rp;
+    const bool live = act && j < NJ;
+    float v[CG];
+    float sm = 0.f;
+    {
+      const float* r = xs + (min(j, NJ - 1) * 3) * Fin;
+      float xv[3][3];  // [kt][kf]
+#pragma unroll
+      for (int kt = 0; kt < 3; ++kt) {
+        xv[kt][0] = r[kt * Fin + fi0];
+        xv[kt][1] = r[kt * Fin + fi1];
+        xv[kt][2] = r[kt * Fin + fi2];
+      }
+#pragma unroll
+      for (int e = 0; e < CG; ++e) {
+        float acc = bi[e];
+#pragma unroll
+        for (int kf = 0; kf < 3; ++kf)
+#pragma unroll
+          for (int kt = 0; kt < 3; ++kt) acc = fmaf(wr[e][kf * 3 + kt], xv[kt][kf], acc);
+        v[e] = live ? acc : 0.f;
+        sm += v[e];
+      }
+    }
+    // row statistics: 5 waves per row, two-pass (mean, then centred squares)
+    sm = wave_sum(sm);
+    if (lane == 0) red[0][w] = sm;
+    __syncthreads();
+    float mean = 0.f;
+#pragma unroll
+    for (int k2 = 0; k2 < WPR; ++k2) mean += red[0][rp * WPR + k2];
+    mean /= n1;
+    float qq = 0.f;
+#pragma unroll
+    for (int e = 0; e < CG; ++e) qq += live ? (v[e] - mean) * (v[e] - mean) : 0.f;
+    qq = wave_sum(qq);
+    if (lane == 0) red[1][w] = qq;
+    __syncthreads();
+    float var = 0.f;
+#pragma unroll
+    for (int k2 = 0; k2 < WPR; ++k2) var += red[1][rp * WPR + k2];
+    const float rstd = 1.0f / sqrtf(var / n1 + eps1);
+    if (live) {
+      float y[CG];
+#pragma unroll
+      for (int e = 0; e < CG; ++e) {
+        const float t = (v[e] - mean) * rstd * gg[e] + bb[e];
+        y[e] = t >= 0.f ? t : t * slope1;
+      }
+      *reinterpret_cast<typename Tr::frag*>(b1r + (j * F1 + f1) * C1P + cg * CG) = Tr::from8(y);
+    }
+    // red[0] is rewritten next pass only after every wave passed the barrier above
+  }
+  __syncthreads();
+
+  if (w >= TT2) return;  // waves 8, 9: block 1 only (no barrier below)
+  // block 2: wave w -> output row t2 = t20 + w, reading block-1 rows j = 2w + kt
+  const int t2 = t20 + w;
+  if (t2 >= T2) return;  // no barrier below
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  // all (<= 2 x 2) output tiles of the row accumulate together, so each
+  // K step issues 4 independent MFMAs behind 4 fragment reads
+  const int mt = (F2 + 15) / 16, ntl = C2 / 16;
+  float* yw = yv + w * F2 * C2;
+  int fis[2][3];
+  bool frow[2];
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm) {
+    const int fo = tm * 16 + fr;
+    frow[tm] = tm < mt && fo < F2;
+#pragma unroll
+    for (int kf = 0; kf < 3; ++kf) fis[tm][kf] = reflect_idx(2 * (frow[tm] ? fo : 0) - 1 + kf, F1) * C1P;
+  }
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < 2; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int kt = 0; kt < 3; ++kt) {
+    const T* brow = b1r + (2 * w + kt) * F1 * C1P;
+#pragma unroll
+    for (int kf = 0; kf < 3; ++kf)
+#pragma unroll
+      for (int c0 = 0; c0 < C1; c0 += 32) {
+        const int ci = c0 + fk, k = (kt * 3 + kf) * C1 + ci;
+        typename Tr::frag fa[2], fbw[2];
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm) fa[tm] = frow[tm] ? Tr::load(brow + fis[tm][kf] + ci) : Tr::zero();
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) fbw[tn] = tn < ntl ? Tr::load(wl + (tn * 16 + fr) * KP + k) : Tr::zero();
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < 2; ++tn) Tr::mma(acc[tm][tn], fa[tm], fbw[tn]);
+      }
+  }
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < 2; ++tn) {
+      if (tm >= mt || tn >= ntl) continue;
+      const int co = tn * 16 + fr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int f = tm * 16 + 4 * (lane >> 4) + r;
+        if (f < F2) yw[f * C2 + co] = acc[tm][tn][r] + (b2 ? b2[co] : 0.f);
+      }
+    }
+  // the wave's own LDS row: LN over F2*C2 (wave-local), LeakyReLU, store
+  const int nout = F2 * C2;
+  float s2 = 0.f;
+  for (int o = lane; o < nout; o += 64) s2 += yw[o];
+  const float m2 = wave_sum(s2) / nout;
+  float q2 = 0.f;
+  for (int o = lane; o < nout; o += 64) q2 += (yw[o] - m2) * (yw[o] - m2);
+  const float r2 = 1.0f / sqrtf(wave_sum(q2) / nout + eps2);
+  const long long ob = ((long long)b * T2 + t2) * nout;
+  for (int o = lane; o < nout; o += 64) {
+    float y = (yw[o] - m2) * r2 * g2[o] + be2[o];
+    y = y >= 0.f ? y : y * slope2;
+    st(out, ob + o, y, out_bf16);
+  }
+}
+
 __global__ void cast_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long long n) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
     y[i] = f32_to_bf16(x[i]);
@@ -442,6 +645,39 @@ SBK_API int sbk_conv_block_mfma(int in_bf16, const void* x, int B, int Tin, int 
     hipLaunchKernelGGL(conv_block_mfma_kernel<float>, dim3(B * Tout), dim3(256), lds, s,
                        reinterpret_cast<const float*>(x), B, Tin, Fin, Cin, Tout, Fout, Cout,
                        reinterpret_cast<const float*>(wperm), bias, g, beta, eps, slope, out, out_bf16);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+SBK_API int sbk_conv_frontend2(int dtype_bf16, const float* x, int B, int Tin, int Fin, const float* w1,
+                               const float* b1, const float* g1, const float* be1, float eps1, float slope1, int C1,
+                               const void* wp2, const float* b2, const float* g2, const float* be2, float eps2,
+                               float slope2, int C2, void* out, int out_bf16, int* Tout_, int* Fout_, void* stream) {
+  if (B <= 0 || Tin < 2 || Fin < 4 || C1 != 64 || C2 % 16 || C2 <= 0) return SBK_ERR_ARG;
+  const int T1 = (Tin - 1) / 2 + 1, F1 = (Fin - 1) / 2 + 1;
+  const int T2 = (T1 - 1) / 2 + 1, F2 = (F1 - 1) / 2 + 1;
+  if (Tout_) *Tout_ = T2;
+  if (Fout_) *Fout_ = F2;
+  if (!x) return 0;
+  if (F1 > 40 || T1 < 2 || F1 < 2 || F2 > 32 || C2 > 32) return SBK_ERR_ARG;
+  constexpr int TT2 = 8, NJ = 2 * TT2 + 1;
+  const size_t esz = dtype_bf16 ? 2 : 4;
+  const size_t lds = (size_t)C2 * (9 * C1 + 8) * esz +
+                     (size_t)std::max(TT2 * F2 * C2, (NJ * 3 * Fin + 3) & ~3) * 4 + (size_t)NJ * F1 * (C1 + 8) * esz;
+  if (dtype_bf16 && lds > 160 * 1024 - 1024) return SBK_ERR_ARG;
+  const dim3 grid(B * ((T2 + TT2 - 1) / TT2));
+  hipStream_t s = (hipStream_t)stream;
+  if (!dtype_bf16) return SBK_ERR_ARG;  // fp32 path: the per-block kernels (LDS would not fit)
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&frontend2_kernel<bf16_t, 64>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((frontend2_kernel<bf16_t, 64>), grid, dim3(640), lds, s, x, Tin, Fin, T1, F1, T2, F2, w1, b1, g1,
+                     be1, eps1, slope1, reinterpret_cast<const bf16_t*>(wp2), C2, b2, g2, be2, eps2, slope2, out,
+                     out_bf16);
   SBK_CHECK_LAUNCH();
   return 0;
 }

@@ -57,6 +57,26 @@ class ConvBlock(nn.Module):
         if self.training and c.dropout_0.p > 0:
             raise NotImplementedError("dropout in training mode is not implemented in HIP yet")
 
+    def params(self):
+        """(conv weight, bias, ln weight, ln bias, ln eps, leaky slope) of the fused block."""
+        c = self.convs
+        conv = c.conv_0.conv
+        ln = c.norm_0.norm
+        bias = conv.bias.detach() if conv.bias is not None else None
+        return (conv.weight.detach().contiguous(), bias, ln.weight.detach(), ln.bias.detach(), ln.eps,
+                c.act_0.negative_slope)
+
+    def wperm(self, dtype):
+        """Weights as (Cout, time, freq, Cin) in the compute dtype (implicit-GEMM B operand)."""
+        conv = self.convs.conv_0.conv
+        if not hasattr(self, "_wc"):
+            self._wc = _enc.WeightCache()
+
+        def make():
+            w = conv.weight.detach().permute(0, 3, 2, 1).contiguous()  # (Cout, time, freq, Cin)
+            return _enc.cast_bf16(w) if dtype == torch.bfloat16 else w
+        return self._wc.get(("wperm", dtype), [conv.weight], make)
+
     def run(self, x, out_dtype):
         self._check()
         c = self.convs
@@ -72,14 +92,7 @@ class ConvBlock(nn.Module):
         if x.dim() == 3:
             x = x.unsqueeze(-1)
         dtype = x.dtype if x.dtype == torch.bfloat16 else _f32
-        key = ("wperm", dtype)
-        if not hasattr(self, "_wc"):
-            self._wc = _enc.WeightCache()
-
-        def make():
-            w = conv.weight.detach().permute(0, 3, 2, 1).contiguous()  # (Cout, time, freq, Cin)
-            return _enc.cast_bf16(w) if dtype == torch.bfloat16 else w
-        wp = self._wc.get(key, [conv.weight], make)
+        wp = self.wperm(dtype)
         return _enc.conv_block_mfma(x.contiguous(), wp, bias, ln.weight.detach(), ln.bias.detach(), ln.eps, slope,
                                     out_dtype)
 
@@ -118,9 +131,24 @@ class ConvolutionFrontEnd(nn.Module):
             shape = blk.out_shape
             block_out_shapes.append(shape)
 
+    def _fusable2(self, x, dtype):
+        if dtype != torch.bfloat16 or len(self.block_names) != 2 or x.dim() != 3:
+            return False
+        b1, b2 = (getattr(self, n) for n in self.block_names)
+        for blk in (b1, b2):
+            blk._check()
+        c1, c2 = b1.convs.conv_0.conv, b2.convs.conv_0.conv
+        return (c1.in_channels == 1 and c1.out_channels == 64 and c2.in_channels == 64
+                and c2.out_channels % 16 == 0 and c2.out_channels <= 32 and (x.shape[2] - 1) // 2 + 1 <= 40)
+
     def run(self, x, last_dtype):
         """Intermediate block outputs in the compute dtype, the last in `last_dtype`."""
         dtype = _enc.compute_dtype()
+        if self._fusable2(x, dtype):
+            # both blocks in one kernel: the block-1 activation stays in LDS
+            b1, b2 = (getattr(self, n) for n in self.block_names)
+            return _enc.conv_frontend2(x.float().contiguous(), b1.params(), b2.params(), b2.wperm(dtype),
+                                       last_dtype)
         n = len(self.block_names)
         for i, name in enumerate(self.block_names):
             x = getattr(self, name).run(x, last_dtype if i == n - 1 else dtype)

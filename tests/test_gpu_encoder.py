@@ -104,6 +104,29 @@ def test_fused_ffn_vs_unfused(dev, D, H, M):
     assert_close(out2, z, rtol=2e-2, name="ffn in-place")
 
 
+@pytest.mark.parametrize("T,F", [(1501, 80), (101, 80), (7, 40)])
+def test_fused_frontend_vs_blockwise(dev, T, F):
+    """sbk_conv_frontend2 (both ConvBlocks in one kernel, bf16 compute) vs the
+    two per-block kernels at the same rounding points, within 2e-2 (a
+    different fp32 summation order in block 1's LayerNorm can flip a bf16
+    rounding of the intermediate).  The fp32 path runs the per-block kernels."""
+    from speechbrain_amd.lobes.models.convolution import ConvolutionFrontEnd
+    torch.manual_seed(0)
+    cnn = ConvolutionFrontEnd(input_shape=(8, 10, F), num_blocks=2, num_layers_per_block=1, out_channels=(64, 32),
+                              kernel_sizes=(3, 3), strides=(2, 2), residuals=(False, False)).to(dev).eval()
+    x = torch.randn(3, T, F, device=dev)
+    b1, b2 = cnn.convblock_0, cnn.convblock_1
+    with torch.no_grad():
+        y = cnn.run(x, torch.float32)
+        ref = b2.run(b1.run(x, torch.float32), torch.float32)
+        assert y.shape == ref.shape
+        assert_close(y, ref, rtol=0, name="frontend fp32")
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y16 = cnn.run(x, torch.bfloat16)
+            r16 = b2.run(b1.run(x, torch.bfloat16), torch.bfloat16)
+    assert_close(y16.float(), r16.float(), rtol=2e-2, name="frontend bf16")
+
+
 # ----------------------------------------------------------------------------- modules vs golden
 def test_conv_frontend_vs_golden(golden, dev):
     from speechbrain_amd.lobes.models.convolution import ConvolutionFrontEnd
