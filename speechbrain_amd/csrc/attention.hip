@@ -96,8 +96,14 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
   const int d_model = H * dh;
   const long long row3 = 3LL * d_model;
   const int nqb = (Tn + QB - 1) / QB;
-  const int qb = blockIdx.x % nqb;
-  const int bh = blockIdx.x / nqb;
+  // XCD-aware bijective remap: workgroups are dealt round-robin to the 8 XCDs;
+  // give each XCD a contiguous run of tiles so the query blocks of one (b, h)
+  // share an L2 and its K/V/positional rows are fetched from HBM once.
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int qb = tile % nqb;
+  const int bh = tile / nqb;
   const int h = bh % H, b = bh / H;
   const int i0 = qb * QB;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
