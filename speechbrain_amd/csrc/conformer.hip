@@ -101,23 +101,37 @@ __global__ void __launch_bounds__(256) dwconv_ln_swish_kernel(const T* __restric
                                                               const float* __restrict__ g,
                                                               const float* __restrict__ beta, float eps, void* out,
                                                               int out_bf16) {
+  // Phase 0: the TT + K - 1 input rows (zero-padded at the sequence ends) are
+  // staged into LDS with 16-B loads; phase 1: thread c slides its K taps over
+  // its channel's column (register window) into an fp32 LDS tile; phase 2:
+  // one wave per timestep normalises across channels, 4 channels per lane,
+  // Swish, 8-/16-B stores.  Needs C % (64 * 4) == 0 and 16-B aligned rows.
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* cv = reinterpret_cast<float*>(smem);  // TT x C
+  constexpr int NR = TT + K - 1;
+  T* xs = reinterpret_cast<T*>(smem);                                          // NR x C
+  float* cv = reinterpret_cast<float*>(smem + (((size_t)NR * C * sizeof(T) + 15) & ~(size_t)15));  // TT x C
   const int ntile = (Tn + TT - 1) / TT;
   const int b = blockIdx.x / ntile;
   const int t0 = (blockIdx.x - b * ntile) * TT;
   const int nt = min(TT, Tn - t0);
   const T* xb = x + (long long)b * Tn * C;
+  constexpr int VEC = 16 / sizeof(T);
+  const int vpr = C / VEC;  // 16-B vectors per row
+  for (int i = threadIdx.x; i < NR * vpr; i += blockDim.x) {
+    const int r = i / vpr, cv0 = (i - r * vpr) * VEC;
+    const int t = t0 - padL + r;
+    uint4 val = make_uint4(0, 0, 0, 0);
+    if (t >= 0 && t < Tn) val = *reinterpret_cast<const uint4*>(xb + (long long)t * C + cv0);
+    *reinterpret_cast<uint4*>(xs + r * C + cv0) = val;
+  }
+  __syncthreads();
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float wk[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) wk[k] = w[c * K + k];
-    float win[TT + K - 1];
+    float win[NR];
 #pragma unroll
-    for (int r = 0; r < TT + K - 1; ++r) {
-      const int t = t0 - padL + r;
-      win[r] = (t >= 0 && t < Tn) ? ld(xb, (long long)t * C + c) : 0.f;
-    }
+    for (int r = 0; r < NR; ++r) win[r] = ld(xs, r * C + c);
     const float bc = bias ? bias[c] : 0.f;
 #pragma unroll
     for (int tt = 0; tt < TT; ++tt) {
@@ -129,22 +143,39 @@ __global__ void __launch_bounds__(256) dwconv_ln_swish_kernel(const T* __restric
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int tt = wid; tt < nt; tt += 4) {
+  const int nw = blockDim.x >> 6;
+  for (int tt = wid; tt < nt; tt += nw) {
     const float* r = cv + tt * C;
     float s = 0.f;
-    for (int c = lane; c < C; c += 64) s += r[c];
+    for (int c = 4 * lane; c < C; c += 256) {
+      const float4 v = *reinterpret_cast<const float4*>(r + c);
+      s += (v.x + v.y) + (v.z + v.w);
+    }
     const float mean = wave_sum(s) / C;
     float q = 0.f;
-    for (int c = lane; c < C; c += 64) {
-      const float d = r[c] - mean;
-      q += d * d;
+    for (int c = 4 * lane; c < C; c += 256) {
+      const float4 v = *reinterpret_cast<const float4*>(r + c);
+      q += (v.x - mean) * (v.x - mean) + (v.y - mean) * (v.y - mean) + (v.z - mean) * (v.z - mean) +
+           (v.w - mean) * (v.w - mean);
     }
     const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
     const long long ob = ((long long)b * Tn + t0 + tt) * C;
-    for (int c = lane; c < C; c += 64) {
-      float y = (r[c] - mean) * rstd * g[c] + beta[c];
-      y = y * (1.0f / (1.0f + expf(-y)));
-      st(out, ob + c, y, out_bf16);
+    for (int c = 4 * lane; c < C; c += 256) {
+      const float4 v = *reinterpret_cast<const float4*>(r + c);
+      float y[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float z = (y[e] - mean) * rstd * g[c + e] + beta[c + e];
+        y[e] = z * (1.0f / (1.0f + __expf(-z)));
+      }
+      if (out_bf16) {
+        uint2 pk;
+        pk.x = (uint32_t)f32_to_bf16(y[0]) | ((uint32_t)f32_to_bf16(y[1]) << 16);
+        pk.y = (uint32_t)f32_to_bf16(y[2]) | ((uint32_t)f32_to_bf16(y[3]) << 16);
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(out) + ob + c) = pk;
+      } else {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + ob + c) = make_float4(y[0], y[1], y[2], y[3]);
+      }
     }
   }
 }
@@ -581,10 +612,11 @@ SBK_API int sbk_dwconv_ln_swish(int in_bf16, const void* x, int B, int Tn, int C
   if (B <= 0 || Tn <= 0 || C <= 0 || K <= 0) return SBK_ERR_ARG;
   const int padL = causal ? K - 1 : (K - 1) / 2;
   hipStream_t s = (hipStream_t)stream;
-  if (K == 31 && (size_t)16 * C * 4 <= 64 * 1024) {
+  if (K == 31 && C % 256 == 0 && (size_t)(16 + 30) * C * 4 + (size_t)16 * C * 4 <= 64 * 1024) {
     constexpr int TT = 16;
     const int grid = B * ((Tn + TT - 1) / TT);
-    const size_t lds = (size_t)TT * C * 4;
+    const size_t esz = in_bf16 ? 2 : 4;
+    const size_t lds = (((size_t)(TT + 30) * C * esz + 15) & ~(size_t)15) + (size_t)TT * C * 4;
     if (in_bf16)
       hipLaunchKernelGGL((dwconv_ln_swish_kernel<bf16_t, 31, TT>), dim3(grid), dim3(256), lds, s,
                          reinterpret_cast<const bf16_t*>(x), B, Tn, C, w, bias, padL, g, beta, eps, out, out_bf16);
