@@ -9,21 +9,37 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import speechbrain_amd._lib as _L  # noqa: E402
+if os.environ.get("SBK_PROBE_LIB"):
+    _L.LIB_PATH = os.environ["SBK_PROBE_LIB"]  # probe builds of a kernel (not product)
 from speechbrain_amd import _enc  # noqa: E402
 from speechbrain_amd._lib import lib, ptr, stream_of  # noqa: E402
 
 
 def timeit(fn, reps=50, warm=5):
+    """Device time per call: `reps` calls captured in one HIP graph and
+    replayed, so host dispatch cost is excluded (kernels run back to back)."""
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(reps):
-        fn()
+    for _ in range(3):
+        g.replay()
     e1.record()
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / reps * 1000.0  # us
+    return e0.elapsed_time(e1) / (3 * reps) * 1000.0  # us
 
 
 def gemm_bench():
@@ -39,10 +55,24 @@ def gemm_bench():
         r = torch.randn(M, N // 2 if act == "glu" else N, device=dev) if res else None
         fl = 2.0 * M * N * K
         line = f"{name:9s} M={M} N={N} K={K}:"
-        for tile in (2, 3, 8, 9, 10):
+        for tile in (2, 9, 18, 19, 20, 21, 22):
             us = timeit(lambda: _enc.gemm(a, w, bias=b, act=act, res=r, out_dtype=od, tile=tile))
             line += f" t{tile} {us:6.1f}us {fl / us / 1e6:6.0f}TF"
+        # library reference point (plain GEMM, no fused epilogue): hipBLASLt via torch
+        us = timeit(lambda: torch.mm(a, w.t()))
+        line += f" | torch.mm {us:6.1f}us {fl / us / 1e6:6.0f}TF"
         print(line, flush=True)
+
+
+def gemm_one(name="qkv", tile=2):
+    """One GEMM shape/tile, 50 launches (for counter passes)."""
+    dev = torch.device("cuda")
+    M = 12032
+    N, K = {"qkv": (768, 256), "out_proj": (256, 256), "ffn_down": (256, 1024)}[name]
+    a = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
+    us = timeit(lambda: _enc.gemm(a, w, out_dtype=torch.bfloat16, tile=tile))
+    print(f"{name} tile {tile}: {us:.1f}us", flush=True)
 
 
 def attn_bench():
@@ -101,5 +131,7 @@ if __name__ == "__main__":
         attn_bench()
     if what in ("misc", "all"):
         misc_bench()
+    if what == "gemm1":
+        gemm_one(sys.argv[2] if len(sys.argv) > 2 else "qkv", int(sys.argv[3]) if len(sys.argv) > 3 else 2)
     if what in ("ffn", "all"):
         ffn_bench()

@@ -17,14 +17,31 @@ OBJ = os.path.join(CSRC, "build")
 LIB = os.path.join(HERE, "libsbk.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
+# -amdgpu-mfma-vgpr-form: MFMA accumulators in VGPRs.  With the default AGPR
+# form the register allocator shuffled accumulators through v_accvgpr_* moves
+# on every loop iteration of the GEMM / attention kernels (1,252 and 1,692
+# static moves).
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
-          "-Wno-unused-result", "-fvisibility=hidden"]
+          "-Wno-unused-result", "-fvisibility=hidden", "-mllvm", "-amdgpu-mfma-vgpr-form"]
 
 
-def _compile(src):
+def _flags_changed():
+    """Objects are rebuilt when the compile flags change (stamp under build/)."""
+    stamp = os.path.join(OBJ, "flags.txt")
+    want = " ".join([HIPCC] + CFLAGS)
+    have = open(stamp).read() if os.path.exists(stamp) else ""
+    if have != want:
+        os.makedirs(OBJ, exist_ok=True)
+        with open(stamp, "w") as f:
+            f.write(want)
+        return True
+    return False
+
+
+def _compile(src, force=False):
     obj = os.path.join(OBJ, os.path.basename(src).replace(".hip", ".o"))
     deps = [src] + glob.glob(os.path.join(CSRC, "*.h"))
-    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
+    if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return obj, None
     cmd = [HIPCC, *CFLAGS, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -37,8 +54,9 @@ def build(verbose=False, jobs=None):
     os.makedirs(OBJ, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     jobs = jobs or min(len(srcs), max(1, min(16, os.cpu_count() or 4)))
+    force = _flags_changed()
     with cf.ThreadPoolExecutor(jobs) as ex:
-        results = list(ex.map(_compile, srcs))
+        results = list(ex.map(lambda src: _compile(src, force), srcs))
     errs = [e for _, e in results if e]
     if errs:
         raise RuntimeError("hipcc failed:\n" + "\n".join(errs))

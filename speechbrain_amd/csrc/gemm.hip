@@ -38,121 +38,102 @@ struct Epi {
   int out_bf16;
 };
 
-template <typename T, int BM, int BN, int BK, int NBUF>
-__global__ void __launch_bounds__(256) gemm_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W,
-                                                   int ldw, int M, int N, int K, Epi ep) {
-  using Tr = MT<T>;
-  constexpr int VEC = Tr::VEC;
-  constexpr int LDSR = BK + Tr::PAD;     // LDS row stride (elements)
-  constexpr int WM = BM / 2, WN = BN / 2;
-  constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int CPR = BK / VEC;          // 16-B chunks per row
-  constexpr int ACH = BM * CPR / 256;    // chunks per thread (A)
-  constexpr int BCH = BN * CPR / 256;    // chunks per thread (B)
-  static_assert(ACH >= 1 && BCH >= 1, "tile too small for 256 threads");
+// C tile (fp32, row stride CR, in LDS) -> global through the fused epilogue:
+// bias, activation (GLU pairs [value16 | gate16] column groups), row mask,
+// alpha, fp32 residual; fp32 or bf16 output, 16-/8-B vector stores.
+template <int ACT>
+__device__ __forceinline__ float epi_act(float x, float slope) {
+  if (ACT == ACT_SWISH) return x * (1.0f / (1.0f + __expf(-x)));
+  if (ACT == ACT_LRELU) return x >= 0.f ? x : x * slope;
+  if (ACT == ACT_GELU) return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+  return x;
+}
 
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  T* As = reinterpret_cast<T*>(smem);
-  T* Bs = As + NBUF * BM * LDSR;
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int ntn = (N + BN - 1) / BN;
-  // XCD-aware remap (bijective): workgroups dealt round-robin to the 8 XCDs get
-  // consecutive tiles per XCD, so the N-tiles of one A row-panel share an L2.
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int tile_id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int m0 = (tile_id / ntn) * BM;
-  const int n0 = (tile_id % ntn) * BN;
-
-  uint4 ra[ACH], rb[BCH];
-  auto gload = [&](int k0) {
+// Fast path of store_ctile: the whole tile is in range and every pointer /
+// leading dimension is 16-B (fp32) or 8-B (bf16) aligned.  Each thread owns
+// one fixed output column quad (NT is a multiple of the quads per row), so
+// bias is one float4 load; the row loop has a compile-time trip count and is
+// fully unrolled, so every LDS read / residual load of the tile is in flight
+// at once instead of one dependent round trip per iteration.
+template <int BM, int BN, int NT, int ACT, bool GLU>
+__device__ __forceinline__ void store_ctile_fast(const float* __restrict__ Cs, const Epi& ep, int m0, int n0,
+                                                 int tid) {
+  constexpr int CR = BN + 4;
+  constexpr int NCOL = GLU ? BN / 2 : BN;
+  constexpr int QPR = NCOL / 4;          // column quads per row
+  static_assert(NT % QPR == 0, "thread map");
+  constexpr int RPI = NT / QPR;          // rows per pass
+  constexpr int NPASS = BM / RPI;
+  static_assert(BM % RPI == 0, "rows");
+  const int o = (tid % QPR) * 4, r0 = tid / QPR;
+  const int oc = (GLU ? n0 / 2 : n0) + o;
+  // LDS columns of this quad: GLU tiles hold [value16 | gate16] column groups
+  const int ca = GLU ? 32 * (o >> 4) + (o & 15) : o;
+  float4 ba = make_float4(0.f, 0.f, 0.f, 0.f), bg = ba;
+  if (ep.bias) {
+    ba = *reinterpret_cast<const float4*>(ep.bias + n0 + ca);
+    if (GLU) bg = *reinterpret_cast<const float4*>(ep.bias + n0 + ca + 16);
+  }
 #pragma unroll
-    for (int i = 0; i < ACH; ++i) {
-      const int c = tid + i * 256, r = c / CPR, kc = (c % CPR) * VEC;
-      const int gr = m0 + r, gk = k0 + kc;
-      ra[i] = (gr < M && gk < K) ? *reinterpret_cast<const uint4*>(A + (long long)gr * lda + gk) : make_uint4(0, 0, 0, 0);
+  for (int p = 0; p < NPASS; ++p) {
+    const int r = r0 + p * RPI, row = m0 + r;
+    const float4 a = *reinterpret_cast<const float4*>(Cs + r * CR + ca);
+    float v[4] = {a.x + ba.x, a.y + ba.y, a.z + ba.z, a.w + ba.w};
+    if (GLU) {
+      const float4 gt = *reinterpret_cast<const float4*>(Cs + r * CR + ca + 16);
+      const float gg[4] = {gt.x + bg.x, gt.y + bg.y, gt.z + bg.z, gt.w + bg.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] *= 1.0f / (1.0f + __expf(-gg[e]));
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = epi_act<ACT>(v[e], ep.slope);
     }
+    const float sc = (ep.rowmask && ep.rowmask[row]) ? 0.f : ep.alpha;
 #pragma unroll
-    for (int i = 0; i < BCH; ++i) {
-      const int c = tid + i * 256, r = c / CPR, kc = (c % CPR) * VEC;
-      const int gr = n0 + r, gk = k0 + kc;
-      rb[i] = (gr < N && gk < K) ? *reinterpret_cast<const uint4*>(W + (long long)gr * ldw + gk) : make_uint4(0, 0, 0, 0);
+    for (int e = 0; e < 4; ++e) v[e] *= sc;
+    if (ep.res) {
+      const float4 rv = *reinterpret_cast<const float4*>(ep.res + (long long)row * ep.ldr + oc);
+      v[0] += rv.x; v[1] += rv.y; v[2] += rv.z; v[3] += rv.w;
     }
-  };
-  auto sstore = [&](int buf) {
-    T* as = As + buf * BM * LDSR;
-    T* bs = Bs + buf * BN * LDSR;
-#pragma unroll
-    for (int i = 0; i < ACH; ++i) {
-      const int c = tid + i * 256, r = c / CPR, kc = (c % CPR) * VEC;
-      *reinterpret_cast<uint4*>(as + r * LDSR + kc) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < BCH; ++i) {
-      const int c = tid + i * 256, r = c / CPR, kc = (c % CPR) * VEC;
-      *reinterpret_cast<uint4*>(bs + r * LDSR + kc) = rb[i];
-    }
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = (K + BK - 1) / BK;
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  int cur = 0;
-  const int fr = lane & 15, fk = 8 * (lane >> 4);
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) gload((kt + 1) * BK);
-    const T* as = As + cur * BM * LDSR + (wm * WM + fr) * LDSR + fk;
-    const T* bs = Bs + cur * BN * LDSR + (wn * WN + fr) * LDSR + fk;
-#pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      typename Tr::frag fa[TM], fb[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) fa[i] = Tr::load(as + i * 16 * LDSR + ks * 32);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) fb[j] = Tr::load(bs + j * 16 * LDSR + ks * 32);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) Tr::mma(acc[i][j], fa[i], fb[j]);
-    }
-    if (NBUF == 2) {
-      if (kt + 1 < nk) sstore(cur ^ 1);
-      __syncthreads();
-      cur ^= 1;
-    } else if (kt + 1 < nk) {
-      __syncthreads();  // all waves done reading the single buffer
-      sstore(0);
-      __syncthreads();
+    if (ep.out_bf16) {
+      uint2 pk;
+      pk.x = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
+      pk.y = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
+      *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(ep.out) + (long long)row * ep.ldc + oc) = pk;
+    } else {
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(ep.out) + (long long)row * ep.ldc + oc) =
+          make_float4(v[0], v[1], v[2], v[3]);
     }
   }
-  if (NBUF == 1) __syncthreads();
+}
 
-  // ---- epilogue: accumulators -> LDS C tile -> coalesced vector pass ----
-  // (the staging ring is free: the last loop iteration ended with a barrier)
-  constexpr int CR = BN + 4;  // C tile row stride (floats)
-  float* Cs = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        Cs[(wm * WM + i * 16 + 4 * (lane >> 4) + r) * CR + wn * WN + j * 16 + fr] = acc[i][j][r];
-  __syncthreads();
+__device__ __forceinline__ bool epi_aligned(const Epi& ep) {
+  const uintptr_t m = reinterpret_cast<uintptr_t>(ep.bias) | reinterpret_cast<uintptr_t>(ep.res) |
+                      reinterpret_cast<uintptr_t>(ep.out);
+  return (m & 15) == 0 && (ep.ldr & 3) == 0 && (ep.ldc & 3) == 0;
+}
+
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void store_ctile(const float* __restrict__ Cs, const Epi& ep, int m0, int n0, int M,
+                                            int N, int tid) {
+#ifdef SBK_PROBE_NO_EPI
+  if (Cs[tid] != 12345.f) return;
+#endif
+  if (m0 + BM <= M && n0 + BN <= N && epi_aligned(ep)) {
+    switch (ep.act) {
+      case ACT_NONE: store_ctile_fast<BM, BN, NT, ACT_NONE, false>(Cs, ep, m0, n0, tid); return;
+      case ACT_SWISH: store_ctile_fast<BM, BN, NT, ACT_SWISH, false>(Cs, ep, m0, n0, tid); return;
+      case ACT_GLU: store_ctile_fast<BM, BN, NT, ACT_NONE, true>(Cs, ep, m0, n0, tid); return;
+      case ACT_LRELU: store_ctile_fast<BM, BN, NT, ACT_LRELU, false>(Cs, ep, m0, n0, tid); return;
+      case ACT_GELU: store_ctile_fast<BM, BN, NT, ACT_GELU, false>(Cs, ep, m0, n0, tid); return;
+    }
+  }
+  constexpr int CR = BN + 4;
   const bool glu = ep.act == ACT_GLU;
   const int ncols = glu ? BN / 2 : BN;       // output columns of this tile
   const int oc0 = glu ? n0 / 2 : n0;         // first output column
   const int nout = glu ? N / 2 : N;
-  for (int c = tid; c < BM * (ncols / 4); c += 256) {
+  for (int c = tid; c < BM * (ncols / 4); c += NT) {
     const int r = c / (ncols / 4), o = (c % (ncols / 4)) * 4;
     const int row = m0 + r;
     if (row >= M || oc0 + o >= nout) continue;
@@ -224,15 +205,396 @@ __global__ void __launch_bounds__(256) gemm_kernel(const T* __restrict__ A, int 
   }
 }
 
+template <typename T, int BM, int BN, int BK, int NBUF>
+__global__ void __launch_bounds__(256) gemm_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W,
+                                                   int ldw, int M, int N, int K, Epi ep) {
+  using Tr = MT<T>;
+  constexpr int VEC = Tr::VEC;
+  // LDS row stride (elements): +32 B for bf16 makes the 16-lane ds_read_b128
+  // groups of the fragment reads bank-conflict-free (+16 B left 2-way conflicts)
+  constexpr int LDSR = BK + (sizeof(T) == 2 ? 2 : 1) * Tr::PAD;
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int CPR = BK / VEC;          // 16-B chunks per row
+  constexpr int ACH = BM * CPR / 256;    // chunks per thread (A)
+  constexpr int BCH = BN * CPR / 256;    // chunks per thread (B)
+  static_assert(ACH >= 1 && BCH >= 1, "tile too small for 256 threads");
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* As = reinterpret_cast<T*>(smem);
+  T* Bs = As + NBUF * BM * LDSR;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int ntn = (N + BN - 1) / BN;
+  // XCD-aware remap (bijective): workgroups dealt round-robin to the 8 XCDs get
+  // consecutive tiles per XCD, so the N-tiles of one A row-panel share an L2.
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int tile_id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int m0 = (tile_id / ntn) * BM;
+  const int n0 = (tile_id % ntn) * BN;
+
+  uint4 ra[ACH], rb[BCH];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int c = tid + i * 256, r = c / CPR, kc = (c % CPR) * VEC;
+      const int gr = m0 + r, gk = k0 + kc;
+      ra[i] = (gr < M && gk < K) ? *reinterpret_cast<const uint4*>(A + (long long)gr * lda + gk) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int c = tid + i * 256, r = c / CPR, kc = (c % CPR) * VEC;
+      const int gr = n0 + r, gk = k0 + kc;
+      rb[i] = (gr < N && gk < K) ? *reinterpret_cast<const uint4*>(W + (long long)gr * ldw + gk) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto sstore = [&](int buf) {
+    T* as = As + buf * BM * LDSR;
+    T* bs = Bs + buf * BN * LDSR;
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int c = tid + i * 256, r = c / CPR, kc = (c % CPR) * VEC;
+      *reinterpret_cast<uint4*>(as + r * LDSR + kc) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int c = tid + i * 256, r = c / CPR, kc = (c % CPR) * VEC;
+      *reinterpret_cast<uint4*>(bs + r * LDSR + kc) = rb[i];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#ifdef SBK_PROBE_NO_MAIN
+  const int nk = 1;
+#else
+  const int nk = (K + BK - 1) / BK;
+#endif
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  int cur = 0;
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) gload((kt + 1) * BK);
+    const T* as = As + cur * BM * LDSR + (wm * WM + fr) * LDSR + fk;
+    const T* bs = Bs + cur * BN * LDSR + (wn * WN + fr) * LDSR + fk;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      typename Tr::frag fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = Tr::load(as + i * 16 * LDSR + ks * 32);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = Tr::load(bs + j * 16 * LDSR + ks * 32);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) Tr::mma(acc[i][j], fa[i], fb[j]);
+    }
+    if (NBUF == 2) {
+      if (kt + 1 < nk) sstore(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    } else if (kt + 1 < nk) {
+      __syncthreads();  // all waves done reading the single buffer
+      sstore(0);
+      __syncthreads();
+    }
+  }
+  if (NBUF == 1) __syncthreads();
+
+  // ---- epilogue: accumulators -> LDS C tile -> coalesced vector pass ----
+  // (the staging ring is free: the last loop iteration ended with a barrier)
+  constexpr int CR = BN + 4;  // C tile row stride (floats)
+  float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(wm * WM + i * 16 + 4 * (lane >> 4) + r) * CR + wn * WN + j * 16 + fr] = acc[i][j][r];
+  __syncthreads();
+  store_ctile<BM, BN, 256>(Cs, ep, m0, n0, M, N, tid);
+}
+
 template <typename T, int BM, int BN, int BK, int NBUF = 2>
 int launch(const void* A, int lda, const void* W, int ldw, int M, int N, int K, const Epi& ep, hipStream_t s) {
-  constexpr int LDSR = BK + MT<T>::PAD;
+  constexpr int LDSR = BK + (sizeof(T) == 2 ? 2 : 1) * MT<T>::PAD;
   size_t lds = (size_t)NBUF * (BM + BN) * LDSR * sizeof(T);
   const size_t cbytes = (size_t)BM * (BN + 4) * 4;  // epilogue C tile
   if (cbytes > lds) lds = cbytes;
   const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   hipLaunchKernelGGL((gemm_kernel<T, BM, BN, BK, NBUF>), dim3(grid), dim3(256), lds, s, reinterpret_cast<const T*>(A),
                      lda, reinterpret_cast<const T*>(W), ldw, M, N, K, ep);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+
+// LDS-DMA ring GEMM (bf16, K % 64 == 0, K >= 192): 4 waves (2x2), tile BM x BN,
+// 64-deep K steps staged global -> LDS by global_load_lds_dwordx4 (full
+// 128-B lines, no VGPRs) into a 4-slot ring with 3 steps in flight across one
+// raw barrier per step (counted vmcnt; the tail re-loads the last step into a
+// dead slot so every step waits on the same count).  The LDS image is
+// lane-linear, 16-B chunks XOR-swizzled by (row >> 1) & 7 on the source
+// address and on the fragment reads (conflict-free ds_read_b128).  Out-of-
+// range rows clamp their source to the last row (results never stored).
+template <int BM, int BN>
+__global__ void __launch_bounds__(256) gemm_ring_kernel(const bf16_t* __restrict__ A, int lda,
+                                                        const bf16_t* __restrict__ W, int ldw, int M, int N, int K,
+                                                        Epi ep) {
+  constexpr int BK = 64, NB = 4, NT = 256;
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  constexpr int SLOT = (BM + BN) * BK;          // elements per ring slot
+  constexpr int GA = BM * BK * 2 / 1024 / 4;    // LDS-DMA pieces per wave per step (A)
+  constexpr int GB = BN * BK * 2 / 1024 / 4;    // (B)
+  constexpr int GPS = GA + GB;
+  static_assert(GA >= 1 && GB >= 1 && GA * 4 * 1024 == BM * BK * 2 && GB * 4 * 1024 == BN * BK * 2, "tile");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* ring = reinterpret_cast<bf16_t*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int fr = lane & 15, g = lane >> 4;
+  const int ntn = (N + BN - 1) / BN;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int tile_id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int m0 = (tile_id / ntn) * BM;
+  const int n0 = (tile_id % ntn) * BN;
+  const int nk = K / BK;
+
+  // piece p of a tile covers rows 8p .. 8p+7; lane -> row 8p + lane/8, chunk lane%8
+  const int lrow = lane >> 3, lchk = lane & 7;
+  auto issue = [&](int kt) __attribute__((always_inline)) {
+    bf16_t* dst = ring + (kt % NB) * SLOT;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const int p = i * 4 + w, r = p * 8 + lrow;
+      const int gr = min(m0 + r, M - 1);
+      const bf16_t* src = A + (long long)gr * lda + k0 + ((lchk ^ ((r >> 1) & 7)) << 3);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(dst + p * 8 * BK), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+      const int p = i * 4 + w, r = p * 8 + lrow;
+      const int gr = min(n0 + r, N - 1);
+      const bf16_t* src = W + (long long)gr * ldw + k0 + ((lchk ^ ((r >> 1) & 7)) << 3);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(dst + BM * BK + p * 8 * BK), 16, 0, 0);
+    }
+  };
+  issue(0);
+  issue(1);
+  issue(2);
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int kt = 0; kt < nk; ++kt) {
+    // this wave's pieces of step kt landed (steps kt+1, kt+2 stay in flight);
+    // the barrier publishes every wave's pieces and retires step kt-1's reads
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GPS) : "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue(min(kt + 3, nk - 1));  // into slot (kt+3)%NB = (kt-1)%NB
+    const bf16_t* As = ring + (kt % NB) * SLOT;
+    const bf16_t* Bs = As + BM * BK;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm * WM + i * 16 + fr;
+        fa[i] = *reinterpret_cast<const bf16x8*>(As + r * BK + (((ks * 4 + g) ^ ((r >> 1) & 7)) << 3));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = wn * WN + j * 16 + fr;
+        fb[j] = *reinterpret_cast<const bf16x8*>(Bs + r * BK + (((ks * 4 + g) ^ ((r >> 1) & 7)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail re-loads
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  constexpr int CR = BN + 4;
+  float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(wm * WM + i * 16 + 4 * g + r) * CR + wn * WN + j * 16 + fr] = acc[i][j][r];
+  __syncthreads();
+  store_ctile<BM, BN, NT>(Cs, ep, m0, n0, M, N, tid);
+}
+
+template <int BM, int BN>
+int launch_ring(const void* A, int lda, const void* W, int ldw, int M, int N, int K, const Epi& ep, hipStream_t s) {
+  size_t lds = (size_t)4 * (BM + BN) * 64 * sizeof(bf16_t);
+  const size_t cbytes = (size_t)BM * (BN + 4) * 4;
+  if (cbytes > lds) lds = cbytes;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_ring_kernel<BM, BN>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_ring_kernel<BM, BN>), dim3(grid), dim3(256), lds, s, reinterpret_cast<const bf16_t*>(A),
+                     lda, reinterpret_cast<const bf16_t*>(W), ldw, M, N, K, ep);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int V>
+struct IntC {
+  static constexpr int value = V;
+};
+
+// Deep-prefetch GEMM (bf16): the register-staged double-buffered LDS tile of
+// gemm_kernel, but with NPRE = 4 register stages in flight, so a K step's
+// global loads were issued 3 steps before they are stored to LDS.  At the
+// encoder's K = 256 all of K is requested up front; the shallow pipeline of
+// gemm_kernel (load k+1 while computing k) left every step waiting one full
+// L2/HBM latency.  Loads are unconditional (rows and K clamp; a ragged K tail
+// is zeroed after the load) so the compiler's vmcnt waits stay counted.
+template <int BM, int BN, int BK>
+__global__ void __launch_bounds__(256) gemm_pf_kernel(const bf16_t* __restrict__ A, int lda,
+                                                      const bf16_t* __restrict__ W, int ldw, int M, int N, int K,
+                                                      Epi ep) {
+  constexpr int NT = 256, LDSR = BK + 16;
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  constexpr int CPR = BK / 8, ACH = BM * CPR / NT, BCH = BN * CPR / NT, CH = ACH + BCH;
+  static_assert(ACH >= 1 && BCH >= 1 && ACH * NT == BM * CPR && BCH * NT == BN * CPR, "tile");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* Bs = As + 2 * BM * LDSR;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int ntn = (N + BN - 1) / BN;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int tile_id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int m0 = (tile_id / ntn) * BM;
+  const int n0 = (tile_id % ntn) * BN;
+  const int nk = (K + BK - 1) / BK;
+
+  auto gload = [&](int kt, u32x4 (&rs)[CH]) __attribute__((always_inline)) {
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const bool isA = i < ACH;
+      const int c = tid + (isA ? i : i - ACH) * NT, r = c / CPR, kc = (c % CPR) * 8;
+      const int gk = k0 + kc;
+      const bf16_t* src = isA ? A + (long long)min(m0 + r, M - 1) * lda : W + (long long)min(n0 + r, N - 1) * ldw;
+      u32x4 v = *reinterpret_cast<const u32x4*>(src + min(gk, K - 8));
+      rs[i] = gk < K ? v : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  auto sstore = [&](int buf, const u32x4 (&rs)[CH]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const bool isA = i < ACH;
+      const int c = tid + (isA ? i : i - ACH) * NT, r = c / CPR, kc = (c % CPR) * 8;
+      bf16_t* dst = isA ? As + buf * BM * LDSR : Bs + buf * BN * LDSR;
+      *reinterpret_cast<u32x4*>(dst + r * LDSR + kc) = rs[i];
+    }
+  };
+  u32x4 s0[CH], s1[CH], s2[CH], s3[CH];
+  auto sset = [&](auto U) -> u32x4(&)[CH] {
+    constexpr int u = decltype(U)::value & 3;
+    if constexpr (u == 0) return s0;
+    else if constexpr (u == 1) return s1;
+    else if constexpr (u == 2) return s2;
+    else return s3;
+  };
+  gload(0, s0);
+  gload(min(1, nk - 1), s1);
+  gload(min(2, nk - 1), s2);
+  gload(min(3, nk - 1), s3);
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  sstore(0, s0);
+  __syncthreads();
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  auto step = [&](int kt, auto U) __attribute__((always_inline)) {
+    constexpr int u = decltype(U)::value;
+    const bf16_t* as = As + (kt & 1) * BM * LDSR + (wm * WM + fr) * LDSR + fk;
+    const bf16_t* bs = Bs + (kt & 1) * BN * LDSR + (wn * WN + fr) * LDSR + fk;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(as + i * 16 * LDSR + ks * 32);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(bs + j * 16 * LDSR + ks * 32);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    sstore((kt + 1) & 1, sset(IntC<u + 1>{}));   // tile kt+1 (requested 3 steps ago; a dummy past the end)
+    gload(min(kt + 4, nk - 1), sset(U));          // this set's tile kt is in LDS already
+    __syncthreads();
+  };
+  for (int kt0 = 0; kt0 < nk; kt0 += 4) {
+    step(kt0, IntC<0>{});
+    if (kt0 + 1 < nk) step(kt0 + 1, IntC<1>{});
+    if (kt0 + 2 < nk) step(kt0 + 2, IntC<2>{});
+    if (kt0 + 3 < nk) step(kt0 + 3, IntC<3>{});
+  }
+
+  constexpr int CR = BN + 4;
+  float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(wm * WM + i * 16 + 4 * (lane >> 4) + r) * CR + wn * WN + j * 16 + fr] = acc[i][j][r];
+  __syncthreads();
+  store_ctile<BM, BN, NT>(Cs, ep, m0, n0, M, N, tid);
+}
+
+template <int BM, int BN, int BK>
+int launch_pf(const void* A, int lda, const void* W, int ldw, int M, int N, int K, const Epi& ep, hipStream_t s) {
+  size_t lds = (size_t)2 * (BM + BN) * (BK + 16) * sizeof(bf16_t);
+  const size_t cbytes = (size_t)BM * (BN + 4) * 4;
+  if (cbytes > lds) lds = cbytes;
+  const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_pf_kernel<BM, BN, BK>), dim3(grid), dim3(256), lds, s, reinterpret_cast<const bf16_t*>(A),
+                     lda, reinterpret_cast<const bf16_t*>(W), ldw, M, N, K, ep);
   SBK_CHECK_LAUNCH();
   return 0;
 }
@@ -256,7 +618,7 @@ SBK_API int sbk_gemm(int dtype_bf16, const void* A, int lda, const void* W, int 
   if (act == ACT_GLU && (N % 32)) return SBK_ERR_ARG;  // whole [a16|gate16] groups
   Epi ep{bias, act, slope, res, ldr, alpha, rowmask, out, ldc, out_bf16};
   hipStream_t s = (hipStream_t)stream;
-  if (tile == 0) tile = (dtype_bf16 && K <= 256 && N >= 512) ? 9 : 2;  // measured best (scripts/kbench.py)
+  if (tile == 0) tile = 2;  // measured best for every encoder shape (scripts/kbench.py gemm)
   if (dtype_bf16) {
     switch (tile) {
       case 1: return launch<bf16_t, 128, 128, 64>(A, lda, W, ldw, M, N, K, ep, s);
@@ -268,6 +630,22 @@ SBK_API int sbk_gemm(int dtype_bf16, const void* A, int lda, const void* W, int 
       case 8: return launch<bf16_t, 64, 64, 128, 2>(A, lda, W, ldw, M, N, K, ep, s);
       case 9: return launch<bf16_t, 64, 64, 32, 2>(A, lda, W, ldw, M, N, K, ep, s);
       case 10: return launch<bf16_t, 128, 64, 32, 2>(A, lda, W, ldw, M, N, K, ep, s);
+      case 18: return launch_pf<64, 64, 64>(A, lda, W, ldw, M, N, K, ep, s);
+      case 19: return launch_pf<128, 64, 64>(A, lda, W, ldw, M, N, K, ep, s);
+      case 20: return launch_pf<64, 128, 64>(A, lda, W, ldw, M, N, K, ep, s);
+      case 21: return launch_pf<128, 128, 64>(A, lda, W, ldw, M, N, K, ep, s);
+      case 22: return launch_pf<64, 64, 32>(A, lda, W, ldw, M, N, K, ep, s);
+      case 14: return launch<bf16_t, 64, 256, 32, 2>(A, lda, W, ldw, M, N, K, ep, s);
+      case 15: return launch<bf16_t, 64, 256, 64, 2>(A, lda, W, ldw, M, N, K, ep, s);
+      case 16: return launch<bf16_t, 32, 256, 64, 2>(A, lda, W, ldw, M, N, K, ep, s);
+      case 17: return launch<bf16_t, 64, 128, 32, 2>(A, lda, W, ldw, M, N, K, ep, s);
+      case 11: case 12: case 13: {
+        // LDS-DMA ring: K % 64 == 0, K >= 192, 16-B aligned rows
+        if ((K % 64) || K < 192 || (lda % 8) || (ldw % 8)) return SBK_ERR_ARG;
+        if (tile == 11) return launch_ring<128, 128>(A, lda, W, ldw, M, N, K, ep, s);
+        if (tile == 12) return launch_ring<128, 64>(A, lda, W, ldw, M, N, K, ep, s);
+        return launch_ring<64, 64>(A, lda, W, ldw, M, N, K, ep, s);
+      }
       default: return launch<bf16_t, 64, 64, 64>(A, lda, W, ldw, M, N, K, ep, s);
     }
   }

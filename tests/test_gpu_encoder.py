@@ -46,6 +46,31 @@ def test_gemm_vs_torch(dev, dtype, M, N, K):
     assert_close(out.float(), r3, rtol=tol if dtype == torch.float32 else 1e-2, name="gelu+mask")
 
 
+@pytest.mark.parametrize("tile", [11, 12, 13, 18, 19, 20, 21, 22])
+@pytest.mark.parametrize("M,N,K", [(12032, 768, 256), (1000, 320, 1024), (77, 64, 192), (12032, 512, 640), (300, 96, 200)])
+def test_gemm_ring_tiles_vs_torch(dev, tile, M, N, K):
+    """LDS-DMA ring GEMM (bf16) at every tile shape, incl. ragged M and N, with
+    the fused epilogues (bias + Swish + residual, GLU pairs)."""
+    from speechbrain_amd import _enc
+    g = torch.Generator().manual_seed(M + N + K + tile)
+    a = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) / math.sqrt(K)
+    bias = torch.randn(N, generator=g)
+    res = torch.randn(M, N, generator=g)
+    ad, wd = a.to(dev, torch.bfloat16), w.to(dev, torch.bfloat16)
+    ref = ad.float().cpu() @ wd.float().cpu().t()
+    if K % 64 and tile in (11, 12, 13):
+        pytest.skip("LDS-DMA ring needs K % 64 == 0")
+    out = _enc.gemm(ad, wd, tile=tile)
+    assert_close(out, ref, rtol=2e-3, name="plain")
+    out = _enc.gemm(ad, wd, bias=bias.to(dev), act="swish", res=res.to(dev), alpha=0.5, tile=tile)
+    assert_close(out, res + 0.5 * F.silu(ref + bias), rtol=2e-3, name="swish+res")
+    if N % 32 == 0:
+        gl = _enc.gemm(ad, wd, bias=bias.to(dev), act="glu", tile=tile)
+        v = (ref + bias).view(M, N // 32, 2, 16)
+        assert_close(gl, (v[:, :, 0] * torch.sigmoid(v[:, :, 1])).reshape(M, N // 2), rtol=2e-3, name="glu")
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_gemm_glu_permutation(dev, dtype):
     from speechbrain_amd.lobes.models.transformer.Conformer import ConvolutionModule
