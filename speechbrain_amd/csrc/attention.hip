@@ -44,7 +44,10 @@ struct VLayout {  // bf16: V row-major + ds_read_tr16 ; fp32: V^T staged transpo
 
 template <typename T, int DHP>
 struct FlashLds {
-  static constexpr int PAD = MT<T>::PAD;
+  // bf16: +32 B row pad makes the 16-lane ds_read_b128 groups of the K / P
+  // fragment reads and the ds_read_b64_tr_b16 V reads conflict-free (+16 B
+  // left 2-way conflicts); fp32: +16 B
+  static constexpr int PAD = sizeof(T) == 2 ? 2 * MT<T>::PAD : MT<T>::PAD;
   static constexpr int KR = DHP + PAD;  // Ks / Ps / V(row-major) row stride
   static constexpr int VR = KC + PAD;   // Vt row stride (fp32 path)
   static constexpr size_t ks = (size_t)KC * KR * sizeof(T);
@@ -56,6 +59,12 @@ struct FlashLds {
 };
 
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+
+// component-wise select (a struct-valued ?: takes the operands' addresses and
+// sends the staging arrays to scratch)
+__device__ __forceinline__ uint4 sel4(bool c, const uint4& a) {
+  return make_uint4(c ? a.x : 0u, c ? a.y : 0u, c ? a.z : 0u, c ? a.w : 0u);
+}
 
 // A-operand fragment of V^T (rows d = dbase + (lane&15)) for keys
 // {k0 + 4g .. k0 + 4g + 3} ∪ {k0 + 16 + 4g .. +3}, read from row-major V in
@@ -119,16 +128,38 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     float qu[8], qv[8];
+    const int d0 = 32 * s + 8 * g;
+    if (vec_ok && d0 < dh) {  // 8 consecutive head dims: 16-B (bf16) / 2x16-B (fp32) loads
+      const T* qp = qkv_b + (long long)min(my_i, Tn - 1) * row3 + d0;
+      float qf[8];
+      if constexpr (sizeof(T) == 2) {
+        const uint4 q4 = *reinterpret_cast<const uint4*>(qp);
+        const uint32_t wv[4] = {q4.x, q4.y, q4.z, q4.w};
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int d = 32 * s + 8 * g + e;
-      if (my_i < Tn && d < dh) {
-        const float q = Tr::to_f32(qkv_b[(long long)my_i * row3 + d]);
-        qu[e] = q + pbu[h * dh + d];
-        qv[e] = q + pbv[h * dh + d];
+        for (int e = 0; e < 8; ++e) qf[e] = __uint_as_float((wv[e >> 1] >> (16 * (e & 1))) << 16);
       } else {
-        qu[e] = 0.f;
-        qv[e] = 0.f;
+        const float4 a4 = *reinterpret_cast<const float4*>(qp), b4 = *reinterpret_cast<const float4*>(qp + 4);
+        qf[0] = a4.x; qf[1] = a4.y; qf[2] = a4.z; qf[3] = a4.w;
+        qf[4] = b4.x; qf[5] = b4.y; qf[6] = b4.z; qf[7] = b4.w;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float q = my_i < Tn ? qf[e] : 0.f;
+        qu[e] = my_i < Tn ? q + pbu[h * dh + d0 + e] : 0.f;
+        qv[e] = my_i < Tn ? q + pbv[h * dh + d0 + e] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int d = d0 + e;
+        if (my_i < Tn && d < dh) {
+          const float q = Tr::to_f32(qkv_b[(long long)my_i * row3 + d]);
+          qu[e] = q + pbu[h * dh + d];
+          qv[e] = q + pbv[h * dh + d];
+        } else {
+          qu[e] = 0.f;
+          qv[e] = 0.f;
+        }
       }
     }
     fqu[s] = Tr::from8(qu);
@@ -146,38 +177,43 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
   // ---- staging: registers (vector path) -> LDS ----
   uint4 rk[NKC], rv[NKC], rp[NPC];
   float rm = 0.f;
+  // loads are unconditional (indices clamped into range) and out-of-range
+  // values are zeroed at commit: a predicated load would make the compiler
+  // wait for it on its own path, serialising the prefetch with the chunk math
+  bool okk[NKC], okp[NPC];
   auto fetch = [&](int j0, bool need_v) {
     const int rbase = Tn - QB - i0 + j0;
 #pragma unroll
     for (int i = 0; i < NKC; ++i) {
       const int c = tid + 256 * i, r = c / CPR, d = (c % CPR) * VEC, j = j0 + r;
-      const bool ok = j < Tn && d < dh;
-      rk[i] = ok ? *reinterpret_cast<const uint4*>(qkv_b + (long long)j * row3 + dh + d) : make_uint4(0, 0, 0, 0);
-      rv[i] = (ok && need_v) ? *reinterpret_cast<const uint4*>(qkv_b + (long long)j * row3 + 2 * dh + d)
-                             : make_uint4(0, 0, 0, 0);
+      okk[i] = j < Tn && d < dh;
+      const T* src = qkv_b + (long long)min(j, Tn - 1) * row3 + dh + min(d, dh - VEC);
+      rk[i] = *reinterpret_cast<const uint4*>(src);
+      rv[i] = *reinterpret_cast<const uint4*>(src + (need_v ? dh : 0));  // (stats pass: unused re-read of K)
     }
 #pragma unroll
     for (int i = 0; i < NPC; ++i) {
       const int c = tid + 256 * i, rr = c / CPR, d = (c % CPR) * VEC, r = rbase + rr;
-      rp[i] = (rr < PBR - 1 && r >= 0 && r <= 2 * Tn - 2 && d < dh)
-                  ? *reinterpret_cast<const uint4*>(pk_h + (long long)r * d_model + d)
-                  : make_uint4(0, 0, 0, 0);
+      okp[i] = rr < PBR - 1 && r >= 0 && r <= 2 * Tn - 2 && d < dh;
+      rp[i] = *reinterpret_cast<const uint4*>(pk_h + (long long)min(max(r, 0), 2 * Tn - 2) * d_model +
+                                              min(d, dh - VEC));
     }
     if (tid < KC) {
       const int j = j0 + tid;
-      rm = (j < Tn && !(kpm && kpm[(long long)b * Tn + j])) ? 0.f : -INFINITY;
+      rm = (j < Tn && !(kpm && kpm[(long long)b * Tn + min(j, Tn - 1)])) ? 0.f : -INFINITY;
     }
   };
   auto commit = [&](bool need_v) {
 #pragma unroll
     for (int i = 0; i < NKC; ++i) {
       const int c = tid + 256 * i, r = c / CPR, d = (c % CPR) * VEC;
-      *reinterpret_cast<uint4*>(Ks + r * KR + d) = rk[i];
+      *reinterpret_cast<uint4*>(Ks + r * KR + d) = sel4(okk[i], rk[i]);
       if (need_v) {
+        const uint4 vv = sel4(okk[i], rv[i]);
         if (TRV) {
-          *reinterpret_cast<uint4*>(Vs + r * KR + d) = rv[i];
+          *reinterpret_cast<uint4*>(Vs + r * KR + d) = vv;
         } else {
-          const T* ve = reinterpret_cast<const T*>(&rv[i]);
+          const T* ve = reinterpret_cast<const T*>(&vv);
 #pragma unroll
           for (int e = 0; e < VEC; ++e) Vs[(d + e) * VR + r] = ve[e];
         }
@@ -186,7 +222,7 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
 #pragma unroll
     for (int i = 0; i < NPC; ++i) {
       const int c = tid + 256 * i, rr = c / CPR, d = (c % CPR) * VEC;
-      *reinterpret_cast<uint4*>(Ps + rr * KR + d) = rp[i];
+      *reinterpret_cast<uint4*>(Ps + rr * KR + d) = sel4(okp[i], rp[i]);
     }
     if (tid < KC) Ms[tid] = rm;
   };
@@ -230,7 +266,9 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
     for (int ch = 0; ch < nchunk; ++ch) {
       const int j0 = ch * KC;
       const bool more = ch + 1 < nchunk;
+#ifndef SBK_PROBE_NO_STAGE
       if (vec_ok && more) fetch(j0 + KC, need_v);  // next chunk in flight during this chunk's math
+#endif
 
       // ---- S^T (keys x queries) and G^T (band rows x queries) ----
       f32x4 acc_s[4];
@@ -242,6 +280,7 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
         for (int s = 0; s < KS; ++s) Tr::mma(acc_s[t], Tr::load(a + 32 * s), fqu[s]);
       }
       const int pofs = 48 - 16 * w;
+#ifndef SBK_PROBE_NO_G
 #pragma unroll
       for (int t = 0; t < 5; ++t) {
         f32x4 acc_g = {0.f, 0.f, 0.f, 0.f};
@@ -251,7 +290,10 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
 #pragma unroll
         for (int r = 0; r < 4; ++r) Gw[(16 * t + 4 * g + r) * GS + c16] = acc_g[r];
       }
-      __syncthreads();  // G^T scratch visible to the wave's other lanes
+#endif
+      // G^T scratch is per wave: its LDS writes only need to have completed
+      // (in-order per wave) before the shifted reads, no workgroup barrier
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
       // ---- scores for this lane's query: keys jj = 16t + 4g + r ----
       float sc[4][4];
@@ -332,14 +374,23 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
               const T* vrow = Vs + (16 * t + c16) * VR + 32 * s2 + 4 * g;
               fa = Tr::load2x4(vrow, vrow + 16);
             }
+#ifndef SBK_PROBE_NO_PV
             Tr::mma(acc_o[t], fa, fp);
+#else
+            acc_o[t][0] += fa[0] + fp[0];
+#endif
           }
         }
       }
       __syncthreads();  // every wave done with this chunk's Ks / Vs / Ps / Gs
       if (more) {
+#ifdef SBK_PROBE_NO_STAGE
+        if (vec_ok) {
+        }
+#else
         if (vec_ok)
           commit(need_v);
+#endif
         else
           stage_scalar(j0 + KC, need_v);
         __syncthreads();
@@ -351,12 +402,24 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
     const float inv = PROBS ? 1.0f : 1.0f / l_run;
     T* orow = out + ((long long)b * Tn + my_i) * d_model + h * dh;
 #pragma unroll
-    for (int t = 0; t < NDT; ++t)
+    for (int t = 0; t < NDT; ++t) {
+      const int d = 16 * t + 4 * g;
+      if (vec_ok && d + 3 < dh) {  // 4 consecutive head dims: one 8-B (bf16) / 16-B (fp32) store
+        if constexpr (sizeof(T) == 2) {
+          uint2 pk2;
+          pk2.x = (uint32_t)f32_to_bf16(acc_o[t][0] * inv) | ((uint32_t)f32_to_bf16(acc_o[t][1] * inv) << 16);
+          pk2.y = (uint32_t)f32_to_bf16(acc_o[t][2] * inv) | ((uint32_t)f32_to_bf16(acc_o[t][3] * inv) << 16);
+          *reinterpret_cast<uint2*>(orow + d) = pk2;
+        } else {
+          *reinterpret_cast<float4*>(orow + d) =
+              make_float4(acc_o[t][0] * inv, acc_o[t][1] * inv, acc_o[t][2] * inv, acc_o[t][3] * inv);
+        }
+      } else {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int d = 16 * t + 4 * g + r;
-        if (d < dh) orow[d] = Tr::from_f32(acc_o[t][r] * inv);
+        for (int r = 0; r < 4; ++r)
+          if (d + r < dh) orow[d + r] = Tr::from_f32(acc_o[t][r] * inv);
       }
+    }
   }
 }
 
@@ -369,7 +432,7 @@ int launch(const void* qkv, const void* pk, const float* pbu, const float* pbv, 
   const int VEC = MT<T>::VEC;
   const int d_model = H * dh;
   const int vec_ok = (dh % VEC == 0) && (d_model % VEC == 0) &&
-                     ((reinterpret_cast<uintptr_t>(qkv) | reinterpret_cast<uintptr_t>(pk)) % 16 == 0);
+                     ((reinterpret_cast<uintptr_t>(qkv) | reinterpret_cast<uintptr_t>(pk) | reinterpret_cast<uintptr_t>(out)) % 16 == 0);
   if (probs)
     hipLaunchKernelGGL((relpos_flash_kernel<T, DHP, true>), dim3(grid), dim3(256), lds, s,
                        reinterpret_cast<const T*>(qkv), reinterpret_cast<const T*>(pk), pbu, pbv, kpm, B, Tn, H, dh,

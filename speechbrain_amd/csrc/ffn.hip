@@ -140,12 +140,12 @@ __device__ __forceinline__ void row_ln(float (&z)[T2][MT][4], float (*red)[FFN_B
 #pragma unroll
   for (int j = 0; j < T2; ++j) {
     const int d = (w * T2 + j) * 16 + 4 * g;
+    const float4 g4 = *reinterpret_cast<const float4*>(gam + d), b4 = *reinterpret_cast<const float4*>(bet + d);
+    const float gm[4] = {g4.x, g4.y, g4.z, g4.w}, bt[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float gm = gam[d + e], bt = bet[d + e];
+    for (int e = 0; e < 4; ++e)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) z[j][mt][e] = (z[j][mt][e] - mean[mt]) * rstd[mt] * gm + bt;
-    }
+      for (int mt = 0; mt < MT; ++mt) z[j][mt][e] = (z[j][mt][e] - mean[mt]) * rstd[mt] * gm[e] + bt[e];
   }
 }
 
@@ -160,8 +160,9 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   constexpr int NB = 3;                      // ring slots (2 tiles in flight + 1 being read)
   constexpr int TROWS = 256;                 // rows per weight tile (HC for W1, D for W2)
   constexpr int GL = TROWS * BK * 2 / 16 / NT;  // LDS-DMA instructions per thread per tile (8)
-  constexpr int PER = D / 64;                // LN: floats per lane
-  static_assert(D == 256 && HC / 16 / NW == T && D / 16 / NW == T, "shape");
+  constexpr int PER = D / 64;                // LN: floats per lane (4)
+  static_assert(PER == 4 && D == 256 && HC / 16 / NW == T && D / 16 / NW == T, "shape");
+  static_assert(T == 1, "epilogue residual layout assumes one 16-unit tile per wave");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* ring = reinterpret_cast<bf16_t*>(smem);          // NB x TROWS x BK (linear 128-B rows)
@@ -175,49 +176,35 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   const int m0 = blockIdx.x * BM;
   const int S = (a.H / HC) * SPC;
 
-  // ---- prologue: LayerNorm of the workgroup's rows -> Xn (bf16); b1 -> LDS
-  for (int rr = w; rr < BM; rr += NW) {
-    const int row = m0 + rr;
-    float v[PER];
-    if (row < a.M) {
-      const float* xr = a.x + (long long)row * D + lane * PER;
+  // ---- prologue.  Every HBM read of the launch is issued here, before the
+  // weight stream: the residual x values of this lane's epilogue outputs
+  // (held in VGPRs through the main loop; rows clamped, masked at the end) and
+  // the x rows of the LayerNorm, so their latency overlaps the first weight
+  // tiles instead of being paid again after the last MFMA.
+  constexpr int NRW = (BM + NW - 1) / NW;    // LN rows per wave
+  float4 xres[MT];
 #pragma unroll
-      for (int i = 0; i < PER; i += 4) {
-        const float4 t4 = *reinterpret_cast<const float4*>(xr + i);
-        v[i] = t4.x; v[i + 1] = t4.y; v[i + 2] = t4.z; v[i + 3] = t4.w;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < PER; ++i) v[i] = 0.f;
-    }
-    float sm = 0.f;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) sm += v[i];
-    const float mean = wave_sum(sm) / D;
-    float q = 0.f;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) q += (v[i] - mean) * (v[i] - mean);
-    const float rstd = 1.0f / sqrtf(wave_sum(q) / D + a.eps0);
-    bf16_t* xo = Xn + rr * XS + lane * PER;
-#pragma unroll
-    for (int i = 0; i < PER; i += 4) {
-      const int c = lane * PER + i;
-      uint2 pk;
-      pk.x = (uint32_t)f32_to_bf16((v[i] - mean) * rstd * a.g0[c] + a.b0[c]) |
-             ((uint32_t)f32_to_bf16((v[i + 1] - mean) * rstd * a.g0[c + 1] + a.b0[c + 1]) << 16);
-      pk.y = (uint32_t)f32_to_bf16((v[i + 2] - mean) * rstd * a.g0[c + 2] + a.b0[c + 2]) |
-             ((uint32_t)f32_to_bf16((v[i + 3] - mean) * rstd * a.g0[c + 3] + a.b0[c + 3]) << 16);
-      *reinterpret_cast<uint2*>(xo + i) = pk;
-    }
+  for (int mt = 0; mt < MT; ++mt) {
+    const int row = min(m0 + mt * 16 + fr, a.M - 1);
+    xres[mt] = *reinterpret_cast<const float4*>(a.x + (long long)row * D + w * 16 + 4 * g);
   }
-  for (int i = tid; i < a.H; i += NT) b1s[i] = a.b1[i];
-
+  float4 xv[NRW];
+#pragma unroll
+  for (int i = 0; i < NRW; ++i) {
+    const int rr = w + i * NW, row = min(m0 + rr, a.M - 1);
+    xv[i] = *reinterpret_cast<const float4*>(a.x + (long long)row * D + lane * PER);
+  }
+  const float4 g04 = *reinterpret_cast<const float4*>(a.g0 + lane * PER);
+  const float4 b04 = *reinterpret_cast<const float4*>(a.b0 + lane * PER);
   // ---- weight tile s -> ring slot (LDS-DMA, 1 KB = 8 rows per wave-instruction)
   // lane L of instruction i writes row R0 + L/8, 16-B chunk L%8 (linear image)
   // and fetches source chunk (L%8) ^ ((row >> 1) & 7): the read side applies
   // the same involution.
   const int lrow = lane >> 3, lchk = lane & 7;
   auto issue = [&](int s, int slot) __attribute__((always_inline)) {
+#ifdef SBK_PROBE_NO_DMA
+    if (s >= 0) return;
+#endif
     const int c = s / SPC, r = s - c * SPC;
     const bool p1 = r < K1;
     const bf16_t* base = p1 ? a.w1 + (long long)c * HC * D + r * BK : a.w2 + c * HC + (r - K1) * BK;
@@ -234,6 +221,27 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   };
   issue(0, 0);
   issue(1, 1);
+
+  // LayerNorm of the workgroup's rows -> Xn (bf16); b1 -> LDS
+#pragma unroll
+  for (int i = 0; i < NRW; ++i) {
+    const int rr = w + i * NW;
+    if (rr >= BM) break;
+    const bool live = m0 + rr < a.M;
+    const float v[4] = {live ? xv[i].x : 0.f, live ? xv[i].y : 0.f, live ? xv[i].z : 0.f, live ? xv[i].w : 0.f};
+    const float mean = wave_sum(v[0] + v[1] + v[2] + v[3]) / D;
+    float q = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) q += (v[e] - mean) * (v[e] - mean);
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / D + a.eps0);
+    uint2 pk;
+    pk.x = (uint32_t)f32_to_bf16((v[0] - mean) * rstd * g04.x + b04.x) |
+           ((uint32_t)f32_to_bf16((v[1] - mean) * rstd * g04.y + b04.y) << 16);
+    pk.y = (uint32_t)f32_to_bf16((v[2] - mean) * rstd * g04.z + b04.z) |
+           ((uint32_t)f32_to_bf16((v[3] - mean) * rstd * g04.w + b04.w) << 16);
+    *reinterpret_cast<uint2*>(Xn + rr * XS + lane * PER) = pk;
+  }
+  for (int i = tid; i < a.H; i += NT) b1s[i] = a.b1[i];
 
   f32x4 acc1[T][MT], acc2[T][MT];
 #pragma unroll
@@ -253,6 +261,9 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     // slot (s+2)%NB was last read in step s-1: refill (tail: a harmless reload of the last tile)
     issue(min(s + 2, S - 1), (s + 2) % NB);
     const bf16_t* tile = ring + (s % NB) * TROWS * BK;
+#ifdef SBK_PROBE_NO_MFMA
+    if (r >= 0) continue;
+#endif
     if (r < K1) {
 #pragma unroll
       for (int ks = 0; ks < BK / 32; ++ks) {
@@ -313,6 +324,9 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the tail reloads
 
   // ---- epilogue: lane holds rows m = mt*16 + fr, units d = (w*T + j)*16 + 4g .. +3
+#ifdef SBK_PROBE_NO_EPI
+  if (acc2[0][0][0] != 12345.f) return;
+#endif
   constexpr int T2 = T;
   float z[T2][MT][4];
 #pragma unroll
@@ -321,9 +335,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     const float4 bb = *reinterpret_cast<const float4*>(a.b2 + d);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      const int row = m0 + mt * 16 + fr;
-      float4 xr = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (row < a.M) xr = *reinterpret_cast<const float4*>(a.x + (long long)row * D + d);
+      const float4 xr = xres[mt];
       z[j][mt][0] = xr.x + a.alpha * (acc2[j][mt][0] + bb.x);
       z[j][mt][1] = xr.y + a.alpha * (acc2[j][mt][1] + bb.y);
       z[j][mt][2] = xr.z + a.alpha * (acc2[j][mt][2] + bb.z);
@@ -398,6 +410,14 @@ SBK_API int sbk_ffn(const float* x, int M, int D, int H, const float* g0, const 
                     const float* bn, float epsn, void* u, int u_bf16, void* stream) {
   if (M <= 0 || !sbk_ffn_supported(D, H) || !g0 || !b0 || !w1 || !b1 || !w2 || !b2 || !out) return SBK_ERR_ARG;
   if (act == ACT_GLU || (gn && !u)) return SBK_ERR_ARG;
+  // float4 loads of rows and LayerNorm parameters
+  const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(g0) |
+                       reinterpret_cast<uintptr_t>(b0) | reinterpret_cast<uintptr_t>(b1) |
+                       reinterpret_cast<uintptr_t>(b2) | reinterpret_cast<uintptr_t>(gp) |
+                       reinterpret_cast<uintptr_t>(bp) | reinterpret_cast<uintptr_t>(out) |
+                       reinterpret_cast<uintptr_t>(gn) | reinterpret_cast<uintptr_t>(bn) |
+                       reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(w1) | reinterpret_cast<uintptr_t>(w2);
+  if (al & 15) return SBK_ERR_ARG;
   FfnArgs a;
   a.x = x; a.M = M; a.H = H;
   a.g0 = g0; a.b0 = b0; a.eps0 = eps0;
