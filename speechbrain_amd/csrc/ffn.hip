@@ -202,7 +202,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   // the same involution.
   const int lrow = lane >> 3, lchk = lane & 7;
   auto issue = [&](int s, int slot) __attribute__((always_inline)) {
-#ifdef SBK_PROBE_NO_DMA
+#if defined(SBK_PROBE_NO_DMA) || defined(SBK_PROBE_SKEL)
     if (s >= 0) return;
 #endif
     const int c = s / SPC, r = s - c * SPC;
@@ -261,41 +261,50 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     // slot (s+2)%NB was last read in step s-1: refill (tail: a harmless reload of the last tile)
     issue(min(s + 2, S - 1), (s + 2) % NB);
     const bf16_t* tile = ring + (s % NB) * TROWS * BK;
-#ifdef SBK_PROBE_NO_MFMA
+#if defined(SBK_PROBE_NO_MFMA) || defined(SBK_PROBE_SKEL)
     if (r >= 0) continue;
 #endif
     if (r < K1) {
+      // all fragments of the step are read before the first MFMA (one lgkmcnt drain)
+      bf16x8 fw[BK / 32][T], fx[BK / 32][MT];
 #pragma unroll
       for (int ks = 0; ks < BK / 32; ++ks) {
-        bf16x8 fw[T], fx[MT];
 #pragma unroll
         for (int t = 0; t < T; ++t) {
           const int row = w * (T * 16) + t * 16 + fr;
-          fw[t] = ld8(tile + row * BK + (((ks * 4 + g) ^ ((row >> 1) & 7)) << 3));
+          fw[ks][t] = ld8(tile + row * BK + (((ks * 4 + g) ^ ((row >> 1) & 7)) << 3));
         }
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) fx[mt] = ld8(Xn + (mt * 16 + fr) * XS + r * BK + ks * 32 + fk);
+        for (int mt = 0; mt < MT; ++mt) fx[ks][mt] = ld8(Xn + (mt * 16 + fr) * XS + r * BK + ks * 32 + fk);
+      }
+#pragma unroll
+      for (int ks = 0; ks < BK / 32; ++ks)
 #pragma unroll
         for (int t = 0; t < T; ++t)
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
-            acc1[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[t], fx[mt], acc1[t][mt], 0, 0, 0);
-      }
+            acc1[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ks][t], fx[ks][mt], acc1[t][mt], 0, 0, 0);
       if (r == K1 - 1) {
         // hidden chunk -> +b1, act -> Hs (4 consecutive units per lane, one 8-B store);
         // phase 2 reads it after the next step's barrier
 #pragma unroll
         for (int t = 0; t < T; ++t) {
           const int n = w * (T * 16) + t * 16 + 4 * g;
-          const float4 bb = *reinterpret_cast<const float4*>(b1s + c * HC + n);
+          // b1 from LDS by an explicit ds_read: a compiler-visible LDS (or global)
+          // read here makes it drain the in-flight LDS-DMA weight tiles (vmcnt(0))
+          f32x4 bb;
+          {
+            const uint32_t la = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)(b1s + c * HC + n));
+            asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(bb) : "v"(la) : "memory");
+          }
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
             const f32x4 v = acc1[t][mt];
             uint2 pk;
-            pk.x = (uint32_t)f32_to_bf16(act_fn(v[0] + bb.x, a.act, a.slope)) |
-                   ((uint32_t)f32_to_bf16(act_fn(v[1] + bb.y, a.act, a.slope)) << 16);
-            pk.y = (uint32_t)f32_to_bf16(act_fn(v[2] + bb.z, a.act, a.slope)) |
-                   ((uint32_t)f32_to_bf16(act_fn(v[3] + bb.w, a.act, a.slope)) << 16);
+            pk.x = (uint32_t)f32_to_bf16(act_fn(v[0] + bb[0], a.act, a.slope)) |
+                   ((uint32_t)f32_to_bf16(act_fn(v[1] + bb[1], a.act, a.slope)) << 16);
+            pk.y = (uint32_t)f32_to_bf16(act_fn(v[2] + bb[2], a.act, a.slope)) |
+                   ((uint32_t)f32_to_bf16(act_fn(v[3] + bb[3], a.act, a.slope)) << 16);
             *reinterpret_cast<uint2*>(Hs + (mt * 16 + fr) * HS + n) = pk;
             acc1[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
           }
@@ -303,29 +312,38 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
       }
     } else {
       const int kk = (r - K1) * BK;
+      bf16x8 fw[BK / 32][T], fh[BK / 32][MT];
 #pragma unroll
       for (int ks = 0; ks < BK / 32; ++ks) {
-        bf16x8 fw[T], fh[MT];
 #pragma unroll
         for (int t = 0; t < T; ++t) {
           const int row = w * (T * 16) + t * 16 + fr;
-          fw[t] = ld8(tile + row * BK + (((ks * 4 + g) ^ ((row >> 1) & 7)) << 3));
+          fw[ks][t] = ld8(tile + row * BK + (((ks * 4 + g) ^ ((row >> 1) & 7)) << 3));
         }
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) fh[mt] = ld8(Hs + (mt * 16 + fr) * HS + kk + ks * 32 + fk);
+        for (int mt = 0; mt < MT; ++mt) fh[ks][mt] = ld8(Hs + (mt * 16 + fr) * HS + kk + ks * 32 + fk);
+      }
+#pragma unroll
+      for (int ks = 0; ks < BK / 32; ++ks)
 #pragma unroll
         for (int t = 0; t < T; ++t)
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
-            acc2[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[t], fh[mt], acc2[t][mt], 0, 0, 0);
-      }
+            acc2[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ks][t], fh[ks][mt], acc2[t][mt], 0, 0, 0);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the tail reloads
 
   // ---- epilogue: lane holds rows m = mt*16 + fr, units d = (w*T + j)*16 + 4g .. +3
 #ifdef SBK_PROBE_NO_EPI
-  if (acc2[0][0][0] != 12345.f) return;
+  {
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < T; ++j)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) t += acc2[j][mt][0] + acc2[j][mt][1] + acc2[j][mt][2] + acc2[j][mt][3];
+    if (t != 12345.f) return;
+  }
 #endif
   constexpr int T2 = T;
   float z[T2][MT][4];
