@@ -20,7 +20,8 @@
 //              full rows (cross-wave reduction through LDS), float4 stores.
 // Weight tiles (256 rows x 64 k = 32 KB) stream L2 -> LDS by LDS-DMA
 // (global_load_lds_dwordx4: full 128-B lines, no VGPRs) into a 3-slot ring,
-// two tiles in flight across one raw barrier per K-step (counted vmcnt).
+// two tiles in flight (counted vmcnt).  Each wave stages only the weight rows it
+// multiplies, so the ring steps need no workgroup barrier.
 // The ring image is lane-linear; bank conflicts are removed by XOR-swizzling
 // the 16-B chunk index with (row >> 1) & 7 on the global source address and
 // on the fragment reads.  Per workgroup the 2·D·H weight bytes cross L2 once;
@@ -30,7 +31,9 @@
 // stream, not MFMA (~12 % busy) or HBM, sets the time.
 // Tried and slower: 8-wave register-staged ring (48 us), 4 waves (69 us),
 // fragment-shaped loads straight to VGPRs (64 us), row-owner waves with the
-// hidden chunk in registers (78 us); 16 waves here: 42 us (M = 12032).
+// hidden chunk in registers (78 us).  A shared 3-slot ring with a barrier per
+// K-step took 42 us; wave-private rows (no per-step barrier), a 2-slot ring
+// and chunk-parity Hs: 35 us (M = 12032, H = 1024; 8 waves the same).
 #include "mfma.h"
 
 using namespace sbk;
@@ -62,12 +65,22 @@ struct FfnArgs {
 
 __device__ __forceinline__ bf16x8 ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
-constexpr int FFN_BM = 48, FFN_NW = 16, FFN_NT = FFN_NW * 64;
+template <int V>
+struct IntC {
+  static constexpr int value = V;
+};
 
-__device__ __forceinline__ float act_fn(float v, int act, float slope) {
-  if (act == ACT_SWISH) return v * (1.0f / (1.0f + __expf(-v)));
-  if (act == ACT_LRELU) return v >= 0.f ? v : v * slope;
-  if (act == ACT_GELU) return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+constexpr int FFN_BM = 48;
+#ifndef SBK_FFN_NW
+#define SBK_FFN_NW 16
+#endif
+constexpr int FFN_NW = SBK_FFN_NW, FFN_NT = FFN_NW * 64;
+
+template <int ACT>
+__device__ __forceinline__ float act_fn(float v, float slope) {
+  if (ACT == ACT_SWISH) return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));  // bf16 hidden: approx rcp
+  if (ACT == ACT_LRELU) return v >= 0.f ? v : v * slope;
+  if (ACT == ACT_GELU) return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
   return v;
 }
 
@@ -149,7 +162,20 @@ __device__ __forceinline__ void row_ln(float (&z)[T2][MT][4], float (*red)[FFN_B
   }
 }
 
-template <int D>
+#ifdef SBK_PROBE_TL
+// probe build only: s_memtime timeline of 4 waves (wg 0 wave 0, wg 0 last wave, wg 128, wg 250)
+__device__ unsigned long long g_ffn_tl[16][80];
+#define FFN_TL(i)                                                                 \
+  do {                                                                            \
+    if (tl_rec >= 0 && lane == 0) g_ffn_tl[tl_rec][i] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define FFN_TL(i) \
+  do {            \
+  } while (0)
+#endif
+
+template <int D, int ACT>
 __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   constexpr int BM = FFN_BM, HC = 256, NW = FFN_NW, NT = FFN_NT;
   constexpr int XS = D + 16, HS = HC + 16;   // LDS row strides (elements), +32 B pad: conflict-free b128 reads
@@ -157,24 +183,28 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   constexpr int T = 256 / 16 / FFN_NW;       // 16-row weight tiles per wave (HC/16/NW = D/16/NW)
   constexpr int BK = 64;                     // K per step: one 128-B line per weight row
   constexpr int K1 = D / BK, K2 = HC / BK, SPC = K1 + K2;
-  constexpr int NB = 3;                      // ring slots (2 tiles in flight + 1 being read)
+  constexpr int NB = 2;                      // ring slots: a slot is refilled as soon as its fragments are in VGPRs
   constexpr int TROWS = 256;                 // rows per weight tile (HC for W1, D for W2)
-  constexpr int GL = TROWS * BK * 2 / 16 / NT;  // LDS-DMA instructions per thread per tile (8)
+  constexpr int GL = TROWS * BK * 2 / 16 / NT;  // LDS-DMA instructions per thread per tile (2)
+  static_assert(GL * 8 == T * 16, "each wave stages exactly the weight rows it multiplies");
   constexpr int PER = D / 64;                // LN: floats per lane (4)
   static_assert(PER == 4 && D == 256 && HC / 16 / NW == T && D / 16 / NW == T, "shape");
-  static_assert(T == 1, "epilogue residual layout assumes one 16-unit tile per wave");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* ring = reinterpret_cast<bf16_t*>(smem);          // NB x TROWS x BK (linear 128-B rows)
   bf16_t* Xn = ring + NB * TROWS * BK;                      // BM x XS
   bf16_t* Hs = Xn + BM * XS;                                // BM x HS
-  float* b1s = reinterpret_cast<float*>(Hs + BM * HS);      // H
+  float* b1s = reinterpret_cast<float*>(Hs + 2 * BM * HS);  // H          (Hs: 2 x BM x HS, chunk parity)
   float (*red)[BM] = reinterpret_cast<float (*)[BM]>(b1s + a.H);  // NW x BM
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int fr = lane & 15, g = lane >> 4, fk = 8 * g;
   const int m0 = blockIdx.x * BM;
   const int S = (a.H / HC) * SPC;
+#ifdef SBK_PROBE_TL
+  const int tl_rec = blockIdx.x == 128 ? w : -1;
+#endif
+  FFN_TL(0);
 
   // ---- prologue.  Every HBM read of the launch is issued here, before the
   // weight stream: the residual x values of this lane's epilogue outputs
@@ -182,12 +212,14 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   // the x rows of the LayerNorm, so their latency overlaps the first weight
   // tiles instead of being paid again after the last MFMA.
   constexpr int NRW = (BM + NW - 1) / NW;    // LN rows per wave
-  float4 xres[MT];
+  float4 xres[T][MT];
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int row = min(m0 + mt * 16 + fr, a.M - 1);
-    xres[mt] = *reinterpret_cast<const float4*>(a.x + (long long)row * D + w * 16 + 4 * g);
-  }
+  for (int j = 0; j < T; ++j)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int row = min(m0 + mt * 16 + fr, a.M - 1);
+      xres[j][mt] = *reinterpret_cast<const float4*>(a.x + (long long)row * D + (w * T + j) * 16 + 4 * g);
+    }
   float4 xv[NRW];
 #pragma unroll
   for (int i = 0; i < NRW; ++i) {
@@ -212,7 +244,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     bf16_t* dst = ring + slot * TROWS * BK;
 #pragma unroll
     for (int i = 0; i < GL; ++i) {
-      const int r0 = (i * NW + w) * 8;
+      const int r0 = w * (T * 16) + i * 8;  // the wave's own rows: it is their only reader
       const int row = r0 + lrow;
       const bf16_t* src = base + (long long)row * ld + ((lchk ^ ((row >> 1) & 7)) << 3);
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -252,46 +284,66 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
       acc2[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 
+  // ---- main loop.  Every wave stages (LDS-DMA) and reads only its own weight
+  // rows, so the 2-slot ring needs no workgroup barrier: a slot takes tile
+  // s+2 as soon as the wave's fragments of tile s are in VGPRs.  Barriers
+  // remain only where waves share data: Xn (s == 0) and the hidden chunk Hs
+  // (written at r == K1-1, read from r == K1; double-buffered by chunk parity).
+  // (Tried and slower: fragments of step s+1 read under the MFMAs of step s —
+  // 8 waves 40.8 us, 16 waves spill; weights streamed straight into VGPRs
+  // with 4 steps in flight instead of LDS-DMA — 45 us at 8 or 16 waves.)
+  FFN_TL(1);
   for (int s = 0; s < S; ++s) {
     const int c = s / SPC, r = s - c * SPC;
-    // tile s landed (tile s+1 stays in flight), LDS writes of step s-1 done
+    // this wave's rows of tile s landed (tile s+1 stays in flight)
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    // slot (s+2)%NB was last read in step s-1: refill (tail: a harmless reload of the last tile)
-    issue(min(s + 2, S - 1), (s + 2) % NB);
+    if (s == 0 || r == K1) __builtin_amdgcn_s_barrier();
+    if (s < 34) FFN_TL(2 + 2 * s);
     const bf16_t* tile = ring + (s % NB) * TROWS * BK;
+    bf16_t* Hc = Hs + (c & 1) * BM * HS;  // this chunk's hidden activations
+    // once this step's fragments are in VGPRs its slot takes tile s+2
+    // (tail: a harmless reload of the last tile)
+    auto refill = [&]() __attribute__((always_inline)) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      issue(min(s + 2, S - 1), s % NB);
+    };
+    bf16x8 fw[BK / 32][T], fa[BK / 32][MT];
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const int row = w * (T * 16) + t * 16 + fr;
+        fw[ks][t] = ld8(tile + row * BK + (((ks * 4 + g) ^ ((row >> 1) & 7)) << 3));
+      }
+      const bf16_t* abase = r < K1 ? Xn + r * BK : Hc + (r - K1) * BK;
+      const int ald = r < K1 ? XS : HS;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) fa[ks][mt] = ld8(abase + (mt * 16 + fr) * ald + ks * 32 + fk);
+    }
+    refill();
 #if defined(SBK_PROBE_NO_MFMA) || defined(SBK_PROBE_SKEL)
     if (r >= 0) continue;
 #endif
     if (r < K1) {
-      // all fragments of the step are read before the first MFMA (one lgkmcnt drain)
-      bf16x8 fw[BK / 32][T], fx[BK / 32][MT];
-#pragma unroll
-      for (int ks = 0; ks < BK / 32; ++ks) {
-#pragma unroll
-        for (int t = 0; t < T; ++t) {
-          const int row = w * (T * 16) + t * 16 + fr;
-          fw[ks][t] = ld8(tile + row * BK + (((ks * 4 + g) ^ ((row >> 1) & 7)) << 3));
-        }
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) fx[ks][mt] = ld8(Xn + (mt * 16 + fr) * XS + r * BK + ks * 32 + fk);
-      }
 #pragma unroll
       for (int ks = 0; ks < BK / 32; ++ks)
 #pragma unroll
         for (int t = 0; t < T; ++t)
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
-            acc1[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ks][t], fx[ks][mt], acc1[t][mt], 0, 0, 0);
+            acc1[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ks][t], fa[ks][mt], acc1[t][mt], 0, 0, 0);
       if (r == K1 - 1) {
-        // hidden chunk -> +b1, act -> Hs (4 consecutive units per lane, one 8-B store);
-        // phase 2 reads it after the next step's barrier
+        // hidden chunk -> +b1, act -> Hc (4 consecutive units per lane, one
+        // 8-B store); phase 2 reads it after the next step's barrier.  The
+        // buffer written here was last read in chunk c-2, before every wave
+        // passed chunk c-1's r == K1 barrier.
 #pragma unroll
         for (int t = 0; t < T; ++t) {
           const int n = w * (T * 16) + t * 16 + 4 * g;
-          // b1 from LDS by an explicit ds_read: a compiler-visible LDS (or global)
-          // read here makes it drain the in-flight LDS-DMA weight tiles (vmcnt(0))
+          // b1 and Hs by explicit ds_read / ds_write: compiler-visible LDS
+          // accesses here get an s_waitcnt vmcnt(0) (alias guard against the
+          // in-flight LDS-DMA tiles), draining the weight stream
           f32x4 bb;
           {
             const uint32_t la = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)(b1s + c * HC + n));
@@ -301,38 +353,30 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
           for (int mt = 0; mt < MT; ++mt) {
             const f32x4 v = acc1[t][mt];
             uint2 pk;
-            pk.x = (uint32_t)f32_to_bf16(act_fn(v[0] + bb[0], a.act, a.slope)) |
-                   ((uint32_t)f32_to_bf16(act_fn(v[1] + bb[1], a.act, a.slope)) << 16);
-            pk.y = (uint32_t)f32_to_bf16(act_fn(v[2] + bb[2], a.act, a.slope)) |
-                   ((uint32_t)f32_to_bf16(act_fn(v[3] + bb[3], a.act, a.slope)) << 16);
-            *reinterpret_cast<uint2*>(Hs + (mt * 16 + fr) * HS + n) = pk;
+            pk.x = (uint32_t)f32_to_bf16(act_fn<ACT>(v[0] + bb[0], a.slope)) |
+                   ((uint32_t)f32_to_bf16(act_fn<ACT>(v[1] + bb[1], a.slope)) << 16);
+            pk.y = (uint32_t)f32_to_bf16(act_fn<ACT>(v[2] + bb[2], a.slope)) |
+                   ((uint32_t)f32_to_bf16(act_fn<ACT>(v[3] + bb[3], a.slope)) << 16);
+            const uint32_t la = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) bf16_t*)(Hc + (mt * 16 + fr) * HS + n));
+            const unsigned long long pv = (unsigned long long)pk.x | ((unsigned long long)pk.y << 32);
+            asm volatile("ds_write_b64 %0, %1" ::"v"(la), "v"(pv) : "memory");
             acc1[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
           }
         }
       }
     } else {
-      const int kk = (r - K1) * BK;
-      bf16x8 fw[BK / 32][T], fh[BK / 32][MT];
-#pragma unroll
-      for (int ks = 0; ks < BK / 32; ++ks) {
-#pragma unroll
-        for (int t = 0; t < T; ++t) {
-          const int row = w * (T * 16) + t * 16 + fr;
-          fw[ks][t] = ld8(tile + row * BK + (((ks * 4 + g) ^ ((row >> 1) & 7)) << 3));
-        }
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) fh[ks][mt] = ld8(Hs + (mt * 16 + fr) * HS + kk + ks * 32 + fk);
-      }
 #pragma unroll
       for (int ks = 0; ks < BK / 32; ++ks)
 #pragma unroll
         for (int t = 0; t < T; ++t)
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
-            acc2[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ks][t], fh[ks][mt], acc2[t][mt], 0, 0, 0);
+            acc2[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ks][t], fa[ks][mt], acc2[t][mt], 0, 0, 0);
     }
+    if (s < 34) FFN_TL(3 + 2 * s);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the tail reloads
+  FFN_TL(70);
 
   // ---- epilogue: lane holds rows m = mt*16 + fr, units d = (w*T + j)*16 + 4g .. +3
 #ifdef SBK_PROBE_NO_EPI
@@ -353,13 +397,14 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     const float4 bb = *reinterpret_cast<const float4*>(a.b2 + d);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      const float4 xr = xres[mt];
+      const float4 xr = xres[j][mt];
       z[j][mt][0] = xr.x + a.alpha * (acc2[j][mt][0] + bb.x);
       z[j][mt][1] = xr.y + a.alpha * (acc2[j][mt][1] + bb.y);
       z[j][mt][2] = xr.z + a.alpha * (acc2[j][mt][2] + bb.z);
       z[j][mt][3] = xr.w + a.alpha * (acc2[j][mt][3] + bb.w);
     }
   }
+  FFN_TL(71);
   if (a.gp) row_ln<D, T2, MT, NW>(z, red, a.gp, a.bp, a.epsp, w, g, fr);
   // all residual reads of x are done before out (which may alias x) is written
 #pragma unroll
@@ -394,31 +439,50 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
       }
     }
   }
+  FFN_TL(72);
 }
 
 template <int D>
 size_t ffn_lds(int H) {
-  return ((size_t)3 * 256 * 64 + (size_t)FFN_BM * (D + 16) + (size_t)FFN_BM * (256 + 16)) * sizeof(bf16_t) +
+  constexpr size_t ring = (size_t)2 * 256 * 64;
+  return (ring + (size_t)FFN_BM * (D + 16) + (size_t)2 * FFN_BM * (256 + 16)) * sizeof(bf16_t) +
          (size_t)H * 4 + (size_t)FFN_NW * FFN_BM * 4;
+}
+
+template <int D, int ACT>
+int launch_ffn_act(const FfnArgs& a, size_t lds, hipStream_t s) {
+  static bool attr = false;  // > 64 KB dynamic LDS: opt in once per kernel
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ffn_kernel<D, ACT>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((ffn_kernel<D, ACT>), dim3((a.M + FFN_BM - 1) / FFN_BM), dim3(FFN_NT), lds, s, a);
+  return 0;
 }
 
 template <int D>
 int launch_ffn(const FfnArgs& a, hipStream_t s) {
   const size_t lds = ffn_lds<D>(a.H);
   if (lds > 160 * 1024) return SBK_ERR_ARG;
-  static bool attr = false;  // > 64 KB dynamic LDS: opt in once per kernel
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ffn_kernel<D>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
-    attr = true;
+  switch (a.act) {
+    case ACT_SWISH: return launch_ffn_act<D, ACT_SWISH>(a, lds, s);
+    case ACT_LRELU: return launch_ffn_act<D, ACT_LRELU>(a, lds, s);
+    case ACT_GELU: return launch_ffn_act<D, ACT_GELU>(a, lds, s);
+    case ACT_NONE: return launch_ffn_act<D, ACT_NONE>(a, lds, s);
+    default: return SBK_ERR_ARG;
   }
-  hipLaunchKernelGGL((ffn_kernel<D>), dim3((a.M + FFN_BM - 1) / FFN_BM), dim3(FFN_NT), lds, s, a);
-  return 0;
 }
 
 
 }  // namespace
+
+#ifdef SBK_PROBE_TL
+SBK_API int sbk_probe_ffn_tl(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ffn_tl), sizeof(g_ffn_tl), 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 SBK_API int sbk_ffn_supported(int D, int H) { return D == 256 && H > 0 && H % 256 == 0 && H <= 2048; }
 
