@@ -19,3 +19,16 @@ x = torch.randn(32, 1501, 80, device=dev)
 with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
     us = timeit(lambda: cnn.run(x, torch.bfloat16), reps=20)
 print(f"frontend fused: {us:.1f}us", flush=True)
+
+if os.environ.get("SBK_PROBE_TL"):
+    import ctypes
+    import numpy as np
+    torch.cuda.synchronize()
+    buf = (ctypes.c_ulonglong * 160)()
+    assert ctypes.CDLL(_L.LIB_PATH).sbk_probe_fe_tl(buf) == 0
+    tl = np.array(buf, dtype=np.int64).reshape(10, 16)
+    t0 = tl[:, 0].min()
+    for w in range(10):
+        r = tl[w]
+        last = r[3] if r[3] else r[2]
+        print(f"w{w}: stage {r[1]-r[0]} block1 rows {r[2]-r[1]} {r[3]-r[2] if r[3] else 0} final-bar {r[11]-last} mfma {r[12]-r[11]} epi {r[13]-r[12]} total {r[13]-r[0]}")

@@ -79,6 +79,18 @@ __device__ __forceinline__ bf16x8 vt_frag_tr(const bf16_t* V, int KR, int k0, in
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
+#ifdef SBK_PROBE_TL
+__device__ unsigned long long g_att_tl[4][64];
+#define ATT_TL(i)                                                                        \
+  do {                                                                                   \
+    if (tl_on && lane == 0 && (i) < 64) g_att_tl[w][i] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define ATT_TL(i) \
+  do {            \
+  } while (0)
+#endif
+
 template <typename T, int DHP, bool PROBS>
 __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__ qkv, const T* __restrict__ pk,
                                                            const float* __restrict__ pbu,
@@ -115,6 +127,9 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
   const int bh = tile / nqb;
   const int h = bh % H, b = bh / H;
   const int i0 = qb * QB;
+#ifdef SBK_PROBE_TL
+  const bool tl_on = tile == 200 && sizeof(T) == 2 && !PROBS;
+#endif
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c16 = lane & 15, g = lane >> 4;
   const int i0w = i0 + 16 * w;
@@ -123,7 +138,9 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
   const T* pk_h = pk + h * dh;
   float* Gw = Gs + w * GR * GS;
 
-  // ---- Qu / Qv as B-operand fragments (query on the lane) ----
+  // ---- Qu / Qv as B-operand fragments (query on the lane), pre-scaled by
+  // scale * log2(e) so scores come out of the MFMAs in the exp2 domain ----
+  const float qscale = scale * 1.4426950408889634f;
   typename Tr::frag fqu[KS], fqv[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
@@ -145,8 +162,8 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float q = my_i < Tn ? qf[e] : 0.f;
-        qu[e] = my_i < Tn ? q + pbu[h * dh + d0 + e] : 0.f;
-        qv[e] = my_i < Tn ? q + pbv[h * dh + d0 + e] : 0.f;
+        qu[e] = my_i < Tn ? (q + pbu[h * dh + d0 + e]) * qscale : 0.f;
+        qv[e] = my_i < Tn ? (q + pbv[h * dh + d0 + e]) * qscale : 0.f;
       }
     } else {
 #pragma unroll
@@ -154,8 +171,8 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
         const int d = d0 + e;
         if (my_i < Tn && d < dh) {
           const float q = Tr::to_f32(qkv_b[(long long)my_i * row3 + d]);
-          qu[e] = q + pbu[h * dh + d];
-          qv[e] = q + pbv[h * dh + d];
+          qu[e] = (q + pbu[h * dh + d]) * qscale;
+          qv[e] = (q + pbv[h * dh + d]) * qscale;
         } else {
           qu[e] = 0.f;
           qv[e] = 0.f;
@@ -263,7 +280,9 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
       stage_scalar(0, need_v);
     }
     __syncthreads();
+    ATT_TL(0);
     for (int ch = 0; ch < nchunk; ++ch) {
+      ATT_TL(1 + 6 * ch);
       const int j0 = ch * KC;
       const bool more = ch + 1 < nchunk;
 #ifndef SBK_PROBE_NO_STAGE
@@ -271,31 +290,45 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
 #endif
 
       // ---- S^T (keys x queries) and G^T (band rows x queries) ----
-      f32x4 acc_s[4];
+      // per 32-wide head-dim step: all 9 fragment reads, then the 9 MFMAs;
+      // G^T goes to the scratch only after its last MFMA (no read -> MFMA ->
+      // store serialisation per tile)
+      f32x4 acc_s[4], acc_g[5];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        acc_s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const T* a = Ks + (16 * t + c16) * KR + 8 * g;
+      for (int t = 0; t < 4; ++t) acc_s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < KS; ++s) Tr::mma(acc_s[t], Tr::load(a + 32 * s), fqu[s]);
-      }
+      for (int t = 0; t < 5; ++t) acc_g[t] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int pofs = 48 - 16 * w;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        typename Tr::frag fk[4], fpb[5];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) fk[t] = Tr::load(Ks + (16 * t + c16) * KR + 8 * g + 32 * s);
 #ifndef SBK_PROBE_NO_G
 #pragma unroll
-      for (int t = 0; t < 5; ++t) {
-        f32x4 acc_g = {0.f, 0.f, 0.f, 0.f};
-        const T* a = Ps + (pofs + 16 * t + c16) * KR + 8 * g;
+        for (int t = 0; t < 5; ++t) fpb[t] = Tr::load(Ps + (pofs + 16 * t + c16) * KR + 8 * g + 32 * s);
+#endif
 #pragma unroll
-        for (int s = 0; s < KS; ++s) Tr::mma(acc_g, Tr::load(a + 32 * s), fqv[s]);
+        for (int t = 0; t < 4; ++t) Tr::mma(acc_s[t], fk[t], fqu[s]);
+#ifndef SBK_PROBE_NO_G
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Gw[(16 * t + 4 * g + r) * GS + c16] = acc_g[r];
+        for (int t = 0; t < 5; ++t) Tr::mma(acc_g[t], fpb[t], fqv[s]);
+#endif
       }
+#ifndef SBK_PROBE_NO_G
+#pragma unroll
+      for (int t = 0; t < 5; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Gw[(16 * t + 4 * g + r) * GS + c16] = acc_g[t][r];
 #endif
       // G^T scratch is per wave: its LDS writes only need to have completed
       // (in-order per wave) before the shifted reads, no workgroup barrier
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
+      ATT_TL(2 + 6 * ch);
       // ---- scores for this lane's query: keys jj = 16t + 4g + r ----
+      // (log2 domain: Qu/Qv carry scale * log2(e), probabilities are exp2)
+      const bool masked_chunk = kpm != nullptr || j0 + KC > Tn;  // uniform
       float sc[4][4];
       float cmax = -INFINITY;
 #pragma unroll
@@ -303,7 +336,8 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int jj = 16 * t + 4 * g + r;
-          const float v = (acc_s[t][r] + Gw[(15 - c16 + jj) * GS + c16]) * scale + Ms[jj];
+          float v = acc_s[t][r] + Gw[(15 - c16 + jj) * GS + c16];
+          if (masked_chunk) v += Ms[jj];
           sc[t][r] = v;
           cmax = fmaxf(cmax, v);
         }
@@ -317,10 +351,10 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) ls += __expf(sc[t][r] - mref);
+          for (int r = 0; r < 4; ++r) ls += __builtin_amdgcn_exp2f(sc[t][r] - mref);
         ls += __shfl_xor(ls, 16);
         ls += __shfl_xor(ls, 32);
-        l_run = l_run * __expf(m_run - mref) + ls;
+        l_run = l_run * __builtin_amdgcn_exp2f(m_run - mref) + ls;
         m_run = m_new;
       } else {
         float p[4][4];
@@ -333,19 +367,19 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int j = j0 + 16 * t + 4 * g + r;
-              p[t][r] = __expf(sc[t][r] - mref) * inv;
+              p[t][r] = __builtin_amdgcn_exp2f(sc[t][r] - mref) * inv;
               if (my_i < Tn && j < Tn) prow[j] = p[t][r];
             }
         } else {
           const float m_new = fmaxf(m_run, cmax);
           const float mref = m_new == -INFINITY ? 0.f : m_new;
-          const float alpha = __expf(m_run - mref);
+          const float alpha = __builtin_amdgcn_exp2f(m_run - mref);
           float ls = 0.f;
 #pragma unroll
           for (int t = 0; t < 4; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              p[t][r] = __expf(sc[t][r] - mref);
+              p[t][r] = __builtin_amdgcn_exp2f(sc[t][r] - mref);
               ls += p[t][r];
             }
           ls += __shfl_xor(ls, 16);
@@ -355,6 +389,7 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
 #pragma unroll
           for (int t = 0; t < NDT; ++t) acc_o[t] *= alpha;
         }
+        ATT_TL(3 + 6 * ch);
         // ---- O^T += V^T · P^T  (2 k-steps of 32 keys) ----
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
@@ -382,7 +417,9 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
           }
         }
       }
+      ATT_TL(4 + 6 * ch);
       __syncthreads();  // every wave done with this chunk's Ks / Vs / Ps / Gs
+      ATT_TL(5 + 6 * ch);
       if (more) {
 #ifdef SBK_PROBE_NO_STAGE
         if (vec_ok) {
@@ -397,6 +434,7 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
       }
     }
   }
+  ATT_TL(62);
   // ---- write O (row = this lane's query, cols d = 16t + 4g + r) ----
   if (my_i < Tn) {
     const float inv = PROBS ? 1.0f : 1.0f / l_run;
@@ -461,6 +499,12 @@ SBK_API int sbk_relpos_attention(int dtype_bf16, const void* qkv, const void* pk
   return dh <= 64 ? launch<float, 64>(qkv, pk, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s)
                   : launch<float, 128>(qkv, pk, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s);
 }
+
+#ifdef SBK_PROBE_TL
+SBK_API int sbk_probe_att_tl(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_att_tl), sizeof(g_att_tl), 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 SBK_API long long sbk_relpos_attention_lds(int dtype_bf16, int Tn, int dh) {
   (void)Tn;

@@ -378,12 +378,28 @@ __global__ void __launch_bounds__(256) conv_block_mfma_kernel(const T* __restric
 // normalise it on their own.
 //   x (B, Tin, Fin) fp32; w1 (C1, 3, 3) fp32 in conv_block_c1's tap order;
 //   wp2 (C2, 3 time, 3 freq, C1) T; out (B, T2, F2*C2).
-// Block 1, two rows per pass: thread t owns channels 8*(t%8) .. +7 (their 72
-// taps and LN affine stay in VGPRs) at frequency (t/8) % 40 of row (t/8)/40,
-// so a row is exactly 5 waves; 9 input samples feed 72 FMAs and the 8 outputs
-// leave as one 16-B LDS store.
+// Block 1, one row per wave, on MFMA (the 9 taps padded to one bf16 K step),
+// LN statistics as wave reductions (no workgroup barrier per row).
+// (Tried: two rows per pass over all 10 waves with cross-wave LN reductions
+// and VALU FMAs: 188 us; one row per wave on VALU FMAs: 130 us.)
+#ifdef SBK_PROBE_TL
+__device__ unsigned long long g_fe_tl[10][16];
+#define FE_TL(i)                                                                   \
+  do {                                                                             \
+    if (blockIdx.x == 700 && lane == 0) g_fe_tl[w][i] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define FE_TL(i) \
+  do {           \
+  } while (0)
+#endif
+
+// 10 waves x 8 output rows (17 block-1 rows: passes of 10 and 7 rows).
+// (8 waves x 7 rows with the block-1 LN affine held in VGPRs: 133 us.)
+constexpr int FE_NT = 640, FE_TT2 = 8;
+
 template <typename T, int C1>
-__global__ void __launch_bounds__(640) frontend2_kernel(const float* __restrict__ x, int Tin, int Fin, int T1, int F1,
+__global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restrict__ x, int Tin, int Fin, int T1, int F1,
                                                         int T2, int F2, const float* __restrict__ w1,
                                                         const float* __restrict__ b1, const float* __restrict__ g1,
                                                         const float* __restrict__ be1, float eps1, float slope1,
@@ -392,9 +408,8 @@ __global__ void __launch_bounds__(640) frontend2_kernel(const float* __restrict_
                                                         const float* __restrict__ be2, float eps2, float slope2,
                                                         void* out, int out_bf16) {
   using Tr = MT<T>;
-  constexpr int NT = 640, NW = NT / 64, TT2 = 8, NJ = 2 * TT2 + 1;
-  constexpr int FMAX = 40, CG = 8, WPR = FMAX * (C1 / CG) / 64;  // waves per block-1 row (5)
-  static_assert(C1 == 64 && FMAX * (C1 / CG) * 2 == NT, "block-1 thread map");
+  constexpr int NT = FE_NT, NW = NT / 64, TT2 = FE_TT2, NJ = 2 * TT2 + 1;
+  static_assert(C1 == 64, "block-1 MFMA map: 4 channel tiles");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // LDS row strides padded by 16 B: the MFMA fragment reads of 16 lanes at
   // different output frequencies (b1r rows 2 apart) / channels (wl rows)
@@ -406,103 +421,162 @@ __global__ void __launch_bounds__(640) frontend2_kernel(const float* __restrict_
   float* xs = yv;                                                       // NJ x 3 x Fin (block 1, same space)
   const int xsz = max(TT2 * F2 * C2, (NJ * 3 * Fin + 3) & ~3);
   T* b1r = reinterpret_cast<T*>(yv + xsz);                              // NJ x F1 x C1P
-  __shared__ float red[2][NW];
+  float* w1s = reinterpret_cast<float*>(b1r + NJ * F1 * C1P);           // C1 x 9 block-1 taps
+  float* b1s = w1s + C1 * 9;                                            // C1
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nblk = (T2 + TT2 - 1) / TT2;
   const int b = blockIdx.x / nblk, t20 = (blockIdx.x - b * nblk) * TT2;
   const float* xb = x + (long long)b * Tin * Fin;
+  FE_TL(0);
 
-  // stage block-2 weights (16-B vectors) and the input rows: block-1 row j is
-  // t1 = reflect(2*t20 - 1 + j) and reads x rows reflect(2*t1 - 1 + kt)
-  for (int i = tid; i < C2 * K / Tr::VEC; i += NT) {
-    const int co = (i * Tr::VEC) / K, kk = i * Tr::VEC - co * K;
-    *reinterpret_cast<uint4*>(wl + co * KP + kk) = reinterpret_cast<const uint4*>(wp2)[i];
-  }
-  for (int i = tid; i < NJ * 3 * Fin; i += NT) {
-    const int jk = i / Fin, f = i - jk * Fin;
+  // stage the input rows, the block-2 weights and the block-1 taps / bias,
+  // every load issued before the first LDS store (one latency instead of one
+  // per loop trip): block-1 row j is t1 = reflect(2*t20 - 1 + j) and reads x
+  // rows reflect(2*t1 - 1 + kt)
+  constexpr int XV = (NJ * 3 * 20 + NT - 1) / NT, WV = (32 * 9 * 64 / 8 + NT - 1) / NT;  // vectors per thread (Fin <= 80, C2 <= 32)
+  const int fq4 = Fin / 4;        // Fin % 4 == 0, Fin <= 80 (host-checked)
+  float4 xin[XV];
+  uint4 wvin[WV];
+  const int nwv = C2 * K / Tr::VEC;
+#pragma unroll
+  for (int u = 0; u < XV; ++u) {
+    const int i = tid + u * NT;
+    const int jk = min(i / fq4, NJ * 3 - 1), f4 = i - (i / fq4) * fq4;
     const int j = jk / 3, kt = jk - 3 * j;
     const int t1 = reflect_idx(2 * t20 - 1 + j, T1);
-    xs[i] = xb[(long long)reflect_idx(2 * t1 - 1 + kt, Tin) * Fin + f];
+    xin[u] = *reinterpret_cast<const float4*>(xb + (long long)reflect_idx(2 * t1 - 1 + kt, Tin) * Fin + 4 * f4);
   }
-  const int cg = tid % CG, q = tid / CG, rp = q / FMAX, f1 = q - rp * FMAX;
-  const bool act = f1 < F1;
-  const int f1c = act ? f1 : 0;
-  float wr[CG][9], gg[CG], bb[CG], bi[CG];
 #pragma unroll
-  for (int e = 0; e < CG; ++e) {
-    const int c = cg * CG + e;
+  for (int u = 0; u < WV; ++u) wvin[u] = reinterpret_cast<const uint4*>(wp2)[min(tid + u * NT, nwv - 1)];
+  constexpr int W1V = (C1 * 9 + NT - 1) / NT;  // block-1 taps per thread
+  float w1v[W1V];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) wr[e][t] = w1[c * 9 + t];
-    bi[e] = b1 ? b1[c] : 0.f;
-    gg[e] = g1[f1c * C1 + c];
-    bb[e] = be1[f1c * C1 + c];
+  for (int u = 0; u < W1V; ++u) w1v[u] = w1[min(tid + u * NT, C1 * 9 - 1)];
+  const float b1v = b1 ? b1[tid & (C1 - 1)] : 0.f;
+#pragma unroll
+  for (int u = 0; u < XV; ++u) {
+    const int i = tid + u * NT;
+    if (i < NJ * 3 * fq4) *reinterpret_cast<float4*>(xs + 4 * i) = xin[u];
   }
-  const int fi0 = reflect_idx(2 * f1c - 1, Fin), fi1 = 2 * f1c, fi2 = reflect_idx(2 * f1c + 1, Fin);
+#pragma unroll
+  for (int u = 0; u < WV; ++u) {
+    const int i = tid + u * NT;
+    if (i < nwv) {
+      const int co = (i * Tr::VEC) / K, kk = i * Tr::VEC - co * K;
+      *reinterpret_cast<uint4*>(wl + co * KP + kk) = wvin[u];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < W1V; ++u)
+    if (tid + u * NT < C1 * 9) w1s[tid + u * NT] = w1v[u];
+  if (tid < C1) b1s[tid] = b1v;
+  __syncthreads();  // xs, w1s, b1s staged
+  // block 1 on MFMA, one row per wave (rows w and w + 10): the 3x3 / stride-2
+  // convolution of a row is C^T[c][f1] = W^T[c][tap] · X^T[tap][f1] with the 9
+  // taps zero-padded to one 32-deep bf16 step (conv inputs and taps in bf16,
+  // fp32 accumulation — what the reference computes under autocast): 4 x 3
+  // tiles of 16x16 per row.  A lane then holds 4 consecutive channels of one
+  // frequency per tile, so the row's LayerNorm is two wave reductions (no
+  // workgroup barrier) and each tile leaves as one 8-B LDS store.
+  // tap order k = kf * 3 + kt (conv_block_c1's layout of w1)
+  const int fr = lane & 15, g4 = lane >> 4;
+  bf16x8 wa[4];  // A fragments: W^T rows c = 16 mt + fr, taps 8 g4 .. 8 g4 + 7
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    float t8[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = 8 * g4 + e;
+      t8[e] = k < 9 ? w1s[(16 * mt + fr) * 9 + min(k, 8)] : 0.f;
+    }
+    wa[mt] = MT<bf16_t>::from8(t8);
+  }
+  float4 bias4[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) bias4[mt] = *reinterpret_cast<const float4*>(b1s + 16 * mt + 4 * g4);
+  // this lane's taps of the B fragment: k = 8 g4 + e -> (kt, kf) (k >= 9: zero)
+  int tap_row[8], tap_df[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = min(8 * g4 + e, 8);
+    tap_row[e] = (k % 3) * Fin;
+    tap_df[e] = k / 3 - 1;  // frequency offset: 2 f1 - 1 + kf
+  }
   const float n1 = (float)(F1 * C1);
-  __syncthreads();
-
-  for (int j0 = 0; j0 < NJ; j0 += 2) {
-    const int j = j0 + rp;
-    const bool live = act && j < NJ;
-    float v[CG];
+  FE_TL(1);
+  for (int j = w; j < NJ; j += NW) {
+    const float* r = xs + (j * 3) * Fin;
+    f32x4 acc[4][3];
+#pragma unroll
+    for (int nt = 0; nt < 3; ++nt) {
+      const int f1c = min(16 * nt + fr, F1 - 1);
+      float t8[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xv = r[tap_row[e] + reflect_idx(2 * f1c + tap_df[e], Fin)];
+        t8[e] = 8 * g4 + e < 9 ? xv : 0.f;
+      }
+      const bf16x8 xb8 = MT<bf16_t>::from8(t8);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[mt], xb8, f32x4{bias4[mt].x, bias4[mt].y, bias4[mt].z, bias4[mt].w}, 0, 0, 0);
+    }
     float sm = 0.f;
-    {
-      const float* r = xs + (min(j, NJ - 1) * 3) * Fin;
-      float xv[3][3];  // [kt][kf]
 #pragma unroll
-      for (int kt = 0; kt < 3; ++kt) {
-        xv[kt][0] = r[kt * Fin + fi0];
-        xv[kt][1] = r[kt * Fin + fi1];
-        xv[kt][2] = r[kt * Fin + fi2];
-      }
+    for (int nt = 0; nt < 3; ++nt) {
+      const bool on = 16 * nt + fr < F1;
 #pragma unroll
-      for (int e = 0; e < CG; ++e) {
-        float acc = bi[e];
+      for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-        for (int kf = 0; kf < 3; ++kf)
+        for (int q = 0; q < 4; ++q) sm += on ? acc[mt][nt][q] : 0.f;
+    }
+    const float mean = wave_sum(sm) / n1;
+    float sq = 0.f;
 #pragma unroll
-          for (int kt = 0; kt < 3; ++kt) acc = fmaf(wr[e][kf * 3 + kt], xv[kt][kf], acc);
-        v[e] = live ? acc : 0.f;
-        sm += v[e];
+    for (int nt = 0; nt < 3; ++nt) {
+      const bool on = 16 * nt + fr < F1;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float dv = on ? acc[mt][nt][q] - mean : 0.f;
+          sq += dv * dv;
+        }
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(sq) / n1 + eps1);
+#pragma unroll
+    for (int nt = 0; nt < 3; ++nt) {
+      const int f1 = 16 * nt + fr;
+      if (f1 >= F1) continue;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int c = 16 * mt + 4 * g4;
+        const float4 ga = *reinterpret_cast<const float4*>(g1 + f1 * C1 + c);
+        const float4 ba = *reinterpret_cast<const float4*>(be1 + f1 * C1 + c);
+        const float gg[4] = {ga.x, ga.y, ga.z, ga.w}, bb[4] = {ba.x, ba.y, ba.z, ba.w};
+        float y[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float t = (acc[mt][nt][q] - mean) * rstd * gg[q] + bb[q];
+          y[q] = t >= 0.f ? t : t * slope1;
+        }
+        uint2 pk;
+        pk.x = (uint32_t)f32_to_bf16(y[0]) | ((uint32_t)f32_to_bf16(y[1]) << 16);
+        pk.y = (uint32_t)f32_to_bf16(y[2]) | ((uint32_t)f32_to_bf16(y[3]) << 16);
+        *reinterpret_cast<uint2*>(b1r + (j * F1 + f1) * C1P + c) = pk;
       }
     }
-    // row statistics: 5 waves per row, two-pass (mean, then centred squares)
-    sm = wave_sum(sm);
-    if (lane == 0) red[0][w] = sm;
-    __syncthreads();
-    float mean = 0.f;
-#pragma unroll
-    for (int k2 = 0; k2 < WPR; ++k2) mean += red[0][rp * WPR + k2];
-    mean /= n1;
-    float qq = 0.f;
-#pragma unroll
-    for (int e = 0; e < CG; ++e) qq += live ? (v[e] - mean) * (v[e] - mean) : 0.f;
-    qq = wave_sum(qq);
-    if (lane == 0) red[1][w] = qq;
-    __syncthreads();
-    float var = 0.f;
-#pragma unroll
-    for (int k2 = 0; k2 < WPR; ++k2) var += red[1][rp * WPR + k2];
-    const float rstd = 1.0f / sqrtf(var / n1 + eps1);
-    if (live) {
-      float y[CG];
-#pragma unroll
-      for (int e = 0; e < CG; ++e) {
-        const float t = (v[e] - mean) * rstd * gg[e] + bb[e];
-        y[e] = t >= 0.f ? t : t * slope1;
-      }
-      *reinterpret_cast<typename Tr::frag*>(b1r + (j * F1 + f1) * C1P + cg * CG) = Tr::from8(y);
-    }
-    // red[0] is rewritten next pass only after every wave passed the barrier above
+    FE_TL(2 + j / NW);
   }
   __syncthreads();
+  FE_TL(11);
 
   if (w >= TT2) return;  // waves 8, 9: block 1 only (no barrier below)
   // block 2: wave w -> output row t2 = t20 + w, reading block-1 rows j = 2w + kt
   const int t2 = t20 + w;
   if (t2 >= T2) return;  // no barrier below
-  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  const int fk = 8 * (lane >> 4);
   // all (<= 2 x 2) output tiles of the row accumulate together, so each
   // K step issues 4 independent MFMAs behind 4 fragment reads
   const int mt = (F2 + 15) / 16, ntl = C2 / 16;
@@ -540,6 +614,7 @@ __global__ void __launch_bounds__(640) frontend2_kernel(const float* __restrict_
           for (int tn = 0; tn < 2; ++tn) Tr::mma(acc[tm][tn], fa[tm], fbw[tn]);
       }
   }
+  FE_TL(12);
 #pragma unroll
   for (int tm = 0; tm < 2; ++tm)
 #pragma unroll
@@ -552,20 +627,62 @@ __global__ void __launch_bounds__(640) frontend2_kernel(const float* __restrict_
         if (f < F2) yw[f * C2 + co] = acc[tm][tn][r] + (b2 ? b2[co] : 0.f);
       }
     }
-  // the wave's own LDS row: LN over F2*C2 (wave-local), LeakyReLU, store
-  const int nout = F2 * C2;
+  // the wave's own LDS row: LN over F2*C2 (wave-local), LeakyReLU, store.
+  // Lane l owns elements 8c .. 8c+7 for chunks c = l, l + 64, ... (16-B LDS
+  // reads, 2 x 16-B affine loads, one 16-B bf16 store per chunk)
+  const int nout = F2 * C2;  // multiple of 16 (C2 % 16 == 0)
+  const int nch = nout / 8;
+  constexpr int NCH = (32 * 32 / 8 + 63) / 64;  // chunks per lane (F2, C2 <= 32)
+  float yv8[NCH][8];
   float s2 = 0.f;
-  for (int o = lane; o < nout; o += 64) s2 += yw[o];
+#pragma unroll
+  for (int u = 0; u < NCH; ++u) {
+    const int c = lane + 64 * u;
+    const int cc = min(c, nch - 1);
+    const float4 a0 = *reinterpret_cast<const float4*>(yw + 8 * cc);
+    const float4 a1 = *reinterpret_cast<const float4*>(yw + 8 * cc + 4);
+    const float t8[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      yv8[u][e] = c < nch ? t8[e] : 0.f;
+      s2 += yv8[u][e];
+    }
+  }
   const float m2 = wave_sum(s2) / nout;
   float q2 = 0.f;
-  for (int o = lane; o < nout; o += 64) q2 += (yw[o] - m2) * (yw[o] - m2);
+#pragma unroll
+  for (int u = 0; u < NCH; ++u)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float dv = lane + 64 * u < nch ? yv8[u][e] - m2 : 0.f;
+      q2 += dv * dv;
+    }
   const float r2 = 1.0f / sqrtf(wave_sum(q2) / nout + eps2);
   const long long ob = ((long long)b * T2 + t2) * nout;
-  for (int o = lane; o < nout; o += 64) {
-    float y = (yw[o] - m2) * r2 * g2[o] + be2[o];
-    y = y >= 0.f ? y : y * slope2;
-    st(out, ob + o, y, out_bf16);
+#pragma unroll
+  for (int u = 0; u < NCH; ++u) {
+    const int c = lane + 64 * u;
+    if (c >= nch) continue;
+    const float4* gp = reinterpret_cast<const float4*>(g2 + 8 * c);
+    const float4* bp = reinterpret_cast<const float4*>(be2 + 8 * c);
+    const float4 ga = gp[0], gb = gp[1], ba = bp[0], bb = bp[1];
+    const float gg[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
+    const float bt[8] = {ba.x, ba.y, ba.z, ba.w, bb.x, bb.y, bb.z, bb.w};
+    float y[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float t = (yv8[u][e] - m2) * r2 * gg[e] + bt[e];
+      y[e] = t >= 0.f ? t : t * slope2;
+    }
+    if (out_bf16) {
+      *reinterpret_cast<typename MT<bf16_t>::frag*>(reinterpret_cast<bf16_t*>(out) + ob + 8 * c) = MT<bf16_t>::from8(y);
+    } else {
+      float* o = reinterpret_cast<float*>(out) + ob + 8 * c;
+      *reinterpret_cast<float4*>(o) = make_float4(y[0], y[1], y[2], y[3]);
+      *reinterpret_cast<float4*>(o + 4) = make_float4(y[4], y[5], y[6], y[7]);
+    }
   }
+  FE_TL(13);
 }
 
 __global__ void cast_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long long n) {
@@ -586,6 +703,12 @@ inline int grid_for(long long n, int block) {
 }
 
 }  // namespace
+
+#ifdef SBK_PROBE_TL
+SBK_API int sbk_probe_fe_tl(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fe_tl), sizeof(g_fe_tl), 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 SBK_API int sbk_layernorm(const float* x, int M, int D, const float* g1, const float* b1, float eps1, void* out1,
                           int out1_bf16, const float* g2, const float* b2, float eps2, void* out2, int out2_bf16,
@@ -691,11 +814,17 @@ SBK_API int sbk_conv_frontend2(int dtype_bf16, const float* x, int B, int Tin, i
   if (Tout_) *Tout_ = T2;
   if (Fout_) *Fout_ = F2;
   if (!x) return 0;
-  if (F1 > 40 || T1 < 2 || F1 < 2 || F2 > 32 || C2 > 32) return SBK_ERR_ARG;
-  constexpr int TT2 = 8, NJ = 2 * TT2 + 1;
+  if (F1 > 40 || T1 < 2 || F1 < 2 || F2 > 32 || C2 > 32 || Fin % 4 || Fin > 80) return SBK_ERR_ARG;
+  // 16-B vector loads / stores of x rows, LN affine and out rows
+  if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(g1) | reinterpret_cast<uintptr_t>(be1) |
+       reinterpret_cast<uintptr_t>(g2) | reinterpret_cast<uintptr_t>(be2) | reinterpret_cast<uintptr_t>(out) |
+       reinterpret_cast<uintptr_t>(wp2)) & 15)
+    return SBK_ERR_ARG;
+  constexpr int TT2 = FE_TT2, NJ = 2 * TT2 + 1;
   const size_t esz = dtype_bf16 ? 2 : 4;
   const size_t lds = (size_t)C2 * (9 * C1 + 8) * esz +
-                     (size_t)std::max(TT2 * F2 * C2, (NJ * 3 * Fin + 3) & ~3) * 4 + (size_t)NJ * F1 * (C1 + 8) * esz;
+                     (size_t)std::max(TT2 * F2 * C2, (NJ * 3 * Fin + 3) & ~3) * 4 + (size_t)NJ * F1 * (C1 + 8) * esz +
+                     (size_t)C1 * 10 * 4;  // block-1 taps + bias
   if (dtype_bf16 && lds > 160 * 1024 - 1024) return SBK_ERR_ARG;
   const dim3 grid(B * ((T2 + TT2 - 1) / TT2));
   hipStream_t s = (hipStream_t)stream;
@@ -707,7 +836,7 @@ SBK_API int sbk_conv_frontend2(int dtype_bf16, const float* x, int B, int Tin, i
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  hipLaunchKernelGGL((frontend2_kernel<bf16_t, 64>), grid, dim3(640), lds, s, x, Tin, Fin, T1, F1, T2, F2, w1, b1, g1,
+  hipLaunchKernelGGL((frontend2_kernel<bf16_t, 64>), grid, dim3(FE_NT), lds, s, x, Tin, Fin, T1, F1, T2, F2, w1, b1, g1,
                      be1, eps1, slope1, reinterpret_cast<const bf16_t*>(wp2), C2, b2, g2, be2, eps2, slope2, out,
                      out_bf16);
   SBK_CHECK_LAUNCH();
