@@ -125,7 +125,16 @@ int sbk_gemm(int dtype_bf16, const void* A, int lda, const void* W, int ldw, int
              const float* bias, int act, float slope, const float* res, int ldr, float alpha,
              const uint8_t* rowmask, void* out, int ldc, int out_bf16, int tile, void* stream);
 
-/* 1 if the fused FFN kernel supports d_model D and d_ffn H (D in {256, 512}, H % 256 == 0). */
+/* sbk_gemm (act none, fp32 out) followed by u = LN(out row; ln_g, ln_b, ln_eps) in
+ * the same launch (full-row tiles: N == 256).  The attention output projection +
+ * residual and the convolution module's LayerNorm: attention.py:636 with
+ * Conformer.py:69-72.  u (M, ldu) bf16 when u_bf16, else fp32; tile 0 default. */
+int sbk_gemm_ln(int dtype_bf16, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
+                const float* bias, const float* res, int ldr, float alpha, const uint8_t* rowmask, float* out,
+                int ldc, const float* ln_g, const float* ln_b, float ln_eps, void* u, int ldu, int u_bf16, int tile,
+                void* stream);
+
+/* 1 if the fused FFN kernel supports d_model D and d_ffn H (D == 256, H % 256 == 0, H <= 2048). */
 int sbk_ffn_supported(int D, int H);
 
 /* Fused macaron feed-forward block, bf16 MFMA (Conformer.py:239-260 with

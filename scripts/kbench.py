@@ -75,6 +75,23 @@ def gemm_one(name="qkv", tile=2):
     print(f"{name} tile {tile}: {us:.1f}us", flush=True)
 
 
+def gemmln_bench():
+    dev = torch.device("cuda")
+    M, N, K = 12032, 256, 256
+    a = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev) / 16).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev)
+    res = torch.randn(M, N, device=dev)
+    ln = (torch.ones(N, device=dev), torch.zeros(N, device=dev), 1e-5)
+    for tile in (0, 1, 2):
+        us = timeit(lambda: _enc.gemm_ln(a, w, ln, bias=bias, res=res, tile=tile))
+        print(f"gemm_ln tile {tile}: {us:.1f}us", flush=True)
+    us1 = timeit(lambda: _enc.gemm(a, w, bias=bias, res=res))
+    out = _enc.gemm(a, w, bias=bias, res=res)
+    us2 = timeit(lambda: _enc.layernorm(out, *ln, out1_dtype=torch.bfloat16))
+    print(f"separate: gemm {us1:.1f}us + layernorm {us2:.1f}us", flush=True)
+
+
 def attn_bench():
     dev = torch.device("cuda")
     B, T, H, dh = 32, 376, 4, 64
@@ -135,3 +152,5 @@ if __name__ == "__main__":
         gemm_one(sys.argv[2] if len(sys.argv) > 2 else "qkv", int(sys.argv[3]) if len(sys.argv) > 3 else 2)
     if what in ("ffn", "all"):
         ffn_bench()
+    if what in ("gemmln", "all"):
+        gemmln_bench()

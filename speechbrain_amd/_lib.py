@@ -39,6 +39,8 @@ SIGNATURES = {
     # gemm.hip
     "sbk_gemm_glu_group": [_i],
     "sbk_gemm": [_i, _vp, _i, _vp, _i, _i, _i, _i, _vp, _i, _f, _vp, _i, _f, _vp, _vp, _i, _i, _i, _vp],
+    "sbk_gemm_ln": [_i, _vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _i, _f, _vp, _vp, _i, _vp, _vp, _f, _vp, _i, _i, _i,
+                    _vp],
     # ffn.hip
     "sbk_ffn_supported": [_i, _i],
     "sbk_ffn": [_vp, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _i, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _vp, _f,

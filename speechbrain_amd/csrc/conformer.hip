@@ -34,6 +34,78 @@ __device__ __forceinline__ void st(void* p, long long i, float v, int bf) {
 
 // One wave per row.  y1 = LN1(x) (written to out1 if non-null);
 // if g2: y2 = LN2(y1) written to out2.  Rows up to D = 64 * 16 elements.
+// D == 256 rows: lane l owns columns 4l .. 4l+3 (16-B loads, 8-/16-B
+// stores), a wave normalises RPW rows with every load issued up front and the
+// RPW reductions interleaved.  Same arithmetic as layernorm_kernel.
+template <int RPW>
+__global__ void __launch_bounds__(256) layernorm256_kernel(const float* __restrict__ x, int M,
+                                                           const float* __restrict__ g1, const float* __restrict__ b1,
+                                                           float eps1, void* out1, int out1_bf16,
+                                                           const float* __restrict__ g2,
+                                                           const float* __restrict__ b2, float eps2, void* out2,
+                                                           int out2_bf16) {
+  constexpr int D = 256;
+  const int lane = threadIdx.x & 63;
+  const long long row0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  float v[RPW][4], sm[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const long long row = min(row0 + r, (long long)M - 1);
+    const float4 t = *reinterpret_cast<const float4*>(x + row * D + 4 * lane);
+    v[r][0] = t.x; v[r][1] = t.y; v[r][2] = t.z; v[r][3] = t.w;
+  }
+  auto norm = [&](const float* g, const float* b, float eps) __attribute__((always_inline)) {
+    const float4 g4 = *reinterpret_cast<const float4*>(g + 4 * lane);
+    const float4 b4 = *reinterpret_cast<const float4*>(b + 4 * lane);
+    const float gg[4] = {g4.x, g4.y, g4.z, g4.w}, bb[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) sm[r] = v[r][0] + v[r][1] + v[r][2] + v[r][3];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) sm[r] += __shfl_xor(sm[r], o);
+    float sq[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      sm[r] *= 1.0f / D;
+      sq[r] = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sq[r] += (v[r][e] - sm[r]) * (v[r][e] - sm[r]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) sq[r] += __shfl_xor(sq[r], o);
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const float rstd = 1.0f / sqrtf(sq[r] * (1.0f / D) + eps);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[r][e] = (v[r][e] - sm[r]) * rstd * gg[e] + bb[e];
+    }
+  };
+  auto store = [&](void* out, int bf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const long long row = row0 + r;
+      if (row >= M) continue;
+      if (bf) {
+        uint2 pk;
+        pk.x = (uint32_t)f32_to_bf16(v[r][0]) | ((uint32_t)f32_to_bf16(v[r][1]) << 16);
+        pk.y = (uint32_t)f32_to_bf16(v[r][2]) | ((uint32_t)f32_to_bf16(v[r][3]) << 16);
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(out) + row * D + 4 * lane) = pk;
+      } else {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + row * D + 4 * lane) =
+            make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
+      }
+    }
+  };
+  norm(g1, b1, eps1);
+  if (out1) store(out1, out1_bf16);
+  if (!g2) return;
+  norm(g2, b2, eps2);
+  store(out2, out2_bf16);
+}
+
 template <int PER>
 __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict__ x, int M, int D,
                                                         const float* g1, const float* b1, float eps1, void* out1,
@@ -715,6 +787,17 @@ SBK_API int sbk_layernorm(const float* x, int M, int D, const float* g1, const f
                           void* stream) {
   if (M <= 0 || D <= 0 || D > 1024) return SBK_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(g1) |
+                       reinterpret_cast<uintptr_t>(b1) | reinterpret_cast<uintptr_t>(g2) |
+                       reinterpret_cast<uintptr_t>(b2) | reinterpret_cast<uintptr_t>(out1) |
+                       reinterpret_cast<uintptr_t>(out2);
+  if (D == 256 && !(al & 15)) {
+    constexpr int RPW = 4;
+    hipLaunchKernelGGL(layernorm256_kernel<RPW>, dim3((M + 4 * RPW - 1) / (4 * RPW)), dim3(256), 0, s, x, M, g1, b1,
+                       eps1, out1, out1_bf16, g2, b2, eps2, out2, out2_bf16);
+    SBK_CHECK_LAUNCH();
+    return 0;
+  }
   const dim3 grid((M + 3) / 4);
 #define SBK_LN(P)                                                                                       \
   hipLaunchKernelGGL(layernorm_kernel<P>, grid, dim3(256), 0, s, x, M, D, g1, b1, eps1, out1, out1_bf16, g2, \

@@ -36,6 +36,14 @@ struct Epi {
   void* out;
   int ldc;
   int out_bf16;
+  // optional row LayerNorm of the stored rows (full-row tiles, BN == N == 256):
+  // ln_out = LN(out row; ln_g, ln_b, ln_eps)
+  const float* ln_g = nullptr;
+  const float* ln_b = nullptr;
+  float ln_eps = 0.f;
+  void* ln_out = nullptr;
+  int ldu = 0;
+  int ln_bf16 = 0;
 };
 
 // C tile (fp32, row stride CR, in LDS) -> global through the fused epilogue:
@@ -113,12 +121,77 @@ __device__ __forceinline__ bool epi_aligned(const Epi& ep) {
   return (m & 15) == 0 && (ep.ldr & 3) == 0 && (ep.ldc & 3) == 0;
 }
 
+// Full-row epilogue (BN == N == 256, act none, fp32 out): wave w owns rows
+// w*BM/4 .. +BM/4-1, lane l columns 4l .. 4l+3; after the residual stream row
+// is stored, its LayerNorm (two wave reductions) is written to ln_out.  This
+// removes a separate LayerNorm launch and its HBM re-read (Conformer.py:69-72
+// after the attention residual).
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void store_ctile_rowln(const float* __restrict__ Cs, const Epi& ep, int m0, int M,
+                                                  int tid, const float4 (&rres)[BM / 4]) {
+  static_assert(BN == 256 && NT == 256, "row-LN epilogue: 256 columns, 4 waves");
+  constexpr int CR = BN + 4, RPW = BM / 4;
+  const int lane = tid & 63, w = tid >> 6;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 bs = ep.bias ? *reinterpret_cast<const float4*>(ep.bias + 4 * lane) : z4;
+  const float4 g4 = *reinterpret_cast<const float4*>(ep.ln_g + 4 * lane);
+  const float4 b4 = *reinterpret_cast<const float4*>(ep.ln_b + 4 * lane);
+  // all RPW rows at once: independent loads and reductions overlap
+  float v[RPW][4], sm[RPW], sq[RPW];
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int r = w * RPW + rr, row = min(m0 + r, M - 1);
+    const float4 c = *reinterpret_cast<const float4*>(Cs + r * CR + 4 * lane);
+    const float sc = (ep.rowmask && ep.rowmask[row]) ? 0.f : ep.alpha;
+    v[rr][0] = (c.x + bs.x) * sc; v[rr][1] = (c.y + bs.y) * sc;
+    v[rr][2] = (c.z + bs.z) * sc; v[rr][3] = (c.w + bs.w) * sc;
+    v[rr][0] += rres[rr].x; v[rr][1] += rres[rr].y; v[rr][2] += rres[rr].z; v[rr][3] += rres[rr].w;
+    sm[rr] = v[rr][0] + v[rr][1] + v[rr][2] + v[rr][3];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr) sm[rr] += __shfl_xor(sm[rr], o);
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr) {
+    const float mean = sm[rr] * (1.0f / BN);
+    sq[rr] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sq[rr] += (v[rr][e] - mean) * (v[rr][e] - mean);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr) sq[rr] += __shfl_xor(sq[rr], o);
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int r = w * RPW + rr, row = m0 + r;
+    if (row >= M) continue;
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(ep.out) + (long long)row * ep.ldc + 4 * lane) =
+        make_float4(v[rr][0], v[rr][1], v[rr][2], v[rr][3]);
+    const float mean = sm[rr] * (1.0f / BN);
+    const float rstd = 1.0f / sqrtf(sq[rr] * (1.0f / BN) + ep.ln_eps);
+    const float y0 = (v[rr][0] - mean) * rstd * g4.x + b4.x, y1 = (v[rr][1] - mean) * rstd * g4.y + b4.y;
+    const float y2 = (v[rr][2] - mean) * rstd * g4.z + b4.z, y3 = (v[rr][3] - mean) * rstd * g4.w + b4.w;
+    if (ep.ln_bf16) {
+      uint2 pk;
+      pk.x = (uint32_t)f32_to_bf16(y0) | ((uint32_t)f32_to_bf16(y1) << 16);
+      pk.y = (uint32_t)f32_to_bf16(y2) | ((uint32_t)f32_to_bf16(y3) << 16);
+      *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(ep.ln_out) + (long long)row * ep.ldu + 4 * lane) = pk;
+    } else {
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(ep.ln_out) + (long long)row * ep.ldu + 4 * lane) =
+          make_float4(y0, y1, y2, y3);
+    }
+  }
+}
+
 template <int BM, int BN, int NT>
 __device__ __forceinline__ void store_ctile(const float* __restrict__ Cs, const Epi& ep, int m0, int n0, int M,
                                             int N, int tid) {
 #ifdef SBK_PROBE_NO_EPI
   if (Cs[tid] != 12345.f) return;
 #endif
+
   if (m0 + BM <= M && n0 + BN <= N && epi_aligned(ep)) {
     switch (ep.act) {
       case ACT_NONE: store_ctile_fast<BM, BN, NT, ACT_NONE, false>(Cs, ep, m0, n0, tid); return;
@@ -216,9 +289,8 @@ __global__ void __launch_bounds__(256) gemm_kernel(const T* __restrict__ A, int 
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int CPR = BK / VEC;          // 16-B chunks per row
-  constexpr int ACH = BM * CPR / 256;    // chunks per thread (A)
-  constexpr int BCH = BN * CPR / 256;    // chunks per thread (B)
-  static_assert(ACH >= 1 && BCH >= 1, "tile too small for 256 threads");
+  constexpr int ACH = (BM * CPR + 255) / 256;  // chunks per thread (A; the last pass may be partial)
+  constexpr int BCH = (BN * CPR + 255) / 256;  // chunks per thread (B)
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* As = reinterpret_cast<T*>(smem);
@@ -234,6 +306,18 @@ __global__ void __launch_bounds__(256) gemm_kernel(const T* __restrict__ A, int 
   const int tile_id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
   const int m0 = (tile_id / ntn) * BM;
   const int n0 = (tile_id % ntn) * BN;
+  // full-row (BN == 256) tiles are sbk_gemm_ln's: the residual rows of the
+  // row-LN epilogue are fetched here so their latency hides under the K loop
+  constexpr bool ROWLN = BN == 256;
+  float4 rres[ROWLN ? BM / 4 : 1];
+  if constexpr (ROWLN) {
+#pragma unroll
+    for (int rr = 0; rr < BM / 4; ++rr) {
+      const int row = min(m0 + (tid >> 6) * (BM / 4) + rr, M - 1);
+      rres[rr] = ep.res ? *reinterpret_cast<const float4*>(ep.res + (long long)row * ep.ldr + 4 * (tid & 63))
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
 
   uint4 ra[ACH], rb[BCH];
   auto gload = [&](int k0) {
@@ -241,13 +325,15 @@ __global__ void __launch_bounds__(256) gemm_kernel(const T* __restrict__ A, int 
     for (int i = 0; i < ACH; ++i) {
       const int c = tid + i * 256, r = c / CPR, kc = (c % CPR) * VEC;
       const int gr = m0 + r, gk = k0 + kc;
-      ra[i] = (gr < M && gk < K) ? *reinterpret_cast<const uint4*>(A + (long long)gr * lda + gk) : make_uint4(0, 0, 0, 0);
+      ra[i] = (c < BM * CPR && gr < M && gk < K) ? *reinterpret_cast<const uint4*>(A + (long long)gr * lda + gk)
+                                                 : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int c = tid + i * 256, r = c / CPR, kc = (c % CPR) * VEC;
       const int gr = n0 + r, gk = k0 + kc;
-      rb[i] = (gr < N && gk < K) ? *reinterpret_cast<const uint4*>(W + (long long)gr * ldw + gk) : make_uint4(0, 0, 0, 0);
+      rb[i] = (c < BN * CPR && gr < N && gk < K) ? *reinterpret_cast<const uint4*>(W + (long long)gr * ldw + gk)
+                                                 : make_uint4(0, 0, 0, 0);
     }
   };
   auto sstore = [&](int buf) {
@@ -256,12 +342,12 @@ __global__ void __launch_bounds__(256) gemm_kernel(const T* __restrict__ A, int 
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       const int c = tid + i * 256, r = c / CPR, kc = (c % CPR) * VEC;
-      *reinterpret_cast<uint4*>(as + r * LDSR + kc) = ra[i];
+      if (c < BM * CPR) *reinterpret_cast<uint4*>(as + r * LDSR + kc) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int c = tid + i * 256, r = c / CPR, kc = (c % CPR) * VEC;
-      *reinterpret_cast<uint4*>(bs + r * LDSR + kc) = rb[i];
+      if (c < BN * CPR) *reinterpret_cast<uint4*>(bs + r * LDSR + kc) = rb[i];
     }
   };
 
@@ -321,7 +407,10 @@ __global__ void __launch_bounds__(256) gemm_kernel(const T* __restrict__ A, int 
       for (int r = 0; r < 4; ++r)
         Cs[(wm * WM + i * 16 + 4 * (lane >> 4) + r) * CR + wn * WN + j * 16 + fr] = acc[i][j][r];
   __syncthreads();
-  store_ctile<BM, BN, 256>(Cs, ep, m0, n0, M, N, tid);
+  if constexpr (ROWLN)
+    store_ctile_rowln<BM, BN, 256>(Cs, ep, m0, M, tid, rres);
+  else
+    store_ctile<BM, BN, 256>(Cs, ep, m0, n0, M, N, tid);
 }
 
 template <typename T, int BM, int BN, int BK, int NBUF = 2>
@@ -330,6 +419,15 @@ int launch(const void* A, int lda, const void* W, int ldw, int M, int N, int K, 
   size_t lds = (size_t)NBUF * (BM + BN) * LDSR * sizeof(T);
   const size_t cbytes = (size_t)BM * (BN + 4) * 4;  // epilogue C tile
   if (cbytes > lds) lds = cbytes;
+  if (lds > 64 * 1024) {  // opt in once per instantiation
+    static bool attr = false;
+    if (!attr) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_kernel<T, BM, BN, BK, NBUF>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return (int)e;
+      attr = true;
+    }
+  }
   const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   hipLaunchKernelGGL((gemm_kernel<T, BM, BN, BK, NBUF>), dim3(grid), dim3(256), lds, s, reinterpret_cast<const T*>(A),
                      lda, reinterpret_cast<const T*>(W), ldw, M, N, K, ep);
@@ -607,6 +705,38 @@ SBK_API int sbk_gemm_glu_group(int dtype_bf16) { (void)dtype_bf16; return 16; } 
 
 // dtype_bf16: A and W are bf16 (else fp32).  tile: 0 auto, 1 = 128x128, 2 = 64x64, 3 = 128x64 (BK 64,
 // double-buffered); bf16 only: 4/5/6 = 64x64 / 64x128 / 128x64 with BK 256 single buffer,
+// out = res + alpha * (A @ W^T + bias) (rows masked -> 0 before the residual),
+// then u = LN(out row) — the attention output projection and the convolution
+// module's LayerNorm (Conformer.py:69-72, attention.py:636) in one launch.
+// Full-row tiles: N == 256, fp32 out, no activation.
+SBK_API int sbk_gemm_ln(int dtype_bf16, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
+                        const float* bias, const float* res, int ldr, float alpha, const uint8_t* rowmask, float* out,
+                        int ldc, const float* ln_g, const float* ln_b, float ln_eps, void* u, int ldu, int u_bf16,
+                        int tile, void* stream) {
+  if (M <= 0 || N != 256 || K <= 0 || !ln_g || !ln_b || !u || !out) return SBK_ERR_ARG;
+  const int vec = dtype_bf16 ? 8 : 4;
+  if ((K % vec) || (lda % vec) || (ldw % vec) || (ldc % 4) || (ldu % 4) || (res && (ldr % 4))) return SBK_ERR_ARG;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(W) |
+                       reinterpret_cast<uintptr_t>(bias) | reinterpret_cast<uintptr_t>(res) |
+                       reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(ln_g) |
+                       reinterpret_cast<uintptr_t>(ln_b) | reinterpret_cast<uintptr_t>(u);
+  if (al & 15) return SBK_ERR_ARG;
+  Epi ep{bias, ACT_NONE, 0.f, res, ldr, alpha, rowmask, out, ldc, 0};
+  ep.ln_g = ln_g;
+  ep.ln_b = ln_b;
+  ep.ln_eps = ln_eps;
+  ep.ln_out = u;
+  ep.ldu = ldu;
+  ep.ln_bf16 = u_bf16;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype_bf16) {
+    if (tile == 2) return launch<bf16_t, 64, 256, 32, 2>(A, lda, W, ldw, M, N, K, ep, s);
+    if (tile == 1) return launch<bf16_t, 32, 256, 64, 2>(A, lda, W, ldw, M, N, K, ep, s);
+    return launch<bf16_t, 32, 256, 32, 2>(A, lda, W, ldw, M, N, K, ep, s);
+  }
+  return launch<float, 32, 256, 32, 2>(A, lda, W, ldw, M, N, K, ep, s);
+}
+
 // 7 = 128x128 BK 128 single buffer, 8 = 64x64 BK 128 double buffer.
 SBK_API int sbk_gemm(int dtype_bf16, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
                      const float* bias, int act, float slope, const float* res, int ldr, float alpha,
@@ -635,9 +765,6 @@ SBK_API int sbk_gemm(int dtype_bf16, const void* A, int lda, const void* W, int 
       case 20: return launch_pf<64, 128, 64>(A, lda, W, ldw, M, N, K, ep, s);
       case 21: return launch_pf<128, 128, 64>(A, lda, W, ldw, M, N, K, ep, s);
       case 22: return launch_pf<64, 64, 32>(A, lda, W, ldw, M, N, K, ep, s);
-      case 14: return launch<bf16_t, 64, 256, 32, 2>(A, lda, W, ldw, M, N, K, ep, s);
-      case 15: return launch<bf16_t, 64, 256, 64, 2>(A, lda, W, ldw, M, N, K, ep, s);
-      case 16: return launch<bf16_t, 32, 256, 64, 2>(A, lda, W, ldw, M, N, K, ep, s);
       case 17: return launch<bf16_t, 64, 128, 32, 2>(A, lda, W, ldw, M, N, K, ep, s);
       case 11: case 12: case 13: {
         // LDS-DMA ring: K % 64 == 0, K >= 192, 16-B aligned rows

@@ -91,15 +91,19 @@ class ConvolutionModule(nn.Module):
         ps = [w1, w2] + ([b1] if b1 is not None else [])
         return self._wc.get(str(dtype), ps, make)
 
-    def run(self, x2d, B, T, dtype, pad_mask_u8=None, residual=None):
-        """x2d: (B*T, d) fp32 → residual + mask(ConvolutionModule(x)) (fp32)."""
+    def ln_params(self):
+        return (self.layer_norm.weight.detach(), self.layer_norm.bias.detach(), self.layer_norm.eps)
+
+    def run(self, x2d, B, T, dtype, pad_mask_u8=None, residual=None, u=None):
+        """x2d: (B*T, d) fp32 → residual + mask(ConvolutionModule(x)) (fp32).
+        u: LN(x2d) in `dtype` when the producer already computed it."""
         d = x2d.shape[1]
         if d % _enc.glu_group():
             raise NotImplementedError("fused GLU needs d_model % 16 == 0")
         _check_swish(self.after_conv[1])
         w1p, b1p, w2 = self.kernel_weights(dtype)
-        u, _ = _enc.layernorm(x2d, self.layer_norm.weight.detach(), self.layer_norm.bias.detach(),
-                              self.layer_norm.eps, out1_dtype=dtype)
+        if u is None:
+            u, _ = _enc.layernorm(x2d, *self.ln_params(), out1_dtype=dtype)
         g = _enc.gemm(u, w1p, bias=b1p, act="glu", out_dtype=dtype)
         ln = self.after_conv[0]
         v = _enc.dwconv_ln_swish(g, B, T, self.conv.weight.detach(), self.conv.bias.detach() if self.conv.bias is not None
@@ -155,8 +159,10 @@ class ConformerEncoderLayer(nn.Module):
             # FFN1 + norm1 in one kernel, FFN2 + norm2 in one kernel (LayerNorms
             # computed on chip; the next layer's FFN1 normalises its own input)
             x, u = f1[1].run_fused(x, self._ln(f1[0]), 0.5, next_ln=self._ln(self.norm1.norm), next_dtype=dtype)
-            x, attn = self.mha_layer.attend(u, B, T, pos, kpm_u8, dtype, need_attn, residual=x)
-            x = self.convolution_module.run(x, B, T, dtype, kpm_u8, residual=x)
+            # attention output projection + residual + the conv module's LayerNorm in one launch
+            x, attn, uc = self.mha_layer.attend(u, B, T, pos, kpm_u8, dtype, need_attn, residual=x,
+                                                post_ln=self.convolution_module.ln_params())
+            x = self.convolution_module.run(x, B, T, dtype, kpm_u8, residual=x, u=uc)
             x, y = f2[1].run_fused(x, self._ln(f2[0]), 0.5, post_ln=self._ln(self.norm2.norm), out=x,
                                    next_ln=final_ln, next_dtype=_f32)
             return (y, None, attn, True) if final_ln is not None else (x, None, attn, False)
@@ -164,8 +170,9 @@ class ConformerEncoderLayer(nn.Module):
             u_in, _ = _enc.layernorm(x, *self._ln(f1[0]), out1_dtype=dtype)
         x = f1[1].run(u_in, dtype, residual=x, alpha=0.5)
         u, _ = _enc.layernorm(x, *self._ln(self.norm1.norm), out1_dtype=dtype)
-        x, attn = self.mha_layer.attend(u, B, T, pos, kpm_u8, dtype, need_attn, residual=x)
-        x = self.convolution_module.run(x, B, T, dtype, kpm_u8, residual=x)
+        x, attn, uc = self.mha_layer.attend(u, B, T, pos, kpm_u8, dtype, need_attn, residual=x,
+                                            post_ln=self.convolution_module.ln_params())
+        x = self.convolution_module.run(x, B, T, dtype, kpm_u8, residual=x, u=uc)
         u, _ = _enc.layernorm(x, *self._ln(f2[0]), out1_dtype=dtype)
         z = f2[1].run(u, dtype, residual=x, alpha=0.5)
         w2, b2, e2 = self._ln(self.norm2.norm)

@@ -104,9 +104,11 @@ class RelPosMHAXL(nn.Module):
             return tuple(p.detach() for p in ps)
         return self._wc.get("bf16", ps, lambda: tuple(_enc.cast_bf16(p.detach().contiguous()) for p in ps))
 
-    def attend(self, x2d, B, T, pos_embs, kpm_u8, dtype, need_weights, residual=None):
+    def attend(self, x2d, B, T, pos_embs, kpm_u8, dtype, need_weights, residual=None, post_ln=None):
         """Core used by the fused Conformer layer: x2d (B*T, d) in `dtype`.
-        Returns (out (B*T, d) fp32 [+ residual], attn or None)."""
+        Returns (out (B*T, d) fp32 [+ residual], attn or None); with post_ln =
+        (w, b, eps) also u = LN(out) in `dtype` (fused into the output
+        projection when d_model == 256): (out, attn, u)."""
         if self.vbias is not None:
             raise NotImplementedError("vbias=True is not on the RelPosMHAXL hot path")
         w_in, w_pos, w_out = self.kernel_weights(dtype)
@@ -117,7 +119,15 @@ class RelPosMHAXL(nn.Module):
         pk = _enc.gemm(pos.contiguous(), w_pos, out_dtype=dtype)
         o, probs = _enc.relpos_attention(qkv, pk, self.pos_bias_u.detach(), self.pos_bias_v.detach(), kpm_u8, B, T,
                                          self.num_heads, self.head_dim, self.scale, need_weights)
-        out = _enc.gemm(o, w_out, bias=self.out_proj.bias.detach(), res=residual, out_dtype=torch.float32)
+        bias = self.out_proj.bias.detach()
+        if post_ln is not None:
+            if _enc.gemm_ln_supported(self.embed_dim) and _enc.USE_GEMM_LN:
+                out, u = _enc.gemm_ln(o, w_out, post_ln, bias=bias, res=residual, u_dtype=dtype)
+            else:
+                out = _enc.gemm(o, w_out, bias=bias, res=residual, out_dtype=torch.float32)
+                u, _ = _enc.layernorm(out, *post_ln, out1_dtype=dtype)
+            return out, probs, u
+        out = _enc.gemm(o, w_out, bias=bias, res=residual, out_dtype=torch.float32)
         return out, probs
 
     def forward(self, query, key, value, pos_embs, key_padding_mask=None, attn_mask=None,

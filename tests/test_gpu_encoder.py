@@ -72,6 +72,36 @@ def test_gemm_ring_tiles_vs_torch(dev, tile, M, N, K):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("tile", [0, 1, 2])
+@pytest.mark.parametrize("M,K", [(12032, 256), (77, 256), (300, 128), (33, 64)])
+def test_gemm_ln_vs_torch(dev, dtype, tile, M, K):
+    """Output projection + residual + row LayerNorm in one launch (sbk_gemm_ln):
+    out = res + (a @ w.T + bias) with masked rows, u = LN(out).  fp32 within
+    1e-4 (2e-5 GEMM, LN in fp32); bf16 operands: 2e-3 on out, 2e-2 on bf16 u."""
+    from speechbrain_amd import _enc
+    if dtype == torch.float32 and tile:
+        pytest.skip("fp32 has one tile")
+    N = 256
+    g = torch.Generator().manual_seed(M + K + tile)
+    a = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) / math.sqrt(K)
+    bias = torch.randn(N, generator=g)
+    res = torch.randn(M, N, generator=g)
+    lw, lb = 1 + 0.1 * torch.randn(N, generator=g), 0.1 * torch.randn(N, generator=g)
+    mask = (torch.arange(M) % 5 == 2).to(torch.uint8)
+    ad, wd = a.to(dev, dtype), w.to(dev, dtype)
+    ref = ad.float().cpu() @ wd.float().cpu().t() + bias
+    ref[mask.bool()] = 0
+    ref = ref + res
+    uref = F.layer_norm(ref, (N,), lw, lb, 1e-5)
+    out, u = _enc.gemm_ln(ad, wd, (lw.to(dev), lb.to(dev), 1e-5), bias=bias.to(dev), res=res.to(dev),
+                          rowmask=mask.to(dev), u_dtype=dtype, tile=tile)
+    f32 = dtype == torch.float32
+    assert_close(out, ref, rtol=2e-5 if f32 else 2e-3, name="out")
+    assert_close(u.float(), uref, rtol=1e-4 if f32 else 2e-2, name="u")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_gemm_glu_permutation(dev, dtype):
     from speechbrain_amd.lobes.models.transformer.Conformer import ConvolutionModule
     from speechbrain_amd import _enc
