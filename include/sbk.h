@@ -111,6 +111,11 @@ int sbk_rnnt_backward(const float* x, const int* labels, int B, int T, int U1, i
 
 /* ----------------------------------------------------------------- encoder */
 
+/* Key padding mask from relative lengths: out[b, t] = t > floor(rel_len[b] * T)
+ * (uint8, (B, T)); TransformerASR.py:295-301 (make_transformer_src_mask's
+ * length_to_mask on round(wav_len * T) in its fp32 form). */
+int sbk_length_mask(const float* rel_len, int B, int T, uint8_t* out, void* stream);
+
 /* Output channels per wave tile in the GLU-paired GEMM (weights are
  * row-permuted in groups of this size). */
 int sbk_gemm_glu_group(int dtype_bf16);

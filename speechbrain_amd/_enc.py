@@ -39,6 +39,16 @@ def gemm(a, w, bias=None, act=None, slope=0.0, res=None, alpha=1.0, rowmask=None
     return out
 
 
+def length_mask(rel_len, T):
+    """(B, T) uint8: t > floor(rel_len[b] * T) — one launch."""
+    require_device(rel_len)
+    rl = rel_len if (rel_len.dtype == _f32 and rel_len.is_contiguous()) else rel_len.float().contiguous()
+    B = rl.shape[0]
+    out = torch.empty(B, T, device=rl.device, dtype=torch.uint8)
+    check(lib().sbk_length_mask(ptr(rl), B, int(T), ptr(out), stream_of(rl)), "sbk_length_mask")
+    return out
+
+
 def gemm_ln(a, w, ln, bias=None, res=None, alpha=1.0, rowmask=None, out=None, u_dtype=_bf16, tile=0):
     """out = res + alpha * (a @ w.T + bias) (fp32) and u = LN(out; *ln) in one
     launch (N == 256).  Returns (out, u)."""

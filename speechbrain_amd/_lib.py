@@ -38,6 +38,7 @@ SIGNATURES = {
     "sbk_context_window": [_vp, _vp, _i, _i, _i, _i, _i, _vp],
     # gemm.hip
     "sbk_gemm_glu_group": [_i],
+    "sbk_length_mask": [_vp, _i, _i, _vp, _vp],
     "sbk_gemm": [_i, _vp, _i, _vp, _i, _i, _i, _i, _vp, _i, _f, _vp, _i, _f, _vp, _vp, _i, _i, _i, _vp],
     "sbk_gemm_ln": [_i, _vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _i, _f, _vp, _vp, _i, _vp, _vp, _f, _vp, _i, _i, _i,
                     _vp],

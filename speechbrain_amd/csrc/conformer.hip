@@ -757,6 +757,15 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
   FE_TL(13);
 }
 
+// key padding mask from relative lengths (TransformerASR.py:295-301):
+// out[b, t] = t > floor(rel_len[b] * T)   (fp32 product, as torch computes it)
+__global__ void length_mask_kernel(const float* __restrict__ rel_len, int B, int T, uint8_t* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * T) return;
+  const int b = i / T, t = i - b * T;
+  out[i] = (float)t > floorf(rel_len[b] * (float)T) ? 1 : 0;
+}
+
 __global__ void cast_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long long n) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
     y[i] = f32_to_bf16(x[i]);
@@ -922,6 +931,14 @@ SBK_API int sbk_conv_frontend2(int dtype_bf16, const float* x, int B, int Tin, i
   hipLaunchKernelGGL((frontend2_kernel<bf16_t, 64>), grid, dim3(FE_NT), lds, s, x, Tin, Fin, T1, F1, T2, F2, w1, b1, g1,
                      be1, eps1, slope1, reinterpret_cast<const bf16_t*>(wp2), C2, b2, g2, be2, eps2, slope2, out,
                      out_bf16);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+SBK_API int sbk_length_mask(const float* rel_len, int B, int T, uint8_t* out, void* stream) {
+  if (B <= 0 || T <= 0 || !rel_len || !out) return SBK_ERR_ARG;
+  hipLaunchKernelGGL(length_mask_kernel, dim3((B * T + 255) / 256), dim3(256), 0, (hipStream_t)stream, rel_len, B, T,
+                     out);
   SBK_CHECK_LAUNCH();
   return 0;
 }

@@ -110,8 +110,7 @@ class TransformerASR(nn.Module):
         """TransformerASR.py:295-301: arange(T) > floor(wav_len·T) (uint8)."""
         if wav_len is None:
             return None
-        abs_len = torch.floor(wav_len.to(device=device, dtype=_f32) * T)
-        return (torch.arange(T, device=device)[None, :].to(abs_len) > abs_len[:, None]).to(torch.uint8).contiguous()
+        return _enc.length_mask(wav_len.to(device=device), T)
 
     def encode(self, src, wav_len=None):
         """Encoder forward (TransformerASR.py:279-316) → (B, T, d_model) fp32."""

@@ -308,3 +308,15 @@ def test_full_size_encoder_bf16_vs_fp32(dev):
     err = (y16.float() - y32).abs()
     assert y16.dtype == torch.float32 and torch.isfinite(y16).all()
     assert err.max().item() < 0.1 and err.mean().item() < 0.01, (err.max().item(), err.mean().item())
+
+
+def test_length_mask_vs_reference_formula(dev):
+    """sbk_length_mask == (arange(T) > floor(wav_len * T)) (TransformerASR.py:295-301),
+    bit-exact, incl. lengths whose product lands exactly on an integer."""
+    from speechbrain_amd import _enc
+    g = torch.Generator().manual_seed(5)
+    for T in (1, 7, 376, 1000):
+        rel = torch.cat([torch.rand(13, generator=g), torch.tensor([1.0, 0.5, 0.25, 0.0, 0.8, 1 / 3])])
+        ref = (torch.arange(T)[None, :].to(torch.float32) > torch.floor(rel * T)[:, None]).to(torch.uint8)
+        out = _enc.length_mask(rel.to(dev), T).cpu()
+        assert torch.equal(out, ref), T
