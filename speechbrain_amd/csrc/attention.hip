@@ -54,7 +54,7 @@ struct FlashLds {
   static constexpr size_t vt = VLayout<T>::TR ? (size_t)KC * KR * sizeof(T) : (size_t)DHP * VR * sizeof(T);
   static constexpr size_t ps = (size_t)PBR * KR * sizeof(T);
   static constexpr size_t gs = (size_t)4 * GR * GS * 4;
-  static constexpr size_t ms = (size_t)KC * 4;
+  static constexpr size_t ms = (size_t)(KC + 4) * 4;  // key mask + 'chunk has a masked key' flag
   static constexpr size_t bytes = ks + vt + ps + gs + ms;
 };
 
@@ -107,6 +107,7 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
   constexpr int CPR = DHP / VEC; // 16-B chunks per staged row
   constexpr int NKC = KC * CPR / 256;   // K (and V) chunks per thread
   constexpr int NPC = PBR * CPR / 256;  // P-band chunks per thread
+  static_assert(KC == 64, "mask staging: one wave per chunk");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* Ks = reinterpret_cast<T*>(smem);
   T* Vs = reinterpret_cast<T*>(smem + L::ks);
@@ -241,7 +242,11 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
       const int c = tid + 256 * i, rr = c / CPR, d = (c % CPR) * VEC;
       *reinterpret_cast<uint4*>(Ps + rr * KR + d) = sel4(okp[i], rp[i]);
     }
-    if (tid < KC) Ms[tid] = rm;
+    if (tid < KC) {  // wave 0 (KC == 64): mask values and the chunk's any-masked flag
+      Ms[tid] = rm;
+      const bool anym = __any(rm != 0.f);
+      if (tid == 0) reinterpret_cast<int*>(Ms)[KC] = anym;
+    }
   };
   auto stage_scalar = [&](int j0, bool need_v) {  // unaligned head dims (e.g. d=144, H=4)
     const int rbase = Tn - QB - i0 + j0;
@@ -264,7 +269,10 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
     }
     if (tid < KC) {
       const int j = j0 + tid;
-      Ms[tid] = (j < Tn && !(kpm && kpm[(long long)b * Tn + j])) ? 0.f : -INFINITY;
+      const float mv = (j < Tn && !(kpm && kpm[(long long)b * Tn + j])) ? 0.f : -INFINITY;
+      Ms[tid] = mv;
+      const bool anym = __any(mv != 0.f);
+      if (tid == 0) reinterpret_cast<int*>(Ms)[KC] = anym;
     }
   };
 
@@ -328,7 +336,7 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
       ATT_TL(2 + 6 * ch);
       // ---- scores for this lane's query: keys jj = 16t + 4g + r ----
       // (log2 domain: Qu/Qv carry scale * log2(e), probabilities are exp2)
-      const bool masked_chunk = kpm != nullptr || j0 + KC > Tn;  // uniform
+      const bool masked_chunk = __builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(Ms)[KC]) != 0;
       float sc[4][4];
       float cmax = -INFINITY;
 #pragma unroll
