@@ -206,6 +206,85 @@ int sbk_relpos_attention(int dtype_bf16, const void* qkv, const void* pk, const 
 /* LDS bytes one attention workgroup needs (host-side capacity check). */
 long long sbk_relpos_attention_lds(int dtype_bf16, int T, int dh);
 
+/* ------------------------------------------------------------ training path
+ * Backward of the Conformer-Transducer encoder (csrc/backward.hip).  The
+ * dense contractions of the backward (dX = dY W, dW = dY^T X, attention's
+ * batched products) are plain library GEMMs; these entry points are the
+ * element-wise / reduction / layout parts.  *_bf16 flags select bf16 (1)
+ * or fp32 (0) storage per operand. */
+
+/* LayerNorm backward over rows of x (M, D) fp32, D <= 2560 (nn.LayerNorm as
+ * used by normalization.py:172-223, Conformer.py:178,194,340 and the ConvBlock
+ * (freq x channel) norm, convolution.py:169-175):
+ *   dx = rstd (dy g - mean(dy g) - xhat mean(dy g xhat)) (+ dres if non-null);
+ * part (sbk_layernorm_bwd_blocks(M), 2, D) receives per-block [dgamma | dbeta]
+ * partials (reduce with sbk_colsum).  part may be null. */
+int sbk_layernorm_bwd_blocks(int M);
+int sbk_layernorm_bwd(const float* x, const void* dy, int dy_bf16, int M, int D, const float* g, float eps,
+                      const float* dres, float* dx, float* part, void* stream);
+
+/* LayerNorm forward for rows up to D = 2560 (the ConvBlock norm over freq x channels). */
+int sbk_layernorm_wide(const float* x, int M, int D, const float* g, const float* b, float eps, void* y, int y_bf16,
+                       void* stream);
+
+/* out[c] (+)= sum_r part[r, c] (deterministic). */
+int sbk_colsum(const float* part, int rows, int cols, float* out, int accumulate, void* stream);
+
+/* out[c] (+)= sum_r x[r, c]; part: sbk_rowsum_chunks(rows) * cols floats. (Linear bias gradients.) */
+int sbk_rowsum_chunks(long long rows);
+int sbk_rowsum(const void* x, int x_bf16, long long rows, int cols, float* part, float* out, int accumulate,
+               void* stream);
+
+/* Activations and their backward: mode 1 Swish (activations.py:111-142),
+ * 2 GLU over [a | gate] halves of 2*cols inputs (Conformer.py:73-79, nn.GLU(dim=1)),
+ * 3 LeakyReLU(slope) (convolution.py:169-175).  dx has the shape of x. */
+int sbk_act_fwd(int mode, const void* x, int x_bf16, long long rows, int cols, void* y, int y_bf16, float slope,
+                void* stream);
+int sbk_act_bwd(int mode, const void* x, int x_bf16, const void* dy, int dy_bf16, long long rows, int cols, void* dx,
+                int dx_bf16, float slope, void* stream);
+
+/* Depthwise Conv1d over time with bias (Conformer.py:80-86,106; zero pad (K-1)/2,
+ * or K-1 left when causal): x, y (B*T, C). */
+int sbk_dwconv_fwd(const void* x, int x_bf16, int B, int T, int C, const float* w, const float* bias, int K,
+                   int causal, void* y, int y_bf16, void* stream);
+/* Its backward: dx (optional) and per-chunk partials part (sbk_dwconv_wgrad_chunks(B, T), C, K + 1)
+ * of [dw taps | dbias] (reduce with sbk_colsum).  K <= 31. */
+int sbk_dwconv_wgrad_chunks(int B, int T);
+int sbk_dwconv_bwd(const void* x, int x_bf16, const float* dy, int B, int T, int C, const float* w, int K, int causal,
+                   void* dx, int dx_bf16, float* part, void* stream);
+
+/* RelPosMHAXL softmax backward (attention.py:594-631): P (B, H, T, T) fp32
+ * probabilities, dP = dO V^T; dS = scale * P (dP - rowsum(P dP)) (B, H, T, T)
+ * and its pre-rel_shift image dBD (B, H, T, 2T-1) with dBD[i, T-1-i+j] = dS[i, j]
+ * (rel_shift :468-483 transposed), zero outside the band. */
+int sbk_relpos_softmax_bwd(const float* P, const void* dP, int dP_bf16, int B, int H, int T, float scale, void* dS,
+                           void* dBD, int out_bf16, void* stream);
+
+/* Conv2d 3x3 stride 2 "same" reflect padding (CNN.py:616-700) as a GEMM:
+ * x (B, Ti, Fi, Ci) -> col (B*To*Fo, ldcol >= 9*Ci), columns ordered (kt, kf, ci),
+ * zero beyond 9*Ci; col2im is its adjoint (reflected taps folded back), dx (B, Ti, Fi, Ci). */
+int sbk_im2col3s2(const void* x, int x_bf16, int B, int Ti, int Fi, int Ci, int ldcol, void* col, int col_bf16,
+                  void* stream);
+int sbk_col2im3s2(const void* dcol, int dcol_bf16, int B, int Ti, int Fi, int Ci, int ldcol, void* dx, int dx_bf16,
+                  void* stream);
+
+/* Transducer_joint "sum" (transducer_joint.py:57-95): z[b,t,u,:] = act(tn[b,t,:] + pn[b,u,:]),
+ * act 0 none, 3 LeakyReLU(slope), 5 tanh, 6 ReLU; tn (B, T, J), pn (B, U1, J) fp32, z fp32/bf16.
+ * Backward: dtn = sum_u dz act', dpn = sum_t dz act'. */
+int sbk_joint_fwd(const float* tn, const float* pn, int B, int T, int U1, int J, int act, float slope, void* z,
+                  int z_bf16, void* stream);
+int sbk_joint_bwd(const float* tn, const float* pn, const void* dz, int dz_bf16, int B, int T, int U1, int J, int act,
+                  float slope, float* dtn, float* dpn, void* stream);
+
+/* Dropout + residual (nn.Dropout before the residual adds of Conformer.py:242-259,
+ * attention.py:630, convolution.py:175, TransformerASR custom_src_module):
+ *   out = res + alpha * rowmask0(drop_p(x)),  drop_p(x) = keep ? x / (1 - p) : 0,
+ * keep drawn from a counter-based hash of (seed, element index), so the backward is
+ * the same call on dy with res = null.  res / rowmask may be null; p = 0 skips the draw. */
+int sbk_dropout_add(const void* x, int x_bf16, const float* res, long long rows, int cols,
+                    const unsigned char* rowmask, float alpha, float p, unsigned long long seed, void* out,
+                    int out_bf16, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,456 @@
+"""Autograd functions of the training path (config 4: Conformer-Transducer
+under Brain DDP).
+
+The inference path (``_enc`` + the nn.Module drop-ins) fuses whole
+sub-blocks into single kernels and keeps nothing.  When gradients are
+needed the modules run this chain instead: every forward op is still a
+libsbk.so HIP kernel (MFMA GEMM, rel-pos attention, LayerNorm, activations,
+depthwise conv, im2col), and each ``backward`` pairs HIP kernels
+(csrc/backward.hip: LayerNorm / activation / depthwise-conv / softmax
+backward, col2im, joint reductions) with plain library GEMMs (torch.mm →
+hipBLASLt) for the dense dX = dY·W and dW = dYᵀ·X contractions.
+
+Numerics follow torch.autocast: under bf16 the GEMM operands and the
+activations saved for them are bf16, reductions, LayerNorm statistics and the
+residual stream are fp32, and weight gradients are formed from bf16
+operands and returned in fp32.  Without autocast everything is fp32 — the
+parity path checked against autograd of the oracle restatement.
+"""
+import torch
+from torch.autograd import Function
+
+from . import _enc
+from ._lib import check, lib, ptr, stream_of
+
+_f32 = torch.float32
+_bf16 = torch.bfloat16
+
+ACT_CODE = {"swish": 1, "glu": 2, "leaky_relu": 3}
+
+
+def _bf(t):
+    return int(t.dtype == _bf16)
+
+
+def _cont(t):
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def _as(t, dtype):
+    """Row-contiguous t in dtype (fp32 -> bf16 through the HIP cast kernel)."""
+    t = _cont(t)
+    if t.dtype == dtype:
+        return t
+    if dtype == _bf16 and t.dtype == _f32:
+        return _enc.cast_bf16(t)
+    return t.to(dtype)
+
+
+def rowsum(x, out=None, accumulate=False):
+    """(rows, cols) fp32/bf16 -> (cols,) fp32 column sums (Linear bias grads)."""
+    x = _cont(x)
+    rows, cols = x.shape
+    L = lib()
+    part = torch.empty(int(L.sbk_rowsum_chunks(rows)) * cols, device=x.device, dtype=_f32)
+    if out is None:
+        out = torch.empty(cols, device=x.device, dtype=_f32)
+    check(L.sbk_rowsum(ptr(x), _bf(x), rows, cols, ptr(part), ptr(out), int(accumulate), stream_of(x)), "sbk_rowsum")
+    return out
+
+
+def colsum(part, rows, cols):
+    out = torch.empty(cols, device=part.device, dtype=_f32)
+    check(lib().sbk_colsum(ptr(part), rows, cols, ptr(out), 0, stream_of(part)), "sbk_colsum")
+    return out
+
+
+# ------------------------------------------------------- dropout / residual
+def drop_add(x, res=None, alpha=1.0, rowmask=None, p=0.0, seed=0, out_dtype=_f32):
+    """out = res + alpha * rowmask0(dropout_p(x)) — one HIP launch (sbk_dropout_add)."""
+    x = _cont(x)
+    cols = x.shape[-1]
+    rows = x.numel() // cols
+    out = torch.empty(x.shape, device=x.device, dtype=out_dtype)
+    if res is not None and (res.dtype != _f32 or not res.is_contiguous()):
+        raise ValueError("residual must be fp32, contiguous")
+    check(lib().sbk_dropout_add(ptr(x), _bf(x), ptr(res), rows, cols, ptr(rowmask), float(alpha), float(p),
+                                int(seed), ptr(out), _bf(out), stream_of(x)), "sbk_dropout_add")
+    return out
+
+
+def new_seed():
+    """Dropout seed drawn from torch's default CPU generator (no device sync;
+    reproducible under torch.manual_seed)."""
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+class DropAddFn(Function):
+    """res + alpha * rowmask0(Dropout(p)(x)): nn.Dropout followed by the
+    residual adds / masked_fill_ of Conformer.py:242-259, :113-114."""
+
+    @staticmethod
+    def forward(ctx, x, res, alpha, rowmask, p, out_dtype):
+        seed = new_seed() if p > 0 else 0
+        ctx.cfg = (alpha, p, seed, x.dtype)
+        ctx.save_for_backward(rowmask)
+        ctx.has_res = res is not None
+        return drop_add(x, res.detach() if res is not None else None, alpha, rowmask, p, seed, out_dtype)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (rowmask,) = ctx.saved_tensors
+        alpha, p, seed, xdt = ctx.cfg
+        dx = drop_add(dy, None, alpha, rowmask, p, seed, xdt) if ctx.needs_input_grad[0] else None
+        return dx, (dy if ctx.has_res else None), None, None, None, None
+
+
+def dropout(x, p, training, out_dtype=None):
+    out_dtype = x.dtype if out_dtype is None else out_dtype
+    if not training or p == 0:
+        return x if x.dtype == out_dtype else _as(x, out_dtype)
+    return DropAddFn.apply(x, None, 1.0, None, float(p), out_dtype)
+
+
+class CastFn(Function):
+    """Differentiable fp32 <-> bf16 cast (HIP cast kernel forward)."""
+
+    @staticmethod
+    def forward(ctx, x, dtype):
+        ctx.src = x.dtype
+        return _as(x, dtype)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return _as(dy, ctx.src), None
+
+
+def to_dtype(x, dtype):
+    x = _cont(x)
+    return x if x.dtype == dtype else CastFn.apply(x, dtype)
+
+
+# --------------------------------------------------------------------- Linear
+class LinearFn(Function):
+    """y = res + alpha * rowmask0(a @ w.T + b) (nn.Linear / 1x1 Conv1d;
+    linear.py:15-76, attention.py:549-553,581,636,823-839, Conformer.py:73-92),
+    residual, scale and row mask fused into the MFMA GEMM epilogue.
+    a (M, K) in the compute dtype; w the fp32 parameter; wk its kernel copy."""
+
+    @staticmethod
+    def forward(ctx, a, w, bias, wk, out_dtype, res, alpha, rowmask):
+        out = _enc.gemm(a, wk, bias=None if bias is None else bias.detach(), res=None if res is None else
+                        res.detach(), alpha=alpha, rowmask=rowmask, out_dtype=out_dtype)
+        ctx.save_for_backward(a, wk, rowmask)
+        ctx.wshape = tuple(w.shape)
+        ctx.has_bias = bias is not None
+        ctx.has_res = res is not None
+        ctx.alpha = alpha
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        a, wk, rowmask = ctx.saved_tensors
+        if ctx.alpha != 1.0 or rowmask is not None:
+            g = drop_add(dy, None, ctx.alpha, rowmask, 0.0, 0, a.dtype)
+            gb = g if a.dtype == _f32 else None
+        else:
+            g = _as(dy, a.dtype)
+            gb = dy
+        da = torch.mm(g, wk) if ctx.needs_input_grad[0] else None
+        dw = torch.mm(g.t(), a).float().view(ctx.wshape) if ctx.needs_input_grad[1] else None
+        db = None
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = rowsum(gb if gb is not None else drop_add(dy, None, ctx.alpha, rowmask, 0.0, 0, _f32))
+        dres = dy if ctx.has_res and ctx.needs_input_grad[5] else None
+        return da, dw, db, None, None, dres, None, None
+
+
+def kernel_weight(w, dtype, cache, key):
+    """Kernel-ready copy of a weight (bf16 cast cached per parameter version)."""
+    w2 = w.detach().reshape(w.shape[0], -1)  # Conv1d (N, K, 1) weights as (N, K)
+    if dtype == _f32:
+        return _cont(w2)
+    return cache.get(key, [w], lambda: _enc.cast_bf16(_cont(w2)))
+
+
+def linear(a, w, bias, dtype, cache, key, out_dtype=_f32, res=None, alpha=1.0, rowmask=None):
+    """Linear through LinearFn; a is cast to the compute dtype first."""
+    return LinearFn.apply(to_dtype(a, dtype), w, bias, kernel_weight(w, dtype, cache, key), out_dtype, res, alpha,
+                          rowmask)
+
+
+# ------------------------------------------------------------------ LayerNorm
+class LayerNormFn(Function):
+    """Row LayerNorm of fp32 x (M, D) (normalization.py:172-223, nn.LayerNorm)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps, out_dtype):
+        x = _cont(x)
+        M, D = x.shape
+        if D <= 1024:
+            y, _ = _enc.layernorm(x, w.detach().reshape(-1), b.detach().reshape(-1), eps, out1_dtype=out_dtype)
+        else:
+            y = torch.empty(M, D, device=x.device, dtype=out_dtype)
+            check(lib().sbk_layernorm_wide(ptr(x), M, D, ptr(w.detach()), ptr(b.detach()), float(eps), ptr(y),
+                                           _bf(y), stream_of(x)), "sbk_layernorm_wide")
+        ctx.save_for_backward(x, w)
+        ctx.eps = eps
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = _cont(dy)
+        M, D = x.shape
+        L = lib()
+        nblk = int(L.sbk_layernorm_bwd_blocks(M))
+        part = torch.empty(nblk * 2 * D, device=x.device, dtype=_f32)
+        dx = torch.empty(M, D, device=x.device, dtype=_f32)
+        check(L.sbk_layernorm_bwd(ptr(x), ptr(dy), _bf(dy), M, D, ptr(w.detach()), float(ctx.eps), None, ptr(dx),
+                                  ptr(part), stream_of(x)), "sbk_layernorm_bwd")
+        gb = colsum(part, nblk, 2 * D)
+        return dx, gb[:D].view_as(w), gb[D:].view_as(w), None, None
+
+
+def layer_norm(x, mod, out_dtype=_f32):
+    return LayerNormFn.apply(x, mod.weight, mod.bias, mod.eps, out_dtype)
+
+
+# ---------------------------------------------------------------- activations
+class ActFn(Function):
+    """Swish / GLU / LeakyReLU (activations.py:111-142, Conformer.py:73-79,
+    convolution.py:169-175).  GLU halves the last dim ([a | gate])."""
+
+    @staticmethod
+    def forward(ctx, x, mode, slope, out_dtype):
+        x = _cont(x)
+        rows = x.shape[0]
+        cols = x.shape[1] // 2 if mode == 2 else x.shape[1]
+        y = torch.empty(rows, cols, device=x.device, dtype=out_dtype)
+        check(lib().sbk_act_fwd(mode, ptr(x), _bf(x), rows, cols, ptr(y), _bf(y), float(slope), stream_of(x)),
+              "sbk_act_fwd")
+        ctx.save_for_backward(x)
+        ctx.mode, ctx.slope, ctx.cols = mode, slope, cols
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = _cont(dy)
+        dx = torch.empty_like(x)
+        check(lib().sbk_act_bwd(ctx.mode, ptr(x), _bf(x), ptr(dy), _bf(dy), x.shape[0], ctx.cols, ptr(dx), _bf(dx),
+                                float(ctx.slope), stream_of(x)), "sbk_act_bwd")
+        return dx, None, None, None
+
+
+def act(x, name, slope=0.0, out_dtype=None):
+    return ActFn.apply(x, ACT_CODE[name], slope, x.dtype if out_dtype is None else out_dtype)
+
+
+# ------------------------------------------------------------ depthwise conv
+class DwConvFn(Function):
+    """Depthwise Conv1d over time + bias (Conformer.py:80-86,106).
+    g (B*T, C) in the compute dtype -> (B*T, C) fp32."""
+
+    @staticmethod
+    def forward(ctx, g, w, bias, B, T, causal):
+        g = _cont(g)
+        C = g.shape[1]
+        K = w.shape[-1]
+        y = torch.empty(B * T, C, device=g.device, dtype=_f32)
+        wk = _cont(w.detach().reshape(C, K))
+        check(lib().sbk_dwconv_fwd(ptr(g), _bf(g), B, T, C, ptr(wk), ptr(None if bias is None else bias.detach()), K,
+                                   int(causal), ptr(y), 0, stream_of(g)), "sbk_dwconv_fwd")
+        ctx.save_for_backward(g, wk)
+        ctx.dims = (B, T, C, K, causal, bias is not None, tuple(w.shape))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        g, wk = ctx.saved_tensors
+        B, T, C, K, causal, has_bias, wshape = ctx.dims
+        dy = _as(dy, _f32)
+        L = lib()
+        nch = int(L.sbk_dwconv_wgrad_chunks(B, T))
+        part = torch.empty(nch * C * (K + 1), device=g.device, dtype=_f32)
+        dg = torch.empty_like(g) if ctx.needs_input_grad[0] else None
+        check(L.sbk_dwconv_bwd(ptr(g), _bf(g), ptr(dy), B, T, C, ptr(wk), K, int(causal), ptr(dg),
+                               _bf(g), ptr(part), stream_of(g)), "sbk_dwconv_bwd")
+        red = colsum(part, nch, C * (K + 1)).view(C, K + 1)
+        dw = red[:, :K].reshape(wshape)
+        db = red[:, K].contiguous() if has_bias else None
+        return dg, dw, db, None, None, None
+
+
+# ------------------------------------------------------ rel-pos attention
+class RelPosAttentionFn(Function):
+    """RelPosMHAXL core (attention.py:566-631, rel_shift :468-483).
+    qkv (B*T, 3d) head-interleaved, pk (2T-1, d), both in the compute dtype;
+    pbu / pbv the (dh, H) parameters (read as (H, dh), attention.py:584-590).
+    Returns (out (B*T, d), probs (B, H, T, T) fp32, no grad)."""
+
+    @staticmethod
+    def forward(ctx, qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale, p=0.0):
+        qkv, pk = _cont(qkv), _cont(pk)
+        o, P = _enc.relpos_attention(qkv, pk, pbu.detach(), pbv.detach(), kpm, B, T, H, dh, scale, need_probs=True)
+        seed = 0
+        attn = P
+        if p > 0:
+            # attention-probability dropout (attention.py:626): o = drop(P) V
+            seed = new_seed()
+            attn = drop_add(P, None, 1.0, None, p, seed, _f32)
+            v = qkv.view(B, T, H, 3, dh)[:, :, :, 2].permute(0, 2, 1, 3)
+            o = torch.matmul(_as(attn, qkv.dtype), v).permute(0, 2, 1, 3).reshape(B * T, H * dh)
+        ctx.save_for_backward(qkv, pk, pbu, pbv, P, attn)
+        ctx.dims = (B, T, H, dh, scale, p, seed)
+        ctx.mark_non_differentiable(attn)
+        return o, attn
+
+    @staticmethod
+    def backward(ctx, do, _dP_unused):
+        qkv, pk, pbu, pbv, P, attn = ctx.saved_tensors
+        B, T, H, dh, scale, p, seed = ctx.dims
+        dt = qkv.dtype
+        W = 2 * T - 1
+        q5 = qkv.view(B, T, H, 3, dh)
+        q = q5[:, :, :, 0].permute(0, 2, 1, 3)  # (B, H, T, dh) views
+        k = q5[:, :, :, 1].permute(0, 2, 1, 3)
+        v = q5[:, :, :, 2].permute(0, 2, 1, 3)
+        pkh = pk.view(W, H, dh).permute(1, 0, 2)  # (H, W, dh)
+        do_h = _as(do, dt).view(B, T, H, dh).permute(0, 2, 1, 3)
+        Pc = _enc.cast_bf16(attn) if dt == _bf16 else attn
+        dv = torch.matmul(Pc.transpose(-1, -2), do_h)  # (B, H, T, dh)
+        dP = torch.matmul(do_h, v.transpose(-1, -2))  # (B, H, T, T)
+        dP = _cont(dP)
+        if p > 0:
+            dP = drop_add(dP, None, 1.0, None, p, seed, dP.dtype)
+        dS = torch.empty(B, H, T, T, device=qkv.device, dtype=dt)
+        dBD = torch.empty(B, H, T, W, device=qkv.device, dtype=dt)
+        check(lib().sbk_relpos_softmax_bwd(ptr(P), ptr(dP), _bf(dP), B, H, T, float(scale), ptr(dS), ptr(dBD), _bf(dS),
+                                           stream_of(P)), "sbk_relpos_softmax_bwd")
+        u = pbu.detach().reshape(H, 1, dh).to(dt)
+        vb = pbv.detach().reshape(H, 1, dh).to(dt)
+        dq_ac = torch.matmul(dS, k)  # (B, H, T, dh)
+        dq_bd = torch.matmul(dBD, pkh.unsqueeze(0))  # (B, H, T, dh)
+        dk = torch.matmul(dS.transpose(-1, -2), q + u)
+        # dpk[h] = sum_b dBD[b, h]^T (q + v)[b, h]
+        qv = (q + vb).permute(1, 0, 2, 3).reshape(H, B * T, dh)
+        dBD_h = dBD.permute(1, 3, 0, 2).reshape(H, W, B * T)
+        dpk = torch.matmul(dBD_h, qv)  # (H, W, dh)
+        dq = dq_ac + dq_bd
+        dqkv = torch.stack([dq, dk, dv], dim=3)  # (B, H, T, 3, dh)
+        dqkv = dqkv.permute(0, 2, 1, 3, 4).reshape(B * T, 3 * H * dh)
+        dpk = dpk.permute(1, 0, 2).reshape(W, H * dh)
+        dpbu = dq_ac.float().sum(dim=(0, 2)).reshape(pbu.shape)
+        dpbv = dq_bd.float().sum(dim=(0, 2)).reshape(pbv.shape)
+        return dqkv, dpk, dpbu, dpbv, None, None, None, None, None, None, None
+
+
+# --------------------------------------------------------------- ConvBlock
+class ConvBlockFn(Function):
+    """ConvBlock with one layer (convolution.py:112-175): Conv2d 3x3 stride 2
+    "same" reflect padding (CNN.py:616-700) -> LayerNorm over (freq, chan)
+    -> LeakyReLU, as im2col (HIP) + MFMA GEMM + wide LayerNorm + activation.
+    x (B, Ti, Fi, Ci) -> (B, To, Fo, Co)."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, ln_w, ln_b, eps, slope, dtype, out_dtype):
+        x = _cont(x)
+        B, Ti, Fi, Ci = x.shape
+        Co = w.shape[0]
+        To, Fo = (Ti - 1) // 2 + 1, (Fi - 1) // 2 + 1
+        vec = 8 if dtype == _bf16 else 4
+        ldcol = -(-9 * Ci // vec) * vec
+        N = B * To * Fo
+        L = lib()
+        s = stream_of(x)
+        col = torch.empty(N, ldcol, device=x.device, dtype=dtype)
+        check(L.sbk_im2col3s2(ptr(x), _bf(x), B, Ti, Fi, Ci, ldcol, ptr(col), _bf(col), s), "sbk_im2col3s2")
+        # weight (Co, Ci, kf, kt) -> (Co, kt, kf, Ci) -> (Co, ldcol)
+        wp = torch.zeros(Co, ldcol, device=x.device, dtype=_f32)
+        wp[:, : 9 * Ci] = w.detach().permute(0, 3, 2, 1).reshape(Co, 9 * Ci)
+        wk = _as(wp, dtype)
+        c = _enc.gemm(col, wk, bias=None if bias is None else bias.detach(), out_dtype=_f32)
+        c2 = c.view(B * To, Fo * Co)
+        n = torch.empty(B * To, Fo * Co, device=x.device, dtype=_f32)
+        check(L.sbk_layernorm_wide(ptr(c2), B * To, Fo * Co, ptr(ln_w.detach()), ptr(ln_b.detach()), float(eps),
+                                   ptr(n), 0, s), "sbk_layernorm_wide")
+        y = torch.empty(B * To, Fo * Co, device=x.device, dtype=out_dtype)
+        check(L.sbk_act_fwd(3, ptr(n), 0, B * To, Fo * Co, ptr(y), _bf(y), float(slope), s), "sbk_act_fwd")
+        ctx.save_for_backward(col, wk, c2, n, ln_w)
+        ctx.dims = (B, Ti, Fi, Ci, Co, To, Fo, ldcol, eps, slope, bias is not None, tuple(w.shape), x.dtype)
+        return y.view(B, To, Fo, Co)
+
+    @staticmethod
+    def backward(ctx, dy):
+        col, wk, c2, n, ln_w = ctx.saved_tensors
+        B, Ti, Fi, Ci, Co, To, Fo, ldcol, eps, slope, has_bias, wshape, xdt = ctx.dims
+        L = lib()
+        s = stream_of(col)
+        dy = _cont(dy).view(B * To, Fo * Co)
+        dn = torch.empty(B * To, Fo * Co, device=col.device, dtype=_f32)
+        check(L.sbk_act_bwd(3, ptr(n), 0, ptr(dy), _bf(dy), B * To, Fo * Co, ptr(dn), 0, float(slope), s),
+              "sbk_act_bwd")
+        nblk = int(L.sbk_layernorm_bwd_blocks(B * To))
+        D = Fo * Co
+        part = torch.empty(nblk * 2 * D, device=col.device, dtype=_f32)
+        dc = torch.empty(B * To, D, device=col.device, dtype=_f32)
+        check(L.sbk_layernorm_bwd(ptr(c2), ptr(dn), 0, B * To, D, ptr(ln_w.detach()), float(eps), None, ptr(dc),
+                                  ptr(part), s), "sbk_layernorm_bwd")
+        gb = colsum(part, nblk, 2 * D)
+        dlw, dlb = gb[:D].view_as(ln_w), gb[D:].view_as(ln_w)
+        dc = dc.view(B * To * Fo, Co)
+        g = _as(dc, col.dtype)
+        dwp = torch.mm(g.t(), col).float()  # (Co, ldcol)
+        dw = dwp[:, : 9 * Ci].reshape(Co, 3, 3, Ci).permute(0, 3, 2, 1).reshape(wshape)
+        db = rowsum(dc) if has_bias else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dcol = torch.mm(g, wk)  # (N, ldcol)
+            dx = torch.empty(B, Ti, Fi, Ci, device=col.device, dtype=xdt)
+            check(L.sbk_col2im3s2(ptr(dcol), _bf(dcol), B, Ti, Fi, Ci, ldcol, ptr(dx), _bf(dx), s), "sbk_col2im3s2")
+        return dx, dw, db, dlw, dlb, None, None, None, None
+
+
+# ---------------------------------------------------------- transducer joint
+class JointFn(Function):
+    """Transducer_joint "sum" + nonlinearity (transducer_joint.py:57-95):
+    tn (B, T, J), pn (B, U1, J) fp32 -> z (B, T, U1, J)."""
+
+    @staticmethod
+    def forward(ctx, tn, pn, act_code, slope, out_dtype):
+        tn, pn = _as(tn, _f32), _as(pn, _f32)
+        B, T, J = tn.shape
+        U1 = pn.shape[1]
+        z = torch.empty(B, T, U1, J, device=tn.device, dtype=out_dtype)
+        check(lib().sbk_joint_fwd(ptr(tn), ptr(pn), B, T, U1, J, act_code, float(slope), ptr(z), _bf(z),
+                                  stream_of(tn)), "sbk_joint_fwd")
+        ctx.save_for_backward(tn, pn)
+        ctx.a = (act_code, slope)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        tn, pn = ctx.saved_tensors
+        B, T, J = tn.shape
+        U1 = pn.shape[1]
+        dz = _cont(dz)
+        dtn = torch.empty_like(tn)
+        dpn = torch.empty_like(pn)
+        check(lib().sbk_joint_bwd(ptr(tn), ptr(pn), ptr(dz), _bf(dz), B, T, U1, J, ctx.a[0], float(ctx.a[1]), ptr(dtn),
+                                  ptr(dpn), stream_of(tn)), "sbk_joint_bwd")
+        return dtn, dpn, None, None, None
+
+
+def needs_grad(*tensors_or_modules):
+    """True when autograd must see this call (grad mode on and something requires grad)."""
+    if not torch.is_grad_enabled():
+        return False
+    for t in tensors_or_modules:
+        if isinstance(t, torch.Tensor):
+            if t.requires_grad:
+                return True
+        elif isinstance(t, torch.nn.Module):
+            if any(p.requires_grad for p in t.parameters()):
+                return True
+    return False

@@ -64,6 +64,24 @@ SIGNATURES = {
     # attention.hip
     "sbk_relpos_attention": [_i, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _vp],
     "sbk_relpos_attention_lds": [_i, _i, _i],
+    # backward.hip (training path)
+    "sbk_layernorm_bwd_blocks": [_i],
+    "sbk_layernorm_bwd": [_vp, _vp, _i, _i, _i, _vp, _f, _vp, _vp, _vp, _vp],
+    "sbk_layernorm_wide": [_vp, _i, _i, _vp, _vp, _f, _vp, _i, _vp],
+    "sbk_colsum": [_vp, _i, _i, _vp, _i, _vp],
+    "sbk_rowsum_chunks": [_ll],
+    "sbk_rowsum": [_vp, _i, _ll, _i, _vp, _vp, _i, _vp],
+    "sbk_act_fwd": [_i, _vp, _i, _ll, _i, _vp, _i, _f, _vp],
+    "sbk_act_bwd": [_i, _vp, _i, _vp, _i, _ll, _i, _vp, _i, _f, _vp],
+    "sbk_dwconv_fwd": [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _i, _vp],
+    "sbk_dwconv_wgrad_chunks": [_i, _i],
+    "sbk_dwconv_bwd": [_vp, _i, _vp, _i, _i, _i, _vp, _i, _i, _vp, _i, _vp, _vp],
+    "sbk_relpos_softmax_bwd": [_vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _i, _vp],
+    "sbk_im2col3s2": [_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp],
+    "sbk_col2im3s2": [_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp],
+    "sbk_joint_fwd": [_vp, _vp, _i, _i, _i, _i, _i, _f, _vp, _i, _vp],
+    "sbk_dropout_add": [_vp, _i, _vp, _ll, _i, _vp, _f, _f, ctypes.c_ulonglong, _vp, _i, _vp],
+    "sbk_joint_bwd": [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp],
 }
 RESTYPES = {"sbk_relpos_attention_lds": ctypes.c_longlong, "sbk_rnnt_workspace_floats": ctypes.c_longlong}
 

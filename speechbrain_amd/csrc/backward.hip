@@ -1,0 +1,660 @@
+// Training-path kernels (backward of the Conformer-Transducer hot path).
+//
+// The forward inference path fuses aggressively (ffn.hip, attention.hip,
+// conformer.hip).  Training needs the intermediate activations, so the
+// autograd path (speechbrain_amd/_autograd.py) runs the same arithmetic as a
+// chain of smaller launches and differentiates each:
+//
+//   LayerNorm backward            nn.LayerNorm (normalization.py:172-223), row
+//                                 LNs of the Conformer and the (freq x chan)
+//                                 LN of ConvBlock (convolution.py:169-175)
+//   activations fwd/bwd           Swish (activations.py:111-142), GLU
+//                                 (Conformer.py:73-79), LeakyReLU
+//   depthwise conv fwd/bwd        Conformer.py:80-86,106
+//   rel-pos softmax backward      attention.py:594-631 (softmax, rel_shift
+//                                 :468-483 transposed into the band layout)
+//   im2col / col2im (reflect)     Conv2d "same" reflect padding
+//                                 (CNN.py:616-700) for the ConvBlock GEMMs
+//   transducer joint fwd/bwd      transducer_joint.py:57-95 ("sum" + act)
+//
+// Dense contractions of the backward (dX = dY W, dW = dY^T X, the attention
+// batched products) are plain library GEMMs (hipBLASLt through torch.mm);
+// everything here is bandwidth-bound elementwise / reduction work: coalesced
+// rows, one wave per row where a row reduction is needed, deterministic
+// per-block partial sums (no float atomics) reduced by sbk_colsum.
+#include "mfma.h"
+
+#include <algorithm>
+
+using namespace sbk;
+
+namespace {
+
+__device__ __forceinline__ float ldv(const void* p, long long i, int bf) {
+  return bf ? bf16_to_f32(reinterpret_cast<const bf16_t*>(p)[i]) : reinterpret_cast<const float*>(p)[i];
+}
+__device__ __forceinline__ void stv(void* p, long long i, float v, int bf) {
+  if (bf)
+    reinterpret_cast<bf16_t*>(p)[i] = f32_to_bf16(v);
+  else
+    reinterpret_cast<float*>(p)[i] = v;
+}
+
+inline int grid_for(long long n, int block, int cap = 16384) {
+  long long g = (n + block - 1) / block;
+  return (int)(g > cap ? cap : (g < 1 ? 1 : g));
+}
+
+// ---------------------------------------------------------------- LayerNorm
+// One wave per row (grid-stride over rows); lane owns columns lane + 64 i.
+//   xhat = (x - mean) * rstd, gy = dy * g
+//   dx   = rstd * (gy - mean(gy) - xhat * mean(gy * xhat))   (+ dres)
+//   dg  += dy * xhat, db += dy     (per-block partials, rows fixed per block)
+template <int PER>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(const float* __restrict__ x, const void* __restrict__ dy,
+                                                     int dy_bf16, int M, int D, const float* __restrict__ g,
+                                                     float eps, const float* __restrict__ dres,
+                                                     float* __restrict__ dx, float* __restrict__ part) {
+  __shared__ float red[2 * 64 * PER];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float ag[PER], ab[PER], gg[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    ag[i] = 0.f;
+    ab[i] = 0.f;
+    gg[i] = c < D ? g[c] : 0.f;
+  }
+  const float invD = 1.0f / D;
+  for (long long row = (long long)blockIdx.x * 4 + w; row < M; row += (long long)gridDim.x * 4) {
+    const float* xr = x + row * D;
+    float v[PER], d[PER];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      v[i] = c < D ? xr[c] : 0.f;
+      d[i] = c < D ? ldv(dy, row * D + c, dy_bf16) : 0.f;
+      s += v[i];
+    }
+    const float mean = wave_sum(s) * invD;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      const float t = c < D ? v[i] - mean : 0.f;
+      q += t * t;
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) * invD + eps);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      v[i] = (v[i] - mean) * rstd;  // xhat (0 beyond D since d == 0 there)
+      const float gy = d[i] * gg[i];
+      s1 += gy;
+      s2 += gy * v[i];
+      ag[i] += d[i] * v[i];
+      ab[i] += d[i];
+    }
+    s1 = wave_sum(s1) * invD;
+    s2 = wave_sum(s2) * invD;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      if (c < D) {
+        float r = rstd * (d[i] * gg[i] - s1 - v[i] * s2);
+        if (dres) r += dres[row * D + c];
+        dx[row * D + c] = r;
+      }
+    }
+  }
+  if (!part) return;
+  // waves add their column partials into one LDS slab in turn
+  for (int ww = 0; ww < 4; ++ww) {
+    if (w == ww) {
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        red[lane + 64 * i] = ww ? red[lane + 64 * i] + ag[i] : ag[i];
+        red[64 * PER + lane + 64 * i] = ww ? red[64 * PER + lane + 64 * i] + ab[i] : ab[i];
+      }
+    }
+    __syncthreads();
+  }
+  for (int c = threadIdx.x; c < D; c += blockDim.x) {
+    part[(long long)blockIdx.x * 2 * D + c] = red[c];
+    part[(long long)blockIdx.x * 2 * D + D + c] = red[64 * PER + c];
+  }
+}
+
+// Row LayerNorm forward for the wide (freq x channel) rows of ConvBlock
+// (D up to 2560): one wave per row; y fp32 or bf16.
+template <int PER>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x, int M, int D,
+                                                     const float* __restrict__ g, const float* __restrict__ b,
+                                                     float eps, void* __restrict__ y, int y_bf16) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float* xr = x + row * D;
+  float v[PER];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < D ? xr[c] : 0.f;
+    s += v[i];
+  }
+  const float mean = wave_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    const float t = c < D ? v[i] - mean : 0.f;
+    q += t * t;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / D + eps);
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    if (c < D) stv(y, row * D + c, (v[i] - mean) * rstd * g[c] + b[c], y_bf16);
+  }
+}
+
+// part[j, c] = sum of x[r, c] over rows r of chunk j (thread per column).
+__global__ void rowsum_partial_kernel(const void* __restrict__ x, int x_bf16, long long rows, int cols, int rows_per,
+                                      float* __restrict__ part) {
+  const int c = blockIdx.y * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  const long long r0 = (long long)blockIdx.x * rows_per;
+  const long long r1 = min(r0 + rows_per, rows);
+  float s = 0.f;
+  for (long long r = r0; r < r1; ++r) s += ldv(x, r * cols + c, x_bf16);
+  part[(long long)blockIdx.x * cols + c] = s;
+}
+
+// out[c] (+)= sum_r part[r, c]  — deterministic column reduction.
+__global__ void colsum_kernel(const float* __restrict__ part, int rows, int cols, float* __restrict__ out,
+                              int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int r = 0; r < rows; ++r) s += part[(long long)r * cols + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+// ------------------------------------------------------------- activations
+// mode 1 Swish y = x sigmoid(x); 2 GLU y = a sigmoid(b), x = [a | b] (2 cols);
+// 3 LeakyReLU(slope).  rows x cols outputs.
+__global__ void act_fwd_kernel(int mode, const void* __restrict__ x, int x_bf16, long long rows, int cols,
+                               void* __restrict__ y, int y_bf16, float slope) {
+  const long long n = rows * cols;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    float r;
+    if (mode == 2) {
+      const long long row = i / cols, c = i - row * cols;
+      const float a = ldv(x, row * 2 * cols + c, x_bf16), b = ldv(x, row * 2 * cols + cols + c, x_bf16);
+      r = a * (1.0f / (1.0f + expf(-b)));
+    } else {
+      const float v = ldv(x, i, x_bf16);
+      r = mode == 1 ? v * (1.0f / (1.0f + expf(-v))) : (v >= 0.f ? v : v * slope);
+    }
+    stv(y, i, r, y_bf16);
+  }
+}
+
+// Backward of act_fwd_kernel; dx has the shape of x (GLU: rows x 2 cols).
+__global__ void act_bwd_kernel(int mode, const void* __restrict__ x, int x_bf16, const void* __restrict__ dy,
+                               int dy_bf16, long long rows, int cols, void* __restrict__ dx, int dx_bf16,
+                               float slope) {
+  const long long n = rows * cols;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float g = ldv(dy, i, dy_bf16);
+    if (mode == 2) {
+      const long long row = i / cols, c = i - row * cols;
+      const long long ia = row * 2 * cols + c, ib = ia + cols;
+      const float a = ldv(x, ia, x_bf16), b = ldv(x, ib, x_bf16);
+      const float s = 1.0f / (1.0f + expf(-b));
+      stv(dx, ia, g * s, dx_bf16);
+      stv(dx, ib, g * a * s * (1.0f - s), dx_bf16);
+    } else if (mode == 1) {
+      const float v = ldv(x, i, x_bf16);
+      const float s = 1.0f / (1.0f + expf(-v));
+      stv(dx, i, g * (s + v * s * (1.0f - s)), dx_bf16);
+    } else {
+      const float v = ldv(x, i, x_bf16);
+      stv(dx, i, v > 0.f ? g : g * slope, dx_bf16);
+    }
+  }
+}
+
+// ------------------------------------------------------- depthwise conv1d
+// y[b, t, c] = bias[c] + sum_k w[c, k] x[b, t + k - padL, c]   (zero padding)
+__global__ void dwconv_fwd_kernel(const void* __restrict__ x, int x_bf16, int B, int T, int C,
+                                  const float* __restrict__ w, const float* __restrict__ bias, int K, int padL,
+                                  void* __restrict__ y, int y_bf16) {
+  const long long n = (long long)B * T * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long bt = i / C;
+    const int t = (int)(bt % T);
+    const long long base = (bt - t) * C + c;
+    float s = bias ? bias[c] : 0.f;
+    for (int k = 0; k < K; ++k) {
+      const int ts = t + k - padL;
+      if (ts >= 0 && ts < T) s += w[c * K + k] * ldv(x, base + (long long)ts * C, x_bf16);
+    }
+    stv(y, i, s, y_bf16);
+  }
+}
+
+// dx[b, t, c] = sum_k w[c, k] dy[b, t - k + padL, c]
+__global__ void dwconv_dgrad_kernel(const float* __restrict__ dy, int B, int T, int C, const float* __restrict__ w,
+                                    int K, int padL, void* __restrict__ dx, int dx_bf16) {
+  const long long n = (long long)B * T * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long bt = i / C;
+    const int t = (int)(bt % T);
+    const long long base = (bt - t) * C + c;
+    float s = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const int to = t - k + padL;
+      if (to >= 0 && to < T) s += w[c * K + k] * dy[base + (long long)to * C];
+    }
+    stv(dx, i, s, dx_bf16);
+  }
+}
+
+// Per-chunk partial weight / bias gradients: chunk j covers sequence rows
+// [j*rows_per, (j+1)*rows_per) of one utterance-major (B*T) list; one thread
+// per channel accumulates its K taps.  part: (nchunk, C, K + 1) [taps | bias].
+template <int KMAX>
+__global__ void __launch_bounds__(256) dwconv_wgrad_kernel(const void* __restrict__ x, int x_bf16,
+                                                           const float* __restrict__ dy, int B, int T, int C, int K,
+                                                           int padL, int rows_per, float* __restrict__ part) {
+  const int c = blockIdx.y * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float acc[KMAX + 1];
+#pragma unroll
+  for (int k = 0; k <= KMAX; ++k) acc[k] = 0.f;
+  const long long r0 = (long long)blockIdx.x * rows_per;
+  const long long r1 = min(r0 + rows_per, (long long)B * T);
+  for (long long r = r0; r < r1; ++r) {
+    const int t = (int)(r % T);
+    const long long base = (r - t) * C + c;
+    const float g = dy[r * C + c];
+    acc[KMAX] += g;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      if (k < K) {
+        const int ts = t + k - padL;
+        if (ts >= 0 && ts < T) acc[k] += g * ldv(x, base + (long long)ts * C, x_bf16);
+      }
+    }
+  }
+  float* p = part + ((long long)blockIdx.x * C + c) * (K + 1);
+  for (int k = 0; k < K; ++k) p[k] = acc[k];
+  p[K] = acc[KMAX];
+}
+
+// -------------------------------------------------- rel-pos softmax backward
+// One block per score row (b, h, i).  P (B, H, T, T) fp32 probabilities,
+// dP = dO V^T.  dS = scale * P * (dP - sum_j P dP); the positional branch's
+// gradient in the pre-shift layout dBD[i, r] = dS[i, j] with r = T-1-i+j
+// (the inverse of rel_shift, attention.py:468-483), zero outside the band.
+__global__ void __launch_bounds__(256) relpos_softmax_bwd_kernel(const float* __restrict__ P,
+                                                                 const void* __restrict__ dP, int dP_bf16, int T,
+                                                                 float scale, void* __restrict__ dS,
+                                                                 void* __restrict__ dBD, int out_bf16) {
+  __shared__ float red[16];
+  const long long row = blockIdx.x;
+  const int i = (int)(row % T);
+  const float* pr = P + row * T;
+  float s = 0.f;
+  for (int j = threadIdx.x; j < T; j += blockDim.x) s += pr[j] * ldv(dP, row * T + j, dP_bf16);
+  s = block_sum(s, red);
+  const int W = 2 * T - 1;
+  for (int r = threadIdx.x; r < W; r += blockDim.x) {
+    const int j = r - (T - 1 - i);
+    float v = 0.f;
+    if (j >= 0 && j < T) {
+      v = scale * pr[j] * (ldv(dP, row * T + j, dP_bf16) - s);
+      stv(dS, row * T + j, v, out_bf16);
+    }
+    stv(dBD, row * W + r, v, out_bf16);
+  }
+}
+
+// ------------------------------------------- ConvBlock im2col / col2im
+// Conv2d k3 stride 2 "same" reflect padding (pad 1 each side, CNN.py:659-700,
+// get_padding_elem :1459-1481).  x (B, Ti, Fi, Ci); col (B*To*Fo, 9*Ci) with
+// column order (kt, kf, ci) — the (Cout, kt, kf, Ci) weight permutation.
+__device__ __forceinline__ int reflect1(int p, int n) {  // padded index p -> source index
+  const int s = p - 1;
+  return s < 0 ? -s : (s >= n ? 2 * n - 2 - s : s);
+}
+
+__global__ void im2col3s2_kernel(const void* __restrict__ x, int x_bf16, int B, int Ti, int Fi, int Ci, int To,
+                                 int Fo, int ldcol, void* __restrict__ col, int col_bf16) {
+  const long long n = (long long)B * To * Fo * ldcol;
+  const int kcols = 9 * Ci;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int kk = (int)(i % ldcol);
+    long long q = i / ldcol;
+    if (kk >= kcols) {  // K padding up to the GEMM's vector width
+      stv(col, i, 0.f, col_bf16);
+      continue;
+    }
+    const int ci = kk % Ci;
+    const int kf = (kk / Ci) % 3;
+    const int kt = kk / (3 * Ci);
+    const int fo = (int)(q % Fo); q /= Fo;
+    const int to = (int)(q % To);
+    const int b = (int)(q / To);
+    const int ti = reflect1(2 * to + kt, Ti), fi = reflect1(2 * fo + kf, Fi);
+    stv(col, i, ldv(x, (((long long)b * Ti + ti) * Fi + fi) * Ci + ci, x_bf16), col_bf16);
+  }
+}
+
+// dx[b, ti, fi, ci] = sum over padded positions (pt, pf) that reflect onto
+// (ti, fi) and taps (kt, kf) with pt = 2 to + kt, pf = 2 fo + kf of dcol.
+__global__ void col2im3s2_kernel(const void* __restrict__ dcol, int dcol_bf16, int B, int Ti, int Fi, int Ci, int To,
+                                 int Fo, int ldcol, void* __restrict__ dx, int dx_bf16) {
+  const long long n = (long long)B * Ti * Fi * Ci;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % Ci);
+    long long q = i / Ci;
+    const int fi = (int)(q % Fi); q /= Fi;
+    const int ti = (int)(q % Ti);
+    const int b = (int)(q / Ti);
+    // padded positions mapping onto ti: ti + 1, and the mirrored ones
+    int pts[3], npt = 0, pfs[3], npf = 0;  // Ti == 3: ti = 1 is hit from both borders
+    pts[npt++] = ti + 1;
+    if (ti == 1) pts[npt++] = 0;
+    if (ti == Ti - 2 && Ti >= 2) pts[npt++] = Ti + 1;
+    pfs[npf++] = fi + 1;
+    if (fi == 1) pfs[npf++] = 0;
+    if (fi == Fi - 2 && Fi >= 2) pfs[npf++] = Fi + 1;
+    float s = 0.f;
+    for (int a = 0; a < npt; ++a)
+      for (int kt = 0; kt < 3; ++kt) {
+        const int d = pts[a] - kt;
+        if (d < 0 || (d & 1)) continue;
+        const int to = d >> 1;
+        if (to >= To) continue;
+        for (int e = 0; e < npf; ++e)
+          for (int kf = 0; kf < 3; ++kf) {
+            const int df = pfs[e] - kf;
+            if (df < 0 || (df & 1)) continue;
+            const int fo = df >> 1;
+            if (fo >= Fo) continue;
+            s += ldv(dcol, (((long long)b * To + to) * Fo + fo) * ldcol + (kt * 3 + kf) * Ci + ci, dcol_bf16);
+          }
+      }
+    stv(dx, i, s, dx_bf16);
+  }
+}
+
+// ------------------------------------------------- transducer joint ("sum")
+// z[b, t, u, :] = act(tn[b, t, :] + pn[b, u, :]); act 0 none, 3 LeakyReLU,
+// 5 tanh, 6 ReLU.  Rows of J contiguous; out fp32 or bf16.
+__device__ __forceinline__ float joint_act(int act, float v, float slope) {
+  if (act == 3) return v >= 0.f ? v : v * slope;
+  if (act == 5) return tanhf(v);
+  if (act == 6) return v > 0.f ? v : 0.f;
+  return v;
+}
+__device__ __forceinline__ float joint_dact(int act, float v, float slope) {
+  if (act == 3) return v > 0.f ? 1.f : slope;
+  if (act == 5) { const float t = tanhf(v); return 1.f - t * t; }
+  if (act == 6) return v > 0.f ? 1.f : 0.f;
+  return 1.f;
+}
+
+__global__ void joint_fwd_kernel(const float* __restrict__ tn, const float* __restrict__ pn, int T, int U1, int J,
+                                 int act, float slope, void* __restrict__ z, int z_bf16) {
+  // block per (b, t, u) row
+  const long long row = blockIdx.x;
+  const int u = (int)(row % U1);
+  const long long bt = row / U1;
+  const int b = (int)(bt / T);
+  const float* a = tn + bt * J;
+  const float* c = pn + ((long long)b * U1 + u) * J;
+  for (int j = threadIdx.x; j < J; j += blockDim.x) stv(z, row * J + j, joint_act(act, a[j] + c[j], slope), z_bf16);
+}
+
+// dtn[b, t, :] = sum_u dz * act'(.)  (block per (b, t))
+__global__ void joint_bwd_tn_kernel(const float* __restrict__ tn, const float* __restrict__ pn,
+                                    const void* __restrict__ dz, int dz_bf16, int T, int U1, int J, int act,
+                                    float slope, float* __restrict__ dtn) {
+  const long long bt = blockIdx.x;
+  const int b = (int)(bt / T);
+  for (int j = threadIdx.x; j < J; j += blockDim.x) {
+    const float a = tn[bt * J + j];
+    float s = 0.f;
+    for (int u = 0; u < U1; ++u)
+      s += ldv(dz, (bt * U1 + u) * J + j, dz_bf16) * joint_dact(act, a + pn[((long long)b * U1 + u) * J + j], slope);
+    dtn[bt * J + j] = s;
+  }
+}
+
+// dpn[b, u, :] = sum_t dz * act'(.)  (block per (b, u))
+__global__ void joint_bwd_pn_kernel(const float* __restrict__ tn, const float* __restrict__ pn,
+                                    const void* __restrict__ dz, int dz_bf16, int T, int U1, int J, int act,
+                                    float slope, float* __restrict__ dpn) {
+  const long long bu = blockIdx.x;
+  const int b = (int)(bu / U1), u = (int)(bu % U1);
+  for (int j = threadIdx.x; j < J; j += blockDim.x) {
+    const float c = pn[bu * J + j];
+    float s = 0.f;
+    for (int t = 0; t < T; ++t) {
+      const long long bt = (long long)b * T + t;
+      s += ldv(dz, (bt * U1 + u) * J + j, dz_bf16) * joint_dact(act, tn[bt * J + j] + c, slope);
+    }
+    dpn[bu * J + j] = s;
+  }
+}
+
+// ------------------------------------------------ dropout / residual add
+// Counter-based keep mask: bit-identical for the forward and the backward
+// launch of one (seed, element) pair, independent of grid shape.
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ bool keep_elem(unsigned long long seed, long long i, unsigned thresh) {
+  return (unsigned)(mix64(seed + (unsigned long long)i * 0x9E3779B97F4A7C15ull) >> 40) < thresh;
+}
+
+// out = res + alpha * rowmask0(drop(x)); drop(x) = keep ? x / (1 - p) : 0.
+// The backward of this op is the same launch on dy with res = null.
+__global__ void dropout_add_kernel(const void* __restrict__ x, int x_bf16, const float* __restrict__ res,
+                                   long long rows, int cols, const unsigned char* __restrict__ rowmask, float alpha,
+                                   unsigned thresh, float inv_keep, unsigned long long seed, int use_drop,
+                                   void* __restrict__ out, int out_bf16) {
+  const long long n = rows * cols;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    float v = ldv(x, i, x_bf16) * alpha;
+    if (use_drop) v = keep_elem(seed, i, thresh) ? v * inv_keep : 0.f;
+    if (rowmask && rowmask[i / cols]) v = 0.f;
+    if (res) v += res[i];
+    stv(out, i, v, out_bf16);
+  }
+}
+
+}  // namespace
+
+SBK_API int sbk_dropout_add(const void* x, int x_bf16, const float* res, long long rows, int cols,
+                            const unsigned char* rowmask, float alpha, float p, unsigned long long seed, void* out,
+                            int out_bf16, void* stream) {
+  if (rows < 0 || cols <= 0 || !(p >= 0.f) || p >= 1.f) return SBK_ERR_ARG;
+  if (rows == 0) return 0;
+  const double keep = 1.0 - (double)p;
+  const unsigned thresh = (unsigned)std::min(keep * 16777216.0, 16777216.0);
+  dropout_add_kernel<<<grid_for(rows * cols, 256), 256, 0, (hipStream_t)stream>>>(
+      x, x_bf16, res, rows, cols, rowmask, alpha, thresh, (float)(1.0 / keep), seed, p > 0.f, out, out_bf16);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+SBK_API int sbk_layernorm_bwd_blocks(int M) { return grid_for((M + 3) / 4, 1, 1024); }
+
+SBK_API int sbk_layernorm_bwd(const float* x, const void* dy, int dy_bf16, int M, int D, const float* g, float eps,
+                              const float* dres, float* dx, float* part, void* stream) {
+  if (M <= 0 || D <= 0 || D > 2560) return SBK_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = sbk_layernorm_bwd_blocks(M);
+  if (D <= 256)
+    ln_bwd_kernel<4><<<grid, 256, 0, s>>>(x, dy, dy_bf16, M, D, g, eps, dres, dx, part);
+  else if (D <= 1024)
+    ln_bwd_kernel<16><<<grid, 256, 0, s>>>(x, dy, dy_bf16, M, D, g, eps, dres, dx, part);
+  else
+    ln_bwd_kernel<40><<<grid, 256, 0, s>>>(x, dy, dy_bf16, M, D, g, eps, dres, dx, part);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+SBK_API int sbk_layernorm_wide(const float* x, int M, int D, const float* g, const float* b, float eps, void* y,
+                               int y_bf16, void* stream) {
+  if (M <= 0 || D <= 0 || D > 2560) return SBK_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = (M + 3) / 4;
+  if (D <= 256)
+    ln_fwd_kernel<4><<<grid, 256, 0, s>>>(x, M, D, g, b, eps, y, y_bf16);
+  else if (D <= 1024)
+    ln_fwd_kernel<16><<<grid, 256, 0, s>>>(x, M, D, g, b, eps, y, y_bf16);
+  else
+    ln_fwd_kernel<40><<<grid, 256, 0, s>>>(x, M, D, g, b, eps, y, y_bf16);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+SBK_API int sbk_rowsum_chunks(long long rows) { return (int)std::min<long long>(256, std::max<long long>(1, rows / 64)); }
+
+// out (cols) fp32 = sum over rows of x (rows, cols) (+ out when accumulate);
+// part: sbk_rowsum_chunks(rows) * cols floats of scratch.
+SBK_API int sbk_rowsum(const void* x, int x_bf16, long long rows, int cols, float* part, float* out, int accumulate,
+                       void* stream) {
+  if (rows <= 0 || cols <= 0) return SBK_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int nchunk = sbk_rowsum_chunks(rows);
+  const int rows_per = (int)((rows + nchunk - 1) / nchunk);
+  dim3 grid(nchunk, (cols + 255) / 256);
+  rowsum_partial_kernel<<<grid, 256, 0, s>>>(x, x_bf16, rows, cols, rows_per, part);
+  SBK_CHECK_LAUNCH();
+  colsum_kernel<<<(cols + 255) / 256, 256, 0, s>>>(part, nchunk, cols, out, accumulate);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+SBK_API int sbk_colsum(const float* part, int rows, int cols, float* out, int accumulate, void* stream) {
+  if (rows <= 0 || cols <= 0) return SBK_ERR_ARG;
+  colsum_kernel<<<(cols + 255) / 256, 256, 0, (hipStream_t)stream>>>(part, rows, cols, out, accumulate);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+SBK_API int sbk_act_fwd(int mode, const void* x, int x_bf16, long long rows, int cols, void* y, int y_bf16,
+                        float slope, void* stream) {
+  if (mode < 1 || mode > 3 || rows < 0 || cols <= 0) return SBK_ERR_ARG;
+  if (rows == 0) return 0;
+  act_fwd_kernel<<<grid_for(rows * cols, 256), 256, 0, (hipStream_t)stream>>>(mode, x, x_bf16, rows, cols, y, y_bf16,
+                                                                              slope);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+SBK_API int sbk_act_bwd(int mode, const void* x, int x_bf16, const void* dy, int dy_bf16, long long rows, int cols,
+                        void* dx, int dx_bf16, float slope, void* stream) {
+  if (mode < 1 || mode > 3 || rows < 0 || cols <= 0) return SBK_ERR_ARG;
+  if (rows == 0) return 0;
+  act_bwd_kernel<<<grid_for(rows * cols, 256), 256, 0, (hipStream_t)stream>>>(mode, x, x_bf16, dy, dy_bf16, rows,
+                                                                              cols, dx, dx_bf16, slope);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+SBK_API int sbk_dwconv_fwd(const void* x, int x_bf16, int B, int T, int C, const float* w, const float* bias, int K,
+                           int causal, void* y, int y_bf16, void* stream) {
+  if (B <= 0 || T <= 0 || C <= 0 || K <= 0 || K > 64) return SBK_ERR_ARG;
+  const int padL = causal ? K - 1 : (K - 1) / 2;
+  dwconv_fwd_kernel<<<grid_for((long long)B * T * C, 256), 256, 0, (hipStream_t)stream>>>(x, x_bf16, B, T, C, w, bias,
+                                                                                          K, padL, y, y_bf16);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+SBK_API int sbk_dwconv_wgrad_chunks(int B, int T) {
+  const long long rows = (long long)B * T;
+  return (int)std::min<long long>(256, std::max<long long>(1, rows / 32));
+}
+
+// dx (optional) and per-chunk (nchunk, C, K+1) weight|bias partials.
+SBK_API int sbk_dwconv_bwd(const void* x, int x_bf16, const float* dy, int B, int T, int C, const float* w, int K,
+                           int causal, void* dx, int dx_bf16, float* part, void* stream) {
+  if (B <= 0 || T <= 0 || C <= 0 || K <= 0 || K > 31) return SBK_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int padL = causal ? K - 1 : (K - 1) / 2;
+  if (dx) {
+    dwconv_dgrad_kernel<<<grid_for((long long)B * T * C, 256), 256, 0, s>>>(dy, B, T, C, w, K, padL, dx, dx_bf16);
+    SBK_CHECK_LAUNCH();
+  }
+  if (part) {
+    const int nchunk = sbk_dwconv_wgrad_chunks(B, T);
+    const long long rows = (long long)B * T;
+    const int rows_per = (int)((rows + nchunk - 1) / nchunk);
+    dim3 grid(nchunk, (C + 255) / 256);
+    dwconv_wgrad_kernel<31><<<grid, 256, 0, s>>>(x, x_bf16, dy, B, T, C, K, padL, rows_per, part);
+    SBK_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+SBK_API int sbk_relpos_softmax_bwd(const float* P, const void* dP, int dP_bf16, int B, int H, int T, float scale,
+                                   void* dS, void* dBD, int out_bf16, void* stream) {
+  if (B <= 0 || H <= 0 || T <= 0) return SBK_ERR_ARG;
+  relpos_softmax_bwd_kernel<<<B * H * T, 256, 0, (hipStream_t)stream>>>(P, dP, dP_bf16, T, scale, dS, dBD, out_bf16);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+SBK_API int sbk_im2col3s2(const void* x, int x_bf16, int B, int Ti, int Fi, int Ci, int ldcol, void* col,
+                          int col_bf16, void* stream) {
+  if (B <= 0 || Ti < 2 || Fi < 2 || Ci <= 0 || ldcol < 9 * Ci) return SBK_ERR_ARG;
+  const int To = (Ti - 1) / 2 + 1, Fo = (Fi - 1) / 2 + 1;
+  im2col3s2_kernel<<<grid_for((long long)B * To * Fo * ldcol, 256), 256, 0, (hipStream_t)stream>>>(
+      x, x_bf16, B, Ti, Fi, Ci, To, Fo, ldcol, col, col_bf16);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+SBK_API int sbk_col2im3s2(const void* dcol, int dcol_bf16, int B, int Ti, int Fi, int Ci, int ldcol, void* dx,
+                          int dx_bf16, void* stream) {
+  if (B <= 0 || Ti < 2 || Fi < 2 || Ci <= 0 || ldcol < 9 * Ci) return SBK_ERR_ARG;
+  const int To = (Ti - 1) / 2 + 1, Fo = (Fi - 1) / 2 + 1;
+  col2im3s2_kernel<<<grid_for((long long)B * Ti * Fi * Ci, 256), 256, 0, (hipStream_t)stream>>>(
+      dcol, dcol_bf16, B, Ti, Fi, Ci, To, Fo, ldcol, dx, dx_bf16);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+SBK_API int sbk_joint_fwd(const float* tn, const float* pn, int B, int T, int U1, int J, int act, float slope, void* z,
+                          int z_bf16, void* stream) {
+  if (B <= 0 || T <= 0 || U1 <= 0 || J <= 0) return SBK_ERR_ARG;
+  joint_fwd_kernel<<<(unsigned)((long long)B * T * U1), 256, 0, (hipStream_t)stream>>>(tn, pn, T, U1, J, act, slope,
+                                                                                     z, z_bf16);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+SBK_API int sbk_joint_bwd(const float* tn, const float* pn, const void* dz, int dz_bf16, int B, int T, int U1, int J,
+                          int act, float slope, float* dtn, float* dpn, void* stream) {
+  if (B <= 0 || T <= 0 || U1 <= 0 || J <= 0) return SBK_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  joint_bwd_tn_kernel<<<(unsigned)((long long)B * T), 256, 0, s>>>(tn, pn, dz, dz_bf16, T, U1, J, act, slope, dtn);
+  SBK_CHECK_LAUNCH();
+  joint_bwd_pn_kernel<<<(unsigned)((long long)B * U1), 256, 0, s>>>(tn, pn, dz, dz_bf16, T, U1, J, act, slope, dpn);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}

@@ -7,6 +7,7 @@ match the reference (convblock_i.convs.conv_0.conv.*, .norm_0.norm.*)."""
 import torch
 import torch.nn as nn
 
+from ... import _autograd as A
 from ... import _enc
 from ...nnet.CNN import Conv2d
 from ...nnet.normalization import LayerNorm
@@ -54,8 +55,6 @@ class ConvBlock(nn.Module):
         if (self.num_layers != 1 or not c.conv_0.fusable() or not isinstance(norm, LayerNorm)
                 or not isinstance(act, nn.LeakyReLU)):
             raise NotImplementedError("fused ConvBlock supports 1 x (Conv2d k3 s2 reflect + LayerNorm + LeakyReLU)")
-        if self.training and c.dropout_0.p > 0:
-            raise NotImplementedError("dropout in training mode is not implemented in HIP yet")
 
     def params(self):
         """(conv weight, bias, ln weight, ln bias, ln eps, leaky slope) of the fused block."""
@@ -96,7 +95,27 @@ class ConvBlock(nn.Module):
         return _enc.conv_block_mfma(x.contiguous(), wp, bias, ln.weight.detach(), ln.bias.detach(), ln.eps, slope,
                                     out_dtype)
 
+    def train_run(self, x, dtype, out_dtype):
+        """Differentiable block (training path): im2col + MFMA GEMM + (freq x
+        chan) LayerNorm + LeakyReLU (ConvBlockFn) + Dropout."""
+        self._check()
+        c = self.convs
+        conv = c.conv_0.conv
+        ln = c.norm_0.norm
+        if x.dim() == 3:
+            x = x.unsqueeze(-1)
+        if x.dtype != dtype and conv.in_channels > 1:
+            x = A.to_dtype(x, dtype)
+        y = A.ConvBlockFn.apply(x, conv.weight, conv.bias, ln.weight, ln.bias, ln.eps, c.act_0.negative_slope, dtype,
+                                out_dtype)
+        return A.dropout(y, c.dropout_0.p, self.training)
+
+    def wants_train_path(self, x):
+        return A.needs_grad(self, x) or (self.training and self.convs.dropout_0.p > 0)
+
     def forward(self, x):
+        if self.wants_train_path(x):
+            return self.train_run(x, _enc.compute_dtype(), _f32)
         return self.run(x, _f32)
 
 
@@ -144,6 +163,12 @@ class ConvolutionFrontEnd(nn.Module):
     def run(self, x, last_dtype):
         """Intermediate block outputs in the compute dtype, the last in `last_dtype`."""
         dtype = _enc.compute_dtype()
+        blocks = [getattr(self, n) for n in self.block_names]
+        if any(b.wants_train_path(x) for b in blocks):
+            n = len(blocks)
+            for i, b in enumerate(blocks):
+                x = b.train_run(x, dtype, last_dtype if i == n - 1 else dtype)
+            return x
         if self._fusable2(x, dtype):
             # both blocks in one kernel: the block-1 activation stays in LDS
             b1, b2 = (getattr(self, n) for n in self.block_names)

@@ -27,6 +27,7 @@ from typing import Optional
 import torch
 import torch.nn as nn
 
+from .... import _autograd as A
 from .... import _enc
 from ....nnet.activations import Swish
 from ....nnet.attention import PositionalwiseFeedForward, RelPosMHAXL
@@ -112,12 +113,32 @@ class ConvolutionModule(nn.Module):
         return _enc.gemm(v, w2, bias=lin.bias.detach() if lin.bias is not None else None, rowmask=pad_mask_u8,
                          res=residual, out_dtype=_f32)
 
+    def train_run(self, x2d, B, T, dtype, pad_mask_u8=None, residual=None):
+        """Differentiable chain (training path, _autograd): residual +
+        mask(ConvolutionModule(x2d)), each op a HIP kernel with its backward."""
+        _check_swish(self.after_conv[1])
+        d = x2d.shape[1]
+        u = A.layer_norm(x2d, self.layer_norm, out_dtype=dtype)
+        pw = self.bottleneck[0]
+        h = A.linear(u, pw.weight, pw.bias, dtype, self._wc, "t_pw", out_dtype=dtype)
+        g = A.act(h, "glu")
+        c = A.DwConvFn.apply(g, self.conv.weight, self.conv.bias, B, T, self.causal)
+        n = A.layer_norm(c, self.after_conv[0], out_dtype=_f32)
+        s = A.act(n, "swish", out_dtype=dtype)
+        lin = self.after_conv[2]
+        p = self.after_conv[3].p if self.training else 0.0
+        if p == 0:
+            return A.linear(s, lin.weight, lin.bias, dtype, self._wc, "t_lin", res=residual, rowmask=pad_mask_u8)
+        y = A.linear(s, lin.weight, lin.bias, dtype, self._wc, "t_lin")
+        return A.DropAddFn.apply(y, residual, 1.0, pad_mask_u8, float(p), _f32)
+
     def forward(self, x, mask=None):
-        if self.training and self.after_conv[3].p > 0:
-            raise NotImplementedError("dropout in training mode is not implemented in HIP yet")
         B, T, d = x.shape
         m = mask.reshape(B * T).to(torch.uint8).contiguous() if mask is not None else None
-        return self.run(x.float().reshape(B * T, d).contiguous(), B, T, _enc.compute_dtype(), m).view(B, T, d)
+        x2d = x.float().reshape(B * T, d).contiguous()
+        if A.needs_grad(self, x) or (self.training and self.after_conv[3].p > 0):
+            return self.train_run(x2d, B, T, _enc.compute_dtype(), m).view(B, T, d)
+        return self.run(x2d, B, T, _enc.compute_dtype(), m).view(B, T, d)
 
 
 class ConformerEncoderLayer(nn.Module):
@@ -183,6 +204,25 @@ class ConformerEncoderLayer(nn.Module):
         x, _ = _enc.layernorm(z, w2, b2, e2, out1_dtype=_f32)
         return x, None, attn, False
 
+    def train_layer(self, x, B, T, pos, kpm_u8, dtype):
+        """Differentiable layer (training path): x (B*T, d) fp32 → (x_out, attn).
+        Same arithmetic as `fused`, as HIP kernels with backward (_autograd);
+        dropout (training mode) after the FFN activation, on the FFN and conv
+        outputs and on the attention probabilities, as the reference places it."""
+        f1, f2 = self.ffn_module1, self.ffn_module2
+        tr = self.training
+        u = A.layer_norm(x, f1[0], out_dtype=dtype)
+        x = f1[1].train_run(u, dtype, residual=x, alpha=0.5, out_p=f1[2].p if tr else 0.0)
+        u = A.layer_norm(x, self.norm1.norm, out_dtype=dtype)
+        x, attn = self.mha_layer.train_attend(u, B, T, pos, kpm_u8, dtype, residual=x)
+        x = self.convolution_module.train_run(x, B, T, dtype, kpm_u8, residual=x)
+        u = A.layer_norm(x, f2[0], out_dtype=dtype)
+        z = f2[1].train_run(u, dtype, residual=x, alpha=0.5, out_p=f2[2].p if tr else 0.0)
+        return A.layer_norm(z, self.norm2.norm, out_dtype=_f32), attn
+
+    def wants_train_path(self, x):
+        return A.needs_grad(self, x) or (self.training and self.ffn_module1[2].p > 0)
+
     def forward(self, x, src_mask: Optional[torch.Tensor] = None,
                 src_key_padding_mask: Optional[torch.Tensor] = None, pos_embs: Optional[torch.Tensor] = None):
         if src_mask is not None:
@@ -190,8 +230,12 @@ class ConformerEncoderLayer(nn.Module):
         B, T, d = x.shape
         dtype = _enc.compute_dtype()
         kpm = src_key_padding_mask.to(torch.uint8).contiguous() if src_key_padding_mask is not None else None
+        x2d = x.float().reshape(B * T, d).contiguous()
+        if self.wants_train_path(x):
+            y, attn = self.train_layer(x2d, B, T, pos_embs.reshape(-1, d).float(), kpm, dtype)
+            return y.view(B, T, d), attn
         pos = _enc.to_compute(pos_embs.reshape(-1, d), dtype)
-        y, _, attn, _ = self.fused(x.float().reshape(B * T, d).contiguous(), B, T, pos, kpm, dtype, True)
+        y, _, attn, _ = self.fused(x2d, B, T, pos, kpm, dtype, True)
         return y.view(B, T, d), attn
 
 
@@ -208,8 +252,24 @@ class ConformerEncoder(nn.Module):
         self.norm = LayerNorm(d_model, eps=1e-6)
         self.attention_type = attention_type
 
+    def train_run(self, src2d, B, T, pos_embs, kpm_u8, dtype):
+        """Differentiable stack (training path) on (B*T, d) fp32 → (y, [attn])."""
+        d = src2d.shape[1]
+        pos = pos_embs.reshape(-1, d).float()
+        x = src2d
+        attns = []
+        for layer in self.layers:
+            x, a = layer.train_layer(x, B, T, pos, kpm_u8, dtype)
+            attns.append(a)
+        return A.layer_norm(x, self.norm.norm, out_dtype=_f32), attns
+
+    def wants_train_path(self, x):
+        return any(layer.wants_train_path(x) for layer in self.layers) or A.needs_grad(self.norm, x)
+
     def run(self, src2d, B, T, pos_embs, kpm_u8, dtype, need_attn):
         """Fused stack on (B*T, d) fp32 → ((B*T, d) fp32, [attn])."""
+        if self.wants_train_path(src2d):
+            return self.train_run(src2d, B, T, pos_embs, kpm_u8, dtype)
         d = src2d.shape[1]
         pos = _enc.to_compute(pos_embs.reshape(-1, d), dtype)
         x = src2d

@@ -16,6 +16,7 @@ from typing import Optional
 import torch
 import torch.nn as nn
 
+from .... import _autograd as A
 from .... import _enc
 from ....nnet.activations import Swish
 from ....nnet.attention import RelPosEncXL
@@ -118,11 +119,17 @@ class TransformerASR(nn.Module):
             bz, t, ch1, ch2 = src.shape
             src = src.reshape(bz, t, ch1 * ch2)
         B, T, Fin = src.shape
-        if self.training and self.custom_src_module.layers[1].p > 0:
-            raise NotImplementedError("dropout in training mode is not implemented in HIP yet")
         dtype = _enc.compute_dtype()
         kpm = self.key_padding_mask(T, wav_len, src.device)
         lin = self.custom_src_module.layers[0]
+        drop = self.custom_src_module.layers[1]
+        if A.needs_grad(self, src) or (self.training and (drop.p > 0 or self.encoder.wants_train_path(src))):
+            # training path: differentiable HIP chain (_autograd)
+            x = A.linear(src.reshape(B * T, Fin), lin.w.weight, lin.w.bias, dtype, lin._wc, "t_w", out_dtype=_f32)
+            x = A.dropout(x, drop.p, self.training)
+            pos = self.positional_encoding.table(T, src.device, _f32)
+            y, _ = self.encoder.train_run(x, B, T, pos, kpm, dtype)
+            return y.view(B, T, -1)
         a = _enc.to_compute(src.reshape(B * T, Fin), dtype)
         x = _enc.gemm(a, lin.kernel_weight(dtype), bias=lin.w.bias.detach(), out_dtype=_f32)
         pos = self.positional_encoding.table(T, src.device, _f32)

@@ -11,6 +11,7 @@ import math
 import torch
 import torch.nn as nn
 
+from .. import _autograd as A
 from .. import _enc
 from .activations import Swish
 
@@ -130,6 +131,20 @@ class RelPosMHAXL(nn.Module):
         out = _enc.gemm(o, w_out, bias=bias, res=residual, out_dtype=torch.float32)
         return out, probs
 
+    def train_attend(self, x2d, B, T, pos, kpm_u8, dtype, residual=None):
+        """Differentiable attention block (training path): x2d (B*T, d) →
+        (residual + out_proj(attn(x2d)) fp32, attention probabilities after dropout)."""
+        if self.vbias is not None:
+            raise NotImplementedError("vbias=True is not on the RelPosMHAXL hot path")
+        qkv = A.linear(x2d, self.in_proj_weight, None, dtype, self._wc, "t_in", out_dtype=dtype)
+        pk = A.linear(pos.reshape(-1, self.embed_dim), self.linear_pos.weight, None, dtype, self._wc, "t_pos",
+                      out_dtype=dtype)
+        p = self.dropout_att.p if self.training else 0.0
+        o, attn = A.RelPosAttentionFn.apply(qkv, pk, self.pos_bias_u, self.pos_bias_v, kpm_u8, B, T,
+                                            self.num_heads, self.head_dim, self.scale, float(p))
+        out = A.linear(o, self.out_proj.weight, self.out_proj.bias, dtype, self._wc, "t_out", res=residual)
+        return out, attn
+
     def forward(self, query, key, value, pos_embs, key_padding_mask=None, attn_mask=None,
                 return_attn_weights=True):
         """attention.py:485-639.  Self-attention only (query, key and value
@@ -140,14 +155,15 @@ class RelPosMHAXL(nn.Module):
             raise NotImplementedError("cross-attention RelPosMHAXL is not on the accelerated path")
         if attn_mask is not None:
             raise NotImplementedError("attn_mask is not supported by the fused kernel (encoder passes none)")
-        if self.training and self.dropout > 0:
-            raise NotImplementedError("attention dropout in training mode is not implemented in HIP yet")
         B, T, d = query.shape
         dtype = _enc.compute_dtype()
         x2d = query.reshape(B * T, d)
-        x2d = _enc.to_compute(x2d, dtype)
         kpm = key_padding_mask.to(torch.uint8).contiguous() if key_padding_mask is not None else None
-        out, attn = self.attend(x2d, B, T, pos_embs, kpm, dtype, return_attn_weights)
+        if A.needs_grad(self, query) or (self.training and self.dropout > 0):
+            out, attn = self.train_attend(x2d.float(), B, T, pos_embs.float(), kpm, dtype)
+        else:
+            x2d = _enc.to_compute(x2d, dtype)
+            out, attn = self.attend(x2d, B, T, pos_embs, kpm, dtype, return_attn_weights)
         out = out.view(B, T, d)
         if return_attn_weights:
             return out, attn
@@ -195,6 +211,22 @@ class PositionalwiseFeedForward(nn.Module):
         h = _enc.gemm(u2d, w1, bias=self.ffn[0].bias.detach(), act=act, slope=slope, out_dtype=dtype)
         return _enc.gemm(h, w2, bias=self.ffn[3].bias.detach(), res=residual, alpha=alpha, out_dtype=torch.float32)
 
+    def train_run(self, u2d, dtype, residual=None, alpha=1.0, out_p=0.0):
+        """Differentiable FFN (training path): residual + alpha * Dropout(out_p)(FFN(u2d))."""
+        act, slope = self.act_name()
+        if act == "relu":
+            act, slope = "leaky_relu", 0.0  # ReLU = LeakyReLU(0), same backward
+        if act not in ("swish", "leaky_relu"):
+            raise NotImplementedError(f"activation {act} has no backward kernel yet")
+        l1, l2 = self.ffn[0], self.ffn[3]
+        h = A.linear(u2d, l1.weight, l1.bias, dtype, self._wc, "t1", out_dtype=dtype)
+        h = A.act(h, act, slope)
+        h = A.dropout(h, self.ffn[2].p, self.training)
+        if out_p == 0:
+            return A.linear(h, l2.weight, l2.bias, dtype, self._wc, "t2", res=residual, alpha=alpha)
+        y = A.linear(h, l2.weight, l2.bias, dtype, self._wc, "t2")
+        return A.DropAddFn.apply(y, residual, float(alpha), None, float(out_p), torch.float32)
+
     def fusable(self, dtype):
         """True when the whole LN→FFN→residual block can run as one kernel."""
         return (dtype == torch.bfloat16 and self.act_name()[0] != "glu"
@@ -211,10 +243,10 @@ class PositionalwiseFeedForward(nn.Module):
                         post_ln=post_ln, next_ln=next_ln, next_dtype=next_dtype, out=out)
 
     def forward(self, x):
-        if self.training and self.ffn[2].p > 0:
-            raise NotImplementedError("FFN dropout in training mode is not implemented in HIP yet")
         shp = x.shape
         dtype = _enc.compute_dtype()
         u = x.reshape(-1, shp[-1])
+        if A.needs_grad(self, x) or (self.training and self.ffn[2].p > 0):
+            return self.train_run(A.to_dtype(u, dtype), dtype).view(*shp[:-1], -1)
         u = _enc.to_compute(u, dtype)
         return self.run(u, dtype).view(*shp[:-1], -1)

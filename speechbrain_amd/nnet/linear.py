@@ -2,6 +2,7 @@
 (state_dict keys: w.weight, w.bias)."""
 import torch
 
+from .. import _autograd as A
 from .. import _enc
 
 
@@ -28,6 +29,9 @@ class Linear(torch.nn.Module):
             x = x.reshape(x.shape[0], x.shape[1], x.shape[2] * x.shape[3])
         dtype = _enc.compute_dtype()
         shp = x.shape
+        if A.needs_grad(self, x):
+            y = A.linear(x.reshape(-1, shp[-1]), self.w.weight, self.w.bias, dtype, self._wc, "t_w")
+            return y.view(*shp[:-1], -1)
         a = _enc.to_compute(x.reshape(-1, shp[-1]), dtype)
         b = self.w.bias.detach() if self.w.bias is not None else None
         return _enc.gemm(a, self.kernel_weight(dtype), bias=b).view(*shp[:-1], -1)

@@ -25,6 +25,10 @@ Fixture inventory (all float32 unless noted):
                    RelPosEncXL and rel_shift vectors
                    (lobes/models/convolution.py, lobes/models/transformer/*,
                    nnet/attention.py)
+  train.npz        gradients of sum(R * encode(cnn(feats), wav_len)) w.r.t.
+                   every ConvolutionFrontEnd / TransformerASR parameter and
+                   the input features (reference autograd, weights of
+                   conformer.npz), for the training-path backward kernels
 The RNN-T known answer (tests/unittests/test_losses.py:109-152) needs numba
 and is pinned as a literal in tests/test_oracle_golden.py instead.
 """
@@ -265,11 +269,46 @@ def gen_conformer():
     np.savez_compressed(os.path.join(OUT, "conformer.npz"), **out)
 
 
+def gen_train():
+    """Reference autograd through ConvolutionFrontEnd + TransformerASR.encode
+    (dropout 0, so train and eval arithmetic agree), weights from conformer.npz."""
+    g0 = np.load(os.path.join(OUT, "conformer.npz"))
+    cnn = ConvolutionFrontEnd(input_shape=(8, 10, 80), num_blocks=2, num_layers_per_block=1,
+                              out_channels=(64, 32), kernel_sizes=(3, 3), strides=(2, 2),
+                              residuals=(False, False), dropout=0.0)
+    tr = TransformerASR(tgt_vocab=10, input_size=640, d_model=64, nhead=4,
+                        num_encoder_layers=2, num_decoder_layers=0, d_ffn=128,
+                        dropout=0.0, encoder_module="conformer",
+                        attention_type="RelPosMHAXL", normalize_before=True,
+                        causal=False)
+    for pre, m in (("cnn.", cnn), ("tr.", tr)):
+        m.load_state_dict({k[len(pre):]: torch.from_numpy(g0[k]) for k in g0.files if k.startswith(pre)})
+        m.train()
+    out = {}
+    feats = torch.from_numpy(g0["feats"]).clone().requires_grad_(True)
+    wav_len = torch.from_numpy(g0["wav_len"])
+    y = tr.encode(cnn(feats), wav_len)
+    R = torch.randn(y.shape, generator=torch.Generator().manual_seed(7))
+    (y * R).sum().backward()
+    out["R"] = t2n(R)
+    out["y"] = t2n(y)
+    out["grad_feats"] = t2n(feats.grad)
+    for pre, m in (("cnn.", cnn), ("tr.", tr)):
+        for k, p in m.named_parameters():
+            if p.grad is not None:
+                out["grad." + pre + k] = t2n(p.grad)
+    np.savez_compressed(os.path.join(OUT, "train.npz"), **out)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["train"]:
+        gen_train()
+        sys.exit(0)
     gen_fbank_wavs()
     gen_features()
     gen_specaug()
     gen_conformer()
+    gen_train()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

@@ -1,0 +1,291 @@
+"""Training path: backward kernels of
+csrc/backward.hip and the differentiable module chain (_autograd) vs the
+reference's own autograd (tests/golden/train.npz) and vs torch autograd of
+the same op on CPU.
+
+Tolerances: fp32 gradients within 1e-4 of the largest reference gradient of
+the tensor (|a-b| <= 1e-4 * max|b|) — the backward sums differ from the
+reference's only in fp32 summation order; bf16 paths are checked against
+fp32 with a cosine-similarity bound."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import assert_close
+import oracle.conformer as OC
+
+pytestmark = pytest.mark.gpu
+
+
+def assert_grad(a, b, rtol=1e-4, name=""):
+    a = a.detach().float().cpu()
+    b = torch.as_tensor(b).float()
+    assert a.shape == b.shape, f"{name}: shape {tuple(a.shape)} != {tuple(b.shape)}"
+    scale = max(b.abs().max().item(), 1e-12)
+    err = (a - b).abs().max().item()
+    assert err <= rtol * scale, f"{name}: max err {err:.3e} vs scale {scale:.3e}"
+
+
+def cosine(a, b):
+    a, b = a.detach().float().flatten().cpu(), b.detach().float().flatten().cpu()
+    return (a @ b / (a.norm() * b.norm() + 1e-30)).item()
+
+
+# ----------------------------------------------------------------- kernels
+def test_dropout_add(dev):
+    from speechbrain_amd import _autograd as A
+    x = torch.randn(2000, 513, device=dev)
+    res = torch.randn(2000, 513, device=dev)
+    y0 = A.drop_add(x, res, 0.5, None, 0.0, 0)
+    assert_close(y0, res + 0.5 * x, rtol=1e-6, name="p=0")
+    y = A.drop_add(x, None, 1.0, None, 0.1, 1234)
+    kept = y != 0
+    frac = 1 - kept.float().mean().item()
+    assert abs(frac - 0.1) < 0.005, frac
+    assert_close(y[kept], x[kept] / 0.9, rtol=1e-6, name="scale")
+    # same seed -> same mask (the backward regenerates it); different seed -> different mask
+    y2 = A.drop_add(torch.ones_like(x), None, 1.0, None, 0.1, 1234)
+    assert torch.equal(y2 != 0, kept)
+    y3 = A.drop_add(torch.ones_like(x), None, 1.0, None, 0.1, 99)
+    assert not torch.equal(y3 != 0, kept)
+    mask = (torch.arange(2000, device=dev) % 3 == 0).to(torch.uint8)
+    y4 = A.drop_add(x, res, 2.0, mask, 0.0, 0, torch.bfloat16)
+    ref = res + 2 * x
+    ref[mask.bool()] = res[mask.bool()]
+    assert_close(y4.float(), ref, rtol=1e-2, name="rowmask bf16")
+
+
+def test_dropout_autograd(dev):
+    from speechbrain_amd import _autograd as A
+    torch.manual_seed(0)
+    x = torch.randn(300, 64, device=dev, requires_grad=True)
+    res = torch.randn(300, 64, device=dev, requires_grad=True)
+    y = A.DropAddFn.apply(x, res, 0.5, None, 0.2, torch.float32)
+    g = torch.randn_like(y)
+    y.backward(g)
+    keep = ((y - res).detach() != 0)
+    assert_close(x.grad, torch.where(keep, g * 0.5 / 0.8, torch.zeros_like(g)), rtol=1e-6, name="dx")
+    assert_close(res.grad, g, rtol=0, name="dres")
+
+
+@pytest.mark.parametrize("D", [64, 256, 640, 2560])
+@pytest.mark.parametrize("dy_bf16", [False, True])
+def test_layernorm_bwd(dev, D, dy_bf16):
+    from speechbrain_amd import _autograd as A
+    g = torch.Generator().manual_seed(D)
+    M = 1003
+    x = torch.randn(M, D, generator=g) * 2 + 0.3
+    ln = torch.nn.LayerNorm(D)
+    with torch.no_grad():
+        ln.weight.copy_(1 + 0.2 * torch.randn(D, generator=g))
+        ln.bias.copy_(0.1 * torch.randn(D, generator=g))
+    dy = torch.randn(M, D, generator=g)
+    if dy_bf16:
+        dy = dy.to(torch.bfloat16).float()
+    xr = x.clone().requires_grad_(True)
+    F.layer_norm(xr, (D,), ln.weight, ln.bias, 1e-5).backward(dy)
+    lnd = torch.nn.LayerNorm(D).to(dev)
+    lnd.load_state_dict(ln.state_dict())
+    xd = x.to(dev).requires_grad_(True)
+    y = A.layer_norm(xd, lnd)
+    assert_close(y, F.layer_norm(x, (D,), ln.weight, ln.bias, 1e-5).detach(), rtol=1e-5, name="fwd")
+    y.backward(dy.to(dev).to(torch.bfloat16) if dy_bf16 else dy.to(dev))
+    assert_grad(xd.grad, xr.grad, name="dx")
+    assert_grad(lnd.weight.grad, ln.weight.grad, name="dgamma")
+    assert_grad(lnd.bias.grad, ln.bias.grad, name="dbeta")
+
+
+@pytest.mark.parametrize("name", ["swish", "glu", "leaky_relu"])
+def test_act_bwd(dev, name):
+    from speechbrain_amd import _autograd as A
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(777, 96, generator=g) * 3
+    xr = x.clone().requires_grad_(True)
+    ref = {"swish": lambda t: t * torch.sigmoid(t), "glu": lambda t: F.glu(t, dim=-1),
+           "leaky_relu": lambda t: F.leaky_relu(t, 0.01)}[name](xr)
+    dy = torch.randn(ref.shape, generator=g)
+    ref.backward(dy)
+    xd = x.to(dev).requires_grad_(True)
+    y = A.act(xd, name, 0.01)
+    assert_close(y, ref.detach(), rtol=1e-5, name="fwd")
+    y.backward(dy.to(dev))
+    assert_grad(xd.grad, xr.grad, rtol=1e-5, name="dx")
+
+
+@pytest.mark.parametrize("K,causal", [(31, False), (7, True), (3, False)])
+def test_dwconv_fwd_bwd(dev, K, causal):
+    from speechbrain_amd import _autograd as A
+    g = torch.Generator().manual_seed(K)
+    B, T, C = 3, 77, 64
+    x = torch.randn(B, T, C, generator=g)
+    w = torch.randn(C, 1, K, generator=g) / math.sqrt(K)
+    b = torch.randn(C, generator=g)
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
+    pad = K - 1 if causal else (K - 1) // 2
+    ref = F.conv1d(xr.transpose(1, 2), wr, br, padding=pad, groups=C)
+    if causal:
+        ref = ref[..., :-pad]
+    ref = ref.transpose(1, 2)
+    dy = torch.randn(ref.shape, generator=g)
+    ref.backward(dy)
+    xd, wd, bd = (t.to(dev).requires_grad_(True) for t in (x, w, b))
+    y = A.DwConvFn.apply(xd.reshape(B * T, C), wd, bd, B, T, causal)
+    assert_close(y.view(B, T, C), ref.detach(), rtol=1e-5, name="fwd")
+    y.backward(dy.to(dev).reshape(B * T, C))
+    assert_grad(xd.grad, xr.grad, name="dx")
+    assert_grad(wd.grad, wr.grad, name="dw")
+    assert_grad(bd.grad, br.grad, name="db")
+
+
+@pytest.mark.parametrize("Ti,Fi,Ci,Co", [(101, 80, 1, 64), (51, 40, 64, 32), (3, 3, 8, 16), (8, 5, 16, 16)])
+def test_conv_block_fn_vs_oracle(dev, Ti, Fi, Ci, Co):
+    """im2col (reflect pad) + MFMA GEMM + (freq x chan) LayerNorm + LeakyReLU
+    and its backward (col2im) vs autograd of the oracle ConvBlock."""
+    from speechbrain_amd import _autograd as A
+    g = torch.Generator().manual_seed(Ti * Ci)
+    B = 2
+    x = torch.randn(B, Ti, Fi, Ci, generator=g)
+    w = torch.randn(Co, Ci, 3, 3, generator=g) / math.sqrt(9 * Ci)
+    b = 0.1 * torch.randn(Co, generator=g)
+    To, Fo = (Ti - 1) // 2 + 1, (Fi - 1) // 2 + 1
+    lw = 1 + 0.1 * torch.randn(Fo, Co, generator=g)
+    lb = 0.1 * torch.randn(Fo, Co, generator=g)
+    leaves = [t.clone().requires_grad_(True) for t in (x, w, b, lw, lb)]
+    sd = {"conv_0.conv.weight": leaves[1], "conv_0.conv.bias": leaves[2], "norm_0.norm.weight": leaves[3],
+          "norm_0.norm.bias": leaves[4]}
+    ref = OC.conv_block(leaves[0], sd, "")
+    dy = torch.randn(ref.shape, generator=g)
+    ref.backward(dy)
+    dl = [t.to(dev).requires_grad_(True) for t in (x, w, b, lw, lb)]
+    y = A.ConvBlockFn.apply(dl[0], dl[1], dl[2], dl[3], dl[4], 1e-5, 0.01, torch.float32, torch.float32)
+    assert_close(y, ref.detach(), rtol=1e-4, name="fwd")
+    y.backward(dy.to(dev))
+    for n, a, r in zip(("dx", "dw", "db", "dln_w", "dln_b"), dl, leaves):
+        assert_grad(a.grad, r.grad, name=n)
+
+
+@pytest.mark.parametrize("T,lens", [(37, [37, 30, 21]), (97, [97, 60, 5])])
+def test_relpos_attention_bwd_vs_oracle(dev, T, lens):
+    from speechbrain_amd.nnet.attention import RelPosEncXL, RelPosMHAXL
+    torch.manual_seed(T)
+    d, H = 64, 4
+    mha = RelPosMHAXL(embed_dim=d, num_heads=H)
+    B = len(lens)
+    x = torch.randn(B, T, d)
+    pe = RelPosEncXL(d)(x)
+    kpm = torch.arange(T)[None] >= torch.tensor(lens)[:, None]
+    sd = {k: v.clone().requires_grad_(True) for k, v in mha.state_dict().items()}
+    xr = x.clone().requires_grad_(True)
+    ref, ref_attn = OC.rel_pos_mha(xr, pe, sd, "", H, kpm)
+    dy = torch.randn(ref.shape)
+    ref.backward(dy)
+    mha = mha.to(dev).train()
+    xd = x.to(dev).requires_grad_(True)
+    out, attn = mha(xd, xd, xd, pe.to(dev), key_padding_mask=kpm.to(dev))
+    assert_close(out, ref.detach(), name="fwd")
+    assert_close(attn, ref_attn.detach(), name="attn")
+    out.backward(dy.to(dev))
+    assert_grad(xd.grad, xr.grad, name="dx")
+    for k, p in mha.named_parameters():
+        assert_grad(p.grad, sd[k].grad, name=k)
+
+
+@pytest.mark.parametrize("act", [0, 3, 5, 6])
+def test_joint_fwd_bwd(dev, act):
+    from speechbrain_amd import _autograd as A
+    g = torch.Generator().manual_seed(act)
+    B, T, U1, J = 2, 9, 5, 130
+    tn = torch.randn(B, T, J, generator=g)
+    pn = torch.randn(B, U1, J, generator=g)
+    tr, pr = tn.clone().requires_grad_(True), pn.clone().requires_grad_(True)
+    z = tr.unsqueeze(2) + pr.unsqueeze(1)
+    z = {0: lambda t: t, 3: lambda t: F.leaky_relu(t, 0.01), 5: torch.tanh, 6: F.relu}[act](z)
+    dz = torch.randn(z.shape, generator=g)
+    z.backward(dz)
+    td, pd = tn.to(dev).requires_grad_(True), pn.to(dev).requires_grad_(True)
+    y = A.JointFn.apply(td, pd, act, 0.01, torch.float32)
+    assert_close(y, z.detach(), rtol=1e-5, name="fwd")
+    y.backward(dz.to(dev))
+    assert_grad(td.grad, tr.grad, rtol=1e-5, name="dtn")
+    assert_grad(pd.grad, pr.grad, rtol=1e-5, name="dpn")
+
+
+# ------------------------------------------------------------- whole encoder
+def _modules(golden, dev, dropout=0.0):
+    from speechbrain_amd.lobes.models.convolution import ConvolutionFrontEnd
+    from speechbrain_amd.lobes.models.transformer.TransformerASR import TransformerASR
+    g = golden("conformer")
+    cnn = ConvolutionFrontEnd(input_shape=(8, 10, 80), num_blocks=2, num_layers_per_block=1, out_channels=(64, 32),
+                              kernel_sizes=(3, 3), strides=(2, 2), residuals=(False, False), dropout=dropout)
+    tr = TransformerASR(tgt_vocab=10, input_size=640, d_model=64, nhead=4, num_encoder_layers=2,
+                        num_decoder_layers=0, d_ffn=128, dropout=dropout, encoder_module="conformer",
+                        attention_type="RelPosMHAXL", normalize_before=True, causal=False)
+    for pre, m in (("cnn.", cnn), ("tr.", tr)):
+        m.load_state_dict({k[len(pre):]: torch.from_numpy(g[k]) for k in g.files if k.startswith(pre)}, strict=True)
+    return cnn.to(dev).train(), tr.to(dev).train(), g
+
+
+def test_encoder_grads_vs_reference(golden, dev):
+    """fp32 training path: every parameter gradient and the feature gradient
+    of sum(R * encode(cnn(feats))) vs the reference's autograd (train.npz)."""
+    cnn, tr, g = _modules(golden, dev)
+    gt = golden("train")
+    feats = torch.from_numpy(g["feats"]).to(dev).requires_grad_(True)
+    y = tr.encode(cnn(feats), torch.from_numpy(g["wav_len"]).to(dev))
+    assert_close(y, gt["y"], name="y")
+    (y * torch.from_numpy(gt["R"]).to(dev)).sum().backward()
+    assert_grad(feats.grad, gt["grad_feats"], name="feats")
+    n = 0
+    for pre, m in (("cnn.", cnn), ("tr.", tr)):
+        for k, p in m.named_parameters():
+            key = "grad." + pre + k
+            if key in gt.files:
+                assert p.grad is not None, key
+                assert_grad(p.grad, gt[key], name=key)
+                n += 1
+            else:
+                assert p.grad is None or not p.grad.any(), key
+    assert n == sum(1 for k in gt.files if k.startswith("grad."))
+
+
+def test_encoder_grads_bf16_autocast(golden, dev):
+    """bf16 operands (autocast) vs the reference fp32 gradients: cosine > 0.99 per tensor."""
+    cnn, tr, g = _modules(golden, dev)
+    gt = golden("train")
+    feats = torch.from_numpy(g["feats"]).to(dev)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = tr.encode(cnn(feats), torch.from_numpy(g["wav_len"]).to(dev))
+    assert y.dtype == torch.float32
+    (y * torch.from_numpy(gt["R"]).to(dev)).sum().backward()
+    for pre, m in (("cnn.", cnn), ("tr.", tr)):
+        for k, p in m.named_parameters():
+            key = "grad." + pre + k
+            if key in gt.files:
+                c = cosine(p.grad, torch.from_numpy(gt[key]))
+                assert c > 0.99, (key, c)
+
+
+def test_encoder_train_dropout(golden, dev):
+    """Training mode with dropout 0.1 (recipe value): stochastic, finite, and
+    identical for identical seeds; eval mode is deterministic and dropout-free."""
+    cnn, tr, g = _modules(golden, dev, dropout=0.1)
+    feats = torch.from_numpy(g["feats"]).to(dev)
+    wl = torch.from_numpy(g["wav_len"]).to(dev)
+    torch.manual_seed(5)
+    y1 = tr.encode(cnn(feats), wl)
+    y1.sum().backward()
+    torch.manual_seed(5)
+    y2 = tr.encode(cnn(feats), wl)
+    y3 = tr.encode(cnn(feats), wl)
+    assert torch.isfinite(y1).all()
+    assert torch.equal(y1, y2)
+    assert not torch.equal(y1, y3)
+    assert all(torch.isfinite(p.grad).all() for p in tr.parameters() if p.grad is not None)
+    cnn.eval()
+    tr.eval()
+    with torch.no_grad():
+        ye = tr.encode(cnn(feats), wl)
+    assert_close(ye, golden("train")["y"], name="eval")

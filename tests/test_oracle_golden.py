@@ -171,6 +171,29 @@ def test_conformer_encoder_direct(golden):
     assert_close(OC.rel_shift(torch.from_numpy(g["relshift_in"])), g["relshift_out"], rtol=0)
 
 
+def test_conformer_grads_vs_reference(golden):
+    """Oracle autograd (CPU restatement) vs the reference's own gradients
+    (train.npz): pins the checker used by tests/test_gpu_train.py."""
+    g = golden("conformer")
+    gt = golden("train")
+    sd_c = {k: v.clone().requires_grad_(True) for k, v in _sub(g, "cnn.").items()}
+    sd_t = {k: v.clone().requires_grad_(True) for k, v in _sub(g, "tr.").items()}
+    feats = torch.from_numpy(g["feats"]).clone().requires_grad_(True)
+    y = OC.transformer_asr_encode(OC.conv_frontend(feats, sd_c), sd_t, "", 2, 4, torch.from_numpy(g["wav_len"]))
+    assert_close(y, gt["y"], rtol=1e-5, name="y")
+    (y * torch.from_numpy(gt["R"])).sum().backward()
+    pairs = [("grad_feats", feats)] + [("grad.cnn." + k, v) for k, v in sd_c.items()] + \
+        [("grad.tr." + k, v) for k, v in sd_t.items()]
+    n = 0
+    for key, t in pairs:
+        if key in gt.files:
+            ref = gt[key]
+            err = np.abs(t.grad.numpy() - ref).max()
+            assert err <= 1e-5 * max(np.abs(ref).max(), 1e-12), (key, err)
+            n += 1
+    assert n == len([k for k in gt.files if k.startswith("grad")])
+
+
 KAT_LOGITS = np.array([[[[0.1, 0.6, 0.1, 0.1, 0.1], [0.1, 0.1, 0.6, 0.1, 0.1], [0.1, 0.1, 0.2, 0.8, 0.1]],
                         [[0.1, 0.6, 0.1, 0.1, 0.1], [0.1, 0.1, 0.2, 0.1, 0.1], [0.7, 0.1, 0.2, 0.1, 0.1]]]],
                       np.float32)
