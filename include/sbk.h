@@ -270,11 +270,15 @@ int sbk_col2im3s2(const void* dcol, int dcol_bf16, int B, int Ti, int Fi, int Ci
 
 /* Transducer_joint "sum" (transducer_joint.py:57-95): z[b,t,u,:] = act(tn[b,t,:] + pn[b,u,:]),
  * act 0 none, 3 LeakyReLU(slope), 5 tanh, 6 ReLU; tn (B, T, J), pn (B, U1, J) fp32, z fp32/bf16.
- * Backward: dtn = sum_u dz act', dpn = sum_t dz act'. */
+ * Backward: dtn = sum_u dz act', dpn = sum_t dz act' — one pass over dz (block per
+ * (b, 16-frame run, 512 columns)), per-run dpn partials in ws
+ * (sbk_joint_bwd_workspace_floats floats) reduced deterministically.  Vector paths for J % 4 == 0
+ * (fwd) / J % 2 == 0 (bwd), scalar otherwise. */
+long long sbk_joint_bwd_workspace_floats(int B, int T, int U1, int J);
 int sbk_joint_fwd(const float* tn, const float* pn, int B, int T, int U1, int J, int act, float slope, void* z,
                   int z_bf16, void* stream);
 int sbk_joint_bwd(const float* tn, const float* pn, const void* dz, int dz_bf16, int B, int T, int U1, int J, int act,
-                  float slope, float* dtn, float* dpn, void* stream);
+                  float slope, float* dtn, float* dpn, float* ws, void* stream);
 
 /* Dropout + residual (nn.Dropout before the residual adds of Conformer.py:242-259,
  * attention.py:630, convolution.py:175, TransformerASR custom_src_module):

@@ -20,6 +20,12 @@ def t(fn, n=5):
 
 
 fl = 2.0 * M * N * K
+for tile in (2, 1, 3, 7, 11, 12, 19, 21):
+    try:
+        s = t(lambda: _enc.gemm(a, w, tile=tile))
+        print(f"sbk_gemm tile {tile}: {s*1e3:.3f} ms  {fl/s/1e12:.1f} TF/s", flush=True)
+    except Exception as e:
+        print("tile", tile, "failed", e)
 for name, fn in [("sbk_gemm f32out", lambda: _enc.gemm(a, w)),
                  ("torch.mm bf16out", lambda: torch.mm(a, w.t())),
                  ("torch.mm f32out", lambda: torch.mm(a, w.t(), out_dtype=torch.float32) if hasattr(torch.mm, "__call__") else None)]:

@@ -65,6 +65,27 @@ def colsum(part, rows, cols):
 
 
 # ------------------------------------------------------- dropout / residual
+def wgrad(g, a):
+    """dW = g^T a in fp32 for g (M, N), a (M, K) — the weight gradient of a
+    Linear.  For the tall-skinny case (M >> N, K: M = B*T rows, N, K <= 1024)
+    one library GEMM has too few output tiles to fill 256 CUs, so the
+    reduction over M is split into S batched GEMMs (fp32 outputs) summed in
+    a fixed order."""
+    M, N = g.shape
+    K = a.shape[1]
+    S = 1
+    while S < 16 and M // (2 * S) >= 1024 and (N // 64) * (K // 64) * S < 1024:
+        S *= 2
+    kw = {"out_dtype": _f32} if g.dtype == _bf16 else {}
+    if S == 1:
+        return torch.mm(g.t(), a, **kw)
+    m = M // S
+    head = torch.bmm(g[: S * m].view(S, m, N).transpose(1, 2), a[: S * m].view(S, m, K), **kw).sum(0)
+    if S * m < M:
+        head += torch.mm(g[S * m:].t(), a[S * m:], **kw)
+    return head
+
+
 def drop_add(x, res=None, alpha=1.0, rowmask=None, p=0.0, seed=0, out_dtype=_f32):
     """out = res + alpha * rowmask0(dropout_p(x)) — one HIP launch (sbk_dropout_add)."""
     x = _cont(x)
@@ -157,7 +178,7 @@ class LinearFn(Function):
             g = _as(dy, a.dtype)
             gb = dy
         da = torch.mm(g, wk) if ctx.needs_input_grad[0] else None
-        dw = torch.mm(g.t(), a).float().view(ctx.wshape) if ctx.needs_input_grad[1] else None
+        dw = wgrad(g, a).view(ctx.wshape) if ctx.needs_input_grad[1] else None
         db = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = rowsum(gb if gb is not None else drop_add(dy, None, ctx.alpha, rowmask, 0.0, 0, _f32))
@@ -401,7 +422,7 @@ class ConvBlockFn(Function):
         dlw, dlb = gb[:D].view_as(ln_w), gb[D:].view_as(ln_w)
         dc = dc.view(B * To * Fo, Co)
         g = _as(dc, col.dtype)
-        dwp = torch.mm(g.t(), col).float()  # (Co, ldcol)
+        dwp = wgrad(g, col)  # (Co, ldcol)
         dw = dwp[:, : 9 * Ci].reshape(Co, 3, 3, Ci).permute(0, 3, 2, 1).reshape(wshape)
         db = rowsum(dc) if has_bias else None
         dx = None
@@ -437,8 +458,10 @@ class JointFn(Function):
         dz = _cont(dz)
         dtn = torch.empty_like(tn)
         dpn = torch.empty_like(pn)
-        check(lib().sbk_joint_bwd(ptr(tn), ptr(pn), ptr(dz), _bf(dz), B, T, U1, J, ctx.a[0], float(ctx.a[1]), ptr(dtn),
-                                  ptr(dpn), stream_of(tn)), "sbk_joint_bwd")
+        L = lib()
+        ws = torch.empty(int(L.sbk_joint_bwd_workspace_floats(B, T, U1, J)), device=tn.device, dtype=_f32)
+        check(L.sbk_joint_bwd(ptr(tn), ptr(pn), ptr(dz), _bf(dz), B, T, U1, J, ctx.a[0], float(ctx.a[1]), ptr(dtn),
+                              ptr(dpn), ptr(ws), stream_of(tn)), "sbk_joint_bwd")
         return dtn, dpn, None, None, None
 
 

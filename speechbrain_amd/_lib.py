@@ -81,9 +81,10 @@ SIGNATURES = {
     "sbk_col2im3s2": [_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp],
     "sbk_joint_fwd": [_vp, _vp, _i, _i, _i, _i, _i, _f, _vp, _i, _vp],
     "sbk_dropout_add": [_vp, _i, _vp, _ll, _i, _vp, _f, _f, ctypes.c_ulonglong, _vp, _i, _vp],
-    "sbk_joint_bwd": [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp],
+    "sbk_joint_bwd": [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp],
+    "sbk_joint_bwd_workspace_floats": [_i, _i, _i, _i],
 }
-RESTYPES = {"sbk_relpos_attention_lds": ctypes.c_longlong, "sbk_rnnt_workspace_floats": ctypes.c_longlong}
+RESTYPES = {"sbk_relpos_attention_lds": ctypes.c_longlong, "sbk_joint_bwd_workspace_floats": ctypes.c_longlong, "sbk_rnnt_workspace_floats": ctypes.c_longlong}
 
 _lib = None
 _load_error = None

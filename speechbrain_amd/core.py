@@ -83,7 +83,7 @@ class Brain:
     def init_optimizers(self):
         self.optimizer = self.opt_class(self.modules.parameters())
 
-    def zero_grad(self, set_to_none=False):
+    def zero_grad(self, set_to_none=True):
         self.optimizer.zero_grad(set_to_none)
 
     @contextlib.contextmanager

@@ -160,26 +160,52 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
-// part[j, c] = sum of x[r, c] over rows r of chunk j (thread per column).
+// part[j, c] = sum of x[r, c] over rows r of chunk j (thread per column;
+// 8 loads in flight per thread).
 __global__ void rowsum_partial_kernel(const void* __restrict__ x, int x_bf16, long long rows, int cols, int rows_per,
                                       float* __restrict__ part) {
   const int c = blockIdx.y * blockDim.x + threadIdx.x;
   if (c >= cols) return;
   const long long r0 = (long long)blockIdx.x * rows_per;
   const long long r1 = min(r0 + rows_per, rows);
-  float s = 0.f;
-  for (long long r = r0; r < r1; ++r) s += ldv(x, r * cols + c, x_bf16);
-  part[(long long)blockIdx.x * cols + c] = s;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  long long r = r0;
+  for (; r + 8 <= r1; r += 8) {
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = ldv(x, (r + i) * cols + c, x_bf16);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i & 3] += v[i];
+  }
+  for (; r < r1; ++r) s[0] += ldv(x, r * cols + c, x_bf16);
+  part[(long long)blockIdx.x * cols + c] = (s[0] + s[1]) + (s[2] + s[3]);
 }
 
-// out[c] (+)= sum_r part[r, c]  — deterministic column reduction.
-__global__ void colsum_kernel(const float* __restrict__ part, int rows, int cols, float* __restrict__ out,
-                              int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
-  float s = 0.f;
-  for (int r = 0; r < rows; ++r) s += part[(long long)r * cols + c];
-  out[c] = accumulate ? out[c] + s : s;
+// out[c] (+)= sum_r part[r, c] — deterministic column reduction.  A block
+// covers 64 columns with 16 waves; wave w sums rows w, w + 16, ... and the 16
+// wave partials are added in a fixed order.
+__global__ void __launch_bounds__(1024) colsum_kernel(const float* __restrict__ part, int rows, int cols,
+                                                      float* __restrict__ out, int accumulate) {
+  __shared__ float red[16][65];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float s[2] = {0.f, 0.f};
+  if (c < cols) {
+    int r = w;
+    for (; r + 16 < rows; r += 32) {
+      s[0] += part[(long long)r * cols + c];
+      s[1] += part[(long long)(r + 16) * cols + c];
+    }
+    if (r < rows) s[0] += part[(long long)r * cols + c];
+  }
+  red[w][lane] = s[0] + s[1];
+  __syncthreads();
+  if (w == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][lane];
+    out[c] = accumulate ? out[c] + t : t;
+  }
 }
 
 // ------------------------------------------------------------- activations
@@ -228,73 +254,85 @@ __global__ void act_bwd_kernel(int mode, const void* __restrict__ x, int x_bf16,
 }
 
 // ------------------------------------------------------- depthwise conv1d
-// y[b, t, c] = bias[c] + sum_k w[c, k] x[b, t + k - padL, c]   (zero padding)
-__global__ void dwconv_fwd_kernel(const void* __restrict__ x, int x_bf16, int B, int T, int C,
-                                  const float* __restrict__ w, const float* __restrict__ bias, int K, int padL,
-                                  void* __restrict__ y, int y_bf16) {
-  const long long n = (long long)B * T * C;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    const long long bt = i / C;
-    const int t = (int)(bt % T);
-    const long long base = (bt - t) * C + c;
-    float s = bias ? bias[c] : 0.f;
-    for (int k = 0; k < K; ++k) {
-      const int ts = t + k - padL;
-      if (ts >= 0 && ts < T) s += w[c * K + k] * ldv(x, base + (long long)ts * C, x_bf16);
-    }
-    stv(y, i, s, y_bf16);
+// Register-window kernels: a thread owns one channel c of one utterance b
+// and a run of DW_RUN consecutive frames; the 31-tap window of x slides
+// through VGPRs (one load per output instead of K).  Taps beyond K are zero,
+// so one KMAX = 31 instantiation serves every K <= 31.
+//   y[b, t, c] = bias[c] + sum_k w[c, k] x[b, t + k - padL, c]   (zero padding)
+constexpr int DW_KMAX = 31;
+constexpr int DW_RUN = 32;
+
+__global__ void __launch_bounds__(256) dwconv_fwd_kernel(const void* __restrict__ x, int x_bf16, int B, int T, int C,
+                                                         const float* __restrict__ w, const float* __restrict__ bias,
+                                                         int K, int padL, int reverse, void* __restrict__ y,
+                                                         int y_bf16) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nrun = (T + DW_RUN - 1) / DW_RUN;
+  const int b = blockIdx.y / nrun, t0 = (blockIdx.y % nrun) * DW_RUN;
+  if (c >= C) return;
+  float wk[DW_KMAX], win[DW_KMAX];
+#pragma unroll
+  for (int k = 0; k < DW_KMAX; ++k) wk[k] = k < K ? w[c * K + (reverse ? K - 1 - k : k)] : 0.f;
+  const long long base = (long long)b * T * C + c;
+#pragma unroll
+  for (int k = 0; k < DW_KMAX - 1; ++k) {
+    const int ts = t0 + k - padL;
+    win[k] = (k < K - 1 && ts >= 0 && ts < T) ? ldv(x, base + (long long)ts * C, x_bf16) : 0.f;
+  }
+  const float b0 = bias ? bias[c] : 0.f;
+  const int t1 = min(t0 + DW_RUN, T);
+  for (int t = t0; t < t1; ++t) {
+    const int ts = t + K - 1 - padL;
+    win[DW_KMAX - 1] = 0.f;
+#pragma unroll
+    for (int k = 0; k < DW_KMAX; ++k)
+      if (k == K - 1) win[k] = (ts >= 0 && ts < T) ? ldv(x, base + (long long)ts * C, x_bf16) : 0.f;
+    float s = b0;
+#pragma unroll
+    for (int k = 0; k < DW_KMAX; ++k) s += wk[k] * win[k];
+    stv(y, base + (long long)t * C, s, y_bf16);
+#pragma unroll
+    for (int k = 0; k < DW_KMAX - 1; ++k) win[k] = win[k + 1];
   }
 }
 
-// dx[b, t, c] = sum_k w[c, k] dy[b, t - k + padL, c]
-__global__ void dwconv_dgrad_kernel(const float* __restrict__ dy, int B, int T, int C, const float* __restrict__ w,
-                                    int K, int padL, void* __restrict__ dx, int dx_bf16) {
-  const long long n = (long long)B * T * C;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    const long long bt = i / C;
-    const int t = (int)(bt % T);
-    const long long base = (bt - t) * C + c;
-    float s = 0.f;
-    for (int k = 0; k < K; ++k) {
-      const int to = t - k + padL;
-      if (to >= 0 && to < T) s += w[c * K + k] * dy[base + (long long)to * C];
-    }
-    stv(dx, i, s, dx_bf16);
-  }
-}
-
-// Per-chunk partial weight / bias gradients: chunk j covers sequence rows
-// [j*rows_per, (j+1)*rows_per) of one utterance-major (B*T) list; one thread
-// per channel accumulates its K taps.  part: (nchunk, C, K + 1) [taps | bias].
-template <int KMAX>
+// Per-run partial weight / bias gradients: part (B * nrun, C, K + 1) of
+// [dw taps | dbias], dw[c, k] = sum_t dy[b, t, c] x[b, t + k - padL, c].
 __global__ void __launch_bounds__(256) dwconv_wgrad_kernel(const void* __restrict__ x, int x_bf16,
                                                            const float* __restrict__ dy, int B, int T, int C, int K,
-                                                           int padL, int rows_per, float* __restrict__ part) {
-  const int c = blockIdx.y * blockDim.x + threadIdx.x;
+                                                           int padL, float* __restrict__ part) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nrun = (T + DW_RUN - 1) / DW_RUN;
+  const int b = blockIdx.y / nrun, t0 = (blockIdx.y % nrun) * DW_RUN;
   if (c >= C) return;
-  float acc[KMAX + 1];
+  float acc[DW_KMAX + 1], win[DW_KMAX];
 #pragma unroll
-  for (int k = 0; k <= KMAX; ++k) acc[k] = 0.f;
-  const long long r0 = (long long)blockIdx.x * rows_per;
-  const long long r1 = min(r0 + rows_per, (long long)B * T);
-  for (long long r = r0; r < r1; ++r) {
-    const int t = (int)(r % T);
-    const long long base = (r - t) * C + c;
-    const float g = dy[r * C + c];
-    acc[KMAX] += g;
+  for (int k = 0; k <= DW_KMAX; ++k) acc[k] = 0.f;
+  const long long base = (long long)b * T * C + c;
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      if (k < K) {
-        const int ts = t + k - padL;
-        if (ts >= 0 && ts < T) acc[k] += g * ldv(x, base + (long long)ts * C, x_bf16);
-      }
-    }
+  for (int k = 0; k < DW_KMAX - 1; ++k) {
+    const int ts = t0 + k - padL;
+    win[k] = (k < K - 1 && ts >= 0 && ts < T) ? ldv(x, base + (long long)ts * C, x_bf16) : 0.f;
   }
-  float* p = part + ((long long)blockIdx.x * C + c) * (K + 1);
-  for (int k = 0; k < K; ++k) p[k] = acc[k];
-  p[K] = acc[KMAX];
+  const int t1 = min(t0 + DW_RUN, T);
+  for (int t = t0; t < t1; ++t) {
+    const int ts = t + K - 1 - padL;
+    win[DW_KMAX - 1] = 0.f;
+#pragma unroll
+    for (int k = 0; k < DW_KMAX; ++k)
+      if (k == K - 1) win[k] = (ts >= 0 && ts < T) ? ldv(x, base + (long long)ts * C, x_bf16) : 0.f;
+    const float g = dy[base + (long long)t * C];
+    acc[DW_KMAX] += g;
+#pragma unroll
+    for (int k = 0; k < DW_KMAX; ++k) acc[k] += g * win[k];
+#pragma unroll
+    for (int k = 0; k < DW_KMAX - 1; ++k) win[k] = win[k + 1];
+  }
+  float* p = part + ((long long)blockIdx.y * C + c) * (K + 1);
+#pragma unroll
+  for (int k = 0; k < DW_KMAX; ++k)
+    if (k < K) p[k] = acc[k];
+  p[K] = acc[DW_KMAX];
 }
 
 // -------------------------------------------------- rel-pos softmax backward
@@ -411,48 +449,116 @@ __device__ __forceinline__ float joint_dact(int act, float v, float slope) {
   return 1.f;
 }
 
-__global__ void joint_fwd_kernel(const float* __restrict__ tn, const float* __restrict__ pn, int T, int U1, int J,
-                                 int act, float slope, void* __restrict__ z, int z_bf16) {
-  // block per (b, t, u) row
-  const long long row = blockIdx.x;
-  const int u = (int)(row % U1);
-  const long long bt = row / U1;
+// z[b, t, u, :] for all u of one (b, t): block per (b, t), thread per 4
+// columns (float4 tn/pn loads, 8/16-byte stores); tn read once per (b, t).
+__global__ void __launch_bounds__(256) joint_fwd_kernel(const float* __restrict__ tn, const float* __restrict__ pn,
+                                                        int T, int U1, int J, int act, float slope,
+                                                        void* __restrict__ z, int z_bf16) {
+  const long long bt = blockIdx.x;
   const int b = (int)(bt / T);
-  const float* a = tn + bt * J;
-  const float* c = pn + ((long long)b * U1 + u) * J;
-  for (int j = threadIdx.x; j < J; j += blockDim.x) stv(z, row * J + j, joint_act(act, a[j] + c[j], slope), z_bf16);
+  for (int j = threadIdx.x * 4; j < J; j += blockDim.x * 4) {
+    const float4 a = *reinterpret_cast<const float4*>(tn + bt * J + j);
+    for (int u = 0; u < U1; ++u) {
+      const float4 c = *reinterpret_cast<const float4*>(pn + ((long long)b * U1 + u) * J + j);
+      const float v0 = joint_act(act, a.x + c.x, slope), v1 = joint_act(act, a.y + c.y, slope);
+      const float v2 = joint_act(act, a.z + c.z, slope), v3 = joint_act(act, a.w + c.w, slope);
+      const long long o = (bt * U1 + u) * J + j;
+      if (z_bf16) {
+        uint2 q;
+        q.x = (unsigned)f32_to_bf16(v0) | ((unsigned)f32_to_bf16(v1) << 16);
+        q.y = (unsigned)f32_to_bf16(v2) | ((unsigned)f32_to_bf16(v3) << 16);
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(z) + o) = q;
+      } else {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(z) + o) = make_float4(v0, v1, v2, v3);
+      }
+    }
+  }
 }
 
-// dtn[b, t, :] = sum_u dz * act'(.)  (block per (b, t))
-__global__ void joint_bwd_tn_kernel(const float* __restrict__ tn, const float* __restrict__ pn,
-                                    const void* __restrict__ dz, int dz_bf16, int T, int U1, int J, int act,
-                                    float slope, float* __restrict__ dtn) {
+// Scalar variants for J not a multiple of the vector width.
+__global__ void joint_fwd_scalar_kernel(const float* __restrict__ tn, const float* __restrict__ pn, int T, int U1,
+                                        int J, int act, float slope, void* __restrict__ z, int z_bf16) {
   const long long bt = blockIdx.x;
   const int b = (int)(bt / T);
   for (int j = threadIdx.x; j < J; j += blockDim.x) {
     const float a = tn[bt * J + j];
-    float s = 0.f;
     for (int u = 0; u < U1; ++u)
-      s += ldv(dz, (bt * U1 + u) * J + j, dz_bf16) * joint_dact(act, a + pn[((long long)b * U1 + u) * J + j], slope);
+      stv(z, (bt * U1 + u) * J + j, joint_act(act, a + pn[((long long)b * U1 + u) * J + j], slope), z_bf16);
+  }
+}
+
+__global__ void joint_bwd_scalar_kernel(const float* __restrict__ tn, const float* __restrict__ pn,
+                                        const void* __restrict__ dz, int dz_bf16, int T, int U1, int J, int act,
+                                        float slope, float* __restrict__ dtn, float* __restrict__ part, int B) {
+  const long long bt = blockIdx.x;  // part: (T, B, U1, J) — one run per frame
+  const int b = (int)(bt / T), t = (int)(bt % T);
+  for (int j = threadIdx.x; j < J; j += blockDim.x) {
+    const float a = tn[bt * J + j];
+    float s = 0.f;
+    for (int u = 0; u < U1; ++u) {
+      const float g = ldv(dz, (bt * U1 + u) * J + j, dz_bf16) * joint_dact(act, a + pn[((long long)b * U1 + u) * J + j], slope);
+      s += g;
+      part[(((long long)t * B + b) * U1 + u) * J + j] = g;
+    }
     dtn[bt * J + j] = s;
   }
 }
 
-// dpn[b, u, :] = sum_t dz * act'(.)  (block per (b, u))
-__global__ void joint_bwd_pn_kernel(const float* __restrict__ tn, const float* __restrict__ pn,
-                                    const void* __restrict__ dz, int dz_bf16, int T, int U1, int J, int act,
-                                    float slope, float* __restrict__ dpn) {
-  const long long bu = blockIdx.x;
-  const int b = (int)(bu / U1), u = (int)(bu % U1);
-  for (int j = threadIdx.x; j < J; j += blockDim.x) {
-    const float c = pn[bu * J + j];
-    float s = 0.f;
-    for (int t = 0; t < T; ++t) {
-      const long long bt = (long long)b * T + t;
-      s += ldv(dz, (bt * U1 + u) * J + j, dz_bf16) * joint_dact(act, tn[bt * J + j] + c, slope);
-    }
-    dpn[bu * J + j] = s;
+// Joint backward, dz read once: block per (b, run of JB_T frames, 512
+// columns); thread per 2 columns keeps tn and dtn of its JB_T frames in
+// VGPRs and loops u: dtn[b, t, :] = sum_u dz act'(.) (complete), and the
+// run's partial dpn[b, u, :] = sum_{t in run} dz act'(.) -> part (nrun, B, U1, J).
+constexpr int JB_T = 16;
+__global__ void __launch_bounds__(256) joint_bwd_kernel(const float* __restrict__ tn, const float* __restrict__ pn,
+                                                        const void* __restrict__ dz, int dz_bf16, int B, int T, int U1,
+                                                        int J, int act, float slope, float* __restrict__ dtn,
+                                                        float* __restrict__ part) {
+  const int nrun = (T + JB_T - 1) / JB_T;
+  const int b = blockIdx.y / nrun, run = blockIdx.y % nrun, t0 = run * JB_T;
+  const int j = (blockIdx.x * blockDim.x + threadIdx.x) * 2;
+  if (j >= J) return;
+  const int nt = min(JB_T, T - t0);
+  float a0[JB_T], a1[JB_T], d0[JB_T], d1[JB_T];
+#pragma unroll
+  for (int i = 0; i < JB_T; ++i) {
+    const bool ok = i < nt;
+    const long long r = ((long long)b * T + t0 + (ok ? i : 0)) * J + j;
+    const float2 v = *reinterpret_cast<const float2*>(tn + r);
+    a0[i] = v.x;
+    a1[i] = v.y;
+    d0[i] = 0.f;
+    d1[i] = 0.f;
   }
+  for (int u = 0; u < U1; ++u) {
+    const float2 c = *reinterpret_cast<const float2*>(pn + ((long long)b * U1 + u) * J + j);
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < JB_T; ++i) {
+      if (i < nt) {
+        const long long o = (((long long)b * T + t0 + i) * U1 + u) * J + j;
+        float g0, g1;
+        if (dz_bf16) {
+          const unsigned q = *reinterpret_cast<const unsigned*>(reinterpret_cast<const bf16_t*>(dz) + o);
+          g0 = bf16_to_f32((bf16_t)(q & 0xffffu));
+          g1 = bf16_to_f32((bf16_t)(q >> 16));
+        } else {
+          const float2 q = *reinterpret_cast<const float2*>(reinterpret_cast<const float*>(dz) + o);
+          g0 = q.x;
+          g1 = q.y;
+        }
+        g0 *= joint_dact(act, a0[i] + c.x, slope);
+        g1 *= joint_dact(act, a1[i] + c.y, slope);
+        d0[i] += g0;
+        d1[i] += g1;
+        s0 += g0;
+        s1 += g1;
+      }
+    }
+    *reinterpret_cast<float2*>(part + (((long long)run * B + b) * U1 + u) * J + j) = make_float2(s0, s1);
+  }
+#pragma unroll
+  for (int i = 0; i < JB_T; ++i)
+    if (i < nt) *reinterpret_cast<float2*>(dtn + ((long long)b * T + t0 + i) * J + j) = make_float2(d0[i], d1[i]);
 }
 
 // ------------------------------------------------ dropout / residual add
@@ -498,7 +604,7 @@ SBK_API int sbk_dropout_add(const void* x, int x_bf16, const float* res, long lo
   return 0;
 }
 
-SBK_API int sbk_layernorm_bwd_blocks(int M) { return grid_for((M + 3) / 4, 1, 1024); }
+SBK_API int sbk_layernorm_bwd_blocks(int M) { return grid_for((M + 3) / 4, 1, 256); }
 
 SBK_API int sbk_layernorm_bwd(const float* x, const void* dy, int dy_bf16, int M, int D, const float* g, float eps,
                               const float* dres, float* dx, float* part, void* stream) {
@@ -530,7 +636,7 @@ SBK_API int sbk_layernorm_wide(const float* x, int M, int D, const float* g, con
   return 0;
 }
 
-SBK_API int sbk_rowsum_chunks(long long rows) { return (int)std::min<long long>(256, std::max<long long>(1, rows / 64)); }
+SBK_API int sbk_rowsum_chunks(long long rows) { return (int)std::min<long long>(128, std::max<long long>(1, rows / 64)); }
 
 // out (cols) fp32 = sum over rows of x (rows, cols) (+ out when accumulate);
 // part: sbk_rowsum_chunks(rows) * cols floats of scratch.
@@ -543,14 +649,14 @@ SBK_API int sbk_rowsum(const void* x, int x_bf16, long long rows, int cols, floa
   dim3 grid(nchunk, (cols + 255) / 256);
   rowsum_partial_kernel<<<grid, 256, 0, s>>>(x, x_bf16, rows, cols, rows_per, part);
   SBK_CHECK_LAUNCH();
-  colsum_kernel<<<(cols + 255) / 256, 256, 0, s>>>(part, nchunk, cols, out, accumulate);
+  colsum_kernel<<<(cols + 63) / 64, 1024, 0, s>>>(part, nchunk, cols, out, accumulate);
   SBK_CHECK_LAUNCH();
   return 0;
 }
 
 SBK_API int sbk_colsum(const float* part, int rows, int cols, float* out, int accumulate, void* stream) {
   if (rows <= 0 || cols <= 0) return SBK_ERR_ARG;
-  colsum_kernel<<<(cols + 255) / 256, 256, 0, (hipStream_t)stream>>>(part, rows, cols, out, accumulate);
+  colsum_kernel<<<(cols + 63) / 64, 1024, 0, (hipStream_t)stream>>>(part, rows, cols, out, accumulate);
   SBK_CHECK_LAUNCH();
   return 0;
 }
@@ -577,35 +683,32 @@ SBK_API int sbk_act_bwd(int mode, const void* x, int x_bf16, const void* dy, int
 
 SBK_API int sbk_dwconv_fwd(const void* x, int x_bf16, int B, int T, int C, const float* w, const float* bias, int K,
                            int causal, void* y, int y_bf16, void* stream) {
-  if (B <= 0 || T <= 0 || C <= 0 || K <= 0 || K > 64) return SBK_ERR_ARG;
+  if (B <= 0 || T <= 0 || C <= 0 || K <= 0 || K > DW_KMAX) return SBK_ERR_ARG;
   const int padL = causal ? K - 1 : (K - 1) / 2;
-  dwconv_fwd_kernel<<<grid_for((long long)B * T * C, 256), 256, 0, (hipStream_t)stream>>>(x, x_bf16, B, T, C, w, bias,
-                                                                                          K, padL, y, y_bf16);
+  const int nrun = (T + DW_RUN - 1) / DW_RUN;
+  dim3 grid((C + 255) / 256, B * nrun);
+  dwconv_fwd_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(x, x_bf16, B, T, C, w, bias, K, padL, 0, y, y_bf16);
   SBK_CHECK_LAUNCH();
   return 0;
 }
 
-SBK_API int sbk_dwconv_wgrad_chunks(int B, int T) {
-  const long long rows = (long long)B * T;
-  return (int)std::min<long long>(256, std::max<long long>(1, rows / 32));
-}
+SBK_API int sbk_dwconv_wgrad_chunks(int B, int T) { return B * ((T + DW_RUN - 1) / DW_RUN); }
 
-// dx (optional) and per-chunk (nchunk, C, K+1) weight|bias partials.
+// dx (optional) and per-run (nchunk, C, K+1) weight|bias partials.  dx is the
+// forward kernel on dy with the taps reversed and padL' = K - 1 - padL.
 SBK_API int sbk_dwconv_bwd(const void* x, int x_bf16, const float* dy, int B, int T, int C, const float* w, int K,
                            int causal, void* dx, int dx_bf16, float* part, void* stream) {
-  if (B <= 0 || T <= 0 || C <= 0 || K <= 0 || K > 31) return SBK_ERR_ARG;
+  if (B <= 0 || T <= 0 || C <= 0 || K <= 0 || K > DW_KMAX) return SBK_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int padL = causal ? K - 1 : (K - 1) / 2;
+  const int nrun = (T + DW_RUN - 1) / DW_RUN;
+  dim3 grid((C + 255) / 256, B * nrun);
   if (dx) {
-    dwconv_dgrad_kernel<<<grid_for((long long)B * T * C, 256), 256, 0, s>>>(dy, B, T, C, w, K, padL, dx, dx_bf16);
+    dwconv_fwd_kernel<<<grid, 256, 0, s>>>(dy, 0, B, T, C, w, nullptr, K, K - 1 - padL, 1, dx, dx_bf16);
     SBK_CHECK_LAUNCH();
   }
   if (part) {
-    const int nchunk = sbk_dwconv_wgrad_chunks(B, T);
-    const long long rows = (long long)B * T;
-    const int rows_per = (int)((rows + nchunk - 1) / nchunk);
-    dim3 grid(nchunk, (C + 255) / 256);
-    dwconv_wgrad_kernel<31><<<grid, 256, 0, s>>>(x, x_bf16, dy, B, T, C, K, padL, rows_per, part);
+    dwconv_wgrad_kernel<<<grid, 256, 0, s>>>(x, x_bf16, dy, B, T, C, K, padL, part);
     SBK_CHECK_LAUNCH();
   }
   return 0;
@@ -642,19 +745,39 @@ SBK_API int sbk_col2im3s2(const void* dcol, int dcol_bf16, int B, int Ti, int Fi
 SBK_API int sbk_joint_fwd(const float* tn, const float* pn, int B, int T, int U1, int J, int act, float slope, void* z,
                           int z_bf16, void* stream) {
   if (B <= 0 || T <= 0 || U1 <= 0 || J <= 0) return SBK_ERR_ARG;
-  joint_fwd_kernel<<<(unsigned)((long long)B * T * U1), 256, 0, (hipStream_t)stream>>>(tn, pn, T, U1, J, act, slope,
-                                                                                     z, z_bf16);
+  if (J % 4)
+    joint_fwd_scalar_kernel<<<(unsigned)((long long)B * T), 256, 0, (hipStream_t)stream>>>(tn, pn, T, U1, J, act,
+                                                                                          slope, z, z_bf16);
+  else
+    joint_fwd_kernel<<<(unsigned)((long long)B * T), 256, 0, (hipStream_t)stream>>>(tn, pn, T, U1, J, act, slope, z,
+                                                                                   z_bf16);
   SBK_CHECK_LAUNCH();
   return 0;
 }
 
+SBK_API long long sbk_joint_bwd_workspace_floats(int B, int T, int U1, int J) {
+  return (long long)(J % 2 ? T : (T + JB_T - 1) / JB_T) * B * U1 * J;
+}
+
+// ws: sbk_joint_bwd_workspace_floats() floats (per-run dpn partials).
 SBK_API int sbk_joint_bwd(const float* tn, const float* pn, const void* dz, int dz_bf16, int B, int T, int U1, int J,
-                          int act, float slope, float* dtn, float* dpn, void* stream) {
-  if (B <= 0 || T <= 0 || U1 <= 0 || J <= 0) return SBK_ERR_ARG;
+                          int act, float slope, float* dtn, float* dpn, float* ws, void* stream) {
+  if (B <= 0 || T <= 0 || U1 <= 0 || J <= 0 || !ws) return SBK_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  joint_bwd_tn_kernel<<<(unsigned)((long long)B * T), 256, 0, s>>>(tn, pn, dz, dz_bf16, T, U1, J, act, slope, dtn);
+  int nrun;
+  if (J % 2) {
+    nrun = T;
+    joint_bwd_scalar_kernel<<<(unsigned)((long long)B * T), 256, 0, s>>>(tn, pn, dz, dz_bf16, T, U1, J, act, slope,
+                                                                         dtn, ws, B);
+  } else {
+    nrun = (T + JB_T - 1) / JB_T;
+    dim3 grid((J / 2 + 255) / 256, B * nrun);
+    joint_bwd_kernel<<<grid, 256, 0, s>>>(tn, pn, dz, dz_bf16, B, T, U1, J, act, slope, dtn, ws);
+  }
   SBK_CHECK_LAUNCH();
-  joint_bwd_pn_kernel<<<(unsigned)((long long)B * U1), 256, 0, s>>>(tn, pn, dz, dz_bf16, T, U1, J, act, slope, dpn);
+  const long long cols = (long long)B * U1 * J;
+  if (cols > 0x7fffffffLL) return SBK_ERR_ARG;
+  colsum_kernel<<<(unsigned)((cols + 63) / 64), 1024, 0, s>>>(ws, nrun, (int)cols, dpn, 0);
   SBK_CHECK_LAUNCH();
   return 0;
 }

@@ -748,7 +748,11 @@ SBK_API int sbk_gemm(int dtype_bf16, const void* A, int lda, const void* W, int 
   if (act == ACT_GLU && (N % 32)) return SBK_ERR_ARG;  // whole [a16|gate16] groups
   Epi ep{bias, act, slope, res, ldr, alpha, rowmask, out, ldc, out_bf16};
   hipStream_t s = (hipStream_t)stream;
-  if (tile == 0) tile = 2;  // measured best for every encoder shape (scripts/kbench.py gemm)
+  // tile 2 (64x64x64) measured best for every encoder shape (M = B*T = 12032,
+  // scripts/kbench.py gemm); the joint-output projection of the transducer
+  // (M = B*T*U1 = 782080, N = 1000, K = 1024) runs 1.5x faster on 128x128x128
+  // (scripts/logits_gemm_probe.py: 3.69 -> 2.46 ms, 652 TF/s).
+  if (tile == 0) tile = (dtype_bf16 && (long long)M * N >= (32LL << 20) && K >= 512 && N >= 256) ? 7 : 2;
   if (dtype_bf16) {
     switch (tile) {
       case 1: return launch<bf16_t, 128, 128, 64>(A, lda, W, ldw, M, N, K, ep, s);

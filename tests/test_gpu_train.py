@@ -194,21 +194,29 @@ def test_relpos_attention_bwd_vs_oracle(dev, T, lens):
 
 
 @pytest.mark.parametrize("act", [0, 3, 5, 6])
-def test_joint_fwd_bwd(dev, act):
+@pytest.mark.parametrize("J", [130, 131, 1024])
+@pytest.mark.parametrize("z_bf16", [False, True])
+def test_joint_fwd_bwd(dev, act, J, z_bf16):
+    """Vector (J % 4 == 0 / J % 2 == 0) and scalar paths; 37 frames = two
+    16-frame runs + a ragged one; bf16 z / dz: the reference is fed the same
+    bf16-rounded dz and compared at bf16 resolution for z."""
     from speechbrain_amd import _autograd as A
-    g = torch.Generator().manual_seed(act)
-    B, T, U1, J = 2, 9, 5, 130
+    g = torch.Generator().manual_seed(act + J)
+    B, T, U1 = 2, 37, 5
     tn = torch.randn(B, T, J, generator=g)
     pn = torch.randn(B, U1, J, generator=g)
     tr, pr = tn.clone().requires_grad_(True), pn.clone().requires_grad_(True)
     z = tr.unsqueeze(2) + pr.unsqueeze(1)
     z = {0: lambda t: t, 3: lambda t: F.leaky_relu(t, 0.01), 5: torch.tanh, 6: F.relu}[act](z)
     dz = torch.randn(z.shape, generator=g)
+    zdt = torch.bfloat16 if z_bf16 else torch.float32
+    dz = dz.to(zdt).float()
     z.backward(dz)
     td, pd = tn.to(dev).requires_grad_(True), pn.to(dev).requires_grad_(True)
-    y = A.JointFn.apply(td, pd, act, 0.01, torch.float32)
-    assert_close(y, z.detach(), rtol=1e-5, name="fwd")
-    y.backward(dz.to(dev))
+    y = A.JointFn.apply(td, pd, act, 0.01, zdt)
+    assert y.dtype == zdt
+    assert_close(y.float(), z.detach(), rtol=1e-5 if not z_bf16 else 8e-3, name="fwd")
+    y.backward(dz.to(dev).to(zdt))
     assert_grad(td.grad, tr.grad, rtol=1e-5, name="dtn")
     assert_grad(pd.grad, pr.grad, rtol=1e-5, name="dpn")
 
