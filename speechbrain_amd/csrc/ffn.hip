@@ -34,6 +34,12 @@
 // hidden chunk in registers (78 us).  A shared 3-slot ring with a barrier per
 // K-step took 42 us; wave-private rows (no per-step barrier), a 2-slot ring
 // and chunk-parity Hs: 35 us (M = 12032, H = 1024; 8 waves the same).
+// Also tried (compile-time options, off): a per-XCD rotated hidden-chunk order
+// (SBK_FFN_ROT, 34.4 -> 35.0 us) and a 3-slot ring with a single hidden buffer
+// (SBK_FFN_NB3, 37.2 us).  Neither L2 channel contention nor in-flight bytes
+// is the limit; the LDS traffic is: per 64-deep step the 16 waves read
+// 8 KB of fragments each (6 KB of it the shared activation tile) besides
+// the 32 KB DMA fill, ~1,250 LDS cycles per step.
 #include "mfma.h"
 
 using namespace sbk;
@@ -183,7 +189,13 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   constexpr int T = 256 / 16 / FFN_NW;       // 16-row weight tiles per wave (HC/16/NW = D/16/NW)
   constexpr int BK = 64;                     // K per step: one 128-B line per weight row
   constexpr int K1 = D / BK, K2 = HC / BK, SPC = K1 + K2;
+#ifdef SBK_FFN_NB3
+  constexpr int NB = 3;                      // ring slots, two tiles in flight behind the one being read
+  constexpr int HSB = 1;                     // single hidden buffer (LDS for the third slot)
+#else
   constexpr int NB = 2;                      // ring slots: a slot is refilled as soon as its fragments are in VGPRs
+  constexpr int HSB = 2;                     // hidden chunk double-buffered by chunk parity
+#endif
   constexpr int TROWS = 256;                 // rows per weight tile (HC for W1, D for W2)
   constexpr int GL = TROWS * BK * 2 / 16 / NT;  // LDS-DMA instructions per thread per tile (2)
   static_assert(GL * 8 == T * 16, "each wave stages exactly the weight rows it multiplies");
@@ -194,13 +206,22 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   bf16_t* ring = reinterpret_cast<bf16_t*>(smem);          // NB x TROWS x BK (linear 128-B rows)
   bf16_t* Xn = ring + NB * TROWS * BK;                      // BM x XS
   bf16_t* Hs = Xn + BM * XS;                                // BM x HS
-  float* b1s = reinterpret_cast<float*>(Hs + 2 * BM * HS);  // H          (Hs: 2 x BM x HS, chunk parity)
+  float* b1s = reinterpret_cast<float*>(Hs + HSB * BM * HS);  // H          (Hs: HSB x BM x HS)
   float (*red)[BM] = reinterpret_cast<float (*)[BM]>(b1s + a.H);  // NW x BM
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int fr = lane & 15, g = lane >> 4, fk = 8 * g;
   const int m0 = blockIdx.x * BM;
-  const int S = (a.H / HC) * SPC;
+  const int NCH = a.H / HC;
+  const int S = NCH * SPC;
+#ifdef SBK_FFN_ROT
+  // hidden chunks in a per-workgroup rotated order: the workgroups of one XCD
+  // (blockIdx = xcd mod 8) start on different weight chunks, so their
+  // concurrent L2 reads spread over different lines/channels
+  const int rot = (blockIdx.x >> 3) % NCH;
+#else
+  const int rot = 0;
+#endif
 #ifdef SBK_PROBE_TL
   const int tl_rec = blockIdx.x == 128 ? w : -1;
 #endif
@@ -237,7 +258,8 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
 #if defined(SBK_PROBE_NO_DMA) || defined(SBK_PROBE_SKEL)
     if (s >= 0) return;
 #endif
-    const int c = s / SPC, r = s - c * SPC;
+    const int cl = s / SPC, r = s - cl * SPC;
+    const int c = cl + rot < NCH ? cl + rot : cl + rot - NCH;  // physical hidden chunk
     const bool p1 = r < K1;
     const bf16_t* base = p1 ? a.w1 + (long long)c * HC * D + r * BK : a.w2 + c * HC + (r - K1) * BK;
     const int ld = p1 ? D : a.H;
@@ -253,6 +275,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   };
   issue(0, 0);
   issue(1, 1);
+  if (NB == 3) issue(2, 2);
 
   // LayerNorm of the workgroup's rows -> Xn (bf16); b1 -> LDS
 #pragma unroll
@@ -296,17 +319,17 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   for (int s = 0; s < S; ++s) {
     const int c = s / SPC, r = s - c * SPC;
     // this wave's rows of tile s landed (tile s+1 stays in flight)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL * (NB - 1)) : "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (s == 0 || r == K1) __builtin_amdgcn_s_barrier();
+    if (s == 0 || r == K1 || (HSB == 1 && r == K1 - 1 && c > 0)) __builtin_amdgcn_s_barrier();
     if (s < 34) FFN_TL(2 + 2 * s);
     const bf16_t* tile = ring + (s % NB) * TROWS * BK;
-    bf16_t* Hc = Hs + (c & 1) * BM * HS;  // this chunk's hidden activations
+    bf16_t* Hc = Hs + (HSB == 2 ? (c & 1) : 0) * BM * HS;  // this chunk's hidden activations
     // once this step's fragments are in VGPRs its slot takes tile s+2
     // (tail: a harmless reload of the last tile)
     auto refill = [&]() __attribute__((always_inline)) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      issue(min(s + 2, S - 1), s % NB);
+      issue(min(s + NB, S - 1), s % NB);
     };
     bf16x8 fw[BK / 32][T], fa[BK / 32][MT];
 #pragma unroll
@@ -346,7 +369,8 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
           // in-flight LDS-DMA tiles), draining the weight stream
           f32x4 bb;
           {
-            const uint32_t la = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)(b1s + c * HC + n));
+            const int pc = c + rot < NCH ? c + rot : c + rot - NCH;
+            const uint32_t la = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)(b1s + pc * HC + n));
             asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(bb) : "v"(la) : "memory");
           }
 #pragma unroll
@@ -444,8 +468,12 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
 
 template <int D>
 size_t ffn_lds(int H) {
-  constexpr size_t ring = (size_t)2 * 256 * 64;
-  return (ring + (size_t)FFN_BM * (D + 16) + (size_t)2 * FFN_BM * (256 + 16)) * sizeof(bf16_t) +
+#ifdef SBK_FFN_NB3
+  constexpr size_t ring = (size_t)3 * 256 * 64, hsb = 1;
+#else
+  constexpr size_t ring = (size_t)2 * 256 * 64, hsb = 2;
+#endif
+  return (ring + (size_t)FFN_BM * (D + 16) + hsb * FFN_BM * (256 + 16)) * sizeof(bf16_t) +
          (size_t)H * 4 + (size_t)FFN_NW * FFN_BM * 4;
 }
 
