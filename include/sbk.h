@@ -203,6 +203,12 @@ int sbk_relpos_attention(int dtype_bf16, const void* qkv, const void* pk, const 
                          const uint8_t* kpm, int B, int T, int H, int dh, float scale, void* out, float* probs,
                          void* stream);
 
+/* Same with the positional rows at row stride ldp (>= d): the p_k of every layer
+ * can come from ONE linear_pos GEMM over the stacked weights, (2T-1, L*d), layer l
+ * at column offset l*d. */
+int sbk_relpos_attention_ld(int dtype_bf16, const void* qkv, const void* pk, int ldp, const float* pbu,
+                            const float* pbv, const unsigned char* kpm, int B, int T, int H, int dh, float scale,
+                            void* out, float* probs, void* stream);
 /* LDS bytes one attention workgroup needs (host-side capacity check). */
 long long sbk_relpos_attention_lds(int dtype_bf16, int T, int dh);
 

@@ -181,10 +181,12 @@ def relpos_attention(qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale, need_probs=Fals
     """Fused RelPosMHAXL core.  qkv: (B*T, 3d) head-interleaved, pk: (2T-1, d),
     both bf16 or fp32; returns (out (B*T, d) in qkv.dtype, probs or None)."""
     d = H * dh
+    if pk.stride(-1) != 1 or pk.shape[-1] != d:
+        raise ValueError("pk must be (2T-1, d) with unit column stride")
     out = torch.empty(B * T, d, device=qkv.device, dtype=qkv.dtype)
     probs = torch.empty(B, H, T, T, device=qkv.device, dtype=_f32) if need_probs else None
-    rc = lib().sbk_relpos_attention(int(_is_bf16(qkv)), ptr(qkv), ptr(pk), ptr(pbu), ptr(pbv), ptr(kpm), B, T, H, dh,
-                                    float(scale), ptr(out), ptr(probs), stream_of(qkv))
+    rc = lib().sbk_relpos_attention_ld(int(_is_bf16(qkv)), ptr(qkv), ptr(pk), pk.stride(0), ptr(pbu), ptr(pbv),
+                                       ptr(kpm), B, T, H, dh, float(scale), ptr(out), ptr(probs), stream_of(qkv))
     check(rc, "sbk_relpos_attention")
     return out, probs
 

@@ -97,7 +97,7 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
                                                            const float* __restrict__ pbv,
                                                            const uint8_t* __restrict__ kpm, int B, int Tn, int H,
                                                            int dh, float scale, T* __restrict__ out,
-                                                           float* __restrict__ probs, int vec_ok) {
+                                                           float* __restrict__ probs, int vec_ok, int ldp) {
   using Tr = MT<T>;
   using L = FlashLds<T, DHP>;
   constexpr int KR = L::KR, VR = L::VR, VEC = Tr::VEC;
@@ -213,7 +213,7 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
     for (int i = 0; i < NPC; ++i) {
       const int c = tid + 256 * i, rr = c / CPR, d = (c % CPR) * VEC, r = rbase + rr;
       okp[i] = rr < PBR - 1 && r >= 0 && r <= 2 * Tn - 2 && d < dh;
-      rp[i] = *reinterpret_cast<const uint4*>(pk_h + (long long)min(max(r, 0), 2 * Tn - 2) * d_model +
+      rp[i] = *reinterpret_cast<const uint4*>(pk_h + (long long)min(max(r, 0), 2 * Tn - 2) * ldp +
                                               min(d, dh - VEC));
     }
     if (tid < KC) {
@@ -264,7 +264,7 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
     }
     for (int e = tid; e < PBR * DHP; e += 256) {
       const int rr = e / DHP, d = e - rr * DHP, r = rbase + rr;
-      Ps[rr * KR + d] = (rr < PBR - 1 && r >= 0 && r <= 2 * Tn - 2 && d < dh) ? pk_h[(long long)r * d_model + d]
+      Ps[rr * KR + d] = (rr < PBR - 1 && r >= 0 && r <= 2 * Tn - 2 && d < dh) ? pk_h[(long long)r * ldp + d]
                                                                               : Tr::from_f32(0.f);
     }
     if (tid < KC) {
@@ -470,23 +470,23 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
 }
 
 template <typename T, int DHP>
-int launch(const void* qkv, const void* pk, const float* pbu, const float* pbv, const uint8_t* kpm, int B, int Tn,
-           int H, int dh, float scale, void* out, float* probs, hipStream_t s) {
+int launch(const void* qkv, const void* pk, int ldp, const float* pbu, const float* pbv, const uint8_t* kpm, int B,
+           int Tn, int H, int dh, float scale, void* out, float* probs, hipStream_t s) {
   constexpr size_t lds = FlashLds<T, DHP>::bytes;
   static_assert(lds <= 160 * 1024, "LDS budget");
   const int grid = B * H * ((Tn + QB - 1) / QB);
   const int VEC = MT<T>::VEC;
   const int d_model = H * dh;
-  const int vec_ok = (dh % VEC == 0) && (d_model % VEC == 0) &&
+  const int vec_ok = (dh % VEC == 0) && (d_model % VEC == 0) && (ldp % VEC == 0) &&
                      ((reinterpret_cast<uintptr_t>(qkv) | reinterpret_cast<uintptr_t>(pk) | reinterpret_cast<uintptr_t>(out)) % 16 == 0);
   if (probs)
     hipLaunchKernelGGL((relpos_flash_kernel<T, DHP, true>), dim3(grid), dim3(256), lds, s,
                        reinterpret_cast<const T*>(qkv), reinterpret_cast<const T*>(pk), pbu, pbv, kpm, B, Tn, H, dh,
-                       scale, reinterpret_cast<T*>(out), probs, vec_ok);
+                       scale, reinterpret_cast<T*>(out), probs, vec_ok, ldp);
   else
     hipLaunchKernelGGL((relpos_flash_kernel<T, DHP, false>), dim3(grid), dim3(256), lds, s,
                        reinterpret_cast<const T*>(qkv), reinterpret_cast<const T*>(pk), pbu, pbv, kpm, B, Tn, H, dh,
-                       scale, reinterpret_cast<T*>(out), probs, vec_ok);
+                       scale, reinterpret_cast<T*>(out), probs, vec_ok, ldp);
   SBK_CHECK_LAUNCH();
   return 0;
 }
@@ -496,16 +496,22 @@ int launch(const void* qkv, const void* pk, const float* pbu, const float* pbv, 
 // qkv: (B, T, 3*d) head-interleaved in_proj output [h][q|k|v][dh];
 // pk: (2T-1, d) linear_pos output; pbu/pbv: (H*dh) fp32; kpm: (B, T) uint8 or null;
 // out: (B, T, d); probs: (B, H, T, T) fp32 or null.
+SBK_API int sbk_relpos_attention_ld(int dtype_bf16, const void* qkv, const void* pk, int ldp, const float* pbu,
+                                    const float* pbv, const uint8_t* kpm, int B, int Tn, int H, int dh, float scale,
+                                    void* out, float* probs, void* stream) {
+  if (B <= 0 || Tn <= 0 || H <= 0 || dh <= 0 || dh > 128 || ldp < H * dh) return SBK_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype_bf16)
+    return dh <= 64 ? launch<bf16_t, 64>(qkv, pk, ldp, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s)
+                    : launch<bf16_t, 128>(qkv, pk, ldp, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s);
+  return dh <= 64 ? launch<float, 64>(qkv, pk, ldp, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s)
+                  : launch<float, 128>(qkv, pk, ldp, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s);
+}
+
 SBK_API int sbk_relpos_attention(int dtype_bf16, const void* qkv, const void* pk, const float* pbu, const float* pbv,
                                  const uint8_t* kpm, int B, int Tn, int H, int dh, float scale, void* out, float* probs,
                                  void* stream) {
-  if (B <= 0 || Tn <= 0 || H <= 0 || dh <= 0 || dh > 128) return SBK_ERR_ARG;
-  hipStream_t s = (hipStream_t)stream;
-  if (dtype_bf16)
-    return dh <= 64 ? launch<bf16_t, 64>(qkv, pk, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s)
-                    : launch<bf16_t, 128>(qkv, pk, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s);
-  return dh <= 64 ? launch<float, 64>(qkv, pk, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s)
-                  : launch<float, 128>(qkv, pk, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s);
+  return sbk_relpos_attention_ld(dtype_bf16, qkv, pk, H * dh, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, stream);
 }
 
 #ifdef SBK_PROBE_TL

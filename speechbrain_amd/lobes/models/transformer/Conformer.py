@@ -166,13 +166,13 @@ class ConformerEncoderLayer(nn.Module):
     def _ln(self, mod):
         return mod.weight.detach(), mod.bias.detach(), mod.eps
 
-    def fused(self, x, B, T, pos, kpm_u8, dtype, need_attn, u_in=None, next_ln=None, final_ln=None):
+    def fused(self, x, B, T, pos, kpm_u8, dtype, need_attn, u_in=None, next_ln=None, final_ln=None, pk=None):
         """One layer.  x: (B*T, d) fp32 residual stream; pos: (2T-1, d) in
         dtype; u_in: LN_ffn1(x) if a previous kernel already produced it;
         next_ln: (w, b, eps) of the NEXT consumer's LayerNorm to chain after
         norm2; final_ln: the encoder's closing LayerNorm, applied on chip by
-        the fused-FFN path.  Returns (x_out fp32, u_next or None, attn or
-        None, final_ln_applied)."""
+        the fused-FFN path; pk: this layer's linear_pos(pos) if precomputed.
+        Returns (x_out fp32, u_next or None, attn or None, final_ln_applied)."""
         if self.training and self.drop.p > 0:
             raise NotImplementedError("dropout in training mode is not implemented in HIP yet")
         f1, f2 = self.ffn_module1, self.ffn_module2
@@ -182,7 +182,7 @@ class ConformerEncoderLayer(nn.Module):
             x, u = f1[1].run_fused(x, self._ln(f1[0]), 0.5, next_ln=self._ln(self.norm1.norm), next_dtype=dtype)
             # attention output projection + residual + the conv module's LayerNorm in one launch
             x, attn, uc = self.mha_layer.attend(u, B, T, pos, kpm_u8, dtype, need_attn, residual=x,
-                                                post_ln=self.convolution_module.ln_params())
+                                                post_ln=self.convolution_module.ln_params(), pk=pk)
             x = self.convolution_module.run(x, B, T, dtype, kpm_u8, residual=x, u=uc)
             x, y = f2[1].run_fused(x, self._ln(f2[0]), 0.5, post_ln=self._ln(self.norm2.norm), out=x,
                                    next_ln=final_ln, next_dtype=_f32)
@@ -192,7 +192,7 @@ class ConformerEncoderLayer(nn.Module):
         x = f1[1].run(u_in, dtype, residual=x, alpha=0.5)
         u, _ = _enc.layernorm(x, *self._ln(self.norm1.norm), out1_dtype=dtype)
         x, attn, uc = self.mha_layer.attend(u, B, T, pos, kpm_u8, dtype, need_attn, residual=x,
-                                            post_ln=self.convolution_module.ln_params())
+                                            post_ln=self.convolution_module.ln_params(), pk=pk)
         x = self.convolution_module.run(x, B, T, dtype, kpm_u8, residual=x, u=uc)
         u, _ = _enc.layernorm(x, *self._ln(f2[0]), out1_dtype=dtype)
         z = f2[1].run(u, dtype, residual=x, alpha=0.5)
@@ -251,6 +251,18 @@ class ConformerEncoder(nn.Module):
                                   attention_type=attention_type) for i in range(num_layers)])
         self.norm = LayerNorm(d_model, eps=1e-6)
         self.attention_type = attention_type
+        self._wc = _enc.WeightCache()
+
+    def stacked_pos_weight(self, dtype):
+        """linear_pos weights of all layers stacked (L*d, d) in the compute dtype,
+        so p_k of every layer comes from one GEMM (p_k depends only on the
+        positional table, not on the layer input)."""
+        ws = [layer.mha_layer.linear_pos.weight for layer in self.layers]
+
+        def make():
+            w = torch.cat([p.detach() for p in ws], dim=0).contiguous()
+            return _enc.cast_bf16(w) if dtype == _bf16 else w
+        return self._wc.get(("pos", dtype), ws, make)
 
     def train_run(self, src2d, B, T, pos_embs, kpm_u8, dtype):
         """Differentiable stack (training path) on (B*T, d) fp32 → (y, [attn])."""
@@ -272,6 +284,7 @@ class ConformerEncoder(nn.Module):
             return self.train_run(src2d, B, T, pos_embs, kpm_u8, dtype)
         d = src2d.shape[1]
         pos = _enc.to_compute(pos_embs.reshape(-1, d), dtype)
+        pk_all = _enc.gemm(pos, self.stacked_pos_weight(dtype), out_dtype=dtype)  # (2T-1, L*d)
         x = src2d
         u = None
         attns = []
@@ -282,7 +295,7 @@ class ConformerEncoder(nn.Module):
             fn = self.norm.norm
             final_ln = (fn.weight.detach(), fn.bias.detach(), fn.eps) if nxt is None else None
             x, u, a, done = layer.fused(x, B, T, pos, kpm_u8, dtype, need_attn, u_in=u, next_ln=next_ln,
-                                        final_ln=final_ln)
+                                        final_ln=final_ln, pk=pk_all[:, i * d:(i + 1) * d])
             attns.append(a)
             if done:
                 return x, attns

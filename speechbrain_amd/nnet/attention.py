@@ -105,7 +105,7 @@ class RelPosMHAXL(nn.Module):
             return tuple(p.detach() for p in ps)
         return self._wc.get("bf16", ps, lambda: tuple(_enc.cast_bf16(p.detach().contiguous()) for p in ps))
 
-    def attend(self, x2d, B, T, pos_embs, kpm_u8, dtype, need_weights, residual=None, post_ln=None):
+    def attend(self, x2d, B, T, pos_embs, kpm_u8, dtype, need_weights, residual=None, post_ln=None, pk=None):
         """Core used by the fused Conformer layer: x2d (B*T, d) in `dtype`.
         Returns (out (B*T, d) fp32 [+ residual], attn or None); with post_ln =
         (w, b, eps) also u = LN(out) in `dtype` (fused into the output
