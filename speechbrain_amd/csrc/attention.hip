@@ -55,7 +55,16 @@ struct FlashLds {
   static constexpr size_t ps = (size_t)PBR * KR * sizeof(T);
   static constexpr size_t gs = (size_t)4 * GR * GS * 4;
   static constexpr size_t ms = (size_t)(KC + 4) * 4;  // key mask + 'chunk has a masked key' flag
+#ifdef SBK_ATT_NOALIAS
   static constexpr size_t bytes = ks + vt + ps + gs + ms;
+#else
+  // The per-wave G^T scratch aliases the K and positional-band tiles, which
+  // are dead once every wave's S / G MFMAs have consumed them (one barrier):
+  // 66 -> 40 KB per workgroup, three workgroups per CU instead of two, and
+  // the 768 workgroups of a B = 32, T = 376 launch fit in one round.
+  static_assert(gs <= ks + ps, "G^T scratch fits over Ks + Ps");
+  static constexpr size_t bytes = ks + ps + vt + ms;
+#endif
 };
 
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
@@ -109,11 +118,21 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
   constexpr int NPC = PBR * CPR / 256;  // P-band chunks per thread
   static_assert(KC == 64, "mask staging: one wave per chunk");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+#ifdef SBK_ATT_NOALIAS
   T* Ks = reinterpret_cast<T*>(smem);
   T* Vs = reinterpret_cast<T*>(smem + L::ks);
   T* Ps = reinterpret_cast<T*>(smem + L::ks + L::vt);
   float* Gs = reinterpret_cast<float*>(smem + L::ks + L::vt + L::ps);
   float* Ms = reinterpret_cast<float*>(smem + L::ks + L::vt + L::ps + L::gs);
+  constexpr bool ALIAS = false;
+#else
+  T* Ks = reinterpret_cast<T*>(smem);
+  T* Ps = reinterpret_cast<T*>(smem + L::ks);
+  T* Vs = reinterpret_cast<T*>(smem + L::ks + L::ps);
+  float* Gs = reinterpret_cast<float*>(smem);  // over Ks + Ps (dead after the S / G MFMAs)
+  float* Ms = reinterpret_cast<float*>(smem + L::ks + L::ps + L::vt);
+  constexpr bool ALIAS = true;
+#endif
 
   const int d_model = H * dh;
   const long long row3 = 3LL * d_model;
@@ -323,6 +342,7 @@ __global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__
         for (int t = 0; t < 5; ++t) Tr::mma(acc_g[t], fpb[t], fqv[s]);
 #endif
       }
+      if (ALIAS) __syncthreads();  // every wave's Ks / Ps fragment reads are done: the scratch may overwrite them
 #ifndef SBK_PROBE_NO_G
 #pragma unroll
       for (int t = 0; t < 5; ++t)

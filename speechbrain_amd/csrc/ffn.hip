@@ -9,7 +9,7 @@
 // Dropout), 0.5-scaled residuals, norm2 after the second FFN) and
 // speechbrain/nnet/attention.py:823-839 (PositionalwiseFeedForward).
 //
-// Design (MI355X): one workgroup (16 waves) owns BM = 48 rows for
+// Design (MI355X): one workgroup (8 waves) owns BM = 48 rows for
 // the whole block, so neither LN0(x) nor the (BM x H) hidden activation ever
 // leaves the CU:
 //   prologue : x rows (fp32) -> LayerNorm -> bf16 Xn, resident in LDS; b1 -> LDS;
@@ -34,6 +34,8 @@
 // hidden chunk in registers (78 us).  A shared 3-slot ring with a barrier per
 // K-step took 42 us; wave-private rows (no per-step barrier), a 2-slot ring
 // and chunk-parity Hs: 35 us (M = 12032, H = 1024; 8 waves the same).
+// 8 waves with the LayerNorm'd rows held in VGPRs for every phase-1 step
+// (SBK_FFN_XREG, default): 36.7 -> 31.9 us at H = 1024, 58.2 -> 48.5 at 2048.
 // Also tried (compile-time options, off): a per-XCD rotated hidden-chunk order
 // (SBK_FFN_ROT, 34.4 -> 35.0 us) and a 3-slot ring with a single hidden buffer
 // (SBK_FFN_NB3, 37.2 us).  Neither L2 channel contention nor in-flight bytes
@@ -78,7 +80,10 @@ struct IntC {
 
 constexpr int FFN_BM = 48;
 #ifndef SBK_FFN_NW
-#define SBK_FFN_NW 16
+#define SBK_FFN_NW 8
+#endif
+#ifndef SBK_FFN_NO_XREG
+#define SBK_FFN_XREG  // LN'd rows held in VGPRs (needs the 8-wave budget: 226 VGPRs, 2 waves/SIMD)
 #endif
 constexpr int FFN_NW = SBK_FFN_NW, FFN_NT = FFN_NW * 64;
 
@@ -316,12 +321,33 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   // 8 waves 40.8 us, 16 waves spill; weights streamed straight into VGPRs
   // with 4 steps in flight instead of LDS-DMA — 45 us at 8 or 16 waves.)
   FFN_TL(1);
+#ifdef SBK_FFN_XREG
+  // the LayerNorm'd rows are the A operand of every phase-1 step: hold their
+  // fragments in VGPRs for the whole launch instead of re-reading them from
+  // LDS in every chunk (8 waves: 96 VGPRs; cuts the per-step LDS reads)
+  constexpr bool XREG = true;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  bf16x8 xa[K1][BK / 32][MT];
+#pragma unroll
+  for (int r = 0; r < K1; ++r)
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) xa[r][ks][mt] = ld8(Xn + (mt * 16 + fr) * XS + r * BK + ks * 32 + fk);
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+  for (int r = 0; r < SPC; ++r) {
+    const int s = c * SPC + r;
+#else
+  constexpr bool XREG = false;
   for (int s = 0; s < S; ++s) {
     const int c = s / SPC, r = s - c * SPC;
+#endif
     // this wave's rows of tile s landed (tile s+1 stays in flight)
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL * (NB - 1)) : "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (s == 0 || r == K1 || (HSB == 1 && r == K1 - 1 && c > 0)) __builtin_amdgcn_s_barrier();
+    if ((s == 0 && !XREG) || r == K1 || (HSB == 1 && r == K1 - 1 && c > 0)) __builtin_amdgcn_s_barrier();
     if (s < 34) FFN_TL(2 + 2 * s);
     const bf16_t* tile = ring + (s % NB) * TROWS * BK;
     bf16_t* Hc = Hs + (HSB == 2 ? (c & 1) : 0) * BM * HS;  // this chunk's hidden activations
@@ -342,7 +368,15 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
       const bf16_t* abase = r < K1 ? Xn + r * BK : Hc + (r - K1) * BK;
       const int ald = r < K1 ? XS : HS;
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) fa[ks][mt] = ld8(abase + (mt * 16 + fr) * ald + ks * 32 + fk);
+      for (int mt = 0; mt < MT; ++mt) {
+#ifdef SBK_FFN_XREG
+        if (r < K1) {
+          fa[ks][mt] = xa[r < K1 ? r : 0][ks][mt];
+          continue;
+        }
+#endif
+        fa[ks][mt] = ld8(abase + (mt * 16 + fr) * ald + ks * 32 + fk);
+      }
     }
     refill();
 #if defined(SBK_PROBE_NO_MFMA) || defined(SBK_PROBE_SKEL)
