@@ -212,6 +212,18 @@ int sbk_relpos_attention_ld(int dtype_bf16, const void* qkv, const void* pk, int
 /* LDS bytes one attention workgroup needs (host-side capacity check). */
 long long sbk_relpos_attention_lds(int dtype_bf16, int T, int dh);
 
+/* Whole Conformer convolution module in one launch (csrc/convmod.hip; Conformer.py:54-115,254-255),
+ * bf16 MFMA: out = x + rowmask0(Linear2(Swish(LN1(dwconv_K(GLU(Linear1(LN0(x))))))));
+ * x, out (B*T, 256) fp32, out must not alias x; w1p (512, 256) bf16 rows GLU-permuted in
+ * [value16 | gate16] groups (sbk_gemm_glu_group), b1p permuted alike; wc (K, 256) fp32 taps
+ * (tap-major: the transpose of Conv1d.weight (256, 1, K)),
+ * bc (256) or null; w2 (256, 256) bf16, b2 or null; kpm (B*T) uint8 or null.  K <= 31. */
+int sbk_conv_module_supported(int D, int K);
+int sbk_conv_module(const float* x, float* out, int B, int T, int D, const float* ln0_w, const float* ln0_b,
+                    float eps0, const void* w1p, const float* b1p, const float* wc, const float* bc, int K, int causal,
+                    const float* ln1_w, const float* ln1_b, float eps1, const void* w2, const float* b2,
+                    const unsigned char* kpm, void* stream);
+
 /* ------------------------------------------------------------ training path
  * Backward of the Conformer-Transducer encoder (csrc/backward.hip).  The
  * dense contractions of the backward (dX = dY W, dW = dY^T X, attention's

@@ -1,0 +1,27 @@
+"""Conv-module kernel s_memtime phase timeline (probe build -DSBK_PROBE_TL; never the product)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import speechbrain_amd._lib as _L  # noqa: E402
+_L.LIB_PATH = os.environ["SBK_PROBE_LIB"]
+from speechbrain_amd.lobes.models.transformer.Conformer import ConvolutionModule  # noqa: E402
+
+dev = torch.device("cuda")
+B, T = 32, 376
+cm = ConvolutionModule(256, 31).to(dev).eval()
+x = torch.randn(B * T, 256, device=dev)
+with torch.no_grad():
+    for _ in range(5):
+        cm.run_fused(x, B, T, None)
+torch.cuda.synchronize()
+buf = (ctypes.c_ulonglong * 32)()
+assert ctypes.CDLL(_L.LIB_PATH).sbk_probe_cm_tl(buf) == 0
+tl = np.array(buf, dtype=np.int64).reshape(4, 8)
+print("P0 | P1 | P2a | P2b | P3 | total")
+for r in tl:
+    print(" | ".join(str(r[i + 1] - r[i]) for i in range(5)), "|", r[5] - r[0])

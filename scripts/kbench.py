@@ -55,7 +55,7 @@ def gemm_bench():
         r = torch.randn(M, N // 2 if act == "glu" else N, device=dev) if res else None
         fl = 2.0 * M * N * K
         line = f"{name:9s} M={M} N={N} K={K}:"
-        for tile in (2, 9, 18, 19, 20, 21, 22):
+        for tile in (2, 1, 3, 7, 10, 17, 12, 13):
             us = timeit(lambda: _enc.gemm(a, w, bias=b, act=act, res=r, out_dtype=od, tile=tile))
             line += f" t{tile} {us:6.1f}us {fl / us / 1e6:6.0f}TF"
         # library reference point (plain GEMM, no fused epilogue): hipBLASLt via torch
@@ -90,6 +90,18 @@ def gemmln_bench():
     out = _enc.gemm(a, w, bias=bias, res=res)
     us2 = timeit(lambda: _enc.layernorm(out, *ln, out1_dtype=torch.bfloat16))
     print(f"separate: gemm {us1:.1f}us + layernorm {us2:.1f}us", flush=True)
+
+
+def convmod_bench():
+    from speechbrain_amd.lobes.models.transformer.Conformer import ConvolutionModule
+    dev = torch.device("cuda")
+    B, T = 32, 376
+    cm = ConvolutionModule(256, 31).to(dev).eval()
+    x = torch.randn(B * T, 256, device=dev)
+    with torch.no_grad():
+        us = timeit(lambda: cm.run_fused(x, B, T, None))
+        us2 = timeit(lambda: cm.run(x, B, T, torch.bfloat16, None, residual=x))
+    print(f"conv_module fused {us:.1f}us | chain {us2:.1f}us", flush=True)
 
 
 def attn_bench():
@@ -150,6 +162,8 @@ if __name__ == "__main__":
         misc_bench()
     if what == "gemm1":
         gemm_one(sys.argv[2] if len(sys.argv) > 2 else "qkv", int(sys.argv[3]) if len(sys.argv) > 3 else 2)
+    if what in ("convmod", "all"):
+        convmod_bench()
     if what in ("ffn", "all"):
         ffn_bench()
     if what in ("gemmln", "all"):

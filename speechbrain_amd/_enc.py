@@ -130,6 +130,23 @@ def dwconv_ln_swish(x, B, T, w, bias, causal, ln_w, ln_b, eps, out_dtype):
     return out
 
 
+def conv_module_supported(D, K):
+    return bool(lib().sbk_conv_module_supported(int(D), int(K)))
+
+
+def conv_module(x, B, T, ln0, w1p, b1p, wc, bc, causal, ln1, w2, b2, kpm=None):
+    """Fused Conformer convolution module (bf16 MFMA, one launch):
+    x + rowmask0(after_conv(dwconv(GLU(pointwise(LN0(x)))))).  x: (B*T, 256) fp32."""
+    require_device(x, w1p, w2)
+    K = wc.shape[0]  # wc: (K, d) tap-major
+    out = torch.empty_like(x)
+    rc = lib().sbk_conv_module(ptr(x), ptr(out), B, T, x.shape[1], ptr(ln0[0]), ptr(ln0[1]), float(ln0[2]), ptr(w1p),
+                               ptr(b1p), ptr(wc), ptr(bc), K, int(causal), ptr(ln1[0]), ptr(ln1[1]), float(ln1[2]),
+                               ptr(w2), ptr(b2), ptr(kpm), stream_of(x))
+    check(rc, "sbk_conv_module")
+    return out
+
+
 def conv_block_c1(x, w, bias, ln_w, ln_b, eps, slope, out_dtype):
     """ConvBlock with one input channel: x (B, T, F) fp32 → (B, T', F', C)."""
     require_device(x)

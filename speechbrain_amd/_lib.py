@@ -65,6 +65,10 @@ SIGNATURES = {
     "sbk_relpos_attention": [_i, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _vp],
     "sbk_relpos_attention_lds": [_i, _i, _i],
     "sbk_relpos_attention_ld": [_i, _vp, _vp, _i, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _vp],
+    # convmod.hip
+    "sbk_conv_module_supported": [_i, _i],
+    "sbk_conv_module": [_vp, _vp, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _f, _vp, _vp, _vp,
+                        _vp],
     # backward.hip (training path)
     "sbk_layernorm_bwd_blocks": [_i],
     "sbk_layernorm_bwd": [_vp, _vp, _i, _i, _i, _vp, _f, _vp, _vp, _vp, _vp],

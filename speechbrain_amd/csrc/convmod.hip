@@ -1,0 +1,382 @@
+// Fused Conformer convolution module (bf16 MFMA), one launch per layer:
+//
+//   u   = LN0(x)                                   (ConvolutionModule.layer_norm)
+//   g   = GLU(u · W1^T + b1)                       (bottleneck: 1x1 Conv1d d->2d + GLU)
+//   c   = depthwise_conv_k(g) + bc                 (conv, zero padding, causal or centred)
+//   v   = Swish(LN1(c))                            (after_conv[0..1])
+//   out = x + rowmask0(v · W2^T + b2)              (after_conv[2], masked_fill_, residual)
+//
+// Reference: speechbrain/lobes/models/transformer/Conformer.py:54-115
+// (ConvolutionModule) and :254-255 (x + convolution_module(x, conv_mask)).
+//
+// Design (MI355X): a workgroup (16 waves) owns CM_BM = 48 consecutive frames
+// of ONE utterance; B * ceil(T / 48) = 256 workgroups at B = 32, T = 376 —
+// one per CU.  The k - 1 halo frames the depthwise conv needs are recomputed
+// through LN0 and the GLU GEMM (78 rows for 48 outputs), so no intermediate
+// leaves the CU: u, g and v live in LDS (u and v share a buffer), x is read
+// once (plus the halo) and out written once.  This replaces four launches
+// (LN, GLU GEMM, dwconv+LN+Swish, projection GEMM) and the HBM round trips of
+// g and v.
+//   phase 0: x rows (78) -> LN0 -> bf16 U (LDS); rows outside [0, T) -> 0
+//   phase 1: G = GLU(U W1p^T + b1p): wave w owns permuted weight rows
+//            32w .. 32w+31 = GLU group w, so value and gate of a channel land
+//            in the same lane; frames outside [0, T) -> 0
+//            (the conv's zero padding)
+//   phase 2: thread (channel c, quarter h) slides a 31-tap register window
+//            down G for 12 frames into an fp32 LDS tile; then one wave per frame:
+//            LN1 over the channels (4 per lane), Swish -> bf16 V (LDS, over U)
+//            (per-frame wave sums in the conv's thread map cost 34 us: 48
+//            dependent cross-lane reductions per wave)
+//   phase 3: Y = V W2^T (wave w: 16 output units x 48 frames) + b2, row mask,
+//            + x (fp32), float4 stores
+// Weight fragments are loaded straight from global (L2-resident: every
+// workgroup reads the same 384 KB) one K-step ahead of the MFMAs.
+#include "mfma.h"
+
+using namespace sbk;
+
+namespace {
+
+constexpr int CM_D = 256;          // d_model (channels)
+constexpr int CM_BM = 48;          // output frames per workgroup
+constexpr int CM_KMAX = 31;        // max depthwise taps
+constexpr int CM_ROWS = 80;        // staged frames (BM + K - 1 <= 78, padded to 5 m-tiles)
+constexpr int CM_MT1 = CM_ROWS / 16;
+constexpr int CM_MT3 = CM_BM / 16;
+constexpr int CM_NW = 16, CM_NT = CM_NW * 64;
+constexpr int CM_S = CM_D + 16;    // LDS row stride (elements): conflict-free b128 fragment reads
+
+struct ConvModArgs {
+  const float* x;  // (B*T, D) fp32 residual stream
+  float* out;      // (B*T, D) fp32 (must not alias x: neighbours read the halo)
+  int B, T, K, padL;
+  const float *g0, *b0;
+  float eps0;
+  const bf16_t* w1;  // (2D, D) GLU-permuted [value16 | gate16] row groups
+  const float* b1;   // (2D) permuted like w1
+  const float* wc;   // (K, D) depthwise taps, tap-major (host-transposed once)
+  const float* bc;   // (D) or null
+  const float *g1, *b1n;
+  float eps1;
+  const bf16_t* w2;  // (D, D)
+  const float* b2;   // (D) or null
+  const uint8_t* kpm;  // (B*T) padding mask or null
+};
+
+#ifdef SBK_PROBE_TL
+__device__ unsigned long long g_cm_tl[4][8];
+#define CM_TL(i)                                                                                   \
+  do {                                                                                             \
+    if ((blockIdx.x == 100 || blockIdx.x == 7) && (threadIdx.x & 63) == 0 && (threadIdx.x >> 6) < 2) \
+      g_cm_tl[(blockIdx.x == 7) * 2 + (threadIdx.x >> 6)][i] = __builtin_amdgcn_s_memtime();        \
+  } while (0)
+#else
+#define CM_TL(i) \
+  do {           \
+  } while (0)
+#endif
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
+// operations, not for its outstanding global loads (a __syncthreads() fence
+// would drain the weight / residual loads issued ahead of their phase).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ bf16x8 ld8g(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+__global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* Us = reinterpret_cast<bf16_t*>(smem);  // CM_ROWS x CM_S (U, later V)
+  bf16_t* Gs = Us + CM_ROWS * CM_S;              // CM_ROWS x CM_S
+  float* Cv = reinterpret_cast<float*>(Gs + CM_ROWS * CM_S);  // CM_BM x CM_D fp32 conv output
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int fr = lane & 15, g = lane >> 4, fk = 8 * g;
+  const int nblk = (a.T + CM_BM - 1) / CM_BM;
+  const int b = blockIdx.x / nblk, t0 = (blockIdx.x % nblk) * CM_BM;
+  const int f0 = t0 - a.padL;  // frame of staged row 0
+  const int nrows = CM_BM + a.K - 1;
+  const long long ubase = (long long)b * a.T;
+  CM_TL(0);
+  // first K-step of the phase-1 weights and of the phase-3 weights and the
+  // residual rows are issued up front: their latency overlaps phases 0-2
+  constexpr int T1 = 2;                  // phase-1 tiles per wave: (value, gate) of GLU group w
+  constexpr int T3 = CM_D / 16 / CM_NW;  // phase-3 output tiles per wave (1)
+  const bf16_t* wrow1 = a.w1 + (long long)(w * 32 + fr) * CM_D + fk;
+  const bf16_t* wrow3 = a.w2 + (long long)(w * 16 * T3 + fr) * CM_D + fk;
+  bf16x8 fw1[2][T1][2];  // [buffer][tile][ks]
+#pragma unroll
+  for (int t = 0; t < T1; ++t)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) fw1[0][t][ks] = ld8g(wrow1 + t * 16 * CM_D + ks * 32);
+
+  // ---- phase 0: LN0 of the staged frames -> U (bf16) ----
+  // all of the wave's row loads are issued before the first reduction
+  {
+    constexpr int RPW = CM_ROWS / CM_NW;  // rows per wave (5)
+    const float4 g04 = *reinterpret_cast<const float4*>(a.g0 + lane * 4);
+    const float4 b04 = *reinterpret_cast<const float4*>(a.b0 + lane * 4);
+    float4 xv[RPW];
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int r = w + i * CM_NW, f = min(max(f0 + r, 0), a.T - 1);
+      xv[i] = *reinterpret_cast<const float4*>(a.x + (ubase + f) * CM_D + lane * 4);
+    }
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int r = w + i * CM_NW, f = f0 + r;
+      const bool live = r < nrows && f >= 0 && f < a.T;
+      const float v[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+      const float mean = wave_sum(v[0] + v[1] + v[2] + v[3]) * (1.0f / CM_D);
+      float q = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) q += (v[e] - mean) * (v[e] - mean);
+      const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / CM_D) + a.eps0);
+      uint2 pk = make_uint2(0u, 0u);
+      if (live) {
+        pk.x = (uint32_t)f32_to_bf16((v[0] - mean) * rstd * g04.x + b04.x) |
+               ((uint32_t)f32_to_bf16((v[1] - mean) * rstd * g04.y + b04.y) << 16);
+        pk.y = (uint32_t)f32_to_bf16((v[2] - mean) * rstd * g04.z + b04.z) |
+               ((uint32_t)f32_to_bf16((v[3] - mean) * rstd * g04.w + b04.w) << 16);
+      }
+      *reinterpret_cast<uint2*>(Us + r * CM_S + lane * 4) = pk;
+    }
+  }
+  lds_barrier();
+  CM_TL(1);
+
+  // ---- phase 1: G = GLU(U W1p^T + b1p) over CM_ROWS frames ----
+  {
+    f32x4 acc[T1][CM_MT1];
+#pragma unroll
+    for (int t = 0; t < T1; ++t)
+#pragma unroll
+      for (int mt = 0; mt < CM_MT1; ++mt) acc[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bf16_t* wrow = wrow1;
+    auto& fw = fw1;
+#ifndef SBK_PROBE_NO_P1
+#pragma unroll
+    for (int kk = 0; kk < CM_D / 64; ++kk) {
+#else
+    for (int kk = 0; kk < 0; ++kk) {
+#endif
+      const int cur = kk & 1;
+      if (kk + 1 < CM_D / 64) {
+#pragma unroll
+        for (int t = 0; t < T1; ++t)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) fw[cur ^ 1][t][ks] = ld8g(wrow + t * 16 * CM_D + (kk + 1) * 64 + ks * 32);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 fa[CM_MT1];
+#pragma unroll
+        for (int mt = 0; mt < CM_MT1; ++mt)
+          fa[mt] = *reinterpret_cast<const bf16x8*>(Us + (mt * 16 + fr) * CM_S + kk * 64 + ks * 32 + fk);
+#pragma unroll
+        for (int t = 0; t < T1; ++t)
+#pragma unroll
+          for (int mt = 0; mt < CM_MT1; ++mt)
+            acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[cur][t][ks], fa[mt], acc[t][mt], 0, 0, 0);
+      }
+    }
+    // GLU epilogue: lane holds frames mt*16 + fr, units 4g..4g+3 of each
+    // tile; tiles (0, 1) = (value, gate) of channel group w
+    {
+      const int ch = w * 16 + 4 * g;                 // output channels ch .. ch + 3
+      const int pa = w * 32 + 4 * g, pg = pa + 16;   // permuted rows of value / gate
+      const float4 ba = *reinterpret_cast<const float4*>(a.b1 + pa);
+      const float4 bg = *reinterpret_cast<const float4*>(a.b1 + pg);
+      const float bav[4] = {ba.x, ba.y, ba.z, ba.w}, bgv[4] = {bg.x, bg.y, bg.z, bg.w};
+#pragma unroll
+      for (int mt = 0; mt < CM_MT1; ++mt) {
+        const int r = mt * 16 + fr, f = f0 + r;
+        const bool live = r < nrows && f >= 0 && f < a.T;
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float va = acc[0][mt][e] + bav[e], vg = acc[1][mt][e] + bgv[e];
+          o[e] = live ? va * (1.0f / (1.0f + __expf(-vg))) : 0.f;
+        }
+        uint2 pk;
+        pk.x = (uint32_t)f32_to_bf16(o[0]) | ((uint32_t)f32_to_bf16(o[1]) << 16);
+        pk.y = (uint32_t)f32_to_bf16(o[2]) | ((uint32_t)f32_to_bf16(o[3]) << 16);
+        *reinterpret_cast<uint2*>(Gs + r * CM_S + ch) = pk;
+      }
+    }
+  }
+  lds_barrier();
+  CM_TL(2);
+
+  bf16x8 fw3[2][T3][2];
+#pragma unroll
+  for (int t = 0; t < T3; ++t)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) fw3[0][t][ks] = ld8g(wrow3 + t * 16 * CM_D + ks * 32);
+  float4 xr[T3][CM_MT3];
+#pragma unroll
+  for (int t = 0; t < T3; ++t)
+#pragma unroll
+    for (int mt = 0; mt < CM_MT3; ++mt) {
+      const int f = min(t0 + mt * 16 + fr, a.T - 1);
+      xr[t][mt] = *reinterpret_cast<const float4*>(a.x + (ubase + f) * CM_D + w * 16 * T3 + t * 16 + 4 * g);
+    }
+
+  // ---- phase 2: depthwise conv (register window) -> fp32 tile; LN1 -> Swish -> V (over U) ----
+#ifndef SBK_PROBE_NO_P2
+  {
+    // 2a: thread (channel c, quarter h) slides the taps down its channel for 12 frames
+    const int c = tid & (CM_D - 1), h = tid >> 8;  // channel, quarter of the frames
+    constexpr int NF = CM_BM / (CM_NT / CM_D);
+    float wk[CM_KMAX];
+#pragma unroll
+    for (int k = 0; k < CM_KMAX; ++k) wk[k] = k < a.K ? a.wc[k * CM_D + c] : 0.f;  // (K, D): coalesced
+    const float bias = a.bc ? a.bc[c] : 0.f;
+    float win[NF + CM_KMAX - 1];
+#pragma unroll
+    for (int r = 0; r < NF + CM_KMAX - 1; ++r) {
+      const int rr = h * NF + r;
+      win[r] = rr < CM_ROWS ? bf16_to_f32(Gs[rr * CM_S + c]) : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      float s = bias;
+#pragma unroll
+      for (int k = 0; k < CM_KMAX; ++k) s = fmaf(wk[k], win[i + k], s);
+      Cv[(h * NF + i) * CM_D + c] = s;
+    }
+  }
+  lds_barrier();
+  CM_TL(3);
+  {
+    // 2b: one wave per frame, 4 channels per lane
+    const float4 g14 = *reinterpret_cast<const float4*>(a.g1 + lane * 4);
+    const float4 b14 = *reinterpret_cast<const float4*>(a.b1n + lane * 4);
+    const float gm[4] = {g14.x, g14.y, g14.z, g14.w}, bt[4] = {b14.x, b14.y, b14.z, b14.w};
+    for (int fi = w; fi < CM_BM; fi += CM_NW) {
+      const float4 v4 = *reinterpret_cast<const float4*>(Cv + fi * CM_D + lane * 4);
+      float v[4] = {v4.x, v4.y, v4.z, v4.w};
+      const float mean = wave_sum((v[0] + v[1]) + (v[2] + v[3])) * (1.0f / CM_D);
+      float q = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) q += (v[e] - mean) * (v[e] - mean);
+      const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / CM_D) + a.eps1);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float z = (v[e] - mean) * rstd * gm[e] + bt[e];
+        v[e] = z * (1.0f / (1.0f + __expf(-z)));
+      }
+      uint2 pk;
+      pk.x = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
+      pk.y = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
+      *reinterpret_cast<uint2*>(Us + fi * CM_S + lane * 4) = pk;
+    }
+  }
+#endif
+  lds_barrier();
+  CM_TL(4);
+
+  // ---- phase 3: out = x + rowmask0(V W2^T + b2) ----
+  {
+    f32x4 acc[T3][CM_MT3];
+#pragma unroll
+    for (int t = 0; t < T3; ++t)
+#pragma unroll
+      for (int mt = 0; mt < CM_MT3; ++mt) acc[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bf16_t* wrow = wrow3;
+    auto& fw = fw3;
+#pragma unroll
+    for (int kk = 0; kk < CM_D / 64; ++kk) {
+      const int cur = kk & 1;
+      if (kk + 1 < CM_D / 64) {
+#pragma unroll
+        for (int t = 0; t < T3; ++t)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) fw[cur ^ 1][t][ks] = ld8g(wrow + t * 16 * CM_D + (kk + 1) * 64 + ks * 32);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 fa[CM_MT3];
+#pragma unroll
+        for (int mt = 0; mt < CM_MT3; ++mt)
+          fa[mt] = *reinterpret_cast<const bf16x8*>(Us + (mt * 16 + fr) * CM_S + kk * 64 + ks * 32 + fk);
+#pragma unroll
+        for (int t = 0; t < T3; ++t)
+#pragma unroll
+          for (int mt = 0; mt < CM_MT3; ++mt)
+            acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[cur][t][ks], fa[mt], acc[t][mt], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < T3; ++t) {
+      const int d = w * 16 * T3 + t * 16 + 4 * g;
+      const float4 bb = a.b2 ? *reinterpret_cast<const float4*>(a.b2 + d) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int mt = 0; mt < CM_MT3; ++mt) {
+        const int f = t0 + mt * 16 + fr;
+        if (f >= a.T) continue;
+        const bool m = a.kpm && a.kpm[ubase + f];
+        const float4 xv = xr[t][mt];
+        float4 o;
+        o.x = xv.x + (m ? 0.f : acc[t][mt][0] + bb.x);
+        o.y = xv.y + (m ? 0.f : acc[t][mt][1] + bb.y);
+        o.z = xv.z + (m ? 0.f : acc[t][mt][2] + bb.z);
+        o.w = xv.w + (m ? 0.f : acc[t][mt][3] + bb.w);
+        *reinterpret_cast<float4*>(a.out + (ubase + f) * CM_D + d) = o;
+      }
+    }
+  }
+  CM_TL(5);
+}
+
+constexpr size_t conv_module_lds() {
+  return (size_t)2 * CM_ROWS * CM_S * sizeof(bf16_t) + (size_t)CM_BM * CM_D * sizeof(float);
+}
+
+}  // namespace
+
+#ifdef SBK_PROBE_TL
+SBK_API int sbk_probe_cm_tl(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cm_tl), sizeof(g_cm_tl), 0, hipMemcpyDeviceToHost);
+}
+#endif
+
+SBK_API int sbk_conv_module_supported(int D, int K) { return D == CM_D && K >= 1 && K <= CM_KMAX; }
+
+SBK_API int sbk_conv_module(const float* x, float* out, int B, int T, int D, const float* ln0_w, const float* ln0_b,
+                            float eps0, const void* w1p, const float* b1p, const float* wc, const float* bc, int K,
+                            int causal, const float* ln1_w, const float* ln1_b, float eps1, const void* w2,
+                            const float* b2, const unsigned char* kpm, void* stream) {
+  if (B <= 0 || T <= 0 || !sbk_conv_module_supported(D, K) || !x || !out || x == out) return SBK_ERR_ARG;
+  if (!ln0_w || !ln0_b || !w1p || !b1p || !wc || !ln1_w || !ln1_b || !w2) return SBK_ERR_ARG;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
+                       reinterpret_cast<uintptr_t>(ln0_w) | reinterpret_cast<uintptr_t>(ln0_b) |
+                       reinterpret_cast<uintptr_t>(w1p) | reinterpret_cast<uintptr_t>(b1p) |
+                       reinterpret_cast<uintptr_t>(w2) | reinterpret_cast<uintptr_t>(b2);
+  if (al & 15) return SBK_ERR_ARG;
+  ConvModArgs a;
+  a.x = x; a.out = out; a.B = B; a.T = T; a.K = K; a.padL = causal ? K - 1 : (K - 1) / 2;
+  a.g0 = ln0_w; a.b0 = ln0_b; a.eps0 = eps0;
+  a.w1 = reinterpret_cast<const bf16_t*>(w1p); a.b1 = b1p;
+  a.wc = wc; a.bc = bc;
+  a.g1 = ln1_w; a.b1n = ln1_b; a.eps1 = eps1;
+  a.w2 = reinterpret_cast<const bf16_t*>(w2); a.b2 = b2;
+  a.kpm = reinterpret_cast<const uint8_t*>(kpm);
+  const long long grid = (long long)B * ((T + CM_BM - 1) / CM_BM);
+  if (grid > 0x7fffffffLL) return SBK_ERR_ARG;
+  constexpr size_t lds = conv_module_lds();
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_module_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(conv_module_kernel, dim3((unsigned)grid), dim3(CM_NT), lds, (hipStream_t)stream, a);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}

@@ -38,6 +38,10 @@ __all__ = ["ConvolutionModule", "ConformerEncoderLayer", "ConformerEncoder"]
 _f32 = torch.float32
 _bf16 = torch.bfloat16
 
+# Fused convolution-module kernel on the bf16 path (sbk_conv_module); the
+# four-launch chain (LN, GLU GEMM, dwconv+LN+Swish, projection) otherwise.
+USE_CONV_MODULE_KERNEL = True
+
 
 def _check_swish(act_module):
     if not (isinstance(act_module, Swish) or type(act_module).__name__ == "Swish"):
@@ -113,6 +117,24 @@ class ConvolutionModule(nn.Module):
         return _enc.gemm(v, w2, bias=lin.bias.detach() if lin.bias is not None else None, rowmask=pad_mask_u8,
                          res=residual, out_dtype=_f32)
 
+    def fusable(self, dtype, d):
+        """True when the whole module can run as one kernel (sbk_conv_module)."""
+        return (dtype == _bf16 and _enc.conv_module_supported(d, self.conv.weight.shape[-1])
+                and self.bottleneck[0].bias is not None and isinstance(self.after_conv[1], Swish)
+                and getattr(self.after_conv[1], "beta", 1) == 1)
+
+    def run_fused(self, x2d, B, T, pad_mask_u8=None):
+        """x2d + mask(ConvolutionModule(x2d)) in one launch (bf16 MFMA)."""
+        w1p, b1p, w2 = self.kernel_weights(_bf16)
+        ln = self.after_conv[0]
+        lin = self.after_conv[2]
+        wc = self._wc.get("taps", [self.conv.weight], lambda: self.conv.weight.detach().reshape(
+            self.conv.weight.shape[0], -1).t().contiguous())  # (K, d): coalesced tap loads
+        return _enc.conv_module(x2d, B, T, self.ln_params(), w1p, b1p, wc,
+                                self.conv.bias.detach() if self.conv.bias is not None else None, self.causal,
+                                (ln.weight.detach(), ln.bias.detach(), ln.eps), w2,
+                                lin.bias.detach() if lin.bias is not None else None, pad_mask_u8)
+
     def train_run(self, x2d, B, T, dtype, pad_mask_u8=None, residual=None):
         """Differentiable chain (training path, _autograd): residual +
         mask(ConvolutionModule(x2d)), each op a HIP kernel with its backward."""
@@ -180,10 +202,17 @@ class ConformerEncoderLayer(nn.Module):
             # FFN1 + norm1 in one kernel, FFN2 + norm2 in one kernel (LayerNorms
             # computed on chip; the next layer's FFN1 normalises its own input)
             x, u = f1[1].run_fused(x, self._ln(f1[0]), 0.5, next_ln=self._ln(self.norm1.norm), next_dtype=dtype)
-            # attention output projection + residual + the conv module's LayerNorm in one launch
-            x, attn, uc = self.mha_layer.attend(u, B, T, pos, kpm_u8, dtype, need_attn, residual=x,
-                                                post_ln=self.convolution_module.ln_params(), pk=pk)
-            x = self.convolution_module.run(x, B, T, dtype, kpm_u8, residual=x, u=uc)
+            cm = self.convolution_module
+            if USE_CONV_MODULE_KERNEL and cm.fusable(dtype, x.shape[1]):
+                # attention (+ output projection + residual), then the whole
+                # convolution module (its LayerNorms included) in one launch
+                x, attn = self.mha_layer.attend(u, B, T, pos, kpm_u8, dtype, need_attn, residual=x, pk=pk)
+                x = cm.run_fused(x, B, T, kpm_u8)
+            else:
+                # attention output projection + residual + the conv module's LayerNorm in one launch
+                x, attn, uc = self.mha_layer.attend(u, B, T, pos, kpm_u8, dtype, need_attn, residual=x,
+                                                    post_ln=cm.ln_params(), pk=pk)
+                x = cm.run(x, B, T, dtype, kpm_u8, residual=x, u=uc)
             x, y = f2[1].run_fused(x, self._ln(f2[0]), 0.5, post_ln=self._ln(self.norm2.norm), out=x,
                                    next_ln=final_ln, next_dtype=_f32)
             return (y, None, attn, True) if final_ln is not None else (x, None, attn, False)

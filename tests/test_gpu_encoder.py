@@ -320,3 +320,37 @@ def test_length_mask_vs_reference_formula(dev):
         ref = (torch.arange(T)[None, :].to(torch.float32) > torch.floor(rel * T)[:, None]).to(torch.uint8)
         out = _enc.length_mask(rel.to(dev), T).cpu()
         assert torch.equal(out, ref), T
+
+
+@pytest.mark.parametrize("B,T,K,causal,masked", [(32, 376, 31, False, True), (3, 37, 31, False, True),
+                                                 (2, 50, 7, True, False), (4, 97, 15, False, True),
+                                                 (1, 5, 31, False, False)])
+def test_fused_conv_module_vs_chain(dev, B, T, K, causal, masked):
+    """sbk_conv_module (LN -> GLU GEMM -> dwconv -> LN -> Swish -> GEMM -> mask ->
+    residual in one launch, halo frames recomputed per 48-frame block) vs the
+    four-launch chain at the same bf16 rounding points: within 2e-2 of
+    LayerNorm-scale values (fp32 summation order can flip single bf16
+    roundings of the intermediates); and vs the fp32 oracle within 0.1."""
+    from speechbrain_amd.lobes.models.transformer.Conformer import ConvolutionModule
+    from speechbrain_amd import _enc
+    torch.manual_seed(K + T)
+    cm = ConvolutionModule(256, K, causal=causal).to(dev).eval()
+    with torch.no_grad():
+        for p in cm.parameters():
+            p.add_(0.05 * torch.randn_like(p))
+    x = (torch.randn(B * T, 256) * 2 + 0.3).to(dev)
+    kpm = None
+    if masked:
+        lens = torch.randint(1, T + 1, (B,))
+        lens[0] = T
+        kpm = (torch.arange(T)[None] >= lens[:, None]).to(torch.uint8).reshape(-1).to(dev)
+    assert cm.fusable(torch.bfloat16, 256)
+    with torch.no_grad():
+        y = cm.run_fused(x, B, T, kpm)
+        ref = cm.run(x, B, T, torch.bfloat16, kpm, residual=x)
+    assert_close(y, ref, rtol=2e-2, name="fused vs chain")
+    sd = {k: v.cpu() for k, v in cm.state_dict().items()}
+    pm = kpm.cpu().bool().view(B, T, 1) if kpm is not None else None
+    r32 = x.cpu().view(B, T, 256) + OC.conv_module(x.cpu().view(B, T, 256), sd, "", K, causal, pm)
+    err = (y.cpu().view(B, T, 256) - r32).abs().max().item()
+    assert err < 0.1, err
