@@ -5,7 +5,8 @@
     torchrun --nproc-per-node N bench_train.py ...
 
 One step = Brain.fit_batch on one synthetic batch per GPU (B=32 x 15 s,
-already in HBM): Fbank → SpecAugment (recipe params) → ConvolutionFrontEnd →
+already in HBM): Fbank → InputNormalization (global) → SpecAugment (recipe
+params) → ConvolutionFrontEnd →
 12-layer Conformer (d=256) → Linear(256→1024) TN; prediction net one-hot
 Embedding → GRU(1024) → Linear(1024→1024, no bias) PN; "sum" joint +
 LeakyReLU (sbk_joint_fwd) → Linear(1024→1000, no bias) logits (fp32) →
@@ -57,7 +58,9 @@ def build_modules(d_model=256, layers=12, dropout=0.1):
         "Tjoint": Transducer_joint(joint="sum", nonlinearity=torch.nn.LeakyReLU),
         "transducer_lin": Linear(input_size=J, n_neurons=V, bias=False),
     }
+    from speechbrain_amd.processing.features import InputNormalization
     hp = {"compute_features": Fbank(sample_rate=SR, n_fft=400, n_mels=80),
+          "normalize": InputNormalization(norm_type="global", update_until_epoch=4),
           # conformer_small.yaml:252-262
           "augmentation": SpecAugment(time_warp=True, time_warp_window=5, time_warp_mode="bicubic", freq_mask=True,
                                       freq_mask_width=(0, 30), n_freq_mask=2, time_mask=True,
@@ -78,6 +81,7 @@ def brain_class():
             wavs, wav_lens, tokens_bos, _, _ = batch
             with torch.no_grad():
                 feats = self.hparams["compute_features"](wavs)
+                feats = self.hparams["normalize"](feats, wav_lens, epoch=0)
                 if stage == Stage.TRAIN:
                     feats = self.hparams["augmentation"](feats)
             src = self.modules.CNN(feats)
@@ -174,7 +178,7 @@ def main():
             "value": round(value, 1), "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "fp32" if args.fp32 else "bf16", "data": "synthetic",
-            "config": {"workload": f"C4: Fbank→SpecAugment→CNN→Conformer {args.layers}L d=256 → TN/PN → sum joint "
+            "config": {"workload": f"C4: Fbank→InputNorm→SpecAugment→CNN→Conformer {args.layers}L d=256 → TN/PN → sum joint "
                                    f"LeakyReLU → Linear(1024→1000) → RNN-T; Adam; clip 5.0",
                        "global_batch": world * args.batch, "seq_len": T_e, "U_max": 64, "vocab": V,
                        "parallelism": f"ddp{world}"},

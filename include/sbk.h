@@ -224,6 +224,21 @@ int sbk_conv_module(const float* x, float* out, int B, int T, int D, const float
                     const float* ln1_w, const float* ln1_b, float eps1, const void* w2, const float* b2,
                     const unsigned char* kpm, void* stream);
 
+/* InputNormalization (processing/features.py:940-1231), csrc/norm.hip.  x (B, T, F) fp32,
+ * len (B) relative lengths (frames = rintf(len * T), clamped to [0, T]), F <= 256.
+ *   partials: part = sbk_inorm_slices(T) Welford slices per (b, f), 3 doubles each;
+ *   stats:    per-utterance mean / unbiased std (>= eps; NaN for <= 1 frame) into mean, std (B, F)
+ *             (either may be null); with cur_mean / cur_std (F) also their batch means, and
+ *             upd 1: glob = cur, 2: glob = keep * glob + wgt * cur (in place);
+ *   apply:    y = (x - mean) / std, per utterance (B, F) or shared (F); y may alias x. */
+int sbk_inorm_slices(int T);
+int sbk_inorm_partials(const float* x, const float* len, int B, int T, int F, double* part, void* stream);
+int sbk_inorm_stats(const double* part, int B, int T, int F, int mean_norm, int std_norm, float eps, float* mean,
+                    float* std, float* cur_mean, float* cur_std, int upd, float keep, float wgt, float* glob_mean,
+                    float* glob_std, void* stream);
+int sbk_inorm_apply(const float* x, int B, int T, int F, const float* mean, const float* std, int per_utt, float* y,
+                    void* stream);
+
 /* ------------------------------------------------------------ training path
  * Backward of the Conformer-Transducer encoder (csrc/backward.hip).  The
  * dense contractions of the backward (dX = dY W, dW = dY^T X, attention's

@@ -249,3 +249,66 @@ def mfcc(wav, deltas_on=True, context=True, sample_rate=16000, f_min=0,
     if context:
         m = context_window(m, left_frames, right_frames)
     return m
+
+
+class InputNormalization:
+    """CPU restatement of speechbrain/processing/features.py:940-1231
+    (InputNormalization): per-utterance mean / unbiased std over the first
+    round(len * T) frames (:1017-1024, :1120-1145), then sentence / batch /
+    global / speaker normalisation with the reference's moving averages
+    (:1026-1117).  Stateful like the reference (count, glob_*, spk_dict_*)."""
+
+    def __init__(self, mean_norm=True, std_norm=True, norm_type="global", avg_factor=None, update_until_epoch=3):
+        self.mean_norm, self.std_norm, self.norm_type = mean_norm, std_norm, norm_type
+        self.avg_factor, self.update_until_epoch = avg_factor, update_until_epoch
+        self.glob_mean = torch.tensor([0])
+        self.glob_std = torch.tensor([0])
+        self.spk_mean, self.spk_std, self.spk_count = {}, {}, {}
+        self.count = 0
+        self.eps = 1e-10
+        self.training = True
+
+    def _stats(self, x):
+        mean = torch.mean(x, dim=0) if self.mean_norm else torch.tensor([0.0])
+        std = torch.std(x, dim=0) if self.std_norm else torch.tensor([1.0])
+        return mean, torch.max(std, self.eps * torch.ones_like(std))
+
+    def __call__(self, x, lengths, spk_ids=torch.tensor([]), epoch=0):
+        means, stds = [], []
+        for b in range(x.shape[0]):
+            n = int(torch.round(lengths[b] * x.shape[1]).int())
+            m, s = self._stats(x[b, 0:n, ...])
+            means.append(m)
+            stds.append(s)
+            if self.norm_type == "sentence":
+                x[b] = (x[b] - m) / s
+            if self.norm_type == "speaker":
+                k = int(spk_ids[b][0])
+                if self.training:
+                    if k not in self.spk_mean:
+                        self.spk_mean[k], self.spk_std[k], self.spk_count[k] = m, s, 1
+                    else:
+                        self.spk_count[k] += 1
+                        w = 1 / self.spk_count[k] if self.avg_factor is None else self.avg_factor
+                        self.spk_mean[k] = (1 - w) * self.spk_mean[k] + w * m
+                        self.spk_std[k] = (1 - w) * self.spk_std[k] + w * s
+                    sm, ss = self.spk_mean[k], self.spk_std[k]
+                else:
+                    sm, ss = (self.spk_mean[k], self.spk_std[k]) if k in self.spk_mean else (m, s)
+                x[b] = (x[b] - sm) / ss
+        if self.norm_type in ("batch", "global"):
+            cm = torch.mean(torch.stack(means), dim=0)
+            cs = torch.mean(torch.stack(stds), dim=0)
+            if self.norm_type == "batch":
+                x = (x - cm) / cs
+            else:
+                if self.training:
+                    if self.count == 0:
+                        self.glob_mean, self.glob_std = cm, cs
+                    elif epoch < self.update_until_epoch:
+                        w = 1 / (self.count + 1) if self.avg_factor is None else self.avg_factor
+                        self.glob_mean = (1 - w) * self.glob_mean + w * cm
+                        self.glob_std = (1 - w) * self.glob_std + w * cs
+                    self.count += 1
+                x = (x - self.glob_mean) / self.glob_std
+        return x

@@ -65,6 +65,11 @@ SIGNATURES = {
     "sbk_relpos_attention": [_i, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _vp],
     "sbk_relpos_attention_lds": [_i, _i, _i],
     "sbk_relpos_attention_ld": [_i, _vp, _vp, _i, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _vp],
+    # norm.hip
+    "sbk_inorm_slices": [_i],
+    "sbk_inorm_partials": [_vp, _vp, _i, _i, _i, _vp, _vp],
+    "sbk_inorm_stats": [_vp, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp, _i, _f, _f, _vp, _vp, _vp],
+    "sbk_inorm_apply": [_vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp],
     # convmod.hip
     "sbk_conv_module_supported": [_i, _i],
     "sbk_conv_module": [_vp, _vp, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _f, _vp, _vp, _vp,

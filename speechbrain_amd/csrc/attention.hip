@@ -31,6 +31,9 @@ using namespace sbk;
 
 namespace {
 
+#ifndef SBK_ATT_MINW
+#define SBK_ATT_MINW 2  // waves per SIMD the register budget must allow
+#endif
 constexpr int QB = 64;        // queries per workgroup
 constexpr int KC = 64;        // keys per chunk
 constexpr int PBR = KC + QB;  // positional band rows staged per chunk (127 used)
@@ -101,7 +104,7 @@ __device__ unsigned long long g_att_tl[4][64];
 #endif
 
 template <typename T, int DHP, bool PROBS>
-__global__ void __launch_bounds__(256) relpos_flash_kernel(const T* __restrict__ qkv, const T* __restrict__ pk,
+__global__ void __launch_bounds__(256, SBK_ATT_MINW) relpos_flash_kernel(const T* __restrict__ qkv, const T* __restrict__ pk,
                                                            const float* __restrict__ pbu,
                                                            const float* __restrict__ pbv,
                                                            const uint8_t* __restrict__ kpm, int B, int Tn, int H,

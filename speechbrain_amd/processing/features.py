@@ -11,10 +11,11 @@ import math
 import torch
 
 from .. import ops
+from .._lib import check as _check, lib as _lib, ptr as _ptr, require_device as _require_device, stream_of as _stream_of
 
 logger = logging.getLogger(__name__)
 
-__all__ = ["STFT", "spectral_magnitude", "Filterbank", "DCT", "Deltas", "ContextWindow"]
+__all__ = ["STFT", "spectral_magnitude", "Filterbank", "DCT", "Deltas", "ContextWindow", "InputNormalization"]
 
 
 class _DevCache:
@@ -296,3 +297,152 @@ class ContextWindow(torch.nn.Module):
             y = y.transpose(1, 2).reshape(B, Fd * self.context_len, Tn, C)
             return y.transpose(1, 2)
         return ops.context_window(x, self.left_frames, self.right_frames)
+
+
+class InputNormalization(torch.nn.Module):
+    """Mean / variance normalisation (features.py:940-1231) on HIP
+    (csrc/norm.hip): the per-utterance statistics of the whole batch in two
+    launches (fp64 Welford slices, then the merge — no per-utterance host
+    loop and no host sync), the normalisation in a third.  norm_type
+    "sentence" | "batch" | "global" | "speaker" with the reference's moving
+    averages; sentence and speaker modes write into x and return it, batch and
+    global return a new tensor, as the reference does.  The statistics state
+    (count, glob_mean, glob_std, spk_dict_*) round-trips through
+    _statistics_dict / _load_statistics_dict / _save / _load."""
+
+    def __init__(self, mean_norm=True, std_norm=True, norm_type="global", avg_factor=None, requires_grad=False,
+                 update_until_epoch=3):
+        super().__init__()
+        self.mean_norm = mean_norm
+        self.std_norm = std_norm
+        self.norm_type = norm_type
+        self.avg_factor = avg_factor
+        self.requires_grad = requires_grad
+        self.glob_mean = torch.tensor([0])
+        self.glob_std = torch.tensor([0])
+        self.spk_dict_mean = {}
+        self.spk_dict_std = {}
+        self.spk_dict_count = {}
+        self.weight = 1.0
+        self.count = 0
+        self.eps = 1e-10
+        self.update_until_epoch = update_until_epoch
+
+    def _batch_stats(self, x, lengths, glob_update=None):
+        """Per-utterance (B, F) mean / std, and for batch / global also the
+        batch means (F,) with the global moving average applied in place."""
+        _require_device(x)
+        B, T = x.shape[0], x.shape[1]
+        F = x[0, 0].numel()
+        lib = _lib()
+        lens = lengths.to(device=x.device, dtype=torch.float32).contiguous()
+        part = torch.empty(B * int(lib.sbk_inorm_slices(T)) * F * 3, device=x.device, dtype=torch.float64)
+        s = _stream_of(x)
+        _check(lib.sbk_inorm_partials(_ptr(x), _ptr(lens), B, T, F, _ptr(part), s), "sbk_inorm_partials")
+        mean = torch.empty(B, F, device=x.device, dtype=torch.float32)
+        std = torch.empty(B, F, device=x.device, dtype=torch.float32)
+        cur = None
+        upd, keep, w, gm, gs = 0, 0.0, 0.0, None, None
+        if self.norm_type in ("batch", "global"):
+            cur = (torch.empty(F, device=x.device, dtype=torch.float32),
+                   torch.empty(F, device=x.device, dtype=torch.float32))
+            if glob_update is not None:
+                upd, w = glob_update
+                keep = 1.0 - w
+                if upd == 1:
+                    gm = torch.empty(F, device=x.device, dtype=torch.float32)
+                    gs = torch.empty(F, device=x.device, dtype=torch.float32)
+                else:  # blended in place; a (1,) state (mean_norm / std_norm off) is widened first
+                    gm = self.glob_mean.to(device=x.device, dtype=torch.float32).expand(F).contiguous()
+                    gs = self.glob_std.to(device=x.device, dtype=torch.float32).expand(F).contiguous()
+        _check(lib.sbk_inorm_stats(_ptr(part), B, T, F, int(self.mean_norm), int(self.std_norm),
+                                      float(self.eps), _ptr(mean), _ptr(std),
+                                      _ptr(cur[0] if cur else None), _ptr(cur[1] if cur else None), upd,
+                                      float(keep), float(w), _ptr(gm), _ptr(gs), s), "sbk_inorm_stats")
+        if upd:
+            # the reference's statistics are (1,) tensors when that normalisation is off
+            self.glob_mean = gm if self.mean_norm else gm[:1].clone()
+            self.glob_std = gs if self.std_norm else gs[:1].clone()
+        return mean, std, cur
+
+    def _normalize(self, x, mean, std, per_utt, out):
+        B, T = x.shape[0], x.shape[1]
+        F = x[0, 0].numel()
+        _check(_lib().sbk_inorm_apply(_ptr(x), B, T, F, _ptr(mean), _ptr(std), int(per_utt),
+                                            _ptr(out), _stream_of(x)), "sbk_inorm_apply")
+        return out
+
+    def forward(self, x, lengths, spk_ids=torch.tensor([]), epoch=0):
+        if x.dtype != torch.float32 or not x.is_contiguous():
+            raise TypeError("InputNormalization kernels take contiguous fp32 features")
+        glob_update = None
+        if self.norm_type == "global" and self.training:
+            if self.count == 0:
+                glob_update = (1, 1.0)
+            elif epoch < self.update_until_epoch:
+                self.weight = 1 / (self.count + 1) if self.avg_factor is None else self.avg_factor
+                glob_update = (2, float(self.weight))
+        mean, std, cur = self._batch_stats(x, lengths, glob_update)
+        if self.norm_type == "sentence":
+            return self._normalize(x, mean, std, True, x)
+        if self.norm_type == "speaker":
+            sm, ss = [], []
+            for b in range(x.shape[0]):
+                k = int(spk_ids[b][0])
+                m, s = mean[b], std[b]
+                if self.training:
+                    if k not in self.spk_dict_mean:
+                        self.spk_dict_mean[k], self.spk_dict_std[k], self.spk_dict_count[k] = m, s, 1
+                    else:
+                        self.spk_dict_count[k] += 1
+                        self.weight = 1 / self.spk_dict_count[k] if self.avg_factor is None else self.avg_factor
+                        self.spk_dict_mean[k] = (1 - self.weight) * self.spk_dict_mean[k] + self.weight * m
+                        self.spk_dict_std[k] = (1 - self.weight) * self.spk_dict_std[k] + self.weight * s
+                    sm.append(self.spk_dict_mean[k])
+                    ss.append(self.spk_dict_std[k])
+                else:
+                    sm.append(self.spk_dict_mean.get(k, m))
+                    ss.append(self.spk_dict_std.get(k, s))
+            return self._normalize(x, torch.stack(sm).contiguous(), torch.stack(ss).contiguous(), True, x)
+        if self.norm_type == "batch":
+            return self._normalize(x, cur[0], cur[1], False, torch.empty_like(x))
+        if self.norm_type == "global":
+            if self.training:
+                self.count = self.count + 1
+            gm = self.glob_mean.to(device=x.device, dtype=torch.float32).expand(mean.shape[1]).contiguous()
+            gs = self.glob_std.to(device=x.device, dtype=torch.float32).expand(mean.shape[1]).contiguous()
+            return self._normalize(x, gm, gs, False, torch.empty_like(x))
+        return x
+
+    # statistics state (features.py:1147-1231)
+    def _statistics_dict(self):
+        return {"count": self.count, "glob_mean": self.glob_mean, "glob_std": self.glob_std,
+                "spk_dict_mean": self.spk_dict_mean, "spk_dict_std": self.spk_dict_std,
+                "spk_dict_count": self.spk_dict_count}
+
+    def _load_statistics_dict(self, state):
+        self.count = state["count"]
+        self.glob_mean = state["glob_mean"]
+        self.glob_std = state["glob_std"]
+        self.spk_dict_mean = dict(state["spk_dict_mean"])
+        self.spk_dict_std = dict(state["spk_dict_std"])
+        self.spk_dict_count = dict(state["spk_dict_count"])
+        return state
+
+    def to(self, device):
+        self = super().to(device)
+        if isinstance(self.glob_mean, torch.Tensor):
+            self.glob_mean = self.glob_mean.to(device)
+            self.glob_std = self.glob_std.to(device)
+        for k in self.spk_dict_mean:
+            self.spk_dict_mean[k] = self.spk_dict_mean[k].to(device)
+            self.spk_dict_std[k] = self.spk_dict_std[k].to(device)
+        return self
+
+    def _save(self, path):
+        torch.save(self._statistics_dict(), path)
+
+    def _load(self, path, end_of_epoch=False, device=None):
+        del end_of_epoch
+        self._load_statistics_dict(torch.load(path, map_location=device, weights_only=True))
+

@@ -25,6 +25,10 @@ Fixture inventory (all float32 unless noted):
                    RelPosEncXL and rel_shift vectors
                    (lobes/models/convolution.py, lobes/models/transformer/*,
                    nnet/attention.py)
+  inputnorm.npz    InputNormalization (global / batch / sentence / speaker,
+                   training and eval, running statistics over 4 batches and
+                   3 epochs, ragged relative lengths incl. one-frame and
+                   rounding-tie lengths) (processing/features.py:940-1231)
   train.npz        gradients of sum(R * encode(cnn(feats), wav_len)) w.r.t.
                    every ConvolutionFrontEnd / TransformerASR parameter and
                    the input features (reference autograd, weights of
@@ -269,6 +273,42 @@ def gen_conformer():
     np.savez_compressed(os.path.join(OUT, "conformer.npz"), **out)
 
 
+def gen_inputnorm():
+    out = {}
+    g = torch.Generator().manual_seed(11)
+    B, T, Fd = 4, 37, 40
+    batches = [3.0 * torch.randn(B, T, Fd, generator=g) + 1.5 for _ in range(4)]
+    lens = [torch.tensor([1.0, 0.5, 0.8, 0.3]), torch.tensor([1.0, 1.0, 0.9, 0.05]),
+            torch.tensor([0.7, 1.0, 0.6, 0.25]), torch.tensor([1.0, 0.2, 1.0, 0.99])]
+    spk = [torch.tensor([[0], [1], [0], [2]]), torch.tensor([[1], [1], [3], [0]]),
+           torch.tensor([[2], [0], [1], [1]]), torch.tensor([[3], [3], [0], [2]])]
+    for i in range(4):
+        out[f"x{i}"] = t2n(batches[i])
+        out[f"len{i}"] = t2n(lens[i])
+        out[f"spk{i}"] = spk[i].numpy()
+    cases = {"global": dict(norm_type="global"), "global_avg": dict(norm_type="global", avg_factor=0.1),
+             "batch": dict(norm_type="batch"), "sentence": dict(norm_type="sentence"),
+             "speaker": dict(norm_type="speaker"), "global_nostd": dict(norm_type="global", std_norm=False),
+             "global_until1": dict(norm_type="global", update_until_epoch=1)}
+    for name, kw in cases.items():
+        m = F.InputNormalization(**kw)
+        m.train()
+        step = 0
+        for epoch in range(3):
+            for i in range(4):
+                y = m(batches[i].clone(), lens[i], spk_ids=spk[i], epoch=epoch)
+                if epoch != 1:
+                    out[f"{name}_train_e{epoch}_b{i}"] = t2n(y)
+                step += 1
+        if kw["norm_type"] == "global":
+            out[f"{name}_glob_mean"] = t2n(m.glob_mean)
+            out[f"{name}_glob_std"] = t2n(m.glob_std)
+            out[f"{name}_count"] = np.array(m.count)
+        m.eval()
+        out[f"{name}_eval_b0"] = t2n(m(batches[0].clone(), lens[0], spk_ids=spk[0], epoch=5))
+    np.savez_compressed(os.path.join(OUT, "inputnorm.npz"), **out)
+
+
 def gen_train():
     """Reference autograd through ConvolutionFrontEnd + TransformerASR.encode
     (dropout 0, so train and eval arithmetic agree), weights from conformer.npz."""
@@ -304,11 +344,15 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["train"]:
         gen_train()
         sys.exit(0)
+    if sys.argv[1:] == ["inputnorm"]:
+        gen_inputnorm()
+        sys.exit(0)
     gen_fbank_wavs()
     gen_features()
     gen_specaug()
     gen_conformer()
     gen_train()
+    gen_inputnorm()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

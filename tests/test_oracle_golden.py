@@ -171,6 +171,32 @@ def test_conformer_encoder_direct(golden):
     assert_close(OC.rel_shift(torch.from_numpy(g["relshift_in"])), g["relshift_out"], rtol=0)
 
 
+INORM_CASES = {"global": dict(norm_type="global"), "global_avg": dict(norm_type="global", avg_factor=0.1),
+               "batch": dict(norm_type="batch"), "sentence": dict(norm_type="sentence"),
+               "speaker": dict(norm_type="speaker"), "global_nostd": dict(norm_type="global", std_norm=False),
+               "global_until1": dict(norm_type="global", update_until_epoch=1)}
+
+
+@pytest.mark.parametrize("name", list(INORM_CASES))
+def test_input_normalization_oracle(golden, name):
+    """oracle.features.InputNormalization vs the reference run (inputnorm.npz):
+    12 training batches over 3 epochs (running statistics) then eval."""
+    g = golden("inputnorm")
+    m = OF.InputNormalization(**INORM_CASES[name])
+    for epoch in range(3):
+        for i in range(4):
+            y = m(torch.from_numpy(g[f"x{i}"]).clone(), torch.from_numpy(g[f"len{i}"]),
+                  spk_ids=torch.from_numpy(g[f"spk{i}"]), epoch=epoch)
+            if epoch != 1:
+                assert_close(y, g[f"{name}_train_e{epoch}_b{i}"], rtol=1e-5, name=f"e{epoch} b{i}")
+    if name.startswith("global"):
+        assert m.count == int(g[f"{name}_count"])
+        assert_close(m.glob_mean, g[f"{name}_glob_mean"], rtol=1e-6)
+    m.training = False
+    y = m(torch.from_numpy(g["x0"]).clone(), torch.from_numpy(g["len0"]), spk_ids=torch.from_numpy(g["spk0"]), epoch=5)
+    assert_close(y, g[f"{name}_eval_b0"], rtol=1e-5, name="eval")
+
+
 def test_conformer_grads_vs_reference(golden):
     """Oracle autograd (CPU restatement) vs the reference's own gradients
     (train.npz): pins the checker used by tests/test_gpu_train.py."""
