@@ -256,10 +256,12 @@ def main():
             for p in probes:
                 p.__exit__()
         kern = {}
-        for p, label in zip(probes, ("ffn_kernel<256> (fused macaron FFN)", "gemm_kernel<bf16> (projections, all tiles)")):
+        labels = (("ffn_kernel<256, 1> (fused macaron FFN)", "ffn_kernel<256, 1>"),
+                  ("gemm_kernel<bf16> (projections, all tiles)", "gemm_kernel<unsigned short, 64, 64, 64, 2>"))
+        for p, (label, pmc_key) in zip(probes, labels):
             ms, n, fl = p.result()
             if n:
-                kern[p.name] = {"kernel": label, "launches_per_step": n // max(1, args.steps),
+                kern[p.name] = {"kernel": label, "pmc_key": pmc_key, "launches_per_step": n // max(1, args.steps),
                                 "avg_launch_us": round(1000.0 * ms / n, 3),
                                 "achieved": round(fl / (ms * 1e-3) / 1e12, 2),
                                 "step_share_ms": round(ms / args.steps, 4)}
@@ -285,7 +287,7 @@ def main():
             "roofline": None if dom is None else {
                 "bound": "mfma", "kernel": dom["kernel"], "achieved": dom["achieved"], "peak": PEAK_BF16_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(dom["achieved"] / PEAK_BF16_TFLOPS, 4),
-                "traffic": traffic.get(dom["kernel"].split(" ")[0]),
+                "traffic": traffic.get(dom["pmc_key"]),
                 "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch)",
                 "launches_per_step": dom["launches_per_step"], "avg_launch_us": dom["avg_launch_us"],
                 "step_algorithmic_tflop": round(total_flops / 1e12, 4),
