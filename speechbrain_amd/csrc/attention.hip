@@ -72,6 +72,17 @@ struct FlashLds {
 
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 
+// Out-of-range K / V / positional rows are zeroed at commit.  (Tried:
+// committing the clamped loads unmasked — the rows only meet masked scores —
+// measured 36 -> 54 us: the compiler then sank the prefetch loads to their
+// stores; and head dims >= dh must stay zero when dh is not a multiple of the
+// 8-dim Q fragment, whose vector loads then read the next section.)
+#ifdef SBK_ATT_NO_ZERO_OOR
+#define STAGE_SEL(ok, v) (v)
+#else
+#define STAGE_SEL(ok, v) sel4((ok), (v))
+#endif
+
 // component-wise select (a struct-valued ?: takes the operands' addresses and
 // sends the staging arrays to scratch)
 __device__ __forceinline__ uint4 sel4(bool c, const uint4& a) {
@@ -247,9 +258,9 @@ __global__ void __launch_bounds__(256, SBK_ATT_MINW) relpos_flash_kernel(const T
 #pragma unroll
     for (int i = 0; i < NKC; ++i) {
       const int c = tid + 256 * i, r = c / CPR, d = (c % CPR) * VEC;
-      *reinterpret_cast<uint4*>(Ks + r * KR + d) = sel4(okk[i], rk[i]);
+      *reinterpret_cast<uint4*>(Ks + r * KR + d) = STAGE_SEL(okk[i], rk[i]);
       if (need_v) {
-        const uint4 vv = sel4(okk[i], rv[i]);
+        const uint4 vv = STAGE_SEL(okk[i], rv[i]);
         if (TRV) {
           *reinterpret_cast<uint4*>(Vs + r * KR + d) = vv;
         } else {
@@ -262,7 +273,7 @@ __global__ void __launch_bounds__(256, SBK_ATT_MINW) relpos_flash_kernel(const T
 #pragma unroll
     for (int i = 0; i < NPC; ++i) {
       const int c = tid + 256 * i, rr = c / CPR, d = (c % CPR) * VEC;
-      *reinterpret_cast<uint4*>(Ps + rr * KR + d) = sel4(okp[i], rp[i]);
+      *reinterpret_cast<uint4*>(Ps + rr * KR + d) = STAGE_SEL(okp[i], rp[i]);
     }
     if (tid < KC) {  // wave 0 (KC == 64): mask values and the chunk's any-masked flag
       Ms[tid] = rm;
