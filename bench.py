@@ -13,10 +13,11 @@ captured once into a HIP graph and replayed.  Rank 0 prints ONE JSON line.
 
 Also reported (rank 0, N=1 path of the contract):
   roofline      the dominant kernel (the fused FFN; the projection GEMMs are
-                listed beside it) timed with HIP events around each of its
-                launches during an eager pass of K steps on the launch
-                stream; achieved = algorithmic FLOPs / time; traffic = HBM
-                bytes per launch from the committed rocprofv3 PMC pass.
+                listed beside it): its launches of one step re-issued back to
+                back from a HIP graph on the launch stream and timed with HIP
+                events (average launch duration, as rocprofv3 reports it);
+                achieved = algorithmic FLOPs / time; traffic = HBM bytes per
+                launch from the committed rocprofv3 PMC passes.
   cpu_baseline  the from-scratch CPU restatement (oracle/, PyTorch CPU fp32)
                 of the same path on a bounded sample, host threads stated.
 """
@@ -104,10 +105,14 @@ def cpu_baseline(d_model, n_utt=16, reps=4):
 
 
 class _LaunchProbe:
-    """Wraps one speechbrain_amd._enc entry point so that every bf16 launch is
-    bracketed by HIP events on the launch stream (torch's current stream, the
-    one the ctypes kernels are launched on) and its algorithmic FLOPs are
-    accumulated: `flops_of(*args, **kw)` -> FLOPs of that call."""
+    """Wraps one speechbrain_amd._enc entry point and records every bf16 call
+    of one eager step (arguments kept alive) with its algorithmic FLOPs
+    (`flops_of(*args, **kw)`).  `replay_time()` then captures exactly those
+    calls, back to back, `reps` times into one HIP graph on the launch stream
+    (torch's current stream, the one the ctypes kernels use) and times the
+    replays with HIP events: the average launch duration of the kernel as it
+    runs inside the step's graph, without per-launch event or host gaps — the
+    quantity rocprofv3 --kernel-trace reports for it."""
 
     def __init__(self, name, flops_of, is_bf16):
         from speechbrain_amd import _enc
@@ -116,34 +121,49 @@ class _LaunchProbe:
         self.orig = getattr(_enc, name)
         self.flops_of = flops_of
         self.is_bf16 = is_bf16
-        self.events = []
+        self.calls = []
         self.flops = 0.0
 
     def __enter__(self):
         probe = self
 
         def wrapped(*args, **kw):
-            if not probe.is_bf16(*args, **kw):
-                return probe.orig(*args, **kw)
-            s = torch.cuda.current_stream()
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record(s)
-            out = probe.orig(*args, **kw)
-            e1.record(s)
-            probe.events.append((e0, e1))
-            probe.flops += probe.flops_of(*args, **kw)
-            return out
+            if probe.is_bf16(*args, **kw):
+                probe.calls.append((args, kw))
+                probe.flops += probe.flops_of(*args, **kw)
+            return probe.orig(*args, **kw)
         setattr(self._enc, self.name, wrapped)  # callers resolve _enc.<name> at call time
         return self
 
     def __exit__(self, *exc):
         setattr(self._enc, self.name, self.orig)
 
-    def result(self):
+    def replay_time(self, reps=10, rounds=3):
+        """(ms per step's worth of launches, launches per step, FLOPs per step)."""
+        if not self.calls:
+            return 0.0, 0, 0.0
+
+        def body():
+            for a, k in self.calls:
+                self.orig(*a, **k)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            body()
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(reps):
+                body()
+        g.replay()
         torch.cuda.synchronize()
-        ms = sum(e0.elapsed_time(e1) for e0, e1 in self.events)
-        return ms, len(self.events), self.flops
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(rounds):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / (rounds * reps), len(self.calls), self.flops
 
 
 def _ffn_flops(x, ln0, w1, *a, **k):
@@ -240,18 +260,15 @@ def main():
 
     if rank == 0:
         total_flops = encoder_flops(args.batch, T_e, args.d_model)
-        # per-kernel timing: HIP events around each launch over K eager steps
+        # per-kernel timing: the dominant kernels' launches of one step,
+        # replayed back to back from a HIP graph and timed with HIP events
         bf = lambda t: t.dtype == torch.bfloat16  # noqa: E731
         probes = [_LaunchProbe("ffn", _ffn_flops, lambda x, ln0, w1, *a, **k: bf(w1)),
                   _LaunchProbe("gemm", _gemm_flops, lambda a, w, *r, **k: bf(a))]
         for p in probes:
             p.__enter__()
         try:
-            for _ in range(args.steps):
-                # park the GPU while the host enqueues the step, so the events
-                # time kernels back to back, not host launch gaps
-                torch.cuda._sleep(50_000_000)
-                step()
+            step()
         finally:
             for p in probes:
                 p.__exit__()
@@ -259,12 +276,12 @@ def main():
         labels = (("ffn_kernel<256, 1> (fused macaron FFN)", "ffn_kernel<256, 1>"),
                   ("gemm_kernel<bf16> (projections, all tiles)", "gemm_kernel<unsigned short, 64, 64, 64, 2>"))
         for p, (label, pmc_key) in zip(probes, labels):
-            ms, n, fl = p.result()
+            ms, n, fl = p.replay_time()
             if n:
-                kern[p.name] = {"kernel": label, "pmc_key": pmc_key, "launches_per_step": n // max(1, args.steps),
+                kern[p.name] = {"kernel": label, "pmc_key": pmc_key, "launches_per_step": n,
                                 "avg_launch_us": round(1000.0 * ms / n, 3),
                                 "achieved": round(fl / (ms * 1e-3) / 1e12, 2),
-                                "step_share_ms": round(ms / args.steps, 4)}
+                                "step_share_ms": round(ms, 4)}
         dom = max(kern.values(), key=lambda k: k["step_share_ms"]) if kern else None
         traffic = load_traffic()
         res = {
