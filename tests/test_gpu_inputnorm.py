@@ -71,3 +71,17 @@ def test_input_normalization_state_roundtrip(dev, tmp_path):
     m2._load(p)
     assert m2.count == 1
     assert torch.equal(m2.glob_mean.cpu(), m.glob_mean.cpu())
+
+
+def test_input_normalization_reference_unittest(dev):
+    """tests/unittests/test_features.py:100-119 of the reference: traceable,
+    and exact on [1, 2, 3, 0, 0, 0] with relative length 0.5."""
+    from speechbrain_amd.processing.features import InputNormalization
+    norm = InputNormalization().to(dev)
+    inputs = torch.randn([10, 101, 20], device=dev)
+    inp_len = torch.ones([10], device=dev)
+    assert torch.jit.trace(norm, (inputs, inp_len), check_trace=False)
+    norm = InputNormalization().to(dev)
+    inputs = torch.FloatTensor([1, 2, 3, 0, 0, 0]).to(dev).unsqueeze(0).unsqueeze(2)
+    out_norm = norm(inputs, torch.FloatTensor([0.5]).to(dev)).squeeze()
+    assert torch.equal(out_norm, torch.FloatTensor([-1, 0, 1, -2, -2, -2]).to(dev))
