@@ -71,6 +71,11 @@ def gemm_ln(a, w, ln, bias=None, res=None, alpha=1.0, rowmask=None, out=None, u_
     return out, u
 
 
+# RelPosMHAXL in_proj (a plain bf16 GEMM) on hipBLASLt instead of sbk_gemm:
+# 11.8 vs 15.0 us alone (scripts/kbench.py gemm) but no change in the graph-
+# replayed step (233.8k vs 232.9-234.2k audio-s/s): off.
+QKV_LIBRARY_GEMM = False
+
 # The fused projection + LayerNorm (sbk_gemm_ln) measures the same as the two
 # launches it replaces at M = 12032 (15.1 vs 8.5 + 6.3 us): off by default.
 USE_GEMM_LN = False
