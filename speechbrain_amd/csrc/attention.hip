@@ -328,6 +328,9 @@ __global__ void __launch_bounds__(256, SBK_ATT_MINW) relpos_flash_kernel(const T
       const bool more = ch + 1 < nchunk;
 #ifndef SBK_PROBE_NO_STAGE
       if (vec_ok && more) fetch(j0 + KC, need_v);  // next chunk in flight during this chunk's math
+#ifdef SBK_ATT_PIN_FETCH
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch loads above the chunk math
+#endif
 #endif
 
       // ---- S^T (keys x queries) and G^T (band rows x queries) ----
@@ -503,6 +506,278 @@ __global__ void __launch_bounds__(256, SBK_ATT_MINW) relpos_flash_kernel(const T
   }
 }
 
+// ---------------------------------------------------------------------------
+// The encoder's inference path — bf16, dh = 64, no probabilities — with
+// three workgroups per CU.  The kernel above carries the next chunk's K / V /
+// band rows in 32 VGPRs (194 in all), so it runs two waves per SIMD: at
+// B = 32, T = 376 its 768 workgroups take 1.5 rounds of 512.  Its score
+// assembly was also 16 serialised LDS round trips per chunk (a per-chunk
+// "any key masked" branch split it into read -> wait -> add steps).
+// Here the tiles go global -> LDS by LDS-DMA (global_load_lds_dwordx4: no
+// VGPRs, no ds_write) into unpadded 128-B rows whose 16-B chunks are
+// XOR-swizzled on the global source address — K and the band:
+// chunk ^ ((row >> 1) & 7), conflict-free ds_read_b128 fragments; V:
+// chunk ^ (((row >> 1) & 3) << 1), conflict-free ds_read_b64_tr_b16.  G^T goes
+// to a query-major scratch with the rel_shift applied on the write (row R of
+// query ii lands at position R - (15 - ii); the first / last tile's positions
+// outside the chunk's 64 keys clamp onto two spare slots), so the scores are
+// four aligned 16-B reads, and the key mask is added unconditionally.  Row
+// max / sum: permlane half-swaps.  Two barriers per chunk:
+//   A  this chunk's K / band landed in every wave and every wave is past the
+//      previous chunk's P·V  -> key mask, then issue this chunk's V;
+//   B  V landed and every wave's S / G fragment reads are done -> read the
+//      scratch and the mask, then issue the next chunk's K / band, which land
+//      under the softmax and P·V.
+// The tiles are distinct __shared__ objects and the other LDS accesses come
+// before a DMA is issued, so the compiler's LDS-DMA alias guard (a vmcnt wait
+// before an LDS access it cannot tell apart from a DMA in flight) has little
+// to wait for.  50.3 KB of LDS and <= 168 VGPRs: three workgroups per CU.
+namespace dmak {
+constexpr int RB = 64;   // bf16 per staged row (dh = 64): 128 B
+constexpr int PB = 128;  // band rows staged per chunk (127 used)
+constexpr int G2 = 72;   // G scratch row (floats): 18 16-B slots, ≡ 2 mod 4
+constexpr int GO = 4;    // scratch index of key 0 (spare slots GO - 1 and GO + KC)
+__device__ __forceinline__ int swz_kp(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ int swz_v(int row) { return ((row >> 1) & 3) << 1; }
+// One LDS-DMA piece (64 lanes x 16 B to lds + 16 * lane), issued from inline
+// asm: the compiler then sees no LDS write in flight and puts no alias-guard
+// vmcnt wait before the LDS reads of the other tiles (with the builtin it
+// waited for the next chunk's K / band before the P·V reads).  dma_barrier's
+// vmcnt(0) + s_barrier is what orders the fills and the reads.
+__device__ __forceinline__ void dma16(const bf16_t* src, bf16_t* lds) {
+  const uint32_t la = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)((__attribute__((address_space(3))) bf16_t*)lds));
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(la) : "memory", "m0");
+}
+// this wave's DMA pieces and LDS accesses done, then the workgroup barrier
+__device__ __forceinline__ void dma_barrier() {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+// V^T A-operand fragment (as vt_frag_tr) from the swizzled V tile;
+// swz_v(r + 16) == swz_v(r)
+__device__ __forceinline__ bf16x8 vt_frag_swz(const bf16_t* V, int k0, int dbase, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int r0 = k0 + 4 * g + q, col = dbase + 4 * p;
+  const bf16_t* a0 = V + r0 * RB + ((((col >> 3) ^ swz_v(r0)) << 3) | (col & 7));
+  const bf16_t* a1 = a0 + 16 * RB;
+  const bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4_t*)(a0));
+  const bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4_t*)(a1));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+}  // namespace dmak
+
+__global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* __restrict__ qkv,
+                                                                  const bf16_t* __restrict__ pk, int ldp,
+                                                                  const float* __restrict__ pbu,
+                                                                  const float* __restrict__ pbv,
+                                                                  const uint8_t* __restrict__ kpm, int Tn, int H,
+                                                                  float scale, bf16_t* __restrict__ out) {
+  using namespace dmak;
+  constexpr int dh = 64;
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[KC * RB];
+  __shared__ __attribute__((aligned(16))) bf16_t Ps[PB * RB];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[KC * RB];
+  __shared__ __attribute__((aligned(16))) float Gs[4 * 16 * G2];
+  __shared__ __attribute__((aligned(16))) float Ms[KC];
+
+  const int d_model = H * dh;
+  const long long row3 = 3LL * d_model;
+  const int nqb = (Tn + QB - 1) / QB;
+  const int nwg = gridDim.x, orig = blockIdx.x;  // XCD-aware bijective remap, as above
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int qb = tile % nqb, bh = tile / nqb;
+  const int h = bh % H, b = bh / H;
+  const int i0 = qb * QB;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c16 = lane & 15, g = lane >> 4;
+  const int my_i = i0 + 16 * w + c16;
+  const bf16_t* qkv_b = qkv + (long long)b * Tn * row3 + h * 3 * dh;
+  const bf16_t* pk_h = pk + h * dh;
+  float* gq = Gs + w * 16 * G2 + c16 * G2 + GO;  // this lane's query row of the G scratch, at key 0
+  const int lrow = lane >> 3, lchk = lane & 7;   // DMA piece: 8 rows x 8 16-B chunks
+
+  auto dma_kp = [&](int j0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {  // K rows 16w .. 16w+15
+      const int r0 = 16 * w + 8 * i, row = r0 + lrow;
+      dma16(qkv_b + (long long)min(j0 + row, Tn - 1) * row3 + dh + ((lchk ^ swz_kp(row)) << 3), Ks + r0 * RB);
+    }
+    const int rbase = Tn - QB - i0 + j0;  // band row 0
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // band rows 32w .. 32w+31
+      const int r0 = 32 * w + 8 * i, rr = r0 + lrow;
+      const int pr = min(max(rbase + rr, 0), 2 * Tn - 2);
+      dma16(pk_h + (long long)pr * ldp + ((lchk ^ swz_kp(rr)) << 3), Ps + r0 * RB);
+    }
+  };
+  auto dma_v = [&](int j0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r0 = 16 * w + 8 * i, row = r0 + lrow;
+      dma16(qkv_b + (long long)min(j0 + row, Tn - 1) * row3 + 2 * dh + ((lchk ^ swz_v(row)) << 3), Vs + r0 * RB);
+    }
+  };
+  // padding byte of key j0 + lane, fetched a chunk ahead and only compared
+  // when Ms is written (a compare right after the load waited for it)
+  auto key_byte = [&](int j0) -> int { return kpm ? (int)kpm[(long long)b * Tn + min(j0 + lane, Tn - 1)] : 0; };
+
+  dma_kp(0);
+  int rm = w == 0 ? key_byte(0) : 0;
+
+  // Qu / Qv B-operand fragments, pre-scaled into the exp2 domain
+  const float qscale = scale * 1.4426950408889634f;
+  bf16x8 fqu[2], fqv[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int d0 = 32 * s + 8 * g;
+    const uint4 q4 = *reinterpret_cast<const uint4*>(qkv_b + (long long)min(my_i, Tn - 1) * row3 + d0);
+    const uint32_t wv[4] = {q4.x, q4.y, q4.z, q4.w};
+    // biases by unconditional vector loads (guarded scalar loads each became
+    // a branch and a full wait)
+    const f32x4 bu0 = *reinterpret_cast<const f32x4*>(pbu + h * dh + d0);
+    const f32x4 bu1 = *reinterpret_cast<const f32x4*>(pbu + h * dh + d0 + 4);
+    const f32x4 bv0 = *reinterpret_cast<const f32x4*>(pbv + h * dh + d0);
+    const f32x4 bv1 = *reinterpret_cast<const f32x4*>(pbv + h * dh + d0 + 4);
+    float qu[8], qv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float q = __uint_as_float((wv[e >> 1] >> (16 * (e & 1))) << 16);
+      const float bu = e < 4 ? bu0[e & 3] : bu1[e & 3], bv = e < 4 ? bv0[e & 3] : bv1[e & 3];
+      qu[e] = my_i < Tn ? (q + bu) * qscale : 0.f;
+      qv[e] = my_i < Tn ? (q + bv) * qscale : 0.f;
+    }
+    fqu[s] = MT<bf16_t>::from8(qu);
+    fqv[s] = MT<bf16_t>::from8(qv);
+  }
+
+  float m_run = -INFINITY, l_run = 0.f;
+  f32x4 acc_o[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc_o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nchunk = (Tn + KC - 1) / KC;
+  const int pofs = 48 - 16 * w;
+  for (int ch = 0; ch < nchunk; ++ch) {
+    const int j0 = ch * KC;
+    const bool more = ch + 1 < nchunk;
+    dma_barrier();  // A
+    if (w == 0) {  // key mask (0 / -inf); keys past Tn are masked, so the clamped rows staged for them never count
+      Ms[lane] = (j0 + lane < Tn && rm == 0) ? 0.f : -INFINITY;
+      if (more) rm = key_byte(j0 + KC);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    dma_v(j0);
+
+    // S^T = K·Qu^T (4 tiles), G^T = P_band·Qv^T (5 tiles)
+    f32x4 acc_s[4], acc_g[5];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc_s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 5; ++t) acc_g[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 fk[4], fpb[5];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int row = 16 * t + c16;
+        fk[t] = *reinterpret_cast<const bf16x8*>(Ks + row * RB + (((4 * s + g) ^ swz_kp(row)) << 3));
+      }
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        const int row = pofs + 16 * t + c16;
+        fpb[t] = *reinterpret_cast<const bf16x8*>(Ps + row * RB + (((4 * s + g) ^ swz_kp(row)) << 3));
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc_s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fk[t], fqu[s], acc_s[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 5; ++t) acc_g[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fpb[t], fqv[s], acc_g[t], 0, 0, 0);
+    }
+    // rel_shift on the write: row R = 16t + 4g + r -> position R - (15 - c16)
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int p = 16 * t + 4 * g + r + c16 - 15;
+        if (t == 0) p = max(p, -1);
+        if (t == 4) p = min(p, KC);
+        gq[p] = acc_g[t][r];
+      }
+    dma_barrier();  // B
+
+    // scores for this lane's query, keys jj = 16t + 4g + r (log2 domain)
+    f32x4 gv[4], mk[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      gv[t] = *reinterpret_cast<const f32x4*>(gq + 16 * t + 4 * g);
+      mk[t] = *reinterpret_cast<const f32x4*>(Ms + 16 * t + 4 * g);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) dma_kp(j0 + KC);
+    float p[4][4];
+    float cmax = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        p[t][r] = acc_s[t][r] + gv[t][r] + mk[t][r];
+        cmax = fmaxf(cmax, p[t][r]);
+      }
+    cmax = col4_max(cmax);
+    const float m_new = fmaxf(m_run, cmax);
+    const float mref = m_new == -INFINITY ? 0.f : m_new;
+    const float alpha = __builtin_amdgcn_exp2f(m_run - mref);
+    float ls = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        p[t][r] = __builtin_amdgcn_exp2f(p[t][r] - mref);
+        ls += p[t][r];
+      }
+    l_run = l_run * alpha + col4_sum(ls);
+    m_run = m_new;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc_o[t] *= alpha;
+    // O^T += V^T · P^T (2 k-steps of 32 keys, permuted-k fragments as above)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      float pv[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pv[r] = p[2 * s2][r];
+        pv[4 + r] = p[2 * s2 + 1][r];
+      }
+      const bf16x8 fp = MT<bf16_t>::from8(pv);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        acc_o[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt_frag_swz(Vs, 32 * s2, 16 * t, lane), fp, acc_o[t], 0, 0, 0);
+    }
+  }
+  if (my_i < Tn) {
+    const float inv = 1.0f / l_run;
+    bf16_t* orow = out + ((long long)b * Tn + my_i) * d_model + h * dh;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      uint2 pk2;
+      pk2.x = (uint32_t)f32_to_bf16(acc_o[t][0] * inv) | ((uint32_t)f32_to_bf16(acc_o[t][1] * inv) << 16);
+      pk2.y = (uint32_t)f32_to_bf16(acc_o[t][2] * inv) | ((uint32_t)f32_to_bf16(acc_o[t][3] * inv) << 16);
+      *reinterpret_cast<uint2*>(orow + 16 * t + 4 * g) = pk2;
+    }
+  }
+}
+
+int launch_dma(const void* qkv, const void* pk, int ldp, const float* pbu, const float* pbv, const uint8_t* kpm, int B,
+               int Tn, int H, float scale, void* out, hipStream_t s) {
+  const int grid = B * H * ((Tn + QB - 1) / QB);
+  hipLaunchKernelGGL(relpos_flash_dma_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<const bf16_t*>(qkv),
+                     reinterpret_cast<const bf16_t*>(pk), ldp, pbu, pbv, kpm, Tn, H, scale,
+                     reinterpret_cast<bf16_t*>(out));
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
 template <typename T, int DHP>
 int launch(const void* qkv, const void* pk, int ldp, const float* pbu, const float* pbv, const uint8_t* kpm, int B,
            int Tn, int H, int dh, float scale, void* out, float* probs, hipStream_t s) {
@@ -535,6 +810,12 @@ SBK_API int sbk_relpos_attention_ld(int dtype_bf16, const void* qkv, const void*
                                     void* out, float* probs, void* stream) {
   if (B <= 0 || Tn <= 0 || H <= 0 || dh <= 0 || dh > 128 || ldp < H * dh) return SBK_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
+#ifndef SBK_ATT_NO_DMA
+  // the encoder's inference path: bf16, dh = 64, no probabilities
+  if (dtype_bf16 && dh == 64 && !probs && ldp % 8 == 0 &&
+      ((reinterpret_cast<uintptr_t>(qkv) | reinterpret_cast<uintptr_t>(pk) | reinterpret_cast<uintptr_t>(out)) % 16) == 0)
+    return launch_dma(qkv, pk, ldp, pbu, pbv, kpm, B, Tn, H, scale, out, s);
+#endif
   if (dtype_bf16)
     return dh <= 64 ? launch<bf16_t, 64>(qkv, pk, ldp, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s)
                     : launch<bf16_t, 128>(qkv, pk, ldp, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s);

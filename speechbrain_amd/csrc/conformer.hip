@@ -123,7 +123,7 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
     v[i] = c < D ? xr[c] : 0.f;
     s += v[i];
   }
-  float mean = wave_sum(s) / D;
+  float mean = wave_sum_v(s) / D;
   float q = 0.f;
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
@@ -131,7 +131,7 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
     const float d = c < D ? v[i] - mean : 0.f;
     q += d * d;
   }
-  float rstd = 1.0f / sqrtf(wave_sum(q) / D + eps1);
+  float rstd = 1.0f / sqrtf(wave_sum_v(q) / D + eps1);
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int c = lane + 64 * i;
@@ -144,7 +144,7 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
   s = 0.f;
 #pragma unroll
   for (int i = 0; i < PER; ++i) s += (lane + 64 * i) < D ? v[i] : 0.f;
-  mean = wave_sum(s) / D;
+  mean = wave_sum_v(s) / D;
   q = 0.f;
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
@@ -152,7 +152,7 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
     const float d = c < D ? v[i] - mean : 0.f;
     q += d * d;
   }
-  rstd = 1.0f / sqrtf(wave_sum(q) / D + eps2);
+  rstd = 1.0f / sqrtf(wave_sum_v(q) / D + eps2);
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int c = lane + 64 * i;
@@ -223,14 +223,14 @@ __global__ void __launch_bounds__(256) dwconv_ln_swish_kernel(const T* __restric
       const float4 v = *reinterpret_cast<const float4*>(r + c);
       s += (v.x + v.y) + (v.z + v.w);
     }
-    const float mean = wave_sum(s) / C;
+    const float mean = wave_sum_v(s) / C;
     float q = 0.f;
     for (int c = 4 * lane; c < C; c += 256) {
       const float4 v = *reinterpret_cast<const float4*>(r + c);
       q += (v.x - mean) * (v.x - mean) + (v.y - mean) * (v.y - mean) + (v.z - mean) * (v.z - mean) +
            (v.w - mean) * (v.w - mean);
     }
-    const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
+    const float rstd = 1.0f / sqrtf(wave_sum_v(q) / C + eps);
     const long long ob = ((long long)b * Tn + t0 + tt) * C;
     for (int c = 4 * lane; c < C; c += 256) {
       const float4 v = *reinterpret_cast<const float4*>(r + c);
@@ -290,13 +290,13 @@ __global__ void __launch_bounds__(256) dwconv_ln_swish_generic(const T* __restri
     const float* r = cv + tt * C;
     float s = 0.f;
     for (int c = lane; c < C; c += 64) s += r[c];
-    const float mean = wave_sum(s) / C;
+    const float mean = wave_sum_v(s) / C;
     float q = 0.f;
     for (int c = lane; c < C; c += 64) {
       const float d = r[c] - mean;
       q += d * d;
     }
-    const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
+    const float rstd = 1.0f / sqrtf(wave_sum_v(q) / C + eps);
     const long long ob = ((long long)b * Tn + t0 + tt) * C;
     for (int c = lane; c < C; c += 64) {
       float y = (r[c] - mean) * rstd * g[c] + beta[c];
@@ -603,7 +603,7 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
 #pragma unroll
         for (int q = 0; q < 4; ++q) sm += on ? acc[mt][nt][q] : 0.f;
     }
-    const float mean = wave_sum(sm) / n1;
+    const float mean = wave_sum_v(sm) / n1;
     float sq = 0.f;
 #pragma unroll
     for (int nt = 0; nt < 3; ++nt) {
@@ -616,7 +616,7 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
           sq += dv * dv;
         }
     }
-    const float rstd = 1.0f / sqrtf(wave_sum(sq) / n1 + eps1);
+    const float rstd = 1.0f / sqrtf(wave_sum_v(sq) / n1 + eps1);
 #pragma unroll
     for (int nt = 0; nt < 3; ++nt) {
       const int f1 = 16 * nt + fr;
@@ -720,7 +720,7 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
       s2 += yv8[u][e];
     }
   }
-  const float m2 = wave_sum(s2) / nout;
+  const float m2 = wave_sum_v(s2) / nout;
   float q2 = 0.f;
 #pragma unroll
   for (int u = 0; u < NCH; ++u)
@@ -729,7 +729,7 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
       const float dv = lane + 64 * u < nch ? yv8[u][e] - m2 : 0.f;
       q2 += dv * dv;
     }
-  const float r2 = 1.0f / sqrtf(wave_sum(q2) / nout + eps2);
+  const float r2 = 1.0f / sqrtf(wave_sum_v(q2) / nout + eps2);
   const long long ob = ((long long)b * T2 + t2) * nout;
 #pragma unroll
   for (int u = 0; u < NCH; ++u) {

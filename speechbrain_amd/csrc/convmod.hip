@@ -130,11 +130,11 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       const int r = w + i * CM_NW, f = f0 + r;
       const bool live = r < nrows && f >= 0 && f < a.T;
       const float v[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
-      const float mean = wave_sum(v[0] + v[1] + v[2] + v[3]) * (1.0f / CM_D);
+      const float mean = wave_sum_v(v[0] + v[1] + v[2] + v[3]) * (1.0f / CM_D);
       float q = 0.f;
 #pragma unroll
       for (int e = 0; e < 4; ++e) q += (v[e] - mean) * (v[e] - mean);
-      const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / CM_D) + a.eps0);
+      const float rstd = 1.0f / sqrtf(wave_sum_v(q) * (1.0f / CM_D) + a.eps0);
       uint2 pk = make_uint2(0u, 0u);
       if (live) {
         pk.x = (uint32_t)f32_to_bf16((v[0] - mean) * rstd * g04.x + b04.x) |
@@ -170,6 +170,9 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) fw[cur ^ 1][t][ks] = ld8g(wrow + t * 16 * CM_D + (kk + 1) * 64 + ks * 32);
       }
+      // keep the prefetch here: left alone the scheduler sank every fragment
+      // load onto its MFMAs (load -> vmcnt(0) -> MFMA, one L2 round trip each)
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         bf16x8 fa[CM_MT1];
@@ -233,14 +236,18 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
     constexpr int NF = CM_BM / (CM_NT / CM_D);
     float wk[CM_KMAX];
 #pragma unroll
-    for (int k = 0; k < CM_KMAX; ++k) wk[k] = k < a.K ? a.wc[k * CM_D + c] : 0.f;  // (K, D): coalesced
+    // unconditional loads (clamped address + select): a guarded load compiled
+    // to a branch and a full wait per element, serialising the 31 tap loads
+    // and the 42 window reads
+    for (int k = 0; k < CM_KMAX; ++k) {  // (K, D): coalesced
+      const float v = a.wc[min(k, a.K - 1) * CM_D + c];
+      wk[k] = k < a.K ? v : 0.f;
+    }
     const float bias = a.bc ? a.bc[c] : 0.f;
+    static_assert((CM_NT / CM_D) * NF + CM_KMAX - 1 <= CM_ROWS, "every window row is staged");
     float win[NF + CM_KMAX - 1];
 #pragma unroll
-    for (int r = 0; r < NF + CM_KMAX - 1; ++r) {
-      const int rr = h * NF + r;
-      win[r] = rr < CM_ROWS ? bf16_to_f32(Gs[rr * CM_S + c]) : 0.f;
-    }
+    for (int r = 0; r < NF + CM_KMAX - 1; ++r) win[r] = bf16_to_f32(Gs[(h * NF + r) * CM_S + c]);
 #pragma unroll
     for (int i = 0; i < NF; ++i) {
       float s = bias;
@@ -259,11 +266,11 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
     for (int fi = w; fi < CM_BM; fi += CM_NW) {
       const float4 v4 = *reinterpret_cast<const float4*>(Cv + fi * CM_D + lane * 4);
       float v[4] = {v4.x, v4.y, v4.z, v4.w};
-      const float mean = wave_sum((v[0] + v[1]) + (v[2] + v[3])) * (1.0f / CM_D);
+      const float mean = wave_sum_v((v[0] + v[1]) + (v[2] + v[3])) * (1.0f / CM_D);
       float q = 0.f;
 #pragma unroll
       for (int e = 0; e < 4; ++e) q += (v[e] - mean) * (v[e] - mean);
-      const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / CM_D) + a.eps1);
+      const float rstd = 1.0f / sqrtf(wave_sum_v(q) * (1.0f / CM_D) + a.eps1);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float z = (v[e] - mean) * rstd * gm[e] + bt[e];
@@ -297,6 +304,9 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) fw[cur ^ 1][t][ks] = ld8g(wrow + t * 16 * CM_D + (kk + 1) * 64 + ks * 32);
       }
+      // keep the prefetch here: left alone the scheduler sank every fragment
+      // load onto its MFMAs (load -> vmcnt(0) -> MFMA, one L2 round trip each)
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         bf16x8 fa[CM_MT3];

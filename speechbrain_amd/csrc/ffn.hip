@@ -112,8 +112,7 @@ __device__ __forceinline__ void row_ln(float (&z)[T2][MT][4], float (*red)[FFN_B
       for (int j = 0; j < T2; ++j)
 #pragma unroll
         for (int e = 0; e < 4; ++e) s += z[j][mt][e];
-      s += __shfl_xor(s, 16);
-      s += __shfl_xor(s, 32);
+      s = col4_sum(s);
       part[mt] = s;
     }
     __syncthreads();
@@ -143,8 +142,7 @@ __device__ __forceinline__ void row_ln(float (&z)[T2][MT][4], float (*red)[FFN_B
           const float dv = z[j][mt][e] - mean[mt];
           s += dv * dv;
         }
-      s += __shfl_xor(s, 16);
-      s += __shfl_xor(s, 32);
+      s = col4_sum(s);
       part[mt] = s;
     }
     __syncthreads();
@@ -289,11 +287,11 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     if (rr >= BM) break;
     const bool live = m0 + rr < a.M;
     const float v[4] = {live ? xv[i].x : 0.f, live ? xv[i].y : 0.f, live ? xv[i].z : 0.f, live ? xv[i].w : 0.f};
-    const float mean = wave_sum(v[0] + v[1] + v[2] + v[3]) / D;
+    const float mean = wave_sum_v(v[0] + v[1] + v[2] + v[3]) / D;
     float q = 0.f;
 #pragma unroll
     for (int e = 0; e < 4; ++e) q += (v[e] - mean) * (v[e] - mean);
-    const float rstd = 1.0f / sqrtf(wave_sum(q) / D + a.eps0);
+    const float rstd = 1.0f / sqrtf(wave_sum_v(q) / D + a.eps0);
     uint2 pk;
     pk.x = (uint32_t)f32_to_bf16((v[0] - mean) * rstd * g04.x + b04.x) |
            ((uint32_t)f32_to_bf16((v[1] - mean) * rstd * g04.y + b04.y) << 16);

@@ -31,6 +31,41 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// VALU-only cross-lane reductions (gfx950).  __shfl_xor lowers to
+// ds_bpermute_b32: each step is an LDS-pipe round trip (~50+ cycles) behind a
+// full lgkmcnt wait.  These use DPP row permutes and the gfx950
+// v_permlane32_swap / v_permlane16_swap half-swaps instead.  Every step adds
+// the same two operands in both partner lanes (involutive permutes), so all
+// lanes of the reduced group end with the identical value.
+//
+// sum / max over the 4 lanes {l, l^16, l^32, l^48}: one column of a 16x16
+// MFMA tile
+__device__ __forceinline__ float col4_sum(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+__device__ __forceinline__ float col4_max(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// whole-wave sum: row_mirror, row_half_mirror, quad_perm [2,3,0,1] and
+// [1,0,3,2] inside each 16-lane row, then col4_sum across the rows
+__device__ __forceinline__ float wave_sum_v(float v) {
+  v += dpp_f32<0x140>(v);
+  v += dpp_f32<0x141>(v);
+  v += dpp_f32<0x4E>(v);
+  v += dpp_f32<0xB1>(v);
+  return col4_sum(v);
+}
+
 // Monotone float <-> int32 key so that atomicMax on the key orders floats.
 __device__ __forceinline__ int float_to_key(float f) {
   int i = __float_as_int(f);

@@ -114,10 +114,11 @@ class RelPosMHAXL(nn.Module):
             raise NotImplementedError("vbias=True is not on the RelPosMHAXL hot path")
         w_in, w_pos, w_out = self.kernel_weights(dtype)
         qkv = _enc.gemm(x2d, w_in, out_dtype=dtype)
-        pos = pos_embs.reshape(-1, self.embed_dim)
-        if pos.dtype != dtype:
-            pos = _enc.cast_bf16(pos.float().contiguous()) if dtype == torch.bfloat16 else pos.float()
-        pk = _enc.gemm(pos.contiguous(), w_pos, out_dtype=dtype)
+        if pk is None:  # the encoder passes its one stacked linear_pos GEMM's slice
+            pos = pos_embs.reshape(-1, self.embed_dim)
+            if pos.dtype != dtype:
+                pos = _enc.cast_bf16(pos.float().contiguous()) if dtype == torch.bfloat16 else pos.float()
+            pk = _enc.gemm(pos.contiguous(), w_pos, out_dtype=dtype)
         o, probs = _enc.relpos_attention(qkv, pk, self.pos_bias_u.detach(), self.pos_bias_v.detach(), kpm_u8, B, T,
                                          self.num_heads, self.head_dim, self.scale, need_weights)
         bias = self.out_proj.bias.detach()

@@ -252,6 +252,46 @@ def test_relpos_mha_module_vs_oracle(dev):
     assert_close(attn, ref_attn, name="attn")
 
 
+def _relpos_ref(qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale):
+    """fp32 torch evaluation of attention.py:566-631 on the kernel's operand
+    layout: qkv (B*T, 3d) head-interleaved [h][q|k|v][dh], pk (2T-1, d)."""
+    x = qkv.float().view(B, T, H, 3, dh)
+    q, k, v = x[:, :, :, 0], x[:, :, :, 1], x[:, :, :, 2]
+    p = pk.float().reshape(2 * T - 1, H, dh)
+    ac = torch.einsum("bihd,bjhd->bhij", q + pbu.view(H, dh), k)
+    bd_full = torch.einsum("bihd,rhd->bhir", q + pbv.view(H, dh), p)
+    i = torch.arange(T, device=qkv.device)[:, None]
+    j = torch.arange(T, device=qkv.device)[None]
+    bd = bd_full[:, :, i, T - 1 - i + j]  # rel_shift in closed form
+    s = ((ac + bd) * scale).masked_fill(kpm[:, None, None, :], float("-inf"))
+    return torch.einsum("bhij,bjhd->bihd", s.softmax(-1), v).reshape(B * T, H * dh)
+
+
+@pytest.mark.parametrize("T,lens,strided", [(37, [37, 30, 21], False), (97, [97, 60, 5], True),
+                                            (376, [376, 376, 200, 1], True)])
+def test_relpos_attention_bf16_vs_torch(dev, T, lens, strided):
+    """The encoder's attention path (bf16, dh = 64, no probabilities: the
+    LDS-DMA kernel) vs an fp32 torch evaluation on the same bf16 operands:
+    ragged key-padding masks incl. a 1-key utterance, and the strided p_k slice
+    the encoder passes (one stacked linear_pos GEMM).  P is rounded to bf16 for
+    the P·V MFMA, so outputs (~N(0,1) averages) agree to 2e-2."""
+    from speechbrain_amd import _enc
+    g = torch.Generator().manual_seed(T)
+    B, H, dh = len(lens), 4, 64
+    d = H * dh
+    qkv = torch.randn(B * T, 3 * d, generator=g).to(torch.bfloat16).to(dev)
+    pk_all = torch.randn(2 * T - 1, 3 * d, generator=g).to(torch.bfloat16).to(dev)
+    pk = pk_all[:, d:2 * d] if strided else pk_all[:, :d].contiguous()
+    pbu = (0.1 * torch.randn(d, generator=g)).to(dev)
+    pbv = (0.1 * torch.randn(d, generator=g)).to(dev)
+    kpm = (torch.arange(T)[None] >= torch.tensor(lens)[:, None]).to(dev)
+    scale = 1.0 / math.sqrt(d)
+    out, _ = _enc.relpos_attention(qkv, pk, pbu, pbv, kpm.to(torch.uint8).contiguous(), B, T, H, dh, scale)
+    ref = _relpos_ref(qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale)
+    assert out.dtype == torch.bfloat16
+    assert_close(out, ref, rtol=2e-2, name="attn_bf16")
+
+
 def test_encoder_bf16_autocast_close(golden, dev):
     g = golden("conformer")
     tr = _tr(g, dev)
