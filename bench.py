@@ -174,6 +174,11 @@ def _gemm_flops(a, w, *r, **k):
     return gemm_flops(a.shape[0], w.shape[0], a.shape[1])
 
 
+def _attn_flops(qkv, pk, pbu, pbv, kpm, B, T, H, dh, *a, **k):
+    """scores 2·T·d + 2·(2T−1)·d and P·V 2·T·d per query token."""
+    return float(B) * T * H * dh * (8 * T - 2)
+
+
 def load_traffic():
     """Per-launch HBM bytes of the profiled kernels (rocprofv3 PMC FETCH_SIZE x2
     (gfx950 correction) + WRITE_SIZE), committed under profiles/."""
@@ -264,7 +269,8 @@ def main():
         # replayed back to back from a HIP graph and timed with HIP events
         bf = lambda t: t.dtype == torch.bfloat16  # noqa: E731
         probes = [_LaunchProbe("ffn", _ffn_flops, lambda x, ln0, w1, *a, **k: bf(w1)),
-                  _LaunchProbe("gemm", _gemm_flops, lambda a, w, *r, **k: bf(a))]
+                  _LaunchProbe("gemm", _gemm_flops, lambda a, w, *r, **k: bf(a)),
+                  _LaunchProbe("relpos_attention", _attn_flops, lambda qkv, *a, **k: bf(qkv))]
         for p in probes:
             p.__enter__()
         try:
@@ -274,7 +280,8 @@ def main():
                 p.__exit__()
         kern = {}
         labels = (("ffn_kernel<256, 1> (fused macaron FFN)", "ffn_kernel<256, 1>"),
-                  ("gemm_kernel<bf16> (projections, all tiles)", "gemm_kernel<unsigned short, 64, 64, 64, 2>"))
+                  ("gemm_kernel<bf16> (projections, all tiles)", "gemm_kernel<unsigned short, 64, 64, 64, 2>"),
+                  ("relpos_flash_dma_kernel (rel-pos attention)", "relpos_flash_dma_kernel"))
         for p, (label, pmc_key) in zip(probes, labels):
             ms, n, fl = p.replay_time()
             if n:
