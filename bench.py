@@ -199,6 +199,71 @@ def max_over_ranks(elapsed, world, device):
     return float(t.item())
 
 
+def per_rank(elapsed, world, device):
+    """Every rank's wall time, in rank order (reported beside the max)."""
+    if world <= 1:
+        return [elapsed]
+    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [float(x.item()) for x in out]
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(script, argv, n):
+    """`--gpus N` without a torchrun launcher: start N child processes of
+    `script` (one per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set as torchrun
+    would, rendezvous on 127.0.0.1) and return the worst exit code.  Called
+    before this process touches the GPU, so the parent never initialises HIP;
+    the children are started (not exec'd) and the parent waits for all."""
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, script, *argv], env=env))
+    codes = [p.wait() for p in procs]
+    return max(codes, key=abs)
+
+
+def rank_env(gpus):
+    """(world, rank, local_rank) from the torchrun environment; the world size
+    must equal --gpus (a launcher that started fewer ranks than asked for would
+    otherwise report a silently wrong scaling point)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != gpus:
+        raise SystemExit(f"--gpus {gpus} but WORLD_SIZE={world}: launch with torchrun --nproc-per-node {gpus} "
+                         f"or without WORLD_SIZE set (bench.py then starts the ranks itself)")
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def launch_plumbing(args):
+    """`--plumbing`: the launcher + rendezvous + max-over-ranks timing on CPU
+    (gloo), a fixed sleep per rank instead of the GPU step.  Used by the CPU
+    test of the multi-rank contract."""
+    world, rank, _ = rank_env(args.gpus)
+    if world > 1:
+        dist.init_process_group("gloo")
+        assert dist.get_world_size() == args.gpus
+    t0 = time.perf_counter()
+    time.sleep(0.05 * (1 + rank))
+    mine = time.perf_counter() - t0
+    elapsed = max_over_ranks(mine, world, torch.device("cpu"))
+    ranks = per_rank(mine, world, torch.device("cpu"))
+    if rank == 0:
+        print(json.dumps({"metric": "plumbing", "n_gpus": world, "elapsed": elapsed, "rank_s": ranks,
+                          "world_from_dist": dist.get_world_size() if world > 1 else 1}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -208,15 +273,20 @@ def main():
     ap.add_argument("--batch", type=int, default=BATCH)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--plumbing", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(os.path.abspath(__file__), sys.argv[1:], args.gpus))
+    if args.plumbing:
+        return launch_plumbing(args)
+
+    world, rank, local = rank_env(args.gpus)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        assert dist.get_world_size() == args.gpus
 
     fbank, cnn, tr = build_model(args.d_model, dev)
     g = torch.Generator().manual_seed(1234 + rank)
@@ -258,7 +328,9 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+    mine = time.perf_counter() - t0
+    elapsed = max_over_ranks(mine, world, dev)
+    rank_ms = [round(1000.0 * t / args.steps, 4) for t in per_rank(mine, world, dev)]
     ms_per_step = 1000.0 * elapsed / args.steps
     audio = world * args.batch * SECONDS * args.steps
     value = audio / elapsed
@@ -299,6 +371,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
+            "rank_ms_per_step": rank_ms,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

@@ -130,9 +130,10 @@ def main():
     ap.add_argument("--fp32", action="store_true", help="no autocast (parity mode)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import bench
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(bench.launch_ranks(os.path.abspath(__file__), sys.argv[1:], args.gpus))
+    world, rank, local = bench.rank_env(args.gpus)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     run_opts = {"device": str(dev), "auto_mix_prec": False if args.fp32 else "bf16", "max_grad_norm": 5.0}
@@ -162,11 +163,9 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    mine = time.perf_counter() - t0
+    elapsed = bench.max_over_ranks(mine, world, dev)
+    rank_ms = [round(1000.0 * t / args.steps, 3) for t in bench.per_rank(mine, world, dev)]
     ms = 1000.0 * elapsed / args.steps
     value = world * args.batch * SECONDS * args.steps / elapsed
     if rank == 0:
@@ -176,7 +175,8 @@ def main():
         print(json.dumps({
             "metric": "audio-sec/sec Conformer-Transducer train step (Brain DDP, HIP RNN-T), B=32x15s per GPU",
             "value": round(value, 1), "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "warmup": args.warmup, "ms_per_step": round(ms, 3), "rank_ms_per_step": rank_ms,
+            "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "fp32" if args.fp32 else "bf16", "data": "synthetic",
             "config": {"workload": f"C4: Fbank→InputNorm→SpecAugment→CNN→Conformer {args.layers}L d=256 → TN/PN → sum joint "
                                    f"LeakyReLU → Linear(1024→1000) → RNN-T; Adam; clip 5.0",

@@ -37,3 +37,33 @@ def test_max_over_ranks_gloo():
 def test_max_over_ranks_single():
     import bench
     assert bench.max_over_ranks(0.25, 1, torch.device("cpu")) == 0.25
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """`python bench.py --gpus 2` with no launcher starts two ranks itself;
+    the JSON reports n_gpus == 2 and the slowest rank's time (rank 1 sleeps
+    twice as long as rank 0)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--plumbing"],
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["world_from_dist"] == 2
+    assert len(res["rank_s"]) == 2 and res["elapsed"] == max(res["rank_s"])
+    assert res["rank_s"][1] >= 0.1
+
+
+def test_bench_rejects_world_mismatch():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--plumbing"],
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
