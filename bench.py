@@ -55,6 +55,19 @@ def build_model(d_model, dev, layers=12):
     return fbank.to(dev).eval(), cnn.to(dev).eval(), tr.to(dev).eval()
 
 
+def make_step(fbank, cnn, tr, wav, wav_len):
+    """The timed step: Fbank (fused spectrum kernel + top_db clamp) → both
+    ConvBlocks in one bf16 kernel → TransformerASR.encode under bf16 autocast
+    (fused FFN / conv-module / LDS-DMA attention kernels).  Also what
+    tests/test_gpu_bench_parity.py runs against the fp32 oracle."""
+    def step():
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            feats = fbank(wav)
+            src = cnn.run(feats, torch.bfloat16)
+            return tr.encode(src, wav_len)
+    return step
+
+
 def encoder_flops(B, T_e, d, dff=1024, k=31, H=4, layers=12, T1=751, F1=40, T2=376, F2=20, c1=64, c2=32,
                   in_dim=640):
     """Algorithmic FLOPs of one step: per layer QKV 6d², out 2d²,
@@ -293,11 +306,7 @@ def main():
     wav = (0.1 * torch.randn(args.batch, int(SR * SECONDS), generator=g)).to(dev)
     wav_len = torch.ones(args.batch, device=dev)
 
-    def step():
-        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
-            feats = fbank(wav)
-            src = cnn.run(feats, torch.bfloat16)
-            return tr.encode(src, wav_len)
+    step = make_step(fbank, cnn, tr, wav, wav_len)
 
     out = step()
     T_e = out.shape[1]

@@ -66,6 +66,21 @@ int sbk_filterbank_slots(int T, int F);
 int sbk_topdb_clamp(float* x, const float* slot_max, int nslot, long long per_seq, int nseq, float top_db,
                     void* stream);
 
+/* Backward of the dB + top_db stage of Filterbank (features.py:691-712, what
+ * autograd gives the reference for freeze=False filters, :476-482):
+ * x = linear filterbank energies (N, per_seq) recomputed with
+ * sbk_filterbank(log_mel=0), g = dL/d(output) -> dx = dL/dx, including the
+ * amax (top_db reference) path with ties split as torch.maximum / amax do.
+ * stats: 3*N floats of workspace.  log_mel=0 copies g. */
+int sbk_filterbank_db_bwd(const float* x, const float* g, int N, long long per_seq, int log_mel, float multiplier,
+                          float db_offset, float amin, float top_db, float* stats, float* dx, void* stream);
+
+/* Dense filter-matrix gradient partials: part[c] (F, M) = sum over rows of chunk
+ * c of spec[r, :]^T dx[r, :] (rows = N*T, M <= 128); reduce the
+ * ceil(rows / rows_per_chunk) partials with sbk_colsum. */
+int sbk_filterbank_wgrad(const float* spec, const float* dx, long long rows, int F, int M, long long rows_per_chunk,
+                         float* part, void* stream);
+
 /* spectral_magnitude (features.py:347-356): y[i] = f(sum_q x[i, q]^2), q < L. */
 int sbk_magnitude(const float* x, float* y, long long n, int L, float power, float eps, int log_mag, void* stream);
 

@@ -71,11 +71,6 @@ def gemm_ln(a, w, ln, bias=None, res=None, alpha=1.0, rowmask=None, out=None, u_
     return out, u
 
 
-# RelPosMHAXL in_proj (a plain bf16 GEMM) on hipBLASLt instead of sbk_gemm:
-# 11.8 vs 15.0 us alone (scripts/kbench.py gemm) but no change in the graph-
-# replayed step (233.8k vs 232.9-234.2k audio-s/s): off.
-QKV_LIBRARY_GEMM = False
-
 # The fused projection + LayerNorm (sbk_gemm_ln) measures the same as the two
 # launches it replaces at M = 12032 (15.1 vs 8.5 + 6.3 us): off by default.
 USE_GEMM_LN = False
@@ -234,9 +229,16 @@ def to_compute(x, dtype):
 
 
 def compute_dtype():
-    """bf16 MFMA under torch.autocast(device_type='cuda', dtype=bf16|fp16),
-    exact-f32 MFMA otherwise."""
+    """bf16 MFMA under torch.autocast(device_type='cuda', dtype=bf16),
+    exact-f32 MFMA otherwise.  fp16 autocast (the reference's
+    `--auto_mix_prec`, core.py:905-919) has no kernels here and raises rather
+    than silently computing in bf16."""
     if torch.is_autocast_enabled("cuda"):
+        dt = torch.get_autocast_dtype("cuda")
+        if dt != _bf16:
+            raise NotImplementedError(
+                f"speechbrain_amd kernels compute in bf16 or fp32; torch.autocast(dtype={dt}) is not supported. "
+                "Use torch.autocast('cuda', dtype=torch.bfloat16) (Brain: auto_mix_prec='bf16') or no autocast.")
         return _bf16
     return _f32
 

@@ -32,6 +32,8 @@ SIGNATURES = {
     "sbk_spectrum_slots": [_i, _i, _i, _i, _i],
     "sbk_filterbank_slots": [_i, _i],
     "sbk_topdb_clamp": [_vp, _vp, _i, _ll, _i, _f, _vp],
+    "sbk_filterbank_db_bwd": [_vp, _vp, _i, _ll, _i, _f, _f, _f, _f, _vp, _vp, _vp],
+    "sbk_filterbank_wgrad": [_vp, _vp, _ll, _i, _i, _ll, _vp, _vp],
     "sbk_magnitude": [_vp, _vp, _ll, _i, _f, _f, _i, _vp],
     "sbk_dct": [_vp, _vp, _vp, _ll, _i, _i, _vp],
     "sbk_deltas": [_vp, _vp, _i, _i, _i, _i, _i, _vp],

@@ -13,8 +13,10 @@ unchanged).  MI355X choices:
     two large ring all-reduces over xGMI instead of four 25 MB ones);
     `gradient_as_bucket_view` so gradients live in the buckets (no copy);
   * mixed precision is bf16 autocast (same exponent range as fp32, so no
-    GradScaler — the reference's fp16 scaler path is kept for
-    `auto_mix_prec="fp16"`);
+    GradScaler).  The reference's `--auto_mix_prec` (True) means fp16
+    autocast + GradScaler; here True selects bf16 and says so in the log,
+    and "fp16" raises — the kernels have no fp16 path, and computing bf16
+    under an fp16 request would change numerics without telling the caller;
   * everything the modules compute runs on libsbk.so HIP kernels.
 """
 import contextlib
@@ -38,7 +40,7 @@ class Brain:
 
     modules: dict of nn.Modules; opt_class: callable(params) -> optimizer;
     run_opts: device, distributed_launch, distributed_backend,
-    auto_mix_prec (False | True/"bf16" | "fp16"), max_grad_norm (5.0),
+    auto_mix_prec (False | True/"bf16"; "fp16" raises), max_grad_norm (5.0),
     grad_accumulation_factor (1), nonfinite_patience (3),
     find_unused_parameters (False), bucket_cap_mb (64).
     """
@@ -49,8 +51,12 @@ class Brain:
         self.distributed_launch = bool(run_opts.get("distributed_launch", False))
         self.distributed_backend = run_opts.get("distributed_backend", "nccl")
         amp = run_opts.get("auto_mix_prec", False)
-        self.amp_dtype = {False: None, None: None, True: torch.bfloat16, "bf16": torch.bfloat16,
-                          "fp16": torch.float16}[amp]
+        if amp in ("fp16", torch.float16):
+            raise NotImplementedError("auto_mix_prec='fp16': the speechbrain_amd kernels compute in bf16 or fp32; "
+                                      "use auto_mix_prec='bf16' (no GradScaler needed) or False")
+        if amp is True:
+            logger.warning("auto_mix_prec=True runs bf16 autocast on MI355X (the reference uses fp16 + GradScaler)")
+        self.amp_dtype = {False: None, None: None, True: torch.bfloat16, "bf16": torch.bfloat16}[amp]
         self.max_grad_norm = float(run_opts.get("max_grad_norm", 5.0))
         self.grad_accumulation_factor = int(run_opts.get("grad_accumulation_factor", 1))
         self.nonfinite_patience = int(run_opts.get("nonfinite_patience", 3))
@@ -62,7 +68,6 @@ class Brain:
         self.step = 0
         self.optimizer_step = 0
         self.nonfinite_count = 0
-        self.scaler = torch.amp.GradScaler("cuda") if self.amp_dtype == torch.float16 else None
         self._wrap_distributed()
         self.optimizer = None
         if opt_class is not None:
@@ -129,15 +134,9 @@ class Brain:
             outputs = self.compute_forward(batch, Stage.TRAIN)
             loss = self.compute_objectives(outputs, batch, Stage.TRAIN)
         with self.no_sync(not should_step):
-            scaled = loss / self.grad_accumulation_factor
-            (self.scaler.scale(scaled) if self.scaler is not None else scaled).backward()
+            (loss / self.grad_accumulation_factor).backward()
         if should_step:
-            if self.scaler is not None:
-                self.scaler.unscale_(self.optimizer)
-                if self.check_gradients(loss):
-                    self.scaler.step(self.optimizer)
-                self.scaler.update()
-            elif self.check_gradients(loss):
+            if self.check_gradients(loss):
                 self.optimizer.step()
             self.zero_grad()
             self.optimizer_step += 1

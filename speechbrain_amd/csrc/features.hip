@@ -23,6 +23,16 @@ using namespace sbk;
 
 namespace {
 
+// Filterbank._amplitude_to_DB before the top_db clamp (features.py:701-702):
+// multiplier·log10(clamp(x, amin)) − multiplier·db_multiplier, with x ≤ amin
+// mapped to the host-rounded dB of amin (exactly −100 for 1e-10).  One
+// definition shared by the forward kernels and the backward's recompute, so
+// the backward sees bit-identical dB values (tie detection against top_db).
+__device__ __forceinline__ float to_db(float x, float amin, float amin_db, float mult, float off) {
+  return x <= amin ? amin_db : mult * log10f(x) - off;
+}
+
+
 struct FftPlan {
   int nc;          // complex FFT size (n_fft / 2)
   int nstages;
@@ -383,7 +393,7 @@ __global__ void __launch_bounds__(256) spec_kernel(SpecArgs a, FftPlan plan) {
     for (int q = 0; q < L; ++q) acc = fmaf(pf[q], w[q], acc);
     if (a.log_mel) {
       // clamp(x, amin) -> the host-rounded dB of amin exactly (-100 for 1e-10)
-      acc = acc <= a.amin ? a.amin_db : a.multiplier * log10f(acc) - a.db_offset;
+      acc = to_db(acc, a.amin, a.amin_db, a.multiplier, a.db_offset);
       lmax = fmaxf(lmax, acc);
     }
     orow[f * a.M + j] = acc;
@@ -433,7 +443,7 @@ __global__ void __launch_bounds__(256) filterbank_kernel(FbArgs a) {
       for (int q = 0; q < L; ++q) acc = fmaf(pf[q], w[q], acc);
     }
     if (a.log_mel) {
-      acc = acc <= a.amin ? a.amin_db : a.multiplier * log10f(acc) - a.db_offset;
+      acc = to_db(acc, a.amin, a.amin_db, a.multiplier, a.db_offset);
       lmax = fmaxf(lmax, acc);
     }
     a.out[(r0 + rr) * a.M + j] = acc;
@@ -859,7 +869,7 @@ __global__ void __launch_bounds__(NT) spec_static_kernel(SpecArgs a) {
       float acc = 0.f;
       for (int q = 0; q < L; ++q) acc = fmaf(pf[q], w[q], acc);
       if (a.log_mel) {
-        acc = acc <= a.amin ? a.amin_db : a.multiplier * log10f(acc) - a.db_offset;
+        acc = to_db(acc, a.amin, a.amin_db, a.multiplier, a.db_offset);
         lmax = fmaxf(lmax, acc);
       }
       orow[f * a.M + j] = acc;
@@ -1109,6 +1119,120 @@ SBK_API int sbk_context_window(const float* x, float* y, int N, int T, int F, in
   const int L = left + right + 1;
   hipLaunchKernelGGL(context_kernel, dim3(grid_for((long long)N * T * F * L, 256)), dim3(256), 0,
                      (hipStream_t)stream, x, y, N, T, F, left, L);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Filterbank backward (freeze=False learnable filters, features.py:476-482;
+// the reference gets it from autograd of matmul → clamp → log10 → amax → max)
+// ---------------------------------------------------------------------------
+namespace {
+
+// Per sequence n (one 1024-thread block): xdb = to_db(x), m = max xdb,
+// thr = m − top_db; count of elements at m; G = Σ g over elements the clamp
+// selected (xdb < thr: g, xdb == thr: g/2 — torch.maximum splits ties).
+__global__ void __launch_bounds__(1024) fb_db_stats_kernel(const float* __restrict__ x, const float* __restrict__ g,
+                                                           long long per_seq, float amin, float amin_db, float mult,
+                                                           float off, float top_db, float* __restrict__ stats) {
+  __shared__ float red[16];
+  const int n = blockIdx.x;
+  const float* xs = x + (long long)n * per_seq;
+  const float* gs = g + (long long)n * per_seq;
+  float m = -INFINITY;
+  for (long long i = threadIdx.x; i < per_seq; i += blockDim.x) m = fmaxf(m, to_db(xs[i], amin, amin_db, mult, off));
+  m = block_max(m, red);
+  const float thr = m - top_db;
+  float cnt = 0.f, gthr = 0.f;
+  for (long long i = threadIdx.x; i < per_seq; i += blockDim.x) {
+    const float d = to_db(xs[i], amin, amin_db, mult, off);
+    cnt += d == m ? 1.f : 0.f;
+    gthr += d < thr ? gs[i] : (d == thr ? 0.5f * gs[i] : 0.f);
+  }
+  cnt = block_sum(cnt, red);
+  gthr = block_sum(gthr, red);
+  if (threadIdx.x == 0) {
+    stats[3 * n] = m;
+    stats[3 * n + 1] = cnt;
+    stats[3 * n + 2] = gthr;
+  }
+}
+
+// dx = d/dx of the dB + top_db clamp: the element's own path
+// (xdb > thr: g, == thr: g/2), plus G/count at the argmax elements (amax
+// backward), through log10 (g·mult / (x·ln 10)) and the amin clamp (x ≥ amin).
+__global__ void __launch_bounds__(256) fb_db_bwd_kernel(const float* __restrict__ x, const float* __restrict__ g,
+                                                        const float* __restrict__ stats, long long per_seq, int log_mel,
+                                                        float amin, float amin_db, float mult, float off, float top_db,
+                                                        float* __restrict__ dx) {
+  const int n = blockIdx.y;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= per_seq) return;
+  const long long k = (long long)n * per_seq + i;
+  const float xv = x[k], gv = g[k];
+  if (!log_mel) {
+    dx[k] = gv;
+    return;
+  }
+  const float m = stats[3 * n], thr = m - top_db;
+  const float d = to_db(xv, amin, amin_db, mult, off);
+  float gd = d > thr ? gv : (d == thr ? 0.5f * gv : 0.f);
+  if (d == m) gd += stats[3 * n + 2] / stats[3 * n + 1];
+  dx[k] = xv >= amin ? (gd * mult) / (xv * 2.302585093f) : 0.f;
+}
+
+// Weight gradient partials: part[c, f, j] = Σ_{r in row chunk c} spec[r, f]·dx[r, j].
+// Block (4 frequency rows, chunk c); wave w owns f = 4·blockIdx.x + w, lane
+// owns j = lane, lane + 64 (M ≤ 128).  Reduced over chunks by sbk_colsum.
+__global__ void __launch_bounds__(256) fb_wgrad_kernel(const float* __restrict__ spec, const float* __restrict__ dx,
+                                                       long long rows, int F, int M, long long rows_per_chunk,
+                                                       float* __restrict__ part) {
+  const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const long long r0 = (long long)blockIdx.y * rows_per_chunk;
+  const long long r1 = min(rows, r0 + rows_per_chunk);
+  if (f >= F) return;
+  float a0 = 0.f, a1 = 0.f;
+  for (long long r = r0; r < r1; ++r) {
+    const float sv = spec[r * F + f];
+    if (lane < M) a0 = fmaf(sv, dx[r * M + lane], a0);
+    if (lane + 64 < M) a1 = fmaf(sv, dx[r * M + lane + 64], a1);
+  }
+  float* o = part + (long long)blockIdx.y * F * M + (long long)f * M;
+  if (lane < M) o[lane] = a0;
+  if (lane + 64 < M) o[lane + 64] = a1;
+}
+
+}  // namespace
+
+// dB/top_db backward of Filterbank: x = linear filterbank energies (N, per_seq)
+// (recomputed with sbk_filterbank(log_mel=0)), g = dL/d(output); dx = dL/dx.
+// stats: 3·N floats of workspace.
+SBK_API int sbk_filterbank_db_bwd(const float* x, const float* g, int N, long long per_seq, int log_mel,
+                                  float multiplier, float db_offset, float amin, float top_db, float* stats, float* dx,
+                                  void* stream) {
+  if (N <= 0 || per_seq <= 0 || (log_mel && !stats)) return SBK_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const float amin_db = multiplier * (float)log10((double)amin) - db_offset;
+  if (log_mel) {
+    hipLaunchKernelGGL(fb_db_stats_kernel, dim3(N), dim3(1024), 0, s, x, g, per_seq, amin, amin_db, multiplier,
+                       db_offset, top_db, stats);
+    SBK_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(fb_db_bwd_kernel, dim3((unsigned)((per_seq + 255) / 256), N), dim3(256), 0, s, x, g, stats,
+                     per_seq, log_mel, amin, amin_db, multiplier, db_offset, top_db, dx);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+// Partial weight gradient of the dense filter matrix: part (nchunk, F, M)
+// with nchunk = ceil(rows / rows_per_chunk); sum with sbk_colsum.
+SBK_API int sbk_filterbank_wgrad(const float* spec, const float* dx, long long rows, int F, int M,
+                                 long long rows_per_chunk, float* part, void* stream) {
+  if (rows <= 0 || F <= 0 || M <= 0 || M > 128 || rows_per_chunk <= 0) return SBK_ERR_ARG;
+  const long long nchunk = (rows + rows_per_chunk - 1) / rows_per_chunk;
+  hipLaunchKernelGGL(fb_wgrad_kernel, dim3((unsigned)((F + 3) / 4), (unsigned)nchunk), dim3(256), 0,
+                     (hipStream_t)stream, spec, dx, rows, F, M, rows_per_chunk, part);
   SBK_CHECK_LAUNCH();
   return 0;
 }

@@ -54,7 +54,10 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ x
   if (lane == 0) {
     lpb[row] = xr[blank] - lse;
     const int Um = U1 - 1;
-    lpl[row] = u < Um ? xr[labels[b * Um + u]] - lse : 0.f;
+    const int y = u < Um ? labels[b * Um + u] : 0;
+    // a label outside [0, V) poisons its cell (NaN loss) instead of reading
+    // past the row
+    lpl[row] = u < Um ? ((unsigned)y < (unsigned)V ? xr[y] - lse : __builtin_nanf("")) : 0.f;
     if (lse_out) lse_out[row] = lse;
   }
 }
@@ -69,6 +72,12 @@ __global__ void __launch_bounds__(256) lattice_kernel(const float* __restrict__ 
   const int b = blockIdx.x;
   const bool fwd = blockIdx.y == 0;
   const int Tb = Tl[b], Ub = Ul[b];
+  if (Tb < 1 || Tb > T || Ub < 0 || Ub > U1 - 1) {
+    // lengths outside the (T, U1) lattice: NaN loss for this utterance, no
+    // access outside its slab or the 2*U1 diagonal buffer
+    if (threadIdx.x == 0) logp[(fwd ? 0 : gridDim.x) + b] = __builtin_nanf("");
+    return;
+  }
   const long long base = (long long)b * T * U1;
   const float* pb = lpb + base;
   const float* pl = lpl + base;
@@ -145,7 +154,9 @@ __global__ void sparse_grad_kernel(const float* __restrict__ lpb, const float* _
     const float b00 = logp[B + b];
     const long long base = (long long)b * T * U1;
     float vb = 0.f, vl = 0.f;
-    if (t < Tb && u <= Ub) {
+    if (Tb < 1 || Tb > T || Ub < 0 || Ub > U1 - 1) {
+      vb = vl = __builtin_nanf("");  // invalid lengths: NaN gradient, as the loss
+    } else if (t < Tb && u <= Ub) {
       const float a = alpha[i];
       if (t < Tb - 1) {
         const float s = (a + beta[base + (long long)(t + 1) * U1 + u]) + lpb[i];

@@ -249,3 +249,82 @@ def context_window(x: torch.Tensor, left: int, right: int) -> torch.Tensor:
 @context_window.register_fake
 def _(x, left, right):
     return x.new_empty(x.shape[0], x.shape[1], x.shape[2] * (left + right + 1))
+
+
+# ---------------------------------------------------------------------------
+# autograd for the learnable-filter path (Filterbank(freeze=False),
+# Fbank/MFCC(requires_grad=True); features.py:476-482): the reference gets
+# these gradients from torch autograd; here they are HIP kernels too
+# ---------------------------------------------------------------------------
+
+@torch.library.custom_op("sbk::filterbank_dense_bwd", mutates_args=())
+def filterbank_dense_bwd(grad: torch.Tensor, spec: torch.Tensor, mat: torch.Tensor, log_mel: bool,
+                         multiplier: float, db_offset: float, amin: float,
+                         top_db: float) -> tuple[torch.Tensor, torch.Tensor]:
+    """(dL/dspec, dL/dmat) of filterbank_dense: the linear energies are
+    recomputed by the forward's own kernel (bit-identical dB values for the
+    top_db tie rule), sbk_filterbank_db_bwd differentiates dB + top_db,
+    dspec = dx·matᵀ runs on the dense filterbank kernel with matᵀ, and dmat
+    is a chunked specᵀ·dx reduced by sbk_colsum (deterministic)."""
+    require_device(grad, spec, mat)
+    spec = _c(spec.to(_f32))
+    mat = _c(mat.to(_f32))
+    grad = _c(grad.to(_f32))
+    N, T, Fd = spec.shape
+    M = mat.shape[1]
+    L = _lib.lib()
+    s = stream_of(spec)
+    x = torch.empty(N, T, M, device=spec.device, dtype=_f32)
+    check(L.sbk_filterbank(ptr(spec), N, T, Fd, None, None, None, None, ptr(mat), M, 0, multiplier, db_offset, amin,
+                           ptr(x), None, s), "sbk_filterbank(recompute)")
+    dx = torch.empty_like(x)
+    stats = torch.empty(3 * N, device=spec.device, dtype=_f32)
+    check(L.sbk_filterbank_db_bwd(ptr(x), ptr(grad), N, T * M, int(log_mel), multiplier, db_offset, amin, top_db,
+                                  ptr(stats), ptr(dx), s), "sbk_filterbank_db_bwd")
+    matT = mat.t().contiguous()
+    dspec = torch.empty(N, T, Fd, device=spec.device, dtype=_f32)
+    check(L.sbk_filterbank(ptr(dx), N, T, M, None, None, None, None, ptr(matT), Fd, 0, 1.0, 0.0, 0.0, ptr(dspec),
+                           None, s), "sbk_filterbank(dx·matT)")
+    rows = N * T
+    chunk = 256
+    nch = (rows + chunk - 1) // chunk
+    part = torch.empty(nch, Fd * M, device=spec.device, dtype=_f32)
+    check(L.sbk_filterbank_wgrad(ptr(spec), ptr(dx), rows, Fd, M, chunk, ptr(part), s), "sbk_filterbank_wgrad")
+    dmat = torch.empty(Fd, M, device=spec.device, dtype=_f32)
+    check(L.sbk_colsum(ptr(part), nch, Fd * M, ptr(dmat), 0, s), "sbk_colsum")
+    return dspec, dmat
+
+
+@filterbank_dense_bwd.register_fake
+def _(grad, spec, mat, log_mel, multiplier, db_offset, amin, top_db):
+    return spec.new_empty(spec.shape), mat.new_empty(mat.shape)
+
+
+def _fbd_setup(ctx, inputs, output):
+    spec, mat, log_mel, mult, off, amin, top_db = inputs
+    ctx.save_for_backward(spec, mat)
+    ctx.args = (log_mel, mult, off, amin, top_db)
+
+
+def _fbd_backward(ctx, grad):
+    spec, mat = ctx.saved_tensors
+    dspec, dmat = filterbank_dense_bwd(grad, spec, mat, *ctx.args)
+    return (dspec if ctx.needs_input_grad[0] else None, dmat if ctx.needs_input_grad[1] else None,
+            None, None, None, None, None)
+
+
+filterbank_dense.register_autograd(_fbd_backward, setup_context=_fbd_setup)
+
+
+def _dct_setup(ctx, inputs, output):
+    ctx.save_for_backward(inputs[1])
+
+
+def _dct_backward(ctx, grad):
+    """y = x·D is linear: dx = g·Dᵀ on the same kernel (the DCT matrix is a
+    fixed buffer in the reference, so it gets no gradient)."""
+    (mat,) = ctx.saved_tensors
+    return dct(grad, mat.t().contiguous()), None
+
+
+dct.register_autograd(_dct_backward, setup_context=_dct_setup)

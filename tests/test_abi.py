@@ -102,3 +102,31 @@ def test_feature_module_attributes():
     with pytest.raises(ValueError):
         DCT(input_size=10, n_out=20)
     assert ContextWindow(2, 3).context_len == 6
+
+
+def test_fp16_autocast_raises_not_bf16():
+    """fp16 autocast (the reference's --auto_mix_prec) has no kernels: the
+    modules raise instead of silently computing in bf16."""
+    import pytest
+    import torch
+    from speechbrain_amd import _enc
+    prev = (torch.is_autocast_enabled("cuda"), torch.get_autocast_dtype("cuda"))
+    try:
+        torch.set_autocast_enabled("cuda", True)
+        torch.set_autocast_dtype("cuda", torch.float16)
+        with pytest.raises(NotImplementedError):
+            _enc.compute_dtype()
+        torch.set_autocast_dtype("cuda", torch.bfloat16)
+        assert _enc.compute_dtype() == torch.bfloat16
+    finally:
+        torch.set_autocast_enabled("cuda", prev[0])
+        torch.set_autocast_dtype("cuda", prev[1])
+    assert _enc.compute_dtype() == torch.float32
+
+
+def test_brain_rejects_fp16_amp():
+    import pytest
+    from speechbrain_amd.core import Brain
+    with pytest.raises(NotImplementedError):
+        Brain(modules={}, run_opts={"device": "cpu", "auto_mix_prec": "fp16"})
+    assert Brain(modules={}, run_opts={"device": "cpu", "auto_mix_prec": True}).amp_dtype is not None

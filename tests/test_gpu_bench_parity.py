@@ -1,0 +1,72 @@
+"""The exact path bench.py times — Fbank (fused spectrum kernel + top_db
+clamp) → both ConvBlocks in the fused bf16 frontend2 kernel →
+TransformerASR.encode under bf16 autocast (fused FFN, conv-module and LDS-DMA
+rel-pos attention kernels), eager and HIP-graph replayed — against the fp32
+CPU oracle (oracle/conformer.py, pinned to the reference's fixtures) on full
+15 s utterances with the bench's seeded weights.
+
+Tolerance: derived, not hand-picked.  The same oracle is
+run under torch.autocast("cpu", dtype=bfloat16), which rounds every GEMM /
+convolution operand to bf16 (fp32 accumulate) — the rounding a bf16 MFMA
+implementation cannot avoid.  Its deviation from the fp32 oracle, e_emu, sets
+the scale; the HIP path must stay within FACTOR·e_emu in both max and mean
+absolute error.  Observed values are printed (pytest -s) and recorded in
+DESIGN.md §4."""
+import os
+
+import pytest
+import torch
+
+import oracle.conformer as OC
+
+pytestmark = pytest.mark.gpu
+
+FACTOR = 1.5
+
+
+def _oracle(wav, wav_len, sd_cnn, sd_tr, bf16):
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    with torch.no_grad():
+        if bf16:
+            with torch.autocast("cpu", dtype=torch.bfloat16):
+                return OC.fbank_to_encoder(wav, sd_cnn, sd_tr, 12, 4, n_mels=80, wav_len=wav_len).float()
+        return OC.fbank_to_encoder(wav, sd_cnn, sd_tr, 12, 4, n_mels=80, wav_len=wav_len)
+
+
+@pytest.mark.parametrize("lens", [(1.0, 1.0), (1.0, 0.73)])
+def test_bench_step_vs_fp32_oracle(dev, lens):
+    import bench
+    fbank, cnn, tr = bench.build_model(256, dev)
+    g = torch.Generator().manual_seed(1234)
+    wav = 0.1 * torch.randn(2, int(bench.SR * bench.SECONDS), generator=g)
+    wav_len = torch.tensor(lens)
+    wd, ld = wav.to(dev), wav_len.to(dev)
+    step = bench.make_step(fbank, cnn, tr, wd, ld)
+    out = step().float()
+    # graph replay (what the bench times) gives the same bits as eager
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step()
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        gout = step()
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(gout.float(), out)
+    out = out.cpu()
+
+    sd_cnn = {k: v.cpu() for k, v in cnn.state_dict().items()}
+    sd_tr = {k: v.cpu() for k, v in tr.state_dict().items()}
+    ref = _oracle(wav, wav_len, sd_cnn, sd_tr, False)
+    emu = _oracle(wav, wav_len, sd_cnn, sd_tr, True)
+    assert out.shape == ref.shape == (2, 376, 256)
+    # every frame is compared, padded ones included (they are still encoded)
+    e_hip = (out - ref).abs()
+    e_emu = (emu - ref).abs()
+    print(f"\nbench-path parity lens={lens}: HIP bf16 vs fp32 oracle max {e_hip.max():.4e} mean {e_hip.mean():.4e}; "
+          f"bf16-operand oracle vs fp32 oracle max {e_emu.max():.4e} mean {e_emu.mean():.4e}")
+    assert torch.isfinite(out).all()
+    assert float(e_hip.max()) <= FACTOR * float(e_emu.max())
+    assert float(e_hip.mean()) <= FACTOR * float(e_emu.mean())

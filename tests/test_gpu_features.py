@@ -167,3 +167,75 @@ def test_fbank_full_size_properties(dev):
     assert_close(out[:2], ref, name="full")
     one = fb(wav[5:6].to(dev))
     assert torch.equal(one[0], out[5])  # per-utterance top_db: batch-invariant, bit-exact
+
+
+def _rel_max(a, b):
+    a = a.detach().double().cpu() if isinstance(a, torch.Tensor) else torch.as_tensor(a).double()
+    b = torch.as_tensor(b).double()
+    return float((a - b).abs().max() / b.abs().max().clamp(min=1e-30))
+
+
+def test_learnable_filterbank_backward_vs_golden(golden, dev):
+    """Filterbank(freeze=False) trains: y.sum().backward() gives the reference's
+    own autograd gradients of f_central / band (features.py:476-482; golden
+    fb_learn_grad_fc / fb_learn_grad_band), via the HIP dB/top_db backward,
+    the dense matᵀ product and the chunked matrix-gradient reduction."""
+    F, _ = _mods()
+    g = golden("features")
+    mag = torch.from_numpy(g["mag_p1"]).to(dev)
+    fb = F.Filterbank(n_mels=40, freeze=False).to(dev)
+    y = fb(mag)
+    assert_close(y, g["fb_learn"], name="fwd")
+    y.sum().backward()
+    # tolerance: 1e-4 of the largest gradient (fp32 sums of 8,080 dB terms)
+    assert _rel_max(fb.f_central.grad, g["fb_learn_grad_fc"]) < 1e-4
+    assert _rel_max(fb.band.grad, g["fb_learn_grad_band"]) < 1e-4
+
+
+def test_fbank_requires_grad_trains_filters(golden, dev):
+    """Fbank(requires_grad=True) (lobes/features.py:108-112 → freeze=False): the
+    same pipeline as the golden learnable filterbank, so the same gradients."""
+    _, LF = _mods()
+    g = golden("features")
+    fb = LF.Fbank(n_mels=40, requires_grad=True).to(dev)
+    y = fb(torch.from_numpy(g["x"]).to(dev))
+    assert_close(y, g["fb_learn"], name="fwd")
+    y.sum().backward()
+    assert _rel_max(fb.compute_fbanks.f_central.grad, g["fb_learn_grad_fc"]) < 1e-4
+    assert _rel_max(fb.compute_fbanks.band.grad, g["fb_learn_grad_band"]) < 1e-4
+
+
+def test_filterbank_backward_vs_torch_autograd(dev):
+    """dL/dspec and dL/dmat of the dense filterbank (random weights R, a
+    spectrogram with silent frames so the top_db floor and the amin clamp are
+    both active) against torch autograd of the reference's formula
+    (features.py:551,701-711) in float64 on the CPU."""
+    from speechbrain_amd import ops
+    gen = torch.Generator().manual_seed(3)
+    spec = torch.rand(3, 37, 201, generator=gen) ** 4
+    spec[0, :5] = 0.0            # x < amin → clamp path, zero gradient
+    spec[1] *= 1e-6
+    spec[1, 10] = 1.0            # one loud frame → most of utterance 1 floored at max-80 dB
+    mat = torch.rand(201, 40, generator=gen)
+    R = torch.randn(3, 37, 40, generator=gen)
+    sd, md = spec.to(dev).requires_grad_(), mat.to(dev).requires_grad_()
+    y = ops.filterbank_dense(sd, md, True, 10.0, 0.0, 1e-10, 80.0)
+    (y * R.to(dev)).sum().backward()
+    s64, m64 = spec.double().requires_grad_(), mat.double().requires_grad_()
+    x_db = 10.0 * torch.log10(torch.clamp(s64 @ m64, min=1e-10))
+    ref = torch.max(x_db, (x_db.amax(dim=(-2, -1)) - 80.0).view(3, 1, 1))
+    (ref * R.double()).sum().backward()
+    assert float((y.detach().cpu().double() - ref.detach()).abs().max()) < 1e-3
+    assert _rel_max(sd.grad, s64.grad) < 1e-4
+    assert _rel_max(md.grad, m64.grad) < 1e-4
+
+
+def test_dct_backward(dev):
+    F, _ = _mods()
+    gen = torch.Generator().manual_seed(4)
+    x = torch.randn(2, 11, 23, generator=gen)
+    R = torch.randn(2, 11, 20, generator=gen)
+    d = F.DCT(input_size=23, n_out=20)
+    xd = x.to(dev).requires_grad_()
+    (d(xd) * R.to(dev)).sum().backward()
+    assert _rel_max(xd.grad, R @ d.dct_mat.t()) < 1e-5

@@ -134,3 +134,98 @@ def test_full_size_config4(dev):
         # move a gradient by that much relative; small cases are checked at
         # 1e-5..1e-6 above.
         assert_close(x.grad[b:b + 1, :, :ulen[b] + 1], ref_g[:, :, :ulen[b] + 1], rtol=5e-4, name=f"grad{b}")
+
+
+def _fd_nll(lp, labels, Tl, Ul, b, idx, eps=1e-4):
+    """Central difference of the brute-force -log P (float64) of utterance b
+    wrt one log-prob entry (entries perturbed as free inputs)."""
+    a = lp[b].copy()
+    a[idx] += eps
+    hi = OR.brute_force_nll(a, labels[b], Tl[b], Ul[b], 0)
+    a[idx] -= 2 * eps
+    lo = OR.brute_force_nll(a, labels[b], Tl[b], Ul[b], 0)
+    return (hi - lo) / (2 * eps)
+
+
+def test_numba_mode_grads_vs_finite_differences(dev):
+    """Transducer.apply gradients (the reference's cu_kernel_compute_grad
+    contract, transducer_loss.py:183-236: un-normalised d(-log P)/d lp, not
+    divided by T or B) against central differences of the brute-force path
+    sum — independent of the oracle's α/β gradient restatement.  Every lattice
+    cell's blank and label entry of both utterances is checked, plus entries
+    that must get exactly zero gradient (other vocab, cells outside T_b/U_b)."""
+    from speechbrain_amd.nnet.loss.transducer_loss import Transducer
+    logits, labels, Tl, Ul = _case(33, B=2, T=5, U=3, V=6)
+    Tl = np.array([5, 4], np.int32)
+    Ul = np.array([3, 2], np.int32)
+    lp = OR.log_softmax(logits.astype(np.float64))
+    x = torch.from_numpy(lp.astype(np.float32)).to(dev).requires_grad_()
+    loss = Transducer.apply(x, torch.from_numpy(labels).to(dev), torch.from_numpy(Tl).to(dev),
+                            torch.from_numpy(Ul).to(dev), 0, "sum")
+    loss.backward()
+    g = x.grad.cpu().numpy().astype(np.float64)
+    checked = 0
+    for b in range(2):
+        for t in range(Tl[b]):
+            for u in range(Ul[b] + 1):
+                entries = [0] + ([int(labels[b, u])] if u < Ul[b] else [])
+                for v in entries:
+                    fd = _fd_nll(lp, labels, Tl, Ul, b, (t, u, v))
+                    assert abs(g[b, t, u, v] - fd) <= 2e-5 * max(1.0, abs(fd)), (b, t, u, v, g[b, t, u, v], fd)
+                    checked += 1
+                others = [v for v in range(6) if v not in entries]
+                assert np.all(g[b, t, u, others] == 0.0)
+        assert np.all(g[b, Tl[b]:] == 0.0) and np.all(g[b, :, Ul[b] + 1:] == 0.0)
+    assert checked > 40
+    # the loss itself: -log P / T_b summed (Numba semantics)
+    nll = [OR.brute_force_nll(lp[b], labels[b], Tl[b], Ul[b], 0) for b in range(2)]
+    assert abs(loss.item() - sum(n / t for n, t in zip(nll, Tl))) < 1e-5
+
+
+def test_numba_mode_logit_grads_vs_finite_differences(dev):
+    """transducer_loss(use_torchaudio=False) gradient wrt the logits (the
+    wrapper's log_softmax chained, losses.py:79-85) against central
+    differences of brute-force -log P over perturbed logits."""
+    from speechbrain_amd.nnet.losses import transducer_loss
+    logits, labels, _, _ = _case(34, B=1, T=4, U=2, V=5)
+    x = torch.from_numpy(logits).to(dev).requires_grad_()
+    loss = transducer_loss(x, torch.from_numpy(labels).to(dev), torch.ones(1, device=dev),
+                           torch.ones(1, device=dev), 0, use_torchaudio=False)
+    loss.backward()
+    g = x.grad.cpu().numpy()
+    eps = 1e-4
+    base = logits.astype(np.float64)
+    for t in range(4):
+        for u in range(3):
+            for v in range(5):
+                a = base.copy()
+                a[0, t, u, v] += eps
+                hi = OR.brute_force_nll(OR.log_softmax(a)[0], labels[0], 4, 2, 0)
+                a[0, t, u, v] -= 2 * eps
+                lo = OR.brute_force_nll(OR.log_softmax(a)[0], labels[0], 4, 2, 0)
+                fd = (hi - lo) / (2 * eps)
+                assert abs(g[0, t, u, v] - fd) <= 2e-5 * max(1.0, abs(fd)), (t, u, v, g[0, t, u, v], fd)
+
+
+def test_invalid_lengths_and_labels_give_nan_not_corruption(dev):
+    """lengths outside the lattice (U_b > U1-1, T_b > maxT, T_b = 0)
+    or labels outside [0, V) poison that utterance's loss with NaN; the other
+    utterances of the batch are unaffected (no write outside a slab)."""
+    from speechbrain_amd.nnet.loss.transducer_loss import Transducer
+    logits, labels, Tl, Ul = _case(40, B=3, T=6, U=3, V=5)
+    lp = OR.log_softmax(logits.astype(np.float64)).astype(np.float32)
+    good_loss, _, _, _ = OR.transducer_forward(lp, labels, Tl, Ul, 0, "none")
+    for bad in ("U", "T", "T0", "label"):
+        Tb, Ub, lab = Tl.copy(), Ul.copy(), labels.copy()
+        if bad == "U":
+            Ub[1] = 9
+        elif bad == "T":
+            Tb[1] = 7
+        elif bad == "T0":
+            Tb[1] = 0
+        else:
+            lab[1, 0] = 5
+        out = Transducer.apply(torch.from_numpy(lp).to(dev), torch.from_numpy(lab).to(dev),
+                               torch.from_numpy(Tb).to(dev), torch.from_numpy(Ub).to(dev), 0, "none").cpu().numpy()
+        assert np.isnan(out[1]), (bad, out)
+        assert_close(out[[0, 2]], np.asarray(good_loss)[[0, 2]], rtol=1e-6, name=bad)
