@@ -177,7 +177,11 @@ class Filterbank(torch.nn.Module):
         bd = band.unsqueeze(1)
         if self.filter_shape == "triangular":
             slope = (f - fc) / bd
-            m = torch.clamp(torch.minimum(slope + 1.0, -slope + 1.0), min=0.0)
+            # torch.max against a zero tensor (not clamp): at a filter edge
+            # slope = ±1 exactly (the first filter at 0 Hz) the reference's
+            # maximum splits the gradient in half, clamp would pass it whole
+            zero = torch.zeros(1, device=f.device)
+            m = torch.max(zero, torch.min(slope + 1.0, -slope + 1.0))
         elif self.filter_shape == "rectangular":
             m = ((f >= fc - bd) & (f <= fc + bd)).float()
         else:

@@ -21,7 +21,7 @@ import oracle.conformer as OC
 
 pytestmark = pytest.mark.gpu
 
-FACTOR = 1.5
+FACTOR = 1.0  # observed r02: HIP max 0.018 / mean 0.0036 vs e_emu 0.046-0.049 / 0.0067-0.0068
 
 
 def _oracle(wav, wav_len, sd_cnn, sd_tr, bf16):
