@@ -2,6 +2,8 @@
 conformer.hip, attention.hip).  Direct ctypes calls — no Python compute, no
 fallback; used by the nn.Module drop-ins and capturable into HIP graphs
 (no host sync, no allocation outside torch's caching allocator)."""
+from typing import Optional
+
 import torch
 
 from ._lib import check, lib, ptr, require_device, stream_of
@@ -15,60 +17,107 @@ def _is_bf16(t):
     return t.dtype == _bf16
 
 
+# ---------------------------------------------------------------------------
+# torch.library custom ops (sbk::*): every encoder kernel is a dispatcher op,
+# so torch.jit.trace / torch.compile record the launches as graph nodes
+# (instead of baking ctypes results in as constants) and HIP-graph capture
+# sees ordinary stream work.  The Python wrappers below keep the call
+# signatures the modules use.  Optional outputs are returned as 0-element
+# tensors by the ops and mapped back to None by the wrappers.
+# ---------------------------------------------------------------------------
+@torch.library.custom_op("sbk::gemm", mutates_args=())
+def _gemm_op(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], act: int, slope: float,
+             res: Optional[torch.Tensor], alpha: float, rowmask: Optional[torch.Tensor], out_bf16: bool,
+             tile: int) -> torch.Tensor:
+    M, K = a.shape
+    N = w.shape[0]
+    n_out = N // 2 if act == 2 else N
+    out = torch.empty(M, n_out, device=a.device, dtype=_bf16 if out_bf16 else _f32)
+    rc = lib().sbk_gemm(int(_is_bf16(a)), ptr(a), a.stride(0), ptr(w), w.stride(0), M, N, K, ptr(bias), act,
+                        float(slope), ptr(res), res.stride(0) if res is not None else 0, float(alpha),
+                        ptr(rowmask), ptr(out), out.stride(0), int(out_bf16), int(tile), stream_of(a))
+    check(rc, "sbk_gemm")
+    return out
+
+
+@_gemm_op.register_fake
+def _(a, w, bias, act, slope, res, alpha, rowmask, out_bf16, tile):
+    n = w.shape[0] // 2 if act == 2 else w.shape[0]
+    return a.new_empty(a.shape[0], n, dtype=_bf16 if out_bf16 else _f32)
+
+
 def gemm(a, w, bias=None, act=None, slope=0.0, res=None, alpha=1.0, rowmask=None, out=None,
          out_dtype=_f32, tile=0):
     """out = res + alpha * act(a @ w.T + bias), rows with rowmask -> 0 before the
     residual.  a: (M, K), w: (N, K), both bf16 or both fp32."""
     require_device(a, w)
+    if out is not None:
+        raise ValueError("gemm allocates its output (out= is not supported)")
     if a.dtype != w.dtype:
         raise TypeError(f"gemm operand dtypes differ: {a.dtype} vs {w.dtype}")
     if a.stride(-1) != 1 or w.stride(-1) != 1:
         raise ValueError("gemm operands must be K-contiguous")
-    M, K = a.shape
-    N = w.shape[0]
-    code = ACT[act]
-    n_out = N // 2 if code == 2 else N
-    if out is None:
-        out = torch.empty(M, n_out, device=a.device, dtype=out_dtype)
     if res is not None and (res.dtype != _f32 or res.stride(-1) != 1):
         raise ValueError("residual must be fp32, row-contiguous")
-    rc = lib().sbk_gemm(int(_is_bf16(a)), ptr(a), a.stride(0), ptr(w), w.stride(0), M, N, K, ptr(bias), code,
-                        float(slope), ptr(res), res.stride(0) if res is not None else 0, float(alpha),
-                        ptr(rowmask), ptr(out), out.stride(0), int(out.dtype == _bf16), int(tile), stream_of(a))
-    check(rc, "sbk_gemm")
+    return torch.ops.sbk.gemm(a, w, bias, ACT[act], float(slope), res, float(alpha), rowmask,
+                              out_dtype == _bf16, int(tile))
+
+
+@torch.library.custom_op("sbk::length_mask", mutates_args=())
+def _length_mask_op(rel_len: torch.Tensor, T: int) -> torch.Tensor:
+    B = rel_len.shape[0]
+    out = torch.empty(B, T, device=rel_len.device, dtype=torch.uint8)
+    check(lib().sbk_length_mask(ptr(rel_len), B, int(T), ptr(out), stream_of(rel_len)), "sbk_length_mask")
     return out
+
+
+@_length_mask_op.register_fake
+def _(rel_len, T):
+    return rel_len.new_empty(rel_len.shape[0], T, dtype=torch.uint8)
 
 
 def length_mask(rel_len, T):
     """(B, T) uint8: t > floor(rel_len[b] * T) — one launch."""
     require_device(rel_len)
     rl = rel_len if (rel_len.dtype == _f32 and rel_len.is_contiguous()) else rel_len.float().contiguous()
-    B = rl.shape[0]
-    out = torch.empty(B, T, device=rl.device, dtype=torch.uint8)
-    check(lib().sbk_length_mask(ptr(rl), B, int(T), ptr(out), stream_of(rl)), "sbk_length_mask")
-    return out
+    return torch.ops.sbk.length_mask(rl, int(T))
+
+
+@torch.library.custom_op("sbk::gemm_ln", mutates_args=())
+def _gemm_ln_op(a: torch.Tensor, w: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float,
+                bias: Optional[torch.Tensor], res: Optional[torch.Tensor], alpha: float,
+                rowmask: Optional[torch.Tensor], u_bf16: bool, tile: int) -> tuple[torch.Tensor, torch.Tensor]:
+    M, K = a.shape
+    N = w.shape[0]
+    out = torch.empty(M, N, device=a.device, dtype=_f32)
+    u = torch.empty(M, N, device=a.device, dtype=_bf16 if u_bf16 else _f32)
+    rc = lib().sbk_gemm_ln(int(_is_bf16(a)), ptr(a), a.stride(0), ptr(w), w.stride(0), M, N, K, ptr(bias), ptr(res),
+                           res.stride(0) if res is not None else 0, float(alpha), ptr(rowmask), ptr(out),
+                           out.stride(0), ptr(g), ptr(b), float(eps), ptr(u), u.stride(0), int(u_bf16),
+                           int(tile), stream_of(a))
+    check(rc, "sbk_gemm_ln")
+    return out, u
+
+
+@_gemm_ln_op.register_fake
+def _(a, w, g, b, eps, bias, res, alpha, rowmask, u_bf16, tile):
+    return (a.new_empty(a.shape[0], w.shape[0], dtype=_f32),
+            a.new_empty(a.shape[0], w.shape[0], dtype=_bf16 if u_bf16 else _f32))
 
 
 def gemm_ln(a, w, ln, bias=None, res=None, alpha=1.0, rowmask=None, out=None, u_dtype=_bf16, tile=0):
     """out = res + alpha * (a @ w.T + bias) (fp32) and u = LN(out; *ln) in one
     launch (N == 256).  Returns (out, u)."""
     require_device(a, w)
+    if out is not None:
+        raise ValueError("gemm_ln allocates its output (out= is not supported)")
     if a.dtype != w.dtype:
         raise TypeError(f"gemm operand dtypes differ: {a.dtype} vs {w.dtype}")
-    M, K = a.shape
-    N = w.shape[0]
-    if out is None:
-        out = torch.empty(M, N, device=a.device, dtype=_f32)
-    u = torch.empty(M, N, device=a.device, dtype=u_dtype)
     if res is not None and (res.dtype != _f32 or res.stride(-1) != 1):
         raise ValueError("residual must be fp32, row-contiguous")
     g, b, eps = ln
-    rc = lib().sbk_gemm_ln(int(_is_bf16(a)), ptr(a), a.stride(0), ptr(w), w.stride(0), M, N, K, ptr(bias), ptr(res),
-                           res.stride(0) if res is not None else 0, float(alpha), ptr(rowmask), ptr(out),
-                           out.stride(0), ptr(g), ptr(b), float(eps), ptr(u), u.stride(0), int(u_dtype == _bf16),
-                           int(tile), stream_of(a))
-    check(rc, "sbk_gemm_ln")
-    return out, u
+    return torch.ops.sbk.gemm_ln(a, w, g, b, float(eps), bias, res, float(alpha), rowmask, u_dtype == _bf16,
+                                 int(tile))
 
 
 # The fused projection + LayerNorm (sbk_gemm_ln) measures the same as the two
@@ -80,99 +129,208 @@ def gemm_ln_supported(N):
     return int(N) == 256
 
 
+@torch.library.custom_op("sbk::layernorm", mutates_args=())
+def _layernorm_op(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, eps1: float, out1_mode: int,
+                  w2: Optional[torch.Tensor], b2: Optional[torch.Tensor], eps2: float,
+                  out2_bf16: bool) -> tuple[torch.Tensor, torch.Tensor]:
+    """out1_mode: 0 no first output, 1 fp32, 2 bf16."""
+    M, D = x.shape
+    out1 = torch.empty(M, D, device=x.device, dtype=_bf16 if out1_mode == 2 else _f32) if out1_mode else None
+    out2 = torch.empty(M, D, device=x.device, dtype=_bf16 if out2_bf16 else _f32) if w2 is not None else None
+    rc = lib().sbk_layernorm(ptr(x), M, D, ptr(w1), ptr(b1), float(eps1), ptr(out1), int(out1_mode == 2),
+                             ptr(w2), ptr(b2), float(eps2), ptr(out2), int(out2 is not None and out2_bf16),
+                             stream_of(x))
+    check(rc, "sbk_layernorm")
+    e = x.new_empty(0)
+    return (out1 if out1 is not None else e), (out2 if out2 is not None else e)
+
+
+@_layernorm_op.register_fake
+def _(x, w1, b1, eps1, out1_mode, w2, b2, eps2, out2_bf16):
+    o1 = x.new_empty(x.shape, dtype=_bf16 if out1_mode == 2 else _f32) if out1_mode else x.new_empty(0)
+    o2 = x.new_empty(x.shape, dtype=_bf16 if out2_bf16 else _f32) if w2 is not None else x.new_empty(0)
+    return o1, o2
+
+
 def layernorm(x, w1, b1, eps1, out1_dtype=_f32, w2=None, b2=None, eps2=1e-5, out2_dtype=_bf16, out1=None):
     """y1 = LN(x; w1, b1) (returned unless out1_dtype is None); optionally
     y2 = LN(y1; w2, b2) in one pass.  x: (M, D) fp32."""
     require_device(x)
-    M, D = x.shape
-    if out1 is None and out1_dtype is not None:
-        out1 = torch.empty(M, D, device=x.device, dtype=out1_dtype)
-    out2 = torch.empty(M, D, device=x.device, dtype=out2_dtype) if w2 is not None else None
-    rc = lib().sbk_layernorm(ptr(x), M, D, ptr(w1), ptr(b1), float(eps1), ptr(out1),
-                             int(out1 is not None and out1.dtype == _bf16), ptr(w2), ptr(b2), float(eps2), ptr(out2),
-                             int(out2 is not None and out2.dtype == _bf16), stream_of(x))
-    check(rc, "sbk_layernorm")
-    return out1, out2
+    if out1 is not None:
+        raise ValueError("layernorm allocates its output (out1= is not supported)")
+    mode = 0 if out1_dtype is None else (2 if out1_dtype == _bf16 else 1)
+    y1, y2 = torch.ops.sbk.layernorm(x, w1, b1, float(eps1), mode, w2, b2, float(eps2), out2_dtype == _bf16)
+    return (y1 if mode else None), (y2 if w2 is not None else None)
 
 
 def ffn_supported(D, H):
     return bool(lib().sbk_ffn_supported(int(D), int(H)))
 
 
+@torch.library.custom_op("sbk::ffn", mutates_args=())
+def _ffn_op(x: torch.Tensor, g0: torch.Tensor, b0: torch.Tensor, e0: float, w1: torch.Tensor, b1: torch.Tensor,
+            act: int, slope: float, w2: torch.Tensor, b2: torch.Tensor, alpha: float, gp: Optional[torch.Tensor],
+            bp: Optional[torch.Tensor], ep: float, gn: Optional[torch.Tensor], bn: Optional[torch.Tensor], en: float,
+            next_bf16: bool) -> tuple[torch.Tensor, torch.Tensor]:
+    M, D = x.shape
+    H = w1.shape[0]
+    out = torch.empty_like(x)
+    u = torch.empty(M, D, device=x.device, dtype=_bf16 if next_bf16 else _f32) if gn is not None else None
+    rc = lib().sbk_ffn(ptr(x), M, D, H, ptr(g0), ptr(b0), float(e0), ptr(w1), ptr(b1), act, float(slope), ptr(w2),
+                       ptr(b2), float(alpha), ptr(gp), ptr(bp), float(ep), ptr(out), ptr(gn), ptr(bn), float(en),
+                       ptr(u), int(next_bf16), stream_of(x))
+    check(rc, "sbk_ffn")
+    return out, (u if u is not None else x.new_empty(0))
+
+
+@_ffn_op.register_fake
+def _(x, g0, b0, e0, w1, b1, act, slope, w2, b2, alpha, gp, bp, ep, gn, bn, en, next_bf16):
+    return (torch.empty_like(x),
+            x.new_empty(x.shape, dtype=_bf16 if next_bf16 else _f32) if gn is not None else x.new_empty(0))
+
+
 def ffn(x, ln0, w1, b1, act, slope, w2, b2, alpha, post_ln=None, next_ln=None, next_dtype=_bf16, out=None):
     """Fused macaron FFN block (bf16 MFMA): z = x + alpha * FFN(LN0(x));
     out = post_ln(z) if given; u = next_ln(out) (returned) if given.
     x: (M, D) fp32; ln*: (weight, bias, eps); w1 (H, D), w2 (D, H) bf16.
-    `out` may alias x."""
+    `out` is accepted for API compatibility and ignored (a new tensor is
+    returned; the op does not alias its input)."""
     require_device(x, w1, w2)
-    M, D = x.shape
-    H = w1.shape[0]
-    if out is None:
-        out = torch.empty_like(x)
-    u = torch.empty(M, D, device=x.device, dtype=next_dtype) if next_ln is not None else None
     gp, bp, ep = post_ln if post_ln is not None else (None, None, 0.0)
     gn, bn, en = next_ln if next_ln is not None else (None, None, 0.0)
-    rc = lib().sbk_ffn(ptr(x), M, D, H, ptr(ln0[0]), ptr(ln0[1]), float(ln0[2]), ptr(w1), ptr(b1), ACT[act],
-                       float(slope), ptr(w2), ptr(b2), float(alpha), ptr(gp), ptr(bp), float(ep), ptr(out),
-                       ptr(gn), ptr(bn), float(en), ptr(u), int(next_dtype == _bf16), stream_of(x))
-    check(rc, "sbk_ffn")
-    return out, u
+    y, u = torch.ops.sbk.ffn(x, ln0[0], ln0[1], float(ln0[2]), w1, b1, ACT[act], float(slope), w2, b2, float(alpha),
+                             gp, bp, float(ep), gn, bn, float(en), next_dtype == _bf16)
+    return y, (u if next_ln is not None else None)
+
+
+@torch.library.custom_op("sbk::dwconv_ln_swish", mutates_args=())
+def _dwconv_op(x: torch.Tensor, B: int, T: int, w: torch.Tensor, bias: Optional[torch.Tensor], causal: bool,
+               ln_w: torch.Tensor, ln_b: torch.Tensor, eps: float, out_bf16: bool) -> torch.Tensor:
+    C = x.shape[-1]
+    K = w.shape[-1]
+    out = torch.empty(B * T, C, device=x.device, dtype=_bf16 if out_bf16 else _f32)
+    rc = lib().sbk_dwconv_ln_swish(int(_is_bf16(x)), ptr(x), B, T, C, ptr(w), ptr(bias), K, int(causal), ptr(ln_w),
+                                   ptr(ln_b), float(eps), ptr(out), int(out_bf16), stream_of(x))
+    check(rc, "sbk_dwconv_ln_swish")
+    return out
+
+
+@_dwconv_op.register_fake
+def _(x, B, T, w, bias, causal, ln_w, ln_b, eps, out_bf16):
+    return x.new_empty(B * T, x.shape[-1], dtype=_bf16 if out_bf16 else _f32)
 
 
 def dwconv_ln_swish(x, B, T, w, bias, causal, ln_w, ln_b, eps, out_dtype):
     """Depthwise Conv1d over time + LayerNorm(C) + Swish.  x: (B*T, C)."""
-    C = x.shape[-1]
-    K = w.shape[-1]
-    out = torch.empty(B * T, C, device=x.device, dtype=out_dtype)
-    rc = lib().sbk_dwconv_ln_swish(int(_is_bf16(x)), ptr(x), B, T, C, ptr(w), ptr(bias), K, int(causal), ptr(ln_w),
-                                   ptr(ln_b), float(eps), ptr(out), int(out_dtype == _bf16), stream_of(x))
-    check(rc, "sbk_dwconv_ln_swish")
-    return out
+    return torch.ops.sbk.dwconv_ln_swish(x, int(B), int(T), w, bias, bool(causal), ln_w, ln_b, float(eps),
+                                         out_dtype == _bf16)
 
 
 def conv_module_supported(D, K):
     return bool(lib().sbk_conv_module_supported(int(D), int(K)))
 
 
+@torch.library.custom_op("sbk::conv_module", mutates_args=())
+def _conv_module_op(x: torch.Tensor, B: int, T: int, g0: torch.Tensor, b0: torch.Tensor, e0: float,
+                    w1p: torch.Tensor, b1p: torch.Tensor, wc: torch.Tensor, bc: Optional[torch.Tensor], causal: bool,
+                    g1: torch.Tensor, b1: torch.Tensor, e1: float, w2: torch.Tensor, b2: Optional[torch.Tensor],
+                    kpm: Optional[torch.Tensor]) -> torch.Tensor:
+    K = wc.shape[0]  # wc: (K, d) tap-major
+    out = torch.empty_like(x)
+    rc = lib().sbk_conv_module(ptr(x), ptr(out), B, T, x.shape[1], ptr(g0), ptr(b0), float(e0), ptr(w1p), ptr(b1p),
+                               ptr(wc), ptr(bc), K, int(causal), ptr(g1), ptr(b1), float(e1), ptr(w2), ptr(b2),
+                               ptr(kpm), stream_of(x))
+    check(rc, "sbk_conv_module")
+    return out
+
+
+@_conv_module_op.register_fake
+def _(x, B, T, g0, b0, e0, w1p, b1p, wc, bc, causal, g1, b1, e1, w2, b2, kpm):
+    return torch.empty_like(x)
+
+
 def conv_module(x, B, T, ln0, w1p, b1p, wc, bc, causal, ln1, w2, b2, kpm=None):
     """Fused Conformer convolution module (bf16 MFMA, one launch):
     x + rowmask0(after_conv(dwconv(GLU(pointwise(LN0(x)))))).  x: (B*T, 256) fp32."""
     require_device(x, w1p, w2)
-    K = wc.shape[0]  # wc: (K, d) tap-major
-    out = torch.empty_like(x)
-    rc = lib().sbk_conv_module(ptr(x), ptr(out), B, T, x.shape[1], ptr(ln0[0]), ptr(ln0[1]), float(ln0[2]), ptr(w1p),
-                               ptr(b1p), ptr(wc), ptr(bc), K, int(causal), ptr(ln1[0]), ptr(ln1[1]), float(ln1[2]),
-                               ptr(w2), ptr(b2), ptr(kpm), stream_of(x))
-    check(rc, "sbk_conv_module")
+    return torch.ops.sbk.conv_module(x, int(B), int(T), ln0[0], ln0[1], float(ln0[2]), w1p, b1p, wc, bc,
+                                     bool(causal), ln1[0], ln1[1], float(ln1[2]), w2, b2, kpm)
+
+
+@torch.library.custom_op("sbk::conv_block_c1", mutates_args=())
+def _conv_block_c1_op(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, ln_w: torch.Tensor, ln_b: torch.Tensor,
+                      eps: float, slope: float, out_bf16: bool) -> torch.Tensor:
+    B, Tin, Fin = x.shape
+    Cout = w.shape[0]
+    Tout, Fout = (Tin - 1) // 2 + 1, (Fin - 1) // 2 + 1
+    out = torch.empty(B, Tout, Fout, Cout, device=x.device, dtype=_bf16 if out_bf16 else _f32)
+    rc = lib().sbk_conv_block_c1(ptr(x), B, Tin, Fin, Cout, ptr(w), ptr(bias), ptr(ln_w), ptr(ln_b), float(eps),
+                                 float(slope), ptr(out), int(out_bf16), None, None, stream_of(x))
+    check(rc, "sbk_conv_block_c1")
     return out
+
+
+@_conv_block_c1_op.register_fake
+def _(x, w, bias, ln_w, ln_b, eps, slope, out_bf16):
+    B, Tin, Fin = x.shape
+    return x.new_empty(B, (Tin - 1) // 2 + 1, (Fin - 1) // 2 + 1, w.shape[0], dtype=_bf16 if out_bf16 else _f32)
 
 
 def conv_block_c1(x, w, bias, ln_w, ln_b, eps, slope, out_dtype):
     """ConvBlock with one input channel: x (B, T, F) fp32 → (B, T', F', C)."""
     require_device(x)
-    B, Tin, Fin = x.shape
-    Cout = w.shape[0]
+    return torch.ops.sbk.conv_block_c1(x, w, bias, ln_w, ln_b, float(eps), float(slope), out_dtype == _bf16)
+
+
+@torch.library.custom_op("sbk::conv_block_mfma", mutates_args=())
+def _conv_block_mfma_op(x: torch.Tensor, wperm: torch.Tensor, bias: torch.Tensor, ln_w: torch.Tensor,
+                        ln_b: torch.Tensor, eps: float, slope: float, out_bf16: bool) -> torch.Tensor:
+    B, Tin, Fin, Cin = x.shape
+    Cout = wperm.shape[0]
     Tout, Fout = (Tin - 1) // 2 + 1, (Fin - 1) // 2 + 1
-    out = torch.empty(B, Tout, Fout, Cout, device=x.device, dtype=out_dtype)
-    rc = lib().sbk_conv_block_c1(ptr(x), B, Tin, Fin, Cout, ptr(w), ptr(bias), ptr(ln_w), ptr(ln_b), float(eps),
-                                 float(slope), ptr(out), int(out_dtype == _bf16), None, None, stream_of(x))
-    check(rc, "sbk_conv_block_c1")
+    out = torch.empty(B, Tout, Fout, Cout, device=x.device, dtype=_bf16 if out_bf16 else _f32)
+    rc = lib().sbk_conv_block_mfma(int(_is_bf16(x)), ptr(x), B, Tin, Fin, Cin, Cout, ptr(wperm), ptr(bias),
+                                   ptr(ln_w), ptr(ln_b), float(eps), float(slope), ptr(out), int(out_bf16), None,
+                                   None, stream_of(x))
+    check(rc, "sbk_conv_block_mfma")
     return out
+
+
+@_conv_block_mfma_op.register_fake
+def _(x, wperm, bias, ln_w, ln_b, eps, slope, out_bf16):
+    B, Tin, Fin, _ = x.shape
+    return x.new_empty(B, (Tin - 1) // 2 + 1, (Fin - 1) // 2 + 1, wperm.shape[0],
+                       dtype=_bf16 if out_bf16 else _f32)
 
 
 def conv_block_mfma(x, wperm, bias, ln_w, ln_b, eps, slope, out_dtype):
     """ConvBlock implicit GEMM: x (B, T, F, Cin) → (B, T', F', Cout);
     wperm: (Cout, 3, 3, Cin) [time, freq] in x.dtype."""
     require_device(x, wperm)
-    B, Tin, Fin, Cin = x.shape
-    Cout = wperm.shape[0]
-    Tout, Fout = (Tin - 1) // 2 + 1, (Fin - 1) // 2 + 1
-    out = torch.empty(B, Tout, Fout, Cout, device=x.device, dtype=out_dtype)
-    rc = lib().sbk_conv_block_mfma(int(_is_bf16(x)), ptr(x), B, Tin, Fin, Cin, Cout, ptr(wperm), ptr(bias),
-                                   ptr(ln_w), ptr(ln_b), float(eps), float(slope), ptr(out),
-                                   int(out_dtype == _bf16), None, None, stream_of(x))
-    check(rc, "sbk_conv_block_mfma")
+    return torch.ops.sbk.conv_block_mfma(x, wperm, bias, ln_w, ln_b, float(eps), float(slope), out_dtype == _bf16)
+
+
+@torch.library.custom_op("sbk::conv_frontend2", mutates_args=())
+def _conv_frontend2_op(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, g1: torch.Tensor, be1: torch.Tensor,
+                       e1: float, s1: float, wperm2: torch.Tensor, b2: torch.Tensor, g2: torch.Tensor,
+                       be2: torch.Tensor, e2: float, s2: float, out_bf16: bool) -> torch.Tensor:
+    B, Tin, Fin = x.shape
+    C1, C2 = w1.shape[0], wperm2.shape[0]
+    T1, F1 = (Tin - 1) // 2 + 1, (Fin - 1) // 2 + 1
+    T2, F2 = (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1
+    out = torch.empty(B, T2, F2, C2, device=x.device, dtype=_bf16 if out_bf16 else _f32)
+    rc = lib().sbk_conv_frontend2(int(_is_bf16(wperm2)), ptr(x), B, Tin, Fin, ptr(w1), ptr(b1), ptr(g1), ptr(be1),
+                                  float(e1), float(s1), C1, ptr(wperm2), ptr(b2), ptr(g2), ptr(be2), float(e2),
+                                  float(s2), C2, ptr(out), int(out_bf16), None, None, stream_of(x))
+    check(rc, "sbk_conv_frontend2")
     return out
+
+
+@_conv_frontend2_op.register_fake
+def _(x, w1, b1, g1, be1, e1, s1, wperm2, b2, g2, be2, e2, s2, out_bf16):
+    B, Tin, Fin = x.shape
+    T1, F1 = (Tin - 1) // 2 + 1, (Fin - 1) // 2 + 1
+    return x.new_empty(B, (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1, wperm2.shape[0], dtype=_bf16 if out_bf16 else _f32)
 
 
 def conv_frontend2(x, blk1, blk2, wperm2, out_dtype):
@@ -180,18 +338,30 @@ def conv_frontend2(x, blk1, blk2, wperm2, out_dtype):
     blk*: (conv weight, bias, ln weight, ln bias, ln eps, leaky slope);
     wperm2: block-2 weights (C2, 3, 3, C1) in the compute dtype."""
     require_device(x, wperm2)
-    B, Tin, Fin = x.shape
     w1, b1, g1, be1, e1, s1 = blk1
     _, b2, g2, be2, e2, s2 = blk2
-    C1, C2 = w1.shape[0], wperm2.shape[0]
-    T1, F1 = (Tin - 1) // 2 + 1, (Fin - 1) // 2 + 1
-    T2, F2 = (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1
-    out = torch.empty(B, T2, F2, C2, device=x.device, dtype=out_dtype)
-    rc = lib().sbk_conv_frontend2(int(_is_bf16(wperm2)), ptr(x), B, Tin, Fin, ptr(w1), ptr(b1), ptr(g1), ptr(be1),
-                                  float(e1), float(s1), C1, ptr(wperm2), ptr(b2), ptr(g2), ptr(be2), float(e2),
-                                  float(s2), C2, ptr(out), int(out_dtype == _bf16), None, None, stream_of(x))
-    check(rc, "sbk_conv_frontend2")
-    return out
+    return torch.ops.sbk.conv_frontend2(x, w1, b1, g1, be1, float(e1), float(s1), wperm2, b2, g2, be2, float(e2),
+                                        float(s2), out_dtype == _bf16)
+
+
+@torch.library.custom_op("sbk::relpos_attention", mutates_args=())
+def _relpos_attention_op(qkv: torch.Tensor, pk: torch.Tensor, pbu: torch.Tensor, pbv: torch.Tensor,
+                         kpm: Optional[torch.Tensor], B: int, T: int, H: int, dh: int, scale: float,
+                         need_probs: bool) -> tuple[torch.Tensor, torch.Tensor]:
+    d = H * dh
+    out = torch.empty(B * T, d, device=qkv.device, dtype=qkv.dtype)
+    probs = torch.empty(B, H, T, T, device=qkv.device, dtype=_f32) if need_probs else qkv.new_empty(0, dtype=_f32)
+    rc = lib().sbk_relpos_attention_ld(int(_is_bf16(qkv)), ptr(qkv), ptr(pk), pk.stride(0), ptr(pbu), ptr(pbv),
+                                       ptr(kpm), B, T, H, dh, float(scale), ptr(out),
+                                       ptr(probs) if need_probs else None, stream_of(qkv))
+    check(rc, "sbk_relpos_attention")
+    return out, probs
+
+
+@_relpos_attention_op.register_fake
+def _(qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale, need_probs):
+    return (qkv.new_empty(B * T, H * dh),
+            qkv.new_empty(B, H, T, T, dtype=_f32) if need_probs else qkv.new_empty(0, dtype=_f32))
 
 
 def relpos_attention(qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale, need_probs=False):
@@ -200,12 +370,9 @@ def relpos_attention(qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale, need_probs=Fals
     d = H * dh
     if pk.stride(-1) != 1 or pk.shape[-1] != d:
         raise ValueError("pk must be (2T-1, d) with unit column stride")
-    out = torch.empty(B * T, d, device=qkv.device, dtype=qkv.dtype)
-    probs = torch.empty(B, H, T, T, device=qkv.device, dtype=_f32) if need_probs else None
-    rc = lib().sbk_relpos_attention_ld(int(_is_bf16(qkv)), ptr(qkv), ptr(pk), pk.stride(0), ptr(pbu), ptr(pbv),
-                                       ptr(kpm), B, T, H, dh, float(scale), ptr(out), ptr(probs), stream_of(qkv))
-    check(rc, "sbk_relpos_attention")
-    return out, probs
+    out, probs = torch.ops.sbk.relpos_attention(qkv, pk, pbu, pbv, kpm, int(B), int(T), int(H), int(dh),
+                                                float(scale), bool(need_probs))
+    return out, (probs if need_probs else None)
 
 
 def glu_group():
@@ -213,10 +380,21 @@ def glu_group():
     return int(lib().sbk_gemm_glu_group(1))
 
 
-def cast_bf16(x):
+@torch.library.custom_op("sbk::cast_bf16", mutates_args=())
+def _cast_bf16_op(x: torch.Tensor) -> torch.Tensor:
     out = torch.empty(x.shape, device=x.device, dtype=_bf16)
     check(lib().sbk_cast_bf16(ptr(x), ptr(out), x.numel(), stream_of(x)), "sbk_cast_bf16")
     return out
+
+
+@_cast_bf16_op.register_fake
+def _(x):
+    return x.new_empty(x.shape, dtype=_bf16)
+
+
+def cast_bf16(x):
+    """fp32 → bf16 (round to nearest even), contiguous input."""
+    return torch.ops.sbk.cast_bf16(x)
 
 
 def to_compute(x, dtype):

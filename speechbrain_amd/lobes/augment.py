@@ -8,11 +8,33 @@ device generator.  The warp / mask / mean-fill arithmetic runs in
 speechbrain_amd/csrc/augment.hip; the input is mutated in place and
 returned, as in the reference.
 """
+from typing import Optional
+
 import torch
 
 from .._lib import check, lib, ptr, require_device, stream_of
 
 __all__ = ["SpecAugment"]
+
+
+@torch.library.custom_op("sbk::specaugment_", mutates_args=("x",))
+def specaugment_(x: torch.Tensor, N: int, T: int, F: int, c: int, w: int, fm: Optional[torch.Tensor],
+                 tm: Optional[torch.Tensor], use_mean: bool, n_fcells: int) -> None:
+    """Applies the drawn warp (c, w; -1 = none) and freq / time masks
+    (fm, tm: (N, n, 2) int32 [len, pos]) to x (N, T, F) fp32 in place, with
+    the batch-mean fill when use_mean (augment.py:116-201)."""
+    tmp = torch.empty_like(x) if c >= 0 else None
+    partial = torch.empty(2 * N * ((T + 15) // 16), device=x.device, dtype=torch.float32) if use_mean else None
+    n_f = fm.shape[1] if fm is not None else 0
+    n_t = tm.shape[1] if tm is not None else 0
+    rc = lib().sbk_specaugment(ptr(x), N, T, F, c, w, ptr(tmp), ptr(fm), n_f, ptr(tm), n_t, int(use_mean),
+                               ptr(partial), n_fcells, stream_of(x))
+    check(rc, "sbk_specaugment")
+
+
+@specaugment_.register_fake
+def _(x, N, T, F, c, w, fm, tm, use_mean, n_fcells):
+    return None
 
 
 class SpecAugment(torch.nn.Module):
@@ -75,20 +97,13 @@ class SpecAugment(torch.nn.Module):
             c = w = -1  # identical segment sizes: the resize is the identity
         self.last_draws = (c, w, fm, tm)
         dev = x.device
-        n_f = fm.shape[1] if fm is not None else 0
-        n_t = tm.shape[1] if tm is not None else 0
         fm_d = fm.to(dev, non_blocking=True) if fm is not None else None
         tm_d = tm.to(dev, non_blocking=True) if tm is not None else None
-        use_mean = not self.replace_with_zero
         n_fcells = 0
         if fm is not None:
             # number of masked (sequence, freq) cells x T, for the second running mean
             ar = torch.arange(F).view(1, 1, -1)
             cov = ((fm[..., 1:2] <= ar) & (ar < fm[..., 1:2] + fm[..., 0:1])).any(1)
             n_fcells = int(cov.sum()) * T
-        tmp = torch.empty_like(x) if c >= 0 else None
-        partial = torch.empty(2 * N * ((T + 15) // 16), device=dev, dtype=torch.float32) if use_mean else None
-        rc = lib().sbk_specaugment(ptr(x), N, T, F, c, w, ptr(tmp), ptr(fm_d), n_f, ptr(tm_d), n_t, int(use_mean),
-                                   ptr(partial), n_fcells, stream_of(x))
-        check(rc, "sbk_specaugment")
+        torch.ops.sbk.specaugment_(x, N, T, F, c, w, fm_d, tm_d, not self.replace_with_zero, n_fcells)
         return x
