@@ -29,6 +29,13 @@ Fixture inventory (all float32 unless noted):
                    training and eval, running statistics over 4 batches and
                    3 epochs, ragged relative lengths incl. one-frame and
                    rounding-tie lengths) (processing/features.py:940-1231)
+  wav2vec.npz      W2VLatentExtractor (default 7-layer stack at 64 channels and a
+                   small custom one), EncoderWrapper + TransformerEncoder
+                   (pre-norm GELU and post-norm ReLU), MultiheadAttention with
+                   a key padding mask, PositionalEncoding — config 5 modules
+                   (lobes/models/wav2vec.py:28-106,153-227,
+                   lobes/models/transformer/Transformer.py:201-486,
+                   nnet/attention.py:642-778)
   train.npz        gradients of sum(R * encode(cnn(feats), wav_len)) w.r.t.
                    every ConvolutionFrontEnd / TransformerASR parameter and
                    the input features (reference autograd, weights of
@@ -340,7 +347,84 @@ def gen_train():
     np.savez_compressed(os.path.join(OUT, "train.npz"), **out)
 
 
+def gen_wav2vec():
+    from speechbrain.lobes.models.wav2vec import W2VLatentExtractor, EncoderWrapper
+    from speechbrain.lobes.models.transformer.Transformer import TransformerEncoder, PositionalEncoding
+    from speechbrain.nnet.attention import MultiheadAttention
+    out = {}
+    g = torch.Generator().manual_seed(11)
+    wav = 0.1 * torch.randn(2, 6000, generator=g)
+    wav[1, 4500:] = 0.0  # a zero-padded tail
+    out["wav"] = t2n(wav)
+    torch.manual_seed(4)
+    # default kernels / strides (7 layers, k 11/5 then 3/2); 64 channels keep
+    # the fixture small (the 512-channel stack is checked against the oracle)
+    ext = W2VLatentExtractor(out_channels=[64] * 7)
+    ext.eval()
+    for k, v in ext.state_dict().items():
+        out["ext." + k] = t2n(v)
+    with torch.no_grad():
+        lat = ext(wav)
+        out["latents"] = t2n(lat)
+        out["latents_nonorm"] = t2n(ext(wav, normalize_signal=False))
+    out["out_lengths"] = ext.get_output_lengths(torch.tensor([6000, 4500])).numpy().astype(np.int64)
+    torch.manual_seed(5)
+    ext2 = W2VLatentExtractor(out_channels=[32, 32, 48], kernel_sizes=[5, 3, 3], strides=[3, 2, 2])
+    ext2.eval()
+    for k, v in ext2.state_dict().items():
+        out["ext2." + k] = t2n(v)
+    with torch.no_grad():
+        out["latents2"] = t2n(ext2(wav))
+    # encoder wrapper + pre-norm GELU transformer (the wav2vec2 recipe's form,
+    # recipes/LibriSpeech/self-supervised-learning/wav2vec2/hparams/wav2vec2_base.yaml:79-93)
+    torch.manual_seed(6)
+    enc = TransformerEncoder(num_layers=2, nhead=4, d_ffn=128, d_model=64, dropout=0.0,
+                             activation=torch.nn.GELU, normalize_before=True)
+    wrap = EncoderWrapper(64, 64, enc, dropout_encoder_input=0.0)
+    wrap.eval()
+    for k, v in wrap.state_dict().items():
+        out["wrap." + k] = t2n(v)
+    wav_lens = torch.tensor([1.0, 0.7])
+    out["wav_lens"] = t2n(wav_lens)
+    with torch.no_grad():
+        out["embeddings"] = t2n(wrap(lat, wav_lens=wav_lens)["embeddings"])
+        out["embeddings_nolen"] = t2n(wrap(lat)["embeddings"])
+    # post-norm ReLU TransformerEncoder directly, with attention maps
+    torch.manual_seed(7)
+    enc2 = TransformerEncoder(num_layers=2, nhead=2, d_ffn=96, d_model=32, dropout=0.0)
+    enc2.eval()
+    for k, v in enc2.state_dict().items():
+        out["enc2." + k] = t2n(v)
+    src = torch.randn(3, 19, 32, generator=g)
+    kpm = torch.arange(19)[None, :] >= torch.tensor([19, 12, 7])[:, None]
+    out["enc2_src"] = t2n(src)
+    out["enc2_kpm"] = kpm.numpy()
+    with torch.no_grad():
+        y, attn = enc2(src, src_key_padding_mask=kpm)
+    out["enc2_y"] = t2n(y)
+    for i, a in enumerate(attn):
+        out[f"enc2_attn{i}"] = t2n(a)
+    # MultiheadAttention wrapper alone (cross attention, L != S)
+    torch.manual_seed(8)
+    mha = MultiheadAttention(nhead=4, d_model=64)
+    mha.eval()
+    for k, v in mha.state_dict().items():
+        out["mha." + k] = t2n(v)
+    q = torch.randn(2, 9, 64, generator=g)
+    kv = torch.randn(2, 13, 64, generator=g)
+    kpm2 = torch.arange(13)[None, :] >= torch.tensor([13, 10])[:, None]
+    out["mha_q"], out["mha_kv"], out["mha_kpm"] = t2n(q), t2n(kv), kpm2.numpy()
+    with torch.no_grad():
+        o, w = mha(q, kv, kv, key_padding_mask=kpm2)
+    out["mha_out"], out["mha_w"] = t2n(o), t2n(w)
+    out["posenc_64"] = t2n(PositionalEncoding(64)(torch.zeros(1, 37, 64)))
+    np.savez_compressed(os.path.join(OUT, "wav2vec.npz"), **out)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["wav2vec"]:
+        gen_wav2vec()
+        sys.exit(0)
     if sys.argv[1:] == ["train"]:
         gen_train()
         sys.exit(0)
@@ -353,6 +437,7 @@ if __name__ == "__main__":
     gen_conformer()
     gen_train()
     gen_inputnorm()
+    gen_wav2vec()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

@@ -253,3 +253,44 @@ def test_rnnt_brute_force():
             l2, _, _, _ = OR.transducer_forward(lp2, lab, Tb, Ub, 0, "none", np.float64)
             fd = (l2[b] - loss[b]) * Tb[b] / eps
             assert abs(fd - grads[b, t, u, v]) < 1e-4
+
+
+def _sub(g, prefix):
+    return {k[len(prefix):]: torch.from_numpy(g[k]) for k in g.files if k.startswith(prefix)}
+
+
+def test_wav2vec_latent_extractor(golden):
+    """oracle/wav2vec.py vs the reference's W2VLatentExtractor (default
+    kernels/strides at 64 channels, and a custom 3-layer stack)."""
+    import oracle.wav2vec as OW
+    g = golden("wav2vec")
+    wav = torch.from_numpy(g["wav"])
+    sd = _sub(g, "ext.")
+    assert_close(OW.latent_extractor(wav, sd), g["latents"], rtol=1e-5, name="latents")
+    assert_close(OW.latent_extractor(wav, sd, normalize_signal=False), g["latents_nonorm"], rtol=1e-5, name="nonorm")
+    assert np.array_equal(OW.output_lengths([6000, 4500]).numpy(), g["out_lengths"])
+    sd2 = _sub(g, "ext2.")
+    assert_close(OW.latent_extractor(wav, sd2, kernels=(5, 3, 3), strides=(3, 2, 2)), g["latents2"], rtol=1e-5,
+                 name="latents2")
+
+
+def test_wav2vec_encoder_wrapper_and_transformer(golden):
+    import oracle.wav2vec as OW
+    g = golden("wav2vec")
+    lat = torch.from_numpy(g["latents"])
+    sd = _sub(g, "wrap.")
+    y = OW.encoder_wrapper(lat, sd, "", 2, 4, wav_lens=torch.from_numpy(g["wav_lens"]))
+    assert_close(y, g["embeddings"], rtol=1e-5, name="embeddings")
+    assert_close(OW.encoder_wrapper(lat, sd, "", 2, 4), g["embeddings_nolen"], rtol=1e-5, name="nolen")
+    assert_close(OW.positional_encoding(37, 64), g["posenc_64"], rtol=0, name="posenc")
+    sd2 = _sub(g, "enc2.")
+    y2, attn = OW.transformer_encoder(torch.from_numpy(g["enc2_src"]), sd2, "", 2, 2,
+                                      key_padding_mask=torch.from_numpy(g["enc2_kpm"]))
+    assert_close(y2, g["enc2_y"], rtol=1e-5, name="post-norm relu")
+    for i, a in enumerate(attn):
+        assert_close(a, g[f"enc2_attn{i}"], rtol=1e-5, name=f"attn{i}")
+    sdm = _sub(g, "mha.")
+    kv = torch.from_numpy(g["mha_kv"])
+    o, w = OW.mha(torch.from_numpy(g["mha_q"]), kv, kv, sdm, "", 4, torch.from_numpy(g["mha_kpm"]))
+    assert_close(o, g["mha_out"], rtol=1e-5, name="mha out")
+    assert_close(w, g["mha_w"], rtol=1e-5, name="mha weights")
