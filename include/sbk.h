@@ -337,6 +337,49 @@ int sbk_dropout_add(const void* x, int x_bf16, const float* res, long long rows,
                     const unsigned char* rowmask, float alpha, float p, unsigned long long seed, void* out,
                     int out_bf16, void* stream);
 
+/* ---- config 5: wav2vec2 latent extractor + TransformerEncoder (MXFP8) ---- */
+
+/* Per-utterance mean / rstd of F.layer_norm(wav, wav.shape[1:]) (wav2vec.py:92-93):
+ * stats[2b] = mean, stats[2b+1] = 1/sqrt(var + eps). */
+int sbk_w2v_wav_stats(const float* wav, int B, long long S, float eps, float* stats, void* stream);
+
+/* Latent-extractor layer 0 (wav2vec.py:28-88: Conv1d(1 -> C, K, stride, "valid",
+ * no bias) -> LayerNorm(C) -> GELU), waveform normalisation (stats, nullable)
+ * applied on load.  out (B, T0, C): out_mode 0 fp32, 1 bf16, 2 MXFP8 e4m3 with
+ * scales (B*T0, C/32) E8M0 bytes.  C <= 1024, K <= 16. */
+int sbk_w2v_conv0(const float* wav, const float* stats, int B, long long S, int T0, int C, int K, int stride,
+                  const float* w, const float* g, const float* b, float eps, void* out, int out_mode,
+                  uint8_t* scales, void* stream);
+
+/* Row LayerNorm (g non-null; eps) -> activation (0 none, 3 ReLU, 4 GELU) -> fp32 /
+ * bf16 / MXFP8 output, one wave per row, D in {64,...,4096} (powers of two).
+ * Extractor layers 1..6 after their GEMM; TransformerEncoderLayer norm1/norm2
+ * producing the MXFP8 A operands (Transformer.py:321-376). */
+int sbk_ln_act(const void* x, int in_bf16, long long ldx, int M, int D, const float* g, const float* b, float eps,
+               int act, void* out, long long ldo, int out_mode, uint8_t* scales, long long lds, void* stream);
+
+/* MXFP8 GEMM C = epi(A W^T) on v_mfma_scale_f32_32x32x64_f8f6f4: A e4m3 (M, K) +
+ * E8M0 scales (M, K/32); W e4m3 (N, K) + scales.  Row m of A starts at
+ * A + (m / rpb)*a_bs + (m % rpb)*lda (conv rows; rpb >= M for a plain GEMM).
+ * Epilogue: + bias, act (0/3/4), alpha*val + res, out fp32 / bf16 / MXFP8 (+scales).
+ * K % 128 == 0, N % 128 == 0.  Replaces nn.Linear / Conv1d in
+ * Transformer.py:246-376, attention.py:642-839, wav2vec.py:28-88. */
+int sbk_mx_gemm(const uint8_t* A, const uint8_t* SA, long long lda, long long ldsa, long long rpb, long long a_bs,
+                long long s_bs, const uint8_t* W, const uint8_t* SW, long long ldw, long long ldsw, int M, int N,
+                int K, const float* bias, int act, float alpha, const float* res, long long ldr, void* out,
+                long long ldc, int out_mode, uint8_t* out_scales, long long ldso, void* stream);
+
+/* x[m, :] += pe[m % T, :] in place, x (M, D) fp32 (EncoderWrapper positional table). */
+int sbk_add_rows_periodic(float* x, int M, int D, const float* pe, int T, void* stream);
+
+/* MXFP8 quantisation of a fp32 / bf16 (M, K) matrix, K % 32 == 0 (weights, cached). */
+int sbk_mx_quant(const void* x, int in_bf16, long long ldx, int M, int K, uint8_t* q, long long ldq,
+                 uint8_t* scales, long long ldsq, void* stream);
+
+/* fp32 value of an MXFP8 matrix (tests). */
+int sbk_mx_dequant(const uint8_t* q, long long ldq, const uint8_t* scales, long long ldsq, int M, int K, float* out,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -26,6 +26,47 @@ def _p(sd, k):
     return sd[k] if isinstance(sd[k], torch.Tensor) else torch.as_tensor(sd[k])
 
 
+# Operand-rounding emulation (used only to DERIVE the tolerance of the
+# reduced-precision GPU paths, never as a result): `_QMM(t)` rounds a GEMM
+# operand along its last (contraction) axis, `_QACT(t)` an activation that the
+# GPU path keeps in bf16 between kernels.  Both are the identity by default.
+_QMM = None
+_QACT = None
+
+
+def set_rounding(mm=None, act=None):
+    global _QMM, _QACT
+    _QMM, _QACT = mm, act
+
+
+def _qm(t):
+    return _QMM(t) if _QMM is not None else t
+
+
+def _qa(t):
+    return _QACT(t) if _QACT is not None else t
+
+
+def _linear(x, w, b=None):
+    return F.linear(_qm(x), _qm(w), b)
+
+
+def mx_round(t):
+    """MXFP8 rounding of t along its last axis (blocks of 32, power-of-two
+    scale 2^ceil(log2(amax/448)), e4m3 RNE) — the format of csrc/mx.h."""
+    sh = t.shape
+    x = t.float().reshape(-1, sh[-1] // 32, 32)
+    am = x.abs().amax(-1, keepdim=True)
+    e = torch.where(am > 0, torch.ceil(torch.log2(am / 448.0)), torch.full_like(am, -127.0)).clamp(-127, 127)
+    sc = torch.exp2(e)
+    q = (x / sc).clamp(-448, 448).to(torch.float8_e4m3fn).float() * sc
+    return q.reshape(sh)
+
+
+def bf16_round(t):
+    return t.to(torch.bfloat16).float()
+
+
 def latent_extractor(wav, sd, prefix="", kernels=(11, 3, 3, 3, 3, 3, 3), strides=(5, 2, 2, 2, 2, 2, 2),
                      normalize_signal=True, ln_eps=1e-5):
     """wav2vec.py:89-95.  wav (B, S) → latents (B, T', C)."""
@@ -36,7 +77,12 @@ def latent_extractor(wav, sd, prefix="", kernels=(11, 3, 3, 3, 3, 3, 3), strides
     for i, (k, s) in enumerate(zip(kernels, strides)):
         pre = f"{prefix}extractor.convblock_{i}.convs."
         w = _p(sd, pre + "conv_0.conv.weight")
-        h = F.conv1d(x.transpose(1, 2), w, None, stride=s).transpose(1, 2)  # (B, T', C)
+        if i == 0 or _QMM is None:
+            h = F.conv1d(x.transpose(1, 2), w, None, stride=s).transpose(1, 2)  # (B, T', C)
+        else:  # rounding blocks run along the input channels of each tap (the GPU's [tap][in] K order)
+            xq = _qm(x).transpose(1, 2)
+            wq = _qm(w.permute(0, 2, 1)).permute(0, 2, 1)
+            h = F.conv1d(xq, wq, None, stride=s).transpose(1, 2)
         h = F.layer_norm(h, (h.shape[-1],), _p(sd, pre + "norm_0.norm.weight"), _p(sd, pre + "norm_0.norm.bias"),
                          ln_eps)
         x = F.gelu(h)
@@ -71,9 +117,9 @@ def mha(q, k, v, sd, prefix, nhead, key_padding_mask=None):
     dh = E // nhead
     w = _p(sd, prefix + "att.in_proj_weight")
     b = _p(sd, prefix + "att.in_proj_bias")
-    qp = F.linear(q, w[:E], b[:E])
-    kp = F.linear(k, w[E:2 * E], b[E:2 * E])
-    vp = F.linear(v, w[2 * E:], b[2 * E:])
+    qp = _qa(_linear(q, w[:E], b[:E]))
+    kp = _qa(_linear(k, w[E:2 * E], b[E:2 * E]))
+    vp = _qa(_linear(v, w[2 * E:], b[2 * E:]))
     qh = qp.view(B, L, nhead, dh).transpose(1, 2)
     kh = kp.view(B, S, nhead, dh).transpose(1, 2)
     vh = vp.view(B, S, nhead, dh).transpose(1, 2)
@@ -81,8 +127,8 @@ def mha(q, k, v, sd, prefix, nhead, key_padding_mask=None):
     if key_padding_mask is not None:
         s = s.masked_fill(key_padding_mask[:, None, None, :].bool(), float("-inf"))
     p = torch.softmax(s, dim=-1)
-    o = (p @ vh).transpose(1, 2).reshape(B, L, E)
-    o = F.linear(o, _p(sd, prefix + "att.out_proj.weight"), _p(sd, prefix + "att.out_proj.bias"))
+    o = _qa((_qa(p) @ vh).transpose(1, 2).reshape(B, L, E))
+    o = _linear(o, _p(sd, prefix + "att.out_proj.weight"), _p(sd, prefix + "att.out_proj.bias"))
     return o, p.mean(dim=1)
 
 
@@ -98,8 +144,8 @@ def encoder_layer(x, sd, prefix, nhead, act=F.relu, normalize_before=False, key_
     if not normalize_before:
         x = _ln(x, sd, prefix + "norm1.norm", 1e-6)
     src1 = _ln(x, sd, prefix + "norm2.norm", 1e-6) if normalize_before else x
-    h = act(F.linear(src1, _p(sd, prefix + "pos_ffn.ffn.0.weight"), _p(sd, prefix + "pos_ffn.ffn.0.bias")))
-    out = F.linear(h, _p(sd, prefix + "pos_ffn.ffn.3.weight"), _p(sd, prefix + "pos_ffn.ffn.3.bias"))
+    h = act(_linear(src1, _p(sd, prefix + "pos_ffn.ffn.0.weight"), _p(sd, prefix + "pos_ffn.ffn.0.bias")))
+    out = _linear(h, _p(sd, prefix + "pos_ffn.ffn.3.weight"), _p(sd, prefix + "pos_ffn.ffn.3.bias"))
     x = x + out
     if not normalize_before:
         x = _ln(x, sd, prefix + "norm2.norm", 1e-6)
@@ -120,7 +166,7 @@ def encoder_wrapper(latents, sd, prefix, num_layers, nhead, act=F.gelu, normaliz
     """wav2vec.py:193-227 (eval, no mask): Linear → + positional encoding →
     TransformerEncoder with the padding mask of round(wav_lens·T)."""
     T = latents.shape[1]
-    h = F.linear(latents, _p(sd, prefix + "input_projector.weight"), _p(sd, prefix + "input_projector.bias"))
+    h = _linear(latents, _p(sd, prefix + "input_projector.weight"), _p(sd, prefix + "input_projector.bias"))
     kpm = None
     if wav_lens is not None:
         n = torch.round(torch.as_tensor(wav_lens) * T)

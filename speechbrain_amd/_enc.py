@@ -2,6 +2,8 @@
 conformer.hip, attention.hip).  Direct ctypes calls — no Python compute, no
 fallback; used by the nn.Module drop-ins and capturable into HIP graphs
 (no host sync, no allocation outside torch's caching allocator)."""
+import contextlib
+import threading
 from typing import Optional
 
 import torch
@@ -419,6 +421,28 @@ def compute_dtype():
                 "Use torch.autocast('cuda', dtype=torch.bfloat16) (Brain: auto_mix_prec='bf16') or no autocast.")
         return _bf16
     return _f32
+
+
+_MX = threading.local()
+
+
+@contextlib.contextmanager
+def mxfp8(enabled=True):
+    """Run the config-5 encoder's GEMMs (wav2vec2 latent-extractor convs,
+    TransformerEncoder projections) on MXFP8 operands — e4m3 elements with
+    one power-of-two scale per 32 contraction elements, the block-scaled
+    MFMA at 2x the bf16 rate — and the rest of the path in bf16.  GEMMs whose
+    K or N is not a multiple of 128 (the MXFP8 kernel's tile) run in bf16."""
+    prev = getattr(_MX, "on", False)
+    _MX.on = bool(enabled)
+    try:
+        yield
+    finally:
+        _MX.on = prev
+
+
+def mx_enabled():
+    return getattr(_MX, "on", False)
 
 
 class WeightCache:

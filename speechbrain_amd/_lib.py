@@ -57,6 +57,16 @@ SIGNATURES = {
                            _vp, _i, _vp, _vp, _vp],
     "sbk_cast_bf16": [_vp, _vp, _ll, _vp],
     "sbk_swish": [_vp, _vp, _ll, _f, _vp],
+    # w2v.hip (config 5 front-end, row LayerNorm / activation / MXFP8 quantisation)
+    "sbk_w2v_wav_stats": [_vp, _i, _ll, _f, _vp, _vp],
+    "sbk_w2v_conv0": [_vp, _vp, _i, _ll, _i, _i, _i, _i, _vp, _vp, _vp, _f, _vp, _i, _vp, _vp],
+    "sbk_add_rows_periodic": [_vp, _i, _i, _vp, _i, _vp],
+    "sbk_ln_act": [_vp, _i, _ll, _i, _i, _vp, _vp, _f, _i, _vp, _ll, _i, _vp, _ll, _vp],
+    # mxgemm.hip (MXFP8 block-scaled MFMA GEMM)
+    "sbk_mx_gemm": [_vp, _vp, _ll, _ll, _ll, _ll, _ll, _vp, _vp, _ll, _ll, _i, _i, _i, _vp, _i, _f, _vp, _ll, _vp,
+                    _ll, _i, _vp, _ll, _vp],
+    "sbk_mx_quant": [_vp, _i, _ll, _i, _i, _vp, _ll, _vp, _ll, _vp],
+    "sbk_mx_dequant": [_vp, _ll, _vp, _ll, _i, _i, _vp, _vp],
     # augment.hip
     "sbk_specaugment": [_vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _i, _vp, _ll, _vp],
     # rnnt.hip

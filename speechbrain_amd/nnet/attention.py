@@ -15,7 +15,7 @@ from .. import _autograd as A
 from .. import _enc
 from .activations import Swish
 
-__all__ = ["RelPosEncXL", "RelPosMHAXL", "PositionalwiseFeedForward"]
+__all__ = ["RelPosEncXL", "RelPosMHAXL", "PositionalwiseFeedForward", "MultiheadAttention"]
 
 
 class RelPosEncXL(nn.Module):
@@ -251,3 +251,100 @@ class PositionalwiseFeedForward(nn.Module):
             return self.train_run(A.to_dtype(u, dtype), dtype).view(*shp[:-1], -1)
         u = _enc.to_compute(u, dtype)
         return self.run(u, dtype).view(*shp[:-1], -1)
+
+
+class MultiheadAttention(nn.Module):
+    """attention.py:642-778: the wrapper of torch.nn.MultiheadAttention
+    (state_dict keys att.in_proj_weight / att.in_proj_bias /
+    att.out_proj.{weight,bias}).  Self-attention (query is key is value,
+    the TransformerEncoderLayer case) runs as one in_proj GEMM (rows
+    permuted per head to [q_h | k_h | v_h]) → the fused attention kernel
+    (scores·1/√d_head, key padding mask, softmax, P·V; the positional band of
+    the rel-pos kernel is fed zeros) → out_proj GEMM.  Returns
+    (output (B, L, E), head-averaged weights (B, L, S)) like the reference."""
+
+    def __init__(self, nhead, d_model, dropout=0.0, bias=True, add_bias_kv=False, add_zero_attn=False, kdim=None,
+                 vdim=None):
+        super().__init__()
+        self.att = nn.MultiheadAttention(embed_dim=d_model, num_heads=nhead, dropout=dropout, bias=bias,
+                                         add_bias_kv=add_bias_kv, add_zero_attn=add_zero_attn, kdim=kdim, vdim=vdim)
+        self.nhead = nhead
+        self.d_model = d_model
+        self._wc = _enc.WeightCache()
+        self._zeros = {}
+
+    def _check(self):
+        a = self.att
+        if not a._qkv_same_embed_dim or a.bias_k is not None or a.add_zero_attn or a.in_proj_bias is None:
+            raise NotImplementedError("MultiheadAttention: only the default projection layout (bias, no bias_kv, "
+                                      "no zero_attn, kdim = vdim = d_model) is on the HIP path")
+
+    def qkv_weights(self, mode):
+        """in_proj rows permuted to the kernel's per-head [q_h | k_h | v_h]
+        layout, in the compute mode (torch.float32 | torch.bfloat16 | "mx");
+        returns (weight, bias fp32)."""
+        a = self.att
+        ps = [a.in_proj_weight, a.in_proj_bias]
+
+        def make():
+            E, H = self.d_model, self.nhead
+            dh = E // H
+            idx = torch.arange(3 * E, device=a.in_proj_weight.device).view(3, H, dh).transpose(0, 1).reshape(-1)
+            w = a.in_proj_weight.detach()[idx].contiguous()
+            b = a.in_proj_bias.detach()[idx].contiguous().float()
+            return _mode_weight(w, mode), b
+        return self._wc.get(("qkv", str(mode)), ps, make)
+
+    def out_weights(self, mode):
+        w = self.att.out_proj.weight
+        return self._wc.get(("out", str(mode)), [w], lambda: _mode_weight(w.detach().contiguous(), mode))
+
+    def zero_band(self, T, dev, dtype):
+        """(2T-1, E) zeros for the positional term + zero u/v biases (H, dh)."""
+        key = (T, str(dev), dtype)
+        z = self._zeros.get(key)
+        if z is None:
+            E, H = self.d_model, self.nhead
+            z = (torch.zeros(2 * T - 1, E, device=dev, dtype=dtype), torch.zeros(E // H, H, device=dev))
+            self._zeros = {key: z}
+        return z
+
+    def attend(self, qkv, B, T, kpm_u8, need_weights):
+        """qkv (B*T, 3E) per-head layout (bf16 or fp32) → (o (B*T, E), probs (B, H, T, T) or None)."""
+        E, H = self.d_model, self.nhead
+        dh = E // H
+        band, zb = self.zero_band(T, qkv.device, qkv.dtype)
+        return _enc.relpos_attention(qkv, band, zb, zb, kpm_u8, B, T, H, dh, 1.0 / math.sqrt(dh),
+                                     need_probs=need_weights)
+
+    def forward(self, query, key, value, attn_mask=None, key_padding_mask=None, return_attn_weights=True,
+                pos_embs=None):
+        self._check()
+        if attn_mask is not None or pos_embs is not None:
+            raise NotImplementedError("attn_mask / pos_embs are not on the HIP attention path")
+        if not (query is key and key is value):
+            raise NotImplementedError("MultiheadAttention: the HIP path is self-attention (query is key is value)")
+        if A.needs_grad(self, query) or (self.training and self.att.dropout > 0):
+            raise NotImplementedError("MultiheadAttention has no training path yet (inference only)")
+        B, T, E = query.shape
+        mode = _enc.compute_dtype()
+        x2d = _enc.to_compute(query.reshape(B * T, E), mode)
+        w_in, b_in = self.qkv_weights(mode)
+        qkv = _enc.gemm(x2d, w_in, bias=b_in, out_dtype=mode)
+        kpm = key_padding_mask.to(torch.uint8).contiguous() if key_padding_mask is not None else None
+        o, probs = self.attend(qkv, B, T, kpm, bool(return_attn_weights))
+        out = _enc.gemm(o, self.out_weights(mode), bias=self.att.out_proj.bias.detach().float(),
+                        out_dtype=torch.float32).view(B, T, E)
+        if return_attn_weights:
+            return out, probs.mean(dim=1)
+        return out
+
+
+def _mode_weight(w, mode):
+    """A weight in compute mode: fp32 as is, bf16 cast, or "mx" (MXFP8 q, scales)."""
+    if mode == "mx":
+        from .. import _w2v
+        return _w2v.mx_quant(w.float().contiguous())
+    if mode == torch.bfloat16:
+        return _enc.cast_bf16(w.float().contiguous())
+    return w.float().contiguous()

@@ -1,0 +1,228 @@
+"""Config 5 on the GPU: the MXFP8 GEMM / quantisation / LayerNorm kernels
+against exact CPU emulations, the wav2vec2 latent extractor, EncoderWrapper,
+TransformerEncoder and MultiheadAttention against the reference's fixtures
+(fp32), and the bf16 / MXFP8 paths at full config-5 shapes against the fp32
+oracle with tolerances derived from an oracle run with the same operand
+rounding (oracle.wav2vec.set_rounding)."""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import assert_close
+import oracle.wav2vec as OW
+
+pytestmark = pytest.mark.gpu
+
+
+def _sub(g, prefix):
+    return {k[len(prefix):]: torch.from_numpy(g[k]) for k in g.files if k.startswith(prefix)}
+
+
+# ---------------------------------------------------------------- kernels
+def test_mx_quant_matches_emulation(dev):
+    from speechbrain_amd import _w2v
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(37, 256, generator=g) * torch.logspace(-6, 4, 256)[None, :]
+    x[3, :32] = 0.0            # all-zero block → scale byte 0
+    x[5, 40] = 448.0 * 8       # exact power-of-two boundary
+    m = _w2v.mx_quant(x.to(dev))
+    got = _w2v.mx_dequant(m).cpu()
+    assert torch.equal(got, OW.mx_round(x))
+    assert int(m.s[3, 0]) == 0
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 256, 256), (128, 384, 1024), (77, 128, 128)])
+def test_mx_gemm_vs_dequantized_product(dev, M, N, K):
+    """The block-scaled MFMA GEMM equals the fp64 product of the dequantised
+    operands to fp32 accumulation accuracy (e4m3 x e4m3 products are exact
+    in fp32), for the plain, bias+GELU+residual, bf16 and MXFP8 outputs."""
+    from speechbrain_amd import _w2v
+    g = torch.Generator().manual_seed(M + N + K)
+    a = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) * 0.05
+    bias = torch.randn(N, generator=g)
+    res = torch.randn(M, N, generator=g)
+    A, W = _w2v.mx_quant(a.to(dev)), _w2v.mx_quant(w.to(dev))
+    ad, wd = _w2v.mx_dequant(A).cpu().double(), _w2v.mx_dequant(W).cpu().double()
+    ref = ad @ wd.t()
+    y = _w2v.mx_gemm(A, W).cpu().double()
+    tol = 2e-6 * (ad.abs() @ wd.abs().t())
+    assert torch.all((y - ref).abs() <= tol + 1e-30)
+    y2 = _w2v.mx_gemm(A, W, bias=bias.to(dev), act="gelu", alpha=0.5, res=res.to(dev)).cpu().double()
+    ref2 = res.double() + 0.5 * F.gelu(ref + bias.double())
+    assert float((y2 - ref2).abs().max()) < 1e-4
+    yb = _w2v.mx_gemm(A, W, out=torch.bfloat16).cpu().double()
+    assert float(((yb - ref).abs() / ref.abs().clamp(min=1e-3)).median()) < 4e-3
+    ym = _w2v.mx_gemm(A, W, bias=bias.to(dev), act="gelu", out="mx")
+    assert torch.equal(_w2v.mx_dequant(ym).cpu(), OW.mx_round(F.gelu(torch.from_numpy(
+        _w2v.mx_gemm(A, W, bias=bias.to(dev)).cpu().numpy()))))
+
+
+def test_mx_conv_gemm_vs_conv1d(dev):
+    """Conv1d(k=3, stride 2, "valid") over channels-last MXFP8 rows as one
+    GEMM over overlapping rows, per-utterance batch addressing."""
+    from speechbrain_amd import _w2v
+    B, T, C, N = 3, 57, 128, 256
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(B * T, C, generator=g)
+    w = torch.randn(N, C, 3, generator=g) * 0.1
+    X = _w2v.mx_quant(x.to(dev))
+    wm = w.permute(0, 2, 1).reshape(N, 3 * C).contiguous()
+    Wq = _w2v.mx_quant(wm.to(dev))
+    y, T_out = _w2v.mx_conv_gemm(X, B, T, C, 3, 2, Wq)
+    xd = _w2v.mx_dequant(X).cpu().view(B, T, C)
+    wd = _w2v.mx_dequant(Wq).cpu().view(N, 3, C).permute(0, 2, 1)
+    ref = F.conv1d(xd.transpose(1, 2).double(), wd.double(), stride=2).transpose(1, 2).reshape(B * T_out, N)
+    assert T_out == (T - 3) // 2 + 1
+    assert float((y.cpu().double() - ref).abs().max()) < 1e-4
+
+
+@pytest.mark.parametrize("D", [64, 512, 1024, 4096])
+def test_ln_act_vs_torch(dev, D):
+    from speechbrain_amd import _w2v
+    g = torch.Generator().manual_seed(D)
+    x = torch.randn(41, D, generator=g) * 3 + 1
+    gam, bet = torch.randn(D, generator=g), torch.randn(D, generator=g)
+    ref = F.gelu(F.layer_norm(x, (D,), gam, bet, 1e-6))
+    y = _w2v.ln_act(x.to(dev), (gam.to(dev), bet.to(dev), 1e-6), "gelu", torch.float32).cpu()
+    assert_close(y, ref, rtol=2e-5, name="ln_act fp32")
+    yb = _w2v.ln_act(x.to(dev).bfloat16(), (gam.to(dev), bet.to(dev), 1e-6), None, torch.bfloat16).cpu()
+    assert_close(yb.float(), F.layer_norm(x.bfloat16().float(), (D,), gam, bet, 1e-6), rtol=1e-2, name="bf16")
+    m = _w2v.ln_act(x.to(dev), (gam.to(dev), bet.to(dev), 1e-6), "gelu", "mx")
+    assert torch.equal(_w2v.mx_dequant(m).cpu(), OW.mx_round(y))
+
+
+def test_conv0_vs_torch(dev):
+    from speechbrain_amd import _w2v
+    g = torch.Generator().manual_seed(9)
+    wav = 0.1 * torch.randn(2, 3001, generator=g)
+    w = torch.randn(512, 11, generator=g) * 0.3
+    gam, bet = torch.randn(512, generator=g), torch.randn(512, generator=g)
+    xn = F.layer_norm(wav, wav.shape[1:])
+    ref = F.gelu(F.layer_norm(F.conv1d(xn[:, None, :], w[:, None, :], stride=5).transpose(1, 2), (512,), gam, bet,
+                              1e-5)).reshape(-1, 512)
+    st = _w2v.wav_stats(wav.to(dev), 1e-5)
+    y = _w2v.conv0(wav.to(dev), st, w.to(dev), gam.to(dev), bet.to(dev), 1e-5, 5, torch.float32).cpu()
+    assert_close(y, ref, rtol=1e-4, name="conv0")
+    m = _w2v.conv0(wav.to(dev), st, w.to(dev), gam.to(dev), bet.to(dev), 1e-5, 5, "mx")
+    assert torch.equal(_w2v.mx_dequant(m).cpu(), OW.mx_round(y))
+
+
+# ------------------------------------------------------ modules vs fixtures
+def _load(mod, sd):
+    mod.load_state_dict({k: v for k, v in sd.items()}, strict=True)
+    return mod
+
+
+def test_latent_extractor_vs_golden(golden, dev):
+    from speechbrain_amd.lobes.models.wav2vec import W2VLatentExtractor
+    g = golden("wav2vec")
+    wav = torch.from_numpy(g["wav"]).to(dev)
+    ext = _load(W2VLatentExtractor(out_channels=[64] * 7), _sub(g, "ext.")).to(dev).eval()
+    with torch.no_grad():
+        assert_close(ext(wav), g["latents"], rtol=1e-4, name="latents")
+        assert_close(ext(wav, normalize_signal=False), g["latents_nonorm"], rtol=1e-4, name="nonorm")
+    assert np.array_equal(ext.get_output_lengths(torch.tensor([6000, 4500])).numpy(), g["out_lengths"])
+    ext2 = _load(W2VLatentExtractor(out_channels=[32, 32, 48], kernel_sizes=[5, 3, 3], strides=[3, 2, 2]),
+                 _sub(g, "ext2.")).to(dev).eval()
+    with torch.no_grad():
+        assert_close(ext2(wav), g["latents2"], rtol=1e-4, name="latents2")
+
+
+def test_encoder_wrapper_and_transformer_vs_golden(golden, dev):
+    from speechbrain_amd.lobes.models.transformer.Transformer import TransformerEncoder
+    from speechbrain_amd.lobes.models.wav2vec import EncoderWrapper
+    from speechbrain_amd.nnet.attention import MultiheadAttention
+    g = golden("wav2vec")
+    enc = TransformerEncoder(num_layers=2, nhead=4, d_ffn=128, d_model=64, dropout=0.0, activation=torch.nn.GELU,
+                             normalize_before=True)
+    wrap = _load(EncoderWrapper(64, 64, enc, dropout_encoder_input=0.0), _sub(g, "wrap.")).to(dev).eval()
+    lat = torch.from_numpy(g["latents"]).to(dev)
+    with torch.no_grad():
+        y = wrap(lat, wav_lens=torch.from_numpy(g["wav_lens"]).to(dev))["embeddings"]
+        assert_close(y, g["embeddings"], rtol=1e-4, name="embeddings")
+        assert_close(wrap(lat)["embeddings"], g["embeddings_nolen"], rtol=1e-4, name="nolen")
+    enc2 = _load(TransformerEncoder(num_layers=2, nhead=2, d_ffn=96, d_model=32, dropout=0.0),
+                 _sub(g, "enc2.")).to(dev).eval()
+    with torch.no_grad():
+        y2, attn = enc2(torch.from_numpy(g["enc2_src"]).to(dev),
+                        src_key_padding_mask=torch.from_numpy(g["enc2_kpm"]).to(dev))
+    assert_close(y2, g["enc2_y"], rtol=1e-4, name="post-norm relu")
+    for i, a in enumerate(attn):
+        assert_close(a, g[f"enc2_attn{i}"], rtol=1e-4, name=f"attn{i}")
+    # MultiheadAttention (self-attention) vs the oracle pinned to the reference's cross-attention fixture
+    sdm = _sub(g, "mha.")
+    mha = _load(MultiheadAttention(nhead=4, d_model=64), sdm).to(dev).eval()
+    q = torch.from_numpy(g["mha_kv"])
+    kpm = torch.from_numpy(g["mha_kpm"])
+    with torch.no_grad():
+        qd = q.to(dev)
+        o, w = mha(qd, qd, qd, key_padding_mask=kpm.to(dev))
+    ro, rw = OW.mha(q, q, q, sdm, "", 4, kpm)
+    assert_close(o, ro, rtol=1e-4, name="mha out")
+    assert_close(w, rw, rtol=1e-4, name="mha weights")
+
+
+# ----------------------------------------- config 5 at full size vs oracle
+def _c5_model(dev, layers):
+    from speechbrain_amd.lobes.models.transformer.Transformer import TransformerEncoder
+    from speechbrain_amd.lobes.models.wav2vec import EncoderWrapper, W2VLatentExtractor
+    torch.manual_seed(0)
+    ext = W2VLatentExtractor()
+    enc = TransformerEncoder(num_layers=layers, nhead=16, d_ffn=4096, d_model=1024, dropout=0.0,
+                             activation=torch.nn.GELU, normalize_before=True)
+    wrap = EncoderWrapper(512, 1024, enc, dropout_encoder_input=0.0)
+    return ext.to(dev).eval(), wrap.to(dev).eval()
+
+
+def _c5_oracle(wav, lens, ext, wrap, layers, mm=None, act=None):
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    sde = {k: v.cpu() for k, v in ext.state_dict().items()}
+    sdw = {k: v.cpu() for k, v in wrap.state_dict().items()}
+    OW.set_rounding(mm, act)
+    try:
+        with torch.no_grad():
+            return OW.wav2vec_encode(wav, sde, sdw, layers, 16, wav_lens=lens)
+    finally:
+        OW.set_rounding(None, None)
+
+
+@pytest.mark.parametrize("prec", ["mxfp8", "bf16"])
+def test_config5_full_size_vs_oracle(dev, prec):
+    """Two 15 s utterances (one ragged) through W2VLatentExtractor (512 ch)
+    and a 4-layer d=1024 / 16-head / ffn 4096 GELU pre-norm encoder.  The
+    tolerance is the deviation of an oracle run whose GEMM operands carry the
+    same rounding (MXFP8 blocks for the MXFP8 path, bf16 activations between
+    kernels) from the fp32 oracle, times 1.5; observed values are printed."""
+    import speechbrain_amd as sba
+    layers = 4
+    ext, wrap = _c5_model(dev, layers)
+    g = torch.Generator().manual_seed(5)
+    wav = 0.1 * torch.randn(2, 240000, generator=g)
+    lens = torch.tensor([1.0, 0.8])
+    with torch.no_grad():
+        if prec == "mxfp8":
+            with sba.mxfp8():
+                lat, T = ext.run(wav.to(dev), True, "mx")
+                y = wrap.embed(lat, 2, T, lens.to(dev))
+        else:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                lat, T = ext.run(wav.to(dev), True, torch.bfloat16)
+                y = wrap.embed(lat, 2, T, lens.to(dev))
+    y = y.view(2, T, 1024).cpu()
+    assert T == 748
+    ref = _c5_oracle(wav, lens, ext, wrap, layers)
+    if prec == "mxfp8":
+        emu = _c5_oracle(wav, lens, ext, wrap, layers, mm=OW.mx_round, act=OW.bf16_round)
+    else:
+        emu = _c5_oracle(wav, lens, ext, wrap, layers, mm=OW.bf16_round, act=OW.bf16_round)
+    e_gpu, e_emu = (y - ref).abs(), (emu - ref).abs()
+    print(f"\nconfig5 {prec}: GPU vs fp32 oracle max {e_gpu.max():.4e} mean {e_gpu.mean():.4e}; "
+          f"rounded-operand oracle max {e_emu.max():.4e} mean {e_emu.mean():.4e}")
+    assert torch.isfinite(y).all()
+    assert float(e_gpu.mean()) <= 1.5 * float(e_emu.mean())
+    assert float(e_gpu.max()) <= 1.5 * float(e_emu.max())
