@@ -354,7 +354,7 @@ int sbk_w2v_conv0(const float* wav, const float* stats, int B, long long S, int 
 /* Row LayerNorm (g non-null; eps) -> activation (0 none, 3 ReLU, 4 GELU) -> fp32 /
  * bf16 / MXFP8 output, one wave per row, D in {64,...,4096} (powers of two).
  * Extractor layers 1..6 after their GEMM; TransformerEncoderLayer norm1/norm2
- * producing the MXFP8 A operands (Transformer.py:321-376). */
+ * producing the MXFP8 A operands (Transformer.py:321-376).  Other D: fp32 / bf16 only. */
 int sbk_ln_act(const void* x, int in_bf16, long long ldx, int M, int D, const float* g, const float* b, float eps,
                int act, void* out, long long ldo, int out_mode, uint8_t* scales, long long lds, void* stream);
 

@@ -5,11 +5,12 @@
 //   A: e4m3 (M, K) with E8M0 scales (M, K/32), W: e4m3 (N, K) + (N, K/32)
 //   (nn.Linear [out][in] layout; both operands K-contiguous).
 //
-// v_mfma_scale_f32_32x32x64_f8f6f4: lane l holds 32 consecutive K bytes of
-// row (l & 31) starting at k = 32*(l >> 5), and the E8M0 scale of exactly
-// that 32-element block, so the OCP MX block (32 along K) maps one-to-one
-// onto a lane's operand and the hardware applies both scales: no
-// dequantisation and no per-tensor amax reduction.  It runs at 2x the bf16
+// v_mfma_scale_f32_32x32x64_f8f6f4 (layout measured by scripts/mx_probe4.hip):
+// lane l feeds row (l & 31); operand bytes 0-15 of BOTH lane halves form the
+// first 32-element K block and bytes 16-31 the second; the E8M0 scale of
+// block b of row r comes from lane r + 32*b.  So the OCP MX block (32 along
+// K) maps onto two 16-B halves and one scale byte per lane, and the hardware
+// applies both operands' scales: no dequantisation pass, no per-tensor amax.  It runs at 2x the bf16
 // MFMA rate (MI355X_MICROARCH.md, matrix cores).
 //
 // Tile 128 x 128 x 128 B, 4 waves (2 x 2), wave tile 64 x 64 = 2 x 2 MFMA
@@ -155,17 +156,20 @@ __global__ void __launch_bounds__(NT) mx_gemm_kernel(MxArgs p) {
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int c0 = 4 * s + 2 * fh;  // global 16-B chunks c0, c0 + 1 of the row
+      // operand bytes 0-15 of both lane halves form scale block 0 of the
+      // 64-deep step, bytes 16-31 block 1 (scripts/mx_probe4.hip): lane half
+      // h takes the 16-B chunks 4s + h (block 2s) and 4s + 2 + h (block 2s + 1)
+      const int c0 = 4 * s + fh, c1 = 4 * s + 2 + fh;
       i32x8 af[2], bf[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int ra = wm * 64 + i * 32 + fr;
         const int4 x0 = *reinterpret_cast<const int4*>(As + ra * BK + 16 * (c0 ^ (ra & 7)));
-        const int4 x1 = *reinterpret_cast<const int4*>(As + ra * BK + 16 * ((c0 + 1) ^ (ra & 7)));
+        const int4 x1 = *reinterpret_cast<const int4*>(As + ra * BK + 16 * (c1 ^ (ra & 7)));
         af[i] = i32x8{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
         const int rb = wn * 64 + i * 32 + fr;
         const int4 y0 = *reinterpret_cast<const int4*>(Ws + rb * BK + 16 * (c0 ^ (rb & 7)));
-        const int4 y1 = *reinterpret_cast<const int4*>(Ws + rb * BK + 16 * ((c0 + 1) ^ (rb & 7)));
+        const int4 y1 = *reinterpret_cast<const int4*>(Ws + rb * BK + 16 * (c1 ^ (rb & 7)));
         bf[i] = i32x8{y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
       }
       const int sh = 8 * (2 * s + fh);

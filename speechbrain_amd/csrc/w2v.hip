@@ -252,6 +252,43 @@ __global__ void __launch_bounds__(256) ln_act_kernel(const void* __restrict__ x,
   }
 }
 
+// Any D (fp32 / bf16 output): one wave per row, three passes over the row
+// (sum, centred squares, write) — the small / odd widths of test configs.
+__global__ void __launch_bounds__(256) ln_act_generic_kernel(const void* __restrict__ x, int in_bf16, long long ldx,
+                                                             int M, int D, const float* __restrict__ g,
+                                                             const float* __restrict__ be, float eps, int act,
+                                                             void* __restrict__ out, long long ldo, int out_bf16) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int lane = threadIdx.x & 63;
+  auto ld = [&](int c) {
+    return in_bf16 ? bf16_to_f32(reinterpret_cast<const uint16_t*>(x)[(long long)row * ldx + c])
+                   : reinterpret_cast<const float*>(x)[(long long)row * ldx + c];
+  };
+  float mu = 0.f, rs = 1.f;
+  if (g) {
+    float s = 0.f;
+    for (int c = lane; c < D; c += 64) s += ld(c);
+    mu = wave_sum_v(s) / (float)D;
+    float q = 0.f;
+    for (int c = lane; c < D; c += 64) {
+      const float d = ld(c) - mu;
+      q = fmaf(d, d, q);
+    }
+    rs = rsqrtf(wave_sum_v(q) / (float)D + eps);
+  }
+  for (int c = lane; c < D; c += 64) {
+    float v = ld(c);
+    if (g) v = (v - mu) * rs * g[c] + be[c];
+    if (act == 4) v = gelu_erf(v);
+    else if (act == 3) v = fmaxf(v, 0.f);
+    if (out_bf16)
+      reinterpret_cast<uint16_t*>(out)[(long long)row * ldo + c] = f32_to_bf16(v);
+    else
+      reinterpret_cast<float*>(out)[(long long)row * ldo + c] = v;
+  }
+}
+
 template <int V>
 int launch_ln_act(const void* x, int in_bf16, long long ldx, int M, const float* g, const float* be, float eps,
                   int act, void* out, long long ldo, int out_mode, uint8_t* scales, long long lds, hipStream_t s) {
@@ -286,8 +323,9 @@ SBK_API int sbk_w2v_conv0(const float* wav, const float* stats, int B, long long
   return 0;
 }
 
-// Row LayerNorm (g non-null) / activation / output conversion, D in
-// {64, 128, 256, 512, 1024, 2048, 4096}; ld* in elements (scales: bytes).
+// Row LayerNorm (g non-null) / activation / output conversion; MXFP8 output
+// for D in {64, 128, ..., 4096}, fp32 / bf16 for any D; ld* in elements
+// (scales: bytes).
 SBK_API int sbk_ln_act(const void* x, int in_bf16, long long ldx, int M, int D, const float* g, const float* b,
                        float eps, int act, void* out, long long ldo, int out_mode, uint8_t* scales, long long lds,
                        void* stream) {
@@ -302,7 +340,12 @@ SBK_API int sbk_ln_act(const void* x, int in_bf16, long long ldx, int M, int D, 
     case 1024: return launch_ln_act<16>(x, in_bf16, ldx, M, g, b, eps, act, out, ldo, out_mode, scales, lds, s);
     case 2048: return launch_ln_act<32>(x, in_bf16, ldx, M, g, b, eps, act, out, ldo, out_mode, scales, lds, s);
     case 4096: return launch_ln_act<64>(x, in_bf16, ldx, M, g, b, eps, act, out, ldo, out_mode, scales, lds, s);
-    default: return SBK_ERR_ARG;
+    default:
+      if (out_mode == 2 || D <= 0) return SBK_ERR_ARG;
+      hipLaunchKernelGGL(ln_act_generic_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, x, in_bf16, ldx, M, D,
+                         g, b, eps, act, out, ldo, out_mode == 1);
+      SBK_CHECK_LAUNCH();
+      return 0;
   }
 }
 

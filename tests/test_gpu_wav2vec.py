@@ -38,8 +38,11 @@ def test_mx_quant_matches_emulation(dev):
 @pytest.mark.parametrize("M,N,K", [(300, 256, 256), (128, 384, 1024), (77, 128, 128)])
 def test_mx_gemm_vs_dequantized_product(dev, M, N, K):
     """The block-scaled MFMA GEMM equals the fp64 product of the dequantised
-    operands to fp32 accumulation accuracy (e4m3 x e4m3 products are exact
-    in fp32), for the plain, bias+GELU+residual, bf16 and MXFP8 outputs."""
+    operands to accumulation accuracy, for the plain, bias+GELU+residual,
+    bf16 and MXFP8 outputs.  The fp8 MFMA does not accumulate in IEEE fp32
+    (measured on MI355X: |err| up to ~4e-6 * sum|a*b|, vs ~1e-7 for a fp32
+    FMA chain), so the bound is 2e-5 * sum|a*b| — three orders below the
+    e4m3 operand rounding (2^-4 relative) that the end-to-end tests bound."""
     from speechbrain_amd import _w2v
     g = torch.Generator().manual_seed(M + N + K)
     a = torch.randn(M, K, generator=g)
@@ -50,16 +53,17 @@ def test_mx_gemm_vs_dequantized_product(dev, M, N, K):
     ad, wd = _w2v.mx_dequant(A).cpu().double(), _w2v.mx_dequant(W).cpu().double()
     ref = ad @ wd.t()
     y = _w2v.mx_gemm(A, W).cpu().double()
-    tol = 2e-6 * (ad.abs() @ wd.abs().t())
+    tol = 2e-5 * (ad.abs() @ wd.abs().t())
     assert torch.all((y - ref).abs() <= tol + 1e-30)
     y2 = _w2v.mx_gemm(A, W, bias=bias.to(dev), act="gelu", alpha=0.5, res=res.to(dev)).cpu().double()
     ref2 = res.double() + 0.5 * F.gelu(ref + bias.double())
     assert float((y2 - ref2).abs().max()) < 1e-4
     yb = _w2v.mx_gemm(A, W, out=torch.bfloat16).cpu().double()
     assert float(((yb - ref).abs() / ref.abs().clamp(min=1e-3)).median()) < 4e-3
+    # MXFP8 output = the block quantisation of the kernel's own fp32 epilogue values
     ym = _w2v.mx_gemm(A, W, bias=bias.to(dev), act="gelu", out="mx")
-    assert torch.equal(_w2v.mx_dequant(ym).cpu(), OW.mx_round(F.gelu(torch.from_numpy(
-        _w2v.mx_gemm(A, W, bias=bias.to(dev)).cpu().numpy()))))
+    yf = _w2v.mx_gemm(A, W, bias=bias.to(dev), act="gelu").cpu()
+    assert torch.equal(_w2v.mx_dequant(ym).cpu(), OW.mx_round(yf))
 
 
 def test_mx_conv_gemm_vs_conv1d(dev):
@@ -78,7 +82,8 @@ def test_mx_conv_gemm_vs_conv1d(dev):
     wd = _w2v.mx_dequant(Wq).cpu().view(N, 3, C).permute(0, 2, 1)
     ref = F.conv1d(xd.transpose(1, 2).double(), wd.double(), stride=2).transpose(1, 2).reshape(B * T_out, N)
     assert T_out == (T - 3) // 2 + 1
-    assert float((y.cpu().double() - ref).abs().max()) < 1e-4
+    mag = F.conv1d(xd.transpose(1, 2).double().abs(), wd.double().abs(), stride=2).transpose(1, 2).reshape(B * T_out, N)
+    assert torch.all((y.cpu().double() - ref).abs() <= 2e-5 * mag)
 
 
 @pytest.mark.parametrize("D", [64, 512, 1024, 4096])
