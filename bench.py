@@ -127,11 +127,11 @@ class _LaunchProbe:
     runs inside the step's graph, without per-launch event or host gaps — the
     quantity rocprofv3 --kernel-trace reports for it."""
 
-    def __init__(self, name, flops_of, is_bf16):
+    def __init__(self, name, flops_of, is_bf16, module=None):
         from speechbrain_amd import _enc
-        self._enc = _enc
+        self._enc = module if module is not None else _enc
         self.name = name
-        self.orig = getattr(_enc, name)
+        self.orig = getattr(self._enc, name)
         self.flops_of = flops_of
         self.is_bf16 = is_bf16
         self.calls = []
@@ -277,6 +277,190 @@ def launch_plumbing(args):
         dist.destroy_process_group()
 
 
+# ----------------------------------------------------------------- config 5
+C5_LAYERS, C5_D, C5_H, C5_FFN = 24, 1024, 16, 4096
+PEAK_MXFP8_TFLOPS = 5000.0  # MI355X dense FP8 (block-scaled MFMA), MI355X_MICROARCH.md
+
+
+def build_c5(dev, layers=C5_LAYERS):
+    """BASELINE config 5: W2VLatentExtractor defaults (512 ch,
+    k [11,3,...], s [5,2,...]) → EncoderWrapper(Linear 512→1024 + positional
+    encoding) → TransformerEncoder(24L, d=1024, H=16, ffn 4096, GELU,
+    pre-norm).  Random init (torch.manual_seed(0))."""
+    from speechbrain_amd.lobes.models.transformer.Transformer import TransformerEncoder
+    from speechbrain_amd.lobes.models.wav2vec import EncoderWrapper, W2VLatentExtractor
+    torch.manual_seed(0)
+    ext = W2VLatentExtractor()
+    enc = TransformerEncoder(num_layers=layers, nhead=C5_H, d_ffn=C5_FFN, d_model=C5_D, dropout=0.0,
+                             activation=torch.nn.GELU, normalize_before=True)
+    wrap = EncoderWrapper(512, C5_D, enc, dropout_encoder_input=0.0)
+    return ext.to(dev).eval(), wrap.to(dev).eval()
+
+
+def c5_flops(B, S=240000, layers=C5_LAYERS, d=C5_D, dff=C5_FFN, C=512, ks=(11, 3, 3, 3, 3, 3, 3),
+             ss=(5, 2, 2, 2, 2, 2, 2)):
+    """Algorithmic FLOPs of one config-5 step: latent-extractor convs
+    (2·T_i·C_out·C_in·k per utterance), the input projector, and per layer
+    QKV 6d², out 2d², FFN 4·d·dff per token plus scores / P·V 4·T·d."""
+    T, cin, fl = S, 1, 0.0
+    for k, s in zip(ks, ss):
+        T = (T - k) // s + 1
+        fl += 2.0 * B * T * C * cin * k
+        cin = C
+    fl += 2.0 * B * T * C * d
+    per_tok = 6 * d * d + 2 * d * d + 4 * d * dff + 4 * T * d
+    return fl + layers * B * T * per_tok, T
+
+
+def make_c5_step(ext, wrap, wav, wav_len, prec):
+    import speechbrain_amd as sba
+
+    def step():
+        with torch.no_grad():
+            if prec == "mxfp8":
+                with sba.mxfp8():
+                    lat, T = ext.run(wav, True, "mx")
+                    return wrap.embed(lat, wav.shape[0], T, wav_len)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                lat, T = ext.run(wav, True, torch.bfloat16)
+                return wrap.embed(lat, wav.shape[0], T, wav_len)
+    return step
+
+
+def cpu_baseline_c5(n_utt=1, reps=2):
+    """Oracle (PyTorch CPU fp32 restatement, oracle/wav2vec.py) of config 5 on
+    n_utt x 15 s, median of `reps` after a warm-up."""
+    import oracle.wav2vec as OW
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    ext, wrap = build_c5("cpu")
+    sde, sdw = ext.state_dict(), wrap.state_dict()
+    wav = 0.1 * torch.randn(n_utt, int(SR * SECONDS), generator=torch.Generator().manual_seed(0))
+    times = []
+    with torch.no_grad():
+        for r in range(reps + 1):
+            t0 = time.perf_counter()
+            OW.wav2vec_encode(wav, sde, sdw, C5_LAYERS, C5_H, wav_lens=torch.ones(n_utt))
+            if r:
+                times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {"value": round(n_utt * SECONDS / med, 2), "unit": "audio-sec/sec", "cores": threads, "kind": "port",
+            "sample": f"{n_utt} utt x 15 s synthetic, fp32, median of {reps} after 1 warm-up"}
+
+
+def _mha_flops(qkv, pk, pbu, pbv, kpm, B, T, H, dh, *a, **k):
+    """Plain multi-head attention: scores 2·T·dh + P·V 2·T·dh per (query, head)
+    (the zero positional band the rel-pos kernel also evaluates is not counted)."""
+    return float(B) * T * H * dh * 4 * T
+
+
+def _mx_flops(a, w, *r, **k):
+    return 2.0 * a.q.shape[0] * w.q.shape[0] * a.q.shape[1]
+
+
+def run_c5(args, world, rank, dev):
+    prec = args.precision
+    ext, wrap = build_c5(dev)
+    g = torch.Generator().manual_seed(1234 + rank)
+    wav = (0.1 * torch.randn(args.batch, int(SR * SECONDS), generator=g)).to(dev)
+    wav_len = torch.ones(args.batch, device=dev)
+    step = make_c5_step(ext, wrap, wav, wav_len, prec)
+    out = step()
+    T = out.shape[0] // args.batch
+    run = capture(step, args.no_graph)
+    elapsed, rank_ms = time_steps(run, args.steps, args.warmup, world, dev)
+    ms_per_step = 1000.0 * elapsed / args.steps
+    value = world * args.batch * SECONDS * args.steps / elapsed
+    if rank != 0:
+        return
+    total, _ = c5_flops(args.batch)
+    from speechbrain_amd import _enc, _w2v
+    probes = [_LaunchProbe("mx_gemm", _mx_flops, lambda *a, **k: True, module=_w2v),
+              _LaunchProbe("relpos_attention", _mha_flops, lambda qkv, *a, **k: qkv.dtype == torch.bfloat16)]
+    if prec != "mxfp8":
+        probes = [_LaunchProbe("gemm", _gemm_flops, lambda a, w, *r, **k: a.dtype == torch.bfloat16),
+                  probes[1]]
+    for p in probes:
+        p.__enter__()
+    try:
+        step()
+    finally:
+        for p in probes:
+            p.__exit__()
+    kern = {}
+    for p in probes:
+        ms, n, fl = p.replay_time()
+        if n:
+            kern[p.name] = {"kernel": p.name, "launches_per_step": n, "avg_launch_us": round(1000.0 * ms / n, 3),
+                            "achieved": round(fl / (ms * 1e-3) / 1e12, 2), "step_share_ms": round(ms, 4)}
+    dom = max(kern.values(), key=lambda k: k["step_share_ms"])
+    peak = PEAK_MXFP8_TFLOPS if (prec == "mxfp8" and dom["kernel"] == "mx_gemm") else PEAK_BF16_TFLOPS
+    traffic = load_traffic()
+    res = {
+        "metric": "audio-sec/sec wav2vec2 CNN frontend + 24L TransformerEncoder fwd (16kHz, B=32x15s)",
+        "value": round(value, 1), "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "rank_ms_per_step": rank_ms,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "mxfp8" if prec == "mxfp8" else "bf16", "data": "synthetic (0.1·N(0,1) 16 kHz, random-init weights)",
+        "config": {"workload": f"C5: W2VLatentExtractor(512ch, 7 conv) → Linear 512→1024 → TransformerEncoder "
+                               f"{C5_LAYERS}L d={C5_D} H={C5_H} ffn={C5_FFN} GELU pre-norm, B={args.batch}×15s per GPU"
+                               + (" (GEMMs MXFP8 e4m3 + E8M0 block scales, attention bf16)" if prec == "mxfp8"
+                                  else " (bf16)"),
+                   "global_batch": world * args.batch, "seq_len": T, "parallelism": f"replicas{world}",
+                   "hip_graph": not args.no_graph},
+        "roofline": {"bound": "mfma", "kernel": dom["kernel"], "achieved": dom["achieved"], "peak": peak,
+                     "unit": "TFLOP/s", "frac": round(dom["achieved"] / peak, 4),
+                     "traffic": traffic.get(dom["kernel"]), "launches_per_step": dom["launches_per_step"],
+                     "avg_launch_us": dom["avg_launch_us"], "step_algorithmic_tflop": round(total / 1e12, 4),
+                     "step_tflops_achieved": round(total / (ms_per_step * 1e-3) / 1e12, 2),
+                     "other_kernels": [k for k in kern.values() if k is not dom]},
+    }
+    if not args.no_cpu_baseline and world == 1:
+        res["cpu_baseline"] = cpu_baseline_c5()
+    print(json.dumps(res), flush=True)
+
+
+def capture(step, no_graph):
+    """The step captured once into a HIP graph (replayed), or eager."""
+    if no_graph:
+        return step
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        step()
+    torch.cuda.synchronize()
+    capture.graphs.append(graph)  # keep the graph (and its memory pool) alive
+    return graph.replay
+
+
+capture.graphs = []
+
+
+def time_steps(run, steps, warmup, world, dev):
+    """W untimed runs, then exactly K timed, bracketed by barrier + synchronize;
+    returns (max-over-ranks seconds, per-rank ms per step)."""
+    for _ in range(warmup):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    mine = time.perf_counter() - t0
+    return max_over_ranks(mine, world, dev), [round(1000.0 * t / steps, 4) for t in per_rank(mine, world, dev)]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -286,6 +470,9 @@ def main():
     ap.add_argument("--batch", type=int, default=BATCH)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--config", choices=["c3", "c5"], default="c3",
+                    help="c3: Fbank→Conformer (the BASELINE metric, default); c5: wav2vec2 + 24L TransformerEncoder")
+    ap.add_argument("--precision", choices=["mxfp8", "bf16"], default="mxfp8", help="config 5 GEMM precision")
     ap.add_argument("--plumbing", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -300,6 +487,12 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
         assert dist.get_world_size() == args.gpus
+    if args.config == "c5":
+        run_c5(args, world, rank, dev)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     fbank, cnn, tr = build_model(args.d_model, dev)
     g = torch.Generator().manual_seed(1234 + rank)
