@@ -49,6 +49,25 @@ __device__ __forceinline__ float e4m3_to_f32(uint32_t byte) {
   return s ? -v : v;
 }
 
+// max over aligned groups of G consecutive lanes (G = 1, 2, ..., 32), VALU
+// only: DPP row_mirror / row_half_mirror / quad permutes inside 16-lane rows
+// (involutive, so every lane of a group ends with the group max), then
+// v_permlane16_swap to pair rows 0-1 and 2-3 for G = 32.
+template <int G>
+__device__ __forceinline__ float group_max(float v) {
+  static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16 || G == 32, "group size");
+  if (G == 1) return v;
+  if (G >= 16) v = fmaxf(v, dpp_f32<0x140>(v));
+  if (G >= 8) v = fmaxf(v, dpp_f32<0x141>(v));
+  if (G >= 4) v = fmaxf(v, dpp_f32<0x4E>(v));
+  v = fmaxf(v, dpp_f32<0xB1>(v));
+  if (G == 32) {
+    const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+  }
+  return v;
+}
+
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
 }  // namespace sbk

@@ -182,8 +182,48 @@ __global__ void __launch_bounds__(NT) mx_gemm_kernel(MxArgs p) {
     }
   }
 
-  // epilogue straight from the accumulators: C/D of 32x32 tiles,
+  // epilogue from the accumulators: C/D of 32x32 tiles,
   // col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
+  if (OUT == 2) {
+    // MXFP8 output: block amax over the 32 lanes of a tile row (DPP), e4m3
+    // bytes and scales staged in LDS, then written as full 16-B vectors
+    // (byte-wide global stores of the same tile ran ~2x the main loop)
+    constexpr int CS = BN + 16;  // byte row stride of the staged tile
+    uint8_t* Ct = smem;
+    uint8_t* Sc = smem + BM * CS;
+    __syncthreads();  // every wave is done reading the operand stages
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int cl = wn * 64 + j * 32 + fr;
+        const float bv = p.bias ? p.bias[n0 + cl] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          float v = act_f<ACT>(acc[i][j][r] + bv) * p.alpha;
+          if (p.res && m0 + rl < p.M) v += p.res[(long long)(m0 + rl) * p.ldr + n0 + cl];
+          const int sb = mx_scale_byte(group_max<32>(fabsf(v)));
+          const float q = clamp_e4m3(v * mx_inv_scale(sb));
+          Ct[rl * CS + cl] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(q, q, 0, false) & 0xFF);
+          if (fr == 0) Sc[rl * 4 + wn * 2 + j] = (uint8_t)sb;
+        }
+      }
+    }
+    __syncthreads();
+    uint8_t* out = reinterpret_cast<uint8_t*>(p.out);
+#pragma unroll
+    for (int c = tid; c < BM * BN / 16; c += NT) {
+      const int rl = c >> 3, ch = c & 7;
+      if (m0 + rl < p.M)
+        *reinterpret_cast<int4*>(out + (long long)(m0 + rl) * p.ldc + n0 + 16 * ch) =
+            *reinterpret_cast<const int4*>(Ct + rl * CS + 16 * ch);
+    }
+    if (tid < BM && m0 + tid < p.M)
+      *reinterpret_cast<uint32_t*>(p.out_scales + (long long)(m0 + tid) * p.ldso + (n0 >> 5)) =
+          *reinterpret_cast<const uint32_t*>(Sc + tid * 4);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -194,20 +234,8 @@ __global__ void __launch_bounds__(NT) mx_gemm_kernel(MxArgs p) {
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
         float v = act_f<ACT>(acc[i][j][r] + bv) * p.alpha;
-        const bool ok = row < p.M;
-        if (p.res && ok) v += p.res[(long long)row * p.ldr + col];
-        if (OUT == 2) {
-          float am = fabsf(v);
-#pragma unroll
-          for (int s = 1; s < 32; s <<= 1) am = fmaxf(am, __shfl_xor(am, s));
-          const int sb = mx_scale_byte(am);
-          const float q = clamp_e4m3(v * mx_inv_scale(sb));
-          if (ok) {
-            reinterpret_cast<uint8_t*>(p.out)[(long long)row * p.ldc + col] =
-                (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(q, q, 0, false) & 0xFF);
-            if (fr == 0) p.out_scales[(long long)row * p.ldso + (col >> 5)] = (uint8_t)sb;
-          }
-        } else if (ok) {
+        if (row < p.M) {
+          if (p.res) v += p.res[(long long)row * p.ldr + col];
           if (OUT == 1)
             reinterpret_cast<uint16_t*>(p.out)[(long long)row * p.ldc + col] = f32_to_bf16(v);
           else
@@ -248,7 +276,9 @@ SBK_API int sbk_mx_gemm(const uint8_t* A, const uint8_t* SA, long long lda, long
   if ((ldsa | s_bs | ldsw) & 3) return SBK_ERR_ARG;
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(W)) & 15) return SBK_ERR_ARG;
   if ((reinterpret_cast<uintptr_t>(SA) | reinterpret_cast<uintptr_t>(SW)) & 3) return SBK_ERR_ARG;
-  if (out_mode == 2 && !out_scales) return SBK_ERR_ARG;
+  if (out_mode == 2 && (!out_scales || (ldc & 15) || (ldso & 3) ||
+                        ((reinterpret_cast<uintptr_t>(out) & 15) | (reinterpret_cast<uintptr_t>(out_scales) & 3))))
+    return SBK_ERR_ARG;
   if (act != 0 && act != 3 && act != 4) return SBK_ERR_ARG;
   MxArgs p{A, SA, lda, ldsa, rpb, a_bs, s_bs, W, SW, ldw, ldsw, M, N, K, bias, act, alpha, res, ldr,
            out, ldc, out_mode, out_scales, ldso};

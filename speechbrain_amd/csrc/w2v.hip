@@ -153,6 +153,107 @@ __global__ void __launch_bounds__(1024) conv0_kernel(const float* __restrict__ w
   }
 }
 
+// Layer 0, fast form for C = 64*CPL channels (CPL = 1, 2, 4, 8): lane l owns
+// the CPL consecutive channels [l*CPL, l*CPL + CPL) with their K taps in
+// registers, so every LayerNorm statistic is ONE wave reduction (DPP, no
+// LDS, no barrier) and an MXFP8 block of 32 channels is 32/CPL lanes
+// (group_max).  A 256-thread block owns FPW frames per wave; the window of
+// samples all its frames touch is staged (normalised) in LDS once and read
+// as broadcasts.  Each lane stores its CPL outputs of a frame as one 4-/8-B
+// (MXFP8) or CPL*4-B (fp32) vector.
+template <int CPL, int FPW, int KT>  // KT: compile-time tap count (0 = runtime K <= 16)
+__global__ void __launch_bounds__(256) conv0_wave_kernel(const float* __restrict__ wav, const float* __restrict__ stats,
+                                                         long long S, int T0, int K, int stride,
+                                                         const float* __restrict__ w, const float* __restrict__ g,
+                                                         const float* __restrict__ be, float eps,
+                                                         void* __restrict__ out, int out_mode,
+                                                         uint8_t* __restrict__ scales) {
+  extern __shared__ __attribute__((aligned(16))) float xs[];
+  constexpr int C = 64 * CPL, FPB = 4 * FPW;
+  const int nblk_t = (T0 + FPB - 1) / FPB;
+  const int b = blockIdx.x / nblk_t;
+  const int t0 = (blockIdx.x - b * nblk_t) * FPB;
+  const int nr = min(FPB, T0 - t0);
+  const int win = (nr - 1) * stride + K;
+  const float* x = wav + (long long)b * S + (long long)t0 * stride;
+  const float mean = stats ? stats[2 * b] : 0.f, rstd = stats ? stats[2 * b + 1] : 1.f;
+  for (int i = threadIdx.x; i < win; i += blockDim.x) xs[i] = (x[i] - mean) * rstd;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c0 = lane * CPL;
+  constexpr int KM = KT ? KT : 16;
+  if (KT) K = KT;
+  float wk[CPL][KM], gc[CPL], bc[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+#pragma unroll
+    for (int k = 0; k < KM; ++k) wk[j][k] = k < K ? w[(c0 + j) * K + k] : 0.f;
+    gc[j] = g[c0 + j];
+    bc[j] = be[c0 + j];
+  }
+  __syncthreads();
+  const float invC = 1.f / (float)C;
+  for (int f = 0; f < FPW; ++f) {
+    const int r = wv * FPW + f;
+    if (r >= nr) break;
+    const float* xr = xs + r * stride;
+    float v[CPL];
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) v[j] = 0.f;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      if (KT || k < K) {
+        const float xv = xr[k];
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) v[j] = fmaf(wk[j][k], xv, v[j]);
+      }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) s += v[j];
+    const float mu = wave_sum_v(s) * invC;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const float d = v[j] - mu;
+      q = fmaf(d, d, q);
+    }
+    const float rs = rsqrtf(wave_sum_v(q) * invC + eps);
+    float y[CPL];
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) y[j] = gelu_erf((v[j] - mu) * rs * gc[j] + bc[j]);
+    const long long row = (long long)b * T0 + t0 + r;
+    if (out_mode == 2) {
+      float am = 0.f;
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) am = fmaxf(am, fabsf(y[j]));
+      am = group_max<32 / CPL>(am);
+      const int sb = mx_scale_byte(am);
+      const float inv = mx_inv_scale(sb);
+      uint8_t* o = reinterpret_cast<uint8_t*>(out) + row * C + c0;
+      if constexpr (CPL >= 4) {
+#pragma unroll
+        for (int j = 0; j < CPL; j += 4)
+          *reinterpret_cast<uint32_t*>(o + j) = pack4_e4m3(y[j] * inv, y[j + 1] * inv, y[j + 2] * inv, y[j + 3] * inv);
+      } else {
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+          const float qv = clamp_e4m3(y[j] * inv);
+          o[j] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(qv, qv, 0, false) & 0xFF);
+        }
+      }
+      if ((c0 & 31) == 0) scales[row * (C / 32) + (c0 >> 5)] = (uint8_t)sb;
+    } else if (out_mode == 1) {
+      uint16_t* o = reinterpret_cast<uint16_t*>(out) + row * C + c0;
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) o[j] = f32_to_bf16(y[j]);
+    } else {
+      float* o = reinterpret_cast<float*>(out) + row * C + c0;
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) o[j] = y[j];
+    }
+  }
+}
+
 // One wave per row of D = 64*V values; lane l owns the contiguous run
 // [l*V, l*V + V).  ln: LayerNorm with g/b (g null → no LayerNorm);
 // act 0 none, 3 relu, 4 gelu(erf).  in_bf16 selects the input type.
@@ -219,10 +320,7 @@ __global__ void __launch_bounds__(256) ln_act_kernel(const void* __restrict__ x,
       float am = 0.f;
 #pragma unroll
       for (int j = 0; j < BL; ++j) am = fmaxf(am, fabsf(v[nb * BL + j]));
-      if constexpr (V < 32) {
-#pragma unroll
-        for (int s = 1; s < 32 / V; s <<= 1) am = fmaxf(am, __shfl_xor(am, s));
-      }
+      if constexpr (V < 32) am = group_max<32 / V>(am);
       const int sb = mx_scale_byte(am);
       const float inv = mx_inv_scale(sb);
       if constexpr (BL >= 4) {
@@ -313,11 +411,31 @@ SBK_API int sbk_w2v_conv0(const float* wav, const float* stats, int B, long long
   if (B <= 0 || S <= 0 || T0 <= 0 || C <= 0 || C > 1024 || K <= 0 || K > 16 || stride <= 0) return SBK_ERR_ARG;
   if ((long long)(T0 - 1) * stride + K > S) return SBK_ERR_ARG;
   if (out_mode == 2 && ((C % 32) || !scales)) return SBK_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  constexpr int FPW = 32;  // frames per wave: weights loaded once per 128 frames
+  if (C == 64 || C == 128 || C == 256 || C == 512) {
+    const size_t lds = (size_t)((4 * FPW - 1) * stride + K) * sizeof(float);
+    const long long nblk = (long long)B * ((T0 + 4 * FPW - 1) / (4 * FPW));
+#define SBK_CONV0(CPL)                                                                                         \
+  if (K == 11)                                                                                                   \
+    hipLaunchKernelGGL((conv0_wave_kernel<CPL, FPW, 11>), dim3((unsigned)nblk), dim3(256), lds, s, wav, stats, S, \
+                       T0, K, stride, w, g, b, eps, out, out_mode, scales);                                       \
+  else                                                                                                           \
+    hipLaunchKernelGGL((conv0_wave_kernel<CPL, FPW, 0>), dim3((unsigned)nblk), dim3(256), lds, s, wav, stats, S,  \
+                       T0, K, stride, w, g, b, eps, out, out_mode, scales)
+    if (C == 64) SBK_CONV0(1);
+    else if (C == 128) SBK_CONV0(2);
+    else if (C == 256) SBK_CONV0(4);
+    else SBK_CONV0(8);
+#undef SBK_CONV0
+    SBK_CHECK_LAUNCH();
+    return 0;
+  }
   constexpr int R = 16;
   const int threads = ((C + 63) / 64) * 64;
   const size_t lds = (size_t)((R - 1) * stride + K) * sizeof(float);
   const long long nblk = (long long)B * ((T0 + R - 1) / R);
-  hipLaunchKernelGGL(conv0_kernel<R>, dim3((unsigned)nblk), dim3(threads), lds, (hipStream_t)stream, wav, stats, S,
+  hipLaunchKernelGGL(conv0_kernel<R>, dim3((unsigned)nblk), dim3(threads), lds, s, wav, stats, S,
                      T0, C, K, stride, w, g, b, eps, out, out_mode, scales);
   SBK_CHECK_LAUNCH();
   return 0;
