@@ -246,8 +246,214 @@ __global__ void __launch_bounds__(NT) mx_gemm_kernel(MxArgs p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Large-M form: 256 x 128 tile, 8 waves (4 x 2, wave tile 64 x 64), THREE
+// LDS stages with two in flight across each barrier.  The stage fills are
+// inline-asm LDS-DMA pieces (the compiler then sees no LDS write in flight
+// and places no alias-guard vmcnt(0) before the fragment reads), each wave
+// issues exactly 7 per stage (4 A, 2 W, 1 scale dword piece), and the wait
+// that retires stage kt is the counted vmcnt(7) that leaves stage kt+1 in
+// flight, followed by a raw s_barrier (a __syncthreads() would drain it).
+// 2x the W reuse of the 128 x 128 tile; 1 workgroup (8 waves) per CU.
+constexpr int BM2 = 256, NT2 = 512;
+constexpr int SC2 = (BM2 + BN) * 4 + 512;     // A + W scale dwords (+ dummy piece of waves 6-7)
+constexpr int STAGE2 = BM2 * BK + BN * BK + SC2;
+constexpr int NSTAGE2 = 3;
+
+__device__ __forceinline__ void dma(const void* src, void* lds_wave, int bytes16) {
+  const uint32_t la = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)lds_wave));
+  if (bytes16)
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(la) : "memory", "m0");
+  else
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(la) : "memory", "m0");
+}
+
+template <int ACT, int OUT>
+__global__ void __launch_bounds__(NT2) mx_gemm256_kernel(MxArgs p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = wv >> 1, wn = wv & 1;  // 4 x 2 waves
+  const int ntn = p.N / BN, ntm = (p.M + BM2 - 1) / BM2, nt = ntm * ntn;
+  int g = blockIdx.x, tm, tn;
+  if ((ntn & 7) == 0) {
+    // XCD x (= g % 8, the dispatcher's round robin) owns W column tiles
+    // [x*cpx, x*cpx + cpx) for every row tile: its W slice stays resident in
+    // that XCD's L2 and only A streams (each A row block is read once per XCD)
+    const int cpx = ntn >> 3, q = g >> 3;
+    tn = (g & 7) * cpx + q % cpx;
+    tm = q / cpx;
+  } else {
+    if ((nt & 7) == 0) g = (g & 7) * (nt >> 3) + (g >> 3);
+    tm = g / ntn;
+    tn = g - tm * ntn;
+  }
+  const int m0 = tm * BM2, n0 = tn * BN;
+  const int nk = p.K / BK;
+
+  // staging: wave wv moves A rows wv*8 + 64*i + (lane >> 3) (i < 4) and
+  // W rows wv*8 + 64*i + (lane >> 3) (i < 2), chunk lane & 7 (swizzled source)
+  const int lr = lane >> 3, lc = lane & 7;
+  long long aoff[4], woff[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = wv * 8 + 64 * i + lr;
+    aoff[i] = a_row(p, min(m0 + r, p.M - 1)) + 16 * (lc ^ (r & 7));
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = wv * 8 + 64 * i + lr;
+    woff[i] = (long long)(n0 + r) * p.ldw + 16 * (lc ^ (r & 7));
+  }
+  // scale pieces: waves 0-3 A rows 64*wv + lane, waves 4-5 W rows 64*(wv-4) + lane,
+  // waves 6-7 a dummy copy of W row scales into a spare slot (uniform vmcnt)
+  const uint8_t* ssrc;
+  int sdst;
+  if (wv < 4) {
+    ssrc = p.SA + a_srow(p, min(m0 + 64 * wv + lane, p.M - 1));
+    sdst = BM2 * BK + BN * BK + 256 * wv;
+  } else {
+    const int r = 64 * (wv & 1) + lane;
+    ssrc = p.SW + (long long)(n0 + r) * p.ldsw;
+    sdst = BM2 * BK + BN * BK + (wv < 6 ? BM2 * 4 + 256 * (wv - 4) : (BM2 + BN) * 4 + 256 * (wv & 1));
+  }
+
+  auto issue = [&](int kt, int buf) {
+    uint8_t* st = smem + buf * STAGE2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dma(p.A + aoff[i] + (long long)kt * BK, st + (wv * 8 + 64 * i) * BK, 1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) dma(p.W + woff[i] + (long long)kt * BK, st + BM2 * BK + (wv * 8 + 64 * i) * BK, 1);
+    dma(ssrc + kt * 4, st + sdst, 0);
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+
+  const int fr = lane & 31, fh = lane >> 5;
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  for (int kt = 0; kt < nk; ++kt) {
+    // retire stage kt (this wave's pieces), leave stage kt+1 in flight
+    if (kt + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 2 < nk) issue(kt + 2, (kt + 2) % NSTAGE2);
+    const uint8_t* st = smem + (kt % NSTAGE2) * STAGE2;
+    const uint8_t* As = st;
+    const uint8_t* Ws = st + BM2 * BK;
+    const uint32_t* Ss = reinterpret_cast<const uint32_t*>(st + BM2 * BK + BN * BK);
+    uint32_t sa[2], sw[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      sa[i] = Ss[wm * 64 + i * 32 + fr];
+      sw[i] = Ss[BM2 + wn * 64 + i * 32 + fr];
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c0 = 4 * s + fh, c1 = 4 * s + 2 + fh;
+      i32x8 af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int ra = wm * 64 + i * 32 + fr;
+        const int4 x0 = *reinterpret_cast<const int4*>(As + ra * BK + 16 * (c0 ^ (ra & 7)));
+        const int4 x1 = *reinterpret_cast<const int4*>(As + ra * BK + 16 * (c1 ^ (ra & 7)));
+        af[i] = i32x8{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        const int rb = wn * 64 + i * 32 + fr;
+        const int4 y0 = *reinterpret_cast<const int4*>(Ws + rb * BK + 16 * (c0 ^ (rb & 7)));
+        const int4 y1 = *reinterpret_cast<const int4*>(Ws + rb * BK + 16 * (c1 ^ (rb & 7)));
+        bf[i] = i32x8{y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+      }
+      const int sh = 8 * (2 * s + fh);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+              af[i], bf[j], acc[i][j], 0, 0, 0, (int)((sa[i] >> sh) & 0xFF), 0, (int)((sw[j] >> sh) & 0xFF));
+    }
+  }
+
+  if (OUT == 2) {
+    constexpr int CS = BN + 16;
+    uint8_t* Ct = smem;
+    uint8_t* Sc = smem + BM2 * CS;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int cl = wn * 64 + j * 32 + fr;
+        const float bv = p.bias ? p.bias[n0 + cl] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          float v = act_f<ACT>(acc[i][j][r] + bv) * p.alpha;
+          if (p.res && m0 + rl < p.M) v += p.res[(long long)(m0 + rl) * p.ldr + n0 + cl];
+          const int sb = mx_scale_byte(group_max<32>(fabsf(v)));
+          const float q = clamp_e4m3(v * mx_inv_scale(sb));
+          Ct[rl * CS + cl] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(q, q, 0, false) & 0xFF);
+          if (fr == 0) Sc[rl * 4 + wn * 2 + j] = (uint8_t)sb;
+        }
+      }
+    }
+    __syncthreads();
+    uint8_t* out = reinterpret_cast<uint8_t*>(p.out);
+#pragma unroll
+    for (int c = tid; c < BM2 * BN / 16; c += NT2) {
+      const int rl = c >> 3, ch = c & 7;
+      if (m0 + rl < p.M)
+        *reinterpret_cast<int4*>(out + (long long)(m0 + rl) * p.ldc + n0 + 16 * ch) =
+            *reinterpret_cast<const int4*>(Ct + rl * CS + 16 * ch);
+    }
+    if (tid < BM2 && m0 + tid < p.M)
+      *reinterpret_cast<uint32_t*>(p.out_scales + (long long)(m0 + tid) * p.ldso + (n0 >> 5)) =
+          *reinterpret_cast<const uint32_t*>(Sc + tid * 4);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn * 64 + j * 32 + fr;
+      const float bv = p.bias ? p.bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+        float v = act_f<ACT>(acc[i][j][r] + bv) * p.alpha;
+        if (row < p.M) {
+          if (p.res) v += p.res[(long long)row * p.ldr + col];
+          if (OUT == 1)
+            reinterpret_cast<uint16_t*>(p.out)[(long long)row * p.ldc + col] = f32_to_bf16(v);
+          else
+            reinterpret_cast<float*>(p.out)[(long long)row * p.ldc + col] = v;
+        }
+      }
+    }
+  }
+}
+
 template <int ACT>
 int launch_act(const MxArgs& p, hipStream_t s) {
+  if (p.M >= 16 * BM2) {  // enough 256-row tiles to fill the chip
+    const long long nt2 = (long long)((p.M + BM2 - 1) / BM2) * (p.N / BN);
+    const size_t lds2 = NSTAGE2 * STAGE2;
+    switch (p.out_mode) {
+      case 0: hipLaunchKernelGGL((mx_gemm256_kernel<ACT, 0>), dim3((unsigned)nt2), dim3(NT2), lds2, s, p); break;
+      case 1: hipLaunchKernelGGL((mx_gemm256_kernel<ACT, 1>), dim3((unsigned)nt2), dim3(NT2), lds2, s, p); break;
+      default: hipLaunchKernelGGL((mx_gemm256_kernel<ACT, 2>), dim3((unsigned)nt2), dim3(NT2), lds2, s, p); break;
+    }
+    SBK_CHECK_LAUNCH();
+    return 0;
+  }
   const long long nt = (long long)((p.M + BM - 1) / BM) * (p.N / BN);
   const size_t lds = 2 * STAGE;
   switch (p.out_mode) {

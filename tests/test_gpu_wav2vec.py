@@ -35,7 +35,7 @@ def test_mx_quant_matches_emulation(dev):
     assert int(m.s[3, 0]) == 0
 
 
-@pytest.mark.parametrize("M,N,K", [(300, 256, 256), (128, 384, 1024), (77, 128, 128)])
+@pytest.mark.parametrize("M,N,K", [(300, 256, 256), (128, 384, 1024), (77, 128, 128), (4500, 256, 384)])
 def test_mx_gemm_vs_dequantized_product(dev, M, N, K):
     """The block-scaled MFMA GEMM equals the fp64 product of the dequantised
     operands to accumulation accuracy, for the plain, bias+GELU+residual,
