@@ -337,6 +337,12 @@ int sbk_dropout_add(const void* x, int x_bf16, const float* res, long long rows,
                     const unsigned char* rowmask, float alpha, float p, unsigned long long seed, void* out,
                     int out_bf16, void* stream);
 
+/* Transducer decoding step (decoders/transducer.py:137-377): log-softmax of
+ * the joint logits x (R, V) and its top-k per row (ties -> lower index):
+ * vals (R, k) = log-probs, idx (R, k) int64.  k = 1 is the greedy max. */
+int sbk_logsoftmax_topk(const float* x, long long ldx, int R, int V, int k, float* vals, long long* idx,
+                        void* stream);
+
 /* ---- config 5: wav2vec2 latent extractor + TransformerEncoder (MXFP8) ---- */
 
 /* Per-utterance mean / rstd of F.layer_norm(wav, wav.shape[1:]) (wav2vec.py:92-93):

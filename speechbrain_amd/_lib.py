@@ -72,6 +72,7 @@ SIGNATURES = {
     # rnnt.hip
     "sbk_rnnt_forward": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp],
     "sbk_rnnt_workspace_floats": [_i, _i, _i],
+    "sbk_logsoftmax_topk": [_vp, _ll, _i, _i, _i, _vp, _vp, _vp],
     "sbk_rnnt_backward": [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp],
     # attention.hip
     "sbk_relpos_attention": [_i, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _vp],

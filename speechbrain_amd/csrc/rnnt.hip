@@ -272,3 +272,64 @@ SBK_API int sbk_rnnt_backward(const float* x, const int* labels, int B, int T, i
   SBK_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// Transducer decoding (decoders/transducer.py:137-377): log-softmax of the
+// joint logits and their top-k in one pass, one wave per row.  Replaces
+// LogSoftmax → torch.max (greedy, k = 1) / torch.topk (beam) on (rows, V).
+// Ties resolve to the lower vocabulary index.  vals = x[idx] - lse.
+namespace {
+__global__ void __launch_bounds__(256) logsoftmax_topk_kernel(const float* __restrict__ x, long long ldx, int R,
+                                                              int V, int k, float* __restrict__ vals,
+                                                              long long* __restrict__ idx) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= R) return;
+  const int lane = threadIdx.x & 63;
+  const float* xr = x + (long long)row * ldx;
+  float m = -INFINITY;
+  for (int v = lane; v < V; v += 64) m = fmaxf(m, xr[v]);
+  m = wave_max(m);
+  float s = 0.f;
+  for (int v = lane; v < V; v += 64) s += expf(xr[v] - m);
+  const float lse = m + logf(wave_sum(s));
+  int prev_i = -1;
+  float prev_v = INFINITY;
+  for (int j = 0; j < k; ++j) {
+    // next best strictly after (prev_v, prev_i) in (value desc, index asc) order
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int v = lane; v < V; v += 64) {
+      const float xv = xr[v];
+      const bool after = xv < prev_v || (xv == prev_v && v > prev_i);
+      if (after && (xv > bv || (xv == bv && v < bi))) {
+        bv = xv;
+        bi = v;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o);
+      const int oi = __shfl_xor(bi, o);
+      if (ov > bv || (ov == bv && oi < bi)) {
+        bv = ov;
+        bi = oi;
+      }
+    }
+    if (lane == 0) {
+      vals[(long long)row * k + j] = bv - lse;
+      idx[(long long)row * k + j] = bi;
+    }
+    prev_v = bv;
+    prev_i = bi;
+  }
+}
+}  // namespace
+
+SBK_API int sbk_logsoftmax_topk(const float* x, long long ldx, int R, int V, int k, float* vals, long long* idx,
+                                void* stream) {
+  if (R <= 0 || V <= 0 || k <= 0 || k > V) return SBK_ERR_ARG;
+  hipLaunchKernelGGL(logsoftmax_topk_kernel, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x, ldx,
+                     R, V, k, vals, idx);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}

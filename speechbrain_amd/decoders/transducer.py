@@ -1,0 +1,199 @@
+"""Drop-in for speechbrain.decoders.transducer.TransducerBeamSearcher
+(decoders/transducer.py:10-519) on MI355X.
+
+Same constructor, forward and return values as the reference.  What runs
+where:
+  * joint step — the Transducer_joint "sum" kernel (sbk_joint_fwd), the
+    classifier layers (speechbrain_amd Linear on the MFMA GEMM, or whatever
+    modules the recipe passes) and ONE fused log-softmax + top-k kernel
+    (sbk_logsoftmax_topk) instead of LogSoftmax → torch.max / torch.topk;
+  * greedy decode — batched over utterances and fully device-resident: the
+    reference reads every frame's argmax back to the host (`.item()` per
+    utterance per frame) to decide which prediction-network rows to
+    advance; here the PN step runs for the whole batch and a device mask
+    keeps the rows that emitted blank (same result, no host sync inside the
+    T-step loop, so the loop can be graph-captured);
+  * beam search — the reference's host-side hypothesis logic verbatim
+    (state_beam / expand_beam pruning, length-normalised ranking, optional
+    LM fusion), one device→host copy of the k best (log-prob, token) pairs
+    per expansion; scores accumulate in float32 as the reference's tensors do.
+"""
+import numpy as np
+import torch
+
+from .._lib import check, lib, ptr, require_device, stream_of
+
+
+@torch.library.custom_op("sbk::logsoftmax_topk", mutates_args=())
+def logsoftmax_topk(x: torch.Tensor, k: int) -> tuple[torch.Tensor, torch.Tensor]:
+    """x (R, V) logits → (log-probs of the k best (R, k) fp32, their indices (R, k) int64)."""
+    R, V = x.shape
+    vals = torch.empty(R, k, device=x.device, dtype=torch.float32)
+    idx = torch.empty(R, k, device=x.device, dtype=torch.int64)
+    check(lib().sbk_logsoftmax_topk(ptr(x), x.stride(0), R, V, int(k), ptr(vals), ptr(idx), stream_of(x)),
+          "sbk_logsoftmax_topk")
+    return vals, idx
+
+
+@logsoftmax_topk.register_fake
+def _(x, k):
+    return x.new_empty(x.shape[0], k), x.new_empty(x.shape[0], k, dtype=torch.int64)
+
+
+_RNN_NAMES = ["RNN", "LSTM", "GRU", "LiGRU", "LiGRU_Layer"]
+
+
+class TransducerBeamSearcher(torch.nn.Module):
+    def __init__(self, decode_network_lst, tjoint, classifier_network, blank_id, beam_size=4, nbest=5,
+                 lm_module=None, lm_weight=0.0, state_beam=2.3, expand_beam=2.3):
+        super().__init__()
+        self.decode_network_lst = decode_network_lst
+        self.tjoint = tjoint
+        self.classifier_network = classifier_network
+        self.blank_id = blank_id
+        self.beam_size = beam_size
+        self.nbest = nbest
+        self.lm = lm_module
+        self.lm_weight = lm_weight
+        if lm_module is None and lm_weight > 0:
+            raise ValueError("Language model is not provided.")
+        self.state_beam = state_beam
+        self.expand_beam = expand_beam
+        self.softmax = torch.nn.LogSoftmax(dim=-1)
+        if self.beam_size <= 1:
+            self.searcher = self.transducer_greedy_decode
+        else:
+            self.searcher = self.transducer_beam_search_decode
+
+    def forward(self, tn_output):
+        return self.searcher(tn_output)
+
+    # ------------------------------------------------------------ building blocks
+    def _forward_PN(self, out_PN, decode_network_lst, hidden=None):
+        """transducer.py:472-506."""
+        for layer in decode_network_lst:
+            if layer.__class__.__name__ in _RNN_NAMES:
+                out_PN, hidden = layer(out_PN, hidden)
+            else:
+                out_PN = layer(out_PN)
+        return out_PN, hidden
+
+    def _forward_after_joint(self, out, classifier_network):
+        for layer in classifier_network:
+            out = layer(out)
+        return out
+
+    def _joint_topk(self, h_i, out_PN, k):
+        """Joint → classifier → log-softmax → top-k: h_i (B, 1, 1, J), out_PN
+        (B, 1, 1, J) → (log-probs (B, k), tokens (B, k))."""
+        with torch.no_grad():
+            out = self.tjoint(h_i, out_PN)
+            logits = self._forward_after_joint(out, self.classifier_network)
+            logits = logits.reshape(-1, logits.shape[-1])
+            if logits.dtype != torch.float32 or logits.stride(-1) != 1:
+                logits = logits.float().contiguous()
+            return logsoftmax_topk(logits, k)
+
+    def _lm_forward_step(self, inp_tokens, memory):
+        """transducer.py:390-413."""
+        with torch.no_grad():
+            logits, hs = self.lm(inp_tokens, hx=memory)
+            log_probs = self.softmax(logits)
+        return log_probs, hs
+
+    @staticmethod
+    def _select(mask, new, old):
+        """Rows of `new` where mask (B,) else `old` (tensors or LSTM tuples,
+        batch on dim 0 for outputs and dim 1 for RNN hiddens)."""
+        if isinstance(new, tuple):
+            return tuple(TransducerBeamSearcher._select(mask, n, o) for n, o in zip(new, old))
+        return torch.where(mask.view(1, -1, *([1] * (new.dim() - 2))), new, old)
+
+    # ------------------------------------------------------------------ greedy
+    def transducer_greedy_decode(self, tn_output):
+        """transducer.py:137-217, batched and device-resident (see module doc)."""
+        require_device(tn_output)
+        B, T, _ = tn_output.shape
+        dev = tn_output.device
+        input_PN = torch.full((B, 1), self.blank_id, device=dev, dtype=torch.int32)
+        out_PN, hidden = self._forward_PN(input_PN, self.decode_network_lst)
+        tokens = torch.empty(B, T, device=dev, dtype=torch.int64)
+        emitted = torch.empty(B, T, device=dev, dtype=torch.bool)
+        score = torch.zeros(B, device=dev, dtype=torch.float32)
+        for t in range(T):
+            lp, pos = self._joint_topk(tn_output[:, t, :].unsqueeze(1).unsqueeze(1), out_PN.unsqueeze(1), 1)
+            lp, pos = lp[:, 0], pos[:, 0]
+            upd = pos != self.blank_id
+            tokens[:, t] = pos
+            emitted[:, t] = upd
+            score = score + torch.where(upd, lp, torch.zeros_like(lp))
+            input_PN = torch.where(upd.view(B, 1), pos.to(torch.int32).view(B, 1), input_PN)
+            new_out, new_hidden = self._forward_PN(input_PN, self.decode_network_lst, hidden)
+            out_PN = torch.where(upd.view(B, *([1] * (out_PN.dim() - 1))), new_out, out_PN)
+            hidden = self._select(upd, new_hidden, hidden)
+        tk, em = tokens.cpu().numpy(), emitted.cpu().numpy()
+        predictions = [[int(v) for v in tk[b][em[b]]] for b in range(B)]
+        return predictions, score.cpu().exp().mean(), None, None
+
+    # -------------------------------------------------------------------- beam
+    def transducer_beam_search_decode(self, tn_output):
+        """transducer.py:219-377 (per utterance, host-side hypothesis logic)."""
+        require_device(tn_output)
+        f32 = np.float32
+        nbest_batch, nbest_batch_score = [], []
+        dev = tn_output.device
+        for i_batch in range(tn_output.size(0)):
+            input_PN = torch.full((1, 1), self.blank_id, device=dev, dtype=torch.int32)
+            hyp = {"prediction": [self.blank_id], "logp_score": f32(0.0), "hidden_dec": None}
+            if self.lm_weight > 0:
+                hyp["hidden_lm"] = None
+            beam_hyps = [hyp]
+            for t_step in range(tn_output.size(1)):
+                process_hyps = beam_hyps
+                beam_hyps = []
+                while True:
+                    if len(beam_hyps) >= self.beam_size:
+                        break
+                    a_best_hyp = max(process_hyps, key=lambda x: f32(x["logp_score"] / f32(len(x["prediction"]))))
+                    if len(beam_hyps) > 0:
+                        b_best_hyp = max(beam_hyps, key=lambda x: f32(x["logp_score"] / f32(len(x["prediction"]))))
+                        if b_best_hyp["logp_score"] >= self.state_beam + a_best_hyp["logp_score"]:
+                            break
+                    process_hyps.remove(a_best_hyp)
+                    input_PN[0, 0] = a_best_hyp["prediction"][-1]
+                    out_PN, hidden = self._forward_PN(input_PN, self.decode_network_lst, a_best_hyp["hidden_dec"])
+                    lp, pos = self._joint_topk(tn_output[i_batch, t_step, :].view(1, 1, 1, -1),
+                                               out_PN.unsqueeze(0), self.beam_size)
+                    if self.lm_weight > 0:
+                        log_probs_lm, hidden_lm = self._lm_forward_step(input_PN, a_best_hyp["hidden_lm"])
+                    lp = lp[0].cpu().numpy().astype(f32)
+                    pos = [int(v) for v in pos[0].cpu()]
+                    best_logp = lp[0] if pos[0] != self.blank_id else lp[1]
+                    for j in range(len(lp)):
+                        topk_hyp = {"prediction": a_best_hyp["prediction"][:],
+                                    "logp_score": f32(a_best_hyp["logp_score"] + lp[j]),
+                                    "hidden_dec": a_best_hyp["hidden_dec"]}
+                        if pos[j] == self.blank_id:
+                            beam_hyps.append(topk_hyp)
+                            if self.lm_weight > 0:
+                                topk_hyp["hidden_lm"] = a_best_hyp["hidden_lm"]
+                            continue
+                        if lp[j] >= best_logp - f32(self.expand_beam):
+                            topk_hyp["prediction"].append(pos[j])
+                            topk_hyp["hidden_dec"] = hidden
+                            if self.lm_weight > 0:
+                                topk_hyp["hidden_lm"] = hidden_lm
+                                topk_hyp["logp_score"] = f32(topk_hyp["logp_score"] + f32(
+                                    self.lm_weight * float(log_probs_lm[0, 0, pos[j]])))
+                            process_hyps.append(topk_hyp)
+            nbest_hyps = sorted(beam_hyps, key=lambda x: f32(x["logp_score"] / f32(len(x["prediction"]))),
+                                reverse=True)[: self.nbest]
+            all_predictions, all_scores = [], []
+            for h in nbest_hyps:
+                all_predictions.append(h["prediction"][1:])
+                all_scores.append(torch.tensor(f32(h["logp_score"] / f32(len(h["prediction"])))))
+            nbest_batch.append(all_predictions)
+            nbest_batch_score.append(all_scores)
+        return ([nb[0] for nb in nbest_batch],
+                torch.Tensor([float(s[0]) for s in nbest_batch_score]).exp().mean(),
+                nbest_batch, nbest_batch_score)

@@ -36,6 +36,9 @@ Fixture inventory (all float32 unless noted):
                    (lobes/models/wav2vec.py:28-106,153-227,
                    lobes/models/transformer/Transformer.py:201-486,
                    nnet/attention.py:642-778)
+  decoder.npz      TransducerBeamSearcher greedy and beam search on a small
+                   random one-hot-Embedding / GRU / Linear transducer
+                   (decoders/transducer.py:10-519)
   train.npz        gradients of sum(R * encode(cnn(feats), wav_len)) w.r.t.
                    every ConvolutionFrontEnd / TransformerASR parameter and
                    the input features (reference autograd, weights of
@@ -421,7 +424,56 @@ def gen_wav2vec():
     np.savez_compressed(os.path.join(OUT, "wav2vec.npz"), **out)
 
 
+def gen_decoder():
+    """TransducerBeamSearcher (decoders/transducer.py:10-519) on a small random
+    Conformer-Transducer-shaped decoder: one-hot Embedding → GRU → Linear PN,
+    "sum" joint + LeakyReLU, Linear classifier; greedy and beam search."""
+    import speechbrain as sb
+    from speechbrain.decoders.transducer import TransducerBeamSearcher
+    from speechbrain.nnet.transducer.transducer_joint import Transducer_joint
+    out = {}
+    V, J, H, B, T = 7, 16, 10, 3, 12
+    torch.manual_seed(9)
+    emb = sb.nnet.embedding.Embedding(num_embeddings=V, consider_as_one_hot=True, blank_id=0)
+    dec = sb.nnet.RNN.GRU(hidden_size=H, input_shape=(1, 4, V - 1), bidirectional=False)
+    dec_lin = sb.nnet.linear.Linear(input_shape=(1, 4, H), n_neurons=J, bias=False)
+    tjoint = Transducer_joint(joint="sum", nonlinearity=torch.nn.LeakyReLU)
+    cls = sb.nnet.linear.Linear(input_shape=(1, 1, 1, J), n_neurons=V)
+    # blank bias per mode: +1.5 gives the greedy decode plenty of emissions;
+    # the beam search (no max-symbols-per-frame bound in the reference) only
+    # terminates reasonably when blank is usually in the top-k: +3.0
+    bias0 = cls.w.bias.detach().clone()
+    for name, m in (("emb", emb), ("dec", dec), ("dec_lin", dec_lin), ("cls", cls)):
+        for k, v in m.state_dict().items():
+            out[f"{name}.{k}"] = t2n(v)
+    g = torch.Generator().manual_seed(10)
+    tn = 2.0 * torch.randn(B, T, J, generator=g)
+    out["tn"] = t2n(tn)
+    for beam, tag, db in ((1, "greedy", 1.5), (3, "beam", 3.0)):
+        with torch.no_grad():
+            cls.w.bias.copy_(bias0)
+            cls.w.bias[0] += db
+        out[f"{tag}_cls_bias"] = t2n(cls.w.bias)
+        searcher = TransducerBeamSearcher(decode_network_lst=[emb, dec, dec_lin], tjoint=tjoint,
+                                          classifier_network=[cls], blank_id=0, beam_size=beam, nbest=2,
+                                          lm_module=None, lm_weight=0.0, state_beam=2.3, expand_beam=2.3)
+        with torch.no_grad():
+            hyps, score, nbest, nbest_scores = searcher(tn)
+        out[f"{tag}_score"] = np.asarray(float(score), np.float64)
+        for b in range(B):
+            out[f"{tag}_hyp{b}"] = np.asarray(hyps[b], np.int64)
+        if nbest is not None:
+            for b in range(B):
+                for i, (h, sc) in enumerate(zip(nbest[b], nbest_scores[b])):
+                    out[f"{tag}_nbest{b}_{i}"] = np.asarray(h, np.int64)
+                    out[f"{tag}_nbest_score{b}_{i}"] = np.asarray(float(sc), np.float64)
+    np.savez_compressed(os.path.join(OUT, "decoder.npz"), **out)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["decoder"]:
+        gen_decoder()
+        sys.exit(0)
     if sys.argv[1:] == ["wav2vec"]:
         gen_wav2vec()
         sys.exit(0)
@@ -438,6 +490,7 @@ if __name__ == "__main__":
     gen_train()
     gen_inputnorm()
     gen_wav2vec()
+    gen_decoder()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))
