@@ -61,6 +61,14 @@ def gemm(a, w, bias=None, act=None, slope=0.0, res=None, alpha=1.0, rowmask=None
         raise ValueError("gemm operands must be K-contiguous")
     if res is not None and (res.dtype != _f32 or res.stride(-1) != 1):
         raise ValueError("residual must be fp32, row-contiguous")
+    vec = 8 if a.dtype == _bf16 else 4
+    if (a.shape[1] % vec or a.stride(0) % vec or w.stride(0) % vec
+            or (a.data_ptr() | w.data_ptr()) % 16):
+        # the MFMA tiles read K in 16-B vectors: zero-pad K (odd widths such
+        # as a 10-unit prediction-network GRU; the hot-path shapes never pad)
+        Kp = -(-a.shape[1] // vec) * vec
+        a = torch.nn.functional.pad(a, (0, Kp - a.shape[1]))
+        w = torch.nn.functional.pad(w, (0, Kp - w.shape[1]))
     return torch.ops.sbk.gemm(a, w, bias, ACT[act], float(slope), res, float(alpha), rowmask,
                               out_dtype == _bf16, int(tile))
 
