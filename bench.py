@@ -277,6 +277,112 @@ def launch_plumbing(args):
         dist.destroy_process_group()
 
 
+# ----------------------------------------------------------------- config 2
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+
+
+def run_c2(args, world, rank, dev):
+    """BASELINE config 2: the feature kernels on synthetic
+    16 kHz B=32 x 15 s — Fbank(n_mels=80) with Δ and ΔΔ (one stencil kernel:
+    [x | Δ | ΔΔ], 240 dims), then SpecAugment with the recipe parameters
+    (conformer_small.yaml:252-262; host draws from the CPU generator, seed
+    1234+step, as the reference), in place.  HBM-bound: the roofline is GB/s
+    of algorithmic bytes against 8 TB/s."""
+    from speechbrain_amd import ops
+    from speechbrain_amd.lobes.augment import SpecAugment
+    from speechbrain_amd.lobes.features import Fbank
+    fb = Fbank(sample_rate=SR, n_fft=400, n_mels=80).to(dev)
+    sa = SpecAugment(time_warp=True, time_warp_window=5, time_warp_mode="bicubic", freq_mask=True,
+                     freq_mask_width=(0, 30), n_freq_mask=2, time_mask=True, time_mask_width=(0, 40), n_time_mask=2,
+                     replace_with_zero=False)
+    g = torch.Generator().manual_seed(1234 + rank)
+    wav = (0.1 * torch.randn(args.batch, int(SR * SECONDS), generator=g)).to(dev)
+    it = [0]
+
+    def step():
+        torch.manual_seed(1234 + it[0])
+        it[0] += 1
+        with torch.no_grad():
+            feats = fb(wav)
+            feats = ops.deltas(feats, 5, True)
+            return sa(feats)
+    out = step()
+    B, T, F3 = out.shape
+    elapsed, rank_ms = time_steps(step, args.steps, args.warmup, world, dev)
+    ms_per_step = 1000.0 * elapsed / args.steps
+    value = world * args.batch * SECONDS * args.steps / elapsed
+    if rank != 0:
+        return
+    # per-kernel: each op alone, back to back, HIP events on the launch stream
+    f80 = fb(wav)
+    d240 = ops.deltas(f80, 5, True)
+    S = wav.shape[1]
+    kern = []
+    traffic = load_traffic()
+    for name, fn, nbytes, pmc in (
+            ("spec_static_kernel + topdb_clamp (Fbank)", lambda: fb(wav), 4.0 * B * S + 4.0 * B * T * 80,
+             ("spec_static_kernel<2, 200, 8, 320>", "topdb_clamp_kernel")),
+            ("deltas_kernel (x|Δ|ΔΔ)", lambda: ops.deltas(f80, 5, True), 4.0 * B * T * 80 + 4.0 * B * T * 240,
+             ("deltas_kernel<true>",)),
+            ("specaugment (warp + masks + mean fill)", lambda: sa(d240), 2 * 4.0 * B * T * 240,
+             ("warp_kernel", "apply_kernel"))):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 20
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        us = 1000.0 * e0.elapsed_time(e1) / reps
+        tr = [traffic.get(k) for k in pmc]
+        kern.append({"kernel": name, "us": round(us, 2), "algorithmic_bytes": int(nbytes),
+                     "traffic": sum(tr) if all(v is not None for v in tr) else None,
+                     "achieved": round(nbytes / (us * 1e-6) / 1e9, 1), "unit": "GB/s",
+                     "frac": round(nbytes / (us * 1e-6) / 1e9 / PEAK_HBM_GBS, 4)})
+    dom = max(kern, key=lambda k: k["us"])
+    res = {
+        "metric": "audio-sec/sec STFT+Filterbank+Deltas+SpecAugment (16kHz, B=32x15s)",
+        "value": round(value, 1), "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "rank_ms_per_step": rank_ms,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (0.1·N(0,1) 16 kHz)",
+        "config": {"workload": f"C2: Fbank(80) → Δ/ΔΔ (240) → SpecAugment(recipe, in place), B={args.batch}×15s "
+                               f"per GPU, eager (host mask draws per step)",
+                   "global_batch": world * args.batch, "seq_len": T, "parallelism": f"replicas{world}"},
+        "roofline": {"bound": "hbm", "kernel": dom["kernel"], "achieved": dom["achieved"], "peak": PEAK_HBM_GBS,
+                     "unit": "GB/s", "frac": dom["frac"], "traffic": dom["traffic"],
+                     "avg_launch_us": dom["us"], "other_kernels": [k for k in kern if k is not dom]},
+    }
+    if not args.no_cpu_baseline and world == 1:
+        res["cpu_baseline"] = cpu_baseline_c2(args.batch)
+    print(json.dumps(res), flush=True)
+
+
+def cpu_baseline_c2(batch, n_utt=4, reps=3):
+    """Oracle (numpy/PyTorch CPU restatement) of the same C2 step on n_utt x 15 s."""
+    import oracle.augment as OA
+    import oracle.features as OF
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    wav = 0.1 * torch.randn(n_utt, int(SR * SECONDS), generator=torch.Generator().manual_seed(0))
+    times = []
+    for r in range(reps + 1):
+        t0 = time.perf_counter()
+        d = OF.fbank(wav, deltas_on=True, n_mels=80)
+        torch.manual_seed(1234)
+        OA.spec_augment(d, time_warp_window=5, freq_mask_width=(0, 30), time_mask_width=(0, 40),
+                        replace_with_zero=False)
+        if r:
+            times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {"value": round(n_utt * SECONDS / med, 2), "unit": "audio-sec/sec", "cores": threads, "kind": "port",
+            "sample": f"{n_utt} utt x 15 s synthetic, fp32, median of {reps} after 1 warm-up"}
+
+
 # ----------------------------------------------------------------- config 5
 C5_LAYERS, C5_D, C5_H, C5_FFN = 24, 1024, 16, 4096
 PEAK_MXFP8_TFLOPS = 5000.0  # MI355X dense FP8 (block-scaled MFMA), MI355X_MICROARCH.md
@@ -470,8 +576,9 @@ def main():
     ap.add_argument("--batch", type=int, default=BATCH)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--config", choices=["c3", "c5"], default="c3",
-                    help="c3: Fbank→Conformer (the BASELINE metric, default); c5: wav2vec2 + 24L TransformerEncoder")
+    ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c3",
+                    help="c3: Fbank→Conformer (the BASELINE metric, default); c2: feature kernels "
+                         "(Fbank, Δ/ΔΔ, SpecAugment); c5: wav2vec2 + 24L TransformerEncoder")
     ap.add_argument("--precision", choices=["mxfp8", "bf16"], default="mxfp8", help="config 5 GEMM precision")
     ap.add_argument("--plumbing", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -487,8 +594,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
         assert dist.get_world_size() == args.gpus
-    if args.config == "c5":
-        run_c5(args, world, rank, dev)
+    if args.config in ("c2", "c5"):
+        (run_c2 if args.config == "c2" else run_c5)(args, world, rank, dev)
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()
