@@ -168,6 +168,16 @@ int sbk_ffn(const float* x, int M, int D, int H, const float* g0, const float* b
             const float* bp, float epsp, float* out, const float* gn, const float* bn, float epsn, void* u,
             int u_bf16, void* stream);
 
+/* sbk_ffn with a projection tail: with wp (np, D) bf16, np % 256 == 0, the
+ * next-LN output is not written (u must be null) but projected on chip:
+ * yp (M, np) bf16 = LNn(out) wp^T — the following MHSA's in_proj
+ * (attention.py:549-553, Conformer.py:186-197), replacing its QKV GEMM
+ * launch.  wp == null behaves as sbk_ffn. */
+int sbk_ffn_proj(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0, const void* w1,
+                 const float* b1, int act, float slope, const void* w2, const float* b2, float alpha,
+                 const float* gp, const float* bp, float epsp, float* out, const float* gn, const float* bn,
+                 float epsn, void* u, int u_bf16, const void* wp, int np, void* yp, void* stream);
+
 /* LayerNorm (normalization.py:172-223; Conformer.py:178,194,340): one or two
  * chained LayerNorms over rows of x (M, D) fp32, D <= 1024. */
 int sbk_layernorm(const float* x, int M, int D, const float* g1, const float* b1, float eps1, void* out1,

@@ -8,7 +8,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import speechbrain_amd._lib as _L  # noqa: E402
-_L.LIB_PATH = os.environ["SBK_PROBE_LIB"]
+_L.LIB_PATH = os.path.abspath(os.environ["SBK_PROBE_LIB"])
 from speechbrain_amd.lobes.models.transformer.Conformer import ConvolutionModule  # noqa: E402
 
 dev = torch.device("cuda")

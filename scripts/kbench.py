@@ -11,7 +11,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import speechbrain_amd._lib as _L  # noqa: E402
 if os.environ.get("SBK_PROBE_LIB"):
-    _L.LIB_PATH = os.environ["SBK_PROBE_LIB"]  # probe builds of a kernel (not product)
+    _L.LIB_PATH = os.path.abspath(os.environ["SBK_PROBE_LIB"])  # probe builds of a kernel (not product)
 from speechbrain_amd import _enc  # noqa: E402
 from speechbrain_amd._lib import lib, ptr, stream_of  # noqa: E402
 
@@ -150,6 +150,12 @@ def ffn_bench():
             us2 = timeit(lambda: ffn.run(u, torch.bfloat16, residual=x, alpha=0.5))
         fl = 4.0 * M * D * H
         print(f"ffn D={D} H={H} M={M}: fused {us:.1f}us {fl / us / 1e6:.0f} TF/s | 2 gemms {us2:.1f}us", flush=True)
+        wp = (torch.randn(768, D, device=dev) / 16).to(torch.bfloat16)
+        with torch.no_grad():
+            us3 = timeit(lambda: ffn.run_fused_proj(x, ln, 0.5, ln, wp))
+            u = ffn.run_fused(x, ln, 0.5, next_ln=ln)[1]
+            us4 = timeit(lambda: _enc.gemm(u, wp, out_dtype=torch.bfloat16))
+        print(f"ffn+qkv D={D} H={H}: fused {us3:.1f}us | ffn {us:.1f}us + qkv gemm {us4:.1f}us", flush=True)
 
 
 if __name__ == "__main__":

@@ -199,6 +199,41 @@ def _(x, g0, b0, e0, w1, b1, act, slope, w2, b2, alpha, gp, bp, ep, gn, bn, en, 
             x.new_empty(x.shape, dtype=_bf16 if next_bf16 else _f32) if gn is not None else x.new_empty(0))
 
 
+@torch.library.custom_op("sbk::ffn_proj", mutates_args=())
+def _ffn_proj_op(x: torch.Tensor, g0: torch.Tensor, b0: torch.Tensor, e0: float, w1: torch.Tensor,
+                 b1: torch.Tensor, act: int, slope: float, w2: torch.Tensor, b2: torch.Tensor, alpha: float,
+                 gp: Optional[torch.Tensor], bp: Optional[torch.Tensor], ep: float, gn: torch.Tensor,
+                 bn: torch.Tensor, en: float, wp: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    M, D = x.shape
+    H, NP = w1.shape[0], wp.shape[0]
+    out = torch.empty_like(x)
+    y = torch.empty(M, NP, device=x.device, dtype=_bf16)
+    rc = lib().sbk_ffn_proj(ptr(x), M, D, H, ptr(g0), ptr(b0), float(e0), ptr(w1), ptr(b1), act, float(slope),
+                            ptr(w2), ptr(b2), float(alpha), ptr(gp), ptr(bp), float(ep), ptr(out), ptr(gn), ptr(bn),
+                            float(en), None, 1, ptr(wp), NP, ptr(y), stream_of(x))
+    check(rc, "sbk_ffn_proj")
+    return out, y
+
+
+@_ffn_proj_op.register_fake
+def _(x, g0, b0, e0, w1, b1, act, slope, w2, b2, alpha, gp, bp, ep, gn, bn, en, wp):
+    return torch.empty_like(x), x.new_empty((x.shape[0], wp.shape[0]), dtype=_bf16)
+
+
+def ffn_proj_supported(D, H, NP):
+    return ffn_supported(D, H) and NP > 0 and NP % 256 == 0
+
+
+def ffn_proj(x, ln0, w1, b1, act, slope, w2, b2, alpha, next_ln, wp, post_ln=None):
+    """sbk_ffn with the following block's input projection fused on chip:
+    returns (out fp32, next_ln(out) · wp^T in bf16).  wp: (NP, D) bf16, no
+    bias (RelPosMHAXL's in_proj)."""
+    require_device(x, w1, w2, wp)
+    gp, bp, ep = post_ln if post_ln is not None else (None, None, 0.0)
+    return torch.ops.sbk.ffn_proj(x, ln0[0], ln0[1], float(ln0[2]), w1, b1, ACT[act], float(slope), w2, b2,
+                                  float(alpha), gp, bp, float(ep), next_ln[0], next_ln[1], float(next_ln[2]), wp)
+
+
 def ffn(x, ln0, w1, b1, act, slope, w2, b2, alpha, post_ln=None, next_ln=None, next_dtype=_bf16, out=None):
     """Fused macaron FFN block (bf16 MFMA): z = x + alpha * FFN(LN0(x));
     out = post_ln(z) if given; u = next_ln(out) (returned) if given.

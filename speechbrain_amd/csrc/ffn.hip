@@ -9,39 +9,48 @@
 // Dropout), 0.5-scaled residuals, norm2 after the second FFN) and
 // speechbrain/nnet/attention.py:823-839 (PositionalwiseFeedForward).
 //
+// Optional projection tail (sbk_ffn_proj): y = u · Wp^T in bf16 — the
+// MHSA in_proj of the next block (attention.py:549-553, RelPosMHAXL has no
+// in_proj bias) — so u never leaves the CU and the QKV GEMM is no launch of
+// its own.
+//
 // Design (MI355X): one workgroup (8 waves) owns BM = 48 rows for
 // the whole block, so neither LN0(x) nor the (BM x H) hidden activation ever
 // leaves the CU:
-//   prologue : x rows (fp32) -> LayerNorm -> bf16 Xn, resident in LDS; b1 -> LDS;
+//   prologue : x rows (fp32) -> LayerNorm -> bf16 Xn; its MFMA fragments are
+//              then held in VGPRs (96 per lane) for every phase-1 step; b1 -> LDS;
 //   per chunk of HC = 256 hidden units (8 K-steps of 64):
 //     phase 1: Hc^T = W1[c]·Xn^T  -> +b1, act -> bf16 Hs (LDS);
 //     phase 2: acc2^T += W2[:, c]·Hs^T  (accumulators stay in VGPRs);
 //   epilogue : +b2, alpha, residual, optional post-LN and next-LN over the
-//              full rows (cross-wave reduction through LDS), float4 stores.
+//              full rows (cross-wave reduction through LDS), float4 stores;
+//   tail     : (projection) u -> Xn -> VGPR fragments, K1 steps per 256
+//              output columns of Wp through the same ring, bf16 stores.
 // Weight tiles (256 rows x 64 k = 32 KB) stream L2 -> LDS by LDS-DMA
-// (global_load_lds_dwordx4: full 128-B lines, no VGPRs) into a 3-slot ring,
-// two tiles in flight (counted vmcnt).  Each wave stages only the weight rows it
-// multiplies, so the ring steps need no workgroup barrier.
+// (global_load_lds_dwordx4: full 128-B lines, no VGPRs) into a 2-slot ring,
+// one tile in flight behind the one being read (counted vmcnt; the last FFN
+// steps already fetch the projection's first tiles).  Each wave stages only
+// the weight rows it multiplies, so the ring steps need no workgroup barrier.
 // The ring image is lane-linear; bank conflicts are removed by XOR-swizzling
 // the 16-B chunk index with (row >> 1) & 7 on the global source address and
-// on the fragment reads.  Per workgroup the 2·D·H weight bytes cross L2 once;
-// HBM traffic per row: D fp32 in + D fp32 out (+ D u out).
-// Bound: every workgroup streams all 2·D·H weight bytes (1 MB at D=256,
-// H=1024) through its CU; at ~25-30 GB/s per CU of L2->LDS-DMA this per-CU
-// stream, not MFMA (~12 % busy) or HBM, sets the time.
-// Tried and slower: 8-wave register-staged ring (48 us), 4 waves (69 us),
-// fragment-shaped loads straight to VGPRs (64 us), row-owner waves with the
-// hidden chunk in registers (78 us).  A shared 3-slot ring with a barrier per
-// K-step took 42 us; wave-private rows (no per-step barrier), a 2-slot ring
-// and chunk-parity Hs: 35 us (M = 12032, H = 1024; 8 waves the same).
-// 8 waves with the LayerNorm'd rows held in VGPRs for every phase-1 step
-// (SBK_FFN_XREG, default): 36.7 -> 31.9 us at H = 1024, 58.2 -> 48.5 at 2048.
-// Also tried (compile-time options, off): a per-XCD rotated hidden-chunk order
-// (SBK_FFN_ROT, 34.4 -> 35.0 us) and a 3-slot ring with a single hidden buffer
-// (SBK_FFN_NB3, 37.2 us).  Neither L2 channel contention nor in-flight bytes
-// is the limit; the LDS traffic is: per 64-deep step the 16 waves read
-// 8 KB of fragments each (6 KB of it the shared activation tile) besides
-// the 32 KB DMA fill, ~1,250 LDS cycles per step.
+// on the fragment reads.  HBM traffic per row: D fp32 in + D fp32 out (+ D u
+// out, or np bf16 projection outputs).
+//
+// Measured (M = 12032, H = 1024, s_memtime timeline of one workgroup of 251):
+// prologue 10.6k cycles (x rows from HBM in lockstep with every other CU,
+// then tile 0), 32 K-steps of ~650-700 cycles (12 MFMAs = 192 issue cycles
+// per wave, 2 waves per SIMD; ~110 GB/s of weights into the CU, the DMA
+// wait < 80 cycles), +1,400 on each chunk's activation step (Swish on 24
+// values per lane: VALU), epilogue 8.3k (18 MB of out/u stores from every CU
+// at once: HBM).  H = 2048 adds 0.5 us per K-step, so ~14 us of the 29.6 us
+// launch is the fixed prologue/epilogue/launch cost, not the weight stream.
+// Tried and slower or equal: 8-wave register-staged ring (48 us), 4 waves
+// (69 us), fragment-shaped loads straight to VGPRs (64 us), row-owner waves
+// with the hidden chunk in registers (78 us), a shared 3-slot ring with a
+// barrier per K-step (42 us), LN'd rows re-read from LDS each step instead
+// of VGPRs (36.7 us), a per-XCD rotated chunk order (35.0 us), a 3-slot ring
+// with one hidden buffer (37.2 us), a third slot aliased onto Xn after the
+// VGPR load (30.3 us), a tile-contiguous weight image (29.3 us).
 #include "mfma.h"
 
 using namespace sbk;
@@ -69,6 +78,9 @@ struct FfnArgs {
   float epsn;
   void* u;
   int u_bf16;
+  const bf16_t* wp;  // (np, D) projection of next-LN(out), or null
+  int np;
+  bf16_t* yp;  // (M, np) bf16
 };
 
 __device__ __forceinline__ bf16x8 ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
@@ -79,13 +91,7 @@ struct IntC {
 };
 
 constexpr int FFN_BM = 48;
-#ifndef SBK_FFN_NW
-#define SBK_FFN_NW 8
-#endif
-#ifndef SBK_FFN_NO_XREG
-#define SBK_FFN_XREG  // LN'd rows held in VGPRs (needs the 8-wave budget: 226 VGPRs, 2 waves/SIMD)
-#endif
-constexpr int FFN_NW = SBK_FFN_NW, FFN_NT = FFN_NW * 64;
+constexpr int FFN_NW = 8, FFN_NT = FFN_NW * 64;  // 8 waves: LN'd rows fit in VGPRs (2 waves/SIMD)
 
 template <int ACT>
 __device__ __forceinline__ float act_fn(float v, float slope) {
@@ -184,7 +190,7 @@ __device__ unsigned long long g_ffn_tl[16][80];
   } while (0)
 #endif
 
-template <int D, int ACT>
+template <int D, int ACT, bool PROJ>
 __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   constexpr int BM = FFN_BM, HC = 256, NW = FFN_NW, NT = FFN_NT;
   constexpr int XS = D + 16, HS = HC + 16;   // LDS row strides (elements), +32 B pad: conflict-free b128 reads
@@ -192,15 +198,9 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   constexpr int T = 256 / 16 / FFN_NW;       // 16-row weight tiles per wave (HC/16/NW = D/16/NW)
   constexpr int BK = 64;                     // K per step: one 128-B line per weight row
   constexpr int K1 = D / BK, K2 = HC / BK, SPC = K1 + K2;
-#ifdef SBK_FFN_NB3
-  constexpr int NB = 3;                      // ring slots, two tiles in flight behind the one being read
-  constexpr int HSB = 1;                     // single hidden buffer (LDS for the third slot)
-#else
   constexpr int NB = 2;                      // ring slots: a slot is refilled as soon as its fragments are in VGPRs
-  constexpr int HSB = 2;                     // hidden chunk double-buffered by chunk parity
-#endif
-  constexpr int TROWS = 256;                 // rows per weight tile (HC for W1, D for W2)
-  constexpr int GL = TROWS * BK * 2 / 16 / NT;  // LDS-DMA instructions per thread per tile (2)
+  constexpr int TROWS = 256;                 // rows per weight tile (HC for W1, D for W2, 256 output columns of Wp)
+  constexpr int GL = TROWS * BK * 2 / 16 / NT;  // LDS-DMA instructions per thread per tile (4)
   static_assert(GL * 8 == T * 16, "each wave stages exactly the weight rows it multiplies");
   constexpr int PER = D / 64;                // LN: floats per lane (4)
   static_assert(PER == 4 && D == 256 && HC / 16 / NW == T && D / 16 / NW == T, "shape");
@@ -208,23 +208,17 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* ring = reinterpret_cast<bf16_t*>(smem);          // NB x TROWS x BK (linear 128-B rows)
   bf16_t* Xn = ring + NB * TROWS * BK;                      // BM x XS
-  bf16_t* Hs = Xn + BM * XS;                                // BM x HS
-  float* b1s = reinterpret_cast<float*>(Hs + HSB * BM * HS);  // H          (Hs: HSB x BM x HS)
+  bf16_t* Hs = Xn + BM * XS;                                // 2 x BM x HS
+  float* b1s = reinterpret_cast<float*>(Hs + 2 * BM * HS);  // H
   float (*red)[BM] = reinterpret_cast<float (*)[BM]>(b1s + a.H);  // NW x BM
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int fr = lane & 15, g = lane >> 4, fk = 8 * g;
   const int m0 = blockIdx.x * BM;
   const int NCH = a.H / HC;
-  const int S = NCH * SPC;
-#ifdef SBK_FFN_ROT
-  // hidden chunks in a per-workgroup rotated order: the workgroups of one XCD
-  // (blockIdx = xcd mod 8) start on different weight chunks, so their
-  // concurrent L2 reads spread over different lines/channels
-  const int rot = (blockIdx.x >> 3) % NCH;
-#else
-  const int rot = 0;
-#endif
+  const int S = NCH * SPC;                              // FFN K-steps
+  const int SP = PROJ ? (a.np / TROWS) * K1 : 0;        // projection K-steps
+  const int ST = S + SP;
 #ifdef SBK_PROBE_TL
   const int tl_rec = blockIdx.x == 128 ? w : -1;
 #endif
@@ -255,17 +249,22 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   // ---- weight tile s -> ring slot (LDS-DMA, 1 KB = 8 rows per wave-instruction)
   // lane L of instruction i writes row R0 + L/8, 16-B chunk L%8 (linear image)
   // and fetches source chunk (L%8) ^ ((row >> 1) & 7): the read side applies
-  // the same involution.
+  // the same involution.  Steps S.. are the projection's (256 columns of Wp
+  // by 64 k per tile, column block after column block).
   const int lrow = lane >> 3, lchk = lane & 7;
   auto issue = [&](int s, int slot) __attribute__((always_inline)) {
-#if defined(SBK_PROBE_NO_DMA) || defined(SBK_PROBE_SKEL)
-    if (s >= 0) return;
-#endif
-    const int cl = s / SPC, r = s - cl * SPC;
-    const int c = cl + rot < NCH ? cl + rot : cl + rot - NCH;  // physical hidden chunk
-    const bool p1 = r < K1;
-    const bf16_t* base = p1 ? a.w1 + (long long)c * HC * D + r * BK : a.w2 + c * HC + (r - K1) * BK;
-    const int ld = p1 ? D : a.H;
+    const bf16_t* base;
+    int ld;
+    if (PROJ && s >= S) {
+      const int pj = s - S, nc = pj / K1, r = pj - nc * K1;
+      base = a.wp + (long long)nc * TROWS * D + r * BK;
+      ld = D;
+    } else {
+      const int c = s / SPC, r = s - c * SPC;
+      const bool p1 = r < K1;
+      base = p1 ? a.w1 + (long long)c * HC * D + r * BK : a.w2 + c * HC + (r - K1) * BK;
+      ld = p1 ? D : a.H;
+    }
     bf16_t* dst = ring + slot * TROWS * BK;
 #pragma unroll
     for (int i = 0; i < GL; ++i) {
@@ -278,7 +277,6 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   };
   issue(0, 0);
   issue(1, 1);
-  if (NB == 3) issue(2, 2);
 
   // LayerNorm of the workgroup's rows -> Xn (bf16); b1 -> LDS
 #pragma unroll
@@ -313,17 +311,14 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   // ---- main loop.  Every wave stages (LDS-DMA) and reads only its own weight
   // rows, so the 2-slot ring needs no workgroup barrier: a slot takes tile
   // s+2 as soon as the wave's fragments of tile s are in VGPRs.  Barriers
-  // remain only where waves share data: Xn (s == 0) and the hidden chunk Hs
-  // (written at r == K1-1, read from r == K1; double-buffered by chunk parity).
+  // remain only where waves share data: Xn (before the loop) and the hidden
+  // chunk Hs (written at r == K1-1, read from r == K1; double-buffered by
+  // chunk parity).  The LayerNorm'd rows are the A operand of every phase-1
+  // step: their fragments stay in VGPRs for the whole launch (96 VGPRs).
   // (Tried and slower: fragments of step s+1 read under the MFMAs of step s —
   // 8 waves 40.8 us, 16 waves spill; weights streamed straight into VGPRs
   // with 4 steps in flight instead of LDS-DMA — 45 us at 8 or 16 waves.)
   FFN_TL(1);
-#ifdef SBK_FFN_XREG
-  // the LayerNorm'd rows are the A operand of every phase-1 step: hold their
-  // fragments in VGPRs for the whole launch instead of re-reading them from
-  // LDS in every chunk (8 waves: 96 VGPRs; cuts the per-step LDS reads)
-  constexpr bool XREG = true;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   bf16x8 xa[K1][BK / 32][MT];
@@ -337,24 +332,13 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
 #pragma unroll
   for (int r = 0; r < SPC; ++r) {
     const int s = c * SPC + r;
-#else
-  constexpr bool XREG = false;
-  for (int s = 0; s < S; ++s) {
-    const int c = s / SPC, r = s - c * SPC;
-#endif
     // this wave's rows of tile s landed (tile s+1 stays in flight)
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL * (NB - 1)) : "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if ((s == 0 && !XREG) || r == K1 || (HSB == 1 && r == K1 - 1 && c > 0)) __builtin_amdgcn_s_barrier();
+    if (r == K1) __builtin_amdgcn_s_barrier();
     if (s < 34) FFN_TL(2 + 2 * s);
     const bf16_t* tile = ring + (s % NB) * TROWS * BK;
-    bf16_t* Hc = Hs + (HSB == 2 ? (c & 1) : 0) * BM * HS;  // this chunk's hidden activations
-    // once this step's fragments are in VGPRs its slot takes tile s+2
-    // (tail: a harmless reload of the last tile)
-    auto refill = [&]() __attribute__((always_inline)) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      issue(min(s + NB, S - 1), s % NB);
-    };
+    bf16_t* Hc = Hs + (c & 1) * BM * HS;  // this chunk's hidden activations
     bf16x8 fw[BK / 32][T], fa[BK / 32][MT];
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
@@ -363,23 +347,14 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
         const int row = w * (T * 16) + t * 16 + fr;
         fw[ks][t] = ld8(tile + row * BK + (((ks * 4 + g) ^ ((row >> 1) & 7)) << 3));
       }
-      const bf16_t* abase = r < K1 ? Xn + r * BK : Hc + (r - K1) * BK;
-      const int ald = r < K1 ? XS : HS;
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-#ifdef SBK_FFN_XREG
-        if (r < K1) {
-          fa[ks][mt] = xa[r < K1 ? r : 0][ks][mt];
-          continue;
-        }
-#endif
-        fa[ks][mt] = ld8(abase + (mt * 16 + fr) * ald + ks * 32 + fk);
-      }
+      for (int mt = 0; mt < MT; ++mt)
+        fa[ks][mt] = r < K1 ? xa[r < K1 ? r : 0][ks][mt] : ld8(Hc + (mt * 16 + fr) * HS + (r - K1) * BK + ks * 32 + fk);
     }
-    refill();
-#if defined(SBK_PROBE_NO_MFMA) || defined(SBK_PROBE_SKEL)
-    if (r >= 0) continue;
-#endif
+    // once this step's fragments are in VGPRs its slot takes tile s+2 (tail:
+    // the projection's first tiles, or a harmless reload of the last tile)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    issue(min(s + NB, ST - 1), s % NB);
     if (r < K1) {
 #pragma unroll
       for (int ks = 0; ks < BK / 32; ++ks)
@@ -401,8 +376,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
           // in-flight LDS-DMA tiles), draining the weight stream
           f32x4 bb;
           {
-            const int pc = c + rot < NCH ? c + rot : c + rot - NCH;
-            const uint32_t la = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)(b1s + pc * HC + n));
+            const uint32_t la = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)(b1s + c * HC + n));
             asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(bb) : "v"(la) : "memory");
           }
 #pragma unroll
@@ -431,25 +405,14 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     }
     if (s < 34) FFN_TL(3 + 2 * s);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the tail reloads
+  if (!PROJ) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the tail reloads
   FFN_TL(70);
 
   // ---- epilogue: lane holds rows m = mt*16 + fr, units d = (w*T + j)*16 + 4g .. +3
-#ifdef SBK_PROBE_NO_EPI
-  {
-    float t = 0.f;
+  float z[T][MT][4];
 #pragma unroll
-    for (int j = 0; j < T; ++j)
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) t += acc2[j][mt][0] + acc2[j][mt][1] + acc2[j][mt][2] + acc2[j][mt][3];
-    if (t != 12345.f) return;
-  }
-#endif
-  constexpr int T2 = T;
-  float z[T2][MT][4];
-#pragma unroll
-  for (int j = 0; j < T2; ++j) {
-    const int d = (w * T2 + j) * 16 + 4 * g;
+  for (int j = 0; j < T; ++j) {
+    const int d = (w * T + j) * 16 + 4 * g;
     const float4 bb = *reinterpret_cast<const float4*>(a.b2 + d);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -461,11 +424,109 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     }
   }
   FFN_TL(71);
-  if (a.gp) row_ln<D, T2, MT, NW>(z, red, a.gp, a.bp, a.epsp, w, g, fr);
+  if (a.gp) row_ln<D, T, MT, NW>(z, red, a.gp, a.bp, a.epsp, w, g, fr);
+  if (PROJ) {
+    // u = next-LN(out) -> Xn (bf16, the A operand of the projection), then
+    // the out stores: every compiler-visible LDS access precedes them, so no
+    // alias-guard wait drains them before the projection steps
+    float zo[T][MT][4];
+#pragma unroll
+    for (int j = 0; j < T; ++j)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) zo[j][mt][e] = z[j][mt][e];
+    row_ln<D, T, MT, NW>(z, red, a.gn, a.bn, a.epsn, w, g, fr);
+#pragma unroll
+    for (int j = 0; j < T; ++j) {
+      const int d = (w * T + j) * 16 + 4 * g;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        uint2 pk;
+        pk.x = (uint32_t)f32_to_bf16(z[j][mt][0]) | ((uint32_t)f32_to_bf16(z[j][mt][1]) << 16);
+        pk.y = (uint32_t)f32_to_bf16(z[j][mt][2]) | ((uint32_t)f32_to_bf16(z[j][mt][3]) << 16);
+        *reinterpret_cast<uint2*>(Xn + (mt * 16 + fr) * XS + d) = pk;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int r = 0; r < K1; ++r)
+#pragma unroll
+      for (int ks = 0; ks < BK / 32; ++ks)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const uint32_t la =
+              (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) bf16_t*)(Xn + (mt * 16 + fr) * XS + r * BK + ks * 32 + fk));
+          asm volatile("ds_read_b128 %0, %1" : "=v"(xa[r][ks][mt]) : "v"(la) : "memory");
+        }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const bool full = m0 + BM <= a.M;  // every out / projection store of this workgroup is issued
+#pragma unroll
+    for (int j = 0; j < T; ++j) {
+      const int d = (w * T + j) * 16 + 4 * g;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int row = m0 + mt * 16 + fr;
+        if (row < a.M)
+          *reinterpret_cast<float4*>(a.out + (long long)row * D + d) =
+              make_float4(zo[j][mt][0], zo[j][mt][1], zo[j][mt][2], zo[j][mt][3]);
+      }
+    }
+    // ---- projection y = u . Wp^T (bf16), 256 output columns per K1 steps
+    for (int s = S; s < ST; s += K1) {
+      const int nc = (s - S) / K1;
+#pragma unroll
+      for (int r = 0; r < K1; ++r) {
+        // tile s+r landed: younger than it are tile s+r+1 and, on the first
+        // step after a store burst (T*MT stores per lane, all issued only in
+        // full workgroups), those stores
+        if (r == 0 && full)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL * (NB - 1) + T * MT) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL * (NB - 1)) : "memory");
+        const bf16_t* tile = ring + ((s + r) % NB) * TROWS * BK;
+        bf16x8 fw[BK / 32][T];
+#pragma unroll
+        for (int ks = 0; ks < BK / 32; ++ks)
+#pragma unroll
+          for (int t = 0; t < T; ++t) {
+            const int row = w * (T * 16) + t * 16 + fr;
+            fw[ks][t] = ld8(tile + row * BK + (((ks * 4 + g) ^ ((row >> 1) & 7)) << 3));
+          }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        issue(min(s + r + NB, ST - 1), (s + r) % NB);
+#pragma unroll
+        for (int ks = 0; ks < BK / 32; ++ks)
+#pragma unroll
+          for (int t = 0; t < T; ++t)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+              acc1[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ks][t], xa[r][ks][mt], acc1[t][mt], 0, 0, 0);
+      }
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const int n = nc * TROWS + w * (T * 16) + t * 16 + 4 * g;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const int row = m0 + mt * 16 + fr;
+          const f32x4 v = acc1[t][mt];
+          uint2 pk;
+          pk.x = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
+          pk.y = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
+          if (row < a.M) *reinterpret_cast<uint2*>(a.yp + (long long)row * a.np + n) = pk;
+          acc1[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the tail reloads
+    FFN_TL(72);
+    return;
+  }
   // all residual reads of x are done before out (which may alias x) is written
 #pragma unroll
-  for (int j = 0; j < T2; ++j) {
-    const int d = (w * T2 + j) * 16 + 4 * g;
+  for (int j = 0; j < T; ++j) {
+    const int d = (w * T + j) * 16 + 4 * g;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int row = m0 + mt * 16 + fr;
@@ -475,10 +536,10 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     }
   }
   if (a.gn) {
-    row_ln<D, T2, MT, NW>(z, red, a.gn, a.bn, a.epsn, w, g, fr);
+    row_ln<D, T, MT, NW>(z, red, a.gn, a.bn, a.epsn, w, g, fr);
 #pragma unroll
-    for (int j = 0; j < T2; ++j) {
-      const int d = (w * T2 + j) * 16 + 4 * g;
+    for (int j = 0; j < T; ++j) {
+      const int d = (w * T + j) * 16 + 4 * g;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int row = m0 + mt * 16 + fr;
@@ -500,41 +561,36 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
 
 template <int D>
 size_t ffn_lds(int H) {
-#ifdef SBK_FFN_NB3
-  constexpr size_t ring = (size_t)3 * 256 * 64, hsb = 1;
-#else
-  constexpr size_t ring = (size_t)2 * 256 * 64, hsb = 2;
-#endif
-  return (ring + (size_t)FFN_BM * (D + 16) + hsb * FFN_BM * (256 + 16)) * sizeof(bf16_t) +
+  // 2-slot weight ring, Xn, two hidden-chunk buffers, b1, the row-reduction scratch
+  return ((size_t)2 * 256 * 64 + (size_t)FFN_BM * (D + 16) + (size_t)2 * FFN_BM * (256 + 16)) * sizeof(bf16_t) +
          (size_t)H * 4 + (size_t)FFN_NW * FFN_BM * 4;
 }
 
-template <int D, int ACT>
+template <int D, int ACT, bool PROJ>
 int launch_ffn_act(const FfnArgs& a, size_t lds, hipStream_t s) {
   static bool attr = false;  // > 64 KB dynamic LDS: opt in once per kernel
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ffn_kernel<D, ACT>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ffn_kernel<D, ACT, PROJ>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  hipLaunchKernelGGL((ffn_kernel<D, ACT>), dim3((a.M + FFN_BM - 1) / FFN_BM), dim3(FFN_NT), lds, s, a);
+  hipLaunchKernelGGL((ffn_kernel<D, ACT, PROJ>), dim3((a.M + FFN_BM - 1) / FFN_BM), dim3(FFN_NT), lds, s, a);
   return 0;
 }
 
-template <int D>
+template <int D, bool PROJ>
 int launch_ffn(const FfnArgs& a, hipStream_t s) {
   const size_t lds = ffn_lds<D>(a.H);
   if (lds > 160 * 1024) return SBK_ERR_ARG;
   switch (a.act) {
-    case ACT_SWISH: return launch_ffn_act<D, ACT_SWISH>(a, lds, s);
-    case ACT_LRELU: return launch_ffn_act<D, ACT_LRELU>(a, lds, s);
-    case ACT_GELU: return launch_ffn_act<D, ACT_GELU>(a, lds, s);
-    case ACT_NONE: return launch_ffn_act<D, ACT_NONE>(a, lds, s);
+    case ACT_SWISH: return launch_ffn_act<D, ACT_SWISH, PROJ>(a, lds, s);
+    case ACT_LRELU: return launch_ffn_act<D, ACT_LRELU, PROJ>(a, lds, s);
+    case ACT_GELU: return launch_ffn_act<D, ACT_GELU, PROJ>(a, lds, s);
+    case ACT_NONE: return launch_ffn_act<D, ACT_NONE, PROJ>(a, lds, s);
     default: return SBK_ERR_ARG;
   }
 }
-
 
 }  // namespace
 
@@ -546,19 +602,24 @@ SBK_API int sbk_probe_ffn_tl(unsigned long long* out) {
 
 SBK_API int sbk_ffn_supported(int D, int H) { return D == 256 && H > 0 && H % 256 == 0 && H <= 2048; }
 
-SBK_API int sbk_ffn(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0,
-                    const void* w1, const float* b1, int act, float slope, const void* w2, const float* b2,
-                    float alpha, const float* gp, const float* bp, float epsp, float* out, const float* gn,
-                    const float* bn, float epsn, void* u, int u_bf16, void* stream) {
+SBK_API int sbk_ffn_proj(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0,
+                         const void* w1, const float* b1, int act, float slope, const void* w2, const float* b2,
+                         float alpha, const float* gp, const float* bp, float epsp, float* out, const float* gn,
+                         const float* bn, float epsn, void* u, int u_bf16, const void* wp, int np, void* yp,
+                         void* stream) {
   if (M <= 0 || !sbk_ffn_supported(D, H) || !g0 || !b0 || !w1 || !b1 || !w2 || !b2 || !out) return SBK_ERR_ARG;
-  if (act == ACT_GLU || (gn && !u)) return SBK_ERR_ARG;
+  if (act == ACT_GLU || (gn && !u && !wp)) return SBK_ERR_ARG;
+  // projection tail: y = next-LN(out) . Wp^T, whole 256-column blocks; it
+  // replaces the u output
+  if (wp && (!gn || !bn || u || !yp || np <= 0 || np % 256)) return SBK_ERR_ARG;
   // float4 loads of rows and LayerNorm parameters
   const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(g0) |
                        reinterpret_cast<uintptr_t>(b0) | reinterpret_cast<uintptr_t>(b1) |
                        reinterpret_cast<uintptr_t>(b2) | reinterpret_cast<uintptr_t>(gp) |
                        reinterpret_cast<uintptr_t>(bp) | reinterpret_cast<uintptr_t>(out) |
                        reinterpret_cast<uintptr_t>(gn) | reinterpret_cast<uintptr_t>(bn) |
-                       reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(w1) | reinterpret_cast<uintptr_t>(w2);
+                       reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(w1) | reinterpret_cast<uintptr_t>(w2) |
+                       reinterpret_cast<uintptr_t>(wp) | reinterpret_cast<uintptr_t>(yp);
   if (al & 15) return SBK_ERR_ARG;
   FfnArgs a;
   a.x = x; a.M = M; a.H = H;
@@ -568,9 +629,18 @@ SBK_API int sbk_ffn(const float* x, int M, int D, int H, const float* g0, const 
   a.gp = gp; a.bp = bp; a.epsp = epsp;
   a.out = out;
   a.gn = gn; a.bn = bn; a.epsn = epsn; a.u = u; a.u_bf16 = u_bf16;
+  a.wp = reinterpret_cast<const bf16_t*>(wp); a.np = np; a.yp = reinterpret_cast<bf16_t*>(yp);
   hipStream_t s = (hipStream_t)stream;
-  int rc = launch_ffn<256>(a, s);
+  const int rc = wp ? launch_ffn<256, true>(a, s) : launch_ffn<256, false>(a, s);
   if (rc) return rc;
   SBK_CHECK_LAUNCH();
   return 0;
+}
+
+SBK_API int sbk_ffn(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0,
+                    const void* w1, const float* b1, int act, float slope, const void* w2, const float* b2,
+                    float alpha, const float* gp, const float* bp, float epsp, float* out, const float* gn,
+                    const float* bn, float epsn, void* u, int u_bf16, void* stream) {
+  return sbk_ffn_proj(x, M, D, H, g0, b0, eps0, w1, b1, act, slope, w2, b2, alpha, gp, bp, epsp, out, gn, bn, epsn,
+                      u, u_bf16, nullptr, 0, nullptr, stream);
 }

@@ -201,17 +201,26 @@ class ConformerEncoderLayer(nn.Module):
         if f1[1].fusable(dtype) and f2[1].fusable(dtype):
             # FFN1 + norm1 in one kernel, FFN2 + norm2 in one kernel (LayerNorms
             # computed on chip; the next layer's FFN1 normalises its own input)
-            x, u = f1[1].run_fused(x, self._ln(f1[0]), 0.5, next_ln=self._ln(self.norm1.norm), next_dtype=dtype)
+            wq = self.mha_layer.fused_in_proj(dtype) if hasattr(self.mha_layer, "fused_in_proj") else None
+            qkv = None
+            if wq is not None:
+                # ... and the MHSA in_proj on chip too (norm1's output never leaves the CU)
+                x, qkv = f1[1].run_fused_proj(x, self._ln(f1[0]), 0.5, self._ln(self.norm1.norm), wq)
+                u = None
+            else:
+                x, u = f1[1].run_fused(x, self._ln(f1[0]), 0.5, next_ln=self._ln(self.norm1.norm),
+                                       next_dtype=dtype)
             cm = self.convolution_module
             if USE_CONV_MODULE_KERNEL and cm.fusable(dtype, x.shape[1]):
                 # attention (+ output projection + residual), then the whole
                 # convolution module (its LayerNorms included) in one launch
-                x, attn = self.mha_layer.attend(u, B, T, pos, kpm_u8, dtype, need_attn, residual=x, pk=pk)
+                x, attn = self.mha_layer.attend(u, B, T, pos, kpm_u8, dtype, need_attn, residual=x, pk=pk,
+                                                qkv=qkv)
                 x = cm.run_fused(x, B, T, kpm_u8)
             else:
                 # attention output projection + residual + the conv module's LayerNorm in one launch
                 x, attn, uc = self.mha_layer.attend(u, B, T, pos, kpm_u8, dtype, need_attn, residual=x,
-                                                    post_ln=cm.ln_params(), pk=pk)
+                                                    post_ln=cm.ln_params(), pk=pk, qkv=qkv)
                 x = cm.run(x, B, T, dtype, kpm_u8, residual=x, u=uc)
             x, y = f2[1].run_fused(x, self._ln(f2[0]), 0.5, post_ln=self._ln(self.norm2.norm), out=x,
                                    next_ln=final_ln, next_dtype=_f32)

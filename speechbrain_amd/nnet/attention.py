@@ -105,15 +105,26 @@ class RelPosMHAXL(nn.Module):
             return tuple(p.detach() for p in ps)
         return self._wc.get("bf16", ps, lambda: tuple(_enc.cast_bf16(p.detach().contiguous()) for p in ps))
 
-    def attend(self, x2d, B, T, pos_embs, kpm_u8, dtype, need_weights, residual=None, post_ln=None, pk=None):
-        """Core used by the fused Conformer layer: x2d (B*T, d) in `dtype`.
+    def fused_in_proj(self, dtype):
+        """The bf16 in_proj weight when a producer kernel can apply it on chip
+        (sbk_ffn_proj: no in_proj bias, 3·d columns in 256-column blocks), else None."""
+        if dtype != torch.bfloat16 or self.vbias is not None or not self._qkv_same_embed_dim:
+            return None
+        w_in = self.kernel_weights(dtype)[0]
+        return w_in if _enc.ffn_proj_supported(self.embed_dim, 256, w_in.shape[0]) else None
+
+    def attend(self, x2d, B, T, pos_embs, kpm_u8, dtype, need_weights, residual=None, post_ln=None, pk=None,
+               qkv=None):
+        """Core used by the fused Conformer layer: x2d (B*T, d) in `dtype`
+        (or qkv = x2d · in_proj^T already computed by the producer kernel).
         Returns (out (B*T, d) fp32 [+ residual], attn or None); with post_ln =
         (w, b, eps) also u = LN(out) in `dtype` (fused into the output
         projection when d_model == 256): (out, attn, u)."""
         if self.vbias is not None:
             raise NotImplementedError("vbias=True is not on the RelPosMHAXL hot path")
         w_in, w_pos, w_out = self.kernel_weights(dtype)
-        qkv = _enc.gemm(x2d, w_in, out_dtype=dtype)
+        if qkv is None:
+            qkv = _enc.gemm(x2d, w_in, out_dtype=dtype)
         if pk is None:  # the encoder passes its one stacked linear_pos GEMM's slice
             pos = pos_embs.reshape(-1, self.embed_dim)
             if pos.dtype != dtype:
@@ -242,6 +253,15 @@ class PositionalwiseFeedForward(nn.Module):
                   for lin in (self.ffn[0], self.ffn[3]))
         return _enc.ffn(x, ln0, w1, b1, act, slope, w2, b2, alpha,
                         post_ln=post_ln, next_ln=next_ln, next_dtype=next_dtype, out=out)
+
+    def run_fused_proj(self, x, ln0, alpha, next_ln, wp, post_ln=None):
+        """run_fused with the next block's input projection on chip: returns
+        (out fp32, next_ln(out) · wp^T bf16)."""
+        w1, w2 = self.kernel_weights(torch.bfloat16)
+        act, slope = self.act_name()
+        b1, b2 = (lin.bias.detach() if lin.bias is not None else torch.zeros(lin.out_features, device=x.device)
+                  for lin in (self.ffn[0], self.ffn[3]))
+        return _enc.ffn_proj(x, ln0, w1, b1, act, slope, w2, b2, alpha, next_ln, wp, post_ln=post_ln)
 
     def forward(self, x):
         shp = x.shape

@@ -159,6 +159,31 @@ def test_fused_ffn_vs_unfused(dev, D, H, M):
     assert_close(out2, z, rtol=2e-2, name="ffn no post-LN")
 
 
+@pytest.mark.parametrize("H,M,NP", [(1024, 12032, 768), (1024, 1000, 768), (512, 48, 256), (2048, 333, 512)])
+def test_fused_ffn_proj_vs_unfused(dev, H, M, NP):
+    """sbk_ffn_proj (the FFN block + next-LN + the MHSA in_proj, one kernel)
+    vs sbk_ffn's u output through the separate sbk_gemm: the same rounding
+    points (u rounded to bf16, the projection accumulated in fp32 and rounded
+    once), so only summation order differs: 2e-2 as the FFN test.  Ragged M
+    exercises the partial last workgroup (its stores and counted waits)."""
+    from speechbrain_amd import _enc
+    from speechbrain_amd.nnet.attention import PositionalwiseFeedForward
+    from speechbrain_amd.nnet.activations import Swish
+    torch.manual_seed(1)
+    D = 256
+    ffn = PositionalwiseFeedForward(H, input_size=D, activation=Swish).to(dev).eval()
+    x = (torch.randn(M, D) * 2 + 0.5).to(dev)
+    lns = [(torch.randn(D, device=dev) * 0.5 + 1, torch.randn(D, device=dev) * 0.1, 1e-5) for _ in range(2)]
+    wp = _enc.cast_bf16((torch.randn(NP, D) / 16).to(dev))
+    with torch.no_grad():
+        out, y = ffn.run_fused_proj(x, lns[0], 0.5, lns[1], wp)
+        ref, u = ffn.run_fused(x, lns[0], 0.5, next_ln=lns[1])
+        yref = _enc.gemm(u, wp, out_dtype=torch.bfloat16)
+    assert y.shape == (M, NP) and y.dtype == torch.bfloat16
+    assert torch.equal(out, ref), "out must not depend on the projection tail"
+    assert_close(y.float(), yref.float(), rtol=2e-2, name="ffn_proj y")
+
+
 @pytest.mark.parametrize("T,F", [(1501, 80), (101, 80), (7, 40)])
 def test_fused_frontend_vs_blockwise(dev, T, F):
     """sbk_conv_frontend2 (both ConvBlocks in one kernel, bf16 compute) vs the
