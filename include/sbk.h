@@ -124,6 +124,37 @@ long long sbk_rnnt_workspace_floats(int B, int T, int U1);
 int sbk_rnnt_backward(const float* x, const int* labels, int B, int T, int U1, int V, int blank, int mode,
                       const float* ws, const float* scale, int scale_per_b, float* grad, void* stream);
 
+/* The lattice half of sbk_rnnt_forward (α, β, log P, sparse gradients,
+ * reduced loss) for per-cell log-probs already in ws[0 .. 3n) as
+ * [lpb | lpl | lse], n = B*T*U1 — written by sbk_thead_fwd. */
+int sbk_rnnt_lattice(const int* Tl, const int* Ul, int B, int T, int U1, int loss_mode, int reduction, float* ws,
+                     float* out, void* stream);
+
+/* ------------------------------------------------- fused transducer head */
+
+/* Joint ("sum" + nonlinearity, transducer_joint.py:57-95) -> Linear(J -> V,
+ * no bias) -> log-softmax -> RNN-T gather (losses.py:27-85 with
+ * transducer_loss.py:31-106) without the (B, T, U1, V) logits:
+ * z = act(tn[b,t] + pn[b,u]) rounded to bf16, S = z w^T (bf16 MFMA, fp32),
+ * lse / lpb / lpl (B*T*U1 each; the ws layout of sbk_rnnt_lattice).
+ * tn (B, T, J), pn (B, U1, J) fp32; w (V, J) bf16; labels (B, U1-1) int32;
+ * J % 128 == 0, J <= 1024; act 0 none, 3 LeakyReLU (slope), 5 tanh, 6 ReLU. */
+int sbk_thead_fwd(const float* tn, const float* pn, const void* w, const int* labels, int B, int T, int U1, int J,
+                  int V, int blank, int act, float slope, float* lse, float* lpb, float* lpl, void* stream);
+/* V rounded up to the head's column tiles (the row stride of dS). */
+int sbk_thead_vpad(int V);
+/* dS = ∂loss/∂logits (transducer_loss.py:183-236 through the log-softmax),
+ * recomputed from tn, pn, w and the forward's lse, with the sparse
+ * gradients gb, gl (sbk_rnnt_lattice's ws) scaled by scale[b] (scale_per_b)
+ * or scale[0]: ds (B*T*U1, sbk_thead_vpad(V)) bf16, columns >= V zero. */
+int sbk_thead_dlogits(const float* tn, const float* pn, const void* w, const int* labels, int B, int T, int U1,
+                      int J, int V, int blank, int act, float slope, const float* lse, const float* gb,
+                      const float* gl, const float* scale, int scale_per_b, void* ds, void* stream);
+/* dw (V, J) fp32 += ds^T z over the rows t < Tl[b] of every utterance (z
+ * regenerated as in sbk_thead_fwd); dw must be initialised by the caller. */
+int sbk_thead_wgrad(const void* ds, const float* tn, const float* pn, const int* Tl, int B, int T, int U1, int J,
+                    int V, int act, float slope, float* dw, void* stream);
+
 /* ----------------------------------------------------------------- encoder */
 
 /* Key padding mask from relative lengths: out[b, t] = t > floor(rel_len[b] * T)

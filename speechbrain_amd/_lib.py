@@ -44,6 +44,12 @@ SIGNATURES = {
     "sbk_gemm": [_i, _vp, _i, _vp, _i, _i, _i, _i, _vp, _i, _f, _vp, _i, _f, _vp, _vp, _i, _i, _i, _vp],
     "sbk_gemm_ln": [_i, _vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _i, _f, _vp, _vp, _i, _vp, _vp, _f, _vp, _i, _i, _i,
                     _vp],
+    # thead.hip (fused transducer head) and the gathered-lattice RNN-T entry
+    "sbk_thead_vpad": [_i],
+    "sbk_thead_fwd": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp],
+    "sbk_thead_dlogits": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp, _i, _vp, _vp],
+    "sbk_thead_wgrad": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _f, _vp, _vp],
+    "sbk_rnnt_lattice": [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp],
     # ffn.hip
     "sbk_ffn_supported": [_i, _i],
     "sbk_ffn": [_vp, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _i, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _vp, _f,

@@ -225,6 +225,9 @@ __global__ void finalize_kernel(const float* __restrict__ logp, int B, int loss_
 
 }  // namespace
 
+SBK_API int sbk_rnnt_lattice(const int* Tl, const int* Ul, int B, int T, int U1, int loss_mode, int reduction,
+                             float* ws, float* out, void* stream);
+
 // Forward: per-cell log-probs, α, β, log P, sparse grads and the reduced loss.
 //   x: logits (is_logits=1, log-softmax fused) or log-probs (is_logits=0).
 //   ws: workspace of 6*B*T*U1 + 2*B floats: [lpb | lpl | lse | α | β | gb | gl ... ]
@@ -234,19 +237,29 @@ SBK_API int sbk_rnnt_forward(const float* x, const int* labels, const int* Tl, c
                              int V, int blank, int is_logits, int loss_mode, int reduction, float* ws, float* out,
                              void* stream) {
   if (B <= 0 || T <= 0 || U1 <= 0 || V <= 0 || blank < 0 || blank >= V) return SBK_ERR_ARG;
+  const long long n = (long long)B * T * U1;
+  // ws: [lpb | lpl | lse | α | β | gb | gl | log P (2B)]
+  hipLaunchKernelGGL(gather_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x, labels, B, T,
+                     U1, V, blank, is_logits, ws, ws + n, ws + 2 * n);
+  SBK_CHECK_LAUNCH();
+  return sbk_rnnt_lattice(Tl, Ul, B, T, U1, loss_mode, reduction, ws, out, stream);
+}
+
+// The lattice half of sbk_rnnt_forward for log-probs gathered elsewhere (the
+// fused transducer head, thead.hip): ws[lpb | lpl | lse] filled, α, β,
+// log P, sparse grads and the reduced loss computed.
+SBK_API int sbk_rnnt_lattice(const int* Tl, const int* Ul, int B, int T, int U1, int loss_mode, int reduction,
+                             float* ws, float* out, void* stream) {
+  if (B <= 0 || T <= 0 || U1 <= 0 || !ws || !out || !Tl || !Ul) return SBK_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   const long long n = (long long)B * T * U1;
   float* lpb = ws;
   float* lpl = ws + n;
-  float* lse = ws + 2 * n;
   float* alpha = ws + 3 * n;
   float* beta = ws + 4 * n;
   float* gb = ws + 5 * n;
   float* gl = ws + 6 * n;
   float* logp = ws + 7 * n;  // 2B
-  hipLaunchKernelGGL(gather_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, x, labels, B, T, U1, V, blank,
-                     is_logits, lpb, lpl, lse);
-  SBK_CHECK_LAUNCH();
   hipLaunchKernelGGL(lattice_kernel, dim3(B, 2), dim3(U1 >= 256 ? 256 : ((U1 + 63) / 64) * 64), (size_t)2 * U1 * 4, s,
                      lpb, lpl, Tl, Ul, T, U1, alpha, beta, logp);
   SBK_CHECK_LAUNCH();

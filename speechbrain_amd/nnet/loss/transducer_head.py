@@ -1,0 +1,182 @@
+"""Fused transducer head: joint → output projection →
+log-softmax → RNN-T loss without the (B, T, U+1, V) logits.
+
+The LibriSpeech transducer recipe computes
+
+    z      = Transducer_joint(tn.unsqueeze(2), pn.unsqueeze(1))   # (B, T, U+1, J)
+    logits = transducer_lin(z)                                    # (B, T, U+1, V)
+    loss   = transducer_loss(logits, targets, wav_lens, token_lens, blank)
+
+(speechbrain/nnet/transducer/transducer_joint.py:57-95, speechbrain/nnet/
+losses.py:27-85, speechbrain/nnet/loss/transducer_loss.py:31-293).  At config
+4 (B=32, T=376, U+1=65, V=1000) the fp32 logits and their gradient are
+3.13 GB each.  `transducer_head_loss(tn, pn, weight, ...)` computes the same
+loss and the gradients wrt tn, pn and weight from csrc/thead.hip:
+
+  forward   sbk_thead_fwd      z generated on chip, S = z·Wᵀ (bf16 MFMA,
+                               fp32), online log-sum-exp, blank / label
+                               log-probs  →  sbk_rnnt_lattice (α, β, loss)
+  backward  sbk_thead_dlogits  S recomputed → dS = ∂L/∂logits in bf16
+            sbk_gemm           dZ = dS·W
+            sbk_joint_bwd      dTN (sum over U), dPN (sum over T)
+            sbk_thead_wgrad    dW = dSᵀ·z (z regenerated)
+
+so the only (rows × V) tensor is the transient bf16 dS of the backward.
+Numerics: the bf16-autocast recipe's (z and W in bf16, fp32 accumulation);
+the logits are not rounded to bf16 before the log-softmax.
+"""
+import torch
+import torch.nn as nn
+
+from ... import _enc
+from ..._lib import check, lib, ptr, require_device, stream_of
+
+__all__ = ["transducer_head_loss", "TransducerHeadLoss"]
+
+_RED = {"mean": 0, "sum": 1, "none": 2}
+_ACT = {nn.Identity: 0, nn.LeakyReLU: 3, nn.Tanh: 5, nn.ReLU: 6}
+
+
+@torch.library.custom_op("sbk::thead_loss", mutates_args=())
+def thead_loss(tn: torch.Tensor, pn: torch.Tensor, w: torch.Tensor, labels: torch.Tensor, Tl: torch.Tensor,
+               Ul: torch.Tensor, blank: int, reduction: int, loss_mode: int, act: int,
+               slope: float) -> tuple[torch.Tensor, torch.Tensor]:
+    """tn (B, T, J), pn (B, U1, J), w (V, J) fp32 → (loss, RNN-T workspace)."""
+    B, T, J = tn.shape
+    U1, V = pn.shape[1], w.shape[0]
+    L = lib()
+    n = B * T * U1
+    ws = torch.empty(int(L.sbk_rnnt_workspace_floats(B, T, U1)), device=tn.device, dtype=torch.float32)
+    out = torch.empty(B if reduction == 2 else (), device=tn.device, dtype=torch.float32)
+    wb = _enc.cast_bf16(w)
+    s = stream_of(tn)
+    check(L.sbk_thead_fwd(ptr(tn), ptr(pn), ptr(wb), ptr(labels), B, T, U1, J, V, int(blank), int(act), float(slope),
+                          ptr(ws[2 * n:]), ptr(ws), ptr(ws[n:]), s), "sbk_thead_fwd")
+    check(L.sbk_rnnt_lattice(ptr(Tl), ptr(Ul), B, T, U1, int(loss_mode), int(reduction), ptr(ws), ptr(out), s),
+          "sbk_rnnt_lattice")
+    return out, ws
+
+
+@thead_loss.register_fake
+def _(tn, pn, w, labels, Tl, Ul, blank, reduction, loss_mode, act, slope):
+    B, T, _ = tn.shape
+    U1 = pn.shape[1]
+    return tn.new_empty(B if reduction == 2 else ()), tn.new_empty(7 * B * T * U1 + 2 * B)
+
+
+@torch.library.custom_op("sbk::thead_grad", mutates_args=())
+def thead_grad(tn: torch.Tensor, pn: torch.Tensor, w: torch.Tensor, labels: torch.Tensor, Tl: torch.Tensor,
+               ws: torch.Tensor, go: torch.Tensor, blank: int, act: int,
+               slope: float) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """(dtn, dpn, dw) from the forward's workspace; rows scaled by go (one
+    value, or one per utterance)."""
+    B, T, J = tn.shape
+    U1, V = pn.shape[1], w.shape[0]
+    L = lib()
+    n = B * T * U1
+    Vp = int(L.sbk_thead_vpad(V))
+    s = stream_of(tn)
+    wb = _enc.cast_bf16(w)
+    ds = torch.empty(n, Vp, device=tn.device, dtype=torch.bfloat16)
+    check(L.sbk_thead_dlogits(ptr(tn), ptr(pn), ptr(wb), ptr(labels), B, T, U1, J, V, int(blank), int(act),
+                              float(slope), ptr(ws[2 * n:]), ptr(ws[5 * n:]), ptr(ws[6 * n:]), ptr(go),
+                              int(go.numel() > 1), ptr(ds), s), "sbk_thead_dlogits")
+    # dZ = dS · W: W^T zero-padded to Vp columns is the (N, K) operand
+    wt = torch.zeros(J, Vp, device=tn.device, dtype=torch.bfloat16)
+    wt[:, :V] = wb.t()
+    dz = _enc.gemm(ds, wt, out_dtype=torch.bfloat16)
+    dtn = torch.empty_like(tn)
+    dpn = torch.empty_like(pn)
+    jws = torch.empty(int(L.sbk_joint_bwd_workspace_floats(B, T, U1, J)), device=tn.device, dtype=torch.float32)
+    check(L.sbk_joint_bwd(ptr(tn), ptr(pn), ptr(dz), 1, B, T, U1, J, int(act), float(slope), ptr(dtn), ptr(dpn),
+                          ptr(jws), s), "sbk_joint_bwd")
+    del dz
+    dw = torch.zeros(V, J, device=tn.device, dtype=torch.float32)
+    check(L.sbk_thead_wgrad(ptr(ds), ptr(tn), ptr(pn), ptr(Tl), B, T, U1, J, V, int(act), float(slope), ptr(dw), s),
+          "sbk_thead_wgrad")
+    return dtn, dpn, dw
+
+
+@thead_grad.register_fake
+def _(tn, pn, w, labels, Tl, ws, go, blank, act, slope):
+    return torch.empty_like(tn), torch.empty_like(pn), torch.empty_like(w)
+
+
+def _setup(ctx, inputs, output):
+    tn, pn, w, labels, Tl, _, blank, reduction, loss_mode, act, slope = inputs
+    ctx.save_for_backward(tn, pn, w, labels, Tl, output[1])
+    ctx.a = (blank, act, slope)
+    # torchaudio semantics: d(mean)/d(loss_b) = 1/B (as sbk::rnnt)
+    ctx.scale = 1.0 / tn.shape[0] if (loss_mode == 1 and reduction == 0) else 1.0
+
+
+def _backward(ctx, grad_loss, grad_ws):
+    tn, pn, w, labels, Tl, ws = ctx.saved_tensors
+    go = (grad_loss.detach().to(torch.float32).reshape(-1) * ctx.scale).contiguous()
+    dtn, dpn, dw = thead_grad(tn, pn, w, labels, Tl, ws, go, *ctx.a)
+    return dtn, dpn, dw, None, None, None, None, None, None, None, None
+
+
+thead_loss.register_autograd(_backward, setup_context=_setup)
+
+
+def _act_of(nonlinearity):
+    code = _ACT.get(type(nonlinearity))
+    if code is None:
+        raise NotImplementedError(f"joint nonlinearity {type(nonlinearity).__name__} has no HIP kernel")
+    return code, float(getattr(nonlinearity, "negative_slope", 0.0)) if code == 3 else 0.0
+
+
+def transducer_head_loss(tn, pn, weight, targets, input_lens, target_lens, blank_index, reduction="mean",
+                         use_torchaudio=True, nonlinearity=None):
+    """transducer_loss(Linear(Transducer_joint(tn, pn), weight), targets, ...)
+    (losses.py:27-85 semantics: relative lengths rounded against T and the
+    target width; use_torchaudio selects -log P / mean over the batch) with
+    the joint, projection and log-softmax fused.
+    tn (B, T, J) or (B, T, 1, J); pn (B, U+1, J) or (B, 1, U+1, J); weight
+    (V, J) — the bias-free output Linear's weight; nonlinearity the joint's
+    module (default LeakyReLU, the recipe's)."""
+    if reduction not in _RED:
+        raise Exception("Unexpected reduction {}".format(reduction))
+    if tn.dim() == 4:
+        tn = tn[:, :, 0, :]
+    if pn.dim() == 4:
+        pn = pn[:, 0, :, :]
+    require_device(tn, pn, weight, targets)
+    act, slope = _act_of(nonlinearity if nonlinearity is not None else nn.LeakyReLU())
+    B, T, J = tn.shape
+    U1 = pn.shape[1]
+    in_lens = (input_lens * T).round().int()
+    tg_lens = (target_lens * targets.shape[1]).round().int()
+    lab = targets.to(device=tn.device, dtype=torch.int32)
+    if lab.shape[1] < U1 - 1:
+        lab = torch.nn.functional.pad(lab, (0, U1 - 1 - lab.shape[1]))
+    lab = lab[:, : U1 - 1].contiguous()
+    Tl = in_lens.to(device=tn.device, dtype=torch.int32).contiguous()
+    Ul = tg_lens.to(device=tn.device, dtype=torch.int32).contiguous()
+    out, _ = thead_loss(tn.float().contiguous(), pn.float().contiguous(), weight.float().contiguous(), lab, Tl, Ul,
+                        int(blank_index), _RED[reduction], 1 if use_torchaudio else 0, act, slope)
+    return out
+
+
+class TransducerHeadLoss(nn.Module):
+    """Module form: holds the joint nonlinearity and the output projection's
+    weight source (a speechbrain Linear / nn.Linear without bias)."""
+
+    def __init__(self, output_linear, nonlinearity=None, blank_index=0, reduction="mean", use_torchaudio=True):
+        super().__init__()
+        self.output_linear = output_linear
+        self.nonlinearity = nonlinearity if nonlinearity is not None else nn.LeakyReLU()
+        self.blank_index = blank_index
+        self.reduction = reduction
+        self.use_torchaudio = use_torchaudio
+
+    def _weight(self):
+        lin = getattr(self.output_linear, "w", self.output_linear)
+        if getattr(lin, "bias", None) is not None:
+            raise NotImplementedError("the fused head takes a bias-free output projection (the recipe's)")
+        return lin.weight
+
+    def forward(self, tn, pn, targets, input_lens, target_lens):
+        return transducer_head_loss(tn, pn, self._weight(), targets, input_lens, target_lens, self.blank_index,
+                                    self.reduction, self.use_torchaudio, self.nonlinearity)

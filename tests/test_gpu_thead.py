@@ -1,0 +1,86 @@
+"""Fused transducer head (csrc/thead.hip) vs the materialised chain.
+
+Reference path, at the same operand rounding (the bf16-autocast recipe: z and
+W rounded to bf16, fp32 accumulation, fp32 logits): z = bf16(act(tn + pn)),
+logits = z · bf16(W)ᵀ in fp32, then sbk::rnnt (TransducerLogits) — the HIP
+loss pinned to the reference's known answer and the CPU oracle in
+test_gpu_rnnt.py — with torch autograd for ∂/∂(tn, pn, W).
+Tolerances: the loss differs only by fp32 summation order (1e-4 relative).
+The fused backward rounds dS = ∂L/∂logits and dZ to bf16 (2^-9 relative
+each) before the two gradient GEMMs, so gradients are compared normwise:
+‖a − b‖ ≤ 1e-2 ‖b‖ (observed values printed)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _materialised(tn, pn, w, targets, in_rel, tg_rel, blank, reduction, use_torchaudio, slope):
+    from speechbrain_amd.nnet.losses import transducer_loss
+    z = F.leaky_relu(tn.unsqueeze(2) + pn.unsqueeze(1), slope)
+    z = z.to(torch.bfloat16).float()
+    logits = z @ w.to(torch.bfloat16).float().t()
+    return transducer_loss(logits, targets, in_rel, tg_rel, blank, reduction, use_torchaudio=use_torchaudio)
+
+
+def _case(dev, B, T, U, J, V, seed):
+    g = torch.Generator().manual_seed(seed)
+    tn = torch.randn(B, T, J, generator=g)
+    pn = torch.randn(B, U + 1, J, generator=g)
+    w = torch.randn(V, J, generator=g) / J ** 0.5
+    targets = torch.randint(1, V, (B, U), generator=g).int()
+    Tb = torch.tensor([T - (3 * i) % max(T // 2, 1) for i in range(B)])
+    Ub = torch.tensor([U - (2 * i) % max(U // 2, 1) for i in range(B)])
+    return (tn.to(dev), pn.to(dev), w.to(dev), targets.to(dev), (Tb.float() / T).to(dev), (Ub.float() / U).to(dev))
+
+
+def _nrel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("B,T,U,J,V", [(3, 9, 5, 128, 70), (2, 40, 19, 1024, 1000), (4, 17, 64, 256, 129)])
+@pytest.mark.parametrize("use_torchaudio,reduction", [(True, "mean"), (False, "mean"), (True, "none")])
+def test_thead_vs_materialised(dev, B, T, U, J, V, use_torchaudio, reduction):
+    from speechbrain_amd.nnet.loss.transducer_head import transducer_head_loss
+    tn, pn, w, targets, in_rel, tg_rel = _case(dev, B, T, U, J, V, seed=B * 1000 + U)
+    slope = 0.01
+    leaves = [t.clone().requires_grad_() for t in (tn, pn, w)]
+    ref = _materialised(*leaves, targets, in_rel, tg_rel, 0, reduction, use_torchaudio, slope)
+    ref.sum().backward()
+    fl = [t.clone().requires_grad_() for t in (tn, pn, w)]
+    out = transducer_head_loss(*fl, targets, in_rel, tg_rel, 0, reduction, use_torchaudio, torch.nn.LeakyReLU(slope))
+    out.sum().backward()
+    assert out.shape == ref.shape
+    assert torch.allclose(out, ref, rtol=1e-4, atol=1e-5), (out, ref)
+    for name, a, b in zip(("dtn", "dpn", "dW"), fl, leaves):
+        e = _nrel(a.grad, b.grad)
+        print(f"{name}: normwise rel err {e:.2e}")
+        assert e <= 1e-2, f"{name}: {e}"
+
+
+def test_thead_full_c4(dev):
+    """Config-4 shapes (B=32, T=376, U+1=65, J=1024, V=1000): the loss and
+    the gradients against the materialised path (3.1 GB of fp32 logits on
+    the reference side; the fused side's largest tensor is the bf16 dS)."""
+    from speechbrain_amd.nnet.loss.transducer_head import transducer_head_loss
+    B, T, U, J, V = 32, 376, 64, 1024, 1000
+    tn, pn, w, targets, in_rel, tg_rel = _case(dev, B, T, U, J, V, seed=7)
+    tn, pn = tn * 0.5, pn * 0.5
+    fl = [t.clone().requires_grad_() for t in (tn, pn, w)]
+    torch.cuda.reset_peak_memory_stats(dev)
+    base = torch.cuda.memory_allocated(dev)
+    out = transducer_head_loss(*fl, targets, in_rel, tg_rel, 0, "mean", True)
+    out.backward()
+    peak_fused = torch.cuda.max_memory_allocated(dev) - base
+    leaves = [t.clone().requires_grad_() for t in (tn, pn, w)]
+    ref = _materialised(*leaves, targets, in_rel, tg_rel, 0, "mean", True, 0.01)
+    ref.backward()
+    assert torch.isfinite(out) and abs(out.item() - ref.item()) <= 1e-4 * abs(ref.item()), (out.item(), ref.item())
+    for name, a, b in zip(("dtn", "dpn", "dW"), fl, leaves):
+        e = _nrel(a.grad, b.grad)
+        print(f"{name}: normwise rel err {e:.2e}")
+        assert e <= 1e-2, f"{name}: {e}"
+    rows = B * T * (U + 1)
+    print(f"fused peak {peak_fused / 2**30:.2f} GiB vs fp32 logits alone {rows * V * 4 / 2**30:.2f} GiB")
+    assert peak_fused < 2 * rows * V * 4
