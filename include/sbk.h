@@ -137,8 +137,9 @@ int sbk_rnnt_lattice(const int* Tl, const int* Ul, int B, int T, int U1, int los
  * transducer_loss.py:31-106) without the (B, T, U1, V) logits:
  * z = act(tn[b,t] + pn[b,u]) rounded to bf16, S = z w^T (bf16 MFMA, fp32),
  * lse / lpb / lpl (B*T*U1 each; the ws layout of sbk_rnnt_lattice).
- * tn (B, T, J), pn (B, U1, J) fp32; w (V, J) bf16; labels (B, U1-1) int32;
- * J % 128 == 0, J <= 1024; act 0 none, 3 LeakyReLU (slope), 5 tanh, 6 ReLU. */
+ * tn (B, T, J), pn (B, U1, J) fp32; w (sbk_thead_vpad(V), J) bf16 with rows
+ * >= V zero; labels (B, U1-1) int32; J in {128, 256, 512, 1024}; act 0 none,
+ * 3 LeakyReLU (slope), 6 ReLU. */
 int sbk_thead_fwd(const float* tn, const float* pn, const void* w, const int* labels, int B, int T, int U1, int J,
                   int V, int blank, int act, float slope, float* lse, float* lpb, float* lpl, void* stream);
 /* V rounded up to the head's column tiles (the row stride of dS). */
@@ -146,7 +147,8 @@ int sbk_thead_vpad(int V);
 /* dS = ∂loss/∂logits (transducer_loss.py:183-236 through the log-softmax),
  * recomputed from tn, pn, w and the forward's lse, with the sparse
  * gradients gb, gl (sbk_rnnt_lattice's ws) scaled by scale[b] (scale_per_b)
- * or scale[0]: ds (B*T*U1, sbk_thead_vpad(V)) bf16, columns >= V zero. */
+ * or scale[0]: ds (B*T*U1, sbk_thead_vpad(V)) bf16, columns >= V zero;
+ * w as for sbk_thead_fwd. */
 int sbk_thead_dlogits(const float* tn, const float* pn, const void* w, const int* labels, int B, int T, int U1,
                       int J, int V, int blank, int act, float slope, const float* lse, const float* gb,
                       const float* gl, const float* scale, int scale_per_b, void* ds, void* stream);

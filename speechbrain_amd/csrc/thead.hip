@@ -31,12 +31,16 @@ using namespace sbk;
 
 namespace {
 
-constexpr int TH_BM = 64, TH_BN = 64, TH_BK = 64, TH_NT = 256, TH_NB = 3;
+#ifndef SBK_TH_BN
+#define SBK_TH_BN 128
+#endif
+// 96 KB of W ring in either tile width: 12 x 8 KB or 6 x 16 KB
+constexpr int TH_BM = 128, TH_BN = SBK_TH_BN, TH_BK = 64, TH_NT = 512, TH_NB = 12 * 64 / TH_BN;
 
 struct TheadArgs {
   const float* tn;    // (B, T, J) fp32
   const float* pn;    // (B, U1, J) fp32
-  const bf16_t* w;    // (V, J) bf16
+  const bf16_t* w;    // (Vp, J) bf16, rows >= V zero
   const int* labels;  // (B, U1 - 1)
   int B, T, U1, J, V, Vp, blank, act;
   float slope;
@@ -48,12 +52,11 @@ struct TheadArgs {
   bf16_t* ds;  // (M, Vp)
 };
 
-__device__ __forceinline__ float th_act(int act, float v, float slope) {
-  if (act == 3) return v >= 0.f ? v : v * slope;
-  if (act == 5) return tanhf(v);
-  if (act == 6) return v > 0.f ? v : 0.f;
-  return v;
-}
+// The joint nonlinearities of the fused head are all one branch-free form,
+// v >= 0 ? v : v * slope, with slope 1 (identity), 0 (ReLU) or the
+// LeakyReLU slope: the host maps the act code (tanh stays on the
+// materialised path).
+__device__ __forceinline__ float th_act(int, float v, float slope) { return v >= 0.f ? v : v * slope; }
 
 __device__ __forceinline__ bf16x8 ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
@@ -83,206 +86,203 @@ __device__ __forceinline__ uint4 z8(const float* tp, const float* pp, int act, f
   return q;
 }
 
-// 4 waves; wave w owns columns w*16 .. +15 of each 64-column V chunk and all
-// 64 rows (4 m-tiles): a lane holds S[4g + r + 16 mt][v = fr] (16 rows of one
-// column), so a row's reductions over the chunk are 16-lane DPP reductions
-// and the 4 waves' partial (max, sum) merge once, after the last chunk.
-template <int MODE>
+// vmcnt(n) for a run-time n (the number of younger vector-memory operations
+// a wait may leave outstanding); immediates only exist per value
+__device__ __forceinline__ void wait_vm(int n) {
+  switch (n) {
+#define SBK_VM(N) \
+  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+    SBK_VM(0) SBK_VM(1) SBK_VM(2) SBK_VM(3) SBK_VM(4) SBK_VM(5) SBK_VM(6) SBK_VM(7) SBK_VM(8) SBK_VM(9) SBK_VM(10)
+    SBK_VM(11) SBK_VM(12) SBK_VM(13) SBK_VM(14) SBK_VM(15) SBK_VM(16) SBK_VM(17) SBK_VM(18) SBK_VM(19) SBK_VM(20)
+    SBK_VM(21) SBK_VM(22) SBK_VM(23) SBK_VM(24) SBK_VM(25) SBK_VM(26) SBK_VM(27) SBK_VM(28)
+#undef SBK_VM
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// 8 waves x 16 rows = 128 rows per workgroup.  Wave w holds the z fragments
+// of its 16 rows for the whole K = J in VGPRs (J / 32 x 4 registers,
+// generated once from tn / pn), so LDS holds only the W stream: 128 x 64
+// tiles (16 KB) through a 6-slot ring, 5 tiles (80 KB) in flight, one
+// barrier per step.  MODE 0: a lane holds S[w*16 + 4g + r][t*16 + fr] for
+// the 8 column tiles t of the 128-column V chunk, so a row's reductions are
+// in-lane over t plus one 16-lane DPP reduction, and no cross-wave merge is
+// needed.  MODE 1 swaps the MFMA operands (D[v][m]): a lane holds 4
+// consecutive v of one row and stores them as one 8-B bf16 quad.
+// Measured at config 4 (M = 782080, J = 1024, V = 1000): fwd 2.61 ms
+// (614 TF/s), dlogits 2.66 ms; 64-column chunks (12 x 8 KB ring) 3.00 /
+// 4.42 ms; the first version (64-row tiles, z in LDS, 3-slot ring) 8.97 /
+// 7.26 ms.
+template <int MODE, int JK>
 __global__ void __launch_bounds__(TH_NT) thead_kernel(TheadArgs a) {
-  constexpr int BM = TH_BM, BN = TH_BN, BK = TH_BK, NB = TH_NB, MTL = BM / 16;
+  constexpr int J = JK * 32, BN = TH_BN, BK = TH_BK, NB = TH_NB, DEPTH = NB - 1, NTL = BN / 16;
+  constexpr int KS = J / BK;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int J = a.J;
-  bf16_t* As = reinterpret_cast<bf16_t*>(smem);  // BM x J, 16-B chunk c of row r at c ^ (r & 15)
-  bf16_t* ring = As + BM * J;                    // NB x BN x BK, chunk c of row r at c ^ ((r >> 1) & 7)
-  float* capb = reinterpret_cast<float*>(ring + NB * BN * BK);  // MODE 0: blank / label logits, (max, sum) x 4 waves
-  float* capl = capb + BM;
-  float* redm = capl + BM;
-  float* reds = redm + 4 * BM;
+  bf16_t* ring = reinterpret_cast<bf16_t*>(smem);           // NB x BN x BK, chunk c of row r at c ^ ((r >> 1) & 7)
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, g = lane >> 4;
-  const int m0 = blockIdx.x * BM;
-  const int KS = J / BK, NVC = a.Vp / BN, NS = KS * NVC;
+  const int m0 = blockIdx.x * TH_BM;
+  const int NS = KS * (a.Vp / BN);
   const int Um = a.U1 - 1;
 
-  // ---- W tile s (V chunk s / KS, k step s % KS) -> ring slot s % NB:
-  // 8 KB = 8 pieces of 8 rows; wave w issues pieces w and w + 4
-  const int lrow = lane >> 3, lchk = lane & 7;
+  // ---- W tile s (V chunk s / KS, k step s % KS) -> slot s % NB: BN / 8
+  // pieces of 8 rows x 128 B; wave w issues pieces w, w + 8, ...
+  constexpr int PPW = BN / 64;  // pieces per wave per tile
+  static_assert(PPW * 64 == BN, "whole pieces per wave");
+  // (w has Vp rows, the padding zero: no clamp, so the per-lane source is one
+  // base pointer plus a wave-uniform offset)
+  const bf16_t* wlane = a.w + (long long)(w * 8 + (lane >> 3)) * J + (((lane & 7) ^ (((w * 8 + (lane >> 3)) >> 1) & 7)) << 3);
   auto issue = [&](int s) __attribute__((always_inline)) {
     const int vc = s / KS, ks = s - vc * KS;
     bf16_t* dst = ring + (s % NB) * BN * BK;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int p = i * 4 + w, r = p * 8 + lrow;
-      const int v = min(vc * BN + r, a.V - 1);
-      const bf16_t* src = a.w + (long long)v * J + ks * BK + ((lchk ^ ((r >> 1) & 7)) << 3);
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(dst + p * 8 * BK), 16, 0, 0);
-    }
+    for (int i = 0; i < PPW; ++i)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(wlane + ((long long)(vc * BN + 64 * i) * J + ks * BK)),
+          (__attribute__((address_space(3))) void*)(dst + (w * 8 + 64 * i) * BK), 16, 0, 0);
   };
-  issue(0);
-  issue(1);  // NS = (J / 64) * (Vp / 64) >= 4
+#pragma unroll
+  for (int s = 0; s < DEPTH; ++s)
+    if (s < NS) issue(s);
 
-  // ---- z rows of the tile -> LDS (rows past M clamp; never stored)
+  // ---- z fragments of row w*16 + fr, k = 32 kk + 8 g .. +7 (rows past M clamp)
+  bf16x8 za[JK];
   {
-    const int CPR = J / 8;
-#pragma unroll 4
-    for (int c = tid; c < BM * CPR; c += TH_NT) {
-      const int r = c / CPR, ch = c - r * CPR;
-      const int row = min(m0 + r, a.M - 1);
-      const int u = row % a.U1, bt = row / a.U1, b = bt / a.T;
-      const uint4 q = z8(a.tn + (long long)bt * J + ch * 8, a.pn + ((long long)b * a.U1 + u) * J + ch * 8, a.act,
-                         a.slope);
-      *reinterpret_cast<uint4*>(As + r * J + ((ch ^ (r & 15)) << 3)) = q;
+    const int row = min(m0 + w * 16 + fr, a.M - 1);
+    const int u = row % a.U1, bt = row / a.U1, b = bt / a.T;
+    const float* tp = a.tn + (long long)bt * J + 8 * g;
+    const float* pp = a.pn + ((long long)b * a.U1 + u) * J + 8 * g;
+#pragma unroll
+    for (int kk = 0; kk < JK; ++kk) {
+      const uint4 q = z8(tp + 32 * kk, pp + 32 * kk, a.act, a.slope);
+      za[kk] = *reinterpret_cast<const bf16x8*>(&q);
+      // bound the loads hoisted ahead of their conversions (register
+      // pressure: za alone is 4*JK VGPRs): fragment kk is final here
+      if (kk % 2 == 1) asm volatile("" : "+v"(za[kk]), "+v"(za[kk - 1])::"memory");
     }
   }
-  // this lane's rows: labels (and the dlogits coefficients)
-  int yl[MTL][4];
-  float lsev[MTL][4], cbv[MTL][4], clv[MTL][4], mx[MTL][4], sm[MTL][4];
+  // this lane's 4 rows w*16 + 4g + r: labels, running (max, sum) / dS coefficients
+  int yl[4];
+  float mx[4], sm[4], capb[4], capl[4], lsev[4], cbv[4], clv[4];
 #pragma unroll
-  for (int mt = 0; mt < MTL; ++mt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = min(m0 + mt * 16 + 4 * g + r, a.M - 1);
-      const int u = row % a.U1, b = row / (a.T * a.U1);
-      yl[mt][r] = u < Um ? a.labels[b * Um + u] : -1;
-      mx[mt][r] = -INFINITY;
-      sm[mt][r] = 0.f;
-      if (MODE == 1) {
-        const float sc = a.scale[a.scale_per_b ? b : 0];
-        lsev[mt][r] = a.lse_in[row];
-        cbv[mt][r] = a.gb[row] * sc;
-        clv[mt][r] = a.gl[row] * sc;
-      }
-    }
-  if (MODE == 0 && tid < BM) {
-    capb[tid] = __builtin_nanf("");
-    capl[tid] = __builtin_nanf("");
+  for (int r = 0; r < 4; ++r) {
+    const int row = min(m0 + w * 16 + 4 * g + r, a.M - 1);
+    const int u = row % a.U1, b = row / (a.T * a.U1);
+    yl[r] = u < Um ? a.labels[b * Um + u] : -1;
+    mx[r] = -INFINITY;
+    sm[r] = 0.f;
+    capb[r] = capl[r] = -INFINITY;
   }
-  __syncthreads();
+  // MODE 1 computes D[v][m] (operands swapped): the lane's one row is w*16 + fr
+  int y1 = -1;
+  if (MODE == 1) {
+    const int row = min(m0 + w * 16 + fr, a.M - 1);
+    const int u = row % a.U1, b = row / (a.T * a.U1);
+    const float sc = a.scale[a.scale_per_b ? b : 0];
+    y1 = u < Um ? a.labels[b * Um + u] : -1;
+    lsev[0] = a.lse_in[row];
+    cbv[0] = a.gb[row] * sc;
+    clv[0] = a.gl[row] * sc;
+  }
+  const bool full = m0 + TH_BM <= a.M;  // MODE 1: every dS store of the workgroup is issued (NTL per chunk)
 
-  f32x4 acc[MTL];
+  f32x4 acc[NTL];
 #pragma unroll
-  for (int mt = 0; mt < MTL; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bool stored = false;  // MODE 1: the previous step issued this thread's two dS stores
-  for (int s = 0; s < NS; ++s) {
-    // this wave's pieces of tile s landed (tile s+1 in flight; after a chunk
-    // end in MODE 1 also the two dS stores issued behind it)
-    if (s + 1 >= NS)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (MODE == 1 && stored)
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  for (int t = 0; t < NTL; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int vc = 0; vc < NS / KS; ++vc) {
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int s = vc * KS + ks;
+    // this wave's pieces of tile s landed: younger are the tiles issued
+    // after it and (MODE 1) the 4 dS stores of every chunk end since then
+    {
+      int younger = PPW * min(DEPTH - 1, NS - 1 - s);
+      if (MODE == 1 && full)
+        for (int e = max(0, s - DEPTH); e < s; ++e) younger += (e % KS == KS - 1) ? NTL : 0;
+      wait_vm(younger);
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    stored = false;
-    if (s + 2 < NS) issue(s + 2);  // into the slot read at step s-1
-    const int vc = s / KS, ks = s - vc * KS;
+    if (s + DEPTH < NS) issue(s + DEPTH);  // into the slot read at step s-1
     const bf16_t* tile = ring + (s % NB) * BN * BK;
 #pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
-      const int br = w * 16 + fr;
-      const bf16x8 fb = ld8(tile + br * BK + (((kk * 4 + g) ^ ((br >> 1) & 7)) << 3));
-      const int ch = ks * 8 + kk * 4 + g;
+    for (int h = 0; h < BK / 32; ++h) {
+      bf16x8 fb[NTL];
 #pragma unroll
-      for (int mt = 0; mt < MTL; ++mt) {
-        const bf16x8 fa = ld8(As + (mt * 16 + fr) * J + ((ch ^ fr) << 3));
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[mt], 0, 0, 0);
+      for (int t = 0; t < NTL; ++t) {
+        const int br = t * 16 + fr;
+        fb[t] = ld8(tile + br * BK + (((h * 4 + g) ^ ((br >> 1) & 7)) << 3));
       }
+#pragma unroll
+      for (int t = 0; t < NTL; ++t)
+        acc[t] = MODE == 0 ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(za[ks * 2 + h], fb[t], acc[t], 0, 0, 0)
+                           : __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[t], za[ks * 2 + h], acc[t], 0, 0, 0);
     }
-    if (ks != KS - 1) continue;
-    // ---- V chunk vc complete: S[rows][v], v = vc*BN + w*16 + fr
-    const int v = vc * BN + w * 16 + fr;
-    const bool valid = v < a.V;
+  }
+    // ---- V chunk vc complete: lane holds S[rows 4g + r][v = vc*BN + t*16 + fr]
     if (MODE == 0) {
 #pragma unroll
-      for (int mt = 0; mt < MTL; ++mt)
+      for (int r = 0; r < 4; ++r) {
+        float cm = -INFINITY;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float x = valid ? acc[mt][r] : -INFINITY;
-          const float nm = fmaxf(mx[mt][r], row16_max(x));
-          if (nm != -INFINITY) {
-            const float e = valid ? __expf(x - nm) : 0.f;
-            sm[mt][r] = sm[mt][r] * __expf(mx[mt][r] - nm) + row16_sum(e);
-            mx[mt][r] = nm;
-          }
-          const int lr = mt * 16 + 4 * g + r;
-          if (v == a.blank) {
-            const uint32_t la = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) float*)(capb + lr));
-            asm volatile("ds_write_b32 %0, %1" ::"v"(la), "v"(acc[mt][r]) : "memory");
-          }
-          if (valid && v == yl[mt][r]) {
-            const uint32_t la = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) float*)(capl + lr));
-            asm volatile("ds_write_b32 %0, %1" ::"v"(la), "v"(acc[mt][r]) : "memory");
-          }
+        for (int t = 0; t < NTL; ++t) {
+          const int v = vc * BN + t * 16 + fr;
+          if (v < a.V) cm = fmaxf(cm, acc[t][r]);
+          if (v == a.blank) capb[r] = acc[t][r];
+          if (v < a.V && v == yl[r]) capl[r] = acc[t][r];
         }
-    } else {
-      // dS in bf16 -> the slot just read (free once every wave is past its
-      // fragment reads) -> 16-B row stores; the slot is refilled only after
-      // the next step's barrier, behind these reads
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      bf16_t* scr = ring + (s % NB) * BN * BK;  // BM x BN, linear
+        const float nm = fmaxf(mx[r], row16_max(cm));
+        if (nm != -INFINITY) {
+          float e = 0.f;
 #pragma unroll
-      for (int mt = 0; mt < MTL; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float d = 0.f;
-          if (valid) {
-            const float p = __expf(acc[mt][r] - lsev[mt][r]);
-            d = (v == a.blank ? cbv[mt][r] : 0.f) + (v == yl[mt][r] ? clv[mt][r] : 0.f) -
-                p * (cbv[mt][r] + clv[mt][r]);
+          for (int t = 0; t < NTL; ++t) {
+            const int v = vc * BN + t * 16 + fr;
+            e += v < a.V ? __expf(acc[t][r] - nm) : 0.f;
           }
-          const int lr = mt * 16 + 4 * g + r;
-          const uint32_t la =
-              (uint32_t)(uintptr_t)((__attribute__((address_space(3))) bf16_t*)(scr + lr * BN + w * 16 + fr));
-          const uint32_t hv = f32_to_bf16(d);
-          asm volatile("ds_write_b16 %0, %1" ::"v"(la), "v"(hv) : "memory");
+          sm[r] = sm[r] * __expf(mx[r] - nm) + row16_sum(e);
+          mx[r] = nm;
         }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      const bool full = m0 + BM <= a.M;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int c = tid + i * TH_NT, lr = c >> 3, chk = c & 7;
-        const uint32_t la = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) bf16_t*)(scr + lr * BN + chk * 8));
-        uint4 q;
-        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(q) : "v"(la) : "memory");
-        if (m0 + lr < a.M)
-          *reinterpret_cast<uint4*>(a.ds + (long long)(m0 + lr) * a.Vp + vc * BN + chk * 8) = q;
       }
-      stored = full && s + 1 < NS;
+    } else {
+      // lane holds dS rows v = vc*BN + t*16 + 4g .. +3 of row m = w*16 + fr:
+      // one 8-B store of 4 bf16 per tile (a row's 64 columns from 16 lanes)
+      const int row = m0 + w * 16 + fr;
+#pragma unroll
+      for (int t = 0; t < NTL; ++t) {
+        const int v0 = vc * BN + t * 16 + 4 * g;
+        float d[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int v = v0 + r;
+          d[r] = 0.f;
+          if (v < a.V) {
+            const float p = __expf(acc[t][r] - lsev[0]);
+            d[r] = (v == a.blank ? cbv[0] : 0.f) + (v == y1 ? clv[0] : 0.f) - p * (cbv[0] + clv[0]);
+          }
+        }
+        uint2 pk;
+        pk.x = (uint32_t)f32_to_bf16(d[0]) | ((uint32_t)f32_to_bf16(d[1]) << 16);
+        pk.y = (uint32_t)f32_to_bf16(d[2]) | ((uint32_t)f32_to_bf16(d[3]) << 16);
+        if (row < a.M) *reinterpret_cast<uint2*>(a.ds + (long long)row * a.Vp + v0) = pk;
+      }
     }
 #pragma unroll
-    for (int mt = 0; mt < MTL; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < NTL; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   if (MODE == 1) return;
-  // ---- merge the 4 waves' (max, sum) per row; lse and the two log-probs
-  if (fr == 0) {
+  // ---- lse and the two log-probs of this lane's rows (one lane per row writes)
 #pragma unroll
-    for (int mt = 0; mt < MTL; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        redm[w * BM + mt * 16 + 4 * g + r] = mx[mt][r];
-        reds[w * BM + mt * 16 + 4 * g + r] = sm[mt][r];
-      }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid < BM && m0 + tid < a.M) {
-    const int row = m0 + tid;
-    float M = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) M = fmaxf(M, redm[k * BM + tid]);
-    float S = 0.f;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) S += reds[k * BM + tid] * __expf(redm[k * BM + tid] - M);
-    const float l = M + logf(S);
-    const int u = row % a.U1;
-    a.lse[row] = l;
-    a.lpb[row] = capb[tid] - l;
-    // label outside [0, V): NaN (the capture never happened), as gather_kernel
-    a.lpl[row] = u < Um ? capl[tid] - l : 0.f;
+  for (int r = 0; r < 4; ++r) {
+    const float cb = row16_max(capb[r]), cl = row16_max(capl[r]);
+    const int row = m0 + w * 16 + 4 * g + r;
+    if (fr == 0 && row < a.M) {
+      const float l = mx[r] + logf(sm[r]);
+      const int u = row % a.U1;
+      a.lse[row] = l;
+      a.lpb[row] = cb - l;
+      // label outside [0, V): NaN (never captured), as gather_kernel
+      a.lpl[row] = u < Um ? (cl == -INFINITY ? __builtin_nanf("") : cl - l) : 0.f;
+    }
   }
 }
 
@@ -399,38 +399,53 @@ __global__ void __launch_bounds__(256) thead_wgrad_kernel(const bf16_t* __restri
     }
 }
 
-size_t thead_lds(int J, int mode) {
-  return (size_t)TH_BM * J * 2 + (size_t)TH_NB * TH_BN * TH_BK * 2 + (mode == 0 ? (size_t)10 * TH_BM * 4 : 0);
+size_t thead_lds(int mode) {
+  (void)mode;
+  return (size_t)TH_NB * TH_BN * TH_BK * 2;
+}
+
+template <int MODE, int JK>
+int launch_thead_j(const TheadArgs& a, hipStream_t s) {
+  const size_t lds = thead_lds(MODE);
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&thead_kernel<MODE, JK>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((thead_kernel<MODE, JK>), dim3((a.M + TH_BM - 1) / TH_BM), dim3(TH_NT), lds, s, a);
+  SBK_CHECK_LAUNCH();
+  return 0;
 }
 
 template <int MODE>
 int launch_thead(const TheadArgs& a, hipStream_t s) {
-  const size_t lds = thead_lds(a.J, MODE);
-  if (lds > 160 * 1024) return SBK_ERR_ARG;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&thead_kernel<MODE>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return (int)e;
-    attr = true;
+  switch (a.J) {
+    case 128: return launch_thead_j<MODE, 4>(a, s);
+    case 256: return launch_thead_j<MODE, 8>(a, s);
+    case 512: return launch_thead_j<MODE, 16>(a, s);
+    case 1024: return launch_thead_j<MODE, 32>(a, s);
+    default: return SBK_ERR_ARG;
   }
-  hipLaunchKernelGGL((thead_kernel<MODE>), dim3((a.M + TH_BM - 1) / TH_BM), dim3(TH_NT), lds, s, a);
-  SBK_CHECK_LAUNCH();
-  return 0;
 }
 
 int thead_check(const float* tn, const float* pn, const void* w, const int* labels, int B, int T, int U1, int J,
                 int V, int blank, int act) {
   if (!tn || !pn || !w || !labels || B <= 0 || T <= 0 || U1 <= 0 || V <= 0 || blank < 0 || blank >= V)
     return SBK_ERR_ARG;
-  if (J <= 0 || J % 128 || J > 1024) return SBK_ERR_ARG;
-  if (act != 0 && act != 3 && act != 5 && act != 6) return SBK_ERR_ARG;
+  if (J != 128 && J != 256 && J != 512 && J != 1024) return SBK_ERR_ARG;
+  if (act != 0 && act != 3 && act != 6) return SBK_ERR_ARG;
   if ((long long)B * T * U1 > 0x7fffffffLL / 2) return SBK_ERR_ARG;
   if ((reinterpret_cast<uintptr_t>(tn) | reinterpret_cast<uintptr_t>(pn) | reinterpret_cast<uintptr_t>(w)) & 15)
     return SBK_ERR_ARG;
   return 0;
 }
 
+}  // namespace
+
+namespace {
+float act_slope(int act, float slope) { return act == 0 ? 1.f : (act == 6 ? 0.f : slope); }
 }  // namespace
 
 SBK_API int sbk_thead_vpad(int V) { return (V + 127) / 128 * 128; }
@@ -443,7 +458,7 @@ SBK_API int sbk_thead_fwd(const float* tn, const float* pn, const void* w, const
   TheadArgs a{};
   a.tn = tn; a.pn = pn; a.w = reinterpret_cast<const bf16_t*>(w); a.labels = labels;
   a.B = B; a.T = T; a.U1 = U1; a.J = J; a.V = V; a.Vp = sbk_thead_vpad(V); a.blank = blank; a.act = act;
-  a.slope = slope; a.M = B * T * U1;
+  a.slope = act_slope(act, slope); a.M = B * T * U1;
   a.lse = lse; a.lpb = lpb; a.lpl = lpl;
   return launch_thead<0>(a, (hipStream_t)stream);
 }
@@ -456,7 +471,7 @@ SBK_API int sbk_thead_dlogits(const float* tn, const float* pn, const void* w, c
   TheadArgs a{};
   a.tn = tn; a.pn = pn; a.w = reinterpret_cast<const bf16_t*>(w); a.labels = labels;
   a.B = B; a.T = T; a.U1 = U1; a.J = J; a.V = V; a.Vp = sbk_thead_vpad(V); a.blank = blank; a.act = act;
-  a.slope = slope; a.M = B * T * U1;
+  a.slope = act_slope(act, slope); a.M = B * T * U1;
   a.lse_in = lse; a.gb = gb; a.gl = gl; a.scale = scale; a.scale_per_b = scale_per_b;
   a.ds = reinterpret_cast<bf16_t*>(ds);
   return launch_thead<1>(a, (hipStream_t)stream);
@@ -465,6 +480,7 @@ SBK_API int sbk_thead_dlogits(const float* tn, const float* pn, const void* w, c
 SBK_API int sbk_thead_wgrad(const void* ds, const float* tn, const float* pn, const int* Tl, int B, int T, int U1,
                             int J, int V, int act, float slope, float* dw, void* stream) {
   if (!ds || !tn || !pn || !Tl || !dw || B <= 0 || T <= 0 || U1 <= 0 || V <= 0) return SBK_ERR_ARG;
+  if (act != 0 && act != 3 && act != 6) return SBK_ERR_ARG;
   if (J <= 0 || J % 128 || (long long)T * U1 > (1 << 24)) return SBK_ERR_ARG;
   if ((reinterpret_cast<uintptr_t>(ds) | reinterpret_cast<uintptr_t>(tn) | reinterpret_cast<uintptr_t>(pn)) & 15)
     return SBK_ERR_ARG;
@@ -479,7 +495,7 @@ SBK_API int sbk_thead_wgrad(const void* ds, const float* tn, const float* pn, co
   }
   const int Vp = sbk_thead_vpad(V);
   hipLaunchKernelGGL(thead_wgrad_kernel, dim3(Vp / WG_BV, J / WG_BJ, B), dim3(256), lds, (hipStream_t)stream,
-                     reinterpret_cast<const bf16_t*>(ds), Vp, tn, pn, Tl, T, U1, J, V, act, slope, dw);
+                     reinterpret_cast<const bf16_t*>(ds), Vp, tn, pn, Tl, T, U1, J, V, act, act_slope(act, slope), dw);
   SBK_CHECK_LAUNCH();
   return 0;
 }

@@ -34,7 +34,16 @@ from ..._lib import check, lib, ptr, require_device, stream_of
 __all__ = ["transducer_head_loss", "TransducerHeadLoss"]
 
 _RED = {"mean": 0, "sum": 1, "none": 2}
-_ACT = {nn.Identity: 0, nn.LeakyReLU: 3, nn.Tanh: 5, nn.ReLU: 6}
+_ACT = {nn.Identity: 0, nn.LeakyReLU: 3, nn.ReLU: 6}  # (Tanh: the materialised Transducer_joint path)
+
+
+def _padded_bf16(w):
+    """(V, J) fp32 -> (Vp, J) bf16, rows >= V zero (the head's column tiles)."""
+    V, J = w.shape
+    Vp = int(lib().sbk_thead_vpad(V))
+    out = torch.zeros(Vp, J, device=w.device, dtype=torch.bfloat16)
+    out[:V] = _enc.cast_bf16(w)
+    return out
 
 
 @torch.library.custom_op("sbk::thead_loss", mutates_args=())
@@ -48,7 +57,7 @@ def thead_loss(tn: torch.Tensor, pn: torch.Tensor, w: torch.Tensor, labels: torc
     n = B * T * U1
     ws = torch.empty(int(L.sbk_rnnt_workspace_floats(B, T, U1)), device=tn.device, dtype=torch.float32)
     out = torch.empty(B if reduction == 2 else (), device=tn.device, dtype=torch.float32)
-    wb = _enc.cast_bf16(w)
+    wb = _padded_bf16(w)
     s = stream_of(tn)
     check(L.sbk_thead_fwd(ptr(tn), ptr(pn), ptr(wb), ptr(labels), B, T, U1, J, V, int(blank), int(act), float(slope),
                           ptr(ws[2 * n:]), ptr(ws), ptr(ws[n:]), s), "sbk_thead_fwd")
@@ -76,15 +85,13 @@ def thead_grad(tn: torch.Tensor, pn: torch.Tensor, w: torch.Tensor, labels: torc
     n = B * T * U1
     Vp = int(L.sbk_thead_vpad(V))
     s = stream_of(tn)
-    wb = _enc.cast_bf16(w)
+    wb = _padded_bf16(w)
     ds = torch.empty(n, Vp, device=tn.device, dtype=torch.bfloat16)
     check(L.sbk_thead_dlogits(ptr(tn), ptr(pn), ptr(wb), ptr(labels), B, T, U1, J, V, int(blank), int(act),
                               float(slope), ptr(ws[2 * n:]), ptr(ws[5 * n:]), ptr(ws[6 * n:]), ptr(go),
                               int(go.numel() > 1), ptr(ds), s), "sbk_thead_dlogits")
     # dZ = dS · W: W^T zero-padded to Vp columns is the (N, K) operand
-    wt = torch.zeros(J, Vp, device=tn.device, dtype=torch.bfloat16)
-    wt[:, :V] = wb.t()
-    dz = _enc.gemm(ds, wt, out_dtype=torch.bfloat16)
+    dz = _enc.gemm(ds, wb.t().contiguous(), out_dtype=torch.bfloat16)
     dtn = torch.empty_like(tn)
     dpn = torch.empty_like(pn)
     jws = torch.empty(int(L.sbk_joint_bwd_workspace_floats(B, T, U1, J)), device=tn.device, dtype=torch.float32)
