@@ -30,8 +30,9 @@ import torch.nn as nn
 
 from ... import _enc
 from ..._lib import check, lib, ptr, require_device, stream_of
+from ..linear import Linear
 
-__all__ = ["transducer_head_loss", "TransducerHeadLoss"]
+__all__ = ["transducer_head_loss", "TransducerHeadLinear"]
 
 _RED = {"mean": 0, "sum": 1, "none": 2}
 _ACT = {nn.Identity: 0, nn.LeakyReLU: 3, nn.ReLU: 6}  # (Tanh: the materialised Transducer_joint path)
@@ -166,24 +167,31 @@ def transducer_head_loss(tn, pn, weight, targets, input_lens, target_lens, blank
     return out
 
 
-class TransducerHeadLoss(nn.Module):
-    """Module form: holds the joint nonlinearity and the output projection's
-    weight source (a speechbrain Linear / nn.Linear without bias)."""
+class TransducerHeadLinear(Linear):
+    """The recipe's output projection (speechbrain.nnet.linear.Linear,
+    J -> V, bias=False; same constructor, state_dict keys `w.weight` and
+    seeded init) whose forward also takes the joint inputs and returns the
+    fused transducer loss:
 
-    def __init__(self, output_linear, nonlinearity=None, blank_index=0, reduction="mean", use_torchaudio=True):
-        super().__init__()
-        self.output_linear = output_linear
+        lin(z)                                        -> logits (as Linear)
+        lin(tn, pn, targets, input_lens, target_lens) -> loss, no logits
+
+    The loss goes through the module's own forward, so a DDP-wrapped head
+    all-reduces its weight gradient like any other module."""
+
+    def __init__(self, n_neurons, input_shape=None, input_size=None, bias=False, combine_dims=False,
+                 nonlinearity=None, blank_index=0, reduction="mean", use_torchaudio=True):
+        super().__init__(n_neurons, input_shape=input_shape, input_size=input_size, bias=bias,
+                         combine_dims=combine_dims)
         self.nonlinearity = nonlinearity if nonlinearity is not None else nn.LeakyReLU()
         self.blank_index = blank_index
         self.reduction = reduction
         self.use_torchaudio = use_torchaudio
 
-    def _weight(self):
-        lin = getattr(self.output_linear, "w", self.output_linear)
-        if getattr(lin, "bias", None) is not None:
+    def forward(self, x, pn=None, targets=None, input_lens=None, target_lens=None):
+        if pn is None:
+            return super().forward(x)
+        if self.w.bias is not None:
             raise NotImplementedError("the fused head takes a bias-free output projection (the recipe's)")
-        return lin.weight
-
-    def forward(self, tn, pn, targets, input_lens, target_lens):
-        return transducer_head_loss(tn, pn, self._weight(), targets, input_lens, target_lens, self.blank_index,
+        return transducer_head_loss(x, pn, self.w.weight, targets, input_lens, target_lens, self.blank_index,
                                     self.reduction, self.use_torchaudio, self.nonlinearity)

@@ -84,3 +84,24 @@ def test_thead_full_c4(dev):
     rows = B * T * (U + 1)
     print(f"fused peak {peak_fused / 2**30:.2f} GiB vs fp32 logits alone {rows * V * 4 / 2**30:.2f} GiB")
     assert peak_fused < 2 * rows * V * 4
+
+
+def test_head_linear_module(dev):
+    """TransducerHeadLinear: forward(z) is the recipe's Linear; forward(tn,
+    pn, targets, lens) is the fused loss, and seeded construction draws the
+    same weights as Linear (checkpoint keys w.weight)."""
+    from speechbrain_amd.nnet.linear import Linear
+    from speechbrain_amd.nnet.loss.transducer_head import TransducerHeadLinear
+    torch.manual_seed(3)
+    ref = Linear(input_size=128, n_neurons=70, bias=False).to(dev)
+    torch.manual_seed(3)
+    head = TransducerHeadLinear(input_size=128, n_neurons=70, bias=False).to(dev)
+    assert list(head.state_dict()) == list(ref.state_dict()) == ["w.weight"]
+    assert torch.equal(head.w.weight, ref.w.weight)
+    tn, pn, _, targets, in_rel, tg_rel = _case(dev, 3, 9, 5, 128, 70, seed=5)
+    with torch.no_grad():
+        z = F.leaky_relu(tn.unsqueeze(2) + pn.unsqueeze(1), 0.01)
+        assert torch.equal(head(z), ref(z))
+        loss = head(tn, pn, targets, in_rel, tg_rel)
+        want = _materialised(tn, pn, head.w.weight, targets, in_rel, tg_rel, 0, "mean", True, 0.01)
+    assert torch.allclose(loss, want, rtol=1e-4, atol=1e-5), (loss, want)
