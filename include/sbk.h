@@ -190,6 +190,14 @@ int sbk_gemm_ln(int dtype_bf16, const void* A, int lda, const void* W, int ldw, 
 /* 1 if the fused FFN kernel supports d_model D and d_ffn H (D == 256, H % 256 == 0, H <= 2048). */
 int sbk_ffn_supported(int D, int H);
 
+/* Weight-gradient GEMM (bf16 MFMA): C[b] += A[b]^T B[b], A (K, M) and B
+ * (K, N) row-major with row strides lda / ldb (the token rows of dY and X:
+ * dW = dY^T X of nn.Linear / conv backward, linear.py:15-76), C (M, N) fp32
+ * (row stride ldc) accumulated with atomics (caller-initialised); sA / sB /
+ * sC batch strides (elements).  M, N, lda, ldb % 8 == 0; A, B 16-B aligned. */
+int sbk_gemm_tn(const void* A, long long lda, long long sA, const void* B, long long ldb, long long sB, int M, int N,
+                int K, int batch, float* C, long long ldc, long long sC, void* stream);
+
 /* Fused macaron feed-forward block, bf16 MFMA (Conformer.py:239-260 with
  * attention.py:823-839):
  *   z = x + alpha * (act(LN0(x) W1^T + b1) W2^T + b2);  out = LNp(z) if gp;

@@ -67,12 +67,16 @@ def colsum(part, rows, cols):
 # ------------------------------------------------------- dropout / residual
 def wgrad(g, a):
     """dW = g^T a in fp32 for g (M, N), a (M, K) — the weight gradient of a
-    Linear.  For the tall-skinny case (M >> N, K: M = B*T rows, N, K <= 1024)
+    Linear.  bf16: sbk_gemm_tn.  fp32 (the parity mode): for the tall-skinny case (M >> N, K: M = B*T rows, N, K <= 1024)
     one library GEMM has too few output tiles to fill 256 CUs, so the
     reduction over M is split into S batched GEMMs (fp32 outputs) summed in
     a fixed order."""
     M, N = g.shape
     K = a.shape[1]
+    if (g.dtype == _bf16 and a.dtype == _bf16 and N % 8 == 0 and K % 8 == 0 and g.stride(0) % 8 == 0
+            and a.stride(0) % 8 == 0 and (g.data_ptr() | a.data_ptr()) % 16 == 0):
+        # bf16 training path: the token-major weight-gradient MFMA kernel
+        return _enc.gemm_tn(g, a)
     S = 1
     while S < 16 and M // (2 * S) >= 1024 and (N // 64) * (K // 64) * S < 1024:
         S *= 2
@@ -84,6 +88,12 @@ def wgrad(g, a):
     if S * m < M:
         head += torch.mm(g[S * m:].t(), a[S * m:], **kw)
     return head
+
+
+def dgrad(g, wk):
+    """dX = g @ wk for g (M, N), wk (N, K) — the input gradient of a Linear —
+    on the MFMA GEMM (A @ W^T with W = wk^T, a (K, N) copy of the weight)."""
+    return _enc.gemm(_cont(g), _cont(wk.t()), out_dtype=g.dtype)
 
 
 def drop_add(x, res=None, alpha=1.0, rowmask=None, p=0.0, seed=0, out_dtype=_f32):
@@ -177,7 +187,7 @@ class LinearFn(Function):
         else:
             g = _as(dy, a.dtype)
             gb = dy
-        da = torch.mm(g, wk) if ctx.needs_input_grad[0] else None
+        da = dgrad(g, wk) if ctx.needs_input_grad[0] else None
         dw = wgrad(g, a).view(ctx.wshape) if ctx.needs_input_grad[1] else None
         db = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
@@ -427,7 +437,7 @@ class ConvBlockFn(Function):
         db = rowsum(dc) if has_bias else None
         dx = None
         if ctx.needs_input_grad[0]:
-            dcol = torch.mm(g, wk)  # (N, ldcol)
+            dcol = dgrad(g, wk)  # (N, ldcol)
             dx = torch.empty(B, Ti, Fi, Ci, device=col.device, dtype=xdt)
             check(L.sbk_col2im3s2(ptr(dcol), _bf(dcol), B, Ti, Fi, Ci, ldcol, ptr(dx), _bf(dx), s), "sbk_col2im3s2")
         return dx, dw, db, dlw, dlb, None, None, None, None

@@ -73,6 +73,36 @@ def gemm(a, w, bias=None, act=None, slope=0.0, res=None, alpha=1.0, rowmask=None
                               out_dtype == _bf16, int(tile))
 
 
+@torch.library.custom_op("sbk::gemm_tn", mutates_args=())
+def _gemm_tn_op(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    K, M = a.shape[-2], a.shape[-1]
+    N = b.shape[-1]
+    batch = a.shape[0] if a.dim() == 3 else 1
+    out = torch.zeros(*([batch] if a.dim() == 3 else []), M, N, device=a.device, dtype=_f32)
+    sa = a.stride(0) if a.dim() == 3 else 0
+    sb = b.stride(0) if b.dim() == 3 else 0
+    check(lib().sbk_gemm_tn(ptr(a), a.stride(-2), sa, ptr(b), b.stride(-2), sb, M, N, K, batch, ptr(out), N,
+                            M * N if a.dim() == 3 else 0, stream_of(a)), "sbk_gemm_tn")
+    return out
+
+
+@_gemm_tn_op.register_fake
+def _(a, b):
+    return a.new_empty(*a.shape[:-2], a.shape[-1], b.shape[-1], dtype=_f32)
+
+
+def gemm_tn(a, b):
+    """a^T @ b in fp32 for bf16 a (K, M), b (K, N) (or batched (Bt, K, *)):
+    the weight gradient dY^T X without transposing the token-major
+    operands.  Rows must be 16-B aligned and column-contiguous."""
+    require_device(a, b)
+    if a.dtype != _bf16 or b.dtype != _bf16:
+        raise TypeError("gemm_tn takes bf16 operands")
+    if a.stride(-1) != 1 or b.stride(-1) != 1:
+        raise ValueError("gemm_tn operands must be column-contiguous")
+    return torch.ops.sbk.gemm_tn(a, b)
+
+
 @torch.library.custom_op("sbk::length_mask", mutates_args=())
 def _length_mask_op(rel_len: torch.Tensor, T: int) -> torch.Tensor:
     B = rel_len.shape[0]

@@ -50,6 +50,8 @@ SIGNATURES = {
     "sbk_thead_dlogits": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp, _i, _vp, _vp],
     "sbk_thead_wgrad": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _f, _vp, _vp],
     "sbk_rnnt_lattice": [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp],
+    # gemm_tn.hip (weight-gradient GEMM)
+    "sbk_gemm_tn": [_vp, _ll, _ll, _vp, _ll, _ll, _i, _i, _i, _i, _vp, _ll, _ll, _vp],
     # ffn.hip
     "sbk_ffn_supported": [_i, _i],
     "sbk_ffn": [_vp, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _i, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _vp, _f,

@@ -1,0 +1,140 @@
+// Weight-gradient GEMM (bf16 MFMA, fp32 accumulation):
+//
+//   C[b] (+)= A[b]^T · B[b]      A (K, M), B (K, N) row-major, C (M, N) fp32
+//
+// the backward of every nn.Linear / 1x1 conv / im2col conv of the training
+// path (dW = dY^T X: the contraction runs over the B*T token rows, which are
+// the ROWS of both stored operands), and the batched products of the
+// attention backward of the same shape.  Reference sites: the autograd of
+// torch.nn.Linear under speechbrain/nnet/linear.py:15-76 and of the ConvBlock
+// convolutions (speechbrain/lobes/models/convolution.py:112-175).
+//
+// Both operands are staged k-major exactly as stored ([64 k][128 + 16] bf16
+// tiles, register-prefetched one step ahead) and read k-transposed for the
+// MFMA with ds_read_b64_tr_b16, so no transpose pass over the (tokens x
+// features) tensors exists.  128 x 128 output tiles, 4 waves as 2 x 2 (64 x
+// 64 each), and the K (token) range split over workgroups until the grid
+// fills the chip; partial tiles are added into C with fp32 atomics (C is
+// initialised by the caller), columns/rows past M / N never stored.
+#include "mfma.h"
+
+using namespace sbk;
+
+namespace {
+
+constexpr int TN_BM = 128, TN_BN = 128, TN_BK = 64, TN_LD = 144;
+
+__device__ __forceinline__ bf16x8 frag_tr(const bf16_t* X, int k0, int dbase, int lane) {
+  typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const bf16_t* a0 = X + (k0 + 4 * g + q) * TN_LD + dbase + 4 * p;
+  const bf16_t* a1 = a0 + 16 * TN_LD;
+  const bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4_t*)(a0));
+  const bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4_t*)(a1));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+struct TnArgs {
+  const bf16_t* A;
+  const bf16_t* B;
+  float* C;
+  long long lda, ldb, ldc, sA, sB, sC;
+  int M, N, K, kchunk, nsplit;
+};
+
+__global__ void __launch_bounds__(256) gemm_tn_kernel(TnArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t As[TN_BK * TN_LD];
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[TN_BK * TN_LD];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  const int m0 = blockIdx.x * TN_BM, n0 = blockIdx.y * TN_BN;
+  const int bz = blockIdx.z / a.nsplit, sp = blockIdx.z - bz * a.nsplit;
+  const int k0 = sp * a.kchunk, k1 = min(a.K, k0 + a.kchunk);
+  const bf16_t* A = a.A + bz * a.sA;
+  const bf16_t* B = a.B + bz * a.sB;
+  float* C = a.C + bz * a.sC;
+  // 4 chunks of 8 per thread per operand per step: chunk c -> row c >> 4, columns 8 (c & 15)
+  uint4 ra[4], rb[4];
+  auto gload = [&](int kb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + i * 256, r = kb + (c >> 4), cc = (c & 15) * 8;
+      const bool rk = r < k1;
+      const int rr = rk ? r : k0;
+      ra[i] = rk && m0 + cc < a.M ? *reinterpret_cast<const uint4*>(A + (long long)rr * a.lda + m0 + cc)
+                                  : uint4{0u, 0u, 0u, 0u};
+      rb[i] = rk && n0 + cc < a.N ? *reinterpret_cast<const uint4*>(B + (long long)rr * a.ldb + n0 + cc)
+                                  : uint4{0u, 0u, 0u, 0u};
+    }
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (k1 - k0 + TN_BK - 1) / TN_BK;
+  if (nk > 0) gload(k0);
+  for (int kt = 0; kt < nk; ++kt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + i * 256, r = c >> 4, cc = (c & 15) * 8;
+      *reinterpret_cast<uint4*>(As + r * TN_LD + cc) = ra[i];
+      *reinterpret_cast<uint4*>(Bs + r * TN_LD + cc) = rb[i];
+    }
+    __syncthreads();
+    if (kt + 1 < nk) gload(k0 + (kt + 1) * TN_BK);
+#pragma unroll
+    for (int kk = 0; kk < TN_BK / 32; ++kk) {
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = frag_tr(As, kk * 32, wm * 64 + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = frag_tr(Bs, kk * 32, wn * 64 + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // D[m][n]: lane holds rows m = 4g + r, column n = lane & 15 of each tile
+  const int g = lane >> 4, fr = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wm * 64 + i * 16 + 4 * g + r;
+      if (m >= a.M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + fr;
+        if (n < a.N) atomicAdd(C + (long long)m * a.ldc + n, acc[i][j][r]);
+      }
+    }
+}
+
+}  // namespace
+
+// C[b] += A[b]^T B[b] for b < batch.  A (K, M) with row stride lda, B (K, N)
+// row stride ldb, bf16; C (M, N) fp32 row stride ldc (caller-initialised);
+// sA / sB / sC batch strides in elements.  M, N, lda, ldb multiples of 8
+// and A, B 16-B aligned (16-B row chunks).
+SBK_API int sbk_gemm_tn(const void* A, long long lda, long long sA, const void* B, long long ldb, long long sB,
+                        int M, int N, int K, int batch, float* C, long long ldc, long long sC, void* stream) {
+  if (!A || !B || !C || M <= 0 || N <= 0 || K < 0 || batch <= 0) return SBK_ERR_ARG;
+  if ((M | N) % 8 || lda % 8 || ldb % 8 || lda < M || ldb < N || ldc < N) return SBK_ERR_ARG;
+  if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15 || (sA | sB) % 8) return SBK_ERR_ARG;
+  if (K == 0) return 0;
+  const int tm = (M + TN_BM - 1) / TN_BM, tn = (N + TN_BN - 1) / TN_BN;
+  const long long tiles = (long long)tm * tn * batch;
+  // split the token range until ~1024 workgroups (>= 4 per CU), >= 256 rows each
+  int nsplit = 1;
+  while (tiles * nsplit * 2 <= 1024 && (long long)K / (nsplit * 2) >= 256) nsplit *= 2;
+  const int kchunk = ((K + nsplit - 1) / nsplit + TN_BK - 1) / TN_BK * TN_BK;
+  nsplit = (K + kchunk - 1) / kchunk;
+  if ((long long)batch * nsplit > 65535) return SBK_ERR_ARG;
+  TnArgs a{reinterpret_cast<const bf16_t*>(A), reinterpret_cast<const bf16_t*>(B), C, lda, ldb, ldc, sA, sB, sC,
+           M, N, K, kchunk, nsplit};
+  hipLaunchKernelGGL(gemm_tn_kernel, dim3(tm, tn, batch * nsplit), dim3(256), 0, (hipStream_t)stream, a);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
