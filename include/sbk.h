@@ -289,6 +289,16 @@ int sbk_conv_module(const float* x, float* out, int B, int T, int D, const float
                     float eps0, const void* w1p, const float* b1p, const float* wc, const float* bc, int K, int causal,
                     const float* ln1_w, const float* ln1_b, float eps1, const void* w2, const float* b2,
                     const unsigned char* kpm, void* stream);
+/* sbk_conv_module with the MHSA output projection applied first: the module
+ * runs on x_att = x + o wo^T + bo (attention.py:636 out_proj and the residual
+ * of Conformer.py:247-252) without x_att leaving the workgroup except as
+ * this launch's own output rows: out = x_att + rowmask0(ConvModule(x_att)).
+ * o (B*T, 256) bf16 (the attention heads concatenated), wo (256, 256) bf16,
+ * bo (256) fp32 or null; o == null behaves as sbk_conv_module. */
+int sbk_conv_module_pre(const float* x, const void* o, const void* wo, const float* bo, float* out, int B, int T,
+                        int D, const float* ln0_w, const float* ln0_b, float eps0, const void* w1p, const float* b1p,
+                        const float* wc, const float* bc, int K, int causal, const float* ln1_w, const float* ln1_b,
+                        float eps1, const void* w2, const float* b2, const unsigned char* kpm, void* stream);
 
 /* InputNormalization (processing/features.py:940-1231), csrc/norm.hip.  x (B, T, F) fp32,
  * len (B) relative lengths (frames = rintf(len * T), clamped to [0, T]), F <= 256.

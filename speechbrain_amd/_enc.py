@@ -309,27 +309,31 @@ def conv_module_supported(D, K):
 def _conv_module_op(x: torch.Tensor, B: int, T: int, g0: torch.Tensor, b0: torch.Tensor, e0: float,
                     w1p: torch.Tensor, b1p: torch.Tensor, wc: torch.Tensor, bc: Optional[torch.Tensor], causal: bool,
                     g1: torch.Tensor, b1: torch.Tensor, e1: float, w2: torch.Tensor, b2: Optional[torch.Tensor],
-                    kpm: Optional[torch.Tensor]) -> torch.Tensor:
+                    kpm: Optional[torch.Tensor], o: Optional[torch.Tensor], wo: Optional[torch.Tensor],
+                    bo: Optional[torch.Tensor]) -> torch.Tensor:
     K = wc.shape[0]  # wc: (K, d) tap-major
     out = torch.empty_like(x)
-    rc = lib().sbk_conv_module(ptr(x), ptr(out), B, T, x.shape[1], ptr(g0), ptr(b0), float(e0), ptr(w1p), ptr(b1p),
-                               ptr(wc), ptr(bc), K, int(causal), ptr(g1), ptr(b1), float(e1), ptr(w2), ptr(b2),
-                               ptr(kpm), stream_of(x))
-    check(rc, "sbk_conv_module")
+    rc = lib().sbk_conv_module_pre(ptr(x), ptr(o), ptr(wo), ptr(bo), ptr(out), B, T, x.shape[1], ptr(g0), ptr(b0),
+                                   float(e0), ptr(w1p), ptr(b1p), ptr(wc), ptr(bc), K, int(causal), ptr(g1), ptr(b1),
+                                   float(e1), ptr(w2), ptr(b2), ptr(kpm), stream_of(x))
+    check(rc, "sbk_conv_module_pre")
     return out
 
 
 @_conv_module_op.register_fake
-def _(x, B, T, g0, b0, e0, w1p, b1p, wc, bc, causal, g1, b1, e1, w2, b2, kpm):
+def _(x, B, T, g0, b0, e0, w1p, b1p, wc, bc, causal, g1, b1, e1, w2, b2, kpm, o, wo, bo):
     return torch.empty_like(x)
 
 
-def conv_module(x, B, T, ln0, w1p, b1p, wc, bc, causal, ln1, w2, b2, kpm=None):
+def conv_module(x, B, T, ln0, w1p, b1p, wc, bc, causal, ln1, w2, b2, kpm=None, pre=None):
     """Fused Conformer convolution module (bf16 MFMA, one launch):
-    x + rowmask0(after_conv(dwconv(GLU(pointwise(LN0(x)))))).  x: (B*T, 256) fp32."""
+    x + rowmask0(after_conv(dwconv(GLU(pointwise(LN0(x)))))).  x: (B*T, 256) fp32.
+    pre = (o, wo, bo): the module runs on x + o wo^T + bo (the MHSA output
+    projection and residual fused in; o (B*T, 256) bf16)."""
     require_device(x, w1p, w2)
+    o, wo, bo = pre if pre is not None else (None, None, None)
     return torch.ops.sbk.conv_module(x, int(B), int(T), ln0[0], ln0[1], float(ln0[2]), w1p, b1p, wc, bc,
-                                     bool(causal), ln1[0], ln1[1], float(ln1[2]), w2, b2, kpm)
+                                     bool(causal), ln1[0], ln1[1], float(ln1[2]), w2, b2, kpm, o, wo, bo)
 
 
 @torch.library.custom_op("sbk::conv_block_c1", mutates_args=())

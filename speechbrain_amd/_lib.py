@@ -95,6 +95,8 @@ SIGNATURES = {
     "sbk_inorm_apply": [_vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp],
     # convmod.hip
     "sbk_conv_module_supported": [_i, _i],
+    "sbk_conv_module_pre": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _vp, _vp, _i, _i, _vp,
+                            _vp, _f, _vp, _vp, _vp, _vp],
     "sbk_conv_module": [_vp, _vp, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _f, _vp, _vp, _vp,
                         _vp],
     # backward.hip (training path)

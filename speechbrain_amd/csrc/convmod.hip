@@ -61,6 +61,12 @@ struct ConvModArgs {
   const bf16_t* w2;  // (D, D)
   const float* b2;   // (D) or null
   const uint8_t* kpm;  // (B*T) padding mask or null
+  // optional attention output projection applied first (PRE): the module's
+  // input is x + o · wo^T + bo (attention.py:636 and the MHSA residual,
+  // Conformer.py:247-252), never materialised outside the workgroup
+  const bf16_t* o;   // (B*T, D) attention output (heads concatenated)
+  const bf16_t* wo;  // (D, D) out_proj weight
+  const float* bo;   // (D) or null
 };
 
 #ifdef SBK_PROBE_TL
@@ -87,6 +93,7 @@ __device__ __forceinline__ void lds_barrier() {
 
 __device__ __forceinline__ bf16x8 ld8g(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
+template <bool PRE>
 __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* Us = reinterpret_cast<bf16_t*>(smem);  // CM_ROWS x CM_S (U, later V)
@@ -113,6 +120,101 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) fw1[0][t][ks] = ld8g(wrow1 + t * 16 * CM_D + ks * 32);
 
+  if constexpr (PRE) {
+    // ---- phase -1: x_att = x + o wo^T + bo over the staged frames, LN0 -> U
+    // o rows -> Gs (free until phase 1); frames outside [0, T) stage zeros
+    for (int c = tid; c < CM_ROWS * (CM_D / 8); c += CM_NT) {
+      const int r = c / (CM_D / 8), ch = c - r * (CM_D / 8), f = f0 + r;
+      const bool live = r < nrows && f >= 0 && f < a.T;
+      const int fc = min(max(f, 0), a.T - 1);
+      const uint4 v = *reinterpret_cast<const uint4*>(a.o + (ubase + fc) * CM_D + ch * 8);
+      *reinterpret_cast<uint4*>(Gs + r * CM_S + ch * 8) = live ? v : uint4{0u, 0u, 0u, 0u};
+    }
+    // wave w: units w*16 .. +15 (one tile) of all CM_MT1 frame tiles;
+    // D[unit 4g + e][frame mt*16 + fr]
+    const int u0 = w * 16 + 4 * g;
+    float4 xv[CM_MT1];
+#pragma unroll
+    for (int mt = 0; mt < CM_MT1; ++mt) {
+      const int f = min(max(f0 + mt * 16 + fr, 0), a.T - 1);
+      xv[mt] = *reinterpret_cast<const float4*>(a.x + (ubase + f) * CM_D + u0);
+    }
+    const float4 bo4 = a.bo ? *reinterpret_cast<const float4*>(a.bo + u0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const bf16_t* wrowo = a.wo + (long long)(w * 16 + fr) * CM_D + fk;
+    bf16x8 fwo[CM_D / 32];
+#pragma unroll
+    for (int kk = 0; kk < CM_D / 32; ++kk) fwo[kk] = ld8g(wrowo + kk * 32);
+    lds_barrier();
+    f32x4 acc[CM_MT1];
+#pragma unroll
+    for (int mt = 0; mt < CM_MT1; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < CM_D / 32; ++kk)
+#pragma unroll
+      for (int mt = 0; mt < CM_MT1; ++mt)
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            fwo[kk], *reinterpret_cast<const bf16x8*>(Gs + (mt * 16 + fr) * CM_S + kk * 32 + fk), acc[mt], 0, 0, 0);
+    float xa[CM_MT1][4];
+#pragma unroll
+    for (int mt = 0; mt < CM_MT1; ++mt) {
+      xa[mt][0] = xv[mt].x + (acc[mt][0] + bo4.x);
+      xa[mt][1] = xv[mt].y + (acc[mt][1] + bo4.y);
+      xa[mt][2] = xv[mt].z + (acc[mt][2] + bo4.z);
+      xa[mt][3] = xv[mt].w + (acc[mt][3] + bo4.w);
+    }
+    // x_att of this workgroup's output frames -> out (the residual of phase 3)
+#pragma unroll
+    for (int mt = 0; mt < CM_MT1; ++mt) {
+      const int r = mt * 16 + fr, f = f0 + r;
+      if (r >= a.padL && r < a.padL + CM_BM && f < a.T)
+        *reinterpret_cast<float4*>(a.out + (ubase + f) * CM_D + u0) =
+            make_float4(xa[mt][0], xa[mt][1], xa[mt][2], xa[mt][3]);
+    }
+    // LN0 over the 256 units of each frame: 4 per lane, 4 lanes per wave
+    // (col4), 16 waves through LDS (Cv: free until phase 2)
+    float* red = Cv;  // [CM_NW][CM_ROWS] x 2
+    float mean[CM_MT1], rstd[CM_MT1];
+#pragma unroll
+    for (int mt = 0; mt < CM_MT1; ++mt) {
+      const float ps = col4_sum((xa[mt][0] + xa[mt][1]) + (xa[mt][2] + xa[mt][3]));
+      if (g == 0) red[w * CM_ROWS + mt * 16 + fr] = ps;
+    }
+    lds_barrier();
+#pragma unroll
+    for (int mt = 0; mt < CM_MT1; ++mt) {
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < CM_NW; ++k) t += red[k * CM_ROWS + mt * 16 + fr];
+      mean[mt] = t * (1.0f / CM_D);
+      float q = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) q += (xa[mt][e] - mean[mt]) * (xa[mt][e] - mean[mt]);
+      q = col4_sum(q);
+      if (g == 0) red[CM_NW * CM_ROWS + w * CM_ROWS + mt * 16 + fr] = q;
+    }
+    lds_barrier();
+    const float4 g04 = *reinterpret_cast<const float4*>(a.g0 + u0);
+    const float4 b04 = *reinterpret_cast<const float4*>(a.b0 + u0);
+#pragma unroll
+    for (int mt = 0; mt < CM_MT1; ++mt) {
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < CM_NW; ++k) t += red[CM_NW * CM_ROWS + k * CM_ROWS + mt * 16 + fr];
+      rstd[mt] = 1.0f / sqrtf(t * (1.0f / CM_D) + a.eps0);
+      const int r = mt * 16 + fr, f = f0 + r;
+      const bool live = r < nrows && f >= 0 && f < a.T;
+      uint2 pk = make_uint2(0u, 0u);
+      if (live) {
+        pk.x = (uint32_t)f32_to_bf16((xa[mt][0] - mean[mt]) * rstd[mt] * g04.x + b04.x) |
+               ((uint32_t)f32_to_bf16((xa[mt][1] - mean[mt]) * rstd[mt] * g04.y + b04.y) << 16);
+        pk.y = (uint32_t)f32_to_bf16((xa[mt][2] - mean[mt]) * rstd[mt] * g04.z + b04.z) |
+               ((uint32_t)f32_to_bf16((xa[mt][3] - mean[mt]) * rstd[mt] * g04.w + b04.w) << 16);
+      }
+      *reinterpret_cast<uint2*>(Us + r * CM_S + u0) = pk;
+    }
+    // the x_att stores are visible to every wave before phase 3 reads them
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  } else {
   // ---- phase 0: LN0 of the staged frames -> U (bf16) ----
   // all of the wave's row loads are issued before the first reduction
   {
@@ -145,7 +247,9 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       *reinterpret_cast<uint2*>(Us + r * CM_S + lane * 4) = pk;
     }
   }
+  }
   lds_barrier();
+  if constexpr (PRE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   CM_TL(1);
 
   // ---- phase 1: G = GLU(U W1p^T + b1p) over CM_ROWS frames ----
@@ -225,7 +329,8 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
 #pragma unroll
     for (int mt = 0; mt < CM_MT3; ++mt) {
       const int f = min(t0 + mt * 16 + fr, a.T - 1);
-      xr[t][mt] = *reinterpret_cast<const float4*>(a.x + (ubase + f) * CM_D + w * 16 * T3 + t * 16 + 4 * g);
+      // the residual: x, or (PRE) x_att written by phase -1 into out
+      xr[t][mt] = *reinterpret_cast<const float4*>((PRE ? a.out : a.x) + (ubase + f) * CM_D + w * 16 * T3 + t * 16 + 4 * g);
     }
 
   // ---- phase 2: depthwise conv (register window) -> fp32 tile; LN1 -> Swish -> V (over U) ----
@@ -356,10 +461,11 @@ SBK_API int sbk_probe_cm_tl(unsigned long long* out) {
 
 SBK_API int sbk_conv_module_supported(int D, int K) { return D == CM_D && K >= 1 && K <= CM_KMAX; }
 
-SBK_API int sbk_conv_module(const float* x, float* out, int B, int T, int D, const float* ln0_w, const float* ln0_b,
-                            float eps0, const void* w1p, const float* b1p, const float* wc, const float* bc, int K,
-                            int causal, const float* ln1_w, const float* ln1_b, float eps1, const void* w2,
-                            const float* b2, const unsigned char* kpm, void* stream) {
+SBK_API int sbk_conv_module_pre(const float* x, const void* o, const void* wo, const float* bo, float* out, int B,
+                                int T, int D, const float* ln0_w, const float* ln0_b, float eps0, const void* w1p,
+                                const float* b1p, const float* wc, const float* bc, int K, int causal,
+                                const float* ln1_w, const float* ln1_b, float eps1, const void* w2, const float* b2,
+                                const unsigned char* kpm, void* stream) {
   if (B <= 0 || T <= 0 || !sbk_conv_module_supported(D, K) || !x || !out || x == out) return SBK_ERR_ARG;
   if (!ln0_w || !ln0_b || !w1p || !b1p || !wc || !ln1_w || !ln1_b || !w2) return SBK_ERR_ARG;
   const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
@@ -367,6 +473,9 @@ SBK_API int sbk_conv_module(const float* x, float* out, int B, int T, int D, con
                        reinterpret_cast<uintptr_t>(w1p) | reinterpret_cast<uintptr_t>(b1p) |
                        reinterpret_cast<uintptr_t>(w2) | reinterpret_cast<uintptr_t>(b2);
   if (al & 15) return SBK_ERR_ARG;
+  if ((o == nullptr) != (wo == nullptr) ||
+      ((reinterpret_cast<uintptr_t>(o) | reinterpret_cast<uintptr_t>(wo) | reinterpret_cast<uintptr_t>(bo)) & 15))
+    return SBK_ERR_ARG;
   ConvModArgs a;
   a.x = x; a.out = out; a.B = B; a.T = T; a.K = K; a.padL = causal ? K - 1 : (K - 1) / 2;
   a.g0 = ln0_w; a.b0 = ln0_b; a.eps0 = eps0;
@@ -375,18 +484,32 @@ SBK_API int sbk_conv_module(const float* x, float* out, int B, int T, int D, con
   a.g1 = ln1_w; a.b1n = ln1_b; a.eps1 = eps1;
   a.w2 = reinterpret_cast<const bf16_t*>(w2); a.b2 = b2;
   a.kpm = reinterpret_cast<const uint8_t*>(kpm);
+  a.o = reinterpret_cast<const bf16_t*>(o); a.wo = reinterpret_cast<const bf16_t*>(wo); a.bo = bo;
   const long long grid = (long long)B * ((T + CM_BM - 1) / CM_BM);
   if (grid > 0x7fffffffLL) return SBK_ERR_ARG;
   constexpr size_t lds = conv_module_lds();
   static_assert(lds <= 160 * 1024, "LDS budget");
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_module_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
+    for (const void* k : {reinterpret_cast<const void*>(&conv_module_kernel<false>),
+                          reinterpret_cast<const void*>(&conv_module_kernel<true>)}) {
+      hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return (int)e;
+    }
     attr = true;
   }
-  hipLaunchKernelGGL(conv_module_kernel, dim3((unsigned)grid), dim3(CM_NT), lds, (hipStream_t)stream, a);
+  if (o)
+    hipLaunchKernelGGL(conv_module_kernel<true>, dim3((unsigned)grid), dim3(CM_NT), lds, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(conv_module_kernel<false>, dim3((unsigned)grid), dim3(CM_NT), lds, (hipStream_t)stream, a);
   SBK_CHECK_LAUNCH();
   return 0;
+}
+
+SBK_API int sbk_conv_module(const float* x, float* out, int B, int T, int D, const float* ln0_w, const float* ln0_b,
+                            float eps0, const void* w1p, const float* b1p, const float* wc, const float* bc, int K,
+                            int causal, const float* ln1_w, const float* ln1_b, float eps1, const void* w2,
+                            const float* b2, const unsigned char* kpm, void* stream) {
+  return sbk_conv_module_pre(x, nullptr, nullptr, nullptr, out, B, T, D, ln0_w, ln0_b, eps0, w1p, b1p, wc, bc, K,
+                             causal, ln1_w, ln1_b, eps1, w2, b2, kpm, stream);
 }

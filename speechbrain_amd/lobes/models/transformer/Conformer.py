@@ -123,8 +123,9 @@ class ConvolutionModule(nn.Module):
                 and self.bottleneck[0].bias is not None and isinstance(self.after_conv[1], Swish)
                 and getattr(self.after_conv[1], "beta", 1) == 1)
 
-    def run_fused(self, x2d, B, T, pad_mask_u8=None):
-        """x2d + mask(ConvolutionModule(x2d)) in one launch (bf16 MFMA)."""
+    def run_fused(self, x2d, B, T, pad_mask_u8=None, pre=None):
+        """x2d + mask(ConvolutionModule(x2d)) in one launch (bf16 MFMA);
+        pre = (o, wo, bo): on x2d + o wo^T + bo (the MHSA out_proj fused in)."""
         w1p, b1p, w2 = self.kernel_weights(_bf16)
         ln = self.after_conv[0]
         lin = self.after_conv[2]
@@ -133,7 +134,7 @@ class ConvolutionModule(nn.Module):
         return _enc.conv_module(x2d, B, T, self.ln_params(), w1p, b1p, wc,
                                 self.conv.bias.detach() if self.conv.bias is not None else None, self.causal,
                                 (ln.weight.detach(), ln.bias.detach(), ln.eps), w2,
-                                lin.bias.detach() if lin.bias is not None else None, pad_mask_u8)
+                                lin.bias.detach() if lin.bias is not None else None, pad_mask_u8, pre=pre)
 
     def train_run(self, x2d, B, T, dtype, pad_mask_u8=None, residual=None):
         """Differentiable chain (training path, _autograd): residual +
@@ -212,11 +213,16 @@ class ConformerEncoderLayer(nn.Module):
                                        next_dtype=dtype)
             cm = self.convolution_module
             if USE_CONV_MODULE_KERNEL and cm.fusable(dtype, x.shape[1]):
-                # attention (+ output projection + residual), then the whole
+                # attention, then the output projection + residual + the whole
                 # convolution module (its LayerNorms included) in one launch
-                x, attn = self.mha_layer.attend(u, B, T, pos, kpm_u8, dtype, need_attn, residual=x, pk=pk,
-                                                qkv=qkv)
-                x = cm.run_fused(x, B, T, kpm_u8)
+                if hasattr(self.mha_layer, "attend_heads"):
+                    o, attn, pre = self.mha_layer.attend_heads(u, B, T, pos, kpm_u8, dtype, need_attn, pk=pk,
+                                                               qkv=qkv)
+                    x = cm.run_fused(x, B, T, kpm_u8, pre=pre)
+                else:
+                    x, attn = self.mha_layer.attend(u, B, T, pos, kpm_u8, dtype, need_attn, residual=x, pk=pk,
+                                                    qkv=qkv)
+                    x = cm.run_fused(x, B, T, kpm_u8)
             else:
                 # attention output projection + residual + the conv module's LayerNorm in one launch
                 x, attn, uc = self.mha_layer.attend(u, B, T, pos, kpm_u8, dtype, need_attn, residual=x,

@@ -113,6 +113,24 @@ class RelPosMHAXL(nn.Module):
         w_in = self.kernel_weights(dtype)[0]
         return w_in if _enc.ffn_proj_supported(self.embed_dim, 256, w_in.shape[0]) else None
 
+    def attend_heads(self, x2d, B, T, pos_embs, kpm_u8, dtype, need_weights, pk=None, qkv=None):
+        """attend without the output projection: (o (B*T, d) in dtype, attn,
+        (o, out_proj weight, bias)) for a consumer that applies out_proj
+        itself (sbk_conv_module_pre)."""
+        if self.vbias is not None:
+            raise NotImplementedError("vbias=True is not on the RelPosMHAXL hot path")
+        w_in, w_pos, w_out = self.kernel_weights(dtype)
+        if qkv is None:
+            qkv = _enc.gemm(x2d, w_in, out_dtype=dtype)
+        if pk is None:
+            pos = pos_embs.reshape(-1, self.embed_dim)
+            if pos.dtype != dtype:
+                pos = _enc.cast_bf16(pos.float().contiguous()) if dtype == torch.bfloat16 else pos.float()
+            pk = _enc.gemm(pos.contiguous(), w_pos, out_dtype=dtype)
+        o, probs = _enc.relpos_attention(qkv, pk, self.pos_bias_u.detach(), self.pos_bias_v.detach(), kpm_u8, B, T,
+                                         self.num_heads, self.head_dim, self.scale, need_weights)
+        return o, probs, (o, w_out, self.out_proj.bias.detach())
+
     def attend(self, x2d, B, T, pos_embs, kpm_u8, dtype, need_weights, residual=None, post_ln=None, pk=None,
                qkv=None):
         """Core used by the fused Conformer layer: x2d (B*T, d) in `dtype`

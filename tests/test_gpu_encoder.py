@@ -419,3 +419,35 @@ def test_fused_conv_module_vs_chain(dev, B, T, K, causal, masked):
     r32 = x.cpu().view(B, T, 256) + OC.conv_module(x.cpu().view(B, T, 256), sd, "", K, causal, pm)
     err = (y.cpu().view(B, T, 256) - r32).abs().max().item()
     assert err < 0.1, err
+
+
+@pytest.mark.parametrize("B,T,K,causal,masked", [(32, 376, 31, False, True), (3, 37, 31, False, True),
+                                                 (2, 50, 7, True, False), (1, 5, 31, False, False)])
+def test_conv_module_with_out_proj(dev, B, T, K, causal, masked):
+    """sbk_conv_module_pre (the MHSA output projection + residual computed in
+    the conv module's prologue, x_att = x + o Wo^T + bo never written apart
+    from the launch's own rows) vs sbk_gemm(o, Wo, bo, res=x) followed by
+    sbk_conv_module: x_att is the same fp32 product in a different summation
+    order, so the LN0 bf16 rounding can flip — 2e-2 as the other fused
+    module tests."""
+    from speechbrain_amd.lobes.models.transformer.Conformer import ConvolutionModule
+    from speechbrain_amd import _enc
+    torch.manual_seed(K + T + 1)
+    cm = ConvolutionModule(256, K, causal=causal).to(dev).eval()
+    with torch.no_grad():
+        for p in cm.parameters():
+            p.add_(0.05 * torch.randn_like(p))
+    x = (torch.randn(B * T, 256) * 2 + 0.3).to(dev)
+    o = torch.randn(B * T, 256, device=dev).to(torch.bfloat16)
+    wo = _enc.cast_bf16(torch.randn(256, 256, device=dev) / 16)
+    bo = torch.randn(256, device=dev) * 0.1
+    kpm = None
+    if masked:
+        lens = torch.randint(1, T + 1, (B,))
+        lens[0] = T
+        kpm = (torch.arange(T)[None] >= lens[:, None]).to(torch.uint8).reshape(-1).to(dev)
+    with torch.no_grad():
+        y = cm.run_fused(x, B, T, kpm, pre=(o, wo, bo))
+        xa = _enc.gemm(o, wo, bias=bo, res=x)
+        ref = cm.run_fused(xa, B, T, kpm)
+    assert_close(y, ref, rtol=2e-2, name="conv module with out_proj")
