@@ -115,20 +115,29 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
   const bf16_t* wrow1 = a.w1 + (long long)(w * 32 + fr) * CM_D + fk;
   const bf16_t* wrow3 = a.w2 + (long long)(w * 16 * T3 + fr) * CM_D + fk;
   bf16x8 fw1[2][T1][2];  // [buffer][tile][ks]
+  auto load_fw1 = [&]() __attribute__((always_inline)) {
 #pragma unroll
-  for (int t = 0; t < T1; ++t)
+    for (int t = 0; t < T1; ++t)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) fw1[0][t][ks] = ld8g(wrow1 + t * 16 * CM_D + ks * 32);
+      for (int ks = 0; ks < 2; ++ks) fw1[0][t][ks] = ld8g(wrow1 + t * 16 * CM_D + ks * 32);
+  };
+  if constexpr (!PRE) load_fw1();  // (PRE: once phase -1's own fragments are dead)
 
+  // PRE: x_att of this lane's phase-3 outputs (units w*16 + 4g .., frames
+  // t0 + mt*16 + fr), moved across lanes from phase -1's staged-row layout
+  float4 xres[CM_MT3];
   if constexpr (PRE) {
     // ---- phase -1: x_att = x + o wo^T + bo over the staged frames, LN0 -> U
-    // o rows -> Gs (free until phase 1); frames outside [0, T) stage zeros
-    for (int c = tid; c < CM_ROWS * (CM_D / 8); c += CM_NT) {
-      const int r = c / (CM_D / 8), ch = c - r * (CM_D / 8), f = f0 + r;
-      const bool live = r < nrows && f >= 0 && f < a.T;
-      const int fc = min(max(f, 0), a.T - 1);
-      const uint4 v = *reinterpret_cast<const uint4*>(a.o + (ubase + fc) * CM_D + ch * 8);
-      *reinterpret_cast<uint4*>(Gs + r * CM_S + ch * 8) = live ? v : uint4{0u, 0u, 0u, 0u};
+    // every load first (o rows, x rows, wo fragments), then o rows -> Gs
+    // (free until phase 1); frames outside [0, T) stage zeros
+    constexpr int OC = (CM_ROWS * (CM_D / 8) + CM_NT - 1) / CM_NT;  // 16-B o chunks per thread
+    uint4 ov[OC];
+#pragma unroll
+    for (int i = 0; i < OC; ++i) {
+      const int c = min(tid + i * CM_NT, CM_ROWS * (CM_D / 8) - 1);
+      const int r = c / (CM_D / 8), ch = c - r * (CM_D / 8);
+      const int fc = min(max(f0 + r, 0), a.T - 1);
+      ov[i] = *reinterpret_cast<const uint4*>(a.o + (ubase + fc) * CM_D + ch * 8);
     }
     // wave w: units w*16 .. +15 (one tile) of all CM_MT1 frame tiles;
     // D[unit 4g + e][frame mt*16 + fr]
@@ -140,6 +149,16 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       xv[mt] = *reinterpret_cast<const float4*>(a.x + (ubase + f) * CM_D + u0);
     }
     const float4 bo4 = a.bo ? *reinterpret_cast<const float4*>(a.bo + u0) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < OC; ++i) {
+      const int c = tid + i * CM_NT;
+      if (c < CM_ROWS * (CM_D / 8)) {
+        const int r = c / (CM_D / 8), ch = c - r * (CM_D / 8), f = f0 + r;
+        const bool live = r < nrows && f >= 0 && f < a.T;
+        *reinterpret_cast<uint4*>(Gs + r * CM_S + ch * 8) = live ? ov[i] : uint4{0u, 0u, 0u, 0u};
+      }
+    }
+    // (the wo fragments after the o chunks are dead: 128-VGPR budget at 16 waves)
     const bf16_t* wrowo = a.wo + (long long)(w * 16 + fr) * CM_D + fk;
     bf16x8 fwo[CM_D / 32];
 #pragma unroll
@@ -154,6 +173,7 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       for (int mt = 0; mt < CM_MT1; ++mt)
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
             fwo[kk], *reinterpret_cast<const bf16x8*>(Gs + (mt * 16 + fr) * CM_S + kk * 32 + fk), acc[mt], 0, 0, 0);
+    load_fw1();
     float xa[CM_MT1][4];
 #pragma unroll
     for (int mt = 0; mt < CM_MT1; ++mt) {
@@ -162,13 +182,26 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       xa[mt][2] = xv[mt].z + (acc[mt][2] + bo4.z);
       xa[mt][3] = xv[mt].w + (acc[mt][3] + bo4.w);
     }
-    // x_att of this workgroup's output frames -> out (the residual of phase 3)
+    // phase 3's residual: output frame mt*16 + fr is staged row mt*16 + fr +
+    // padL, held (same units) by lane (fr + padL) % 16 of tile (mt*16 + fr +
+    // padL) / 16: two lane permutes per value and a select
+    {
+      const int q = a.padL >> 4, rr = a.padL & 15;  // q <= 1 (K <= 31)
+      const int src = ((lane & 0x30) + ((fr + rr) & 15)) << 2;
+      const bool hi = fr + rr >= 16;
 #pragma unroll
-    for (int mt = 0; mt < CM_MT1; ++mt) {
-      const int r = mt * 16 + fr, f = f0 + r;
-      if (r >= a.padL && r < a.padL + CM_BM && f < a.T)
-        *reinterpret_cast<float4*>(a.out + (ubase + f) * CM_D + u0) =
-            make_float4(xa[mt][0], xa[mt][1], xa[mt][2], xa[mt][3]);
+      for (int mt = 0; mt < CM_MT3; ++mt) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float lo_v = q == 0 ? xa[mt][e] : xa[mt + 1][e];
+          const float hi_v = q == 0 ? xa[mt + 1][e] : xa[mt + 2][e];
+          const float lo = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(lo_v)));
+          const float hv = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(hi_v)));
+          v[e] = hi ? hv : lo;
+        }
+        xres[mt] = make_float4(v[0], v[1], v[2], v[3]);
+      }
     }
     // LN0 over the 256 units of each frame: 4 per lane, 4 lanes per wave
     // (col4), 16 waves through LDS (Cv: free until phase 2)
@@ -212,8 +245,6 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       }
       *reinterpret_cast<uint2*>(Us + r * CM_S + u0) = pk;
     }
-    // the x_att stores are visible to every wave before phase 3 reads them
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   } else {
   // ---- phase 0: LN0 of the staged frames -> U (bf16) ----
   // all of the wave's row loads are issued before the first reduction
@@ -249,7 +280,6 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
   }
   }
   lds_barrier();
-  if constexpr (PRE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   CM_TL(1);
 
   // ---- phase 1: G = GLU(U W1p^T + b1p) over CM_ROWS frames ----
@@ -324,13 +354,17 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) fw3[0][t][ks] = ld8g(wrow3 + t * 16 * CM_D + ks * 32);
   float4 xr[T3][CM_MT3];
+  static_assert(T3 == 1, "phase 3: one 16-unit tile per wave (the units of phase -1)");
 #pragma unroll
   for (int t = 0; t < T3; ++t)
 #pragma unroll
     for (int mt = 0; mt < CM_MT3; ++mt) {
       const int f = min(t0 + mt * 16 + fr, a.T - 1);
-      // the residual: x, or (PRE) x_att written by phase -1 into out
-      xr[t][mt] = *reinterpret_cast<const float4*>((PRE ? a.out : a.x) + (ubase + f) * CM_D + w * 16 * T3 + t * 16 + 4 * g);
+      // the residual: x, or (PRE) x_att from phase -1
+      if constexpr (PRE)
+        xr[t][mt] = xres[mt];
+      else
+        xr[t][mt] = *reinterpret_cast<const float4*>(a.x + (ubase + f) * CM_D + w * 16 * T3 + t * 16 + 4 * g);
     }
 
   // ---- phase 2: depthwise conv (register window) -> fp32 tile; LN1 -> Swish -> V (over U) ----
@@ -467,6 +501,7 @@ SBK_API int sbk_conv_module_pre(const float* x, const void* o, const void* wo, c
                                 const float* ln1_w, const float* ln1_b, float eps1, const void* w2, const float* b2,
                                 const unsigned char* kpm, void* stream) {
   if (B <= 0 || T <= 0 || !sbk_conv_module_supported(D, K) || !x || !out || x == out) return SBK_ERR_ARG;
+  if (o && (causal ? K - 1 : (K - 1) / 2) > 31) return SBK_ERR_ARG;  // phase -1 lane map: padL < 32
   if (!ln0_w || !ln0_b || !w1p || !b1p || !wc || !ln1_w || !ln1_b || !w2) return SBK_ERR_ARG;
   const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
                        reinterpret_cast<uintptr_t>(ln0_w) | reinterpret_cast<uintptr_t>(ln0_b) |
