@@ -219,6 +219,19 @@ int sbk_ffn_proj(const float* x, int M, int D, int H, const float* g0, const flo
                  const float* gp, const float* bp, float epsp, float* out, const float* gn, const float* bn,
                  float epsn, void* u, int u_bf16, const void* wp, int np, void* yp, void* stream);
 
+/* Two consecutive FFN blocks in one launch: block A (g0 .. epsp, as
+ * sbk_ffn with its post-LN) then block B (g0b .. alphab: LN0, weights and
+ * alpha, no post-LN) on A's output, which never leaves the CU; then next-LN
+ * and the projection tail as sbk_ffn_proj.  out receives B's output.  The
+ * Conformer's FFN2 + norm2 of layer i with FFN1 + norm1 + in_proj of layer
+ * i+1 (Conformer.py:239-260, attention.py:549-553); H is common to both. */
+int sbk_ffn_chain(const float* x, int M, int D, int H, int act, float slope, const float* g0, const float* b0,
+                  float eps0, const void* w1, const float* b1, const void* w2, const float* b2, float alpha,
+                  const float* gp, const float* bp, float epsp, const float* g0b, const float* b0b, float eps0b,
+                  const void* w1b, const float* b1b, const void* w2b, const float* b2b, float alphab, float* out,
+                  const float* gn, const float* bn, float epsn, void* u, int u_bf16, const void* wp, int np,
+                  void* yp, void* stream);
+
 /* LayerNorm (normalization.py:172-223; Conformer.py:178,194,340): one or two
  * chained LayerNorms over rows of x (M, D) fp32, D <= 1024. */
 int sbk_layernorm(const float* x, int M, int D, const float* g1, const float* b1, float eps1, void* out1,

@@ -264,6 +264,44 @@ def ffn_proj(x, ln0, w1, b1, act, slope, w2, b2, alpha, next_ln, wp, post_ln=Non
                                   float(alpha), gp, bp, float(ep), next_ln[0], next_ln[1], float(next_ln[2]), wp)
 
 
+@torch.library.custom_op("sbk::ffn_chain", mutates_args=())
+def _ffn_chain_op(x: torch.Tensor, act: int, slope: float, g0: torch.Tensor, b0: torch.Tensor, e0: float,
+                  w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor, alpha: float,
+                  gp: Optional[torch.Tensor], bp: Optional[torch.Tensor], ep: float, g0b: torch.Tensor,
+                  b0b: torch.Tensor, e0b: float, w1b: torch.Tensor, b1b: torch.Tensor, w2b: torch.Tensor,
+                  b2b: torch.Tensor, alphab: float, gn: torch.Tensor, bn: torch.Tensor, en: float,
+                  wp: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    M, D = x.shape
+    H, NP = w1.shape[0], wp.shape[0]
+    out = torch.empty_like(x)
+    y = torch.empty(M, NP, device=x.device, dtype=_bf16)
+    rc = lib().sbk_ffn_chain(ptr(x), M, D, H, act, float(slope), ptr(g0), ptr(b0), float(e0), ptr(w1), ptr(b1),
+                             ptr(w2), ptr(b2), float(alpha), ptr(gp), ptr(bp), float(ep), ptr(g0b), ptr(b0b),
+                             float(e0b), ptr(w1b), ptr(b1b), ptr(w2b), ptr(b2b), float(alphab), ptr(out), ptr(gn),
+                             ptr(bn), float(en), None, 1, ptr(wp), NP, ptr(y), stream_of(x))
+    check(rc, "sbk_ffn_chain")
+    return out, y
+
+
+@_ffn_chain_op.register_fake
+def _(x, act, slope, g0, b0, e0, w1, b1, w2, b2, alpha, gp, bp, ep, g0b, b0b, e0b, w1b, b1b, w2b, b2b, alphab, gn,
+      bn, en, wp):
+    return torch.empty_like(x), x.new_empty((x.shape[0], wp.shape[0]), dtype=_bf16)
+
+
+def ffn_chain(x, a, b, act, slope, next_ln, wp):
+    """Two FFN blocks in one launch — a = (ln0, w1, b1, w2, b2, alpha,
+    post_ln) then b = (ln0, w1, b1, w2, b2, alpha) on a's output, which stays
+    on chip — followed by next_ln and the projection wp (bf16, no bias):
+    returns (b's output fp32, next_ln(out) · wp^T bf16).  The Conformer's
+    FFN2 + norm2 of layer i with FFN1 + norm1 + in_proj of layer i+1."""
+    require_device(x, a[1], b[1], wp)
+    gp, bp, ep = a[6] if a[6] is not None else (None, None, 0.0)
+    return torch.ops.sbk.ffn_chain(x, ACT[act], float(slope), a[0][0], a[0][1], float(a[0][2]), a[1], a[2], a[3],
+                                   a[4], float(a[5]), gp, bp, float(ep), b[0][0], b[0][1], float(b[0][2]), b[1], b[2],
+                                   b[3], b[4], float(b[5]), next_ln[0], next_ln[1], float(next_ln[2]), wp)
+
+
 def ffn(x, ln0, w1, b1, act, slope, w2, b2, alpha, post_ln=None, next_ln=None, next_dtype=_bf16, out=None):
     """Fused macaron FFN block (bf16 MFMA): z = x + alpha * FFN(LN0(x));
     out = post_ln(z) if given; u = next_ln(out) (returned) if given.

@@ -56,6 +56,8 @@ SIGNATURES = {
     "sbk_ffn_supported": [_i, _i],
     "sbk_ffn": [_vp, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _i, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _vp, _f,
                 _vp, _i, _vp],
+    "sbk_ffn_chain": [_vp, _i, _i, _i, _i, _f, _vp, _vp, _f, _vp, _vp, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _f,
+                      _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _f, _vp, _i, _vp, _i, _vp, _vp],
     "sbk_ffn_proj": [_vp, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _i, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _vp,
                      _f, _vp, _i, _vp, _i, _vp, _vp],
     # conformer.hip

@@ -81,6 +81,15 @@ struct FfnArgs {
   const bf16_t* wp;  // (np, D) projection of next-LN(out), or null
   int np;
   bf16_t* yp;  // (M, np) bf16
+  // CHAIN: a second FFN block on the first one's output, which stays on chip
+  // (the first block's `out` is not written): FFN2 + norm2 of layer i, then
+  // FFN1 of layer i+1 with its own LN0, alpha, w1/b1/w2/b2; its result goes
+  // to `out`, next-LN and the projection tail as for a single block
+  const float *g0b, *b0b;
+  float eps0b;
+  const bf16_t *w1b, *w2b;
+  const float *b1b, *b2b;
+  float alphab;
 };
 
 __device__ __forceinline__ bf16x8 ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
@@ -190,7 +199,7 @@ __device__ unsigned long long g_ffn_tl[16][80];
   } while (0)
 #endif
 
-template <int D, int ACT, bool PROJ>
+template <int D, int ACT, bool PROJ, bool CHAIN>
 __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   constexpr int BM = FFN_BM, HC = 256, NW = FFN_NW, NT = FFN_NT;
   constexpr int XS = D + 16, HS = HC + 16;   // LDS row strides (elements), +32 B pad: conflict-free b128 reads
@@ -209,16 +218,17 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   bf16_t* ring = reinterpret_cast<bf16_t*>(smem);          // NB x TROWS x BK (linear 128-B rows)
   bf16_t* Xn = ring + NB * TROWS * BK;                      // BM x XS
   bf16_t* Hs = Xn + BM * XS;                                // 2 x BM x HS
-  float* b1s = reinterpret_cast<float*>(Hs + 2 * BM * HS);  // H
-  float (*red)[BM] = reinterpret_cast<float (*)[BM]>(b1s + a.H);  // NW x BM
+  float* b1s = reinterpret_cast<float*>(Hs + 2 * BM * HS);  // H (CHAIN: 2 H, block A then B)
+  float (*red)[BM] = reinterpret_cast<float (*)[BM]>(b1s + (CHAIN ? 2 : 1) * a.H);  // NW x BM
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int fr = lane & 15, g = lane >> 4, fk = 8 * g;
   const int m0 = blockIdx.x * BM;
   const int NCH = a.H / HC;
-  const int S = NCH * SPC;                              // FFN K-steps
+  const int S = NCH * SPC;                              // K-steps of one FFN block
+  const int SF = CHAIN ? 2 * S : S;                     // FFN K-steps (blocks A, B)
   const int SP = PROJ ? (a.np / TROWS) * K1 : 0;        // projection K-steps
-  const int ST = S + SP;
+  const int ST = SF + SP;
 #ifdef SBK_PROBE_TL
   const int tl_rec = blockIdx.x == 128 ? w : -1;
 #endif
@@ -255,14 +265,18 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   auto issue = [&](int s, int slot) __attribute__((always_inline)) {
     const bf16_t* base;
     int ld;
-    if (PROJ && s >= S) {
-      const int pj = s - S, nc = pj / K1, r = pj - nc * K1;
+    if (PROJ && s >= SF) {
+      const int pj = s - SF, nc = pj / K1, r = pj - nc * K1;
       base = a.wp + (long long)nc * TROWS * D + r * BK;
       ld = D;
     } else {
-      const int c = s / SPC, r = s - c * SPC;
+      const bool sb = CHAIN && s >= S;  // block B
+      const int sl = sb ? s - S : s;
+      const int c = sl / SPC, r = sl - c * SPC;
       const bool p1 = r < K1;
-      base = p1 ? a.w1 + (long long)c * HC * D + r * BK : a.w2 + c * HC + (r - K1) * BK;
+      const bf16_t* w1 = sb ? a.w1b : a.w1;
+      const bf16_t* w2 = sb ? a.w2b : a.w2;
+      base = p1 ? w1 + (long long)c * HC * D + r * BK : w2 + c * HC + (r - K1) * BK;
       ld = p1 ? D : a.H;
     }
     bf16_t* dst = ring + slot * TROWS * BK;
@@ -298,6 +312,8 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     *reinterpret_cast<uint2*>(Xn + rr * XS + lane * PER) = pk;
   }
   for (int i = tid; i < a.H; i += NT) b1s[i] = a.b1[i];
+  if (CHAIN)
+    for (int i = tid; i < a.H; i += NT) b1s[a.H + i] = a.b1b[i];
 
   f32x4 acc1[T][MT], acc2[T][MT];
 #pragma unroll
@@ -328,10 +344,62 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     for (int ks = 0; ks < BK / 32; ++ks)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) xa[r][ks][mt] = ld8(Xn + (mt * 16 + fr) * XS + r * BK + ks * 32 + fk);
+  for (int stage = 0; stage < (CHAIN ? 2 : 1); ++stage) {
+  if (CHAIN && stage == 1) {
+    // ---- between the blocks: A's rows z = x + alpha (acc2 + b2) -> post-LN
+    // (norm2) are B's residual (held in xres) and, through B's LN0, its
+    // phase-1 operand (Xn -> VGPR fragments); nothing goes to HBM
+    float z[T][MT][4];
+#pragma unroll
+    for (int j = 0; j < T; ++j) {
+      const int d = (w * T + j) * 16 + 4 * g;
+      const float4 bb = *reinterpret_cast<const float4*>(a.b2 + d);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const float4 xr = xres[j][mt];
+        z[j][mt][0] = xr.x + a.alpha * (acc2[j][mt][0] + bb.x);
+        z[j][mt][1] = xr.y + a.alpha * (acc2[j][mt][1] + bb.y);
+        z[j][mt][2] = xr.z + a.alpha * (acc2[j][mt][2] + bb.z);
+        z[j][mt][3] = xr.w + a.alpha * (acc2[j][mt][3] + bb.w);
+        acc1[j][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc2[j][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    if (a.gp) row_ln<D, T, MT, NW>(z, red, a.gp, a.bp, a.epsp, w, g, fr);
+#pragma unroll
+    for (int j = 0; j < T; ++j)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) xres[j][mt] = make_float4(z[j][mt][0], z[j][mt][1], z[j][mt][2], z[j][mt][3]);
+    row_ln<D, T, MT, NW>(z, red, a.g0b, a.b0b, a.eps0b, w, g, fr);
+#pragma unroll
+    for (int j = 0; j < T; ++j) {
+      const int d = (w * T + j) * 16 + 4 * g;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        uint2 pk;
+        pk.x = (uint32_t)f32_to_bf16(z[j][mt][0]) | ((uint32_t)f32_to_bf16(z[j][mt][1]) << 16);
+        pk.y = (uint32_t)f32_to_bf16(z[j][mt][2]) | ((uint32_t)f32_to_bf16(z[j][mt][3]) << 16);
+        *reinterpret_cast<uint2*>(Xn + (mt * 16 + fr) * XS + d) = pk;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int r = 0; r < K1; ++r)
+#pragma unroll
+      for (int ks = 0; ks < BK / 32; ++ks)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const uint32_t la =
+              (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) bf16_t*)(Xn + (mt * 16 + fr) * XS + r * BK + ks * 32 + fk));
+          asm volatile("ds_read_b128 %0, %1" : "=v"(xa[r][ks][mt]) : "v"(la) : "memory");
+        }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
   for (int c = 0; c < NCH; ++c)
 #pragma unroll
   for (int r = 0; r < SPC; ++r) {
-    const int s = c * SPC + r;
+    const int s = stage * S + c * SPC + r;
     // this wave's rows of tile s landed (tile s+1 stays in flight)
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL * (NB - 1)) : "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -376,7 +444,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
           // in-flight LDS-DMA tiles), draining the weight stream
           f32x4 bb;
           {
-            const uint32_t la = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)(b1s + c * HC + n));
+            const uint32_t la = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)(b1s + stage * a.H + c * HC + n));
             asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(bb) : "v"(la) : "memory");
           }
 #pragma unroll
@@ -405,26 +473,31 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     }
     if (s < 34) FFN_TL(3 + 2 * s);
   }
+  }  // stage
   if (!PROJ) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the tail reloads
   FFN_TL(70);
 
   // ---- epilogue: lane holds rows m = mt*16 + fr, units d = (w*T + j)*16 + 4g .. +3
+  // (CHAIN: the parameters of block B, which has no post-LN)
+  const float* b2f = CHAIN ? a.b2b : a.b2;
+  const float alphaf = CHAIN ? a.alphab : a.alpha;
+  const float* gpf = CHAIN ? nullptr : a.gp;
   float z[T][MT][4];
 #pragma unroll
   for (int j = 0; j < T; ++j) {
     const int d = (w * T + j) * 16 + 4 * g;
-    const float4 bb = *reinterpret_cast<const float4*>(a.b2 + d);
+    const float4 bb = *reinterpret_cast<const float4*>(b2f + d);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const float4 xr = xres[j][mt];
-      z[j][mt][0] = xr.x + a.alpha * (acc2[j][mt][0] + bb.x);
-      z[j][mt][1] = xr.y + a.alpha * (acc2[j][mt][1] + bb.y);
-      z[j][mt][2] = xr.z + a.alpha * (acc2[j][mt][2] + bb.z);
-      z[j][mt][3] = xr.w + a.alpha * (acc2[j][mt][3] + bb.w);
+      z[j][mt][0] = xr.x + alphaf * (acc2[j][mt][0] + bb.x);
+      z[j][mt][1] = xr.y + alphaf * (acc2[j][mt][1] + bb.y);
+      z[j][mt][2] = xr.z + alphaf * (acc2[j][mt][2] + bb.z);
+      z[j][mt][3] = xr.w + alphaf * (acc2[j][mt][3] + bb.w);
     }
   }
   FFN_TL(71);
-  if (a.gp) row_ln<D, T, MT, NW>(z, red, a.gp, a.bp, a.epsp, w, g, fr);
+  if (gpf) row_ln<D, T, MT, NW>(z, red, gpf, a.bp, a.epsp, w, g, fr);
   if (PROJ) {
     // u = next-LN(out) -> Xn (bf16, the A operand of the projection), then
     // the out stores: every compiler-visible LDS access precedes them, so no
@@ -474,8 +547,8 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
       }
     }
     // ---- projection y = u . Wp^T (bf16), 256 output columns per K1 steps
-    for (int s = S; s < ST; s += K1) {
-      const int nc = (s - S) / K1;
+    for (int s = SF; s < ST; s += K1) {
+      const int nc = (s - SF) / K1;
 #pragma unroll
       for (int r = 0; r < K1; ++r) {
         // tile s+r landed: younger than it are tile s+r+1 and, on the first
@@ -560,36 +633,42 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
 }
 
 template <int D>
-size_t ffn_lds(int H) {
-  // 2-slot weight ring, Xn, two hidden-chunk buffers, b1, the row-reduction scratch
+size_t ffn_lds(int H, bool chain) {
+  // 2-slot weight ring, Xn, two hidden-chunk buffers, b1 (two with CHAIN), the row-reduction scratch
   return ((size_t)2 * 256 * 64 + (size_t)FFN_BM * (D + 16) + (size_t)2 * FFN_BM * (256 + 16)) * sizeof(bf16_t) +
-         (size_t)H * 4 + (size_t)FFN_NW * FFN_BM * 4;
+         (size_t)(chain ? 2 : 1) * H * 4 + (size_t)FFN_NW * FFN_BM * 4;
 }
 
-template <int D, int ACT, bool PROJ>
+template <int D, int ACT, bool PROJ, bool CHAIN>
 int launch_ffn_act(const FfnArgs& a, size_t lds, hipStream_t s) {
   static bool attr = false;  // > 64 KB dynamic LDS: opt in once per kernel
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ffn_kernel<D, ACT, PROJ>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ffn_kernel<D, ACT, PROJ, CHAIN>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  hipLaunchKernelGGL((ffn_kernel<D, ACT, PROJ>), dim3((a.M + FFN_BM - 1) / FFN_BM), dim3(FFN_NT), lds, s, a);
+  hipLaunchKernelGGL((ffn_kernel<D, ACT, PROJ, CHAIN>), dim3((a.M + FFN_BM - 1) / FFN_BM), dim3(FFN_NT), lds, s, a);
   return 0;
 }
 
-template <int D, bool PROJ>
+template <int D, bool PROJ, bool CHAIN>
 int launch_ffn(const FfnArgs& a, hipStream_t s) {
-  const size_t lds = ffn_lds<D>(a.H);
+  const size_t lds = ffn_lds<D>(a.H, CHAIN);
   if (lds > 160 * 1024) return SBK_ERR_ARG;
   switch (a.act) {
-    case ACT_SWISH: return launch_ffn_act<D, ACT_SWISH, PROJ>(a, lds, s);
-    case ACT_LRELU: return launch_ffn_act<D, ACT_LRELU, PROJ>(a, lds, s);
-    case ACT_GELU: return launch_ffn_act<D, ACT_GELU, PROJ>(a, lds, s);
-    case ACT_NONE: return launch_ffn_act<D, ACT_NONE, PROJ>(a, lds, s);
+    case ACT_SWISH: return launch_ffn_act<D, ACT_SWISH, PROJ, CHAIN>(a, lds, s);
+    case ACT_LRELU: return launch_ffn_act<D, ACT_LRELU, PROJ, CHAIN>(a, lds, s);
+    case ACT_GELU: return launch_ffn_act<D, ACT_GELU, PROJ, CHAIN>(a, lds, s);
+    case ACT_NONE: return launch_ffn_act<D, ACT_NONE, PROJ, CHAIN>(a, lds, s);
     default: return SBK_ERR_ARG;
   }
+}
+
+int ffn_dispatch(const FfnArgs& a, hipStream_t s) {
+  const bool proj = a.wp != nullptr, chain = a.w1b != nullptr;
+  if (chain) return proj ? launch_ffn<256, true, true>(a, s) : launch_ffn<256, false, true>(a, s);
+  return proj ? launch_ffn<256, true, false>(a, s) : launch_ffn<256, false, false>(a, s);
 }
 
 }  // namespace
@@ -630,8 +709,53 @@ SBK_API int sbk_ffn_proj(const float* x, int M, int D, int H, const float* g0, c
   a.out = out;
   a.gn = gn; a.bn = bn; a.epsn = epsn; a.u = u; a.u_bf16 = u_bf16;
   a.wp = reinterpret_cast<const bf16_t*>(wp); a.np = np; a.yp = reinterpret_cast<bf16_t*>(yp);
-  hipStream_t s = (hipStream_t)stream;
-  const int rc = wp ? launch_ffn<256, true>(a, s) : launch_ffn<256, false>(a, s);
+  a.g0b = nullptr; a.b0b = nullptr; a.eps0b = 0.f; a.w1b = nullptr; a.w2b = nullptr; a.b1b = nullptr;
+  a.b2b = nullptr; a.alphab = 0.f;
+  const int rc = ffn_dispatch(a, (hipStream_t)stream);
+  if (rc) return rc;
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+// Two consecutive FFN blocks in one launch (the second on the first's
+// output, which never leaves the CU): block A (g0 .. gp: e.g. FFN2 + norm2 of
+// Conformer layer i) then block B (g0b .. alphab: FFN1 of layer i+1, no
+// post-LN), then next-LN / projection tail as sbk_ffn_proj.  out receives
+// block B's output only.
+SBK_API int sbk_ffn_chain(const float* x, int M, int D, int H, int act, float slope, const float* g0, const float* b0,
+                          float eps0, const void* w1, const float* b1, const void* w2, const float* b2, float alpha,
+                          const float* gp, const float* bp, float epsp, const float* g0b, const float* b0b,
+                          float eps0b, const void* w1b, const float* b1b, const void* w2b, const float* b2b,
+                          float alphab, float* out, const float* gn, const float* bn, float epsn, void* u,
+                          int u_bf16, const void* wp, int np, void* yp, void* stream) {
+  if (!g0b || !b0b || !w1b || !b1b || !w2b || !b2b) return SBK_ERR_ARG;
+  if ((reinterpret_cast<uintptr_t>(g0b) | reinterpret_cast<uintptr_t>(b0b) | reinterpret_cast<uintptr_t>(w1b) |
+       reinterpret_cast<uintptr_t>(b1b) | reinterpret_cast<uintptr_t>(w2b) | reinterpret_cast<uintptr_t>(b2b)) & 15)
+    return SBK_ERR_ARG;
+  if (M <= 0 || !sbk_ffn_supported(D, H) || !g0 || !b0 || !w1 || !b1 || !w2 || !b2 || !out) return SBK_ERR_ARG;
+  if (act == ACT_GLU || (gn && !u && !wp)) return SBK_ERR_ARG;
+  if (wp && (!gn || !bn || u || !yp || np <= 0 || np % 256)) return SBK_ERR_ARG;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(g0) |
+                       reinterpret_cast<uintptr_t>(b0) | reinterpret_cast<uintptr_t>(b1) |
+                       reinterpret_cast<uintptr_t>(b2) | reinterpret_cast<uintptr_t>(gp) |
+                       reinterpret_cast<uintptr_t>(bp) | reinterpret_cast<uintptr_t>(out) |
+                       reinterpret_cast<uintptr_t>(gn) | reinterpret_cast<uintptr_t>(bn) |
+                       reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(w1) | reinterpret_cast<uintptr_t>(w2) |
+                       reinterpret_cast<uintptr_t>(wp) | reinterpret_cast<uintptr_t>(yp);
+  if (al & 15) return SBK_ERR_ARG;
+  FfnArgs a;
+  a.x = x; a.M = M; a.H = H;
+  a.g0 = g0; a.b0 = b0; a.eps0 = eps0;
+  a.w1 = reinterpret_cast<const bf16_t*>(w1); a.b1 = b1; a.act = act; a.slope = slope;
+  a.w2 = reinterpret_cast<const bf16_t*>(w2); a.b2 = b2; a.alpha = alpha;
+  a.gp = gp; a.bp = bp; a.epsp = epsp;
+  a.out = out;
+  a.gn = gn; a.bn = bn; a.epsn = epsn; a.u = u; a.u_bf16 = u_bf16;
+  a.wp = reinterpret_cast<const bf16_t*>(wp); a.np = np; a.yp = reinterpret_cast<bf16_t*>(yp);
+  a.g0b = g0b; a.b0b = b0b; a.eps0b = eps0b;
+  a.w1b = reinterpret_cast<const bf16_t*>(w1b); a.w2b = reinterpret_cast<const bf16_t*>(w2b);
+  a.b1b = b1b; a.b2b = b2b; a.alphab = alphab;
+  const int rc = ffn_dispatch(a, (hipStream_t)stream);
   if (rc) return rc;
   SBK_CHECK_LAUNCH();
   return 0;

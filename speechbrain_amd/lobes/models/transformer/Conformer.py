@@ -41,6 +41,9 @@ _bf16 = torch.bfloat16
 # Fused convolution-module kernel on the bf16 path (sbk_conv_module); the
 # four-launch chain (LN, GLU GEMM, dwconv+LN+Swish, projection) otherwise.
 USE_CONV_MODULE_KERNEL = True
+# FFN2 (+ norm2) of layer i and FFN1 (+ norm1 + in_proj) of layer i+1 in one
+# launch (sbk_ffn_chain), the out_proj in the conv module's prologue
+USE_LAYER_CHAIN = True
 
 
 def _check_swish(act_module):
@@ -189,6 +192,17 @@ class ConformerEncoderLayer(nn.Module):
     def _ln(self, mod):
         return mod.weight.detach(), mod.bias.detach(), mod.eps
 
+    def chainable(self, dtype, d):
+        """Every block of this layer has its fused kernel (the chained stack)."""
+        if self.training and self.drop.p > 0:
+            return False
+        f1, f2 = self.ffn_module1, self.ffn_module2
+        mha = self.mha_layer
+        return (f1[1].fusable(dtype) and f2[1].fusable(dtype) and f1[1].act_name() == f2[1].act_name()
+                and f1[1].ffn[0].out_features == f2[1].ffn[0].out_features
+                and hasattr(mha, "fused_in_proj") and mha.fused_in_proj(dtype) is not None
+                and self.convolution_module.fusable(dtype, d))
+
     def fused(self, x, B, T, pos, kpm_u8, dtype, need_attn, u_in=None, next_ln=None, final_ln=None, pk=None):
         """One layer.  x: (B*T, d) fp32 residual stream; pos: (2T-1, d) in
         dtype; u_in: LN_ffn1(x) if a previous kernel already produced it;
@@ -333,6 +347,8 @@ class ConformerEncoder(nn.Module):
         u = None
         attns = []
         n = len(self.layers)
+        if USE_LAYER_CHAIN and all(layer.chainable(dtype, d) for layer in self.layers):
+            return self._run_chain(x, B, T, pos, kpm_u8, dtype, need_attn, pk_all)
         for i, layer in enumerate(self.layers):
             nxt = self.layers[i + 1].ffn_module1[0] if i + 1 < n else None
             next_ln = (nxt.weight.detach(), nxt.bias.detach(), nxt.eps) if nxt is not None else None
@@ -346,6 +362,36 @@ class ConformerEncoder(nn.Module):
         fn = self.norm.norm
         y, _ = _enc.layernorm(x, fn.weight.detach(), fn.bias.detach(), fn.eps, out1_dtype=_f32)
         return y, attns
+
+    def _run_chain(self, x, B, T, pos, kpm_u8, dtype, need_attn, pk_all):
+        """The fused stack as 3 launches per layer: [FFN2_i + norm2_i +
+        FFN1_{i+1} + norm1_{i+1} + in_proj_{i+1}] (sbk_ffn_chain), attention,
+        [out_proj + residual + conv module] (sbk_conv_module_pre); layer 0's
+        FFN1 is sbk_ffn_proj, the last FFN2 carries the closing LayerNorm."""
+        d = x.shape[1]
+        ln = ConformerEncoderLayer._ln
+        L = self.layers
+        l0 = L[0]
+        f1 = l0.ffn_module1
+        x, qkv = f1[1].run_fused_proj(x, ln(l0, f1[0]), 0.5, ln(l0, l0.norm1.norm), l0.mha_layer.fused_in_proj(dtype))
+        attns = []
+        for i, layer in enumerate(L):
+            _, attn, pre = layer.mha_layer.attend_heads(None, B, T, pos, kpm_u8, dtype, need_attn,
+                                                        pk=pk_all[:, i * d:(i + 1) * d], qkv=qkv)
+            attns.append(attn)
+            x = layer.convolution_module.run_fused(x, B, T, kpm_u8, pre=pre)
+            f2 = layer.ffn_module2
+            if i + 1 < len(L):
+                nl = L[i + 1]
+                a = f2[1].chain_block(ln(layer, f2[0]), 0.5, post_ln=ln(layer, layer.norm2.norm))
+                b = nl.ffn_module1[1].chain_block(ln(nl, nl.ffn_module1[0]), 0.5)
+                act, slope = f2[1].act_name()
+                x, qkv = _enc.ffn_chain(x, a, b, act, slope, ln(nl, nl.norm1.norm), nl.mha_layer.fused_in_proj(dtype))
+            else:
+                fn = self.norm.norm
+                _, y = f2[1].run_fused(x, ln(layer, f2[0]), 0.5, post_ln=ln(layer, layer.norm2.norm),
+                                       next_ln=(fn.weight.detach(), fn.bias.detach(), fn.eps), next_dtype=_f32)
+                return y, attns
 
     def forward(self, src, src_mask: Optional[torch.Tensor] = None,
                 src_key_padding_mask: Optional[torch.Tensor] = None, pos_embs: Optional[torch.Tensor] = None):

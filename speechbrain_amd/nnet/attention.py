@@ -272,6 +272,14 @@ class PositionalwiseFeedForward(nn.Module):
         return _enc.ffn(x, ln0, w1, b1, act, slope, w2, b2, alpha,
                         post_ln=post_ln, next_ln=next_ln, next_dtype=next_dtype, out=out)
 
+    def chain_block(self, ln0, alpha, post_ln=None):
+        """This block's parameters for _enc.ffn_chain: (ln0, w1, b1, w2, b2,
+        alpha, post_ln) in the fused kernel's formats."""
+        w1, w2 = self.kernel_weights(torch.bfloat16)
+        b1, b2 = (lin.bias.detach() if lin.bias is not None else torch.zeros(lin.out_features, device=w1.device)
+                  for lin in (self.ffn[0], self.ffn[3]))
+        return (ln0, w1, b1, w2, b2, alpha, post_ln)
+
     def run_fused_proj(self, x, ln0, alpha, next_ln, wp, post_ln=None):
         """run_fused with the next block's input projection on chip: returns
         (out fp32, next_ln(out) · wp^T bf16)."""

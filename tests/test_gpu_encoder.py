@@ -451,3 +451,50 @@ def test_conv_module_with_out_proj(dev, B, T, K, causal, masked):
         xa = _enc.gemm(o, wo, bias=bo, res=x)
         ref = cm.run_fused(xa, B, T, kpm)
     assert_close(y, ref, rtol=2e-2, name="conv module with out_proj")
+
+
+@pytest.mark.parametrize("H,M", [(1024, 12032), (1024, 1000), (512, 48)])
+def test_ffn_chain_vs_two_launches(dev, H, M):
+    """sbk_ffn_chain (FFN2 + norm2 of layer i, then FFN1 + norm1 + in_proj of
+    layer i+1, the intermediate rows kept on chip) vs sbk_ffn (with norm2)
+    followed by sbk_ffn_proj: the same rounding points, so only summation
+    order differs (2e-2 as the other fused-FFN tests)."""
+    from speechbrain_amd import _enc
+    from speechbrain_amd.nnet.attention import PositionalwiseFeedForward
+    from speechbrain_amd.nnet.activations import Swish
+    torch.manual_seed(2)
+    D = 256
+    fa = PositionalwiseFeedForward(H, input_size=D, activation=Swish).to(dev).eval()
+    fb = PositionalwiseFeedForward(H, input_size=D, activation=Swish).to(dev).eval()
+    x = (torch.randn(M, D) * 2 + 0.5).to(dev)
+    lns = [(torch.randn(D, device=dev) * 0.5 + 1, torch.randn(D, device=dev) * 0.1, 1e-5) for _ in range(4)]
+    wp = _enc.cast_bf16((torch.randn(768, D) / 16).to(dev))
+    with torch.no_grad():
+        out, y = _enc.ffn_chain(x, fa.chain_block(lns[0], 0.5, post_ln=lns[1]), fb.chain_block(lns[2], 0.5),
+                                "swish", 0.0, lns[3], wp)
+        mid, _ = fa.run_fused(x, lns[0], 0.5, post_ln=lns[1])
+        ref, yref = fb.run_fused_proj(mid, lns[2], 0.5, lns[3], wp)
+    assert_close(out, ref, rtol=2e-2, name="chain out")
+    assert_close(y.float(), yref.float(), rtol=2e-2, name="chain projection")
+
+
+def test_encoder_chain_vs_per_layer(dev):
+    """The chained stack (3 launches per layer) vs the per-layer fused path
+    on a config-3 encoder at full size: bf16 rounding points are the same
+    up to summation order, so 2e-2 of LayerNorm-scale values."""
+    from speechbrain_amd.lobes.models.transformer import Conformer as C
+    from speechbrain_amd.lobes.models.transformer.TransformerASR import TransformerASR
+    torch.manual_seed(0)
+    tr = TransformerASR(tgt_vocab=10, input_size=640, d_model=256, nhead=4, num_encoder_layers=12,
+                        num_decoder_layers=0, d_ffn=1024, dropout=0.0, encoder_module="conformer",
+                        attention_type="RelPosMHAXL", normalize_before=True, causal=False).to(dev).eval()
+    src = torch.randn(4, 376, 640, device=dev)
+    lens = torch.tensor([1.0, 0.8, 0.6, 1.0], device=dev)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        y_chain = tr.encode(src, lens)
+        C.USE_LAYER_CHAIN = False
+        try:
+            y_ref = tr.encode(src, lens)
+        finally:
+            C.USE_LAYER_CHAIN = True
+    assert_close(y_chain, y_ref, rtol=2e-2, name="chain vs per-layer")
