@@ -190,6 +190,12 @@ int sbk_gemm_ln(int dtype_bf16, const void* A, int lda, const void* W, int ldw, 
 /* 1 if the fused FFN kernel supports d_model D and d_ffn H (D == 256, H % 256 == 0, H <= 2048). */
 int sbk_ffn_supported(int D, int H);
 
+/* Batched C[b] = A[b] W[b]^T (bf16, K-contiguous rows; fp32 or bf16 out),
+ * element strides sA / sW / sC per batch: the per-(utterance, head) products
+ * of the rel-pos attention backward. */
+int sbk_gemm_batched(const void* A, int lda, long long sA, const void* W, int ldw, long long sW, int M, int N, int K,
+                     int batch, void* out, int ldc, long long sC, int out_bf16, void* stream);
+
 /* Weight-gradient GEMM (bf16 MFMA): C[b] += A[b]^T B[b], A (K, M) and B
  * (K, N) row-major with row strides lda / ldb (the token rows of dY and X:
  * dW = dY^T X of nn.Linear / conv backward, linear.py:15-76), C (M, N) fp32
@@ -381,6 +387,11 @@ int sbk_dwconv_bwd(const void* x, int x_bf16, const float* dy, int B, int T, int
  * (rel_shift :468-483 transposed), zero outside the band. */
 int sbk_relpos_softmax_bwd(const float* P, const void* dP, int dP_bf16, int B, int H, int T, float scale, void* dS,
                            void* dBD, int out_bf16, void* stream);
+/* As sbk_relpos_softmax_bwd with dBD head-major (H, B, T, Wp), Wp = 2T-1
+ * rounded up to 8 with zero pad columns: each head's rows over all
+ * utterances form one 16-B-aligned operand of the dp_k weight gradient. */
+int sbk_relpos_softmax_bwd_hm(const float* P, const void* dP, int dP_bf16, int B, int H, int T, float scale,
+                              void* dS, void* dBD, int out_bf16, void* stream);
 
 /* Conv2d 3x3 stride 2 "same" reflect padding (CNN.py:616-700) as a GEMM:
  * x (B, Ti, Fi, Ci) -> col (B*To*Fo, ldcol >= 9*Ci), columns ordered (kt, kf, ci),

@@ -314,6 +314,9 @@ class DwConvFn(Function):
 
 
 # ------------------------------------------------------ rel-pos attention
+# bf16 backward on sbk_gemm_batched / sbk_gemm_tn (else: library matmuls)
+ATTN_BWD_SBK = True
+
 class RelPosAttentionFn(Function):
     """RelPosMHAXL core (attention.py:566-631, rel_shift :468-483).
     qkv (B*T, 3d) head-interleaved, pk (2T-1, d), both in the compute dtype;
@@ -342,6 +345,8 @@ class RelPosAttentionFn(Function):
         qkv, pk, pbu, pbv, P, attn = ctx.saved_tensors
         B, T, H, dh, scale, p, seed = ctx.dims
         dt = qkv.dtype
+        if ATTN_BWD_SBK and dt == _bf16 and dh % 8 == 0 and T % 8 == 0:
+            return RelPosAttentionFn._backward_sbk(ctx, do)
         W = 2 * T - 1
         q5 = qkv.view(B, T, H, 3, dh)
         q = q5[:, :, :, 0].permute(0, 2, 1, 3)  # (B, H, T, dh) views
@@ -374,6 +379,54 @@ class RelPosAttentionFn(Function):
         dpk = dpk.permute(1, 0, 2).reshape(W, H * dh)
         dpbu = dq_ac.float().sum(dim=(0, 2)).reshape(pbu.shape)
         dpbv = dq_bd.float().sum(dim=(0, 2)).reshape(pbv.shape)
+        return dqkv, dpk, dpbu, dpbv, None, None, None, None, None, None, None
+
+
+    @staticmethod
+    def _backward_sbk(ctx, do):
+        """bf16 backward on the MFMA kernels: per (b, h) batched products
+        (sbk_gemm_batched, sbk_gemm_tn) around the softmax / rel_shift
+        backward (sbk_relpos_softmax_bwd_hm)."""
+        qkv, pk, pbu, pbv, P, attn = ctx.saved_tensors
+        B, T, H, dh, scale, p, seed = ctx.dims
+        dt = qkv.dtype
+        W = 2 * T - 1
+        BH = B * H
+        q5 = qkv.view(B, T, H, 3, dh)
+        # per-(b, h) contiguous operands (B*H, T, dh)
+        q = q5[:, :, :, 0].permute(0, 2, 1, 3).reshape(BH, T, dh)
+        k = q5[:, :, :, 1].permute(0, 2, 1, 3).reshape(BH, T, dh)
+        v = q5[:, :, :, 2].permute(0, 2, 1, 3).reshape(BH, T, dh)
+        do_h = _as(do, dt).view(B, T, H, dh).permute(0, 2, 1, 3).reshape(BH, T, dh)
+        Pc = (_enc.cast_bf16(attn) if attn.dtype != dt else attn).view(BH, T, T)
+        dv = _enc.gemm_tn(Pc, do_h)                            # P^T dO   (BH, T, dh)
+        dP = _enc.gemm_batched(do_h, v, out_dtype=dt)           # dO V^T   (BH, T, T)
+        if p > 0:
+            dP = drop_add(dP, None, 1.0, None, p, seed, dP.dtype)
+        Wp = (W + 7) // 8 * 8
+        dS = torch.empty(BH, T, T, device=qkv.device, dtype=dt)
+        dBD = torch.empty(H, B * T, Wp, device=qkv.device, dtype=dt)  # head-major, zero-padded rows
+        check(lib().sbk_relpos_softmax_bwd_hm(ptr(P), ptr(dP), _bf(dP), B, H, T, float(scale), ptr(dS), ptr(dBD),
+                                              _bf(dS), stream_of(P)), "sbk_relpos_softmax_bwd_hm")
+        u = pbu.detach().reshape(1, H, 1, dh).to(dt)
+        vb = pbv.detach().reshape(1, H, 1, dh).to(dt)
+        kT = k.transpose(1, 2).contiguous()                     # (BH, dh, T)
+        dq_ac = _enc.gemm_batched(dS, kT)                       # dS K     (BH, T, dh) fp32
+        pkT = torch.zeros(H, dh, Wp, device=qkv.device, dtype=dt)
+        pkT[:, :, :W] = pk.view(W, H, dh).permute(1, 2, 0)     # (H, dh, Wp)
+        dq_bd = _enc.gemm_batched(dBD, pkT)                     # dBD P_k  (H, B*T, dh) fp32
+        qu = (q.view(B, H, T, dh) + u).reshape(BH, T, dh)
+        dk = _enc.gemm_tn(dS, qu)                               # dS^T (q + u)
+        qv = (q.view(B, H, T, dh) + vb).permute(1, 0, 2, 3).reshape(H, B * T, dh)
+        dpk = _enc.gemm_tn(dBD, qv)[:, :W]                      # (H, W, dh)
+        dq_bd = dq_bd.view(H, B, T, dh).permute(1, 0, 2, 3)     # (B, H, T, dh)
+        dq_ac = dq_ac.view(B, H, T, dh)
+        dq = dq_ac + dq_bd
+        dqkv = torch.stack([dq, dk.view(B, H, T, dh), dv.view(B, H, T, dh)], dim=3)  # (B, H, T, 3, dh)
+        dqkv = dqkv.permute(0, 2, 1, 3, 4).reshape(B * T, 3 * H * dh).to(dt)
+        dpk = dpk.permute(1, 0, 2).reshape(W, H * dh).to(dt)
+        dpbu = dq_ac.sum(dim=(0, 2)).reshape(pbu.shape)
+        dpbv = dq_bd.sum(dim=(0, 2)).reshape(pbv.shape)
         return dqkv, dpk, dpbu, dpbv, None, None, None, None, None, None, None
 
 

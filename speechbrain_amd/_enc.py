@@ -103,6 +103,32 @@ def gemm_tn(a, b):
     return torch.ops.sbk.gemm_tn(a, b)
 
 
+@torch.library.custom_op("sbk::gemm_batched", mutates_args=())
+def _gemm_batched_op(a: torch.Tensor, w: torch.Tensor, out_bf16: bool) -> torch.Tensor:
+    Bt, M, K = a.shape
+    N = w.shape[1]
+    out = torch.empty(Bt, M, N, device=a.device, dtype=_bf16 if out_bf16 else _f32)
+    check(lib().sbk_gemm_batched(ptr(a), a.stride(1), a.stride(0), ptr(w), w.stride(1), w.stride(0), M, N, K, Bt,
+                                 ptr(out), N, M * N, int(out_bf16), stream_of(a)), "sbk_gemm_batched")
+    return out
+
+
+@_gemm_batched_op.register_fake
+def _(a, w, out_bf16):
+    return a.new_empty(a.shape[0], a.shape[1], w.shape[1], dtype=_bf16 if out_bf16 else _f32)
+
+
+def gemm_batched(a, w, out_dtype=_f32):
+    """a[b] @ w[b]^T for bf16 a (Bt, M, K), w (Bt, N, K) with K-contiguous rows
+    (batch strides arbitrary): (Bt, M, N) fp32 or bf16."""
+    require_device(a, w)
+    if a.dtype != _bf16 or w.dtype != _bf16:
+        raise TypeError("gemm_batched takes bf16 operands")
+    if a.stride(-1) != 1 or w.stride(-1) != 1:
+        raise ValueError("gemm_batched operands must be K-contiguous")
+    return torch.ops.sbk.gemm_batched(a, w, out_dtype == _bf16)
+
+
 @torch.library.custom_op("sbk::length_mask", mutates_args=())
 def _length_mask_op(rel_len: torch.Tensor, T: int) -> torch.Tensor:
     B = rel_len.shape[0]

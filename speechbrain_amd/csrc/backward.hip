@@ -343,23 +343,32 @@ __global__ void __launch_bounds__(256) dwconv_wgrad_kernel(const void* __restric
 __global__ void __launch_bounds__(256) relpos_softmax_bwd_kernel(const float* __restrict__ P,
                                                                  const void* __restrict__ dP, int dP_bf16, int T,
                                                                  float scale, void* __restrict__ dS,
-                                                                 void* __restrict__ dBD, int out_bf16) {
+                                                                 void* __restrict__ dBD, int out_bf16, int B = 0,
+                                                                 int H = 0) {
   __shared__ float red[16];
   const long long row = blockIdx.x;
   const int i = (int)(row % T);
+  // dBD rows (b, h, i), or head-major (h, b, i) when B > 0: then a head's
+  // rows over every utterance are one contiguous (B*T, W) operand
+  long long brow = row;
+  if (B > 0) {
+    const long long bh = row / T;
+    brow = ((bh % H) * B + bh / H) * T + i;
+  }
   const float* pr = P + row * T;
   float s = 0.f;
   for (int j = threadIdx.x; j < T; j += blockDim.x) s += pr[j] * ldv(dP, row * T + j, dP_bf16);
   s = block_sum(s, red);
   const int W = 2 * T - 1;
-  for (int r = threadIdx.x; r < W; r += blockDim.x) {
+  const int ldb = B > 0 ? (W + 7) & ~7 : W;  // head-major: rows padded to 16 B (zeros)
+  for (int r = threadIdx.x; r < ldb; r += blockDim.x) {
     const int j = r - (T - 1 - i);
     float v = 0.f;
-    if (j >= 0 && j < T) {
+    if (r < W && j >= 0 && j < T) {
       v = scale * pr[j] * (ldv(dP, row * T + j, dP_bf16) - s);
       stv(dS, row * T + j, v, out_bf16);
     }
-    stv(dBD, row * W + r, v, out_bf16);
+    stv(dBD, brow * ldb + r, v, out_bf16);
   }
 }
 
@@ -718,6 +727,17 @@ SBK_API int sbk_relpos_softmax_bwd(const float* P, const void* dP, int dP_bf16, 
                                    void* dS, void* dBD, int out_bf16, void* stream) {
   if (B <= 0 || H <= 0 || T <= 0) return SBK_ERR_ARG;
   relpos_softmax_bwd_kernel<<<B * H * T, 256, 0, (hipStream_t)stream>>>(P, dP, dP_bf16, T, scale, dS, dBD, out_bf16);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+// As sbk_relpos_softmax_bwd with dBD written head-major: (H, B, T, Wp),
+// Wp = 2T-1 rounded up to 8 (pad columns zero).
+SBK_API int sbk_relpos_softmax_bwd_hm(const float* P, const void* dP, int dP_bf16, int B, int H, int T, float scale,
+                                      void* dS, void* dBD, int out_bf16, void* stream) {
+  if (B <= 0 || H <= 0 || T <= 0) return SBK_ERR_ARG;
+  relpos_softmax_bwd_kernel<<<B * H * T, 256, 0, (hipStream_t)stream>>>(P, dP, dP_bf16, T, scale, dS, dBD, out_bf16,
+                                                                       B, H);
   SBK_CHECK_LAUNCH();
   return 0;
 }

@@ -44,6 +44,8 @@ struct Epi {
   void* ln_out = nullptr;
   int ldu = 0;
   int ln_bf16 = 0;
+  // batched launches (grid.z): element strides of A, W and out per batch
+  long long sA = 0, sW = 0, sC = 0;
 };
 
 // C tile (fp32, row stride CR, in LDS) -> global through the fused epilogue:
@@ -295,6 +297,11 @@ __global__ void __launch_bounds__(256) gemm_kernel(const T* __restrict__ A, int 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* As = reinterpret_cast<T*>(smem);
   T* Bs = As + NBUF * BM * LDSR;
+  if (gridDim.z > 1) {  // batched: this batch's operands and output
+    A += blockIdx.z * ep.sA;
+    W += blockIdx.z * ep.sW;
+    ep.out = reinterpret_cast<char*>(ep.out) + blockIdx.z * ep.sC * (ep.out_bf16 ? 2 : 4);
+  }
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -414,7 +421,8 @@ __global__ void __launch_bounds__(256) gemm_kernel(const T* __restrict__ A, int 
 }
 
 template <typename T, int BM, int BN, int BK, int NBUF = 2>
-int launch(const void* A, int lda, const void* W, int ldw, int M, int N, int K, const Epi& ep, hipStream_t s) {
+int launch(const void* A, int lda, const void* W, int ldw, int M, int N, int K, const Epi& ep, hipStream_t s,
+           int batch = 1) {
   constexpr int LDSR = BK + (sizeof(T) == 2 ? 2 : 1) * MT<T>::PAD;
   size_t lds = (size_t)NBUF * (BM + BN) * LDSR * sizeof(T);
   const size_t cbytes = (size_t)BM * (BN + 4) * 4;  // epilogue C tile
@@ -429,8 +437,8 @@ int launch(const void* A, int lda, const void* W, int ldw, int M, int N, int K, 
     }
   }
   const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, BK, NBUF>), dim3(grid), dim3(256), lds, s, reinterpret_cast<const T*>(A),
-                     lda, reinterpret_cast<const T*>(W), ldw, M, N, K, ep);
+  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, BK, NBUF>), dim3(grid, 1, batch), dim3(256), lds, s,
+                     reinterpret_cast<const T*>(A), lda, reinterpret_cast<const T*>(W), ldw, M, N, K, ep);
   SBK_CHECK_LAUNCH();
   return 0;
 }
@@ -785,4 +793,20 @@ SBK_API int sbk_gemm(int dtype_bf16, const void* A, int lda, const void* W, int 
     case 3: return launch<float, 128, 64, 32>(A, lda, W, ldw, M, N, K, ep, s);
     default: return launch<float, 64, 64, 32>(A, lda, W, ldw, M, N, K, ep, s);
   }
+}
+
+// Batched C[b] = A[b] · W[b]^T (bf16 operands, K-contiguous rows; fp32 or
+// bf16 out) for b < batch with element strides sA / sW / sC: the per-(b, h)
+// products of the attention backward (dP = dO·V^T, dQ = dS·K, ...), one
+// launch over grid.z.  M, N, K as sbk_gemm (K, lda, ldw % 8 == 0).
+SBK_API int sbk_gemm_batched(const void* A, int lda, long long sA, const void* W, int ldw, long long sW, int M, int N,
+                             int K, int batch, void* out, int ldc, long long sC, int out_bf16, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || batch <= 0 || batch > 65535) return SBK_ERR_ARG;
+  if ((K % 8) || (lda % 8) || (ldw % 8) || (sA % 8) || (sW % 8)) return SBK_ERR_ARG;
+  if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(W)) & 15) return SBK_ERR_ARG;
+  Epi ep{nullptr, ACT_NONE, 0.f, nullptr, 0, 1.f, nullptr, out, ldc, out_bf16};
+  ep.sA = sA;
+  ep.sW = sW;
+  ep.sC = sC;
+  return launch<bf16_t, 64, 64, 64>(A, lda, W, ldw, M, N, K, ep, (hipStream_t)stream, batch);
 }
