@@ -12,8 +12,8 @@ fused Fbank kernel (+top_db clamp) → 2 fused ConvBlocks → src Linear →
 captured once into a HIP graph and replayed.  Rank 0 prints ONE JSON line.
 
 Also reported (rank 0, N=1 path of the contract):
-  roofline      the dominant kernel (the fused FFN; the projection GEMMs are
-                listed beside it): its launches of one step re-issued back to
+  roofline      the dominant kernel (the FFN layer-chain kernel; the other
+                fused encoder kernels are listed beside it): its launches of one step re-issued back to
                 back from a HIP graph on the launch stream and timed with HIP
                 events (average launch duration, as rocprofv3 reports it);
                 achieved = algorithmic FLOPs / time; traffic = HBM bytes per
@@ -181,6 +181,23 @@ class _LaunchProbe:
 
 def _ffn_flops(x, ln0, w1, *a, **k):
     return 4.0 * x.shape[0] * x.shape[1] * w1.shape[0]
+
+
+def _ffn_proj_flops(x, ln0, w1, b1, act, slope, w2, b2, alpha, next_ln, wp, *a, **k):
+    """FFN (2 GEMMs, 4·D·H per row) + the fused next-block projection (2·D·NP)."""
+    return _ffn_flops(x, ln0, w1) + 2.0 * x.shape[0] * x.shape[1] * wp.shape[0]
+
+
+def _ffn_chain_flops(x, a, b, act, slope, next_ln, wp, *r, **k):
+    """Two FFN blocks (a, b) + the fused next-block projection."""
+    M, D = x.shape
+    return 4.0 * M * D * (a[1].shape[0] + b[1].shape[0]) + 2.0 * M * D * wp.shape[0]
+
+
+def _conv_module_flops(x, B, T, ln0, w1p, b1p, wc, bc, causal, ln1, w2, b2, kpm=None, pre=None, **k):
+    """pointwise 2d->(GLU) 4d², depthwise 2kd, pointwise 2d², + out_proj 2d² when fused (pre)."""
+    M, D = x.shape
+    return float(M) * (4 * D * D + 2 * wc.shape[0] * D + 2 * D * D + (2 * D * D if pre is not None else 0))
 
 
 def _gemm_flops(a, w, *r, **k):
@@ -649,7 +666,10 @@ def main():
         # per-kernel timing: the dominant kernels' launches of one step,
         # replayed back to back from a HIP graph and timed with HIP events
         bf = lambda t: t.dtype == torch.bfloat16  # noqa: E731
-        probes = [_LaunchProbe("ffn", _ffn_flops, lambda x, ln0, w1, *a, **k: bf(w1)),
+        probes = [_LaunchProbe("ffn_chain", _ffn_chain_flops, lambda x, a, *r, **k: bf(a[1])),
+                  _LaunchProbe("ffn_proj", _ffn_proj_flops, lambda x, ln0, w1, *a, **k: bf(w1)),
+                  _LaunchProbe("ffn", _ffn_flops, lambda x, ln0, w1, *a, **k: bf(w1)),
+                  _LaunchProbe("conv_module", _conv_module_flops, lambda x, B, T, ln0, w1p, *a, **k: bf(w1p)),
                   _LaunchProbe("gemm", _gemm_flops, lambda a, w, *r, **k: bf(a)),
                   _LaunchProbe("relpos_attention", _attn_flops, lambda qkv, *a, **k: bf(qkv))]
         for p in probes:
@@ -660,7 +680,12 @@ def main():
             for p in probes:
                 p.__exit__()
         kern = {}
-        labels = (("ffn_kernel<256, 1> (fused macaron FFN)", "ffn_kernel<256, 1>"),
+        labels = (("ffn_kernel<256, 1, true, true> (FFN2 + FFN1 + in_proj layer chain)",
+                   "ffn_kernel<256, 1, true, true>"),
+                  ("ffn_kernel<256, 1, true, false> (FFN1 + in_proj, layer 0)", "ffn_kernel<256, 1, true, false>"),
+                  ("ffn_kernel<256, 1, false, false> (final FFN2 + final LayerNorm)",
+                   "ffn_kernel<256, 1, false, false>"),
+                  ("conv_module_kernel<true> (out_proj + residual + conv module)", "conv_module_kernel<true>"),
                   ("gemm_kernel<bf16> (projections, all tiles)", "gemm_kernel<unsigned short, 64, 64, 64, 2>"),
                   ("relpos_flash_dma_kernel (rel-pos attention)", "relpos_flash_dma_kernel"))
         for p, (label, pmc_key) in zip(probes, labels):

@@ -334,7 +334,13 @@ class RelPosAttentionFn(Function):
             seed = new_seed()
             attn = drop_add(P, None, 1.0, None, p, seed, _f32)
             v = qkv.view(B, T, H, 3, dh)[:, :, :, 2].permute(0, 2, 1, 3)
-            o = torch.matmul(_as(attn, qkv.dtype), v).permute(0, 2, 1, 3).reshape(B * T, H * dh)
+            if ATTN_BWD_SBK and qkv.dtype == _bf16 and dh % 8 == 0 and T % 8 == 0:
+                # drop(P) V on the batched MFMA GEMM (V^T as the K-contiguous operand)
+                vT = v.transpose(-1, -2).reshape(B * H, dh, T).contiguous()
+                o = _enc.gemm_batched(_as(attn, qkv.dtype).view(B * H, T, T), vT, out_dtype=qkv.dtype)
+                o = o.view(B, H, T, dh).permute(0, 2, 1, 3).reshape(B * T, H * dh)
+            else:
+                o = torch.matmul(_as(attn, qkv.dtype), v).permute(0, 2, 1, 3).reshape(B * T, H * dh)
         ctx.save_for_backward(qkv, pk, pbu, pbv, P, attn)
         ctx.dims = (B, T, H, dh, scale, p, seed)
         ctx.mark_non_differentiable(attn)
