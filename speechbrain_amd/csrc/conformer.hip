@@ -470,7 +470,17 @@ __device__ unsigned long long g_fe_tl[10][16];
 // (8 waves x 7 rows with the block-1 LN affine held in VGPRs: 133 us.)
 constexpr int FE_NT = 640, FE_TT2 = 8;
 
-template <typename T, int C1>
+// LeakyReLU on a packed pair: max(t, s t) for slopes <= 1 (2 packed-rate ops)
+template <bool LMAX>
+__device__ __forceinline__ float __attribute__((ext_vector_type(2)))
+lrelu2(float __attribute__((ext_vector_type(2))) t, float s) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 ts = t * s;
+  if (LMAX) return f2{fmaxf(t[0], ts[0]), fmaxf(t[1], ts[1])};
+  return f2{t[0] >= 0.f ? t[0] : ts[0], t[1] >= 0.f ? t[1] : ts[1]};
+}
+
+template <typename T, int C1, bool LMAX>
 __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restrict__ x, int Tin, int Fin, int T1, int F1,
                                                         int T2, int F2, const float* __restrict__ w1,
                                                         const float* __restrict__ b1, const float* __restrict__ g1,
@@ -488,8 +498,13 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
   // then spread over the banks instead of hitting one 16-B slot column
   constexpr int C1P = C1 + 8;
   const int K = 9 * C1, KP = K + 8;
+  // region 0: the block-1 LN affine (F1 x C1 gamma, beta; fp32) during block
+  // 1, then the block-2 weights (staged after block 1)
   T* wl = reinterpret_cast<T*>(smem);                                   // C2 x KP block-2 weights
-  float* yv = reinterpret_cast<float*>(wl + C2 * KP);                   // TT2 x F2*C2 (block 2)
+  float* g1s = reinterpret_cast<float*>(smem);                          // F1 x C1
+  float* be1s = g1s + F1 * C1;                                          // F1 x C1
+  const int r0 = (max(C2 * KP * (int)sizeof(T), 2 * F1 * C1 * 4) + 15) & ~15;
+  float* yv = reinterpret_cast<float*>(smem + r0);                      // TT2 x F2*C2 (block 2)
   float* xs = yv;                                                       // NJ x 3 x Fin (block 1, same space)
   const int xsz = max(TT2 * F2 * C2, (NJ * 3 * Fin + 3) & ~3);
   T* b1r = reinterpret_cast<T*>(yv + xsz);                              // NJ x F1 x C1P
@@ -519,8 +534,14 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
     const int t1 = reflect_idx(2 * t20 - 1 + j, T1);
     xin[u] = *reinterpret_cast<const float4*>(xb + (long long)reflect_idx(2 * t1 - 1 + kt, Tin) * Fin + 4 * f4);
   }
+  constexpr int AV = (2 * 40 * 64 / 4 + NT - 1) / NT;  // block-1 affine float4s per thread (F1 <= 40)
+  const int nav = F1 * C1 / 4;
+  float4 afin[AV];
 #pragma unroll
-  for (int u = 0; u < WV; ++u) wvin[u] = reinterpret_cast<const uint4*>(wp2)[min(tid + u * NT, nwv - 1)];
+  for (int u = 0; u < AV; ++u) {
+    const int i = min(tid + u * NT, 2 * nav - 1);
+    afin[u] = i < nav ? reinterpret_cast<const float4*>(g1)[i] : reinterpret_cast<const float4*>(be1)[i - nav];
+  }
   constexpr int W1V = (C1 * 9 + NT - 1) / NT;  // block-1 taps per thread
   float w1v[W1V];
 #pragma unroll
@@ -532,13 +553,8 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
     if (i < NJ * 3 * fq4) *reinterpret_cast<float4*>(xs + 4 * i) = xin[u];
   }
 #pragma unroll
-  for (int u = 0; u < WV; ++u) {
-    const int i = tid + u * NT;
-    if (i < nwv) {
-      const int co = (i * Tr::VEC) / K, kk = i * Tr::VEC - co * K;
-      *reinterpret_cast<uint4*>(wl + co * KP + kk) = wvin[u];
-    }
-  }
+  for (int u = 0; u < AV; ++u)
+    if (tid + u * NT < 2 * nav) reinterpret_cast<float4*>(g1s)[tid + u * NT] = afin[u];
 #pragma unroll
   for (int u = 0; u < W1V; ++u)
     if (tid + u * NT < C1 * 9) w1s[tid + u * NT] = w1v[u];
@@ -546,77 +562,90 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
   __syncthreads();  // xs, w1s, b1s staged
   // block 1 on MFMA, one row per wave (rows w and w + 10): the 3x3 / stride-2
   // convolution of a row is C^T[c][f1] = W^T[c][tap] · X^T[tap][f1] with the 9
-  // taps zero-padded to one 32-deep bf16 step (conv inputs and taps in bf16,
-  // fp32 accumulation — what the reference computes under autocast): 4 x 3
-  // tiles of 16x16 per row.  A lane then holds 4 consecutive channels of one
-  // frequency per tile, so the row's LayerNorm is two wave reductions (no
-  // workgroup barrier) and each tile leaves as one 8-B LDS store.
+  // taps zero-padded to one 16-deep bf16 step (v_mfma_f32_16x16x16_bf16; conv
+  // inputs and taps in bf16, fp32 accumulation — what the reference computes
+  // under autocast): 4 x 3 tiles of 16x16 per row.  A lane then holds 4
+  // consecutive channels of one frequency per tile, so the row's LayerNorm is
+  // two wave reductions (no workgroup barrier) and each tile leaves as one
+  // 8-B LDS store.  VALU budget per row (the phase's bound): the B-fragment
+  // gathers use row-invariant LDS offsets computed once, the LN statistics
+  // and affine run as packed fp32 pairs, bf16 packing is v_cvt_pk_bf16_f32.
   // tap order k = kf * 3 + kt (conv_block_c1's layout of w1)
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+  auto pack2 = [](f32x2 v) __attribute__((always_inline)) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));
+  };
   const int fr = lane & 15, g4 = lane >> 4;
-  bf16x8 wa[4];  // A fragments: W^T rows c = 16 mt + fr, taps 8 g4 .. 8 g4 + 7
+  s16x4 wa[4];  // A fragments: W^T rows c = 16 mt + fr, taps 4 g4 .. 4 g4 + 3 (k >= 9: zero)
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
-    float t8[8];
+    float t4[4];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int k = 8 * g4 + e;
-      t8[e] = k < 9 ? w1s[(16 * mt + fr) * 9 + min(k, 8)] : 0.f;
+    for (int e = 0; e < 4; ++e) {
+      const int k = 4 * g4 + e;
+      t4[e] = k < 9 ? w1s[(16 * mt + fr) * 9 + min(k, 8)] : 0.f;
     }
-    wa[mt] = MT<bf16_t>::from8(t8);
+    wa[mt] = __builtin_bit_cast(s16x4, uint2{pack2(f32x2{t4[0], t4[1]}), pack2(f32x2{t4[2], t4[3]})});
   }
-  float4 bias4[4];
+  f32x4 bias4[4];
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) bias4[mt] = *reinterpret_cast<const float4*>(b1s + 16 * mt + 4 * g4);
-  // this lane's taps of the B fragment: k = 8 g4 + e -> (kt, kf) (k >= 9: zero)
-  int tap_row[8], tap_df[8];
+  for (int mt = 0; mt < 4; ++mt) bias4[mt] = *reinterpret_cast<const f32x4*>(b1s + 16 * mt + 4 * g4);
+  // this lane's B-fragment taps k = 4 g4 + e of output frequency 16 nt + fr,
+  // as row-relative LDS offsets (k >= 9 and frequencies >= F1 read a valid
+  // element: the matching A entries are zero / the column is masked below)
+  int goff[3][4];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int k = min(8 * g4 + e, 8);
-    tap_row[e] = (k % 3) * Fin;
-    tap_df[e] = k / 3 - 1;  // frequency offset: 2 f1 - 1 + kf
+  for (int nt = 0; nt < 3; ++nt) {
+    const int f1c = min(16 * nt + fr, F1 - 1);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = min(4 * g4 + e, 8);
+      goff[nt][e] = (k % 3) * Fin + reflect_idx(2 * f1c + k / 3 - 1, Fin);
+    }
   }
-  const float n1 = (float)(F1 * C1);
+  float colm[3];  // 1 for output frequencies < F1
+#pragma unroll
+  for (int nt = 0; nt < 3; ++nt) colm[nt] = 16 * nt + fr < F1 ? 1.f : 0.f;
+  const float inv_n1 = 1.0f / (float)(F1 * C1);
   FE_TL(1);
   for (int j = w; j < NJ; j += NW) {
     const float* r = xs + (j * 3) * Fin;
     f32x4 acc[4][3];
 #pragma unroll
     for (int nt = 0; nt < 3; ++nt) {
-      const int f1c = min(16 * nt + fr, F1 - 1);
-      float t8[8];
+      const s16x4 xb4 = __builtin_bit_cast(
+          s16x4, uint2{pack2(f32x2{r[goff[nt][0]], r[goff[nt][1]]}), pack2(f32x2{r[goff[nt][2]], r[goff[nt][3]]})});
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float xv = r[tap_row[e] + reflect_idx(2 * f1c + tap_df[e], Fin)];
-        t8[e] = 8 * g4 + e < 9 ? xv : 0.f;
+      for (int mt = 0; mt < 4; ++mt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wa[mt], xb4, bias4[mt], 0, 0, 0);
+    }
+    // LayerNorm over the row's F1 x C1 values (two-pass, packed pairs)
+    f32x2 s2 = {0.f, 0.f};
+#pragma unroll
+    for (int nt = 0; nt < 3; ++nt) {
+      f32x2 sn = {0.f, 0.f};
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) sn += f32x2{acc[mt][nt][0], acc[mt][nt][1]} + f32x2{acc[mt][nt][2], acc[mt][nt][3]};
+      s2 += sn * colm[nt];
+    }
+    const float mean = wave_sum_v(s2.x + s2.y) * inv_n1;
+    const f32x2 mv = {mean, mean};
+    f32x2 q2 = {0.f, 0.f};
+#pragma unroll
+    for (int nt = 0; nt < 3; ++nt) {
+      f32x2 qn = {0.f, 0.f};
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const f32x2 d0 = f32x2{acc[mt][nt][0], acc[mt][nt][1]} - mv, d1 = f32x2{acc[mt][nt][2], acc[mt][nt][3]} - mv;
+        qn += d0 * d0;
+        qn += d1 * d1;
       }
-      const bf16x8 xb8 = MT<bf16_t>::from8(t8);
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[mt], xb8, f32x4{bias4[mt].x, bias4[mt].y, bias4[mt].z, bias4[mt].w}, 0, 0, 0);
+      q2 += qn * colm[nt];
     }
-    float sm = 0.f;
-#pragma unroll
-    for (int nt = 0; nt < 3; ++nt) {
-      const bool on = 16 * nt + fr < F1;
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) sm += on ? acc[mt][nt][q] : 0.f;
-    }
-    const float mean = wave_sum_v(sm) / n1;
-    float sq = 0.f;
-#pragma unroll
-    for (int nt = 0; nt < 3; ++nt) {
-      const bool on = 16 * nt + fr < F1;
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float dv = on ? acc[mt][nt][q] - mean : 0.f;
-          sq += dv * dv;
-        }
-    }
-    const float rstd = 1.0f / sqrtf(wave_sum_v(sq) / n1 + eps1);
+    const float rstd = 1.0f / sqrtf(wave_sum_v(q2.x + q2.y) * inv_n1 + eps1);
+    const f32x2 rv = {rstd, rstd};
 #pragma unroll
     for (int nt = 0; nt < 3; ++nt) {
       const int f1 = 16 * nt + fr;
@@ -624,87 +653,128 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
         const int c = 16 * mt + 4 * g4;
-        const float4 ga = *reinterpret_cast<const float4*>(g1 + f1 * C1 + c);
-        const float4 ba = *reinterpret_cast<const float4*>(be1 + f1 * C1 + c);
-        const float gg[4] = {ga.x, ga.y, ga.z, ga.w}, bb[4] = {ba.x, ba.y, ba.z, ba.w};
-        float y[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float t = (acc[mt][nt][q] - mean) * rstd * gg[q] + bb[q];
-          y[q] = t >= 0.f ? t : t * slope1;
-        }
-        uint2 pk;
-        pk.x = (uint32_t)f32_to_bf16(y[0]) | ((uint32_t)f32_to_bf16(y[1]) << 16);
-        pk.y = (uint32_t)f32_to_bf16(y[2]) | ((uint32_t)f32_to_bf16(y[3]) << 16);
-        *reinterpret_cast<uint2*>(b1r + (j * F1 + f1) * C1P + c) = pk;
+        const f32x4 ga = *reinterpret_cast<const f32x4*>(g1s + f1 * C1 + c);
+        const f32x4 ba = *reinterpret_cast<const f32x4*>(be1s + f1 * C1 + c);
+        f32x2 y0 = (f32x2{acc[mt][nt][0], acc[mt][nt][1]} - mv) * rv * f32x2{ga[0], ga[1]} + f32x2{ba[0], ba[1]};
+        f32x2 y1 = (f32x2{acc[mt][nt][2], acc[mt][nt][3]} - mv) * rv * f32x2{ga[2], ga[3]} + f32x2{ba[2], ba[3]};
+        y0 = lrelu2<LMAX>(y0, slope1);
+        y1 = lrelu2<LMAX>(y1, slope1);
+        *reinterpret_cast<uint2*>(b1r + (j * F1 + f1) * C1P + c) = uint2{pack2(y0), pack2(y1)};
       }
     }
     FE_TL(2 + j / NW);
   }
+  // block-2 weights (L2-resident: every workgroup reads the same 37 KB) into
+  // region 0 once every wave is done with the block-1 affine (loading them
+  // with the stage instead delays the stage's LDS stores more than it saves)
+#pragma unroll
+  for (int u = 0; u < WV; ++u) wvin[u] = reinterpret_cast<const uint4*>(wp2)[min(tid + u * NT, nwv - 1)];
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < WV; ++u) {
+    const int i = tid + u * NT;
+    if (i < nwv) {
+      const int co = (i * Tr::VEC) / K, kk = i * Tr::VEC - co * K;
+      *reinterpret_cast<uint4*>(wl + co * KP + kk) = wvin[u];
+    }
+  }
   __syncthreads();
   FE_TL(11);
 
-  if (w >= TT2) return;  // waves 8, 9: block 1 only (no barrier below)
-  // block 2: wave w -> output row t2 = t20 + w, reading block-1 rows j = 2w + kt
-  const int t2 = t20 + w;
-  if (t2 >= T2) return;  // no barrier below
+  // block 2 as one implicit GEMM over the workgroup's output positions:
+  // rows m = t2_local * F2 + f2 (8 x 20 = 160 = 10 tiles of 16 at config 3, no
+  // padded rows), columns the C2 channels, K = (kt, kf, ci).  Wave w < NMW
+  // owns m-tiles 2w, 2w + 1 against both channel tiles, so each K step issues
+  // 4 MFMAs behind 4 fragment reads, and the LDS operand traffic (the bound of
+  // this phase) is 5 waves' worth instead of one padded row per wave.
+  const int nrow = min(TT2, T2 - t20);  // valid output rows of this workgroup
+  const int Mv = nrow * F2, ntl = C2 / 16;
+  const int nmw = (Mv + 31) / 32;       // waves with MFMA work (<= NW: host-checked F2 <= 32, TT2 = 8)
   const int fk = 8 * (lane >> 4);
-  // all (<= 2 x 2) output tiles of the row accumulate together, so each
-  // K step issues 4 independent MFMAs behind 4 fragment reads
-  const int mt = (F2 + 15) / 16, ntl = C2 / 16;
-  float* yw = yv + w * F2 * C2;
-  int fis[2][3];
-  bool frow[2];
-#pragma unroll
-  for (int tm = 0; tm < 2; ++tm) {
-    const int fo = tm * 16 + fr;
-    frow[tm] = tm < mt && fo < F2;
-#pragma unroll
-    for (int kf = 0; kf < 3; ++kf) fis[tm][kf] = reflect_idx(2 * (frow[tm] ? fo : 0) - 1 + kf, F1) * C1P;
-  }
-  f32x4 acc[2][2];
-#pragma unroll
-  for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-    for (int tn = 0; tn < 2; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-  for (int kt = 0; kt < 3; ++kt) {
-    const T* brow = b1r + (2 * w + kt) * F1 * C1P;
-#pragma unroll
-    for (int kf = 0; kf < 3; ++kf)
-#pragma unroll
-      for (int c0 = 0; c0 < C1; c0 += 32) {
-        const int ci = c0 + fk, k = (kt * 3 + kf) * C1 + ci;
-        typename Tr::frag fa[2], fbw[2];
-#pragma unroll
-        for (int tm = 0; tm < 2; ++tm) fa[tm] = frow[tm] ? Tr::load(brow + fis[tm][kf] + ci) : Tr::zero();
-#pragma unroll
-        for (int tn = 0; tn < 2; ++tn) fbw[tn] = tn < ntl ? Tr::load(wl + (tn * 16 + fr) * KP + k) : Tr::zero();
-#pragma unroll
-        for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-          for (int tn = 0; tn < 2; ++tn) Tr::mma(acc[tm][tn], fa[tm], fbw[tn]);
-      }
-  }
-  FE_TL(12);
-#pragma unroll
-  for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-    for (int tn = 0; tn < 2; ++tn) {
-      if (tm >= mt || tn >= ntl) continue;
-      const int co = tn * 16 + fr;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int f = tm * 16 + 4 * (lane >> 4) + r;
-        if (f < F2) yw[f * C2 + co] = acc[tm][tn][r] + (b2 ? b2[co] : 0.f);
-      }
-    }
-  // the wave's own LDS row: LN over F2*C2 (wave-local), LeakyReLU, store.
-  // Lane l owns elements 8c .. 8c+7 for chunks c = l, l + 64, ... (16-B LDS
-  // reads, 2 x 16-B affine loads, one 16-B bf16 store per chunk)
+  // the epilogue's LN affine and bias, loaded ahead of the MFMA loop (their
+  // latency hides behind it)
   const int nout = F2 * C2;  // multiple of 16 (C2 % 16 == 0)
   const int nch = nout / 8;
   constexpr int NCH = (32 * 32 / 8 + 63) / 64;  // chunks per lane (F2, C2 <= 32)
+  float4 g2v[NCH][2], b2v[NCH][2];
+  if (w < nrow) {
+#pragma unroll
+    for (int u = 0; u < NCH; ++u) {
+      const int c = min(lane + 64 * u, nch - 1);
+      const float4* gp = reinterpret_cast<const float4*>(g2 + 8 * c);
+      const float4* bp = reinterpret_cast<const float4*>(be2 + 8 * c);
+      g2v[u][0] = gp[0];
+      g2v[u][1] = gp[1];
+      b2v[u][0] = bp[0];
+      b2v[u][1] = bp[1];
+    }
+  }
+  if (w < nmw) {
+    int aoff[2][3];  // A-row (m = 32 w + 16 tm + fr) offsets into b1r per kf, kt = 0
+    bool arow[2];
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm) {
+      const int m = 32 * w + 16 * tm + fr;
+      arow[tm] = m < Mv;
+      const int mc = arow[tm] ? m : 0;
+      const int tl = mc / F2, fo = mc - tl * F2;
+#pragma unroll
+      for (int kf = 0; kf < 3; ++kf) aoff[tm][kf] = (2 * tl * F1 + reflect_idx(2 * fo - 1 + kf, F1)) * C1P;
+    }
+    float cb[2];
+#pragma unroll
+    for (int tn = 0; tn < 2; ++tn) cb[tn] = b2 && tn < ntl ? b2[tn * 16 + fr] : 0.f;
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // unconditional fragment reads (rows past Mv / channel tiles past C2 read
+    // valid LDS and are discarded at the store), fully unrolled so the reads
+    // of later K steps issue ahead of the MFMAs
+    const T* wrow[2] = {wl + fr * KP + fk, wl + ((ntl > 1 ? 16 : 0) + fr) * KP + fk};
+#pragma unroll
+    for (int kt = 0; kt < 3; ++kt) {
+      const T* brow = b1r + kt * F1 * C1P + fk;
+#pragma unroll
+      for (int kf = 0; kf < 3; ++kf)
+#pragma unroll
+        for (int c0 = 0; c0 < C1; c0 += 32) {
+          const int k = (kt * 3 + kf) * C1 + c0;
+          typename Tr::frag fa[2], fbw[2];
+#pragma unroll
+          for (int tm = 0; tm < 2; ++tm) fa[tm] = Tr::load(brow + aoff[tm][kf] + c0);
+#pragma unroll
+          for (int tn = 0; tn < 2; ++tn) fbw[tn] = Tr::load(wrow[tn] + k);
+#pragma unroll
+          for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < 2; ++tn) Tr::mma(acc[tm][tn], fa[tm], fbw[tn]);
+        }
+    }
+    // D rows m = 32 w + 16 tm + 4 (lane >> 4) + r -> yv[m][co] (rows of one
+    // output time step are contiguous: yv[t2_local][f2][co])
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn) {
+        if (tn >= ntl) continue;
+        const int co = tn * 16 + fr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = 32 * w + 16 * tm + 4 * (lane >> 4) + r;
+          if (m < Mv) yv[m * C2 + co] = acc[tm][tn][r] + cb[tn];
+        }
+      }
+  }
+  FE_TL(12);
+  __syncthreads();
+  if (w >= nrow) return;  // no barrier below
+  const int t2 = t20 + w;
+  const float* yw = yv + w * F2 * C2;
+  // the wave's own LDS row: LN over F2*C2 (wave-local), LeakyReLU, store.
+  // Lane l owns elements 8c .. 8c+7 for chunks c = l, l + 64, ... (16-B LDS
+  // reads, 2 x 16-B affine loads, one 16-B bf16 store per chunk)
   float yv8[NCH][8];
   float s2 = 0.f;
 #pragma unroll
@@ -735,9 +805,7 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
   for (int u = 0; u < NCH; ++u) {
     const int c = lane + 64 * u;
     if (c >= nch) continue;
-    const float4* gp = reinterpret_cast<const float4*>(g2 + 8 * c);
-    const float4* bp = reinterpret_cast<const float4*>(be2 + 8 * c);
-    const float4 ga = gp[0], gb = gp[1], ba = bp[0], bb = bp[1];
+    const float4 ga = g2v[u][0], gb = g2v[u][1], ba = b2v[u][0], bb = b2v[u][1];
     const float gg[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
     const float bt[8] = {ba.x, ba.y, ba.z, ba.w, bb.x, bb.y, bb.z, bb.w};
     float y[8];
@@ -914,23 +982,28 @@ SBK_API int sbk_conv_frontend2(int dtype_bf16, const float* x, int B, int Tin, i
     return SBK_ERR_ARG;
   constexpr int TT2 = FE_TT2, NJ = 2 * TT2 + 1;
   const size_t esz = dtype_bf16 ? 2 : 4;
-  const size_t lds = (size_t)C2 * (9 * C1 + 8) * esz +
+  const size_t lds = ((std::max((size_t)C2 * (9 * C1 + 8) * esz, (size_t)2 * F1 * C1 * 4) + 15) & ~(size_t)15) +
                      (size_t)std::max(TT2 * F2 * C2, (NJ * 3 * Fin + 3) & ~3) * 4 + (size_t)NJ * F1 * (C1 + 8) * esz +
                      (size_t)C1 * 10 * 4;  // block-1 taps + bias
   if (dtype_bf16 && lds > 160 * 1024 - 1024) return SBK_ERR_ARG;
   const dim3 grid(B * ((T2 + TT2 - 1) / TT2));
   hipStream_t s = (hipStream_t)stream;
   if (!dtype_bf16) return SBK_ERR_ARG;  // fp32 path: the per-block kernels (LDS would not fit)
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&frontend2_kernel<bf16_t, 64>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
-    attr = true;
-  }
-  hipLaunchKernelGGL((frontend2_kernel<bf16_t, 64>), grid, dim3(FE_NT), lds, s, x, Tin, Fin, T1, F1, T2, F2, w1, b1, g1,
-                     be1, eps1, slope1, reinterpret_cast<const bf16_t*>(wp2), C2, b2, g2, be2, eps2, slope2, out,
-                     out_bf16);
+  auto launch = [&](auto kern, bool& attr) -> int {
+    if (!attr) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return (int)e;
+      attr = true;
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(FE_NT), lds, s, x, Tin, Fin, T1, F1, T2, F2, w1, b1, g1, be1, eps1, slope1,
+                       reinterpret_cast<const bf16_t*>(wp2), C2, b2, g2, be2, eps2, slope2, out, out_bf16);
+    return 0;
+  };
+  static bool attr_max = false, attr_sel = false;
+  const int rc = slope1 <= 1.f ? launch(&frontend2_kernel<bf16_t, 64, true>, attr_max)
+                               : launch(&frontend2_kernel<bf16_t, 64, false>, attr_sel);
+  if (rc) return rc;
   SBK_CHECK_LAUNCH();
   return 0;
 }
