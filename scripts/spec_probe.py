@@ -7,6 +7,9 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import speechbrain_amd._lib as _L  # noqa: E402
+if os.environ.get("SBK_PROBE_LIB"):
+    _L.LIB_PATH = os.path.abspath(os.environ["SBK_PROBE_LIB"])  # probe builds of the kernel (not product)
 from speechbrain_amd.lobes.features import Fbank  # noqa: E402
 from speechbrain_amd.processing.features import STFT  # noqa: E402
 from speechbrain_amd import ops  # noqa: E402
