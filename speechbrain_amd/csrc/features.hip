@@ -630,7 +630,12 @@ int fill_plan(FftPlan* p, int nc) {
 // stages saves 9 us and the mel loop 4 us, so neither the FFT nor the
 // filters set the time.  A wave-per-frame variant (three in-register
 // Stockham stages, wave-private LDS exchanges, one block barrier) measured
-// 81 us with global tables and 66 us with LDS tables: not kept.
+// 81 us with global tables and 66 us with LDS tables: not kept.  Workgroups
+// looping over G groups of 8 frames (tables staged once, one slot max per
+// workgroup; the thread index made opaque per group to stop the compiler
+// hoisting every stage's index math out of the loop): 70.6 / 61.7 / 60.9 /
+// 59.7 / 94.5 us for G = 1 / 2 / 4 / 8 / 16 against 55.7 us: per-workgroup
+// setup is not the cost either.
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr int plan_nstages(int nc) {
   int n = 0;
