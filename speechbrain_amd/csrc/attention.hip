@@ -58,16 +58,12 @@ struct FlashLds {
   static constexpr size_t ps = (size_t)PBR * KR * sizeof(T);
   static constexpr size_t gs = (size_t)4 * GR * GS * 4;
   static constexpr size_t ms = (size_t)(KC + 4) * 4;  // key mask + 'chunk has a masked key' flag
-#ifdef SBK_ATT_NOALIAS
-  static constexpr size_t bytes = ks + vt + ps + gs + ms;
-#else
   // The per-wave G^T scratch aliases the K and positional-band tiles, which
   // are dead once every wave's S / G MFMAs have consumed them (one barrier):
   // 66 -> 40 KB per workgroup, three workgroups per CU instead of two, and
   // the 768 workgroups of a B = 32, T = 376 launch fit in one round.
   static_assert(gs <= ks + ps, "G^T scratch fits over Ks + Ps");
   static constexpr size_t bytes = ks + ps + vt + ms;
-#endif
 };
 
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
@@ -77,11 +73,7 @@ typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 // measured 36 -> 54 us: the compiler then sank the prefetch loads to their
 // stores; and head dims >= dh must stay zero when dh is not a multiple of the
 // 8-dim Q fragment, whose vector loads then read the next section.)
-#ifdef SBK_ATT_NO_ZERO_OOR
-#define STAGE_SEL(ok, v) (v)
-#else
 #define STAGE_SEL(ok, v) sel4((ok), (v))
-#endif
 
 // component-wise select (a struct-valued ?: takes the operands' addresses and
 // sends the staging arrays to scratch)
@@ -132,21 +124,12 @@ __global__ void __launch_bounds__(256, SBK_ATT_MINW) relpos_flash_kernel(const T
   constexpr int NPC = PBR * CPR / 256;  // P-band chunks per thread
   static_assert(KC == 64, "mask staging: one wave per chunk");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-#ifdef SBK_ATT_NOALIAS
-  T* Ks = reinterpret_cast<T*>(smem);
-  T* Vs = reinterpret_cast<T*>(smem + L::ks);
-  T* Ps = reinterpret_cast<T*>(smem + L::ks + L::vt);
-  float* Gs = reinterpret_cast<float*>(smem + L::ks + L::vt + L::ps);
-  float* Ms = reinterpret_cast<float*>(smem + L::ks + L::vt + L::ps + L::gs);
-  constexpr bool ALIAS = false;
-#else
   T* Ks = reinterpret_cast<T*>(smem);
   T* Ps = reinterpret_cast<T*>(smem + L::ks);
   T* Vs = reinterpret_cast<T*>(smem + L::ks + L::ps);
   float* Gs = reinterpret_cast<float*>(smem);  // over Ks + Ps (dead after the S / G MFMAs)
   float* Ms = reinterpret_cast<float*>(smem + L::ks + L::ps + L::vt);
   constexpr bool ALIAS = true;
-#endif
 
   const int d_model = H * dh;
   const long long row3 = 3LL * d_model;
@@ -326,12 +309,7 @@ __global__ void __launch_bounds__(256, SBK_ATT_MINW) relpos_flash_kernel(const T
       ATT_TL(1 + 6 * ch);
       const int j0 = ch * KC;
       const bool more = ch + 1 < nchunk;
-#ifndef SBK_PROBE_NO_STAGE
       if (vec_ok && more) fetch(j0 + KC, need_v);  // next chunk in flight during this chunk's math
-#ifdef SBK_ATT_PIN_FETCH
-      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch loads above the chunk math
-#endif
-#endif
 
       // ---- S^T (keys x queries) and G^T (band rows x queries) ----
       // per 32-wide head-dim step: all 9 fragment reads, then the 9 MFMAs;
@@ -348,24 +326,18 @@ __global__ void __launch_bounds__(256, SBK_ATT_MINW) relpos_flash_kernel(const T
         typename Tr::frag fk[4], fpb[5];
 #pragma unroll
         for (int t = 0; t < 4; ++t) fk[t] = Tr::load(Ks + (16 * t + c16) * KR + 8 * g + 32 * s);
-#ifndef SBK_PROBE_NO_G
 #pragma unroll
         for (int t = 0; t < 5; ++t) fpb[t] = Tr::load(Ps + (pofs + 16 * t + c16) * KR + 8 * g + 32 * s);
-#endif
 #pragma unroll
         for (int t = 0; t < 4; ++t) Tr::mma(acc_s[t], fk[t], fqu[s]);
-#ifndef SBK_PROBE_NO_G
 #pragma unroll
         for (int t = 0; t < 5; ++t) Tr::mma(acc_g[t], fpb[t], fqv[s]);
-#endif
       }
       if (ALIAS) __syncthreads();  // every wave's Ks / Ps fragment reads are done: the scratch may overwrite them
-#ifndef SBK_PROBE_NO_G
 #pragma unroll
       for (int t = 0; t < 5; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) Gw[(16 * t + 4 * g + r) * GS + c16] = acc_g[t][r];
-#endif
       // G^T scratch is per wave: its LDS writes only need to have completed
       // (in-order per wave) before the shifted reads, no workgroup barrier
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -454,11 +426,7 @@ __global__ void __launch_bounds__(256, SBK_ATT_MINW) relpos_flash_kernel(const T
               const T* vrow = Vs + (16 * t + c16) * VR + 32 * s2 + 4 * g;
               fa = Tr::load2x4(vrow, vrow + 16);
             }
-#ifndef SBK_PROBE_NO_PV
             Tr::mma(acc_o[t], fa, fp);
-#else
-            acc_o[t][0] += fa[0] + fp[0];
-#endif
           }
         }
       }
@@ -466,13 +434,8 @@ __global__ void __launch_bounds__(256, SBK_ATT_MINW) relpos_flash_kernel(const T
       __syncthreads();  // every wave done with this chunk's Ks / Vs / Ps / Gs
       ATT_TL(5 + 6 * ch);
       if (more) {
-#ifdef SBK_PROBE_NO_STAGE
-        if (vec_ok) {
-        }
-#else
         if (vec_ok)
           commit(need_v);
-#endif
         else
           stage_scalar(j0 + KC, need_v);
         __syncthreads();
@@ -810,12 +773,10 @@ SBK_API int sbk_relpos_attention_ld(int dtype_bf16, const void* qkv, const void*
                                     void* out, float* probs, void* stream) {
   if (B <= 0 || Tn <= 0 || H <= 0 || dh <= 0 || dh > 128 || ldp < H * dh) return SBK_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-#ifndef SBK_ATT_NO_DMA
   // the encoder's inference path: bf16, dh = 64, no probabilities
   if (dtype_bf16 && dh == 64 && !probs && ldp % 8 == 0 &&
       ((reinterpret_cast<uintptr_t>(qkv) | reinterpret_cast<uintptr_t>(pk) | reinterpret_cast<uintptr_t>(out)) % 16) == 0)
     return launch_dma(qkv, pk, ldp, pbu, pbv, kpm, B, Tn, H, scale, out, s);
-#endif
   if (dtype_bf16)
     return dh <= 64 ? launch<bf16_t, 64>(qkv, pk, ldp, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s)
                     : launch<bf16_t, 128>(qkv, pk, ldp, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s);

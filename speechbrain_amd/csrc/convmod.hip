@@ -291,12 +291,8 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       for (int mt = 0; mt < CM_MT1; ++mt) acc[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
     const bf16_t* wrow = wrow1;
     auto& fw = fw1;
-#ifndef SBK_PROBE_NO_P1
 #pragma unroll
     for (int kk = 0; kk < CM_D / 64; ++kk) {
-#else
-    for (int kk = 0; kk < 0; ++kk) {
-#endif
       const int cur = kk & 1;
       if (kk + 1 < CM_D / 64) {
 #pragma unroll
@@ -368,7 +364,6 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
     }
 
   // ---- phase 2: depthwise conv (register window) -> fp32 tile; LN1 -> Swish -> V (over U) ----
-#ifndef SBK_PROBE_NO_P2
   {
     // 2a: thread (channel c, quarter h) slides the taps down its channel for 12 frames
     const int c = tid & (CM_D - 1), h = tid >> 8;  // channel, quarter of the frames
@@ -421,7 +416,6 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       *reinterpret_cast<uint2*>(Us + fi * CM_S + lane * 4) = pk;
     }
   }
-#endif
   lds_barrier();
   CM_TL(4);
 

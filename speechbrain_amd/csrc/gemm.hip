@@ -190,9 +190,6 @@ __device__ __forceinline__ void store_ctile_rowln(const float* __restrict__ Cs, 
 template <int BM, int BN, int NT>
 __device__ __forceinline__ void store_ctile(const float* __restrict__ Cs, const Epi& ep, int m0, int n0, int M,
                                             int N, int tid) {
-#ifdef SBK_PROBE_NO_EPI
-  if (Cs[tid] != 12345.f) return;
-#endif
 
   if (m0 + BM <= M && n0 + BN <= N && epi_aligned(ep)) {
     switch (ep.act) {
@@ -364,11 +361,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(const T* __restrict__ A, int 
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-#ifdef SBK_PROBE_NO_MAIN
-  const int nk = 1;
-#else
   const int nk = (K + BK - 1) / BK;
-#endif
   gload(0);
   sstore(0);
   __syncthreads();
