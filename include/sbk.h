@@ -360,6 +360,9 @@ int sbk_colsum(const float* part, int rows, int cols, float* out, int accumulate
 
 /* out[c] (+)= sum_r x[r, c]; part: sbk_rowsum_chunks(rows) * cols floats. (Linear bias gradients.) */
 int sbk_rowsum_chunks(long long rows);
+/* out[z, c] (+)= sum_r x[z, r, c] for z < batch; part: sbk_rowsum_chunks(rows) * batch * cols floats. */
+int sbk_rowsum_batched(const void* x, int x_bf16, int batch, long long rows, int cols, float* part, float* out,
+                       int accumulate, void* stream);
 int sbk_rowsum(const void* x, int x_bf16, long long rows, int cols, float* part, float* out, int accumulate,
                void* stream);
 

@@ -58,6 +58,18 @@ def rowsum(x, out=None, accumulate=False):
     return out
 
 
+def rowsum_batched(x):
+    """(batch, rows, cols) fp32/bf16 -> (batch, cols) fp32 sums over rows."""
+    x = _cont(x)
+    bt, rows, cols = x.shape
+    L = lib()
+    part = torch.empty(int(L.sbk_rowsum_chunks(rows)) * bt * cols, device=x.device, dtype=_f32)
+    out = torch.empty(bt, cols, device=x.device, dtype=_f32)
+    check(L.sbk_rowsum_batched(ptr(x), _bf(x), bt, rows, cols, ptr(part), ptr(out), 0, stream_of(x)),
+          "sbk_rowsum_batched")
+    return out
+
+
 def colsum(part, rows, cols):
     out = torch.empty(cols, device=part.device, dtype=_f32)
     check(lib().sbk_colsum(ptr(part), rows, cols, ptr(out), 0, stream_of(part)), "sbk_colsum")
@@ -421,6 +433,7 @@ class RelPosAttentionFn(Function):
         pkT = torch.zeros(H, dh, Wp, device=qkv.device, dtype=dt)
         pkT[:, :, :W] = pk.view(W, H, dh).permute(1, 2, 0)     # (H, dh, Wp)
         dq_bd = _enc.gemm_batched(dBD, pkT)                     # dBD P_k  (H, B*T, dh) fp32
+        dpbv = rowsum_batched(dq_bd).reshape(pbv.shape)         # per head: sum over (b, t)
         qu = (q.view(B, H, T, dh) + u).reshape(BH, T, dh)
         dk = _enc.gemm_tn(dS, qu)                               # dS^T (q + u)
         qv = (q.view(B, H, T, dh) + vb).permute(1, 0, 2, 3).reshape(H, B * T, dh)
@@ -431,8 +444,8 @@ class RelPosAttentionFn(Function):
         dqkv = torch.stack([dq, dk.view(B, H, T, dh), dv.view(B, H, T, dh)], dim=3)  # (B, H, T, 3, dh)
         dqkv = dqkv.permute(0, 2, 1, 3, 4).reshape(B * T, 3 * H * dh).to(dt)
         dpk = dpk.permute(1, 0, 2).reshape(W, H * dh).to(dt)
-        dpbu = dq_ac.sum(dim=(0, 2)).reshape(pbu.shape)
-        dpbv = dq_bd.sum(dim=(0, 2)).reshape(pbv.shape)
+        # sum over (b, t): over b as rows (sbk_rowsum), then over t (H*T*dh values)
+        dpbu = rowsum_batched(rowsum(dq_ac.reshape(B, H * T * dh)).view(H, T, dh)).reshape(pbu.shape)
         return dqkv, dpk, dpbu, dpbv, None, None, None, None, None, None, None
 
 

@@ -110,6 +110,7 @@ SIGNATURES = {
     "sbk_colsum": [_vp, _i, _i, _vp, _i, _vp],
     "sbk_rowsum_chunks": [_ll],
     "sbk_rowsum": [_vp, _i, _ll, _i, _vp, _vp, _i, _vp],
+    "sbk_rowsum_batched": [_vp, _i, _i, _ll, _i, _vp, _vp, _i, _vp],
     "sbk_act_fwd": [_i, _vp, _i, _ll, _i, _vp, _i, _f, _vp],
     "sbk_act_bwd": [_i, _vp, _i, _vp, _i, _ll, _i, _vp, _i, _f, _vp],
     "sbk_dwconv_fwd": [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _i, _vp],

@@ -25,6 +25,7 @@
 #include "mfma.h"
 
 #include <algorithm>
+#include <initializer_list>
 
 using namespace sbk;
 
@@ -162,10 +163,17 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x
 
 // part[j, c] = sum of x[r, c] over rows r of chunk j (thread per column;
 // 8 loads in flight per thread).
+// Batched over grid.z: x (batch, rows, cols) -> part[j][z * cols + c], so
+// one colsum over the chunks yields out[z * cols + c].
 __global__ void rowsum_partial_kernel(const void* __restrict__ x, int x_bf16, long long rows, int cols, int rows_per,
                                       float* __restrict__ part) {
   const int c = blockIdx.y * blockDim.x + threadIdx.x;
   if (c >= cols) return;
+  const int z = blockIdx.z;
+  x = x_bf16 ? static_cast<const void*>(reinterpret_cast<const bf16_t*>(x) + (long long)z * rows * cols)
+             : static_cast<const void*>(reinterpret_cast<const float*>(x) + (long long)z * rows * cols);
+  part += (long long)z * cols;
+  const int ldp = cols * gridDim.z;
   const long long r0 = (long long)blockIdx.x * rows_per;
   const long long r1 = min(r0 + rows_per, rows);
   float s[4] = {0.f, 0.f, 0.f, 0.f};
@@ -178,7 +186,7 @@ __global__ void rowsum_partial_kernel(const void* __restrict__ x, int x_bf16, lo
     for (int i = 0; i < 8; ++i) s[i & 3] += v[i];
   }
   for (; r < r1; ++r) s[0] += ldv(x, r * cols + c, x_bf16);
-  part[(long long)blockIdx.x * cols + c] = (s[0] + s[1]) + (s[2] + s[3]);
+  part[(long long)blockIdx.x * ldp + c] = (s[0] + s[1]) + (s[2] + s[3]);
 }
 
 // out[c] (+)= sum_r part[r, c] — deterministic column reduction.  A block
@@ -189,16 +197,20 @@ __global__ void __launch_bounds__(1024) colsum_kernel(const float* __restrict__ 
   __shared__ float red[16][65];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
-  float s[2] = {0.f, 0.f};
+  // 8 independent loads in flight per trip (the partial rows are L2-resident)
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (c < cols) {
     int r = w;
-    for (; r + 16 < rows; r += 32) {
-      s[0] += part[(long long)r * cols + c];
-      s[1] += part[(long long)(r + 16) * cols + c];
+    for (; r + 7 * 16 < rows; r += 8 * 16) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = part[(long long)(r + 16 * k) * cols + c];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s[k] += v[k];
     }
-    if (r < rows) s[0] += part[(long long)r * cols + c];
+    for (; r < rows; r += 16) s[0] += part[(long long)r * cols + c];
   }
-  red[w][lane] = s[0] + s[1];
+  red[w][lane] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
   __syncthreads();
   if (w == 0 && c < cols) {
     float t = 0.f;
@@ -251,6 +263,90 @@ __global__ void act_bwd_kernel(int mode, const void* __restrict__ x, int x_bf16,
       stv(dx, i, v > 0.f ? g : g * slope, dx_bf16);
     }
   }
+}
+
+// 4-wide variants (16-B fp32 / 8-B bf16 accesses) for n % 4 == 0 (GLU:
+// cols % 4 == 0) and aligned pointers — the per-element kernels above issue
+// one 2- or 4-byte access per lane and ran at a third of HBM bandwidth.
+__device__ __forceinline__ float4 ld4(const void* p, long long i, int bf) {
+  if (bf) {
+    const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(p) + i);
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                       __uint_as_float(u.y & 0xffff0000u));
+  }
+  return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + i);
+}
+__device__ __forceinline__ void st4(void* p, long long i, float4 v, int bf) {
+  if (bf) {
+    uint2 u;
+    u.x = (uint32_t)f32_to_bf16(v.x) | ((uint32_t)f32_to_bf16(v.y) << 16);
+    u.y = (uint32_t)f32_to_bf16(v.z) | ((uint32_t)f32_to_bf16(v.w) << 16);
+    *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p) + i) = u;
+  } else {
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(p) + i) = v;
+  }
+}
+__device__ __forceinline__ float sigm(float v) { return 1.0f / (1.0f + expf(-v)); }
+
+template <int MODE>
+__global__ void act_fwd4_kernel(const void* __restrict__ x, int x_bf16, long long rows, int cols,
+                                void* __restrict__ y, int y_bf16, float slope) {
+  const long long n4 = rows * cols / 4;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (long long)gridDim.x * blockDim.x) {
+    const long long i = 4 * q;
+    float4 r;
+    if (MODE == 2) {
+      const long long row = i / cols, c = i - row * cols;
+      const float4 a = ld4(x, row * 2 * cols + c, x_bf16), b = ld4(x, row * 2 * cols + cols + c, x_bf16);
+      r = make_float4(a.x * sigm(b.x), a.y * sigm(b.y), a.z * sigm(b.z), a.w * sigm(b.w));
+    } else {
+      const float4 v = ld4(x, i, x_bf16);
+      if (MODE == 1) r = make_float4(v.x * sigm(v.x), v.y * sigm(v.y), v.z * sigm(v.z), v.w * sigm(v.w));
+      else r = make_float4(v.x >= 0.f ? v.x : v.x * slope, v.y >= 0.f ? v.y : v.y * slope,
+                           v.z >= 0.f ? v.z : v.z * slope, v.w >= 0.f ? v.w : v.w * slope);
+    }
+    st4(y, i, r, y_bf16);
+  }
+}
+
+template <int MODE>
+__global__ void act_bwd4_kernel(const void* __restrict__ x, int x_bf16, const void* __restrict__ dy, int dy_bf16,
+                                long long rows, int cols, void* __restrict__ dx, int dx_bf16, float slope) {
+  const long long n4 = rows * cols / 4;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (long long)gridDim.x * blockDim.x) {
+    const long long i = 4 * q;
+    const float4 g = ld4(dy, i, dy_bf16);
+    if (MODE == 2) {
+      const long long row = i / cols, c = i - row * cols;
+      const long long ia = row * 2 * cols + c, ib = ia + cols;
+      const float4 a = ld4(x, ia, x_bf16), b = ld4(x, ib, x_bf16);
+      const float4 sg = make_float4(sigm(b.x), sigm(b.y), sigm(b.z), sigm(b.w));
+      st4(dx, ia, make_float4(g.x * sg.x, g.y * sg.y, g.z * sg.z, g.w * sg.w), dx_bf16);
+      st4(dx, ib,
+          make_float4(g.x * a.x * sg.x * (1.0f - sg.x), g.y * a.y * sg.y * (1.0f - sg.y),
+                      g.z * a.z * sg.z * (1.0f - sg.z), g.w * a.w * sg.w * (1.0f - sg.w)),
+          dx_bf16);
+    } else {
+      const float4 v = ld4(x, i, x_bf16);
+      float4 r;
+      if (MODE == 1) {
+        const float4 sg = make_float4(sigm(v.x), sigm(v.y), sigm(v.z), sigm(v.w));
+        r = make_float4(g.x * (sg.x + v.x * sg.x * (1.0f - sg.x)), g.y * (sg.y + v.y * sg.y * (1.0f - sg.y)),
+                        g.z * (sg.z + v.z * sg.z * (1.0f - sg.z)), g.w * (sg.w + v.w * sg.w * (1.0f - sg.w)));
+      } else {
+        r = make_float4(v.x > 0.f ? g.x : g.x * slope, v.y > 0.f ? g.y : g.y * slope,
+                        v.z > 0.f ? g.z : g.z * slope, v.w > 0.f ? g.w : g.w * slope);
+      }
+      st4(dx, i, r, dx_bf16);
+    }
+  }
+}
+
+inline bool vec4_ok(long long rows, int cols, int mode, std::initializer_list<const void*> ps) {
+  if (cols % 4 || (rows * cols) % 4) return false;
+  for (const void* p : ps)
+    if (reinterpret_cast<uintptr_t>(p) & 15) return false;
+  return mode >= 1 && mode <= 3;
 }
 
 // ------------------------------------------------------- depthwise conv1d
@@ -598,6 +694,33 @@ __global__ void dropout_add_kernel(const void* __restrict__ x, int x_bf16, const
   }
 }
 
+// 4 consecutive elements per thread (same keep hash per element index as
+// dropout_add_kernel, so the masks are identical); cols % 4 == 0, aligned.
+__global__ void dropout_add4_kernel(const void* __restrict__ x, int x_bf16, const float* __restrict__ res,
+                                    long long rows, int cols, const unsigned char* __restrict__ rowmask, float alpha,
+                                    unsigned thresh, float inv_keep, unsigned long long seed, int use_drop,
+                                    void* __restrict__ out, int out_bf16) {
+  const long long n4 = rows * cols / 4;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (long long)gridDim.x * blockDim.x) {
+    const long long i = 4 * q;
+    float4 v = ld4(x, i, x_bf16);
+    float e[4] = {v.x * alpha, v.y * alpha, v.z * alpha, v.w * alpha};
+    if (use_drop) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) e[k] = keep_elem(seed, i + k, thresh) ? e[k] * inv_keep : 0.f;
+    }
+    if (rowmask && rowmask[i / cols]) e[0] = e[1] = e[2] = e[3] = 0.f;
+    if (res) {
+      const float4 r = *reinterpret_cast<const float4*>(res + i);
+      e[0] += r.x;
+      e[1] += r.y;
+      e[2] += r.z;
+      e[3] += r.w;
+    }
+    st4(out, i, make_float4(e[0], e[1], e[2], e[3]), out_bf16);
+  }
+}
+
 }  // namespace
 
 SBK_API int sbk_dropout_add(const void* x, int x_bf16, const float* res, long long rows, int cols,
@@ -607,13 +730,21 @@ SBK_API int sbk_dropout_add(const void* x, int x_bf16, const float* res, long lo
   if (rows == 0) return 0;
   const double keep = 1.0 - (double)p;
   const unsigned thresh = (unsigned)std::min(keep * 16777216.0, 16777216.0);
+  if (vec4_ok(rows, cols, 1, {x, res, out})) {
+    dropout_add4_kernel<<<grid_for(rows * cols / 4, 256), 256, 0, (hipStream_t)stream>>>(
+        x, x_bf16, res, rows, cols, rowmask, alpha, thresh, (float)(1.0 / keep), seed, p > 0.f, out, out_bf16);
+    SBK_CHECK_LAUNCH();
+    return 0;
+  }
   dropout_add_kernel<<<grid_for(rows * cols, 256), 256, 0, (hipStream_t)stream>>>(
       x, x_bf16, res, rows, cols, rowmask, alpha, thresh, (float)(1.0 / keep), seed, p > 0.f, out, out_bf16);
   SBK_CHECK_LAUNCH();
   return 0;
 }
 
-SBK_API int sbk_layernorm_bwd_blocks(int M) { return grid_for((M + 3) / 4, 1, 256); }
+// up to 1024 workgroups (4 rows per workgroup per trip): at 256 the ~12 rows
+// each wave walked in series left the kernel latency-bound (33 us at 12k x 256)
+SBK_API int sbk_layernorm_bwd_blocks(int M) { return grid_for((M + 3) / 4, 1, 1024); }
 
 SBK_API int sbk_layernorm_bwd(const float* x, const void* dy, int dy_bf16, int M, int D, const float* g, float eps,
                               const float* dres, float* dx, float* part, void* stream) {
@@ -645,22 +776,29 @@ SBK_API int sbk_layernorm_wide(const float* x, int M, int D, const float* g, con
   return 0;
 }
 
-SBK_API int sbk_rowsum_chunks(long long rows) { return (int)std::min<long long>(128, std::max<long long>(1, rows / 64)); }
+// up to 1024 row chunks of >= 8 rows: 128 chunks of ~94 rows (one workgroup
+// per 256 columns each) left most CUs idle (26 us for 12k x 256)
+SBK_API int sbk_rowsum_chunks(long long rows) { return (int)std::min<long long>(1024, std::max<long long>(1, rows / 8)); }
 
 // out (cols) fp32 = sum over rows of x (rows, cols) (+ out when accumulate);
 // part: sbk_rowsum_chunks(rows) * cols floats of scratch.
-SBK_API int sbk_rowsum(const void* x, int x_bf16, long long rows, int cols, float* part, float* out, int accumulate,
-                       void* stream) {
-  if (rows <= 0 || cols <= 0) return SBK_ERR_ARG;
+SBK_API int sbk_rowsum_batched(const void* x, int x_bf16, int batch, long long rows, int cols, float* part,
+                               float* out, int accumulate, void* stream) {
+  if (rows <= 0 || cols <= 0 || batch <= 0 || batch > 65535) return SBK_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int nchunk = sbk_rowsum_chunks(rows);
   const int rows_per = (int)((rows + nchunk - 1) / nchunk);
-  dim3 grid(nchunk, (cols + 255) / 256);
+  dim3 grid(nchunk, (cols + 255) / 256, batch);
   rowsum_partial_kernel<<<grid, 256, 0, s>>>(x, x_bf16, rows, cols, rows_per, part);
   SBK_CHECK_LAUNCH();
-  colsum_kernel<<<(cols + 63) / 64, 1024, 0, s>>>(part, nchunk, cols, out, accumulate);
+  colsum_kernel<<<(batch * cols + 63) / 64, 1024, 0, s>>>(part, nchunk, batch * cols, out, accumulate);
   SBK_CHECK_LAUNCH();
   return 0;
+}
+
+SBK_API int sbk_rowsum(const void* x, int x_bf16, long long rows, int cols, float* part, float* out, int accumulate,
+                       void* stream) {
+  return sbk_rowsum_batched(x, x_bf16, 1, rows, cols, part, out, accumulate, stream);
 }
 
 SBK_API int sbk_colsum(const float* part, int rows, int cols, float* out, int accumulate, void* stream) {
@@ -674,6 +812,15 @@ SBK_API int sbk_act_fwd(int mode, const void* x, int x_bf16, long long rows, int
                         float slope, void* stream) {
   if (mode < 1 || mode > 3 || rows < 0 || cols <= 0) return SBK_ERR_ARG;
   if (rows == 0) return 0;
+  if (vec4_ok(rows, cols, mode, {x, y})) {
+    const int g4 = grid_for(rows * cols / 4, 256);
+    hipStream_t st = (hipStream_t)stream;
+    if (mode == 1) act_fwd4_kernel<1><<<g4, 256, 0, st>>>(x, x_bf16, rows, cols, y, y_bf16, slope);
+    else if (mode == 2) act_fwd4_kernel<2><<<g4, 256, 0, st>>>(x, x_bf16, rows, cols, y, y_bf16, slope);
+    else act_fwd4_kernel<3><<<g4, 256, 0, st>>>(x, x_bf16, rows, cols, y, y_bf16, slope);
+    SBK_CHECK_LAUNCH();
+    return 0;
+  }
   act_fwd_kernel<<<grid_for(rows * cols, 256), 256, 0, (hipStream_t)stream>>>(mode, x, x_bf16, rows, cols, y, y_bf16,
                                                                               slope);
   SBK_CHECK_LAUNCH();
@@ -684,6 +831,15 @@ SBK_API int sbk_act_bwd(int mode, const void* x, int x_bf16, const void* dy, int
                         void* dx, int dx_bf16, float slope, void* stream) {
   if (mode < 1 || mode > 3 || rows < 0 || cols <= 0) return SBK_ERR_ARG;
   if (rows == 0) return 0;
+  if (vec4_ok(rows, cols, mode, {x, dy, dx})) {
+    const int g4 = grid_for(rows * cols / 4, 256);
+    hipStream_t st = (hipStream_t)stream;
+    if (mode == 1) act_bwd4_kernel<1><<<g4, 256, 0, st>>>(x, x_bf16, dy, dy_bf16, rows, cols, dx, dx_bf16, slope);
+    else if (mode == 2) act_bwd4_kernel<2><<<g4, 256, 0, st>>>(x, x_bf16, dy, dy_bf16, rows, cols, dx, dx_bf16, slope);
+    else act_bwd4_kernel<3><<<g4, 256, 0, st>>>(x, x_bf16, dy, dy_bf16, rows, cols, dx, dx_bf16, slope);
+    SBK_CHECK_LAUNCH();
+    return 0;
+  }
   act_bwd_kernel<<<grid_for(rows * cols, 256), 256, 0, (hipStream_t)stream>>>(mode, x, x_bf16, dy, dy_bf16, rows,
                                                                               cols, dx, dx_bf16, slope);
   SBK_CHECK_LAUNCH();

@@ -58,6 +58,35 @@ def test_dropout_add(dev):
     assert_close(y4.float(), ref, rtol=1e-2, name="rowmask bf16")
 
 
+def test_dropout_add_vec4_matches_scalar(dev):
+    """The 4-wide kernel (aligned, cols % 4 == 0) keeps the same per-element
+    mask and values as the per-element kernel (forced by a misaligned view)."""
+    from speechbrain_amd import _autograd as A
+    base = torch.randn(2000 * 512 + 1, device=dev)
+    res = torch.randn(2000, 512, device=dev)
+    mask = (torch.arange(2000, device=dev) % 5 == 0).to(torch.uint8)
+    xa = base[:-1].view(2000, 512).clone()          # aligned -> dropout_add4
+    xs = base[1:].view(2000, 512)                   # 4-byte offset -> per-element kernel
+    xs.copy_(xa)
+    for dt in (torch.float32, torch.bfloat16):
+        ya = A.drop_add(xa, res, 0.7, mask, 0.15, 4321, dt)
+        ys = A.drop_add(xs, res, 0.7, mask, 0.15, 4321, dt)
+        assert torch.equal(ya, ys), dt
+
+
+def test_rowsum_batched(dev):
+    from speechbrain_amd import _autograd as A
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(4, 3001, 72, generator=g)
+    # fp32 sums in a different order: bound by 1e-6 of sum |x| (float64 reference)
+    tol = 1e-6 * x.abs().sum(1).max().item()
+    out = A.rowsum_batched(x.to(dev))
+    assert (out.cpu().double() - x.double().sum(1)).abs().max().item() <= tol
+    xb = x.to(torch.bfloat16)
+    assert (A.rowsum_batched(xb.to(dev)).cpu().double() - xb.double().sum(1)).abs().max().item() <= tol
+    assert (A.rowsum(x[0].to(dev)).cpu().double() - x[0].double().sum(0)).abs().max().item() <= tol
+
+
 def test_dropout_autograd(dev):
     from speechbrain_amd import _autograd as A
     torch.manual_seed(0)
@@ -98,11 +127,12 @@ def test_layernorm_bwd(dev, D, dy_bf16):
     assert_grad(lnd.bias.grad, ln.bias.grad, name="dbeta")
 
 
+@pytest.mark.parametrize("cols", [96, 98])  # 4-wide kernels / per-element kernels (GLU halves 49)
 @pytest.mark.parametrize("name", ["swish", "glu", "leaky_relu"])
-def test_act_bwd(dev, name):
+def test_act_bwd(dev, name, cols):
     from speechbrain_amd import _autograd as A
     g = torch.Generator().manual_seed(3)
-    x = torch.randn(777, 96, generator=g) * 3
+    x = torch.randn(777, cols, generator=g) * 3
     xr = x.clone().requires_grad_(True)
     ref = {"swish": lambda t: t * torch.sigmoid(t), "glu": lambda t: F.glu(t, dim=-1),
            "leaky_relu": lambda t: F.leaky_relu(t, 0.01)}[name](xr)
