@@ -203,6 +203,9 @@ int sbk_gemm_batched(const void* A, int lda, long long sA, const void* W, int ld
  * sC batch strides (elements).  M, N, lda, ldb % 8 == 0; A, B 16-B aligned. */
 int sbk_gemm_tn(const void* A, long long lda, long long sA, const void* B, long long ldb, long long sB, int M, int N,
                 int K, int batch, float* C, long long ldc, long long sC, void* stream);
+/* sbk_gemm_tn with an explicit tile (64 / 128; 0 = auto) and token-range split count (0 = auto). */
+int sbk_gemm_tn_cfg(const void* A, long long lda, long long sA, const void* B, long long ldb, long long sB, int M,
+                    int N, int K, int batch, float* C, long long ldc, long long sC, int tile, int nsplit, void* stream);
 
 /* Fused macaron feed-forward block, bf16 MFMA (Conformer.py:239-260 with
  * attention.py:823-839):

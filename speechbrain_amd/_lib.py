@@ -52,6 +52,7 @@ SIGNATURES = {
     "sbk_rnnt_lattice": [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp],
     # gemm_tn.hip (weight-gradient GEMM)
     "sbk_gemm_tn": [_vp, _ll, _ll, _vp, _ll, _ll, _i, _i, _i, _i, _vp, _ll, _ll, _vp],
+    "sbk_gemm_tn_cfg": [_vp, _ll, _ll, _vp, _ll, _ll, _i, _i, _i, _i, _vp, _ll, _ll, _i, _i, _vp],
     "sbk_gemm_batched": [_vp, _i, _ll, _vp, _i, _ll, _i, _i, _i, _i, _vp, _i, _ll, _i, _vp],
     "sbk_relpos_softmax_bwd_hm": [_vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _i, _vp],
     # ffn.hip
