@@ -132,7 +132,10 @@ def _act_of(nonlinearity):
     code = _ACT.get(type(nonlinearity))
     if code is None:
         raise NotImplementedError(f"joint nonlinearity {type(nonlinearity).__name__} has no HIP kernel")
-    return code, float(getattr(nonlinearity, "negative_slope", 0.0)) if code == 3 else 0.0
+    slope = float(getattr(nonlinearity, "negative_slope", 0.0)) if code == 3 else 0.0
+    if slope > 1.0:
+        raise NotImplementedError("the fused head's kernels take LeakyReLU slopes <= 1")
+    return code, slope
 
 
 def transducer_head_loss(tn, pn, weight, targets, input_lens, target_lens, blank_index, reduction="mean",
