@@ -61,7 +61,9 @@ __global__ void __launch_bounds__(256) gemm_tn_kernel(TnArgs a) {
   // register sets: the loads of step kt + DEPTH are issued right after step
   // kt's set is stored to LDS.  Measured: DEPTH 4 (64-tile) / 2 (128-tile)
   // is no faster than 1 (the step is bound by its store -> barrier -> read
-  // -> MFMA -> barrier chain, not by the global loads) and costs VGPRs.
+  // -> MFMA -> barrier chain, not by the global loads) and costs VGPRs.  A
+  // double-buffered LDS variant (one barrier per step) was no faster either
+  // (t64: 117 vs 112 us at one split; profiles/r02_gemm_sweep*.log).
   constexpr int DEPTH = 1;
   uint4 ra[DEPTH][CA], rb[DEPTH][CB];
   auto gload = [&](uint4 (&xa)[CA], uint4 (&xb)[CB], int kb) __attribute__((always_inline)) {
