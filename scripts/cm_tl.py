@@ -15,13 +15,18 @@ dev = torch.device("cuda")
 B, T = 32, 376
 cm = ConvolutionModule(256, 31).to(dev).eval()
 x = torch.randn(B * T, 256, device=dev)
+pre = None
+if os.environ.get("CM_PRE"):  # the encoder's variant: MHSA out_proj + residual fused in (phase -1)
+    pre = ((torch.randn(B * T, 256, device=dev) * 0.5).to(torch.bfloat16),
+           (torch.randn(256, 256, device=dev) / 16).to(torch.bfloat16), torch.zeros(256, device=dev))
 with torch.no_grad():
     for _ in range(5):
-        cm.run_fused(x, B, T, None)
+        cm.run_fused(x, B, T, None, pre=pre)
 torch.cuda.synchronize()
 buf = (ctypes.c_ulonglong * 32)()
 assert ctypes.CDLL(_L.LIB_PATH).sbk_probe_cm_tl(buf) == 0
 tl = np.array(buf, dtype=np.int64).reshape(4, 8)
-print("P0 | P1 | P2a | P2b | P3 | total")
+print("P0 | P1 | P2a | P2b | P3 | total   (PRE: P0 = [loads+o staging | barrier+MFMA+x_att | LN0])")
 for r in tl:
-    print(" | ".join(str(r[i + 1] - r[i]) for i in range(5)), "|", r[5] - r[0])
+    extra = f"   [{r[6] - r[0]} | {r[7] - r[6]} | {r[1] - r[7]}]" if r[6] else ""
+    print(" | ".join(str(r[i + 1] - r[i]) for i in range(5)), "|", r[5] - r[0], extra)

@@ -139,6 +139,11 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       const int fc = min(max(f0 + r, 0), a.T - 1);
       ov[i] = *reinterpret_cast<const uint4*>(a.o + (ubase + fc) * CM_D + ch * 8);
     }
+    // LN0 affine -> LDS (threads < 128, one float4 each; read after LN0's barrier)
+    float* gb0s = Cv + 2 * CM_NW * CM_ROWS;  // [g0 | b0], past LN0's partial sums
+    const float4 gbv = tid < CM_D / 2 ? *reinterpret_cast<const float4*>((tid < CM_D / 4 ? a.g0 : a.b0) +
+                                                                         4 * (tid % (CM_D / 4)))
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
     // wave w: units w*16 .. +15 (one tile) of all CM_MT1 frame tiles;
     // D[unit 4g + e][frame mt*16 + fr]
     const int u0 = w * 16 + 4 * g;
@@ -158,11 +163,13 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
         *reinterpret_cast<uint4*>(Gs + r * CM_S + ch * 8) = live ? ov[i] : uint4{0u, 0u, 0u, 0u};
       }
     }
+    if (tid < CM_D / 2) *reinterpret_cast<float4*>(gb0s + 4 * tid) = gbv;
     // (the wo fragments after the o chunks are dead: 128-VGPR budget at 16 waves)
     const bf16_t* wrowo = a.wo + (long long)(w * 16 + fr) * CM_D + fk;
     bf16x8 fwo[CM_D / 32];
 #pragma unroll
     for (int kk = 0; kk < CM_D / 32; ++kk) fwo[kk] = ld8g(wrowo + kk * 32);
+    CM_TL(6);
     lds_barrier();
     f32x4 acc[CM_MT1];
 #pragma unroll
@@ -173,7 +180,6 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       for (int mt = 0; mt < CM_MT1; ++mt)
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
             fwo[kk], *reinterpret_cast<const bf16x8*>(Gs + (mt * 16 + fr) * CM_S + kk * 32 + fk), acc[mt], 0, 0, 0);
-    load_fw1();
     float xa[CM_MT1][4];
 #pragma unroll
     for (int mt = 0; mt < CM_MT1; ++mt) {
@@ -203,37 +209,36 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
         xres[mt] = make_float4(v[0], v[1], v[2], v[3]);
       }
     }
+    CM_TL(7);
     // LN0 over the 256 units of each frame: 4 per lane, 4 lanes per wave
     // (col4), 16 waves through LDS (Cv: free until phase 2)
+    // Sum and sum of squares in one pass (one barrier; var = E[x^2] - mean^2
+    // in fp32 on the residual stream), the affine from LDS.
     float* red = Cv;  // [CM_NW][CM_ROWS] x 2
     float mean[CM_MT1], rstd[CM_MT1];
 #pragma unroll
     for (int mt = 0; mt < CM_MT1; ++mt) {
       const float ps = col4_sum((xa[mt][0] + xa[mt][1]) + (xa[mt][2] + xa[mt][3]));
-      if (g == 0) red[w * CM_ROWS + mt * 16 + fr] = ps;
+      const float pq = col4_sum((xa[mt][0] * xa[mt][0] + xa[mt][1] * xa[mt][1]) +
+                                (xa[mt][2] * xa[mt][2] + xa[mt][3] * xa[mt][3]));
+      if (g == 0) {
+        red[w * CM_ROWS + mt * 16 + fr] = ps;
+        red[CM_NW * CM_ROWS + w * CM_ROWS + mt * 16 + fr] = pq;
+      }
     }
     lds_barrier();
+    const float4 g04 = *reinterpret_cast<const float4*>(gb0s + u0);
+    const float4 b04 = *reinterpret_cast<const float4*>(gb0s + CM_D + u0);
 #pragma unroll
     for (int mt = 0; mt < CM_MT1; ++mt) {
-      float t = 0.f;
+      float t = 0.f, t2 = 0.f;
 #pragma unroll
-      for (int k = 0; k < CM_NW; ++k) t += red[k * CM_ROWS + mt * 16 + fr];
+      for (int k = 0; k < CM_NW; ++k) {
+        t += red[k * CM_ROWS + mt * 16 + fr];
+        t2 += red[CM_NW * CM_ROWS + k * CM_ROWS + mt * 16 + fr];
+      }
       mean[mt] = t * (1.0f / CM_D);
-      float q = 0.f;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) q += (xa[mt][e] - mean[mt]) * (xa[mt][e] - mean[mt]);
-      q = col4_sum(q);
-      if (g == 0) red[CM_NW * CM_ROWS + w * CM_ROWS + mt * 16 + fr] = q;
-    }
-    lds_barrier();
-    const float4 g04 = *reinterpret_cast<const float4*>(a.g0 + u0);
-    const float4 b04 = *reinterpret_cast<const float4*>(a.b0 + u0);
-#pragma unroll
-    for (int mt = 0; mt < CM_MT1; ++mt) {
-      float t = 0.f;
-#pragma unroll
-      for (int k = 0; k < CM_NW; ++k) t += red[CM_NW * CM_ROWS + k * CM_ROWS + mt * 16 + fr];
-      rstd[mt] = 1.0f / sqrtf(t * (1.0f / CM_D) + a.eps0);
+      rstd[mt] = 1.0f / sqrtf(fmaxf(t2 * (1.0f / CM_D) - mean[mt] * mean[mt], 0.f) + a.eps0);
       const int r = mt * 16 + fr, f = f0 + r;
       const bool live = r < nrows && f >= 0 && f < a.T;
       uint2 pk = make_uint2(0u, 0u);
@@ -245,6 +250,10 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       }
       *reinterpret_cast<uint2*>(Us + r * CM_S + u0) = pk;
     }
+    // phase-1 weights only now: issued before x_att / LN0, the spill reloads
+    // of this phase (vmcnt is in order) waited for them — 11-13k cycles of
+    // L2-contended loads (every workgroup reads the same rows) in LN0
+    load_fw1();
   } else {
   // ---- phase 0: LN0 of the staged frames -> U (bf16) ----
   // all of the wave's row loads are issued before the first reduction
