@@ -154,6 +154,12 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       xv[mt] = *reinterpret_cast<const float4*>(a.x + (ubase + f) * CM_D + u0);
     }
     const float4 bo4 = a.bo ? *reinterpret_cast<const float4*>(a.bo + u0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    // the wo fragments issued with the row loads (L2: their latency overlaps
+    // the HBM rows' instead of following the o staging)
+    const bf16_t* wrowo = a.wo + (long long)(w * 16 + fr) * CM_D + fk;
+    bf16x8 fwo[CM_D / 32];
+#pragma unroll
+    for (int kk = 0; kk < CM_D / 32; ++kk) fwo[kk] = ld8g(wrowo + kk * 32);
 #pragma unroll
     for (int i = 0; i < OC; ++i) {
       const int c = tid + i * CM_NT;
@@ -164,11 +170,6 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       }
     }
     if (tid < CM_D / 2) *reinterpret_cast<float4*>(gb0s + 4 * tid) = gbv;
-    // (the wo fragments after the o chunks are dead: 128-VGPR budget at 16 waves)
-    const bf16_t* wrowo = a.wo + (long long)(w * 16 + fr) * CM_D + fk;
-    bf16x8 fwo[CM_D / 32];
-#pragma unroll
-    for (int kk = 0; kk < CM_D / 32; ++kk) fwo[kk] = ld8g(wrowo + kk * 32);
     CM_TL(6);
     lds_barrier();
     f32x4 acc[CM_MT1];
