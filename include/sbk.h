@@ -398,6 +398,15 @@ int sbk_relpos_softmax_bwd(const float* P, const void* dP, int dP_bf16, int B, i
  * utterances form one 16-B-aligned operand of the dp_k weight gradient. */
 int sbk_relpos_softmax_bwd_hm(const float* P, const void* dP, int dP_bf16, int B, int H, int T, float scale,
                               void* dS, void* dBD, int out_bf16, void* stream);
+/* Rel-pos attention backward: dqkv (B*T, H*3*dh) in the in_proj layout (b, t, h, {q,k,v}, d) from
+ * dq_ac, dk, dv (B*H, T, dh) and the head-major dq_bd (H, B*T, dh), all fp32: dq = dq_ac + dq_bd.
+ * out fp32 or bf16; dh % 4 == 0, 16-B aligned pointers. */
+int sbk_attn_dqkv(const float* dq_ac, const float* dq_bd, const float* dk, const float* dv, int B, int H, int T,
+                  int dh, void* out, int out_bf16, void* stream);
+/* Rel-pos attention backward operands in one pass: qu = q + bf16(pbu), v, dO as (B*H, T, dh), kT (B*H, dh, T),
+ * qv = q + bf16(pbv) head-major (H, B*T, dh); qkv (B*T, H*3*dh), dO (B*T, H*dh), outputs bf16. */
+int sbk_attn_bwd_prep(const void* qkv, const void* dO, const float* pbu, const float* pbv, int B, int H, int T,
+                      int dh, void* qu, void* qv, void* kT, void* v, void* doh, void* stream);
 
 /* Conv2d 3x3 stride 2 "same" reflect padding (CNN.py:616-700) as a GEMM:
  * x (B, Ti, Fi, Ci) -> col (B*To*Fo, ldcol >= 9*Ci), columns ordered (kt, kf, ci),

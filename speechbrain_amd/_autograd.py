@@ -410,12 +410,14 @@ class RelPosAttentionFn(Function):
         dt = qkv.dtype
         W = 2 * T - 1
         BH = B * H
-        q5 = qkv.view(B, T, H, 3, dh)
-        # per-(b, h) contiguous operands (B*H, T, dh)
-        q = q5[:, :, :, 0].permute(0, 2, 1, 3).reshape(BH, T, dh)
-        k = q5[:, :, :, 1].permute(0, 2, 1, 3).reshape(BH, T, dh)
-        v = q5[:, :, :, 2].permute(0, 2, 1, 3).reshape(BH, T, dh)
-        do_h = _as(do, dt).view(B, T, H, dh).permute(0, 2, 1, 3).reshape(BH, T, dh)
+        # per-(b, h) contiguous operands in one pass (sbk_attn_bwd_prep):
+        # q + u, v, dO (B*H, T, dh); K^T (B*H, dh, T); q + v head-major (H, B*T, dh)
+        mk = lambda *shape: torch.empty(*shape, device=qkv.device, dtype=dt)  # noqa: E731
+        qu, v, do_h, kT, qv = mk(BH, T, dh), mk(BH, T, dh), mk(BH, T, dh), mk(BH, dh, T), mk(H, B * T, dh)
+        do_c = _cont(_as(do, dt))
+        pbu_c, pbv_c = _cont(pbu.detach().float()), _cont(pbv.detach().float())
+        check(lib().sbk_attn_bwd_prep(ptr(qkv), ptr(do_c), ptr(pbu_c), ptr(pbv_c), B, H, T, dh, ptr(qu), ptr(qv),
+                                      ptr(kT), ptr(v), ptr(do_h), stream_of(qkv)), "sbk_attn_bwd_prep")
         Pc = (_enc.cast_bf16(attn) if attn.dtype != dt else attn).view(BH, T, T)
         dv = _enc.gemm_tn(Pc, do_h)                            # P^T dO   (BH, T, dh)
         dP = _enc.gemm_batched(do_h, v, out_dtype=dt)           # dO V^T   (BH, T, T)
@@ -426,23 +428,17 @@ class RelPosAttentionFn(Function):
         dBD = torch.empty(H, B * T, Wp, device=qkv.device, dtype=dt)  # head-major, zero-padded rows
         check(lib().sbk_relpos_softmax_bwd_hm(ptr(P), ptr(dP), _bf(dP), B, H, T, float(scale), ptr(dS), ptr(dBD),
                                               _bf(dS), stream_of(P)), "sbk_relpos_softmax_bwd_hm")
-        u = pbu.detach().reshape(1, H, 1, dh).to(dt)
-        vb = pbv.detach().reshape(1, H, 1, dh).to(dt)
-        kT = k.transpose(1, 2).contiguous()                     # (BH, dh, T)
         dq_ac = _enc.gemm_batched(dS, kT)                       # dS K     (BH, T, dh) fp32
         pkT = torch.zeros(H, dh, Wp, device=qkv.device, dtype=dt)
         pkT[:, :, :W] = pk.view(W, H, dh).permute(1, 2, 0)     # (H, dh, Wp)
         dq_bd = _enc.gemm_batched(dBD, pkT)                     # dBD P_k  (H, B*T, dh) fp32
         dpbv = rowsum_batched(dq_bd).reshape(pbv.shape)         # per head: sum over (b, t)
-        qu = (q.view(B, H, T, dh) + u).reshape(BH, T, dh)
         dk = _enc.gemm_tn(dS, qu)                               # dS^T (q + u)
-        qv = (q.view(B, H, T, dh) + vb).permute(1, 0, 2, 3).reshape(H, B * T, dh)
         dpk = _enc.gemm_tn(dBD, qv)[:, :W]                      # (H, W, dh)
-        dq_bd = dq_bd.view(H, B, T, dh).permute(1, 0, 2, 3)     # (B, H, T, dh)
-        dq_ac = dq_ac.view(B, H, T, dh)
-        dq = dq_ac + dq_bd
-        dqkv = torch.stack([dq, dk.view(B, H, T, dh), dv.view(B, H, T, dh)], dim=3)  # (B, H, T, 3, dh)
-        dqkv = dqkv.permute(0, 2, 1, 3, 4).reshape(B * T, 3 * H * dh).to(dt)
+        # dq = dq_ac + dq_bd, stacked with dk, dv into the in_proj layout, cast: one pass
+        dqkv = torch.empty(B * T, 3 * H * dh, device=qkv.device, dtype=dt)
+        check(lib().sbk_attn_dqkv(ptr(dq_ac), ptr(dq_bd), ptr(dk), ptr(dv), B, H, T, dh, ptr(dqkv), _bf(dqkv),
+                                  stream_of(dq_ac)), "sbk_attn_dqkv")
         dpk = dpk.permute(1, 0, 2).reshape(W, H * dh).to(dt)
         # sum over (b, t): over b as rows (sbk_rowsum), then over t (H*T*dh values)
         dpbu = rowsum_batched(rowsum(dq_ac.reshape(B, H * T * dh)).view(H, T, dh)).reshape(pbu.shape)

@@ -55,6 +55,8 @@ SIGNATURES = {
     "sbk_gemm_tn_cfg": [_vp, _ll, _ll, _vp, _ll, _ll, _i, _i, _i, _i, _vp, _ll, _ll, _i, _i, _vp],
     "sbk_gemm_batched": [_vp, _i, _ll, _vp, _i, _ll, _i, _i, _i, _i, _vp, _i, _ll, _i, _vp],
     "sbk_relpos_softmax_bwd_hm": [_vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _i, _vp],
+    "sbk_attn_dqkv": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _i, _vp],
+    "sbk_attn_bwd_prep": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp],
     # ffn.hip
     "sbk_ffn_supported": [_i, _i],
     "sbk_ffn": [_vp, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _i, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _vp, _f,

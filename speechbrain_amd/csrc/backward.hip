@@ -727,7 +727,91 @@ __global__ void dropout_add4_kernel(const void* __restrict__ x, int x_bf16, cons
   }
 }
 
+// Rel-pos attention backward: dqkv (B*T, H*3*dh) in the in_proj layout
+// (b, t, h, {q,k,v}, d) from the per-(b, h) products — dq = dS K + dBD P_k
+// (the second term head-major (H, B*T, dh)), dk, dv — in one pass (it was an
+// add, a stack, a permuted copy and a dtype cast).  4 d-values per thread.
+__global__ void attn_dqkv_kernel(const float* __restrict__ dq_ac, const float* __restrict__ dq_bd,
+                                 const float* __restrict__ dk, const float* __restrict__ dv, int B, int H, int T,
+                                 int dh, void* __restrict__ out, int out_bf16) {
+  const int d4n = dh / 4;
+  const long long n = (long long)B * T * H * d4n;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (long long)gridDim.x * blockDim.x) {
+    const int d4 = (int)(q % d4n);
+    long long r = q / d4n;
+    const int h = (int)(r % H);
+    r /= H;
+    const int t = (int)(r % T);
+    const int b = (int)(r / T);
+    const long long src = (((long long)b * H + h) * T + t) * dh + 4 * d4;
+    const long long sbd = ((long long)h * B * T + (long long)b * T + t) * dh + 4 * d4;
+    const float4 a = *reinterpret_cast<const float4*>(dq_ac + src);
+    const float4 c = *reinterpret_cast<const float4*>(dq_bd + sbd);
+    const long long o = (((long long)b * T + t) * H + h) * 3 * dh + 4 * d4;
+    st4(out, o, make_float4(a.x + c.x, a.y + c.y, a.z + c.z, a.w + c.w), out_bf16);
+    st4(out, o + dh, *reinterpret_cast<const float4*>(dk + src), out_bf16);
+    st4(out, o + 2 * dh, *reinterpret_cast<const float4*>(dv + src), out_bf16);
+  }
+}
+
+// Rel-pos attention backward operands from the in_proj output and dO in one
+// pass (were seven permuted copies / adds): per (b, h) contiguous
+//   qu = q + bf16(pos_bias_u), v, dO   (B*H, T, dh)
+//   kT (B*H, dh, T),  qv = q + bf16(pos_bias_v) head-major (H, B*T, dh)
+// qkv (B*T, H*3*dh) bf16 in the (h, {q,k,v}, d) layout, dO (B*T, H*dh) bf16.
+// Sums in fp32 rounded once to bf16 (what the torch bf16 add computed).
+__global__ void attn_bwd_prep_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dO,
+                                     const float* __restrict__ pbu, const float* __restrict__ pbv, int B, int H, int T,
+                                     int dh, bf16_t* __restrict__ qu, bf16_t* __restrict__ qv, bf16_t* __restrict__ kT,
+                                     bf16_t* __restrict__ vo, bf16_t* __restrict__ doh) {
+  const long long n = (long long)B * T * H * dh;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const int d = (int)(e % dh);
+    long long r = e / dh;
+    const int h = (int)(r % H);
+    r /= H;
+    const int t = (int)(r % T);
+    const int b = (int)(r / T);
+    const long long src = (((long long)b * T + t) * H + h) * 3 * dh + d;
+    const float q = bf16_to_f32(qkv[src]);
+    const float u = bf16_to_f32(f32_to_bf16(pbu[h * dh + d]));
+    const float vv = bf16_to_f32(f32_to_bf16(pbv[h * dh + d]));
+    const long long bh = (long long)b * H + h;
+    const long long o = (bh * T + t) * dh + d;
+    qu[o] = f32_to_bf16(q + u);
+    qv[((long long)h * B * T + (long long)b * T + t) * dh + d] = f32_to_bf16(q + vv);
+    kT[(bh * dh + d) * T + t] = qkv[src + dh];
+    vo[o] = qkv[src + 2 * dh];
+    doh[o] = dO[(((long long)b * T + t) * H + h) * dh + d];
+  }
+}
+
 }  // namespace
+
+SBK_API int sbk_attn_bwd_prep(const void* qkv, const void* dO, const float* pbu, const float* pbv, int B, int H,
+                              int T, int dh, void* qu, void* qv, void* kT, void* v, void* doh, void* stream) {
+  if (B <= 0 || H <= 0 || T <= 0 || dh <= 0) return SBK_ERR_ARG;
+  const long long n = (long long)B * T * H * dh;
+  attn_bwd_prep_kernel<<<grid_for(n, 256), 256, 0, (hipStream_t)stream>>>(
+      reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<const bf16_t*>(dO), pbu, pbv, B, H, T, dh,
+      reinterpret_cast<bf16_t*>(qu), reinterpret_cast<bf16_t*>(qv), reinterpret_cast<bf16_t*>(kT),
+      reinterpret_cast<bf16_t*>(v), reinterpret_cast<bf16_t*>(doh));
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+SBK_API int sbk_attn_dqkv(const float* dq_ac, const float* dq_bd, const float* dk, const float* dv, int B, int H,
+                          int T, int dh, void* out, int out_bf16, void* stream) {
+  if (B <= 0 || H <= 0 || T <= 0 || dh <= 0 || dh % 4) return SBK_ERR_ARG;
+  if ((reinterpret_cast<uintptr_t>(dq_ac) | reinterpret_cast<uintptr_t>(dq_bd) | reinterpret_cast<uintptr_t>(dk) |
+       reinterpret_cast<uintptr_t>(dv) | reinterpret_cast<uintptr_t>(out)) & 15)
+    return SBK_ERR_ARG;
+  const long long n = (long long)B * T * H * (dh / 4);
+  attn_dqkv_kernel<<<grid_for(n, 256), 256, 0, (hipStream_t)stream>>>(dq_ac, dq_bd, dk, dv, B, H, T, dh, out,
+                                                                       out_bf16);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
 
 SBK_API int sbk_dropout_add(const void* x, int x_bf16, const float* res, long long rows, int cols,
                             const unsigned char* rowmask, float alpha, float p, unsigned long long seed, void* out,
