@@ -23,10 +23,10 @@ with torch.no_grad():
     for _ in range(5):
         cm.run_fused(x, B, T, None, pre=pre)
 torch.cuda.synchronize()
-buf = (ctypes.c_ulonglong * 32)()
+buf = (ctypes.c_ulonglong * 128)()
 assert ctypes.CDLL(_L.LIB_PATH).sbk_probe_cm_tl(buf) == 0
-tl = np.array(buf, dtype=np.int64).reshape(4, 8)
-print("P0 | P1 | P2a | P2b | P3 | total   (PRE: P0 = [loads+o staging | barrier+MFMA+x_att | LN0])")
-for r in tl:
-    extra = f"   [{r[6] - r[0]} | {r[7] - r[6]} | {r[1] - r[7]}]" if r[6] else ""
-    print(" | ".join(str(r[i + 1] - r[i]) for i in range(5)), "|", r[5] - r[0], extra)
+tl = np.array(buf, dtype=np.int64).reshape(16, 8)  # the 16 waves of workgroup 100
+base = tl[:, 0].min()
+print("per wave, cycles from the workgroup's first mark: start | o staged (6) | x_att (7) | LN0 done (1) | P1 (2) | P2a (3) | P2b (4) | end (5)")
+for w, r in enumerate(tl):
+    print(f"w{w:2d}: " + " | ".join(f"{int(r[k] - base):6d}" for k in (0, 6, 7, 1, 2, 3, 4, 5)))

@@ -453,8 +453,8 @@ __global__ void __launch_bounds__(256, SBK_ATT_MINW) relpos_flash_kernel(const T
       if (vec_ok && d + 3 < dh) {  // 4 consecutive head dims: one 8-B (bf16) / 16-B (fp32) store
         if constexpr (sizeof(T) == 2) {
           uint2 pk2;
-          pk2.x = (uint32_t)f32_to_bf16(acc_o[t][0] * inv) | ((uint32_t)f32_to_bf16(acc_o[t][1] * inv) << 16);
-          pk2.y = (uint32_t)f32_to_bf16(acc_o[t][2] * inv) | ((uint32_t)f32_to_bf16(acc_o[t][3] * inv) << 16);
+          pk2.x = pack_bf16x2(acc_o[t][0] * inv, acc_o[t][1] * inv);
+          pk2.y = pack_bf16x2(acc_o[t][2] * inv, acc_o[t][3] * inv);
           *reinterpret_cast<uint2*>(orow + d) = pk2;
         } else {
           *reinterpret_cast<float4*>(orow + d) =
@@ -724,8 +724,8 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       uint2 pk2;
-      pk2.x = (uint32_t)f32_to_bf16(acc_o[t][0] * inv) | ((uint32_t)f32_to_bf16(acc_o[t][1] * inv) << 16);
-      pk2.y = (uint32_t)f32_to_bf16(acc_o[t][2] * inv) | ((uint32_t)f32_to_bf16(acc_o[t][3] * inv) << 16);
+      pk2.x = pack_bf16x2(acc_o[t][0] * inv, acc_o[t][1] * inv);
+      pk2.y = pack_bf16x2(acc_o[t][2] * inv, acc_o[t][3] * inv);
       *reinterpret_cast<uint2*>(orow + 16 * t + 4 * g) = pk2;
     }
   }

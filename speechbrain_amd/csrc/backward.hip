@@ -279,8 +279,8 @@ __device__ __forceinline__ float4 ld4(const void* p, long long i, int bf) {
 __device__ __forceinline__ void st4(void* p, long long i, float4 v, int bf) {
   if (bf) {
     uint2 u;
-    u.x = (uint32_t)f32_to_bf16(v.x) | ((uint32_t)f32_to_bf16(v.y) << 16);
-    u.y = (uint32_t)f32_to_bf16(v.z) | ((uint32_t)f32_to_bf16(v.w) << 16);
+    u.x = pack_bf16x2(v.x, v.y);
+    u.y = pack_bf16x2(v.z, v.w);
     *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p) + i) = u;
   } else {
     *reinterpret_cast<float4*>(reinterpret_cast<float*>(p) + i) = v;

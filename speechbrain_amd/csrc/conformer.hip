@@ -90,8 +90,8 @@ __global__ void __launch_bounds__(256) layernorm256_kernel(const float* __restri
       if (row >= M) continue;
       if (bf) {
         uint2 pk;
-        pk.x = (uint32_t)f32_to_bf16(v[r][0]) | ((uint32_t)f32_to_bf16(v[r][1]) << 16);
-        pk.y = (uint32_t)f32_to_bf16(v[r][2]) | ((uint32_t)f32_to_bf16(v[r][3]) << 16);
+        pk.x = pack_bf16x2(v[r][0], v[r][1]);
+        pk.y = pack_bf16x2(v[r][2], v[r][3]);
         *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(out) + row * D + 4 * lane) = pk;
       } else {
         *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + row * D + 4 * lane) =
@@ -242,8 +242,8 @@ __global__ void __launch_bounds__(256) dwconv_ln_swish_kernel(const T* __restric
       }
       if (out_bf16) {
         uint2 pk;
-        pk.x = (uint32_t)f32_to_bf16(y[0]) | ((uint32_t)f32_to_bf16(y[1]) << 16);
-        pk.y = (uint32_t)f32_to_bf16(y[2]) | ((uint32_t)f32_to_bf16(y[3]) << 16);
+        pk.x = pack_bf16x2(y[0], y[1]);
+        pk.y = pack_bf16x2(y[2], y[3]);
         *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(out) + ob + c) = pk;
       } else {
         *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + ob + c) = make_float4(y[0], y[1], y[2], y[3]);
@@ -839,8 +839,8 @@ __global__ void cast_bf16x4_kernel(const float* __restrict__ x, bf16_t* __restri
   for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (long long)gridDim.x * blockDim.x) {
     const float4 v = reinterpret_cast<const float4*>(x)[q];
     uint2 u;
-    u.x = (uint32_t)f32_to_bf16(v.x) | ((uint32_t)f32_to_bf16(v.y) << 16);
-    u.y = (uint32_t)f32_to_bf16(v.z) | ((uint32_t)f32_to_bf16(v.w) << 16);
+    u.x = pack_bf16x2(v.x, v.y);
+    u.y = pack_bf16x2(v.z, v.w);
     reinterpret_cast<uint2*>(y)[q] = u;
   }
 }

@@ -70,11 +70,11 @@ struct ConvModArgs {
 };
 
 #ifdef SBK_PROBE_TL
-__device__ unsigned long long g_cm_tl[4][8];
-#define CM_TL(i)                                                                                   \
-  do {                                                                                             \
-    if ((blockIdx.x == 100 || blockIdx.x == 7) && (threadIdx.x & 63) == 0 && (threadIdx.x >> 6) < 2) \
-      g_cm_tl[(blockIdx.x == 7) * 2 + (threadIdx.x >> 6)][i] = __builtin_amdgcn_s_memtime();        \
+__device__ unsigned long long g_cm_tl[16][8];
+#define CM_TL(i)                                                                   \
+  do {                                                                             \
+    if (blockIdx.x == 100 && (threadIdx.x & 63) == 0)                              \
+      g_cm_tl[threadIdx.x >> 6][i] = __builtin_amdgcn_s_memtime();                 \
   } while (0)
 #else
 #define CM_TL(i) \
@@ -140,7 +140,7 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       ov[i] = *reinterpret_cast<const uint4*>(a.o + (ubase + fc) * CM_D + ch * 8);
     }
     // LN0 affine -> LDS (threads < 128, one float4 each; read after LN0's barrier)
-    float* gb0s = Cv + 2 * CM_NW * CM_ROWS;  // [g0 | b0], past LN0's partial sums
+    float* gb0s = Cv + 2 * CM_ROWS * (CM_NW + 4);  // [g0 | b0], past LN0's partial sums
     const float4 gbv = tid < CM_D / 2 ? *reinterpret_cast<const float4*>((tid < CM_D / 4 ? a.g0 : a.b0) +
                                                                          4 * (tid % (CM_D / 4)))
                                       : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -215,7 +215,11 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
     // (col4), 16 waves through LDS (Cv: free until phase 2)
     // Sum and sum of squares in one pass (one barrier; var = E[x^2] - mean^2
     // in fp32 on the residual stream), the affine from LDS.
-    float* red = Cv;  // [CM_NW][CM_ROWS] x 2
+    // Partials laid out [row][wave] (+4 pad) so a row's 16 wave partials are
+    // four 16-B reads: with [wave][row] every wave issued 160 ds_read_b32
+    // here, and the CU's LDS pipe spent ~11k cycles on them.
+    constexpr int RS = CM_NW + 4;  // row stride (floats), 16-B aligned
+    float* red = Cv;               // [CM_ROWS][RS] sums, then [CM_ROWS][RS] squares
     float mean[CM_MT1], rstd[CM_MT1];
 #pragma unroll
     for (int mt = 0; mt < CM_MT1; ++mt) {
@@ -223,8 +227,8 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       const float pq = col4_sum((xa[mt][0] * xa[mt][0] + xa[mt][1] * xa[mt][1]) +
                                 (xa[mt][2] * xa[mt][2] + xa[mt][3] * xa[mt][3]));
       if (g == 0) {
-        red[w * CM_ROWS + mt * 16 + fr] = ps;
-        red[CM_NW * CM_ROWS + w * CM_ROWS + mt * 16 + fr] = pq;
+        red[(mt * 16 + fr) * RS + w] = ps;
+        red[CM_ROWS * RS + (mt * 16 + fr) * RS + w] = pq;
       }
     }
     lds_barrier();
@@ -234,9 +238,17 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
     for (int mt = 0; mt < CM_MT1; ++mt) {
       float t = 0.f, t2 = 0.f;
 #pragma unroll
-      for (int k = 0; k < CM_NW; ++k) {
-        t += red[k * CM_ROWS + mt * 16 + fr];
-        t2 += red[CM_NW * CM_ROWS + k * CM_ROWS + mt * 16 + fr];
+      for (int k4 = 0; k4 < CM_NW / 4; ++k4) {
+        const float4 a4 = *reinterpret_cast<const float4*>(red + (mt * 16 + fr) * RS + 4 * k4);
+        const float4 q4 = *reinterpret_cast<const float4*>(red + CM_ROWS * RS + (mt * 16 + fr) * RS + 4 * k4);
+        t += a4.x;
+        t += a4.y;
+        t += a4.z;
+        t += a4.w;
+        t2 += q4.x;
+        t2 += q4.y;
+        t2 += q4.z;
+        t2 += q4.w;
       }
       mean[mt] = t * (1.0f / CM_D);
       rstd[mt] = 1.0f / sqrtf(fmaxf(t2 * (1.0f / CM_D) - mean[mt] * mean[mt], 0.f) + a.eps0);
@@ -244,10 +256,8 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       const bool live = r < nrows && f >= 0 && f < a.T;
       uint2 pk = make_uint2(0u, 0u);
       if (live) {
-        pk.x = (uint32_t)f32_to_bf16((xa[mt][0] - mean[mt]) * rstd[mt] * g04.x + b04.x) |
-               ((uint32_t)f32_to_bf16((xa[mt][1] - mean[mt]) * rstd[mt] * g04.y + b04.y) << 16);
-        pk.y = (uint32_t)f32_to_bf16((xa[mt][2] - mean[mt]) * rstd[mt] * g04.z + b04.z) |
-               ((uint32_t)f32_to_bf16((xa[mt][3] - mean[mt]) * rstd[mt] * g04.w + b04.w) << 16);
+        pk.x = pack_bf16x2((xa[mt][0] - mean[mt]) * rstd[mt] * g04.x + b04.x, (xa[mt][1] - mean[mt]) * rstd[mt] * g04.y + b04.y);
+        pk.y = pack_bf16x2((xa[mt][2] - mean[mt]) * rstd[mt] * g04.z + b04.z, (xa[mt][3] - mean[mt]) * rstd[mt] * g04.w + b04.w);
       }
       *reinterpret_cast<uint2*>(Us + r * CM_S + u0) = pk;
     }
@@ -280,10 +290,8 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       const float rstd = 1.0f / sqrtf(wave_sum_v(q) * (1.0f / CM_D) + a.eps0);
       uint2 pk = make_uint2(0u, 0u);
       if (live) {
-        pk.x = (uint32_t)f32_to_bf16((v[0] - mean) * rstd * g04.x + b04.x) |
-               ((uint32_t)f32_to_bf16((v[1] - mean) * rstd * g04.y + b04.y) << 16);
-        pk.y = (uint32_t)f32_to_bf16((v[2] - mean) * rstd * g04.z + b04.z) |
-               ((uint32_t)f32_to_bf16((v[3] - mean) * rstd * g04.w + b04.w) << 16);
+        pk.x = pack_bf16x2((v[0] - mean) * rstd * g04.x + b04.x, (v[1] - mean) * rstd * g04.y + b04.y);
+        pk.y = pack_bf16x2((v[2] - mean) * rstd * g04.z + b04.z, (v[3] - mean) * rstd * g04.w + b04.w);
       }
       *reinterpret_cast<uint2*>(Us + r * CM_S + lane * 4) = pk;
     }
@@ -345,8 +353,8 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
           o[e] = live ? va * (1.0f / (1.0f + __expf(-vg))) : 0.f;
         }
         uint2 pk;
-        pk.x = (uint32_t)f32_to_bf16(o[0]) | ((uint32_t)f32_to_bf16(o[1]) << 16);
-        pk.y = (uint32_t)f32_to_bf16(o[2]) | ((uint32_t)f32_to_bf16(o[3]) << 16);
+        pk.x = pack_bf16x2(o[0], o[1]);
+        pk.y = pack_bf16x2(o[2], o[3]);
         *reinterpret_cast<uint2*>(Gs + r * CM_S + ch) = pk;
       }
     }
@@ -421,8 +429,8 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
         v[e] = z * (1.0f / (1.0f + __expf(-z)));
       }
       uint2 pk;
-      pk.x = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
-      pk.y = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
+      pk.x = pack_bf16x2(v[0], v[1]);
+      pk.y = pack_bf16x2(v[2], v[3]);
       *reinterpret_cast<uint2*>(Us + fi * CM_S + lane * 4) = pk;
     }
   }

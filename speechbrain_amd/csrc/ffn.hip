@@ -305,10 +305,8 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     for (int e = 0; e < 4; ++e) q += (v[e] - mean) * (v[e] - mean);
     const float rstd = 1.0f / sqrtf(wave_sum_v(q) / D + a.eps0);
     uint2 pk;
-    pk.x = (uint32_t)f32_to_bf16((v[0] - mean) * rstd * g04.x + b04.x) |
-           ((uint32_t)f32_to_bf16((v[1] - mean) * rstd * g04.y + b04.y) << 16);
-    pk.y = (uint32_t)f32_to_bf16((v[2] - mean) * rstd * g04.z + b04.z) |
-           ((uint32_t)f32_to_bf16((v[3] - mean) * rstd * g04.w + b04.w) << 16);
+    pk.x = pack_bf16x2((v[0] - mean) * rstd * g04.x + b04.x, (v[1] - mean) * rstd * g04.y + b04.y);
+    pk.y = pack_bf16x2((v[2] - mean) * rstd * g04.z + b04.z, (v[3] - mean) * rstd * g04.w + b04.w);
     *reinterpret_cast<uint2*>(Xn + rr * XS + lane * PER) = pk;
   }
   for (int i = tid; i < a.H; i += NT) b1s[i] = a.b1[i];
@@ -377,8 +375,8 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         uint2 pk;
-        pk.x = (uint32_t)f32_to_bf16(z[j][mt][0]) | ((uint32_t)f32_to_bf16(z[j][mt][1]) << 16);
-        pk.y = (uint32_t)f32_to_bf16(z[j][mt][2]) | ((uint32_t)f32_to_bf16(z[j][mt][3]) << 16);
+        pk.x = pack_bf16x2(z[j][mt][0], z[j][mt][1]);
+        pk.y = pack_bf16x2(z[j][mt][2], z[j][mt][3]);
         *reinterpret_cast<uint2*>(Xn + (mt * 16 + fr) * XS + d) = pk;
       }
     }
@@ -451,10 +449,8 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
           for (int mt = 0; mt < MT; ++mt) {
             const f32x4 v = acc1[t][mt];
             uint2 pk;
-            pk.x = (uint32_t)f32_to_bf16(act_fn<ACT>(v[0] + bb[0], a.slope)) |
-                   ((uint32_t)f32_to_bf16(act_fn<ACT>(v[1] + bb[1], a.slope)) << 16);
-            pk.y = (uint32_t)f32_to_bf16(act_fn<ACT>(v[2] + bb[2], a.slope)) |
-                   ((uint32_t)f32_to_bf16(act_fn<ACT>(v[3] + bb[3], a.slope)) << 16);
+            pk.x = pack_bf16x2(act_fn<ACT>(v[0] + bb[0], a.slope), act_fn<ACT>(v[1] + bb[1], a.slope));
+            pk.y = pack_bf16x2(act_fn<ACT>(v[2] + bb[2], a.slope), act_fn<ACT>(v[3] + bb[3], a.slope));
             const uint32_t la = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) bf16_t*)(Hc + (mt * 16 + fr) * HS + n));
             const unsigned long long pv = (unsigned long long)pk.x | ((unsigned long long)pk.y << 32);
             asm volatile("ds_write_b64 %0, %1" ::"v"(la), "v"(pv) : "memory");
@@ -516,8 +512,8 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         uint2 pk;
-        pk.x = (uint32_t)f32_to_bf16(z[j][mt][0]) | ((uint32_t)f32_to_bf16(z[j][mt][1]) << 16);
-        pk.y = (uint32_t)f32_to_bf16(z[j][mt][2]) | ((uint32_t)f32_to_bf16(z[j][mt][3]) << 16);
+        pk.x = pack_bf16x2(z[j][mt][0], z[j][mt][1]);
+        pk.y = pack_bf16x2(z[j][mt][2], z[j][mt][3]);
         *reinterpret_cast<uint2*>(Xn + (mt * 16 + fr) * XS + d) = pk;
       }
     }
@@ -585,8 +581,8 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
           const int row = m0 + mt * 16 + fr;
           const f32x4 v = acc1[t][mt];
           uint2 pk;
-          pk.x = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
-          pk.y = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
+          pk.x = pack_bf16x2(v[0], v[1]);
+          pk.y = pack_bf16x2(v[2], v[3]);
           if (row < a.M) *reinterpret_cast<uint2*>(a.yp + (long long)row * a.np + n) = pk;
           acc1[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
@@ -619,8 +615,8 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
         if (row >= a.M) continue;
         if (a.u_bf16) {
           uint2 pk;
-          pk.x = (uint32_t)f32_to_bf16(z[j][mt][0]) | ((uint32_t)f32_to_bf16(z[j][mt][1]) << 16);
-          pk.y = (uint32_t)f32_to_bf16(z[j][mt][2]) | ((uint32_t)f32_to_bf16(z[j][mt][3]) << 16);
+          pk.x = pack_bf16x2(z[j][mt][0], z[j][mt][1]);
+          pk.y = pack_bf16x2(z[j][mt][2], z[j][mt][3]);
           *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(a.u) + (long long)row * D + d) = pk;
         } else {
           *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.u) + (long long)row * D + d) =

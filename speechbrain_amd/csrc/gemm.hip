@@ -107,8 +107,8 @@ __device__ __forceinline__ void store_ctile_fast(const float* __restrict__ Cs, c
     }
     if (ep.out_bf16) {
       uint2 pk;
-      pk.x = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
-      pk.y = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
+      pk.x = pack_bf16x2(v[0], v[1]);
+      pk.y = pack_bf16x2(v[2], v[3]);
       *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(ep.out) + (long long)row * ep.ldc + oc) = pk;
     } else {
       *reinterpret_cast<float4*>(reinterpret_cast<float*>(ep.out) + (long long)row * ep.ldc + oc) =
@@ -177,8 +177,8 @@ __device__ __forceinline__ void store_ctile_rowln(const float* __restrict__ Cs, 
     const float y2 = (v[rr][2] - mean) * rstd * g4.z + b4.z, y3 = (v[rr][3] - mean) * rstd * g4.w + b4.w;
     if (ep.ln_bf16) {
       uint2 pk;
-      pk.x = (uint32_t)f32_to_bf16(y0) | ((uint32_t)f32_to_bf16(y1) << 16);
-      pk.y = (uint32_t)f32_to_bf16(y2) | ((uint32_t)f32_to_bf16(y3) << 16);
+      pk.x = pack_bf16x2(y0, y1);
+      pk.y = pack_bf16x2(y2, y3);
       *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(ep.ln_out) + (long long)row * ep.ldu + 4 * lane) = pk;
     } else {
       *reinterpret_cast<float4*>(reinterpret_cast<float*>(ep.ln_out) + (long long)row * ep.ldu + 4 * lane) =
@@ -256,8 +256,8 @@ __device__ __forceinline__ void store_ctile(const float* __restrict__ Cs, const 
       bf16_t* op = reinterpret_cast<bf16_t*>(ep.out) + (long long)row * ep.ldc + oc;
       if (full && ((reinterpret_cast<uintptr_t>(op) & 7) == 0)) {
         uint2 pk;
-        pk.x = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
-        pk.y = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
+        pk.x = pack_bf16x2(v[0], v[1]);
+        pk.y = pack_bf16x2(v[2], v[3]);
         *reinterpret_cast<uint2*>(op) = pk;
       } else {
 #pragma unroll

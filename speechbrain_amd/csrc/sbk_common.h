@@ -80,9 +80,17 @@ __device__ __forceinline__ float bf16_to_f32(uint16_t h) {
 }
 // Round-to-nearest-even f32 -> bf16 (NaN handled by the hardware cvt path
 // where the compiler emits v_cvt_pk_bf16_f32).
+// fp32 -> bf16, round to nearest even, on the gfx950 conversion instruction
+// (v_cvt_pk_bf16_f32: one VALU op; the software rounding of __float2bfloat16
+// was ~5 and sat in the VALU-bound epilogues of the fused kernels).
 __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
-  __hip_bfloat16 b = __float2bfloat16(f);
-  return *reinterpret_cast<uint16_t*>(&b);
+  return __builtin_bit_cast(uint16_t, (__bf16)f);
+}
+// two values packed (lo in bits 0-15): one v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2_t __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2_t{lo, hi}, b2_t));
 }
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }

@@ -272,8 +272,8 @@ __global__ void __launch_bounds__(TH_NT) thead_kernel(TheadArgs a) {
           }
         }
         uint2 pk;
-        pk.x = (uint32_t)f32_to_bf16(d[0]) | ((uint32_t)f32_to_bf16(d[1]) << 16);
-        pk.y = (uint32_t)f32_to_bf16(d[2]) | ((uint32_t)f32_to_bf16(d[3]) << 16);
+        pk.x = pack_bf16x2(d[0], d[1]);
+        pk.y = pack_bf16x2(d[2], d[3]);
         if (row < a.M) *reinterpret_cast<uint2*>(a.ds + (long long)row * a.Vp + v0) = pk;
       }
     }
