@@ -140,7 +140,7 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       ov[i] = *reinterpret_cast<const uint4*>(a.o + (ubase + fc) * CM_D + ch * 8);
     }
     // LN0 affine -> LDS (threads < 128, one float4 each; read after LN0's barrier)
-    float* gb0s = Cv + 2 * CM_ROWS * (CM_NW + 4);  // [g0 | b0], past LN0's partial sums
+    float* gb0s = Cv + 2 * CM_ROWS * (CM_NW + 4) + 2 * CM_ROWS;  // [g0 | b0], past LN0's partials / statistics
     const float4 gbv = tid < CM_D / 2 ? *reinterpret_cast<const float4*>((tid < CM_D / 4 ? a.g0 : a.b0) +
                                                                          4 * (tid % (CM_D / 4)))
                                       : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -232,15 +232,17 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       }
     }
     lds_barrier();
-    const float4 g04 = *reinterpret_cast<const float4*>(gb0s + u0);
-    const float4 b04 = *reinterpret_cast<const float4*>(gb0s + CM_D + u0);
-#pragma unroll
-    for (int mt = 0; mt < CM_MT1; ++mt) {
+    // final statistics once per row (lanes of waves 0-1: row = 64 w + lane),
+    // not redundantly in all 16 waves: the LN0 phase is VALU-issue bound
+    // (4 waves per SIMD), and the 16-way sums were a third of its VALU work
+    float* stat = red + 2 * CM_ROWS * RS;  // [CM_ROWS] mean, [CM_ROWS] rstd (inside Cv, before gb0s)
+    if (w < (CM_ROWS + 63) / 64 && w * 64 + lane < CM_ROWS) {
+      const int row = w * 64 + lane;
       float t = 0.f, t2 = 0.f;
 #pragma unroll
       for (int k4 = 0; k4 < CM_NW / 4; ++k4) {
-        const float4 a4 = *reinterpret_cast<const float4*>(red + (mt * 16 + fr) * RS + 4 * k4);
-        const float4 q4 = *reinterpret_cast<const float4*>(red + CM_ROWS * RS + (mt * 16 + fr) * RS + 4 * k4);
+        const float4 a4 = *reinterpret_cast<const float4*>(red + row * RS + 4 * k4);
+        const float4 q4 = *reinterpret_cast<const float4*>(red + CM_ROWS * RS + row * RS + 4 * k4);
         t += a4.x;
         t += a4.y;
         t += a4.z;
@@ -250,8 +252,17 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
         t2 += q4.z;
         t2 += q4.w;
       }
-      mean[mt] = t * (1.0f / CM_D);
-      rstd[mt] = 1.0f / sqrtf(fmaxf(t2 * (1.0f / CM_D) - mean[mt] * mean[mt], 0.f) + a.eps0);
+      const float mu = t * (1.0f / CM_D);
+      stat[row] = mu;
+      stat[CM_ROWS + row] = 1.0f / sqrtf(fmaxf(t2 * (1.0f / CM_D) - mu * mu, 0.f) + a.eps0);
+    }
+    lds_barrier();
+    const float4 g04 = *reinterpret_cast<const float4*>(gb0s + u0);
+    const float4 b04 = *reinterpret_cast<const float4*>(gb0s + CM_D + u0);
+#pragma unroll
+    for (int mt = 0; mt < CM_MT1; ++mt) {
+      mean[mt] = stat[mt * 16 + fr];
+      rstd[mt] = stat[CM_ROWS + mt * 16 + fr];
       const int r = mt * 16 + fr, f = f0 + r;
       const bool live = r < nrows && f >= 0 && f < a.T;
       uint2 pk = make_uint2(0u, 0u);
