@@ -231,6 +231,10 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
         red[CM_ROWS * RS + (mt * 16 + fr) * RS + w] = pq;
       }
     }
+    // phase-1 weights issued here: their latency overlaps the statistics
+    // exchange (issued before x_att, the spill reloads of this phase waited
+    // for them: vmcnt is in order)
+    load_fw1();
     lds_barrier();
     // final statistics once per row (lanes of waves 0-1: row = 64 w + lane),
     // not redundantly in all 16 waves: the LN0 phase is VALU-issue bound
@@ -272,10 +276,6 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       }
       *reinterpret_cast<uint2*>(Us + r * CM_S + u0) = pk;
     }
-    // phase-1 weights only now: issued before x_att / LN0, the spill reloads
-    // of this phase (vmcnt is in order) waited for them — 11-13k cycles of
-    // L2-contended loads (every workgroup reads the same rows) in LN0
-    load_fw1();
   } else {
   // ---- phase 0: LN0 of the staged frames -> U (bf16) ----
   // all of the wave's row loads are issued before the first reduction
