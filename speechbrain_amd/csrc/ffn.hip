@@ -51,6 +51,8 @@
 // of VGPRs (36.7 us), a per-XCD rotated chunk order (35.0 us), a 3-slot ring
 // with one hidden buffer (37.2 us), a third slot aliased onto Xn after the
 // VGPR load (30.3 us), a tile-contiguous weight image (29.3 us).
+// Round 2 (layer chain, 58 us): a single-pass row LayerNorm (sum and sum of
+// squares in one LDS exchange, affine prefetched) was no faster (58.4 us).
 #include "mfma.h"
 
 using namespace sbk;
