@@ -39,11 +39,18 @@ struct FftPlan {
   int radix[12];
 };
 
+// Complex arithmetic on packed fp32 pairs (v_pk_add/mul/fma_f32: one VALU op
+// per complex add, two per complex multiply); the spectrum kernel is
+// VALU-issue bound.
+typedef float v2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ v2f tv(float2 a) { return v2f{a.x, a.y}; }
+__device__ __forceinline__ float2 fv(v2f a) { return make_float2(a[0], a[1]); }
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+  // (a.x b.x - a.y b.y, a.x b.y + a.y b.x)
+  return fv(__builtin_elementwise_fma(v2f{-a.y, a.y}, v2f{b.y, b.x}, v2f{a.x, a.x} * tv(b)));
 }
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return fv(tv(a) + tv(b)); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return fv(tv(a) - tv(b)); }
 // multiply by -i
 __device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }
 // multiply by +i
@@ -65,8 +72,8 @@ __device__ __forceinline__ void dft_small<3>(float2* v) {
   float2 t = cadd(v[1], v[2]);
   float2 d = csub(v[1], v[2]);
   float2 y0 = cadd(v[0], t);
-  float2 m = make_float2(v[0].x - 0.5f * t.x, v[0].y - 0.5f * t.y);
-  float2 sd = make_float2(s * d.x, s * d.y);
+  float2 m = fv(tv(v[0]) - 0.5f * tv(t));
+  float2 sd = fv(s * tv(d));
   v[0] = y0;
   v[1] = cadd(m, mul_mi(sd));
   v[2] = cadd(m, mul_pi(sd));
@@ -91,10 +98,10 @@ __device__ __forceinline__ void dft_small<5>(float2* v) {
   float2 t1 = cadd(v[1], v[4]), t2 = cadd(v[2], v[3]);
   float2 t3 = csub(v[1], v[4]), t4 = csub(v[2], v[3]);
   float2 y0 = cadd(v[0], cadd(t1, t2));
-  float2 a = make_float2(v[0].x + c1 * t1.x + c2 * t2.x, v[0].y + c1 * t1.y + c2 * t2.y);
-  float2 b = make_float2(v[0].x + c2 * t1.x + c1 * t2.x, v[0].y + c2 * t1.y + c1 * t2.y);
-  float2 p = make_float2(s1 * t3.x + s2 * t4.x, s1 * t3.y + s2 * t4.y);
-  float2 q = make_float2(s2 * t3.x - s1 * t4.x, s2 * t3.y - s1 * t4.y);
+  float2 a = fv(tv(v[0]) + c1 * tv(t1) + c2 * tv(t2));
+  float2 b = fv(tv(v[0]) + c2 * tv(t1) + c1 * tv(t2));
+  float2 p = fv(s1 * tv(t3) + s2 * tv(t4));
+  float2 q = fv(s2 * tv(t3) - s1 * tv(t4));
   v[0] = y0;
   v[1] = cadd(a, mul_mi(p));
   v[4] = cadd(a, mul_pi(p));
@@ -112,9 +119,9 @@ __device__ __forceinline__ void dft_small<8>(float2* v) {
     a[i] = cadd(v[i], v[i + 4]);
     b[i] = csub(v[i], v[i + 4]);
   }
-  b[1] = make_float2(r * (b[1].x + b[1].y), r * (b[1].y - b[1].x));     // * (r, -r)
+  b[1] = fv(r * (v2f{b[1].x, b[1].y} + v2f{b[1].y, -b[1].x}));          // * (r, -r)
   b[2] = mul_mi(b[2]);                                                  // * -i
-  b[3] = make_float2(r * (-b[3].x + b[3].y), r * (-b[3].y - b[3].x));   // * (-r, -r)
+  b[3] = fv(r * (v2f{-b[3].x, -b[3].y} + v2f{b[3].y, -b[3].x}));        // * (-r, -r)
   dft_small<4>(a);
   dft_small<4>(b);
 #pragma unroll
