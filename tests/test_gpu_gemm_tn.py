@@ -22,6 +22,39 @@ def test_gemm_tn(dev, K, M, N, batch):
     assert ((c - ref).abs() <= bound).all(), ((c - ref).abs() / bound).max()
 
 
+@pytest.mark.parametrize("tile", [64, 128])
+@pytest.mark.parametrize("nsplit", [1, 3, 8])
+def test_gemm_tn_cfg_tiles_and_splits(dev, tile, nsplit):
+    """Every (tile, split) configuration of sbk_gemm_tn_cfg — plain stores at
+    one split, fp32 atomics otherwise — on ragged M, N (multiples of 8) and a
+    K that does not divide into the splits."""
+    from speechbrain_amd._lib import lib, ptr, stream_of
+    torch.manual_seed(tile + nsplit)
+    K, M, N = 3001, 200, 136
+    a = torch.randn(K, M, device=dev).to(torch.bfloat16)
+    b = torch.randn(K, N, device=dev).to(torch.bfloat16)
+    c = torch.zeros(M, N, device=dev)
+    assert lib().sbk_gemm_tn_cfg(ptr(a), M, 0, ptr(b), N, 0, M, N, K, 1, ptr(c), N, 0, tile, nsplit,
+                                 stream_of(a)) == 0
+    ref = a.float().t() @ b.float()
+    bound = 1e-5 * (a.float().abs().t() @ b.float().abs()) + 1e-6
+    assert ((c - ref).abs() <= bound).all(), ((c - ref).abs() / bound).max()
+
+
+def test_cast_bf16_paths_bit_exact(dev):
+    """sbk_cast_bf16 (4-wide and per-element kernels) rounds exactly as torch's
+    .to(bfloat16) (round to nearest even), incl. ties, infinities and NaN."""
+    from speechbrain_amd import _enc
+    torch.manual_seed(1)
+    base = torch.randn(4097, device=dev) * 3
+    base[:8] = torch.tensor([1.00390625, 1.01171875, -2.0078125, 65504.0, float("inf"), -float("inf"), 0.0, -0.0])
+    for x in (base[:4096].contiguous(), base[1:].contiguous(), base[1:4096].clone()):  # n % 4 == 0 / odd sizes
+        y = _enc.cast_bf16(x)
+        assert torch.equal(y.view(torch.int16), x.to(torch.bfloat16).view(torch.int16))
+    nan = _enc.cast_bf16(torch.full((8,), float("nan"), device=dev))
+    assert torch.isnan(nan.float()).all()
+
+
 def test_linear_backward_on_sbk(dev):
     """LinearFn backward in bf16: dX = dY W (sbk_gemm), dW = dY^T X
     (sbk_gemm_tn), db = column sums, against torch autograd on the same bf16
