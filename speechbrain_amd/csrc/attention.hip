@@ -512,6 +512,18 @@ __device__ __forceinline__ void dma16(const bf16_t* src, bf16_t* lds) {
       (uint32_t)(uintptr_t)((__attribute__((address_space(3))) bf16_t*)lds));
   asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(la) : "memory", "m0");
 }
+// The same piece from a wave-uniform base (SGPR pair) plus a per-lane byte
+// offset computed once before the chunk loop; m0 (the LDS destination) is a
+// precomputed scalar.  The interior chunks issue their DMAs with no VALU
+// address arithmetic at all (the clamped form above cost ~75 VALU
+// instructions per chunk, 8 of them quarter-rate multiplies, in a kernel
+// whose chunk time is VALU issue).
+__device__ __forceinline__ void dma16s(const void* sbase, uint32_t voff, uint32_t la) {
+  asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(la) : "memory", "m0");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* lds) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)lds));
+}
 // this wave's DMA pieces and LDS accesses done, then the workgroup barrier
 __device__ __forceinline__ void dma_barrier() {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -543,7 +555,7 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
   __shared__ __attribute__((aligned(16))) bf16_t Ps[PB * RB];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[KC * RB];
   __shared__ __attribute__((aligned(16))) float Gs[4 * 16 * G2];
-  __shared__ __attribute__((aligned(16))) float Ms[KC];
+  __shared__ __attribute__((aligned(16))) float Ms[KC + 4];  // key mask + 'chunk has a masked key' flag
 
   const int d_model = H * dh;
   const long long row3 = 3LL * d_model;
@@ -554,21 +566,50 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
   const int qb = tile % nqb, bh = tile / nqb;
   const int h = bh % H, b = bh / H;
   const int i0 = qb * QB;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c16 = lane & 15, g = lane >> 4;
   const int my_i = i0 + 16 * w + c16;
+#ifdef SBK_PROBE_TL
+  const bool tl_on = tile == 200;
+#endif
   const bf16_t* qkv_b = qkv + (long long)b * Tn * row3 + h * 3 * dh;
   const bf16_t* pk_h = pk + h * dh;
   float* gq = Gs + w * 16 * G2 + c16 * G2 + GO;  // this lane's query row of the G scratch, at key 0
   const int lrow = lane >> 3, lchk = lane & 7;   // DMA piece: 8 rows x 8 16-B chunks
 
+  // per-lane byte offsets of the interior-chunk DMA pieces (row stride x row
+  // + swizzled 16-B chunk); the chunk's base goes in the scalar operand
+  uint32_t offk[2], offv[2], offp[4], lak[2], lav[2], lap[4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r0 = 16 * w + 8 * i, row = r0 + lrow;
+    offk[i] = (uint32_t)(row * row3 + ((lchk ^ swz_kp(row)) << 3)) * 2u;
+    offv[i] = (uint32_t)(row * row3 + ((lchk ^ swz_v(row)) << 3)) * 2u;
+    lak[i] = lds_addr(Ks + r0 * RB);
+    lav[i] = lds_addr(Vs + r0 * RB);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r0 = 32 * w + 8 * i, rr = r0 + lrow;
+    offp[i] = (uint32_t)(rr * ldp + ((lchk ^ swz_kp(rr)) << 3)) * 2u;
+    lap[i] = lds_addr(Ps + r0 * RB);
+  }
   auto dma_kp = [&](int j0) {
+    const int rbase = Tn - QB - i0 + j0;  // band row 0
+    if (j0 + KC <= Tn && rbase >= 0 && rbase + PB <= 2 * Tn - 1) {  // no row clamped
+      const bf16_t* sk = qkv_b + (long long)j0 * row3 + dh;
+      const bf16_t* sp = pk_h + (long long)rbase * ldp;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) dma16s(sk, offk[i], lak[i]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dma16s(sp, offp[i], lap[i]);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {  // K rows 16w .. 16w+15
       const int r0 = 16 * w + 8 * i, row = r0 + lrow;
       dma16(qkv_b + (long long)min(j0 + row, Tn - 1) * row3 + dh + ((lchk ^ swz_kp(row)) << 3), Ks + r0 * RB);
     }
-    const int rbase = Tn - QB - i0 + j0;  // band row 0
 #pragma unroll
     for (int i = 0; i < 4; ++i) {  // band rows 32w .. 32w+31
       const int r0 = 32 * w + 8 * i, rr = r0 + lrow;
@@ -577,6 +618,12 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
     }
   };
   auto dma_v = [&](int j0) {
+    if (j0 + KC <= Tn) {
+      const bf16_t* sv = qkv_b + (long long)j0 * row3 + 2 * dh;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) dma16s(sv, offv[i], lav[i]);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int r0 = 16 * w + 8 * i, row = r0 + lrow;
@@ -587,6 +634,7 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
   // when Ms is written (a compare right after the load waited for it)
   auto key_byte = [&](int j0) -> int { return kpm ? (int)kpm[(long long)b * Tn + min(j0 + lane, Tn - 1)] : 0; };
 
+  ATT_TL(0);
   dma_kp(0);
   int rm = w == 0 ? key_byte(0) : 0;
 
@@ -626,8 +674,12 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
     const int j0 = ch * KC;
     const bool more = ch + 1 < nchunk;
     dma_barrier();  // A
+    ATT_TL(1 + 5 * ch);
     if (w == 0) {  // key mask (0 / -inf); keys past Tn are masked, so the clamped rows staged for them never count
-      Ms[lane] = (j0 + lane < Tn && rm == 0) ? 0.f : -INFINITY;
+      const bool mkd = !(j0 + lane < Tn && rm == 0);
+      Ms[lane] = mkd ? -INFINITY : 0.f;
+      const unsigned long long anym = __ballot(mkd);
+      if (lane == 0) Ms[KC] = anym ? 1.f : 0.f;
       if (more) rm = key_byte(j0 + KC);
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -667,15 +719,16 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
         if (t == 4) p = min(p, KC);
         gq[p] = acc_g[t][r];
       }
+    ATT_TL(2 + 5 * ch);
     dma_barrier();  // B
+    ATT_TL(3 + 5 * ch);
 
     // scores for this lane's query, keys jj = 16t + 4g + r (log2 domain)
-    f32x4 gv[4], mk[4];
+    f32x4 gv[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      gv[t] = *reinterpret_cast<const f32x4*>(gq + 16 * t + 4 * g);
-      mk[t] = *reinterpret_cast<const f32x4*>(Ms + 16 * t + 4 * g);
-    }
+    for (int t = 0; t < 4; ++t) gv[t] = *reinterpret_cast<const f32x4*>(gq + 16 * t + 4 * g);
+    // the mask is added only in chunks that hold a masked key (uniform branch)
+    const bool chunk_masked = __builtin_amdgcn_readfirstlane(__float_as_uint(Ms[KC])) != 0u;
     __builtin_amdgcn_sched_barrier(0);
     if (more) dma_kp(j0 + KC);
     float p[4][4];
@@ -683,10 +736,19 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        p[t][r] = acc_s[t][r] + gv[t][r] + mk[t][r];
-        cmax = fmaxf(cmax, p[t][r]);
+      for (int r = 0; r < 4; ++r) p[t][r] = acc_s[t][r] + gv[t][r];
+    if (chunk_masked) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const f32x4 mk = *reinterpret_cast<const f32x4*>(Ms + 16 * t + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) p[t][r] += mk[r];
       }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cmax = fmaxf(cmax, p[t][r]);
     cmax = col4_max(cmax);
     const float m_new = fmaxf(m_run, cmax);
     const float mref = m_new == -INFINITY ? 0.f : m_new;
@@ -703,6 +765,7 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
     m_run = m_new;
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc_o[t] *= alpha;
+    ATT_TL(4 + 5 * ch);
     // O^T += V^T · P^T (2 k-steps of 32 keys, permuted-k fragments as above)
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -717,6 +780,7 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
       for (int t = 0; t < 4; ++t)
         acc_o[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt_frag_swz(Vs, 32 * s2, 16 * t, lane), fp, acc_o[t], 0, 0, 0);
     }
+    ATT_TL(5 + 5 * ch);
   }
   if (my_i < Tn) {
     const float inv = 1.0f / l_run;
@@ -729,6 +793,7 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
       *reinterpret_cast<uint2*>(orow + 16 * t + 4 * g) = pk2;
     }
   }
+  ATT_TL(62);
 }
 
 int launch_dma(const void* qkv, const void* pk, int ldp, const float* pbu, const float* pbv, const uint8_t* kpm, int B,

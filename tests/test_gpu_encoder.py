@@ -293,7 +293,8 @@ def _relpos_ref(qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale):
 
 
 @pytest.mark.parametrize("T,lens,strided", [(37, [37, 30, 21], False), (97, [97, 60, 5], True),
-                                            (376, [376, 376, 200, 1], True)])
+                                            (376, [376, 376, 200, 1], True), (640, [640, 640], False),
+                                            (256, None, True)])
 def test_relpos_attention_bf16_vs_torch(dev, T, lens, strided):
     """The encoder's attention path (bf16, dh = 64, no probabilities: the
     LDS-DMA kernel) vs an fp32 torch evaluation on the same bf16 operands:
@@ -302,6 +303,8 @@ def test_relpos_attention_bf16_vs_torch(dev, T, lens, strided):
     the P·V MFMA, so outputs (~N(0,1) averages) agree to 2e-2."""
     from speechbrain_amd import _enc
     g = torch.Generator().manual_seed(T)
+    no_mask = lens is None  # no key-padding mask at all (kpm = null)
+    lens = [T, T] if no_mask else lens
     B, H, dh = len(lens), 4, 64
     d = H * dh
     qkv = torch.randn(B * T, 3 * d, generator=g).to(torch.bfloat16).to(dev)
@@ -311,7 +314,8 @@ def test_relpos_attention_bf16_vs_torch(dev, T, lens, strided):
     pbv = (0.1 * torch.randn(d, generator=g)).to(dev)
     kpm = (torch.arange(T)[None] >= torch.tensor(lens)[:, None]).to(dev)
     scale = 1.0 / math.sqrt(d)
-    out, _ = _enc.relpos_attention(qkv, pk, pbu, pbv, kpm.to(torch.uint8).contiguous(), B, T, H, dh, scale)
+    out, _ = _enc.relpos_attention(qkv, pk, pbu, pbv, None if no_mask else kpm.to(torch.uint8).contiguous(),
+                                   B, T, H, dh, scale)
     ref = _relpos_ref(qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale)
     assert out.dtype == torch.bfloat16
     assert_close(out, ref, rtol=2e-2, name="attn_bf16")
