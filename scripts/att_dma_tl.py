@@ -42,3 +42,31 @@ for w in range(4):
         nxt = r[b + 5] if ch < 5 else r[62]
         parts.append(f"{r[b+1]-r[b]:5d} {r[b+2]-r[b+1]:5d} {r[b+3]-r[b+2]:5d} {r[b+4]-r[b+3]:5d} {nxt-r[b+4]:5d}")
     print(f"w{w} pre {r[1]-r[0]:5d} | " + " | ".join(parts) + f" | total {r[62]-r[0]}")
+
+# per-workgroup start / end of the last launch: rounds of residency and the clock
+wg = (ctypes.c_ulonglong * (4096 * 4))()
+assert ctypes.CDLL(_L.LIB_PATH).sbk_probe_att_wg(wg) == 0
+a = np.array(wg, dtype=np.int64).reshape(4096, 4)[: B * H * ((T + 63) // 64)]
+rt0, rt1, mt0, mt1 = a[:, 0], a[:, 1], a[:, 2], a[:, 3]
+t0 = rt0.min()
+life_us = (rt1 - rt0) / 100.0  # memrealtime: 100 MHz
+print(f"workgroups {len(a)}: launch span {(rt1.max() - t0) / 100.0:.2f} us; life us min/med/max "
+      f"{life_us.min():.2f}/{np.median(life_us):.2f}/{life_us.max():.2f}")
+print(f"memtime ticks per us (median): {np.median((mt1 - mt0) / np.maximum(life_us, 1e-3)):.0f}")
+st = (rt0 - t0) / 100.0
+print("start-time histogram (us):", np.histogram(st, bins=10)[0].tolist(), "edges",
+      np.round(np.histogram(st, bins=10)[1], 2).tolist())
+nwg, nqb = len(a), (T + 63) // 64
+orig = np.arange(nwg)
+xcd, q8, r8 = orig & 7, nwg >> 3, nwg & 7
+tile = np.where(xcd < r8, xcd * (q8 + 1), r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3)
+qb = tile % nqb
+for k in range(nqb):
+    print(f"qb {k}: life median {np.median(life_us[qb == k]):.2f} max {life_us[qb == k].max():.2f}")
+for k in range(8):
+    print(f"xcd {k}: life median {np.median(life_us[xcd == k]):.2f} max {life_us[xcd == k].max():.2f}")
+end = (rt1 - t0) / 100.0
+print("end-time histogram (us):", np.histogram(end, bins=10)[0].tolist(), "edges",
+      np.round(np.histogram(end, bins=10)[1], 2).tolist())
+os.makedirs("gpurun_out", exist_ok=True)
+np.save("gpurun_out/att_wg.npy", a)

@@ -96,6 +96,7 @@ __device__ __forceinline__ bf16x8 vt_frag_tr(const bf16_t* V, int KR, int k0, in
 
 #ifdef SBK_PROBE_TL
 __device__ unsigned long long g_att_tl[4][64];
+__device__ unsigned long long g_att_wg[4096][4];  // per workgroup: memtime / memrealtime at start and end, HW_ID
 #define ATT_TL(i)                                                                        \
   do {                                                                                   \
     if (tl_on && lane == 0 && (i) < 64) g_att_tl[w][i] = __builtin_amdgcn_s_memtime(); \
@@ -484,17 +485,34 @@ __global__ void __launch_bounds__(256, SBK_ATT_MINW) relpos_flash_kernel(const T
 // to a query-major scratch with the rel_shift applied on the write (row R of
 // query ii lands at position R - (15 - ii); the first / last tile's positions
 // outside the chunk's 64 keys clamp onto two spare slots), so the scores are
-// four aligned 16-B reads, and the key mask is added unconditionally.  Row
-// max / sum: permlane half-swaps.  Two barriers per chunk:
+// four aligned 16-B reads.  Key padding: a 64-bit bitmap of the chunks that
+// hold a padded key is built once per workgroup; only those chunks (and the
+// last, for keys past Tn) apply a mask, so no wave writes a per-chunk mask row
+// the others wait for.  Row max / sum: permlane half-swaps.  Two barriers per
+// chunk:
 //   A  this chunk's K / band landed in every wave and every wave is past the
-//      previous chunk's P·V  -> key mask, then issue this chunk's V;
+//      previous chunk's P·V  -> issue this chunk's V;
 //   B  V landed and every wave's S / G fragment reads are done -> read the
-//      scratch and the mask, then issue the next chunk's K / band, which land
-//      under the softmax and P·V.
+//      scratch, then issue the next chunk's K / band, which land under the
+//      softmax and P·V.
+// Measured (s_memtime / s_memrealtime per workgroup, B = 32, T = 376,
+// profiles/r02_att_dma_timeline.log): all 768 workgroups start within 1 us
+// (one round, three per CU); a CU's three finish in turn at ~12.5 / 15.3 /
+// 17.5 us (oldest-first issue), i.e. the CU is issue / LDS bound, not waiting
+// on memory.  Tried and slower: six waves x 16 queries per workgroup with
+// double-buffered V and two workgroups per CU (27.5 us: the waves of a second
+// workgroup do not always fit beside the first).
 // The tiles are distinct __shared__ objects and the other LDS accesses come
 // before a DMA is issued, so the compiler's LDS-DMA alias guard (a vmcnt wait
 // before an LDS access it cannot tell apart from a DMA in flight) has little
-// to wait for.  50.3 KB of LDS and <= 168 VGPRs: three workgroups per CU.
+// to wait for.  50 KB of LDS and <= 168 VGPRs: three workgroups per CU.
+#ifdef SBK_PROBE_PRIO
+#define SBK_ATT_PRIO(p) __builtin_amdgcn_s_setprio(p)
+#else
+#define SBK_ATT_PRIO(p) \
+  do {                  \
+  } while (0)
+#endif
 namespace dmak {
 constexpr int RB = 64;   // bf16 per staged row (dh = 64): 128 B
 constexpr int PB = 128;  // band rows staged per chunk (127 used)
@@ -555,7 +573,7 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
   __shared__ __attribute__((aligned(16))) bf16_t Ps[PB * RB];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[KC * RB];
   __shared__ __attribute__((aligned(16))) float Gs[4 * 16 * G2];
-  __shared__ __attribute__((aligned(16))) float Ms[KC + 4];  // key mask + 'chunk has a masked key' flag
+  __shared__ unsigned long long Mb[4];  // per-wave partial bitmaps of the chunks holding a padded key
 
   const int d_model = H * dh;
   const long long row3 = 3LL * d_model;
@@ -630,13 +648,35 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
       dma16(qkv_b + (long long)min(j0 + row, Tn - 1) * row3 + 2 * dh + ((lchk ^ swz_v(row)) << 3), Vs + r0 * RB);
     }
   };
-  // padding byte of key j0 + lane, fetched a chunk ahead and only compared
-  // when Ms is written (a compare right after the load waited for it)
-  auto key_byte = [&](int j0) -> int { return kpm ? (int)kpm[(long long)b * Tn + min(j0 + lane, Tn - 1)] : 0; };
-
   ATT_TL(0);
+#ifdef SBK_PROBE_TL
+  if (tid == 0 && orig < 4096) {
+    g_att_wg[orig][0] = __builtin_amdgcn_s_memrealtime();
+    g_att_wg[orig][2] = __builtin_amdgcn_s_memtime();
+  }
+#endif
   dma_kp(0);
-  int rm = w == 0 ? key_byte(0) : 0;
+  const int nchunk = (Tn + KC - 1) / KC;  // <= 64 (launcher)
+  // Key padding: which chunks hold a padded key, as a 64-bit chunk bitmap
+  // built once (wave w scans chunks w, w + 4, ...; merged after barrier A of
+  // chunk 0).  Chunks without one add no mask at all; keys past Tn are masked
+  // arithmetically in the last chunk.  (A per-chunk mask row written by one
+  // wave made the other three wait for it at every barrier.)
+  {
+    unsigned long long bits = 0;
+    if (kpm) {
+      const uint8_t* kb = kpm + (long long)b * Tn;
+      for (int c0 = w; c0 < nchunk; c0 += 8) {
+        const int c1 = c0 + 4, ja = c0 * KC + lane, jb = c1 * KC + lane;
+        const int ma = kb[min(ja, Tn - 1)];
+        const int mb = c1 < nchunk ? (int)kb[min(jb, Tn - 1)] : 0;
+        if (__ballot(ja < Tn && ma != 0)) bits |= 1ull << c0;
+        if (__ballot(jb < Tn && mb != 0)) bits |= 1ull << c1;
+      }
+    }
+    if (lane == 0) Mb[w] = bits;
+  }
+  uint32_t mlo = 0, mhi = 0;  // the merged bitmap (wave-uniform)
 
   // Qu / Qv B-operand fragments, pre-scaled into the exp2 domain
   const float qscale = scale * 1.4426950408889634f;
@@ -668,19 +708,16 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
   f32x4 acc_o[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc_o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nchunk = (Tn + KC - 1) / KC;
   const int pofs = 48 - 16 * w;
   for (int ch = 0; ch < nchunk; ++ch) {
     const int j0 = ch * KC;
     const bool more = ch + 1 < nchunk;
     dma_barrier();  // A
     ATT_TL(1 + 5 * ch);
-    if (w == 0) {  // key mask (0 / -inf); keys past Tn are masked, so the clamped rows staged for them never count
-      const bool mkd = !(j0 + lane < Tn && rm == 0);
-      Ms[lane] = mkd ? -INFINITY : 0.f;
-      const unsigned long long anym = __ballot(mkd);
-      if (lane == 0) Ms[KC] = anym ? 1.f : 0.f;
-      if (more) rm = key_byte(j0 + KC);
+    if (ch == 0) {
+      const unsigned long long m = Mb[0] | Mb[1] | Mb[2] | Mb[3];
+      mlo = __builtin_amdgcn_readfirstlane((uint32_t)m);
+      mhi = __builtin_amdgcn_readfirstlane((uint32_t)(m >> 32));
     }
     __builtin_amdgcn_sched_barrier(0);
     dma_v(j0);
@@ -704,10 +741,12 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
         const int row = pofs + 16 * t + c16;
         fpb[t] = *reinterpret_cast<const bf16x8*>(Ps + row * RB + (((4 * s + g) ^ swz_kp(row)) << 3));
       }
+      SBK_ATT_PRIO(1);
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc_s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fk[t], fqu[s], acc_s[t], 0, 0, 0);
 #pragma unroll
       for (int t = 0; t < 5; ++t) acc_g[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fpb[t], fqv[s], acc_g[t], 0, 0, 0);
+      SBK_ATT_PRIO(0);
     }
     // rel_shift on the write: row R = 16t + 4g + r -> position R - (15 - c16)
 #pragma unroll
@@ -727,8 +766,7 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
     f32x4 gv[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) gv[t] = *reinterpret_cast<const f32x4*>(gq + 16 * t + 4 * g);
-    // the mask is added only in chunks that hold a masked key (uniform branch)
-    const bool chunk_masked = __builtin_amdgcn_readfirstlane(__float_as_uint(Ms[KC])) != 0u;
+    const bool chunk_padded = ((ch < 32 ? mlo >> ch : mhi >> (ch - 32)) & 1u) != 0u;
     __builtin_amdgcn_sched_barrier(0);
     if (more) dma_kp(j0 + KC);
     float p[4][4];
@@ -737,13 +775,20 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) p[t][r] = acc_s[t][r] + gv[t][r];
-    if (chunk_masked) {
+    if (chunk_padded) {  // uniform branch, only in chunks holding a padded key
+      const uint8_t* kb = kpm + (long long)b * Tn;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const f32x4 mk = *reinterpret_cast<const f32x4*>(Ms + 16 * t + 4 * g);
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) p[t][r] += mk[r];
-      }
+        for (int r = 0; r < 4; ++r)
+          if (kb[min(j0 + 16 * t + 4 * g + r, Tn - 1)]) p[t][r] = -INFINITY;
+    }
+    if (j0 + KC > Tn) {  // last chunk: keys past Tn (their staged rows are clamped copies)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (j0 + 16 * t + 4 * g + r >= Tn) p[t][r] = -INFINITY;
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -776,9 +821,11 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
         pv[4 + r] = p[2 * s2 + 1][r];
       }
       const bf16x8 fp = MT<bf16_t>::from8(pv);
+      SBK_ATT_PRIO(1);
 #pragma unroll
       for (int t = 0; t < 4; ++t)
         acc_o[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt_frag_swz(Vs, 32 * s2, 16 * t, lane), fp, acc_o[t], 0, 0, 0);
+      SBK_ATT_PRIO(0);
     }
     ATT_TL(5 + 5 * ch);
   }
@@ -794,6 +841,13 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
     }
   }
   ATT_TL(62);
+#ifdef SBK_PROBE_TL
+  __syncthreads();
+  if (tid == 0 && orig < 4096) {
+    g_att_wg[orig][1] = __builtin_amdgcn_s_memrealtime();
+    g_att_wg[orig][3] = __builtin_amdgcn_s_memtime();
+  }
+#endif
 }
 
 int launch_dma(const void* qkv, const void* pk, int ldp, const float* pbu, const float* pbv, const uint8_t* kpm, int B,
@@ -839,7 +893,7 @@ SBK_API int sbk_relpos_attention_ld(int dtype_bf16, const void* qkv, const void*
   if (B <= 0 || Tn <= 0 || H <= 0 || dh <= 0 || dh > 128 || ldp < H * dh) return SBK_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   // the encoder's inference path: bf16, dh = 64, no probabilities
-  if (dtype_bf16 && dh == 64 && !probs && ldp % 8 == 0 &&
+  if (dtype_bf16 && dh == 64 && !probs && ldp % 8 == 0 && Tn <= 64 * 64 &&
       ((reinterpret_cast<uintptr_t>(qkv) | reinterpret_cast<uintptr_t>(pk) | reinterpret_cast<uintptr_t>(out)) % 16) == 0)
     return launch_dma(qkv, pk, ldp, pbu, pbv, kpm, B, Tn, H, scale, out, s);
   if (dtype_bf16)
@@ -858,6 +912,9 @@ SBK_API int sbk_relpos_attention(int dtype_bf16, const void* qkv, const void* pk
 #ifdef SBK_PROBE_TL
 SBK_API int sbk_probe_att_tl(unsigned long long* out) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_att_tl), sizeof(g_att_tl), 0, hipMemcpyDeviceToHost);
+}
+SBK_API int sbk_probe_att_wg(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_att_wg), sizeof(g_att_wg), 0, hipMemcpyDeviceToHost);
 }
 #endif
 
