@@ -506,13 +506,6 @@ __global__ void __launch_bounds__(256, SBK_ATT_MINW) relpos_flash_kernel(const T
 // before a DMA is issued, so the compiler's LDS-DMA alias guard (a vmcnt wait
 // before an LDS access it cannot tell apart from a DMA in flight) has little
 // to wait for.  50 KB of LDS and <= 168 VGPRs: three workgroups per CU.
-#ifdef SBK_PROBE_PRIO
-#define SBK_ATT_PRIO(p) __builtin_amdgcn_s_setprio(p)
-#else
-#define SBK_ATT_PRIO(p) \
-  do {                  \
-  } while (0)
-#endif
 namespace dmak {
 constexpr int RB = 64;   // bf16 per staged row (dh = 64): 128 B
 constexpr int PB = 128;  // band rows staged per chunk (127 used)
@@ -741,12 +734,10 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
         const int row = pofs + 16 * t + c16;
         fpb[t] = *reinterpret_cast<const bf16x8*>(Ps + row * RB + (((4 * s + g) ^ swz_kp(row)) << 3));
       }
-      SBK_ATT_PRIO(1);
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc_s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fk[t], fqu[s], acc_s[t], 0, 0, 0);
 #pragma unroll
       for (int t = 0; t < 5; ++t) acc_g[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fpb[t], fqv[s], acc_g[t], 0, 0, 0);
-      SBK_ATT_PRIO(0);
     }
     // rel_shift on the write: row R = 16t + 4g + r -> position R - (15 - c16)
 #pragma unroll
@@ -821,11 +812,9 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
         pv[4 + r] = p[2 * s2 + 1][r];
       }
       const bf16x8 fp = MT<bf16_t>::from8(pv);
-      SBK_ATT_PRIO(1);
 #pragma unroll
       for (int t = 0; t < 4; ++t)
         acc_o[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt_frag_swz(Vs, 32 * s2, 16 * t, lane), fp, acc_o[t], 0, 0, 0);
-      SBK_ATT_PRIO(0);
     }
     ATT_TL(5 + 5 * ch);
   }
