@@ -1,5 +1,5 @@
 import os, sys, torch
-sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import speechbrain_amd._lib as _L
 if os.environ.get("SBK_PROBE_LIB"):
     _L.LIB_PATH = os.path.abspath(os.environ["SBK_PROBE_LIB"])
