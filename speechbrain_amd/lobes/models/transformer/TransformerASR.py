@@ -132,6 +132,6 @@ class TransformerASR(nn.Module):
             return y.view(B, T, -1)
         a = _enc.to_compute(src.reshape(B * T, Fin), dtype)
         x = _enc.gemm(a, lin.kernel_weight(dtype), bias=lin.w.bias.detach(), out_dtype=_f32)
-        pos = self.positional_encoding.table(T, src.device, _f32)
+        pos = self.positional_encoding.table(T, src.device, dtype)  # a constant table: cached in the compute dtype
         y, _ = self.encoder.run(x, B, T, pos, kpm, dtype, False)
         return y.view(B, T, -1)

@@ -20,8 +20,9 @@ __all__ = ["RelPosEncXL", "RelPosMHAXL", "PositionalwiseFeedForward", "Multihead
 
 class RelPosEncXL(nn.Module):
     """attention.py:312-359.  The (1, 2T-1, d) table depends only on T and d;
-    it is built once per (T, device) on the host from the registered
-    inv_freq buffer and cached."""
+    it is built once per (T, device, dtype) on the host from the registered
+    inv_freq buffer and cached (the bf16 encoder path takes the bf16 table, so
+    no step casts it)."""
 
     def __init__(self, emb_dim):
         super().__init__()
@@ -41,8 +42,10 @@ class RelPosEncXL(nn.Module):
             pe_half[:, 0::2] = torch.sin(pos * inv)
             pe_half[:, 1::2] = torch.cos(pos * inv)  # cos(-x) == cos(x): past/future equal
             pe = torch.cat([torch.flip(pe_half, (0,)), pe_half[1:]], dim=0).unsqueeze(0)
-            pe = pe.to(device=device, dtype=dtype)
-            self._cache = {key: pe}
+            pe = pe.to(device=device, dtype=dtype)  # bf16: round-to-nearest-even, as the cast kernel
+            if len(self._cache) >= 8:
+                self._cache.clear()
+            self._cache[key] = pe
         return pe
 
     def forward(self, x: torch.Tensor):
