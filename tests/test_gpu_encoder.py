@@ -294,12 +294,13 @@ def _relpos_ref(qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale):
 
 @pytest.mark.parametrize("T,lens,strided", [(37, [37, 30, 21], False), (97, [97, 60, 5], True),
                                             (376, [376, 376, 200, 1], True), (640, [640, 640], False),
-                                            (256, None, True)])
+                                            (256, None, True), (2200, [2200, 2100], False)])
 def test_relpos_attention_bf16_vs_torch(dev, T, lens, strided):
     """The encoder's attention path (bf16, dh = 64, no probabilities: the
     LDS-DMA kernel) vs an fp32 torch evaluation on the same bf16 operands:
     ragged key-padding masks incl. a 1-key utterance, and the strided p_k slice
-    the encoder passes (one stacked linear_pos GEMM).  P is rounded to bf16 for
+    the encoder passes (one stacked linear_pos GEMM); T = 2200 puts padded keys in
+    chunks 32-34 (the high word of the kernel's chunk bitmap).  P is rounded to bf16 for
     the P·V MFMA, so outputs (~N(0,1) averages) agree to 2e-2."""
     from speechbrain_amd import _enc
     g = torch.Generator().manual_seed(T)
