@@ -363,3 +363,60 @@ def test_relpos_attention_bwd_bf16_sbk_vs_library(dev, T, lens):
         e = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
         print(f"{name}: {e:.2e}")
         assert e <= 2e-2, (name, e)
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_full_size_encoder_grads_vs_oracle(dev, bf16):
+    """Config-4 encoder at full size (ConvolutionFrontEnd(64, 32) + 12-layer
+    Conformer, d = 256, 2 x 15 s, one utterance at 80 % length, dropout off):
+    every parameter gradient of the HIP training path against autograd of the
+    fp32 oracle on the same weights and features (TransformerASR.py:279-316,
+    Conformer.py:157-383 backward).  fp32: relative L2 error <= 2e-3 per tensor
+    (measured on MI355X: <= 1.5e-4 for every encoder parameter, <= 8.7e-4 for
+    the ConvBlock parameters, whose gradients sum ~60k cancelling
+    position terms per weight); bf16 autocast: cosine >= 0.99 per tensor
+    (measured >= 0.9988, the positional-bias gradients lowest)."""
+    from speechbrain_amd.lobes.features import Fbank
+    from speechbrain_amd.lobes.models.convolution import ConvolutionFrontEnd
+    from speechbrain_amd.lobes.models.transformer.TransformerASR import TransformerASR
+    torch.manual_seed(0)
+    cnn = ConvolutionFrontEnd(input_shape=(8, 10, 80), num_blocks=2, num_layers_per_block=1, out_channels=(64, 32),
+                              kernel_sizes=(3, 3), strides=(2, 2), residuals=(False, False)).to(dev).train()
+    tr = TransformerASR(tgt_vocab=100, input_size=640, d_model=256, nhead=4, num_encoder_layers=12,
+                        num_decoder_layers=0, d_ffn=1024, dropout=0.0, encoder_module="conformer",
+                        attention_type="RelPosMHAXL", normalize_before=True, causal=False).to(dev).train()
+    for mod in list(cnn.modules()) + list(tr.modules()):
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    g = torch.Generator().manual_seed(11)
+    wav = 0.1 * torch.randn(2, 240000, generator=g)
+    lens = torch.tensor([1.0, 0.8])
+    feats = Fbank(n_mels=80)(wav.to(dev)).detach()
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf16):
+        y = tr.encode(cnn(feats), lens.to(dev))
+    R = torch.randn(y.shape, generator=torch.Generator().manual_seed(7))
+    (y.float() * R.to(dev)).sum().backward()
+    sd_c = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in cnn.state_dict().items()}
+    sd_t = {k: v.detach().cpu().clone().requires_grad_(v.is_floating_point()) for k, v in tr.state_dict().items()}
+    yr = OC.transformer_asr_encode(OC.conv_frontend(feats.cpu(), sd_c), sd_t, "", 12, 4, lens)
+    (yr * R).sum().backward()
+    rows = []
+    for mod, sd in ((cnn, sd_c), (tr, sd_t)):
+        for k, p in mod.named_parameters():
+            ref_g = sd[k].grad
+            if ref_g is None:
+                continue
+            assert p.grad is not None, f"{k}: no gradient on the HIP path"
+            a, b = p.grad.detach().float().cpu(), ref_g.float()
+            rel = (a - b).abs().max().item() / max(b.abs().max().item(), 1e-12)
+            l2 = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+            rows.append((k, rel, l2, cosine(a, b)))
+    assert len(rows) > 12 * 20
+    for k, rel, l2, c in sorted(rows, key=lambda r: -r[1])[:8]:
+        print(f"{k}: max-norm rel {rel:.2e}, l2 rel {l2:.2e}, cosine {c:.6f}")
+    if bf16:
+        worst = min(rows, key=lambda r: r[3])
+        assert worst[3] >= 0.99, f"{worst[0]}: bf16 gradient cosine {worst[3]:.4f}"
+    else:
+        worst = max(rows, key=lambda r: r[2])
+        assert worst[2] <= 2e-3, f"{worst[0]}: fp32 gradient l2 rel error {worst[2]:.2e}"
