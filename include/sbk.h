@@ -293,7 +293,9 @@ int sbk_relpos_attention(int dtype_bf16, const void* qkv, const void* pk, const 
 
 /* Same with the positional rows at row stride ldp (>= d): the p_k of every layer
  * can come from ONE linear_pos GEMM over the stacked weights, (2T-1, L*d), layer l
- * at column offset l*d. */
+ * at column offset l*d.  bf16, dh == 64, no probs, ldp % 8 == 0, 16-B aligned
+ * operands and T <= 4096 take the LDS-DMA kernel (key padding as a per-workgroup
+ * chunk bitmap); every other case takes the general kernel.  Same results. */
 int sbk_relpos_attention_ld(int dtype_bf16, const void* qkv, const void* pk, int ldp, const float* pbu,
                             const float* pbv, const unsigned char* kpm, int B, int T, int H, int dh, float scale,
                             void* out, float* probs, void* stream);
