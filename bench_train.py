@@ -194,7 +194,8 @@ def main():
             "vs_baseline": None, "dtype": "fp32" if args.fp32 else "bf16", "data": "synthetic",
             "config": {"workload": f"C4: Fbank→InputNorm→SpecAugment→CNN→Conformer {args.layers}L d=256 → TN/PN → sum joint "
                                    f"LeakyReLU → Linear(1024→1000) → RNN-T; Adam; clip 5.0",
-                       "transducer_head": args.head,
+                       # without autocast the fused head runs the fp32 materialised chain
+                       "transducer_head": "materialised (fp32)" if args.fp32 else args.head,
                        "global_batch": world * args.batch, "seq_len": T_e, "U_max": 64, "vocab": V,
                        "parallelism": f"ddp{world}"},
             "step_algorithmic_tflop": round(fl / 1e12, 3),

@@ -190,11 +190,15 @@ int sbk_gemm_ln(int dtype_bf16, const void* A, int lda, const void* W, int ldw, 
 /* 1 if the fused FFN kernel supports d_model D and d_ffn H (D == 256, H % 256 == 0, H <= 2048). */
 int sbk_ffn_supported(int D, int H);
 
-/* Batched C[b] = A[b] W[b]^T (bf16, K-contiguous rows; fp32 or bf16 out),
- * element strides sA / sW / sC per batch: the per-(utterance, head) products
- * of the rel-pos attention backward. */
-int sbk_gemm_batched(const void* A, int lda, long long sA, const void* W, int ldw, long long sW, int M, int N, int K,
-                     int batch, void* out, int ldc, long long sC, int out_bf16, void* stream);
+/* Batched C[z] = A[z] W[z]^T (bf16 (dtype_bf16) or fp32 operands, K-contiguous
+ * rows; fp32 or bf16 out), element strides sA / sW per batch; batch z is
+ * stored at (z / zdiv) * sCo + (z % zdiv) * sC when zdiv > 0, else at z * sC.
+ * The per-(utterance, head) products of the rel-pos attention backward and
+ * the dropout product drop(P) V (attention.py:626-633), written straight
+ * into the (B*T, H*dh) layout with zdiv = H. */
+int sbk_gemm_batched(int dtype_bf16, const void* A, int lda, long long sA, const void* W, int ldw, long long sW, int M,
+                     int N, int K, int batch, void* out, int ldc, long long sC, int zdiv, long long sCo, int out_bf16,
+                     void* stream);
 
 /* Weight-gradient GEMM (bf16 MFMA): C[b] += A[b]^T B[b], A (K, M) and B
  * (K, N) row-major with row strides lda / ldb (the token rows of dY and X:
@@ -206,6 +210,12 @@ int sbk_gemm_tn(const void* A, long long lda, long long sA, const void* B, long 
 /* sbk_gemm_tn with an explicit tile (64 / 128; 0 = auto) and token-range split count (0 = auto). */
 int sbk_gemm_tn_cfg(const void* A, long long lda, long long sA, const void* B, long long ldb, long long sB, int M,
                     int N, int K, int batch, float* C, long long ldc, long long sC, int tile, int nsplit, void* stream);
+/* Exact-fp32 weight-gradient GEMM (v_mfma_f32_16x16x4_f32): arguments as
+ * sbk_gemm_tn_cfg with fp32 A, B and tile 64; any M, N, lda, ldb (element-wise
+ * loads when not 16-B aligned); nsplit 0 = choose, 1 = deterministic.  The
+ * fp32 (parity) training path. */
+int sbk_gemm_tn_f32(const float* A, long long lda, long long sA, const float* B, long long ldb, long long sB, int M,
+                    int N, int K, int batch, float* C, long long ldc, long long sC, int nsplit, void* stream);
 
 /* Fused macaron feed-forward block, bf16 MFMA (Conformer.py:239-260 with
  * attention.py:823-839):
@@ -342,8 +352,8 @@ int sbk_inorm_apply(const float* x, int B, int T, int F, const float* mean, cons
 /* ------------------------------------------------------------ training path
  * Backward of the Conformer-Transducer encoder (csrc/backward.hip).  The
  * dense contractions of the backward (dX = dY W, dW = dY^T X, attention's
- * batched products) are plain library GEMMs; these entry points are the
- * element-wise / reduction / layout parts.  *_bf16 flags select bf16 (1)
+ * batched products) run on sbk_gemm / sbk_gemm_tn{,_f32} / sbk_gemm_batched;
+ * these entry points are the element-wise / reduction / layout parts.  *_bf16 flags select bf16 (1)
  * or fp32 (0) storage per operand. */
 
 /* LayerNorm backward over rows of x (M, D) fp32, D <= 2560 (nn.LayerNorm as
@@ -389,26 +399,32 @@ int sbk_dwconv_wgrad_chunks(int B, int T);
 int sbk_dwconv_bwd(const void* x, int x_bf16, const float* dy, int B, int T, int C, const float* w, int K, int causal,
                    void* dx, int dx_bf16, float* part, void* stream);
 
-/* RelPosMHAXL softmax backward (attention.py:594-631): P (B, H, T, T) fp32
- * probabilities, dP = dO V^T; dS = scale * P (dP - rowsum(P dP)) (B, H, T, T)
- * and its pre-rel_shift image dBD (B, H, T, 2T-1) with dBD[i, T-1-i+j] = dS[i, j]
- * (rel_shift :468-483 transposed), zero outside the band. */
-int sbk_relpos_softmax_bwd(const float* P, const void* dP, int dP_bf16, int B, int H, int T, float scale, void* dS,
-                           void* dBD, int out_bf16, void* stream);
-/* As sbk_relpos_softmax_bwd with dBD head-major (H, B, T, Wp), Wp = 2T-1
- * rounded up to 8 with zero pad columns: each head's rows over all
- * utterances form one 16-B-aligned operand of the dp_k weight gradient. */
-int sbk_relpos_softmax_bwd_hm(const float* P, const void* dP, int dP_bf16, int B, int H, int T, float scale,
-                              void* dS, void* dBD, int out_bf16, void* stream);
-/* Rel-pos attention backward: dqkv (B*T, H*3*dh) in the in_proj layout (b, t, h, {q,k,v}, d) from
- * dq_ac, dk, dv (B*H, T, dh) and the head-major dq_bd (H, B*T, dh), all fp32: dq = dq_ac + dq_bd.
- * out fp32 or bf16; dh % 4 == 0, 16-B aligned pointers. */
+/* RelPosMHAXL backward (attention.py:566-633 differentiated).  Every
+ * per-(b, h) operand is stored over Tp >= T rows (T rounded up to 8) and
+ * dhp >= dh columns, zero-filled, so the MFMA GEMMs' 16-B rows hold for any
+ * T and head size; bf16 (dtype_bf16) or fp32 storage.
+ *   sbk_attn_prep: qu = q + pos_bias_u, v, doh (B*H, Tp, dhp); kT, vT
+ *     (B*H, dhp, Tp); qv = q + pos_bias_v head-major (H, B*T, dhp); pkT
+ *     (H, dhp, Wp) from pk (2T-1, ldp), Wp >= 2T-1.  Outputs nullable.
+ *   sbk_attn_probs_pad (forward dropout, :626): attn = D P (fp32 (B*H, T, T),
+ *     nullable) and Pd = D P over (B*H, Tp, Tp), D = keep / (1 - p) from the
+ *     sbk_dropout_add hash of (seed, index into P).
+ *   sbk_relpos_softmax_bwd_pad: P (B*H, T, T) fp32, dP = dO V^T (B*H, Tp, Tp):
+ *     Pd = D P, dS = scale * P (D dP - rowsum(P D dP)) (B*H, Tp, Tp) and the
+ *     pre-rel_shift image dBD (H, B*T, Wp) with dBD[i, T-1-i+j] = dS[i, j]
+ *     (:468-483 transposed), zero elsewhere.
+ *   sbk_attn_dqkv: dqkv (B*T, H*3*dh) in the in_proj layout from dq_ac, dk,
+ *     dv (B*H, Tp, dhp) and dq_bd (H, B*T, dhp), fp32 in; dq = dq_ac + dq_bd. */
+int sbk_attn_prep(int dtype_bf16, const void* qkv, const void* dO, const void* pk, int ldp, const float* pbu,
+                  const float* pbv, int B, int H, int T, int dh, int Tp, int dhp, int Wp, void* qu, void* qv, void* kT,
+                  void* v, void* vT, void* doh, void* pkT, void* stream);
+int sbk_attn_probs_pad(const float* P, int BH, int T, int Tp, float p, unsigned long long seed, float* attn, void* Pd,
+                       int pd_bf16, void* stream);
+int sbk_relpos_softmax_bwd_pad(int dtype_bf16, const float* P, const void* dP, int B, int H, int T, int Tp, int Wp,
+                               float scale, float p, unsigned long long seed, void* dS, void* Pd, void* dBD,
+                               void* stream);
 int sbk_attn_dqkv(const float* dq_ac, const float* dq_bd, const float* dk, const float* dv, int B, int H, int T,
-                  int dh, void* out, int out_bf16, void* stream);
-/* Rel-pos attention backward operands in one pass: qu = q + bf16(pbu), v, dO as (B*H, T, dh), kT (B*H, dh, T),
- * qv = q + bf16(pbv) head-major (H, B*T, dh); qkv (B*T, H*3*dh), dO (B*T, H*dh), outputs bf16. */
-int sbk_attn_bwd_prep(const void* qkv, const void* dO, const float* pbu, const float* pbv, int B, int H, int T,
-                      int dh, void* qu, void* qv, void* kT, void* v, void* doh, void* stream);
+                  int dh, int Tp, int dhp, void* out, int out_bf16, void* stream);
 
 /* Conv2d 3x3 stride 2 "same" reflect padding (CNN.py:616-700) as a GEMM:
  * x (B, Ti, Fi, Ci) -> col (B*To*Fo, ldcol >= 9*Ci), columns ordered (kt, kf, ci),

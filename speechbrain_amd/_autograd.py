@@ -7,8 +7,10 @@ needed the modules run this chain instead: every forward op is still a
 libsbk.so HIP kernel (MFMA GEMM, rel-pos attention, LayerNorm, activations,
 depthwise conv, im2col), and each ``backward`` pairs HIP kernels
 (csrc/backward.hip: LayerNorm / activation / depthwise-conv / softmax
-backward, col2im, joint reductions) with plain library GEMMs (torch.mm →
-hipBLASLt) for the dense dX = dY·W and dW = dYᵀ·X contractions.
+backward, col2im, joint reductions) with the MFMA GEMMs for the dense
+contractions: dX = dY·W on sbk_gemm, dW = dYᵀ·X on sbk_gemm_tn (bf16) /
+sbk_gemm_tn_f32 (fp32), the attention products on sbk_gemm_batched.  No
+library GEMM runs in either dtype.
 
 Numerics follow torch.autocast: under bf16 the GEMM operands and the
 activations saved for them are bf16, reductions, LayerNorm statistics and the
@@ -79,27 +81,20 @@ def colsum(part, rows, cols):
 # ------------------------------------------------------- dropout / residual
 def wgrad(g, a):
     """dW = g^T a in fp32 for g (M, N), a (M, K) — the weight gradient of a
-    Linear.  bf16: sbk_gemm_tn.  fp32 (the parity mode): for the tall-skinny case (M >> N, K: M = B*T rows, N, K <= 1024)
-    one library GEMM has too few output tiles to fill 256 CUs, so the
-    reduction over M is split into S batched GEMMs (fp32 outputs) summed in
-    a fixed order."""
+    Linear — on the token-major weight-gradient GEMM: sbk_gemm_tn for bf16
+    (16-B rows: N, K padded to multiples of 8 when they are not), the
+    exact-f32 sbk_gemm_tn_f32 for fp32 (any shape)."""
     M, N = g.shape
     K = a.shape[1]
-    if (g.dtype == _bf16 and a.dtype == _bf16 and N % 8 == 0 and K % 8 == 0 and g.stride(0) % 8 == 0
-            and a.stride(0) % 8 == 0 and (g.data_ptr() | a.data_ptr()) % 16 == 0):
-        # bf16 training path: the token-major weight-gradient MFMA kernel
+    if g.dtype == _bf16:
+        a = a if a.dtype == _bf16 else _as(a, _bf16)
+        if (N % 8 or K % 8 or g.stride(0) % 8 or a.stride(0) % 8 or (g.data_ptr() | a.data_ptr()) % 16
+                or g.stride(1) != 1 or a.stride(1) != 1):
+            gp = torch.nn.functional.pad(g, (0, -N % 8))
+            ap = torch.nn.functional.pad(a, (0, -K % 8))
+            return _enc.gemm_tn(gp, ap)[:N, :K]
         return _enc.gemm_tn(g, a)
-    S = 1
-    while S < 16 and M // (2 * S) >= 1024 and (N // 64) * (K // 64) * S < 1024:
-        S *= 2
-    kw = {"out_dtype": _f32} if g.dtype == _bf16 else {}
-    if S == 1:
-        return torch.mm(g.t(), a, **kw)
-    m = M // S
-    head = torch.bmm(g[: S * m].view(S, m, N).transpose(1, 2), a[: S * m].view(S, m, K), **kw).sum(0)
-    if S * m < M:
-        head += torch.mm(g[S * m:].t(), a[S * m:], **kw)
-    return head
+    return _enc.gemm_tn(_cont(g), _cont(_as(a, _f32)))
 
 
 def dgrad(g, wk):
@@ -326,122 +321,88 @@ class DwConvFn(Function):
 
 
 # ------------------------------------------------------ rel-pos attention
-# bf16 backward on sbk_gemm_batched / sbk_gemm_tn (else: library matmuls)
-ATTN_BWD_SBK = True
+def _rup8(n):
+    return (n + 7) // 8 * 8
+
 
 class RelPosAttentionFn(Function):
-    """RelPosMHAXL core (attention.py:566-631, rel_shift :468-483).
-    qkv (B*T, 3d) head-interleaved, pk (2T-1, d), both in the compute dtype;
-    pbu / pbv the (dh, H) parameters (read as (H, dh), attention.py:584-590).
-    Returns (out (B*T, d), probs (B, H, T, T) fp32, no grad)."""
+    """RelPosMHAXL core (attention.py:566-633, rel_shift :468-483) with
+    attention dropout.  qkv (B*T, 3d) head-interleaved, pk (2T-1, d), both in
+    the compute dtype (bf16 or fp32); pbu / pbv the (dh, H) parameters (read
+    as (H, dh), attention.py:584-590).  Returns (out (B*T, d), attention
+    weights after dropout (B, H, T, T) fp32, no grad).
+
+    Forward: the fused attention kernel (probabilities kept); with dropout,
+    drop(P)·V on sbk_gemm_batched.  Backward: per-(b, h) products on
+    sbk_gemm_batched / sbk_gemm_tn{,_f32} around the softmax / dropout /
+    rel_shift backward kernel.  Every per-(b, h) operand is laid out over
+    T and dh rounded up to 8 (zero-filled), so any T and head size takes the
+    same kernels in both dtypes."""
 
     @staticmethod
     def forward(ctx, qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale, p=0.0):
         qkv, pk = _cont(qkv), _cont(pk)
+        dt = qkv.dtype
         o, P = _enc.relpos_attention(qkv, pk, pbu.detach(), pbv.detach(), kpm, B, T, H, dh, scale, need_probs=True)
         seed = 0
         attn = P
         if p > 0:
             # attention-probability dropout (attention.py:626): o = drop(P) V
             seed = new_seed()
-            attn = drop_add(P, None, 1.0, None, p, seed, _f32)
-            v = qkv.view(B, T, H, 3, dh)[:, :, :, 2].permute(0, 2, 1, 3)
-            if ATTN_BWD_SBK and qkv.dtype == _bf16 and dh % 8 == 0 and T % 8 == 0:
-                # drop(P) V on the batched MFMA GEMM (V^T as the K-contiguous operand)
-                vT = v.transpose(-1, -2).reshape(B * H, dh, T).contiguous()
-                o = _enc.gemm_batched(_as(attn, qkv.dtype).view(B * H, T, T), vT, out_dtype=qkv.dtype)
-                o = o.view(B, H, T, dh).permute(0, 2, 1, 3).reshape(B * T, H * dh)
-            else:
-                o = torch.matmul(_as(attn, qkv.dtype), v).permute(0, 2, 1, 3).reshape(B * T, H * dh)
-        ctx.save_for_backward(qkv, pk, pbu, pbv, P, attn)
+            Tp, dhp = _rup8(T), _rup8(dh)
+            L = lib()
+            s = stream_of(qkv)
+            attn = torch.empty_like(P)
+            Pd = torch.empty(B * H, Tp, Tp, device=qkv.device, dtype=dt)
+            check(L.sbk_attn_probs_pad(ptr(P), B * H, T, Tp, float(p), int(seed), ptr(attn), ptr(Pd), _bf(Pd), s),
+                  "sbk_attn_probs_pad")
+            vT = torch.empty(B * H, dhp, Tp, device=qkv.device, dtype=dt)
+            check(L.sbk_attn_prep(_bf(qkv), ptr(qkv), None, None, 0, None, None, B, H, T, dh, Tp, dhp, _rup8(2 * T - 1),
+                                  None, None, None, None, ptr(vT), None, None, s), "sbk_attn_prep")
+            o = _enc.gemm_batched(Pd, vT[:, :dh], out_dtype=dt, M=T, heads=H)   # (B*T, H*dh)
+        ctx.save_for_backward(qkv, pk, pbu, pbv, P)
         ctx.dims = (B, T, H, dh, scale, p, seed)
         ctx.mark_non_differentiable(attn)
         return o, attn
 
     @staticmethod
-    def backward(ctx, do, _dP_unused):
-        qkv, pk, pbu, pbv, P, attn = ctx.saved_tensors
-        B, T, H, dh, scale, p, seed = ctx.dims
-        dt = qkv.dtype
-        if ATTN_BWD_SBK and dt == _bf16 and dh % 8 == 0 and T % 8 == 0:
-            return RelPosAttentionFn._backward_sbk(ctx, do)
-        W = 2 * T - 1
-        q5 = qkv.view(B, T, H, 3, dh)
-        q = q5[:, :, :, 0].permute(0, 2, 1, 3)  # (B, H, T, dh) views
-        k = q5[:, :, :, 1].permute(0, 2, 1, 3)
-        v = q5[:, :, :, 2].permute(0, 2, 1, 3)
-        pkh = pk.view(W, H, dh).permute(1, 0, 2)  # (H, W, dh)
-        do_h = _as(do, dt).view(B, T, H, dh).permute(0, 2, 1, 3)
-        Pc = _enc.cast_bf16(attn) if dt == _bf16 else attn
-        dv = torch.matmul(Pc.transpose(-1, -2), do_h)  # (B, H, T, dh)
-        dP = torch.matmul(do_h, v.transpose(-1, -2))  # (B, H, T, T)
-        dP = _cont(dP)
-        if p > 0:
-            dP = drop_add(dP, None, 1.0, None, p, seed, dP.dtype)
-        dS = torch.empty(B, H, T, T, device=qkv.device, dtype=dt)
-        dBD = torch.empty(B, H, T, W, device=qkv.device, dtype=dt)
-        check(lib().sbk_relpos_softmax_bwd(ptr(P), ptr(dP), _bf(dP), B, H, T, float(scale), ptr(dS), ptr(dBD), _bf(dS),
-                                           stream_of(P)), "sbk_relpos_softmax_bwd")
-        u = pbu.detach().reshape(H, 1, dh).to(dt)
-        vb = pbv.detach().reshape(H, 1, dh).to(dt)
-        dq_ac = torch.matmul(dS, k)  # (B, H, T, dh)
-        dq_bd = torch.matmul(dBD, pkh.unsqueeze(0))  # (B, H, T, dh)
-        dk = torch.matmul(dS.transpose(-1, -2), q + u)
-        # dpk[h] = sum_b dBD[b, h]^T (q + v)[b, h]
-        qv = (q + vb).permute(1, 0, 2, 3).reshape(H, B * T, dh)
-        dBD_h = dBD.permute(1, 3, 0, 2).reshape(H, W, B * T)
-        dpk = torch.matmul(dBD_h, qv)  # (H, W, dh)
-        dq = dq_ac + dq_bd
-        dqkv = torch.stack([dq, dk, dv], dim=3)  # (B, H, T, 3, dh)
-        dqkv = dqkv.permute(0, 2, 1, 3, 4).reshape(B * T, 3 * H * dh)
-        dpk = dpk.permute(1, 0, 2).reshape(W, H * dh)
-        dpbu = dq_ac.float().sum(dim=(0, 2)).reshape(pbu.shape)
-        dpbv = dq_bd.float().sum(dim=(0, 2)).reshape(pbv.shape)
-        return dqkv, dpk, dpbu, dpbv, None, None, None, None, None, None, None
-
-
-    @staticmethod
-    def _backward_sbk(ctx, do):
-        """bf16 backward on the MFMA kernels: per (b, h) batched products
-        (sbk_gemm_batched, sbk_gemm_tn) around the softmax / rel_shift
-        backward (sbk_relpos_softmax_bwd_hm)."""
-        qkv, pk, pbu, pbv, P, attn = ctx.saved_tensors
+    def backward(ctx, do, _dattn_unused):
+        qkv, pk, pbu, pbv, P = ctx.saved_tensors
         B, T, H, dh, scale, p, seed = ctx.dims
         dt = qkv.dtype
         W = 2 * T - 1
+        Tp, dhp, Wp = _rup8(T), _rup8(dh), _rup8(W)
         BH = B * H
-        # per-(b, h) contiguous operands in one pass (sbk_attn_bwd_prep):
-        # q + u, v, dO (B*H, T, dh); K^T (B*H, dh, T); q + v head-major (H, B*T, dh)
-        mk = lambda *shape: torch.empty(*shape, device=qkv.device, dtype=dt)  # noqa: E731
-        qu, v, do_h, kT, qv = mk(BH, T, dh), mk(BH, T, dh), mk(BH, T, dh), mk(BH, dh, T), mk(H, B * T, dh)
-        do_c = _cont(_as(do, dt))
-        pbu_c, pbv_c = _cont(pbu.detach().float()), _cont(pbv.detach().float())
-        check(lib().sbk_attn_bwd_prep(ptr(qkv), ptr(do_c), ptr(pbu_c), ptr(pbv_c), B, H, T, dh, ptr(qu), ptr(qv),
-                                      ptr(kT), ptr(v), ptr(do_h), stream_of(qkv)), "sbk_attn_bwd_prep")
-        Pc = (_enc.cast_bf16(attn) if attn.dtype != dt else attn).view(BH, T, T)
-        dv = _enc.gemm_tn(Pc, do_h)                            # P^T dO   (BH, T, dh)
-        dP = _enc.gemm_batched(do_h, v, out_dtype=dt)           # dO V^T   (BH, T, T)
-        if p > 0:
-            dP = drop_add(dP, None, 1.0, None, p, seed, dP.dtype)
-        Wp = (W + 7) // 8 * 8
-        dS = torch.empty(BH, T, T, device=qkv.device, dtype=dt)
-        dBD = torch.empty(H, B * T, Wp, device=qkv.device, dtype=dt)  # head-major, zero-padded rows
-        check(lib().sbk_relpos_softmax_bwd_hm(ptr(P), ptr(dP), _bf(dP), B, H, T, float(scale), ptr(dS), ptr(dBD),
-                                              _bf(dS), stream_of(P)), "sbk_relpos_softmax_bwd_hm")
-        dq_ac = _enc.gemm_batched(dS, kT)                       # dS K     (BH, T, dh) fp32
-        pkT = torch.zeros(H, dh, Wp, device=qkv.device, dtype=dt)
-        pkT[:, :, :W] = pk.view(W, H, dh).permute(1, 2, 0)     # (H, dh, Wp)
-        dq_bd = _enc.gemm_batched(dBD, pkT)                     # dBD P_k  (H, B*T, dh) fp32
-        dpbv = rowsum_batched(dq_bd).reshape(pbv.shape)         # per head: sum over (b, t)
-        dk = _enc.gemm_tn(dS, qu)                               # dS^T (q + u)
-        dpk = _enc.gemm_tn(dBD, qv)[:, :W]                      # (H, W, dh)
-        # dq = dq_ac + dq_bd, stacked with dk, dv into the in_proj layout, cast: one pass
-        dqkv = torch.empty(B * T, 3 * H * dh, device=qkv.device, dtype=dt)
-        check(lib().sbk_attn_dqkv(ptr(dq_ac), ptr(dq_bd), ptr(dk), ptr(dv), B, H, T, dh, ptr(dqkv), _bf(dqkv),
-                                  stream_of(dq_ac)), "sbk_attn_dqkv")
-        dpk = dpk.permute(1, 0, 2).reshape(W, H * dh).to(dt)
-        # sum over (b, t): over b as rows (sbk_rowsum), then over t (H*T*dh values)
-        dpbu = rowsum_batched(rowsum(dq_ac.reshape(B, H * T * dh)).view(H, T, dh)).reshape(pbu.shape)
+        dev = qkv.device
+        L = lib()
+        s = stream_of(qkv)
+        mk = lambda *shape: torch.empty(*shape, device=dev, dtype=dt)  # noqa: E731
+        # per-(b, h) operands, zero-padded to (Tp, dhp), in one launch
+        qu, v, do_h, kT, qv, pkT = mk(BH, Tp, dhp), mk(BH, Tp, dhp), mk(BH, Tp, dhp), mk(BH, dhp, Tp), \
+            mk(H, B * T, dhp), mk(H, dhp, Wp)
+        do_c = _as(do, dt)
+        check(L.sbk_attn_prep(_bf(qkv), ptr(qkv), ptr(do_c), ptr(pk), pk.stride(0), ptr(_cont(pbu.detach().float())),
+                              ptr(_cont(pbv.detach().float())), B, H, T, dh, Tp, dhp, Wp, ptr(qu), ptr(qv), ptr(kT),
+                              ptr(v), None, ptr(do_h), ptr(pkT), s), "sbk_attn_prep")
+        dP = _enc.gemm_batched(do_h, v, out_dtype=dt)            # dO V^T  (BH, Tp, Tp)
+        dS, Pd = mk(BH, Tp, Tp), mk(BH, Tp, Tp)
+        dBD = mk(H, B * T, Wp)                                    # head-major, zero outside the band
+        check(L.sbk_relpos_softmax_bwd_pad(_bf(dP), ptr(P), ptr(dP), B, H, T, Tp, Wp, float(scale), float(p),
+                                           int(seed), ptr(dS), ptr(Pd), ptr(dBD), s), "sbk_relpos_softmax_bwd_pad")
+        dv = _enc.gemm_tn(Pd, do_h)                               # Pd^T dO  (BH, Tp, dhp)
+        dq_ac = _enc.gemm_batched(dS, kT)                         # dS K     (BH, Tp, dhp)
+        dq_bd = _enc.gemm_batched(dBD, pkT)                       # dBD P_k  (H, B*T, dhp)
+        dk = _enc.gemm_tn(dS, qu)                                 # dS^T (q + u)
+        dpk = torch.zeros(Wp, H * dhp, device=dev, dtype=_f32)    # dBD^T (q + v), head h at columns h*dhp
+        _enc.gemm_tn_into(dBD, qv, dpk, H * dhp, dhp)
+        dqkv = torch.empty(B * T, 3 * H * dh, device=dev, dtype=dt)
+        check(L.sbk_attn_dqkv(ptr(dq_ac), ptr(dq_bd), ptr(dk), ptr(dv), B, H, T, dh, Tp, dhp, ptr(dqkv), _bf(dqkv), s),
+              "sbk_attn_dqkv")
+        dpk = dpk[:W].view(W, H, dhp)[:, :, :dh].reshape(W, H * dh)
+        dpk = _as(dpk, dt)
+        # pos-bias gradients: sums of dq_ac / dq_bd over (b, t) (padded rows are zero)
+        dpbv = rowsum_batched(dq_bd)[:, :dh].reshape(pbv.shape)
+        dpbu = rowsum_batched(rowsum(dq_ac.view(B, H * Tp * dhp)).view(H, Tp, dhp))[:, :dh].reshape(pbu.shape)
         return dqkv, dpk, dpbu, dpbv, None, None, None, None, None, None, None
 
 

@@ -81,9 +81,22 @@ def _gemm_tn_op(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     out = torch.zeros(*([batch] if a.dim() == 3 else []), M, N, device=a.device, dtype=_f32)
     sa = a.stride(0) if a.dim() == 3 else 0
     sb = b.stride(0) if b.dim() == 3 else 0
-    check(lib().sbk_gemm_tn(ptr(a), a.stride(-2), sa, ptr(b), b.stride(-2), sb, M, N, K, batch, ptr(out), N,
-                            M * N if a.dim() == 3 else 0, stream_of(a)), "sbk_gemm_tn")
+    _tn_call(a, a.stride(-2), sa, b, b.stride(-2), sb, M, N, K, batch, out, N, M * N if a.dim() == 3 else 0)
     return out
+
+
+def _tn_call(a, lda, sa, b, ldb, sb, M, N, K, batch, out, ldc, sc):
+    """sbk_gemm_tn (bf16) / sbk_gemm_tn_f32; one token-range split (plain
+    stores, run-to-run identical) under torch.use_deterministic_algorithms."""
+    det = torch.are_deterministic_algorithms_enabled()
+    L = lib()
+    if a.dtype == _bf16:
+        rc = (L.sbk_gemm_tn_cfg(ptr(a), lda, sa, ptr(b), ldb, sb, M, N, K, batch, ptr(out), ldc, sc, 0, 1, stream_of(a))
+              if det else L.sbk_gemm_tn(ptr(a), lda, sa, ptr(b), ldb, sb, M, N, K, batch, ptr(out), ldc, sc, stream_of(a)))
+    else:
+        rc = L.sbk_gemm_tn_f32(ptr(a), lda, sa, ptr(b), ldb, sb, M, N, K, batch, ptr(out), ldc, sc, int(det),
+                               stream_of(a))
+    check(rc, "sbk_gemm_tn")
 
 
 @_gemm_tn_op.register_fake
@@ -92,41 +105,79 @@ def _(a, b):
 
 
 def gemm_tn(a, b):
-    """a^T @ b in fp32 for bf16 a (K, M), b (K, N) (or batched (Bt, K, *)):
-    the weight gradient dY^T X without transposing the token-major
-    operands.  Rows must be 16-B aligned and column-contiguous."""
+    """a^T @ b in fp32 for a (K, M), b (K, N) (or batched (Bt, K, *)), both
+    bf16 (sbk_gemm_tn: rows 16-B aligned, M, N % 8 == 0) or both fp32
+    (sbk_gemm_tn_f32, exact-f32 MFMA, any shape): the weight gradient dY^T X
+    without transposing the token-major operands.  Columns contiguous."""
     require_device(a, b)
-    if a.dtype != _bf16 or b.dtype != _bf16:
-        raise TypeError("gemm_tn takes bf16 operands")
+    if a.dtype != b.dtype or a.dtype not in (_bf16, _f32):
+        raise TypeError(f"gemm_tn takes two bf16 or two fp32 operands (got {a.dtype}, {b.dtype})")
     if a.stride(-1) != 1 or b.stride(-1) != 1:
         raise ValueError("gemm_tn operands must be column-contiguous")
     return torch.ops.sbk.gemm_tn(a, b)
 
 
+def gemm_tn_into(a, b, out, ldc, sC):
+    """out (fp32, caller-initialised) += a[z]^T b[z] with batch z of the
+    result at out + z * sC, rows ldc apart (e.g. per-head blocks of one
+    (rows, H*dh) matrix).  a (Bt, K, M), b (Bt, K, N), same dtype."""
+    require_device(a, b, out)
+    Bt, K, M = a.shape
+    N = b.shape[-1]
+    if a.dtype != b.dtype or out.dtype != _f32 or a.stride(-1) != 1 or b.stride(-1) != 1:
+        raise ValueError("gemm_tn_into: same-dtype column-contiguous operands, fp32 out")
+    if out.numel() < (Bt - 1) * sC + (M - 1) * ldc + N:
+        raise ValueError("gemm_tn_into: output too small")
+    _tn_call(a, a.stride(1), a.stride(0), b, b.stride(1), b.stride(0), M, N, K, Bt, out, ldc, sC)
+    return out
+
+
 @torch.library.custom_op("sbk::gemm_batched", mutates_args=())
-def _gemm_batched_op(a: torch.Tensor, w: torch.Tensor, out_bf16: bool) -> torch.Tensor:
-    Bt, M, K = a.shape
+def _gemm_batched_op(a: torch.Tensor, w: torch.Tensor, out_bf16: bool, M: int, zdiv: int, ldc: int, sC: int,
+                     sCo: int, rows: int) -> torch.Tensor:
+    Bt, _, K = a.shape
     N = w.shape[1]
-    out = torch.empty(Bt, M, N, device=a.device, dtype=_bf16 if out_bf16 else _f32)
-    check(lib().sbk_gemm_batched(ptr(a), a.stride(1), a.stride(0), ptr(w), w.stride(1), w.stride(0), M, N, K, Bt,
-                                 ptr(out), N, M * N, int(out_bf16), stream_of(a)), "sbk_gemm_batched")
+    if zdiv:
+        out = torch.empty(rows, ldc, device=a.device, dtype=_bf16 if out_bf16 else _f32)
+    else:
+        out = torch.empty(Bt, M, N, device=a.device, dtype=_bf16 if out_bf16 else _f32)
+        ldc, sC = N, M * N
+    check(lib().sbk_gemm_batched(int(_is_bf16(a)), ptr(a), a.stride(1), a.stride(0), ptr(w), w.stride(1), w.stride(0),
+                                 M, N, K, Bt, ptr(out), ldc, sC, zdiv, sCo, int(out_bf16), stream_of(a)),
+          "sbk_gemm_batched")
     return out
 
 
 @_gemm_batched_op.register_fake
-def _(a, w, out_bf16):
-    return a.new_empty(a.shape[0], a.shape[1], w.shape[1], dtype=_bf16 if out_bf16 else _f32)
+def _(a, w, out_bf16, M, zdiv, ldc, sC, sCo, rows):
+    dt = _bf16 if out_bf16 else _f32
+    if zdiv:
+        return a.new_empty(rows, ldc, dtype=dt)
+    return a.new_empty(a.shape[0], M, w.shape[1], dtype=dt)
 
 
-def gemm_batched(a, w, out_dtype=_f32):
-    """a[b] @ w[b]^T for bf16 a (Bt, M, K), w (Bt, N, K) with K-contiguous rows
-    (batch strides arbitrary): (Bt, M, N) fp32 or bf16."""
+def gemm_batched(a, w, out_dtype=_f32, M=None, heads=None):
+    """a[z] @ w[z]^T for a (Bt, Ma, K), w (Bt, N, K), both bf16 or both fp32,
+    K-contiguous rows (batch strides arbitrary): (Bt, M, N) in out_dtype over
+    the first M (default Ma) rows of each a[z].  heads=H: batch z = b*H + h is
+    written into a (Bt/H * M, H*N) matrix at rows b*M.., columns h*N.. — the
+    per-head products merged into the (B*T, H*dh) layout in the same launch."""
     require_device(a, w)
-    if a.dtype != _bf16 or w.dtype != _bf16:
-        raise TypeError("gemm_batched takes bf16 operands")
+    if a.dtype != w.dtype or a.dtype not in (_bf16, _f32):
+        raise TypeError(f"gemm_batched takes two bf16 or two fp32 operands (got {a.dtype}, {w.dtype})")
     if a.stride(-1) != 1 or w.stride(-1) != 1:
         raise ValueError("gemm_batched operands must be K-contiguous")
-    return torch.ops.sbk.gemm_batched(a, w, out_dtype == _bf16)
+    Bt, Ma, _ = a.shape
+    N = w.shape[1]
+    M = Ma if M is None else int(M)
+    if not 0 < M <= Ma:
+        raise ValueError("gemm_batched: M out of range")
+    if heads:
+        H = int(heads)
+        if Bt % H:
+            raise ValueError("gemm_batched: batch not a multiple of heads")
+        return torch.ops.sbk.gemm_batched(a, w, out_dtype == _bf16, M, H, H * N, N, M * H * N, Bt // H * M)
+    return torch.ops.sbk.gemm_batched(a, w, out_dtype == _bf16, M, 0, 0, 0, 0, 0)
 
 
 @torch.library.custom_op("sbk::length_mask", mutates_args=())

@@ -53,10 +53,15 @@ SIGNATURES = {
     # gemm_tn.hip (weight-gradient GEMM)
     "sbk_gemm_tn": [_vp, _ll, _ll, _vp, _ll, _ll, _i, _i, _i, _i, _vp, _ll, _ll, _vp],
     "sbk_gemm_tn_cfg": [_vp, _ll, _ll, _vp, _ll, _ll, _i, _i, _i, _i, _vp, _ll, _ll, _i, _i, _vp],
-    "sbk_gemm_batched": [_vp, _i, _ll, _vp, _i, _ll, _i, _i, _i, _i, _vp, _i, _ll, _i, _vp],
-    "sbk_relpos_softmax_bwd_hm": [_vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _i, _vp],
-    "sbk_attn_dqkv": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _i, _vp],
-    "sbk_attn_bwd_prep": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp],
+    "sbk_gemm_tn_f32": [_vp, _ll, _ll, _vp, _ll, _ll, _i, _i, _i, _i, _vp, _ll, _ll, _i, _vp],
+    "sbk_gemm_batched": [_i, _vp, _i, _ll, _vp, _i, _ll, _i, _i, _i, _i, _vp, _i, _ll, _i, _ll, _i, _vp],
+    # backward.hip: rel-pos attention backward over padded rows
+    "sbk_attn_prep": [_i, _vp, _vp, _vp, _i, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp,
+                      _vp, _vp],
+    "sbk_attn_dqkv": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp],
+    "sbk_attn_probs_pad": [_vp, _i, _i, _i, _f, ctypes.c_ulonglong, _vp, _vp, _i, _vp],
+    "sbk_relpos_softmax_bwd_pad": [_i, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, ctypes.c_ulonglong, _vp, _vp, _vp,
+                                   _vp],
     # ffn.hip
     "sbk_ffn_supported": [_i, _i],
     "sbk_ffn": [_vp, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _i, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _vp, _f,
@@ -119,7 +124,6 @@ SIGNATURES = {
     "sbk_dwconv_fwd": [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _i, _vp],
     "sbk_dwconv_wgrad_chunks": [_i, _i],
     "sbk_dwconv_bwd": [_vp, _i, _vp, _i, _i, _i, _vp, _i, _i, _vp, _i, _vp, _vp],
-    "sbk_relpos_softmax_bwd": [_vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _i, _vp],
     "sbk_im2col3s2": [_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp],
     "sbk_col2im3s2": [_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp],
     "sbk_joint_fwd": [_vp, _vp, _i, _i, _i, _i, _i, _f, _vp, _i, _vp],

@@ -18,7 +18,7 @@
 //   transducer joint fwd/bwd      transducer_joint.py:57-95 ("sum" + act)
 //
 // Dense contractions of the backward (dX = dY W, dW = dY^T X, the attention
-// batched products) are plain library GEMMs (hipBLASLt through torch.mm);
+// batched products) run on the MFMA GEMMs of gemm.hip / gemm_tn.hip;
 // everything here is bandwidth-bound elementwise / reduction work: coalesced
 // rows, one wave per row where a row reduction is needed, deterministic
 // per-block partial sums (no float atomics) reduced by sbk_colsum.
@@ -434,46 +434,6 @@ __global__ void __launch_bounds__(256) dwconv_wgrad_kernel(const void* __restric
   p[K] = acc[DW_KMAX];
 }
 
-// -------------------------------------------------- rel-pos softmax backward
-// One block per score row (b, h, i).  P (B, H, T, T) fp32 probabilities,
-// dP = dO V^T.  dS = scale * P * (dP - sum_j P dP); the positional branch's
-// gradient in the pre-shift layout dBD[i, r] = dS[i, j] with r = T-1-i+j
-// (the inverse of rel_shift, attention.py:468-483), zero outside the band.
-// One wave per row (4 rows per workgroup): the row sum is a wave reduction
-// (DPP) instead of a workgroup-barrier reduction over 256 threads on a
-// 376-element row (the first version: 98 us at config 4).
-__global__ void __launch_bounds__(256) relpos_softmax_bwd_wave_kernel(const float* __restrict__ P,
-                                                                      const void* __restrict__ dP, int dP_bf16,
-                                                                      int T, float scale, void* __restrict__ dS,
-                                                                      void* __restrict__ dBD, int out_bf16, int B,
-                                                                      int H, long long nrows) {
-  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= nrows) return;  // whole wave; no barrier below
-  const int lane = threadIdx.x & 63;
-  const int i = (int)(row % T);
-  long long brow = row;
-  if (B > 0) {
-    const long long bh = row / T;
-    brow = ((bh % H) * B + bh / H) * T + i;
-  }
-  const float* pr = P + row * T;
-  float s = 0.f;
-  for (int j = lane; j < T; j += 64) s += pr[j] * ldv(dP, row * T + j, dP_bf16);
-  s = wave_sum_v(s);
-  const int W = 2 * T - 1;
-  const int ldb = B > 0 ? (W + 7) & ~7 : W;
-  for (int r = lane; r < ldb; r += 64) {
-    const int j = r - (T - 1 - i);
-    float v = 0.f;
-    if (r < W && j >= 0 && j < T) {
-      v = scale * pr[j] * (ldv(dP, row * T + j, dP_bf16) - s);
-      stv(dS, row * T + j, v, out_bf16);
-    }
-    stv(dBD, brow * ldb + r, v, out_bf16);
-  }
-}
-
-
 // ------------------------------------------- ConvBlock im2col / col2im
 // Conv2d k3 stride 2 "same" reflect padding (pad 1 each side, CNN.py:659-700,
 // get_padding_elem :1459-1481).  x (B, Ti, Fi, Ci); col (B*To*Fo, 9*Ci) with
@@ -727,88 +687,265 @@ __global__ void dropout_add4_kernel(const void* __restrict__ x, int x_bf16, cons
   }
 }
 
-// Rel-pos attention backward: dqkv (B*T, H*3*dh) in the in_proj layout
-// (b, t, h, {q,k,v}, d) from the per-(b, h) products — dq = dS K + dBD P_k
-// (the second term head-major (H, B*T, dh)), dk, dv — in one pass (it was an
-// add, a stack, a permuted copy and a dtype cast).  4 d-values per thread.
-__global__ void attn_dqkv_kernel(const float* __restrict__ dq_ac, const float* __restrict__ dq_bd,
-                                 const float* __restrict__ dk, const float* __restrict__ dv, int B, int H, int T,
-                                 int dh, void* __restrict__ out, int out_bf16) {
-  const int d4n = dh / 4;
-  const long long n = (long long)B * T * H * d4n;
-  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (long long)gridDim.x * blockDim.x) {
-    const int d4 = (int)(q % d4n);
-    long long r = q / d4n;
-    const int h = (int)(r % H);
-    r /= H;
-    const int t = (int)(r % T);
-    const int b = (int)(r / T);
-    const long long src = (((long long)b * H + h) * T + t) * dh + 4 * d4;
-    const long long sbd = ((long long)h * B * T + (long long)b * T + t) * dh + 4 * d4;
-    const float4 a = *reinterpret_cast<const float4*>(dq_ac + src);
-    const float4 c = *reinterpret_cast<const float4*>(dq_bd + sbd);
-    const long long o = (((long long)b * T + t) * H + h) * 3 * dh + 4 * d4;
-    st4(out, o, make_float4(a.x + c.x, a.y + c.y, a.z + c.z, a.w + c.w), out_bf16);
-    st4(out, o + dh, *reinterpret_cast<const float4*>(dk + src), out_bf16);
-    st4(out, o + 2 * dh, *reinterpret_cast<const float4*>(dv + src), out_bf16);
+// ------------------------------------------ rel-pos attention backward
+// The per-(utterance, head) products of the backward run on the MFMA GEMMs
+// (sbk_gemm_batched, sbk_gemm_tn{,_f32}), whose operands need 16-B rows.  So
+// every per-(b, h) operand is laid out over Tp = T rounded up to 8 rows and
+// dhp = dh rounded up to 8 columns, zero-filled: the padded rows / columns
+// add nothing to any product, and any T or head size takes the same kernels.
+// Storage is bf16 or fp32 (`bf`), the compute dtype of the step.
+
+// Operands from the in_proj output (and dO) of one (b, h) and 64 frames, in
+// two coalesced phases through an LDS tile:
+//   phase 1 (lanes along d): qu = q + pos_bias_u, v, dO  (B*H, Tp, dhp) and
+//           qv = q + pos_bias_v head-major (H, B*T, dhp);
+//   phase 2 (lanes along t): kT, vT (B*H, dhp, Tp).
+// Bias sums in fp32 rounded once to the storage type (torch autocast adds
+// the fp32 parameter to the bf16 projection in fp32 and rounds the sum at
+// the next matmul).  Any output may be null.
+__global__ void __launch_bounds__(256) attn_prep_kernel(const void* __restrict__ qkv, const void* __restrict__ dO,
+                                                        const float* __restrict__ pbu, const float* __restrict__ pbv,
+                                                        int B, int H, int T, int dh, int Tp, int dhp, int bf,
+                                                        void* __restrict__ qu, void* __restrict__ qv,
+                                                        void* __restrict__ kT, void* __restrict__ vo,
+                                                        void* __restrict__ vT, void* __restrict__ doh) {
+  __shared__ float tk[64][65], tv[64][65];
+  const int t0 = blockIdx.x * 64, bh = blockIdx.y, d0 = blockIdx.z * 64;
+  const int b = bh / H, h = bh - b * H, tid = threadIdx.x;
+  {
+    const int d = d0 + (tid & 63);
+    const bool dv = d < dh;
+#pragma unroll 4
+    for (int k = 0; k < 16; ++k) {
+      const int tl = (tid >> 6) + 4 * k, t = t0 + tl;
+      if (t >= Tp || d >= dhp) continue;
+      const bool ok = dv && t < T;
+      const long long src = (((long long)b * T + t) * H + h) * 3 * dh + d;
+      const float q = ok ? ldv(qkv, src, bf) : 0.f;
+      const float kk = ok ? ldv(qkv, src + dh, bf) : 0.f;
+      const float vv = ok ? ldv(qkv, src + 2 * dh, bf) : 0.f;
+      const long long o = ((long long)bh * Tp + t) * dhp + d;
+      if (qu) stv(qu, o, ok ? q + pbu[h * dh + d] : 0.f, bf);
+      if (vo) stv(vo, o, vv, bf);
+      if (doh) stv(doh, o, ok ? ldv(dO, (((long long)b * T + t) * H + h) * dh + d, bf) : 0.f, bf);
+      if (qv && t < T) stv(qv, ((long long)h * B * T + (long long)b * T + t) * dhp + d, dv ? q + pbv[h * dh + d] : 0.f, bf);
+      tk[tl][tid & 63] = kk;
+      tv[tl][tid & 63] = vv;
+    }
+  }
+  if (!kT && !vT) return;  // uniform
+  __syncthreads();
+  const int t = t0 + (tid & 63);
+  if (t >= Tp) return;
+#pragma unroll 4
+  for (int k = 0; k < 16; ++k) {
+    const int dl = (tid >> 6) + 4 * k, d = d0 + dl;
+    if (d >= dhp) break;
+    const long long o = ((long long)bh * dhp + d) * Tp + t;
+    if (kT) stv(kT, o, tk[tid & 63][dl], bf);
+    if (vT) stv(vT, o, tv[tid & 63][dl], bf);
   }
 }
 
-// Rel-pos attention backward operands from the in_proj output and dO in one
-// pass (were seven permuted copies / adds): per (b, h) contiguous
-//   qu = q + bf16(pos_bias_u), v, dO   (B*H, T, dh)
-//   kT (B*H, dh, T),  qv = q + bf16(pos_bias_v) head-major (H, B*T, dh)
-// qkv (B*T, H*3*dh) bf16 in the (h, {q,k,v}, d) layout, dO (B*T, H*dh) bf16.
-// Sums in fp32 rounded once to bf16 (what the torch bf16 add computed).
-__global__ void attn_bwd_prep_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dO,
-                                     const float* __restrict__ pbu, const float* __restrict__ pbv, int B, int H, int T,
-                                     int dh, bf16_t* __restrict__ qu, bf16_t* __restrict__ qv, bf16_t* __restrict__ kT,
-                                     bf16_t* __restrict__ vo, bf16_t* __restrict__ doh) {
-  const long long n = (long long)B * T * H * dh;
+// pkT (H, dhp, Wp) = the linear_pos output pk (W, ldp) per head, transposed
+// (W = 2T-1 relative offsets, Wp rounded up to 8), zero-padded.
+__global__ void __launch_bounds__(256) attn_pkT_kernel(const void* __restrict__ pk, int ldp, int H, int dh, int W,
+                                                       int Wp, int dhp, int bf, void* __restrict__ pkT) {
+  __shared__ float tile[64][65];
+  const int w0 = blockIdx.x * 64, h = blockIdx.y, d0 = blockIdx.z * 64, tid = threadIdx.x;
+  {
+    const int d = d0 + (tid & 63);
+#pragma unroll 4
+    for (int k = 0; k < 16; ++k) {
+      const int wl = (tid >> 6) + 4 * k, w = w0 + wl;
+      tile[wl][tid & 63] = (w < W && d < dh) ? ldv(pk, (long long)w * ldp + h * dh + d, bf) : 0.f;
+    }
+  }
+  __syncthreads();
+  const int w = w0 + (tid & 63);
+  if (w >= Wp) return;
+#pragma unroll 4
+  for (int k = 0; k < 16; ++k) {
+    const int dl = (tid >> 6) + 4 * k, d = d0 + dl;
+    if (d >= dhp) break;
+    stv(pkT, ((long long)h * dhp + d) * Wp + w, tile[tid & 63][dl], bf);
+  }
+}
+
+// Softmax / dropout / rel_shift backward, one wave per padded score row
+// (b, h, i < Tp).  P (B, H, T, T) fp32 probabilities (before dropout), dP =
+// dO V^T over the padded rows (B*H, Tp, Tp), D = the dropout scale of each
+// probability (keep(seed, index of P) / (1 - p), regenerated — the forward's
+// sbk_dropout_add mask), attention.py:594-631:
+//   Pd = D P                                  (the operand of dV = Pd^T dO)
+//   dS = scale * P (D dP - sum_j P D dP)      (B*H, Tp, Tp)
+//   dBD[i, T-1-i+j] = dS[i, j]                (rel_shift :468-483 transposed)
+// dBD head-major (H, B*T, Wp), zero outside the band; padded rows / columns
+// of Pd and dS are zero.
+__global__ void __launch_bounds__(256) relpos_softmax_bwd_pad_kernel(
+    const float* __restrict__ P, const void* __restrict__ dP, float scale, int B, int H, int T, int Tp, int Wp,
+    unsigned thresh, float inv_keep, unsigned long long seed, int use_drop, void* __restrict__ dS,
+    void* __restrict__ Pd, void* __restrict__ dBD, int bf) {
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (long long)B * H * Tp) return;  // whole wave; no barrier below
+  const int lane = threadIdx.x & 63;
+  const long long bh = row / Tp;
+  const int i = (int)(row - bh * Tp);
+  const long long so = row * Tp;
+  if (i >= T) {
+    for (int j = lane; j < Tp; j += 64) {
+      stv(dS, so + j, 0.f, bf);
+      stv(Pd, so + j, 0.f, bf);
+    }
+    return;
+  }
+  const long long pi = (bh * T + i) * T;  // P row; the dropout index base
+  const float* pr = P + pi;
+  auto dscale = [&](int j) __attribute__((always_inline)) {
+    return use_drop ? (keep_elem(seed, pi + j, thresh) ? inv_keep : 0.f) : 1.f;
+  };
+  float s = 0.f;
+  for (int j = lane; j < T; j += 64) s += pr[j] * dscale(j) * ldv(dP, so + j, bf);
+  s = wave_sum_v(s);
+  for (int j = lane; j < Tp; j += 64) {
+    float pd = 0.f, ds = 0.f;
+    if (j < T) {
+      const float p = pr[j], dd = dscale(j);
+      pd = p * dd;
+      ds = scale * p * (dd * ldv(dP, so + j, bf) - s);
+    }
+    stv(Pd, so + j, pd, bf);
+    stv(dS, so + j, ds, bf);
+  }
+  const int h = (int)(bh % H), b = (int)(bh / H);
+  const long long bo = (((long long)h * B + b) * T + i) * Wp;
+  const int W = 2 * T - 1;
+  for (int r = lane; r < Wp; r += 64) {
+    const int j = r - (T - 1 - i);
+    float v = 0.f;
+    if (r < W && j >= 0 && j < T) v = scale * pr[j] * (dscale(j) * ldv(dP, so + j, bf) - s);
+    stv(dBD, bo + r, v, bf);
+  }
+}
+
+// Forward attention dropout (attention.py:626): attn = D P (fp32 (B, H, T, T),
+// the module's returned weights; may be null) and the same values over the
+// padded rows (B*H, Tp, Tp) in the compute dtype — the A operand of
+// drop(P) V on sbk_gemm_batched.  Same mask as sbk_dropout_add on P.
+__global__ void attn_probs_pad_kernel(const float* __restrict__ P, long long BH, int T, int Tp, unsigned thresh,
+                                      float inv_keep, unsigned long long seed, int use_drop, float* __restrict__ attn,
+                                      void* __restrict__ Pd, int bf) {
+  const long long n = BH * Tp * Tp;
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
-    const int d = (int)(e % dh);
-    long long r = e / dh;
+    const int j = (int)(e % Tp);
+    const long long r = e / Tp;
+    const int i = (int)(r % Tp);
+    const long long bh = r / Tp;
+    float v = 0.f;
+    if (i < T && j < T) {
+      const long long idx = (bh * T + i) * T + j;
+      v = P[idx];
+      if (use_drop) v = keep_elem(seed, idx, thresh) ? v * inv_keep : 0.f;
+      if (attn) attn[idx] = v;
+    }
+    stv(Pd, e, v, bf);
+  }
+}
+
+// dqkv (B*T, H*3*dh) in the in_proj layout (b, t, h, {q,k,v}, d) from the
+// per-(b, h) products over padded rows — dq = dS K + dBD P_k (the second
+// term head-major (H, B*T, dhp)), dk, dv (B*H, Tp, dhp) — in one pass.
+// V values per thread (4 when dh % 4 == 0, 16-B loads).
+template <int V>
+__global__ void attn_dqkv_kernel(const float* __restrict__ dq_ac, const float* __restrict__ dq_bd,
+                                 const float* __restrict__ dk, const float* __restrict__ dv, int B, int H, int T,
+                                 int dh, int Tp, int dhp, void* __restrict__ out, int out_bf16) {
+  const int dvn = dh / V;
+  const long long n = (long long)B * T * H * dvn;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (long long)gridDim.x * blockDim.x) {
+    const int d = (int)(q % dvn) * V;
+    long long r = q / dvn;
     const int h = (int)(r % H);
     r /= H;
     const int t = (int)(r % T);
     const int b = (int)(r / T);
-    const long long src = (((long long)b * T + t) * H + h) * 3 * dh + d;
-    const float q = bf16_to_f32(qkv[src]);
-    const float u = bf16_to_f32(f32_to_bf16(pbu[h * dh + d]));
-    const float vv = bf16_to_f32(f32_to_bf16(pbv[h * dh + d]));
-    const long long bh = (long long)b * H + h;
-    const long long o = (bh * T + t) * dh + d;
-    qu[o] = f32_to_bf16(q + u);
-    qv[((long long)h * B * T + (long long)b * T + t) * dh + d] = f32_to_bf16(q + vv);
-    kT[(bh * dh + d) * T + t] = qkv[src + dh];
-    vo[o] = qkv[src + 2 * dh];
-    doh[o] = dO[(((long long)b * T + t) * H + h) * dh + d];
+    const long long src = (((long long)b * H + h) * Tp + t) * dhp + d;
+    const long long sbd = ((long long)h * B * T + (long long)b * T + t) * dhp + d;
+    const long long o = (((long long)b * T + t) * H + h) * 3 * dh + d;
+    if constexpr (V == 4) {
+      const float4 a = *reinterpret_cast<const float4*>(dq_ac + src);
+      const float4 c = *reinterpret_cast<const float4*>(dq_bd + sbd);
+      st4(out, o, make_float4(a.x + c.x, a.y + c.y, a.z + c.z, a.w + c.w), out_bf16);
+      st4(out, o + dh, *reinterpret_cast<const float4*>(dk + src), out_bf16);
+      st4(out, o + 2 * dh, *reinterpret_cast<const float4*>(dv + src), out_bf16);
+    } else {
+      stv(out, o, dq_ac[src] + dq_bd[sbd], out_bf16);
+      stv(out, o + dh, dk[src], out_bf16);
+      stv(out, o + 2 * dh, dv[src], out_bf16);
+    }
   }
 }
 
 }  // namespace
 
-SBK_API int sbk_attn_bwd_prep(const void* qkv, const void* dO, const float* pbu, const float* pbv, int B, int H,
-                              int T, int dh, void* qu, void* qv, void* kT, void* v, void* doh, void* stream) {
-  if (B <= 0 || H <= 0 || T <= 0 || dh <= 0) return SBK_ERR_ARG;
+// Operands of the rel-pos attention products over padded rows (see
+// attn_prep_kernel): qkv (B*T, H*3*dh), dO (B*T, H*dh) (may be null), pk
+// (2T-1, ldp) (may be null); outputs qu, v, doh (B*H, Tp, dhp), kT, vT
+// (B*H, dhp, Tp), qv (H, B*T, dhp), pkT (H, dhp, Wp), each nullable; bf16
+// (dtype_bf16) or fp32 storage throughout.  Tp >= T, dhp >= dh, Wp >= 2T-1.
+SBK_API int sbk_attn_prep(int dtype_bf16, const void* qkv, const void* dO, const void* pk, int ldp, const float* pbu,
+                          const float* pbv, int B, int H, int T, int dh, int Tp, int dhp, int Wp, void* qu, void* qv,
+                          void* kT, void* v, void* vT, void* doh, void* pkT, void* stream) {
+  if (B <= 0 || H <= 0 || T <= 0 || dh <= 0 || Tp < T || dhp < dh || Wp < 2 * T - 1) return SBK_ERR_ARG;
+  if (B * H > 65535 || (dhp + 63) / 64 > 65535) return SBK_ERR_ARG;
+  if ((qu && !pbu) || (qv && !pbv) || (doh && !dO) || (pkT && (!pk || ldp < H * dh))) return SBK_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (qu || qv || kT || v || vT || doh) {
+    attn_prep_kernel<<<dim3((Tp + 63) / 64, B * H, (dhp + 63) / 64), 256, 0, s>>>(
+        qkv, dO, pbu, pbv, B, H, T, dh, Tp, dhp, dtype_bf16, qu, qv, kT, v, vT, doh);
+    SBK_CHECK_LAUNCH();
+  }
+  if (pkT) {
+    attn_pkT_kernel<<<dim3((Wp + 63) / 64, H, (dhp + 63) / 64), 256, 0, s>>>(pk, ldp, H, dh, 2 * T - 1, Wp, dhp,
+                                                                            dtype_bf16, pkT);
+    SBK_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+// dqkv from the padded per-(b, h) gradients (attn_dqkv_kernel); fp32 inputs,
+// out fp32 or bf16.
+SBK_API int sbk_attn_dqkv(const float* dq_ac, const float* dq_bd, const float* dk, const float* dv, int B, int H,
+                          int T, int dh, int Tp, int dhp, void* out, int out_bf16, void* stream) {
+  if (B <= 0 || H <= 0 || T <= 0 || dh <= 0 || Tp < T || dhp < dh) return SBK_ERR_ARG;
+  const bool v4 = dh % 4 == 0 && dhp % 4 == 0 &&
+                  ((reinterpret_cast<uintptr_t>(dq_ac) | reinterpret_cast<uintptr_t>(dq_bd) |
+                    reinterpret_cast<uintptr_t>(dk) | reinterpret_cast<uintptr_t>(dv) |
+                    reinterpret_cast<uintptr_t>(out)) & 15) == 0;
   const long long n = (long long)B * T * H * dh;
-  attn_bwd_prep_kernel<<<grid_for(n, 256), 256, 0, (hipStream_t)stream>>>(
-      reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<const bf16_t*>(dO), pbu, pbv, B, H, T, dh,
-      reinterpret_cast<bf16_t*>(qu), reinterpret_cast<bf16_t*>(qv), reinterpret_cast<bf16_t*>(kT),
-      reinterpret_cast<bf16_t*>(v), reinterpret_cast<bf16_t*>(doh));
+  if (v4)
+    attn_dqkv_kernel<4><<<grid_for(n / 4, 256), 256, 0, (hipStream_t)stream>>>(dq_ac, dq_bd, dk, dv, B, H, T, dh, Tp,
+                                                                               dhp, out, out_bf16);
+  else
+    attn_dqkv_kernel<1><<<grid_for(n, 256), 256, 0, (hipStream_t)stream>>>(dq_ac, dq_bd, dk, dv, B, H, T, dh, Tp,
+                                                                           dhp, out, out_bf16);
   SBK_CHECK_LAUNCH();
   return 0;
 }
 
-SBK_API int sbk_attn_dqkv(const float* dq_ac, const float* dq_bd, const float* dk, const float* dv, int B, int H,
-                          int T, int dh, void* out, int out_bf16, void* stream) {
-  if (B <= 0 || H <= 0 || T <= 0 || dh <= 0 || dh % 4) return SBK_ERR_ARG;
-  if ((reinterpret_cast<uintptr_t>(dq_ac) | reinterpret_cast<uintptr_t>(dq_bd) | reinterpret_cast<uintptr_t>(dk) |
-       reinterpret_cast<uintptr_t>(dv) | reinterpret_cast<uintptr_t>(out)) & 15)
-    return SBK_ERR_ARG;
-  const long long n = (long long)B * T * H * (dh / 4);
-  attn_dqkv_kernel<<<grid_for(n, 256), 256, 0, (hipStream_t)stream>>>(dq_ac, dq_bd, dk, dv, B, H, T, dh, out,
-                                                                       out_bf16);
+static unsigned drop_thresh(float p) {
+  const double keep = 1.0 - (double)p;
+  return (unsigned)std::min(keep * 16777216.0, 16777216.0);
+}
+
+// Forward attention dropout on the probabilities: attn (fp32, may be null)
+// and Pd over padded rows (B*H, Tp, Tp) in the compute dtype.  p = 0: Pd = P.
+SBK_API int sbk_attn_probs_pad(const float* P, int BH, int T, int Tp, float p, unsigned long long seed, float* attn,
+                               void* Pd, int pd_bf16, void* stream) {
+  if (BH <= 0 || T <= 0 || Tp < T || !(p >= 0.f) || p >= 1.f) return SBK_ERR_ARG;
+  const long long n = (long long)BH * Tp * Tp;
+  attn_probs_pad_kernel<<<grid_for(n, 256), 256, 0, (hipStream_t)stream>>>(
+      P, BH, T, Tp, drop_thresh(p), (float)(1.0 / (1.0 - (double)p)), seed, p > 0.f, attn, Pd, pd_bf16);
   SBK_CHECK_LAUNCH();
   return 0;
 }
@@ -969,24 +1106,18 @@ SBK_API int sbk_dwconv_bwd(const void* x, int x_bf16, const float* dy, int B, in
   return 0;
 }
 
-SBK_API int sbk_relpos_softmax_bwd(const float* P, const void* dP, int dP_bf16, int B, int H, int T, float scale,
-                                   void* dS, void* dBD, int out_bf16, void* stream) {
-  if (B <= 0 || H <= 0 || T <= 0) return SBK_ERR_ARG;
-  const long long nrows = (long long)B * H * T;
-  relpos_softmax_bwd_wave_kernel<<<(unsigned)((nrows + 3) / 4), 256, 0, (hipStream_t)stream>>>(
-      P, dP, dP_bf16, T, scale, dS, dBD, out_bf16, 0, 0, nrows);
-  SBK_CHECK_LAUNCH();
-  return 0;
-}
-
-// As sbk_relpos_softmax_bwd with dBD written head-major: (H, B, T, Wp),
-// Wp = 2T-1 rounded up to 8 (pad columns zero).
-SBK_API int sbk_relpos_softmax_bwd_hm(const float* P, const void* dP, int dP_bf16, int B, int H, int T, float scale,
-                                      void* dS, void* dBD, int out_bf16, void* stream) {
-  if (B <= 0 || H <= 0 || T <= 0) return SBK_ERR_ARG;
-  const long long nrows = (long long)B * H * T;
-  relpos_softmax_bwd_wave_kernel<<<(unsigned)((nrows + 3) / 4), 256, 0, (hipStream_t)stream>>>(
-      P, dP, dP_bf16, T, scale, dS, dBD, out_bf16, B, H, nrows);
+// RelPosMHAXL softmax / dropout / rel_shift backward over padded rows
+// (relpos_softmax_bwd_pad_kernel): P (B, H, T, T) fp32, dP (B*H, Tp, Tp);
+// out dS, Pd (B*H, Tp, Tp), dBD (H, B*T, Wp); dP and the outputs bf16
+// (dtype_bf16) or fp32.  p, seed: the forward's attention dropout.
+SBK_API int sbk_relpos_softmax_bwd_pad(int dtype_bf16, const float* P, const void* dP, int B, int H, int T, int Tp,
+                                       int Wp, float scale, float p, unsigned long long seed, void* dS, void* Pd,
+                                       void* dBD, void* stream) {
+  if (B <= 0 || H <= 0 || T <= 0 || Tp < T || Wp < 2 * T - 1 || !(p >= 0.f) || p >= 1.f) return SBK_ERR_ARG;
+  const long long nrows = (long long)B * H * Tp;
+  relpos_softmax_bwd_pad_kernel<<<(unsigned)((nrows + 3) / 4), 256, 0, (hipStream_t)stream>>>(
+      P, dP, scale, B, H, T, Tp, Wp, drop_thresh(p), (float)(1.0 / (1.0 - (double)p)), seed, p > 0.f, dS, Pd, dBD,
+      dtype_bf16);
   SBK_CHECK_LAUNCH();
   return 0;
 }

@@ -44,8 +44,13 @@ struct Epi {
   void* ln_out = nullptr;
   int ldu = 0;
   int ln_bf16 = 0;
-  // batched launches (grid.z): element strides of A, W and out per batch
+  // batched launches (grid.z): element strides of A, W and out per batch;
+  // zdiv > 0 splits the batch index z into (z / zdiv, z % zdiv) with output
+  // strides (sCo, sC) — per-(utterance, head) products written straight
+  // into the (B*T, H*dh) head-interleaved layout
   long long sA = 0, sW = 0, sC = 0;
+  int zdiv = 0;
+  long long sCo = 0;
 };
 
 // C tile (fp32, row stride CR, in LDS) -> global through the fused epilogue:
@@ -295,9 +300,11 @@ __global__ void __launch_bounds__(256) gemm_kernel(const T* __restrict__ A, int 
   T* As = reinterpret_cast<T*>(smem);
   T* Bs = As + NBUF * BM * LDSR;
   if (gridDim.z > 1) {  // batched: this batch's operands and output
-    A += blockIdx.z * ep.sA;
-    W += blockIdx.z * ep.sW;
-    ep.out = reinterpret_cast<char*>(ep.out) + blockIdx.z * ep.sC * (ep.out_bf16 ? 2 : 4);
+    const long long z = blockIdx.z;
+    A += z * ep.sA;
+    W += z * ep.sW;
+    const long long oc = ep.zdiv > 0 ? (z / ep.zdiv) * ep.sCo + (z % ep.zdiv) * ep.sC : z * ep.sC;
+    ep.out = reinterpret_cast<char*>(ep.out) + oc * (ep.out_bf16 ? 2 : 4);
   }
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -788,18 +795,25 @@ SBK_API int sbk_gemm(int dtype_bf16, const void* A, int lda, const void* W, int 
   }
 }
 
-// Batched C[b] = A[b] · W[b]^T (bf16 operands, K-contiguous rows; fp32 or
-// bf16 out) for b < batch with element strides sA / sW / sC: the per-(b, h)
-// products of the attention backward (dP = dO·V^T, dQ = dS·K, ...), one
-// launch over grid.z.  M, N, K as sbk_gemm (K, lda, ldw % 8 == 0).
-SBK_API int sbk_gemm_batched(const void* A, int lda, long long sA, const void* W, int ldw, long long sW, int M, int N,
-                             int K, int batch, void* out, int ldc, long long sC, int out_bf16, void* stream) {
-  if (M <= 0 || N <= 0 || K <= 0 || batch <= 0 || batch > 65535) return SBK_ERR_ARG;
-  if ((K % 8) || (lda % 8) || (ldw % 8) || (sA % 8) || (sW % 8)) return SBK_ERR_ARG;
+// Batched C[z] = A[z] · W[z]^T (bf16 or fp32 operands, K-contiguous rows;
+// fp32 or bf16 out) for z < batch with element strides sA / sW: the
+// per-(b, h) products of the attention backward (dP = dO·V^T, dQ = dS·K, ...)
+// and the dropout product drop(P)·V, one launch over grid.z.  Output: batch
+// z at (z / zdiv) * sCo + (z % zdiv) * sC when zdiv > 0, else z * sC.
+// M, N, K as sbk_gemm (K, lda, ldw multiples of the 16-B vector).
+SBK_API int sbk_gemm_batched(int dtype_bf16, const void* A, int lda, long long sA, const void* W, int ldw,
+                             long long sW, int M, int N, int K, int batch, void* out, int ldc, long long sC, int zdiv,
+                             long long sCo, int out_bf16, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || batch <= 0 || batch > 65535 || zdiv < 0) return SBK_ERR_ARG;
+  const int vec = dtype_bf16 ? 8 : 4;
+  if ((K % vec) || (lda % vec) || (ldw % vec) || (sA % vec) || (sW % vec)) return SBK_ERR_ARG;
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(W)) & 15) return SBK_ERR_ARG;
   Epi ep{nullptr, ACT_NONE, 0.f, nullptr, 0, 1.f, nullptr, out, ldc, out_bf16};
   ep.sA = sA;
   ep.sW = sW;
   ep.sC = sC;
-  return launch<bf16_t, 64, 64, 64>(A, lda, W, ldw, M, N, K, ep, (hipStream_t)stream, batch);
+  ep.zdiv = zdiv;
+  ep.sCo = sCo;
+  if (dtype_bf16) return launch<bf16_t, 64, 64, 64>(A, lda, W, ldw, M, N, K, ep, (hipStream_t)stream, batch);
+  return launch<float, 64, 64, 32>(A, lda, W, ldw, M, N, K, ep, (hipStream_t)stream, batch);
 }

@@ -145,6 +145,96 @@ __global__ void __launch_bounds__(256) gemm_tn_kernel(TnArgs a) {
     }
 }
 
+
+// Exact-fp32 variant (the fp32 parity mode of the training path): the same
+// token-major staging with fp32 operands, 64 x 64 tiles, 32 k-rows per
+// step, read for v_mfma_f32_16x16x4_f32 (lane l: row / column l & 15 of the
+// tile, k-row l >> 4 of the 4-deep slice) — one ds_read_b32 per fragment,
+// the 16 lanes of a k-row on consecutive banks (row stride 64 + 16 floats).
+// Operands with M, N, lda or ldb not a multiple of 4 (or unaligned) load
+// element-wise (`vec` false), so any shape is accepted.
+constexpr int TF_BK = 32, TF_LD = 80;
+
+__global__ void __launch_bounds__(256) gemm_tn_f32_kernel(const float* __restrict__ Ap, const float* __restrict__ Bp,
+                                                          float* __restrict__ Cp, long long lda, long long ldb,
+                                                          long long ldc, long long sA, long long sB, long long sC, int M,
+                                                          int N, int K, int kchunk, int nsplit, int vec) {
+  __shared__ __attribute__((aligned(16))) float As[TF_BK * TF_LD];
+  __shared__ __attribute__((aligned(16))) float Bs[TF_BK * TF_LD];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+  const int bz = blockIdx.z / nsplit, sp = blockIdx.z - bz * nsplit;
+  const int k0 = sp * kchunk, k1 = min(K, k0 + kchunk);
+  const float* A = Ap + bz * sA;
+  const float* B = Bp + bz * sB;
+  float* C = Cp + bz * sC;
+  // 32 k-rows x 64 columns = 512 float4 chunks per operand: 2 per thread
+  float4 ra[2], rb[2];
+  auto ld4 = [&](const float* X, long long ld, int r, int c, int lim) __attribute__((always_inline)) {
+    const float* p = X + (long long)r * ld + c;
+    if (vec) return c < lim ? *reinterpret_cast<const float4*>(p) : make_float4(0.f, 0.f, 0.f, 0.f);
+    return make_float4(c < lim ? p[0] : 0.f, c + 1 < lim ? p[1] : 0.f, c + 2 < lim ? p[2] : 0.f,
+                       c + 3 < lim ? p[3] : 0.f);
+  };
+  auto gload = [&](int kb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + i * 256, r = kb + (c >> 4), cc = (c & 15) * 4;
+      const bool rk = r < k1;
+      ra[i] = rk ? ld4(A, lda, r, m0 + cc, M) : make_float4(0.f, 0.f, 0.f, 0.f);
+      rb[i] = rk ? ld4(B, ldb, r, n0 + cc, N) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (k1 - k0 + TF_BK - 1) / TF_BK;
+  if (nk > 0) gload(k0);
+  const int fr = lane & 15, g = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + i * 256;
+      *reinterpret_cast<float4*>(As + (c >> 4) * TF_LD + (c & 15) * 4) = ra[i];
+      *reinterpret_cast<float4*>(Bs + (c >> 4) * TF_LD + (c & 15) * 4) = rb[i];
+    }
+    __syncthreads();
+    if (kt + 1 < nk) gload(k0 + (kt + 1) * TF_BK);
+#pragma unroll
+    for (int kk = 0; kk < TF_BK / 4; ++kk) {
+      const int kr = (4 * kk + g) * TF_LD;
+      float fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = As[kr + wm * 32 + i * 16 + fr];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = Bs[kr + wn * 32 + j * 16 + fr];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wm * 32 + i * 16 + 4 * g + r;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + wn * 32 + j * 16 + fr;
+        if (n < N) {
+          float* cp = C + (long long)m * ldc + n;
+          if (nsplit == 1) *cp += acc[i][j][r];
+          else atomicAdd(cp, acc[i][j][r]);
+        }
+      }
+    }
+}
+
 }  // namespace
 
 // C[b] += A[b]^T B[b] for b < batch.  A (K, M) with row stride lda, B (K, N)
@@ -197,4 +287,34 @@ SBK_API int sbk_gemm_tn_cfg(const void* A, long long lda, long long sA, const vo
 SBK_API int sbk_gemm_tn(const void* A, long long lda, long long sA, const void* B, long long ldb, long long sB,
                         int M, int N, int K, int batch, float* C, long long ldc, long long sC, void* stream) {
   return sbk_gemm_tn_cfg(A, lda, sA, B, ldb, sB, M, N, K, batch, C, ldc, sC, 0, 0, stream);
+}
+
+// fp32 operands (exact-f32 MFMA): C[b] += A[b]^T B[b], arguments as
+// sbk_gemm_tn; any M, N, lda, ldb (element-wise loads unless all are
+// multiples of 4 with 16-B aligned A, B and batch strides).  The weight
+// gradient dW = dY^T X of the fp32 (parity) training path.  nsplit: token-
+// range splits (0 = choose; 1 = plain stores, deterministic).
+SBK_API int sbk_gemm_tn_f32(const float* A, long long lda, long long sA, const float* B, long long ldb, long long sB,
+                            int M, int N, int K, int batch, float* C, long long ldc, long long sC, int nsplit,
+                            void* stream) {
+  if (!A || !B || !C || M <= 0 || N <= 0 || K < 0 || batch <= 0 || nsplit < 0) return SBK_ERR_ARG;
+  if (lda < M || ldb < N || ldc < N) return SBK_ERR_ARG;
+  if (K == 0) return 0;
+  const int vec = ((M | N) % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 && (sA | sB) % 4 == 0 &&
+                   ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) == 0);
+  const int tm = (M + 63) / 64, tn = (N + 63) / 64;
+  const long long tiles = (long long)tm * tn * batch;
+  if (nsplit == 0) {
+    nsplit = 1;
+    while (tiles * nsplit * 2 <= 1024 && (long long)K / (nsplit * 2) >= 256 &&
+           (long long)M * N * batch * nsplit * 2 <= (4LL << 20))
+      nsplit *= 2;
+  }
+  const int kchunk = ((K + nsplit - 1) / nsplit + TF_BK - 1) / TF_BK * TF_BK;
+  nsplit = (K + kchunk - 1) / kchunk;
+  if ((long long)batch * nsplit > 65535) return SBK_ERR_ARG;
+  hipLaunchKernelGGL(gemm_tn_f32_kernel, dim3(tm, tn, batch * nsplit), dim3(256), 0, (hipStream_t)stream, A, B, C, lda,
+                     ldb, ldc, sA, sB, sC, M, N, K, kchunk, nsplit, vec);
+  SBK_CHECK_LAUNCH();
+  return 0;
 }

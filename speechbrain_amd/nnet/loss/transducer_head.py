@@ -23,11 +23,15 @@ loss and the gradients wrt tn, pn and weight from csrc/thead.hip:
 
 so the only (rows × V) tensor is the transient bf16 dS of the backward.
 Numerics: the bf16-autocast recipe's (z and W in bf16, fp32 accumulation);
-the logits are not rounded to bf16 before the log-softmax.
+the logits are not rounded to bf16 before the log-softmax.  Without bf16
+autocast (the fp32 compute dtype) the head runs the materialised chain on
+the fp32 kernels instead — sbk_joint_fwd → exact-f32 MFMA Linear → the HIP
+RNN-T loss — so an fp32 step never computes in bf16 behind the caller's back.
 """
 import torch
 import torch.nn as nn
 
+from ... import _autograd as A
 from ... import _enc
 from ..._lib import check, lib, ptr, require_device, stream_of
 from ..linear import Linear
@@ -155,6 +159,9 @@ def transducer_head_loss(tn, pn, weight, targets, input_lens, target_lens, blank
         pn = pn[:, 0, :, :]
     require_device(tn, pn, weight, targets)
     act, slope = _act_of(nonlinearity if nonlinearity is not None else nn.LeakyReLU())
+    if _enc.compute_dtype() == torch.float32:
+        return _materialised_fp32(tn, pn, weight, targets, input_lens, target_lens, blank_index, reduction,
+                                  use_torchaudio, act, slope)
     B, T, J = tn.shape
     U1 = pn.shape[1]
     in_lens = (input_lens * T).round().int()
@@ -168,6 +175,22 @@ def transducer_head_loss(tn, pn, weight, targets, input_lens, target_lens, blank
     out, _ = thead_loss(tn.float().contiguous(), pn.float().contiguous(), weight.float().contiguous(), lab, Tl, Ul,
                         int(blank_index), _RED[reduction], 1 if use_torchaudio else 0, act, slope)
     return out
+
+
+def _materialised_fp32(tn, pn, weight, targets, input_lens, target_lens, blank_index, reduction, use_torchaudio,
+                       act, slope):
+    """fp32 compute dtype: Transducer_joint → Linear → transducer_loss as the
+    recipe runs them (transducer_joint.py:57-95, linear.py:15-76,
+    losses.py:27-85), every op an fp32 HIP kernel with its own backward."""
+    from ..losses import transducer_loss
+    B, T, J = tn.shape
+    U1 = pn.shape[1]
+    z = A.JointFn.apply(A.to_dtype(tn.float(), torch.float32), A.to_dtype(pn.float(), torch.float32), act, slope,
+                        torch.float32)
+    logits = A.LinearFn.apply(z.view(B * T * U1, J), weight, None, weight.detach().float().contiguous(),
+                              torch.float32, None, 1.0, None)
+    return transducer_loss(logits.view(B, T, U1, -1), targets, input_lens, target_lens, blank_index, reduction,
+                           use_torchaudio=use_torchaudio)
 
 
 class TransducerHeadLinear(Linear):

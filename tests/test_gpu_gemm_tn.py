@@ -79,3 +79,62 @@ def test_linear_backward_on_sbk(dev):
         e = ((got.float() - want).norm() / want.norm()).item()
         print(f"{name}: normwise rel err {e:.2e}")
         assert e <= tol, (name, e)
+
+
+@pytest.mark.parametrize("K,M,N,batch", [(12032, 256, 1024, 0), (1001, 37, 70, 0), (377, 40, 36, 4), (5, 3, 3, 0)])
+def test_gemm_tn_f32(dev, K, M, N, batch):
+    """Exact-f32 weight-gradient GEMM (sbk_gemm_tn_f32): aligned shapes on
+    the 16-B loads, ragged M / N (37, 70, 3) on the element-wise loads, against
+    float64 on the CPU: only the fp32 summation order differs."""
+    from speechbrain_amd import _enc
+    torch.manual_seed(K + M)
+    shp = (batch,) if batch else ()
+    a = torch.randn(*shp, K, M)
+    b = torch.randn(*shp, K, N)
+    c = _enc.gemm_tn(a.to(dev), b.to(dev)).cpu()
+    ref = a.double().transpose(-1, -2) @ b.double()
+    bound = 1e-5 * (a.double().abs().transpose(-1, -2) @ b.double().abs()) + 1e-6
+    assert c.shape == ref.shape and c.dtype == torch.float32
+    assert ((c.double() - ref).abs() <= bound).all(), ((c.double() - ref).abs() / bound).max()
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gemm_batched_heads(dev, dt):
+    """sbk_gemm_batched in both dtypes, over the first M rows of each batch
+    entry, with batch z = b*H + h written straight into the (B*M, H*N)
+    head-interleaved layout (the attention dropout product drop(P)·V)."""
+    from speechbrain_amd import _enc
+    torch.manual_seed(2)
+    B, H, Mp, M, K, N = 3, 4, 48, 45, 48, 16
+    a = torch.randn(B * H, Mp, K).to(dt)
+    w = torch.randn(B * H, N + 8, K).to(dt)[:, :N]   # strided rows: batch stride (N+8)*K
+    out = _enc.gemm_batched(a.to(dev), w.to(dev), out_dtype=torch.float32, M=M, heads=H).cpu()
+    ref = (a[:, :M].double() @ w.double().transpose(-1, -2)).view(B, H, M, N).permute(0, 2, 1, 3).reshape(B * M, H * N)
+    bound = 1e-5 * (a[:, :M].double().abs() @ w.double().abs().transpose(-1, -2)).view(B, H, M, N).permute(
+        0, 2, 1, 3).reshape(B * M, H * N) + 1e-6
+    assert out.shape == (B * M, H * N)
+    assert ((out.double() - ref).abs() <= bound).all()
+    plain = _enc.gemm_batched(a.to(dev), w.to(dev)).cpu()
+    assert plain.shape == (B * H, Mp, N)
+    assert torch.allclose(plain[:, :M].reshape(B, H, M, N).permute(0, 2, 1, 3).reshape(B * M, H * N), out, rtol=0,
+                          atol=0)
+
+
+def test_linear_backward_fp32_on_sbk(dev):
+    """LinearFn backward in fp32 (the parity mode): dX on the exact-f32
+    sbk_gemm, dW on sbk_gemm_tn_f32 — no library GEMM — against float64,
+    including an odd width (N = 70, K = 37) on the element-wise loads."""
+    from speechbrain_amd import _autograd as A, _enc
+    for M, K, N in ((3000, 256, 1024), (777, 37, 70)):
+        torch.manual_seed(M)
+        x = torch.randn(M, K)
+        w = torch.randn(N, K) / 16
+        b = torch.randn(N)
+        g = torch.randn(M, N)
+        xd, wd, bd = (t.to(dev).requires_grad_() for t in (x, w, b))
+        A.linear(xd, wd, bd, torch.float32, _enc.WeightCache(), "w").backward(g.to(dev))
+        xr, wr, br = (t.double().requires_grad_() for t in (x, w, b))
+        (xr @ wr.t() + br).backward(g.double())
+        for name, got, want in (("dX", xd.grad, xr.grad), ("dW", wd.grad, wr.grad), ("db", bd.grad, br.grad)):
+            e = ((got.cpu().double() - want).norm() / want.norm()).item()
+            assert e <= 1e-5, (M, name, e)
