@@ -84,18 +84,46 @@ def gemm_flops(M, N, K):
     return 2.0 * M * N * K
 
 
+def _usable_cpus():
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
+def pick_threads(probe):
+    """The CPU baseline's thread count: SURVEY §8d times the reference CPU path
+    on the host's cores (torch.set_num_threads(os.cpu_count())).  A GPU box's
+    process may hold only a share of the machine (OMP_NUM_THREADS is set to
+    it), where os.cpu_count() threads oversubscribe; so one short probe pass
+    runs at each candidate — OMP_NUM_THREADS, the affinity mask, os.cpu_count()
+    — and the fastest is used.  Returns (threads, {threads: probe seconds})."""
+    cands = {max(1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0)), _usable_cpus(), os.cpu_count() or 1}
+    cands = sorted(c for c in cands if c >= 1)
+    times = {}
+    for c in cands:
+        torch.set_num_threads(c)
+        probe()  # warm-up at this thread count
+        t0 = time.perf_counter()
+        probe()
+        times[c] = round(time.perf_counter() - t0, 4)
+    best = min(times, key=times.get)
+    torch.set_num_threads(best)
+    return best, times
+
+
 def cpu_baseline(d_model, n_utt=16, reps=4):
     """Oracle (PyTorch CPU fp32 restatement) on n_utt x 15 s, median of `reps`."""
     import oracle.conformer as OC
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    threads = max(1, min(threads, os.cpu_count() or 1))
-    torch.set_num_threads(threads)
     fbank, cnn, tr = build_model(d_model, "cpu")
     sd_cnn = cnn.state_dict()
     sd_tr = tr.state_dict()
     g = torch.Generator().manual_seed(0)
     wav = 0.1 * torch.randn(n_utt, int(SR * SECONDS), generator=g)
     lens = torch.ones(n_utt)
+    with torch.no_grad():
+        threads, tried = pick_threads(lambda: OC.fbank_to_encoder(wav[:2], sd_cnn, sd_tr, 12, 4, n_mels=80,
+                                                                  wav_len=lens[:2]))
     times = []
     with torch.no_grad():
         for r in range(reps + 1):
@@ -114,7 +142,9 @@ def cpu_baseline(d_model, n_utt=16, reps=4):
     except OSError:
         pass
     return {"value": round(n_utt * SECONDS / med, 2), "unit": "audio-sec/sec", "cores": threads, "kind": "port",
-            "sample": f"{n_utt} utt x 15 s synthetic, fp32, median of {reps} after 1 warm-up; CPU: {model}"}
+            "threads_probe_s": tried, "os_cpu_count": os.cpu_count(), "affinity_cpus": _usable_cpus(),
+            "sample": f"{n_utt} utt x 15 s synthetic, fp32, median of {reps} after 1 warm-up; threads = fastest "
+                      f"of {sorted(tried)} on a 2-utterance probe; CPU: {model}"}
 
 
 class _LaunchProbe:
@@ -382,10 +412,8 @@ def cpu_baseline_c2(batch, n_utt=4, reps=3):
     """Oracle (numpy/PyTorch CPU restatement) of the same C2 step on n_utt x 15 s."""
     import oracle.augment as OA
     import oracle.features as OF
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    threads = max(1, min(threads, os.cpu_count() or 1))
-    torch.set_num_threads(threads)
     wav = 0.1 * torch.randn(n_utt, int(SR * SECONDS), generator=torch.Generator().manual_seed(0))
+    threads, tried = pick_threads(lambda: OF.fbank(wav[:1], deltas_on=True, n_mels=80))
     times = []
     for r in range(reps + 1):
         t0 = time.perf_counter()
@@ -397,7 +425,9 @@ def cpu_baseline_c2(batch, n_utt=4, reps=3):
             times.append(time.perf_counter() - t0)
     med = statistics.median(times)
     return {"value": round(n_utt * SECONDS / med, 2), "unit": "audio-sec/sec", "cores": threads, "kind": "port",
-            "sample": f"{n_utt} utt x 15 s synthetic, fp32, median of {reps} after 1 warm-up"}
+            "threads_probe_s": tried, "os_cpu_count": os.cpu_count(), "affinity_cpus": _usable_cpus(),
+            "sample": f"{n_utt} utt x 15 s synthetic, fp32, median of {reps} after 1 warm-up; threads = fastest "
+                      f"of {sorted(tried)} on a 1-utterance probe"}
 
 
 # ----------------------------------------------------------------- config 5
@@ -454,12 +484,12 @@ def cpu_baseline_c5(n_utt=1, reps=2):
     """Oracle (PyTorch CPU fp32 restatement, oracle/wav2vec.py) of config 5 on
     n_utt x 15 s, median of `reps` after a warm-up."""
     import oracle.wav2vec as OW
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    threads = max(1, min(threads, os.cpu_count() or 1))
-    torch.set_num_threads(threads)
     ext, wrap = build_c5("cpu")
     sde, sdw = ext.state_dict(), wrap.state_dict()
     wav = 0.1 * torch.randn(n_utt, int(SR * SECONDS), generator=torch.Generator().manual_seed(0))
+    with torch.no_grad():
+        threads, tried = pick_threads(lambda: OW.wav2vec_encode(wav[:1, :32000], sde, sdw, 2, C5_H,
+                                                                wav_lens=torch.ones(1)))
     times = []
     with torch.no_grad():
         for r in range(reps + 1):
@@ -469,7 +499,9 @@ def cpu_baseline_c5(n_utt=1, reps=2):
                 times.append(time.perf_counter() - t0)
     med = statistics.median(times)
     return {"value": round(n_utt * SECONDS / med, 2), "unit": "audio-sec/sec", "cores": threads, "kind": "port",
-            "sample": f"{n_utt} utt x 15 s synthetic, fp32, median of {reps} after 1 warm-up"}
+            "threads_probe_s": tried, "os_cpu_count": os.cpu_count(), "affinity_cpus": _usable_cpus(),
+            "sample": f"{n_utt} utt x 15 s synthetic, fp32, median of {reps} after 1 warm-up; threads = fastest "
+                      f"of {sorted(tried)} on a 2 s / 2-layer probe"}
 
 
 def _mha_flops(qkv, pk, pbu, pbv, kpm, B, T, H, dh, *a, **k):

@@ -43,7 +43,7 @@ def build_modules(d_model=256, layers=12, dropout=0.1, fused_head=True):
     from speechbrain_amd.lobes.augment import SpecAugment
     from speechbrain_amd.lobes.features import Fbank
     from speechbrain_amd.lobes.models.convolution import ConvolutionFrontEnd
-    from speechbrain_amd.lobes.models.transformer.TransformerASR import TransformerASR
+    from speechbrain_amd.lobes.models.transformer.TransformerASR import EncoderWrapper, TransformerASR
     from speechbrain_amd.nnet.linear import Linear
     from speechbrain_amd.nnet.loss.transducer_head import TransducerHeadLinear
     from speechbrain_amd.nnet.transducer.transducer_joint import Transducer_joint
@@ -52,9 +52,11 @@ def build_modules(d_model=256, layers=12, dropout=0.1, fused_head=True):
         "CNN": ConvolutionFrontEnd(input_shape=(8, 10, 80), num_blocks=2, num_layers_per_block=1,
                                    out_channels=(64, 32), kernel_sizes=(3, 3), strides=(2, 2),
                                    residuals=(False, False), dropout=dropout),
-        "enc": TransformerASR(tgt_vocab=V, input_size=640, d_model=d_model, nhead=4, num_encoder_layers=layers,
-                              num_decoder_layers=0, d_ffn=1024, dropout=dropout, encoder_module="conformer",
-                              attention_type="RelPosMHAXL", normalize_before=True, causal=False),
+        # EncoderWrapper: encode() as forward, so DDP can wrap the encoder
+        "enc": EncoderWrapper(TransformerASR(tgt_vocab=V, input_size=640, d_model=d_model, nhead=4,
+                                             num_encoder_layers=layers, num_decoder_layers=0, d_ffn=1024,
+                                             dropout=dropout, encoder_module="conformer",
+                                             attention_type="RelPosMHAXL", normalize_before=True, causal=False)),
         "enc_lin": Linear(input_size=d_model, n_neurons=J),
         "dec": torch.nn.GRU(V - 1, J, num_layers=1, batch_first=True),
         "dec_lin": Linear(input_size=J, n_neurons=J, bias=False),
@@ -62,6 +64,10 @@ def build_modules(d_model=256, layers=12, dropout=0.1, fused_head=True):
         "transducer_lin": (TransducerHeadLinear(input_size=J, n_neurons=V, bias=False) if fused_head
                            else Linear(input_size=J, n_neurons=V, bias=False)),
     }
+    # TransformerASR always builds the decoder-side target embedding
+    # (TransformerASR.py:136); the transducer recipe never calls it, and DDP
+    # without find_unused_parameters rejects a parameter that gets no gradient
+    mods["enc"].transformer.custom_tgt_module.requires_grad_(False)
     from speechbrain_amd.processing.features import InputNormalization
     hp = {"compute_features": Fbank(sample_rate=SR, n_fft=400, n_mels=80),
           "normalize": InputNormalization(norm_type="global", update_until_epoch=4),
@@ -89,7 +95,7 @@ def brain_class(fused_head=True):
                 if stage == Stage.TRAIN:
                     feats = self.hparams["augmentation"](feats)
             src = self.modules.CNN(feats)
-            x = self.modules.enc.encode(src, wav_lens)
+            x = self.modules.enc(src, wav_lens)
             tn = self.modules.enc_lin(x)  # (B, T, J)
             e = F.one_hot(tokens_bos, V)[..., 1:].float()  # Embedding(consider_as_one_hot, blank 0)
             h, _ = self.modules.dec(e)

@@ -95,13 +95,15 @@ int sbk_deltas(const float* x, float* y, int N, int T, int F, int window_length,
 int sbk_context_window(const float* x, float* y, int N, int T, int F, int left, int right, void* stream);
 
 /* SpecAugment.forward (speechbrain/lobes/augment.py:106-201) on x (N, T, F)
- * fp32, in place: bicubic time warp (c, w; c < 0 = none) through `tmp`,
- * then frequency / time masks given as device int32 (N, n, 2) [len, pos]
- * arrays drawn on the host, filled with 0 or the running means
+ * fp32, in place: time warp (c, w; c < 0 = none; warp_mode 0 bicubic,
+ * 1 bilinear — the align_corners interpolate modes of :134-148) through
+ * `tmp`, then frequency / time masks given as device int32 (N, n, 2)
+ * [len, pos] arrays drawn on the host, filled with 0 or the running means
  * (use_mean; `partial` scratch of 2*N*ceil(T/16) floats; n_fcells = number
  * of frequency-masked cells). */
-int sbk_specaugment(float* x, int N, int T, int F, int c, int w, float* tmp, const int* fmask, int n_fmask,
-                    const int* tmask, int n_tmask, int use_mean, float* partial, long long n_fcells, void* stream);
+int sbk_specaugment(float* x, int N, int T, int F, int c, int w, int warp_mode, float* tmp, const int* fmask,
+                    int n_fmask, const int* tmask, int n_tmask, int use_mean, float* partial, long long n_fcells,
+                    void* stream);
 
 /* ------------------------------------------------------------ RNN-T loss */
 
@@ -309,6 +311,15 @@ int sbk_relpos_attention(int dtype_bf16, const void* qkv, const void* pk, const 
 int sbk_relpos_attention_ld(int dtype_bf16, const void* qkv, const void* pk, int ldp, const float* pbu,
                             const float* pbv, const unsigned char* kpm, int B, int T, int H, int dh, float scale,
                             void* out, float* probs, void* stream);
+/* sbk_relpos_attention_ld with an additive fp32 attention mask (attn_mask,
+ * attention.py:598-611; bool masks as 0 / -inf): score (b, h, i, j) +=
+ * am[b * am_sb + h * am_sh + i * T + j] after the scale, before the key
+ * padding and the softmax.  2-D (T, T) mask: am_sb = am_sh = 0; 3-D
+ * (B*H, T, T): am_sb = H*T*T, am_sh = T*T.  Probabilities optional. */
+int sbk_relpos_attention_mask(int dtype_bf16, const void* qkv, const void* pk, int ldp, const float* pbu,
+                              const float* pbv, const unsigned char* kpm, const float* am, long long am_sb,
+                              long long am_sh, int B, int T, int H, int dh, float scale, void* out, float* probs,
+                              void* stream);
 /* LDS bytes one attention workgroup needs (host-side capacity check). */
 long long sbk_relpos_attention_lds(int dtype_bf16, int T, int dh);
 
@@ -356,7 +367,7 @@ int sbk_inorm_apply(const float* x, int B, int T, int F, const float* mean, cons
  * these entry points are the element-wise / reduction / layout parts.  *_bf16 flags select bf16 (1)
  * or fp32 (0) storage per operand. */
 
-/* LayerNorm backward over rows of x (M, D) fp32, D <= 2560 (nn.LayerNorm as
+/* LayerNorm backward over rows of x (M, D) fp32, D <= 16384 (nn.LayerNorm as
  * used by normalization.py:172-223, Conformer.py:178,194,340 and the ConvBlock
  * (freq x channel) norm, convolution.py:169-175):
  *   dx = rstd (dy g - mean(dy g) - xhat mean(dy g xhat)) (+ dres if non-null);
@@ -366,7 +377,8 @@ int sbk_layernorm_bwd_blocks(int M);
 int sbk_layernorm_bwd(const float* x, const void* dy, int dy_bf16, int M, int D, const float* g, float eps,
                       const float* dres, float* dx, float* part, void* stream);
 
-/* LayerNorm forward for rows up to D = 2560 (the ConvBlock norm over freq x channels). */
+/* LayerNorm forward over rows of any width (the ConvBlock norm over freq x
+ * channels: a wave per row up to D = 2560, a workgroup per row beyond). */
 int sbk_layernorm_wide(const float* x, int M, int D, const float* g, const float* b, float eps, void* y, int y_bf16,
                        void* stream);
 
@@ -426,13 +438,17 @@ int sbk_relpos_softmax_bwd_pad(int dtype_bf16, const float* P, const void* dP, i
 int sbk_attn_dqkv(const float* dq_ac, const float* dq_bd, const float* dk, const float* dv, int B, int H, int T,
                   int dh, int Tp, int dhp, void* out, int out_bf16, void* stream);
 
-/* Conv2d 3x3 stride 2 "same" reflect padding (CNN.py:616-700) as a GEMM:
- * x (B, Ti, Fi, Ci) -> col (B*To*Fo, ldcol >= 9*Ci), columns ordered (kt, kf, ci),
- * zero beyond 9*Ci; col2im is its adjoint (reflected taps folded back), dx (B, Ti, Fi, Ci). */
-int sbk_im2col3s2(const void* x, int x_bf16, int B, int Ti, int Fi, int Ci, int ldcol, void* col, int col_bf16,
-                  void* stream);
-int sbk_col2im3s2(const void* dcol, int dcol_bf16, int B, int Ti, int Fi, int Ci, int ldcol, void* dx, int dx_bf16,
-                  void* stream);
+/* Conv2d with "same" reflect padding (CNN.py:616-700, get_padding_elem
+ * :1459-1481) as a GEMM, any kernel (kt time x kf freq taps), stride (st,
+ * sf) and padding (pt, pf < the input size): x (B, Ti, Fi, Ci) -> col
+ * (B*To*Fo, ldcol >= kt*kf*Ci), columns ordered (time tap, freq tap, ci),
+ * zero beyond kt*kf*Ci; To = (Ti + 2 pt - kt) / st + 1.  col2im is its
+ * adjoint (reflected taps folded back, a deterministic gather), dx
+ * (B, Ti, Fi, Ci). */
+int sbk_im2col(const void* x, int x_bf16, int B, int Ti, int Fi, int Ci, int kt, int kf, int st, int sf, int pt,
+               int pf, int ldcol, void* col, int col_bf16, void* stream);
+int sbk_col2im(const void* dcol, int dcol_bf16, int B, int Ti, int Fi, int Ci, int kt, int kf, int st, int sf, int pt,
+               int pf, int ldcol, void* dx, int dx_bf16, void* stream);
 
 /* Transducer_joint "sum" (transducer_joint.py:57-95): z[b,t,u,:] = act(tn[b,t,:] + pn[b,u,:]),
  * act 0 none, 3 LeakyReLU(slope), 5 tanh, 6 ReLU; tn (B, T, J), pn (B, U1, J) fp32, z fp32/bf16.

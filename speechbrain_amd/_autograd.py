@@ -340,10 +340,13 @@ class RelPosAttentionFn(Function):
     same kernels in both dtypes."""
 
     @staticmethod
-    def forward(ctx, qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale, p=0.0):
+    def forward(ctx, qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale, p=0.0, am=None):
         qkv, pk = _cont(qkv), _cont(pk)
         dt = qkv.dtype
-        o, P = _enc.relpos_attention(qkv, pk, pbu.detach(), pbv.detach(), kpm, B, T, H, dh, scale, need_probs=True)
+        # am: additive attn_mask (_enc.attn_mask_arg), a constant: masked
+        # probabilities are 0, so the backward needs nothing of it
+        o, P = _enc.relpos_attention(qkv, pk, pbu.detach(), pbv.detach(), kpm, B, T, H, dh, scale, need_probs=True,
+                                     am=am)
         seed = 0
         attn = P
         if p > 0:
@@ -403,73 +406,95 @@ class RelPosAttentionFn(Function):
         # pos-bias gradients: sums of dq_ac / dq_bd over (b, t) (padded rows are zero)
         dpbv = rowsum_batched(dq_bd)[:, :dh].reshape(pbv.shape)
         dpbu = rowsum_batched(rowsum(dq_ac.view(B, H * Tp * dhp)).view(H, Tp, dhp))[:, :dh].reshape(pbu.shape)
-        return dqkv, dpk, dpbu, dpbv, None, None, None, None, None, None, None
+        return dqkv, dpk, dpbu, dpbv, None, None, None, None, None, None, None, None
 
 
 # --------------------------------------------------------------- ConvBlock
 class ConvBlockFn(Function):
-    """ConvBlock with one layer (convolution.py:112-175): Conv2d 3x3 stride 2
-    "same" reflect padding (CNN.py:616-700) -> LayerNorm over (freq, chan)
-    -> LeakyReLU, as im2col (HIP) + MFMA GEMM + wide LayerNorm + activation.
-    x (B, Ti, Fi, Ci) -> (B, To, Fo, Co)."""
+    """One ConvBlock layer (convolution.py:112-175): Conv2d with "same"
+    reflect padding (CNN.py:616-700) -> [LayerNorm over (freq, chan)] ->
+    [LeakyReLU], as im2col (HIP) + MFMA GEMM + wide LayerNorm + activation.
+    geom = (kT, kF, sT, sF): time / freq kernel and stride (odd kernels;
+    padding (k - 1) / 2, get_padding_elem :1459-1481).  ln_w None: no norm
+    (ln_b, eps ignored); slope None: no activation (the residual branch's
+    1x1 conv + norm).  x (B, Ti, Fi, Ci) -> (B, To, Fo, Co)."""
 
     @staticmethod
-    def forward(ctx, x, w, bias, ln_w, ln_b, eps, slope, dtype, out_dtype):
+    def forward(ctx, x, w, bias, ln_w, ln_b, eps, slope, dtype, out_dtype, geom):
         x = _cont(x)
+        kt, kf, st, sf = geom
+        pt, pf = (kt - 1) // 2, (kf - 1) // 2
         B, Ti, Fi, Ci = x.shape
         Co = w.shape[0]
-        To, Fo = (Ti - 1) // 2 + 1, (Fi - 1) // 2 + 1
+        To, Fo = (Ti + 2 * pt - kt) // st + 1, (Fi + 2 * pf - kf) // sf + 1
         vec = 8 if dtype == _bf16 else 4
-        ldcol = -(-9 * Ci // vec) * vec
+        K = kt * kf * Ci
+        ldcol = -(-K // vec) * vec
         N = B * To * Fo
         L = lib()
         s = stream_of(x)
         col = torch.empty(N, ldcol, device=x.device, dtype=dtype)
-        check(L.sbk_im2col3s2(ptr(x), _bf(x), B, Ti, Fi, Ci, ldcol, ptr(col), _bf(col), s), "sbk_im2col3s2")
-        # weight (Co, Ci, kf, kt) -> (Co, kt, kf, Ci) -> (Co, ldcol)
+        check(L.sbk_im2col(ptr(x), _bf(x), B, Ti, Fi, Ci, kt, kf, st, sf, pt, pf, ldcol, ptr(col), _bf(col), s),
+              "sbk_im2col")
+        # weight (Co, Ci, kF, kT) -> (Co, kT, kF, Ci) -> (Co, ldcol)
         wp = torch.zeros(Co, ldcol, device=x.device, dtype=_f32)
-        wp[:, : 9 * Ci] = w.detach().permute(0, 3, 2, 1).reshape(Co, 9 * Ci)
+        wp[:, :K] = w.detach().permute(0, 3, 2, 1).reshape(Co, K)
         wk = _as(wp, dtype)
-        c = _enc.gemm(col, wk, bias=None if bias is None else bias.detach(), out_dtype=_f32)
-        c2 = c.view(B * To, Fo * Co)
-        n = torch.empty(B * To, Fo * Co, device=x.device, dtype=_f32)
-        check(L.sbk_layernorm_wide(ptr(c2), B * To, Fo * Co, ptr(ln_w.detach()), ptr(ln_b.detach()), float(eps),
-                                   ptr(n), 0, s), "sbk_layernorm_wide")
-        y = torch.empty(B * To, Fo * Co, device=x.device, dtype=out_dtype)
-        check(L.sbk_act_fwd(3, ptr(n), 0, B * To, Fo * Co, ptr(y), _bf(y), float(slope), s), "sbk_act_fwd")
-        ctx.save_for_backward(col, wk, c2, n, ln_w)
-        ctx.dims = (B, Ti, Fi, Ci, Co, To, Fo, ldcol, eps, slope, bias is not None, tuple(w.shape), x.dtype)
+        D = Fo * Co
+        has_ln, has_act = ln_w is not None, slope is not None
+        c = _enc.gemm(col, wk, bias=None if bias is None else bias.detach(),
+                      out_dtype=_f32 if (has_ln or has_act) else out_dtype)
+        c2 = c.view(B * To, D)
+        n = c2
+        if has_ln:
+            n = torch.empty(B * To, D, device=x.device, dtype=_f32 if has_act else out_dtype)
+            check(L.sbk_layernorm_wide(ptr(c2), B * To, D, ptr(ln_w.detach()), ptr(ln_b.detach()), float(eps),
+                                       ptr(n), _bf(n), s), "sbk_layernorm_wide")
+        y = n
+        if has_act:
+            y = torch.empty(B * To, D, device=x.device, dtype=out_dtype)
+            check(L.sbk_act_fwd(3, ptr(n), 0, B * To, D, ptr(y), _bf(y), float(slope), s), "sbk_act_fwd")
+        ctx.save_for_backward(col, wk, c2 if has_ln else None, n if has_act else None, ln_w)
+        ctx.dims = (B, Ti, Fi, Ci, Co, To, Fo, ldcol, eps, slope, bias is not None, tuple(w.shape), x.dtype,
+                    (kt, kf, st, sf, pt, pf))
         return y.view(B, To, Fo, Co)
 
     @staticmethod
     def backward(ctx, dy):
         col, wk, c2, n, ln_w = ctx.saved_tensors
-        B, Ti, Fi, Ci, Co, To, Fo, ldcol, eps, slope, has_bias, wshape, xdt = ctx.dims
+        B, Ti, Fi, Ci, Co, To, Fo, ldcol, eps, slope, has_bias, wshape, xdt, (kt, kf, st, sf, pt, pf) = ctx.dims
         L = lib()
         s = stream_of(col)
-        dy = _cont(dy).view(B * To, Fo * Co)
-        dn = torch.empty(B * To, Fo * Co, device=col.device, dtype=_f32)
-        check(L.sbk_act_bwd(3, ptr(n), 0, ptr(dy), _bf(dy), B * To, Fo * Co, ptr(dn), 0, float(slope), s),
-              "sbk_act_bwd")
-        nblk = int(L.sbk_layernorm_bwd_blocks(B * To))
         D = Fo * Co
-        part = torch.empty(nblk * 2 * D, device=col.device, dtype=_f32)
-        dc = torch.empty(B * To, D, device=col.device, dtype=_f32)
-        check(L.sbk_layernorm_bwd(ptr(c2), ptr(dn), 0, B * To, D, ptr(ln_w.detach()), float(eps), None, ptr(dc),
-                                  ptr(part), s), "sbk_layernorm_bwd")
-        gb = colsum(part, nblk, 2 * D)
-        dlw, dlb = gb[:D].view_as(ln_w), gb[D:].view_as(ln_w)
-        dc = dc.view(B * To * Fo, Co)
+        dy = _cont(dy).view(B * To, D)
+        dn = dy
+        if slope is not None:
+            dn = torch.empty(B * To, D, device=col.device, dtype=_f32)
+            check(L.sbk_act_bwd(3, ptr(n), _bf(n), ptr(dy), _bf(dy), B * To, D, ptr(dn), 0, float(slope), s),
+                  "sbk_act_bwd")
+        dlw = dlb = None
+        dc = dn
+        if ln_w is not None:
+            nblk = int(L.sbk_layernorm_bwd_blocks(B * To))
+            part = torch.empty(nblk * 2 * D, device=col.device, dtype=_f32)
+            dc = torch.empty(B * To, D, device=col.device, dtype=_f32)
+            check(L.sbk_layernorm_bwd(ptr(c2), ptr(dn), _bf(dn), B * To, D, ptr(ln_w.detach()), float(eps), None,
+                                      ptr(dc), ptr(part), s), "sbk_layernorm_bwd")
+            gb = colsum(part, nblk, 2 * D)
+            dlw, dlb = gb[:D].view_as(ln_w), gb[D:].view_as(ln_w)
+        dc = _cont(dc).view(B * To * Fo, Co)
         g = _as(dc, col.dtype)
+        K = kt * kf * Ci
         dwp = wgrad(g, col)  # (Co, ldcol)
-        dw = dwp[:, : 9 * Ci].reshape(Co, 3, 3, Ci).permute(0, 3, 2, 1).reshape(wshape)
+        dw = dwp[:, :K].reshape(Co, kt, kf, Ci).permute(0, 3, 2, 1).reshape(wshape)
         db = rowsum(dc) if has_bias else None
         dx = None
         if ctx.needs_input_grad[0]:
             dcol = dgrad(g, wk)  # (N, ldcol)
             dx = torch.empty(B, Ti, Fi, Ci, device=col.device, dtype=xdt)
-            check(L.sbk_col2im3s2(ptr(dcol), _bf(dcol), B, Ti, Fi, Ci, ldcol, ptr(dx), _bf(dx), s), "sbk_col2im3s2")
-        return dx, dw, db, dlw, dlb, None, None, None, None
+            check(L.sbk_col2im(ptr(dcol), _bf(dcol), B, Ti, Fi, Ci, kt, kf, st, sf, pt, pf, ldcol, ptr(dx), _bf(dx),
+                               s), "sbk_col2im")
+        return dx, dw, db, dlw, dlb, None, None, None, None, None
 
 
 # ---------------------------------------------------------- transducer joint

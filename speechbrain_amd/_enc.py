@@ -541,31 +541,60 @@ def conv_frontend2(x, blk1, blk2, wperm2, out_dtype):
 @torch.library.custom_op("sbk::relpos_attention", mutates_args=())
 def _relpos_attention_op(qkv: torch.Tensor, pk: torch.Tensor, pbu: torch.Tensor, pbv: torch.Tensor,
                          kpm: Optional[torch.Tensor], B: int, T: int, H: int, dh: int, scale: float,
-                         need_probs: bool) -> tuple[torch.Tensor, torch.Tensor]:
+                         need_probs: bool, am: Optional[torch.Tensor], am_sb: int,
+                         am_sh: int) -> tuple[torch.Tensor, torch.Tensor]:
     d = H * dh
     out = torch.empty(B * T, d, device=qkv.device, dtype=qkv.dtype)
     probs = torch.empty(B, H, T, T, device=qkv.device, dtype=_f32) if need_probs else qkv.new_empty(0, dtype=_f32)
-    rc = lib().sbk_relpos_attention_ld(int(_is_bf16(qkv)), ptr(qkv), ptr(pk), pk.stride(0), ptr(pbu), ptr(pbv),
-                                       ptr(kpm), B, T, H, dh, float(scale), ptr(out),
-                                       ptr(probs) if need_probs else None, stream_of(qkv))
+    if am is None:
+        rc = lib().sbk_relpos_attention_ld(int(_is_bf16(qkv)), ptr(qkv), ptr(pk), pk.stride(0), ptr(pbu), ptr(pbv),
+                                           ptr(kpm), B, T, H, dh, float(scale), ptr(out),
+                                           ptr(probs) if need_probs else None, stream_of(qkv))
+    else:
+        rc = lib().sbk_relpos_attention_mask(int(_is_bf16(qkv)), ptr(qkv), ptr(pk), pk.stride(0), ptr(pbu), ptr(pbv),
+                                             ptr(kpm), ptr(am), am_sb, am_sh, B, T, H, dh, float(scale), ptr(out),
+                                             ptr(probs) if need_probs else None, stream_of(qkv))
     check(rc, "sbk_relpos_attention")
     return out, probs
 
 
 @_relpos_attention_op.register_fake
-def _(qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale, need_probs):
+def _(qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale, need_probs, am, am_sb, am_sh):
     return (qkv.new_empty(B * T, H * dh),
             qkv.new_empty(B, H, T, T, dtype=_f32) if need_probs else qkv.new_empty(0, dtype=_f32))
 
 
-def relpos_attention(qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale, need_probs=False):
+def attn_mask_arg(attn_mask, B, T, H, device):
+    """RelPosMHAXL's attn_mask (attention.py:598-611) as the kernel's additive
+    fp32 mask: (mask (T, T) or (B|1, H, T, T), batch stride, head stride),
+    bool masks as 0 / -inf (masked_fill(-inf) == adding -inf); None -> None."""
+    if attn_mask is None:
+        return None
+    m = attn_mask.to(device)
+    if m.dtype == torch.bool:
+        m = torch.zeros(m.shape, device=device, dtype=_f32).masked_fill_(m, -float("inf"))
+    else:
+        m = m.to(_f32)
+    if m.dim() == 2:
+        if tuple(m.shape) != (T, T):
+            raise ValueError(f"attn_mask {tuple(m.shape)} != ({T}, {T})")
+        return m.contiguous(), 0, 0
+    m = m.reshape(-1, H, T, T).contiguous()  # the reference's view(-1, num_heads, qlen, klen)
+    if m.shape[0] not in (1, B):
+        raise ValueError(f"attn_mask batch {m.shape[0]} does not broadcast to {B}")
+    return m, (H * T * T if m.shape[0] == B else 0), T * T
+
+
+def relpos_attention(qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale, need_probs=False, am=None):
     """Fused RelPosMHAXL core.  qkv: (B*T, 3d) head-interleaved, pk: (2T-1, d),
-    both bf16 or fp32; returns (out (B*T, d) in qkv.dtype, probs or None)."""
+    both bf16 or fp32; am: attn_mask_arg(...) or None.  Returns (out (B*T, d)
+    in qkv.dtype, probs or None)."""
     d = H * dh
     if pk.stride(-1) != 1 or pk.shape[-1] != d:
         raise ValueError("pk must be (2T-1, d) with unit column stride")
+    m, sb, sh = am if am is not None else (None, 0, 0)
     out, probs = torch.ops.sbk.relpos_attention(qkv, pk, pbu, pbv, kpm, int(B), int(T), int(H), int(dh),
-                                                float(scale), bool(need_probs))
+                                                float(scale), bool(need_probs), m, int(sb), int(sh))
     return out, (probs if need_probs else None)
 
 

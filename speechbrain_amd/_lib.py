@@ -90,7 +90,7 @@ SIGNATURES = {
     "sbk_mx_quant": [_vp, _i, _ll, _i, _i, _vp, _ll, _vp, _ll, _vp],
     "sbk_mx_dequant": [_vp, _ll, _vp, _ll, _i, _i, _vp, _vp],
     # augment.hip
-    "sbk_specaugment": [_vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _i, _vp, _ll, _vp],
+    "sbk_specaugment": [_vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _i, _vp, _ll, _vp],
     # rnnt.hip
     "sbk_rnnt_forward": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp],
     "sbk_rnnt_workspace_floats": [_i, _i, _i],
@@ -99,6 +99,7 @@ SIGNATURES = {
     # attention.hip
     "sbk_relpos_attention": [_i, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _vp],
     "sbk_relpos_attention_lds": [_i, _i, _i],
+    "sbk_relpos_attention_mask": [_i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _ll, _ll, _i, _i, _i, _i, _f, _vp, _vp, _vp],
     "sbk_relpos_attention_ld": [_i, _vp, _vp, _i, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _vp],
     # norm.hip
     "sbk_inorm_slices": [_i],
@@ -124,8 +125,8 @@ SIGNATURES = {
     "sbk_dwconv_fwd": [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _i, _vp],
     "sbk_dwconv_wgrad_chunks": [_i, _i],
     "sbk_dwconv_bwd": [_vp, _i, _vp, _i, _i, _i, _vp, _i, _i, _vp, _i, _vp, _vp],
-    "sbk_im2col3s2": [_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp],
-    "sbk_col2im3s2": [_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp],
+    "sbk_im2col": [_vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _vp],
+    "sbk_col2im": [_vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _vp],
     "sbk_joint_fwd": [_vp, _vp, _i, _i, _i, _i, _i, _f, _vp, _i, _vp],
     "sbk_dropout_add": [_vp, _i, _vp, _ll, _i, _vp, _f, _f, ctypes.c_ulonglong, _vp, _i, _vp],
     "sbk_joint_bwd": [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp],

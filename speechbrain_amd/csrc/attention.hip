@@ -113,7 +113,9 @@ __global__ void __launch_bounds__(256, SBK_ATT_MINW) relpos_flash_kernel(const T
                                                            const float* __restrict__ pbv,
                                                            const uint8_t* __restrict__ kpm, int B, int Tn, int H,
                                                            int dh, float scale, T* __restrict__ out,
-                                                           float* __restrict__ probs, int vec_ok, int ldp) {
+                                                           float* __restrict__ probs, int vec_ok, int ldp,
+                                                           const float* __restrict__ am, long long am_sb,
+                                                           long long am_sh) {
   using Tr = MT<T>;
   using L = FlashLds<T, DHP>;
   constexpr int KR = L::KR, VR = L::VR, VEC = Tr::VEC;
@@ -349,6 +351,9 @@ __global__ void __launch_bounds__(256, SBK_ATT_MINW) relpos_flash_kernel(const T
       const bool masked_chunk = __builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(Ms)[KC]) != 0;
       float sc[4][4];
       float cmax = -INFINITY;
+      // additive attention mask (attn_mask, attention.py:604-611), scaled into
+      // the log2 domain of the scores; bool masks arrive as 0 / -inf
+      const float* amrow = am ? am + b * am_sb + h * am_sh + (long long)min(my_i, Tn - 1) * Tn : nullptr;
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -356,6 +361,7 @@ __global__ void __launch_bounds__(256, SBK_ATT_MINW) relpos_flash_kernel(const T
           const int jj = 16 * t + 4 * g + r;
           float v = acc_s[t][r] + Gw[(15 - c16 + jj) * GS + c16];
           if (masked_chunk) v += Ms[jj];
+          if (amrow && j0 + jj < Tn) v += amrow[j0 + jj] * 1.4426950408889634f;
           sc[t][r] = v;
           cmax = fmaxf(cmax, v);
         }
@@ -851,7 +857,8 @@ int launch_dma(const void* qkv, const void* pk, int ldp, const float* pbu, const
 
 template <typename T, int DHP>
 int launch(const void* qkv, const void* pk, int ldp, const float* pbu, const float* pbv, const uint8_t* kpm, int B,
-           int Tn, int H, int dh, float scale, void* out, float* probs, hipStream_t s) {
+           int Tn, int H, int dh, float scale, void* out, float* probs, hipStream_t s, const float* am = nullptr,
+           long long am_sb = 0, long long am_sh = 0) {
   constexpr size_t lds = FlashLds<T, DHP>::bytes;
   static_assert(lds <= 160 * 1024, "LDS budget");
   const int grid = B * H * ((Tn + QB - 1) / QB);
@@ -862,11 +869,11 @@ int launch(const void* qkv, const void* pk, int ldp, const float* pbu, const flo
   if (probs)
     hipLaunchKernelGGL((relpos_flash_kernel<T, DHP, true>), dim3(grid), dim3(256), lds, s,
                        reinterpret_cast<const T*>(qkv), reinterpret_cast<const T*>(pk), pbu, pbv, kpm, B, Tn, H, dh,
-                       scale, reinterpret_cast<T*>(out), probs, vec_ok, ldp);
+                       scale, reinterpret_cast<T*>(out), probs, vec_ok, ldp, am, am_sb, am_sh);
   else
     hipLaunchKernelGGL((relpos_flash_kernel<T, DHP, false>), dim3(grid), dim3(256), lds, s,
                        reinterpret_cast<const T*>(qkv), reinterpret_cast<const T*>(pk), pbu, pbv, kpm, B, Tn, H, dh,
-                       scale, reinterpret_cast<T*>(out), probs, vec_ok, ldp);
+                       scale, reinterpret_cast<T*>(out), probs, vec_ok, ldp, am, am_sb, am_sh);
   SBK_CHECK_LAUNCH();
   return 0;
 }
@@ -896,6 +903,29 @@ SBK_API int sbk_relpos_attention(int dtype_bf16, const void* qkv, const void* pk
                                  const uint8_t* kpm, int B, int Tn, int H, int dh, float scale, void* out, float* probs,
                                  void* stream) {
   return sbk_relpos_attention_ld(dtype_bf16, qkv, pk, H * dh, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, stream);
+}
+
+// sbk_relpos_attention_ld with an additive attention mask am (fp32): score
+// (b, h, i, j) += am[b * am_sb + h * am_sh + i * T + j] after the 1/sqrt(d)
+// scale, before the key-padding mask and the softmax (attention.py:598-611;
+// a bool mask is passed as 0 / -inf).  A 2-D (T, T) mask has am_sb = am_sh
+// = 0, a 3-D (B*H, T, T) one am_sb = H*T*T, am_sh = T*T.  General kernel.
+SBK_API int sbk_relpos_attention_mask(int dtype_bf16, const void* qkv, const void* pk, int ldp, const float* pbu,
+                                      const float* pbv, const uint8_t* kpm, const float* am, long long am_sb,
+                                      long long am_sh, int B, int Tn, int H, int dh, float scale, void* out,
+                                      float* probs, void* stream) {
+  if (B <= 0 || Tn <= 0 || H <= 0 || dh <= 0 || dh > 128 || ldp < H * dh || !am || am_sb < 0 || am_sh < 0)
+    return SBK_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype_bf16)
+    return dh <= 64 ? launch<bf16_t, 64>(qkv, pk, ldp, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s, am, am_sb,
+                                         am_sh)
+                    : launch<bf16_t, 128>(qkv, pk, ldp, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s, am, am_sb,
+                                          am_sh);
+  return dh <= 64 ? launch<float, 64>(qkv, pk, ldp, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s, am, am_sb,
+                                      am_sh)
+                  : launch<float, 128>(qkv, pk, ldp, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s, am, am_sb,
+                                       am_sh);
 }
 
 #ifdef SBK_PROBE_TL

@@ -1,4 +1,4 @@
-// SpecAugment kernels: bicubic time warp, frequency/time masks, mean fill.
+// SpecAugment kernels: bicubic / bilinear time warp, frequency/time masks, mean fill.
 //
 // Reference: speechbrain/lobes/augment.py:106-201 (SpecAugment.forward,
 // time_warp, mask_along_axis).  The random draws (warp centre c and width w,
@@ -46,7 +46,11 @@ __device__ __forceinline__ bool in_masks(const int* m, int n, int nm, int i) {
   return false;
 }
 
-// One block per (n, tile of TT output rows); threads over F.
+// One block per (n, tile of TT output rows); threads over F.  CUBIC: the
+// bicubic resize (A = -0.75, border-clamped taps); else bilinear
+// (time_warp_mode="bilinear": two taps, lambda0 = 1 - lambda1, the upper
+// tap clamped to the last row) — torch's upsample_*2d with align_corners.
+template <bool CUBIC>
 __global__ void __launch_bounds__(256) warp_kernel(const float* __restrict__ x, float* __restrict__ y, int N, int T,
                                                    int F, int c, int w, int TT, const int* __restrict__ fmask,
                                                    int n_fmask, float* __restrict__ partial) {
@@ -77,21 +81,35 @@ __global__ void __launch_bounds__(256) warp_kernel(const float* __restrict__ x, 
       const float fl = floorf(real);
       const float tt = real - fl;
       const int i0 = (int)fl;
-      wt[0] = cubic2(tt + 1.f);
-      wt[1] = cubic1(tt);
-      wt[2] = cubic1(1.f - tt);
-      wt[3] = cubic2(2.f - tt);
+      if (CUBIC) {
+        wt[0] = cubic2(tt + 1.f);
+        wt[1] = cubic1(tt);
+        wt[2] = cubic1(1.f - tt);
+        wt[3] = cubic2(2.f - tt);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) idx[k] = min(max(i0 - 1 + k, 0), in_rows - 1);
+        for (int k = 0; k < 4; ++k) idx[k] = min(max(i0 - 1 + k, 0), in_rows - 1);
+      } else {
+        const float l1 = fminf(fmaxf(tt, 0.f), 1.f);
+        wt[0] = 1.f - l1;
+        wt[1] = l1;
+        wt[2] = wt[3] = 0.f;
+        idx[0] = i0;
+        idx[1] = i0 + (i0 < in_rows - 1 ? 1 : 0);
+        idx[2] = idx[3] = i0;
+      }
     }
     for (int f = threadIdx.x; f < F; f += blockDim.x) {
       float v;
       if (in_rows == out_rows) {
         v = xn[(long long)(src0 + dst) * F + f];
       } else {
-        v = 0.f;
+        if (CUBIC) {
+          v = 0.f;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v += wt[k] * xn[(long long)(src0 + idx[k]) * F + f];
+          for (int k = 0; k < 4; ++k) v += wt[k] * xn[(long long)(src0 + idx[k]) * F + f];
+        } else {
+          v = wt[0] * xn[(long long)(src0 + idx[0]) * F + f] + wt[1] * xn[(long long)(src0 + idx[1]) * F + f];
+        }
       }
       yn[(long long)t * F + f] = v;
       s_all += v;
@@ -184,23 +202,29 @@ __global__ void __launch_bounds__(256) apply_kernel(const float* src, float* x, 
 }  // namespace
 
 // Full SpecAugment application on x (N, T, F) fp32, in place.
-//   warp: c, w (warp skipped when c < 0); tmp: (N, T, F) scratch, required when warping;
+//   warp: c, w (warp skipped when c < 0), warp_mode 0 bicubic / 1 bilinear;
+//   tmp: (N, T, F) scratch, required when warping;
 //   fmask (N, n_fmask, 2) / tmask (N, n_tmask, 2) int32 [len, pos] device arrays (or n_* = 0);
 //   use_mean: fill with the running means (replace_with_zero=False), else 0;
 //   partial: scratch of 2 * N * ceil(T/16) floats (when use_mean);
 //   n_fcells: number of frequency-masked cells (host-computed, for the second mean).
-SBK_API int sbk_specaugment(float* x, int N, int T, int F, int c, int w, float* tmp, const int* fmask, int n_fmask,
+SBK_API int sbk_specaugment(float* x, int N, int T, int F, int c, int w, int warp_mode, float* tmp, const int* fmask,
+                            int n_fmask,
                             const int* tmask, int n_tmask, int use_mean, float* partial, long long n_fcells,
                             void* stream) {
-  if (N <= 0 || T <= 0 || F <= 0) return SBK_ERR_ARG;
+  if (N <= 0 || T <= 0 || F <= 0 || warp_mode < 0 || warp_mode > 1) return SBK_ERR_ARG;
   const int TT = 16;
   const int nblk = N * ((T + TT - 1) / TT);
   hipStream_t s = (hipStream_t)stream;
   const float* src = x;
   if (c >= 0) {
     if (!tmp || c <= 0 || c >= T || w <= 0 || w >= T) return SBK_ERR_ARG;
-    hipLaunchKernelGGL(warp_kernel, dim3(nblk), dim3(256), 0, s, x, tmp, N, T, F, c, w, TT, fmask, n_fmask,
-                       use_mean ? partial : nullptr);
+    if (warp_mode == 0)
+      hipLaunchKernelGGL(warp_kernel<true>, dim3(nblk), dim3(256), 0, s, x, tmp, N, T, F, c, w, TT, fmask, n_fmask,
+                         use_mean ? partial : nullptr);
+    else
+      hipLaunchKernelGGL(warp_kernel<false>, dim3(nblk), dim3(256), 0, s, x, tmp, N, T, F, c, w, TT, fmask, n_fmask,
+                         use_mean ? partial : nullptr);
     SBK_CHECK_LAUNCH();
     src = tmp;
   } else if (use_mean) {

@@ -161,6 +161,72 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
+// Rows wider than 2560 (the default ConvolutionFrontEnd's first block:
+// LayerNorm over 80 freq x 128 channels = 10240): one workgroup per row,
+// three strided passes over the row (mean, variance, output) re-reading it
+// from L2.
+__global__ void __launch_bounds__(256) ln_fwd_row_kernel(const float* __restrict__ x, int M, int D,
+                                                         const float* __restrict__ g, const float* __restrict__ b,
+                                                         float eps, void* __restrict__ y, int y_bf16) {
+  __shared__ float red[16];
+  for (long long row = blockIdx.x; row < M; row += gridDim.x) {
+    const float* xr = x + row * D;
+    float s = 0.f;
+    for (int c = threadIdx.x; c < D; c += blockDim.x) s += xr[c];
+    const float mean = block_sum(s, red) / D;
+    float q = 0.f;
+    for (int c = threadIdx.x; c < D; c += blockDim.x) {
+      const float t = xr[c] - mean;
+      q += t * t;
+    }
+    const float rstd = 1.0f / sqrtf(block_sum(q, red) / D + eps);
+    for (int c = threadIdx.x; c < D; c += blockDim.x) stv(y, row * D + c, (xr[c] - mean) * rstd * g[c] + b[c], y_bf16);
+  }
+}
+
+// Backward of the wide rows: one workgroup per row (grid-stride), the
+// per-workgroup [dgamma | dbeta] partials accumulated in LDS (2 D floats,
+// dynamic) and written once, as ln_bwd_kernel's.
+__global__ void __launch_bounds__(256) ln_bwd_row_kernel(const float* __restrict__ x, const void* __restrict__ dy,
+                                                         int dy_bf16, int M, int D, const float* __restrict__ g,
+                                                         float eps, const float* __restrict__ dres,
+                                                         float* __restrict__ dx, float* __restrict__ part) {
+  __shared__ float red[16];
+  extern __shared__ float acc[];  // [dgamma (D) | dbeta (D)]
+  for (int c = threadIdx.x; c < 2 * D; c += blockDim.x) acc[c] = 0.f;
+  for (long long row = blockIdx.x; row < M; row += gridDim.x) {
+    const float* xr = x + row * D;
+    float s = 0.f;
+    for (int c = threadIdx.x; c < D; c += blockDim.x) s += xr[c];
+    const float mean = block_sum(s, red) / D;
+    float q = 0.f;
+    for (int c = threadIdx.x; c < D; c += blockDim.x) {
+      const float t = xr[c] - mean;
+      q += t * t;
+    }
+    const float rstd = 1.0f / sqrtf(block_sum(q, red) / D + eps);
+    float s1 = 0.f, s2 = 0.f;
+    for (int c = threadIdx.x; c < D; c += blockDim.x) {
+      const float xh = (xr[c] - mean) * rstd, d = ldv(dy, row * D + c, dy_bf16), gy = d * g[c];
+      s1 += gy;
+      s2 += gy * xh;
+      acc[c] += d * xh;  // each column owned by one thread: no LDS race
+      acc[D + c] += d;
+    }
+    s1 = block_sum(s1, red) / D;
+    s2 = block_sum(s2, red) / D;
+    for (int c = threadIdx.x; c < D; c += blockDim.x) {
+      const float xh = (xr[c] - mean) * rstd;
+      float r = rstd * (ldv(dy, row * D + c, dy_bf16) * g[c] - s1 - xh * s2);
+      if (dres) r += dres[row * D + c];
+      dx[row * D + c] = r;
+    }
+  }
+  if (!part) return;
+  __syncthreads();  // acc[D + c] was written by another thread than the one storing it
+  for (int c = threadIdx.x; c < 2 * D; c += blockDim.x) part[(long long)blockIdx.x * 2 * D + c] = acc[c];
+}
+
 // part[j, c] = sum of x[r, c] over rows r of chunk j (thread per column;
 // 8 loads in flight per thread).
 // Batched over grid.z: x (batch, rows, cols) -> part[j][z * cols + c], so
@@ -435,18 +501,23 @@ __global__ void __launch_bounds__(256) dwconv_wgrad_kernel(const void* __restric
 }
 
 // ------------------------------------------- ConvBlock im2col / col2im
-// Conv2d k3 stride 2 "same" reflect padding (pad 1 each side, CNN.py:659-700,
-// get_padding_elem :1459-1481).  x (B, Ti, Fi, Ci); col (B*To*Fo, 9*Ci) with
-// column order (kt, kf, ci) — the (Cout, kt, kf, Ci) weight permutation.
-__device__ __forceinline__ int reflect1(int p, int n) {  // padded index p -> source index
-  const int s = p - 1;
+// Conv2d with "same" reflect padding (CNN.py:616-700, get_padding_elem
+// :1459-1481: (k - 1) / 2 each side for odd k) and any stride: x (B, Ti,
+// Fi, Ci) -> col (B*To*Fo, kt*kf*Ci) with column order (time tap, freq
+// tap, ci) — the (Cout, kT, kF, Ci) weight permutation.  pt / pf < Ti / Fi
+// (one reflection).
+struct ConvGeom {
+  int kt, kf, st, sf, pt, pf;
+};
+
+__device__ __forceinline__ int reflect_idx(int s, int n) {  // unpadded index of padded-minus-pad s
   return s < 0 ? -s : (s >= n ? 2 * n - 2 - s : s);
 }
 
-__global__ void im2col3s2_kernel(const void* __restrict__ x, int x_bf16, int B, int Ti, int Fi, int Ci, int To,
-                                 int Fo, int ldcol, void* __restrict__ col, int col_bf16) {
+__global__ void im2col_kernel(const void* __restrict__ x, int x_bf16, int B, int Ti, int Fi, int Ci, int To, int Fo,
+                              ConvGeom gm, int ldcol, void* __restrict__ col, int col_bf16) {
   const long long n = (long long)B * To * Fo * ldcol;
-  const int kcols = 9 * Ci;
+  const int kcols = gm.kt * gm.kf * Ci;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     const int kk = (int)(i % ldcol);
     long long q = i / ldcol;
@@ -455,20 +526,31 @@ __global__ void im2col3s2_kernel(const void* __restrict__ x, int x_bf16, int B, 
       continue;
     }
     const int ci = kk % Ci;
-    const int kf = (kk / Ci) % 3;
-    const int kt = kk / (3 * Ci);
+    const int kf = (kk / Ci) % gm.kf;
+    const int kt = kk / (gm.kf * Ci);
     const int fo = (int)(q % Fo); q /= Fo;
     const int to = (int)(q % To);
     const int b = (int)(q / To);
-    const int ti = reflect1(2 * to + kt, Ti), fi = reflect1(2 * fo + kf, Fi);
+    const int ti = reflect_idx(to * gm.st + kt - gm.pt, Ti), fi = reflect_idx(fo * gm.sf + kf - gm.pf, Fi);
     stv(col, i, ldv(x, (((long long)b * Ti + ti) * Fi + fi) * Ci + ci, x_bf16), col_bf16);
   }
 }
 
-// dx[b, ti, fi, ci] = sum over padded positions (pt, pf) that reflect onto
-// (ti, fi) and taps (kt, kf) with pt = 2 to + kt, pf = 2 fo + kf of dcol.
-__global__ void col2im3s2_kernel(const void* __restrict__ dcol, int dcol_bf16, int B, int Ti, int Fi, int Ci, int To,
-                                 int Fo, int ldcol, void* __restrict__ dx, int dx_bf16) {
+// padded positions p (0 <= p < n + 2 pad) whose reflection is index i: the
+// direct one and up to two mirrored ones; returns their count
+__device__ __forceinline__ int reflect_sources(int i, int n, int pad, int* p) {
+  int k = 0;
+  p[k++] = i + pad;
+  if (i >= 1 && i <= pad) p[k++] = pad - i;                           // s = -i
+  if (i <= n - 2 && 2 * n - 2 - i <= n - 1 + pad) p[k++] = 2 * n - 2 - i + pad;  // s = 2n - 2 - i
+  return k;
+}
+
+// dx[b, ti, fi, ci] = sum of dcol over the (output position, tap) pairs
+// whose padded input position reflects onto (ti, fi): the adjoint of
+// im2col, as a gather (deterministic).
+__global__ void col2im_kernel(const void* __restrict__ dcol, int dcol_bf16, int B, int Ti, int Fi, int Ci, int To,
+                              int Fo, ConvGeom gm, int ldcol, void* __restrict__ dx, int dx_bf16) {
   const long long n = (long long)B * Ti * Fi * Ci;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     const int ci = (int)(i % Ci);
@@ -476,28 +558,22 @@ __global__ void col2im3s2_kernel(const void* __restrict__ dcol, int dcol_bf16, i
     const int fi = (int)(q % Fi); q /= Fi;
     const int ti = (int)(q % Ti);
     const int b = (int)(q / Ti);
-    // padded positions mapping onto ti: ti + 1, and the mirrored ones
-    int pts[3], npt = 0, pfs[3], npf = 0;  // Ti == 3: ti = 1 is hit from both borders
-    pts[npt++] = ti + 1;
-    if (ti == 1) pts[npt++] = 0;
-    if (ti == Ti - 2 && Ti >= 2) pts[npt++] = Ti + 1;
-    pfs[npf++] = fi + 1;
-    if (fi == 1) pfs[npf++] = 0;
-    if (fi == Fi - 2 && Fi >= 2) pfs[npf++] = Fi + 1;
+    int pts[3], pfs[3];
+    const int npt = reflect_sources(ti, Ti, gm.pt, pts), npf = reflect_sources(fi, Fi, gm.pf, pfs);
     float s = 0.f;
     for (int a = 0; a < npt; ++a)
-      for (int kt = 0; kt < 3; ++kt) {
+      for (int kt = 0; kt < gm.kt; ++kt) {
         const int d = pts[a] - kt;
-        if (d < 0 || (d & 1)) continue;
-        const int to = d >> 1;
+        if (d < 0 || d % gm.st) continue;
+        const int to = d / gm.st;
         if (to >= To) continue;
         for (int e = 0; e < npf; ++e)
-          for (int kf = 0; kf < 3; ++kf) {
+          for (int kf = 0; kf < gm.kf; ++kf) {
             const int df = pfs[e] - kf;
-            if (df < 0 || (df & 1)) continue;
-            const int fo = df >> 1;
+            if (df < 0 || df % gm.sf) continue;
+            const int fo = df / gm.sf;
             if (fo >= Fo) continue;
-            s += ldv(dcol, (((long long)b * To + to) * Fo + fo) * ldcol + (kt * 3 + kf) * Ci + ci, dcol_bf16);
+            s += ldv(dcol, (((long long)b * To + to) * Fo + fo) * ldcol + (kt * gm.kf + kf) * Ci + ci, dcol_bf16);
           }
       }
     stv(dx, i, s, dx_bf16);
@@ -975,9 +1051,22 @@ SBK_API int sbk_layernorm_bwd_blocks(int M) { return grid_for((M + 3) / 4, 1, 10
 
 SBK_API int sbk_layernorm_bwd(const float* x, const void* dy, int dy_bf16, int M, int D, const float* g, float eps,
                               const float* dres, float* dx, float* part, void* stream) {
-  if (M <= 0 || D <= 0 || D > 2560) return SBK_ERR_ARG;
+  if (M <= 0 || D <= 0 || D > 16384) return SBK_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int grid = sbk_layernorm_bwd_blocks(M);
+  if (D > 2560) {  // workgroup per row; dgamma / dbeta partials in LDS
+    const size_t lds = (size_t)2 * D * sizeof(float);
+    static bool attr = false;
+    if (!attr) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ln_bwd_row_kernel),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 16384 * (int)sizeof(float));
+      if (e != hipSuccess) return (int)e;
+      attr = true;
+    }
+    ln_bwd_row_kernel<<<grid, 256, lds, s>>>(x, dy, dy_bf16, M, D, g, eps, dres, dx, part);
+    SBK_CHECK_LAUNCH();
+    return 0;
+  }
   if (D <= 256)
     ln_bwd_kernel<4><<<grid, 256, 0, s>>>(x, dy, dy_bf16, M, D, g, eps, dres, dx, part);
   else if (D <= 1024)
@@ -990,8 +1079,13 @@ SBK_API int sbk_layernorm_bwd(const float* x, const void* dy, int dy_bf16, int M
 
 SBK_API int sbk_layernorm_wide(const float* x, int M, int D, const float* g, const float* b, float eps, void* y,
                                int y_bf16, void* stream) {
-  if (M <= 0 || D <= 0 || D > 2560) return SBK_ERR_ARG;
+  if (M <= 0 || D <= 0) return SBK_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
+  if (D > 2560) {
+    ln_fwd_row_kernel<<<grid_for(M, 1, 4096), 256, 0, s>>>(x, M, D, g, b, eps, y, y_bf16);
+    SBK_CHECK_LAUNCH();
+    return 0;
+  }
   const int grid = (M + 3) / 4;
   if (D <= 256)
     ln_fwd_kernel<4><<<grid, 256, 0, s>>>(x, M, D, g, b, eps, y, y_bf16);
@@ -1122,22 +1216,31 @@ SBK_API int sbk_relpos_softmax_bwd_pad(int dtype_bf16, const float* P, const voi
   return 0;
 }
 
-SBK_API int sbk_im2col3s2(const void* x, int x_bf16, int B, int Ti, int Fi, int Ci, int ldcol, void* col,
-                          int col_bf16, void* stream) {
-  if (B <= 0 || Ti < 2 || Fi < 2 || Ci <= 0 || ldcol < 9 * Ci) return SBK_ERR_ARG;
-  const int To = (Ti - 1) / 2 + 1, Fo = (Fi - 1) / 2 + 1;
-  im2col3s2_kernel<<<grid_for((long long)B * To * Fo * ldcol, 256), 256, 0, (hipStream_t)stream>>>(
-      x, x_bf16, B, Ti, Fi, Ci, To, Fo, ldcol, col, col_bf16);
+static bool conv_geom_ok(int Ti, int Fi, int kt, int kf, int st, int sf, int pt, int pf, int* To, int* Fo) {
+  if (kt <= 0 || kf <= 0 || st <= 0 || sf <= 0 || pt < 0 || pf < 0 || pt >= Ti || pf >= Fi) return false;
+  *To = (Ti + 2 * pt - kt) / st + 1;
+  *Fo = (Fi + 2 * pf - kf) / sf + 1;
+  return Ti + 2 * pt >= kt && Fi + 2 * pf >= kf;
+}
+
+SBK_API int sbk_im2col(const void* x, int x_bf16, int B, int Ti, int Fi, int Ci, int kt, int kf, int st, int sf, int pt,
+                       int pf, int ldcol, void* col, int col_bf16, void* stream) {
+  int To, Fo;
+  if (B <= 0 || Ci <= 0 || !conv_geom_ok(Ti, Fi, kt, kf, st, sf, pt, pf, &To, &Fo) || ldcol < kt * kf * Ci)
+    return SBK_ERR_ARG;
+  im2col_kernel<<<grid_for((long long)B * To * Fo * ldcol, 256), 256, 0, (hipStream_t)stream>>>(
+      x, x_bf16, B, Ti, Fi, Ci, To, Fo, ConvGeom{kt, kf, st, sf, pt, pf}, ldcol, col, col_bf16);
   SBK_CHECK_LAUNCH();
   return 0;
 }
 
-SBK_API int sbk_col2im3s2(const void* dcol, int dcol_bf16, int B, int Ti, int Fi, int Ci, int ldcol, void* dx,
-                          int dx_bf16, void* stream) {
-  if (B <= 0 || Ti < 2 || Fi < 2 || Ci <= 0 || ldcol < 9 * Ci) return SBK_ERR_ARG;
-  const int To = (Ti - 1) / 2 + 1, Fo = (Fi - 1) / 2 + 1;
-  col2im3s2_kernel<<<grid_for((long long)B * Ti * Fi * Ci, 256), 256, 0, (hipStream_t)stream>>>(
-      dcol, dcol_bf16, B, Ti, Fi, Ci, To, Fo, ldcol, dx, dx_bf16);
+SBK_API int sbk_col2im(const void* dcol, int dcol_bf16, int B, int Ti, int Fi, int Ci, int kt, int kf, int st, int sf,
+                       int pt, int pf, int ldcol, void* dx, int dx_bf16, void* stream) {
+  int To, Fo;
+  if (B <= 0 || Ci <= 0 || !conv_geom_ok(Ti, Fi, kt, kf, st, sf, pt, pf, &To, &Fo) || ldcol < kt * kf * Ci)
+    return SBK_ERR_ARG;
+  col2im_kernel<<<grid_for((long long)B * Ti * Fi * Ci, 256), 256, 0, (hipStream_t)stream>>>(
+      dcol, dcol_bf16, B, Ti, Fi, Ci, To, Fo, ConvGeom{kt, kf, st, sf, pt, pf}, ldcol, dx, dx_bf16);
   SBK_CHECK_LAUNCH();
   return 0;
 }

@@ -16,24 +16,28 @@ from .._lib import check, lib, ptr, require_device, stream_of
 
 __all__ = ["SpecAugment"]
 
+_WARP_MODES = {"bicubic": 0, "bilinear": 1}
+
 
 @torch.library.custom_op("sbk::specaugment_", mutates_args=("x",))
 def specaugment_(x: torch.Tensor, N: int, T: int, F: int, c: int, w: int, fm: Optional[torch.Tensor],
-                 tm: Optional[torch.Tensor], use_mean: bool, n_fcells: int) -> None:
-    """Applies the drawn warp (c, w; -1 = none) and freq / time masks
+                 tm: Optional[torch.Tensor], use_mean: bool, n_fcells: int, warp_mode: int = 0) -> None:
+    """Applies the drawn warp (c, w; -1 = none; warp_mode 0 bicubic, 1
+    bilinear) and freq / time masks
     (fm, tm: (N, n, 2) int32 [len, pos]) to x (N, T, F) fp32 in place, with
     the batch-mean fill when use_mean (augment.py:116-201)."""
     tmp = torch.empty_like(x) if c >= 0 else None
     partial = torch.empty(2 * N * ((T + 15) // 16), device=x.device, dtype=torch.float32) if use_mean else None
     n_f = fm.shape[1] if fm is not None else 0
     n_t = tm.shape[1] if tm is not None else 0
-    rc = lib().sbk_specaugment(ptr(x), N, T, F, c, w, ptr(tmp), ptr(fm), n_f, ptr(tm), n_t, int(use_mean),
+    rc = lib().sbk_specaugment(ptr(x), N, T, F, c, w, int(warp_mode), ptr(tmp), ptr(fm), n_f, ptr(tm), n_t,
+                               int(use_mean),
                                ptr(partial), n_fcells, stream_of(x))
     check(rc, "sbk_specaugment")
 
 
 @specaugment_.register_fake
-def _(x, N, T, F, c, w, fm, tm, use_mean, n_fcells):
+def _(x, N, T, F, c, w, fm, tm, use_mean, n_fcells, warp_mode=0):
     return None
 
 
@@ -44,8 +48,11 @@ class SpecAugment(torch.nn.Module):
         super().__init__()
         assert time_warp or freq_mask or time_mask, \
             "at least one of time_warp, time_mask, or freq_mask should be applied"
-        if time_warp and time_warp_mode != "bicubic":
-            raise NotImplementedError("only bicubic time warping is implemented (the recipe mode)")
+        if time_warp and time_warp_mode not in _WARP_MODES:
+            # the reference interpolates with align_corners=True (augment.py:134-148), which torch
+            # accepts for the (bi)linear / bicubic modes only; the other modes raise there too
+            raise ValueError(f"time_warp_mode {time_warp_mode!r}: align_corners interpolation needs one of "
+                             f"{sorted(_WARP_MODES)}")
         self.apply_time_warp = time_warp
         self.time_warp_window = time_warp_window
         self.time_warp_mode = time_warp_mode
@@ -105,5 +112,6 @@ class SpecAugment(torch.nn.Module):
             ar = torch.arange(F).view(1, 1, -1)
             cov = ((fm[..., 1:2] <= ar) & (ar < fm[..., 1:2] + fm[..., 0:1])).any(1)
             n_fcells = int(cov.sum()) * T
-        torch.ops.sbk.specaugment_(x, N, T, F, c, w, fm_d, tm_d, not self.replace_with_zero, n_fcells)
+        torch.ops.sbk.specaugment_(x, N, T, F, c, w, fm_d, tm_d, not self.replace_with_zero, n_fcells,
+                                   _WARP_MODES.get(self.time_warp_mode, 0))
         return x

@@ -203,12 +203,14 @@ class ConformerEncoderLayer(nn.Module):
                 and hasattr(mha, "fused_in_proj") and mha.fused_in_proj(dtype) is not None
                 and self.convolution_module.fusable(dtype, d))
 
-    def fused(self, x, B, T, pos, kpm_u8, dtype, need_attn, u_in=None, next_ln=None, final_ln=None, pk=None):
+    def fused(self, x, B, T, pos, kpm_u8, dtype, need_attn, u_in=None, next_ln=None, final_ln=None, pk=None,
+              am=None):
         """One layer.  x: (B*T, d) fp32 residual stream; pos: (2T-1, d) in
         dtype; u_in: LN_ffn1(x) if a previous kernel already produced it;
         next_ln: (w, b, eps) of the NEXT consumer's LayerNorm to chain after
         norm2; final_ln: the encoder's closing LayerNorm, applied on chip by
-        the fused-FFN path; pk: this layer's linear_pos(pos) if precomputed.
+        the fused-FFN path; pk: this layer's linear_pos(pos) if precomputed;
+        am: the attention mask (_enc.attn_mask_arg) or None.
         Returns (x_out fp32, u_next or None, attn or None, final_ln_applied)."""
         if self.training and self.drop.p > 0:
             raise NotImplementedError("dropout in training mode is not implemented in HIP yet")
@@ -231,16 +233,16 @@ class ConformerEncoderLayer(nn.Module):
                 # convolution module (its LayerNorms included) in one launch
                 if hasattr(self.mha_layer, "attend_heads"):
                     o, attn, pre = self.mha_layer.attend_heads(u, B, T, pos, kpm_u8, dtype, need_attn, pk=pk,
-                                                               qkv=qkv)
+                                                               qkv=qkv, am=am)
                     x = cm.run_fused(x, B, T, kpm_u8, pre=pre)
                 else:
                     x, attn = self.mha_layer.attend(u, B, T, pos, kpm_u8, dtype, need_attn, residual=x, pk=pk,
-                                                    qkv=qkv)
+                                                    qkv=qkv, am=am)
                     x = cm.run_fused(x, B, T, kpm_u8)
             else:
                 # attention output projection + residual + the conv module's LayerNorm in one launch
                 x, attn, uc = self.mha_layer.attend(u, B, T, pos, kpm_u8, dtype, need_attn, residual=x,
-                                                    post_ln=cm.ln_params(), pk=pk, qkv=qkv)
+                                                    post_ln=cm.ln_params(), pk=pk, qkv=qkv, am=am)
                 x = cm.run(x, B, T, dtype, kpm_u8, residual=x, u=uc)
             x, y = f2[1].run_fused(x, self._ln(f2[0]), 0.5, post_ln=self._ln(self.norm2.norm), out=x,
                                    next_ln=final_ln, next_dtype=_f32)
@@ -250,7 +252,7 @@ class ConformerEncoderLayer(nn.Module):
         x = f1[1].run(u_in, dtype, residual=x, alpha=0.5)
         u, _ = _enc.layernorm(x, *self._ln(self.norm1.norm), out1_dtype=dtype)
         x, attn, uc = self.mha_layer.attend(u, B, T, pos, kpm_u8, dtype, need_attn, residual=x,
-                                            post_ln=self.convolution_module.ln_params(), pk=pk)
+                                            post_ln=self.convolution_module.ln_params(), pk=pk, am=am)
         x = self.convolution_module.run(x, B, T, dtype, kpm_u8, residual=x, u=uc)
         u, _ = _enc.layernorm(x, *self._ln(f2[0]), out1_dtype=dtype)
         z = f2[1].run(u, dtype, residual=x, alpha=0.5)
@@ -262,7 +264,7 @@ class ConformerEncoderLayer(nn.Module):
         x, _ = _enc.layernorm(z, w2, b2, e2, out1_dtype=_f32)
         return x, None, attn, False
 
-    def train_layer(self, x, B, T, pos, kpm_u8, dtype):
+    def train_layer(self, x, B, T, pos, kpm_u8, dtype, am=None):
         """Differentiable layer (training path): x (B*T, d) fp32 → (x_out, attn).
         Same arithmetic as `fused`, as HIP kernels with backward (_autograd);
         dropout (training mode) after the FFN activation, on the FFN and conv
@@ -272,7 +274,7 @@ class ConformerEncoderLayer(nn.Module):
         u = A.layer_norm(x, f1[0], out_dtype=dtype)
         x = f1[1].train_run(u, dtype, residual=x, alpha=0.5, out_p=f1[2].p if tr else 0.0)
         u = A.layer_norm(x, self.norm1.norm, out_dtype=dtype)
-        x, attn = self.mha_layer.train_attend(u, B, T, pos, kpm_u8, dtype, residual=x)
+        x, attn = self.mha_layer.train_attend(u, B, T, pos, kpm_u8, dtype, residual=x, am=am)
         x = self.convolution_module.train_run(x, B, T, dtype, kpm_u8, residual=x)
         u = A.layer_norm(x, f2[0], out_dtype=dtype)
         z = f2[1].train_run(u, dtype, residual=x, alpha=0.5, out_p=f2[2].p if tr else 0.0)
@@ -283,17 +285,16 @@ class ConformerEncoderLayer(nn.Module):
 
     def forward(self, x, src_mask: Optional[torch.Tensor] = None,
                 src_key_padding_mask: Optional[torch.Tensor] = None, pos_embs: Optional[torch.Tensor] = None):
-        if src_mask is not None:
-            raise NotImplementedError("src_mask is not supported by the fused attention kernel")
         B, T, d = x.shape
         dtype = _enc.compute_dtype()
         kpm = src_key_padding_mask.to(torch.uint8).contiguous() if src_key_padding_mask is not None else None
+        am = _enc.attn_mask_arg(src_mask, B, T, self.mha_layer.num_heads, x.device)
         x2d = x.float().reshape(B * T, d).contiguous()
         if self.wants_train_path(x):
-            y, attn = self.train_layer(x2d, B, T, pos_embs.reshape(-1, d).float(), kpm, dtype)
+            y, attn = self.train_layer(x2d, B, T, pos_embs.reshape(-1, d).float(), kpm, dtype, am=am)
             return y.view(B, T, d), attn
         pos = _enc.to_compute(pos_embs.reshape(-1, d), dtype)
-        y, _, attn, _ = self.fused(x2d, B, T, pos, kpm, dtype, True)
+        y, _, attn, _ = self.fused(x2d, B, T, pos, kpm, dtype, True, am=am)
         return y.view(B, T, d), attn
 
 
@@ -322,24 +323,25 @@ class ConformerEncoder(nn.Module):
             return _enc.cast_bf16(w) if dtype == _bf16 else w
         return self._wc.get(("pos", dtype), ws, make)
 
-    def train_run(self, src2d, B, T, pos_embs, kpm_u8, dtype):
+    def train_run(self, src2d, B, T, pos_embs, kpm_u8, dtype, am=None):
         """Differentiable stack (training path) on (B*T, d) fp32 → (y, [attn])."""
         d = src2d.shape[1]
         pos = pos_embs.reshape(-1, d).float()
         x = src2d
         attns = []
         for layer in self.layers:
-            x, a = layer.train_layer(x, B, T, pos, kpm_u8, dtype)
+            x, a = layer.train_layer(x, B, T, pos, kpm_u8, dtype, am=am)
             attns.append(a)
         return A.layer_norm(x, self.norm.norm, out_dtype=_f32), attns
 
     def wants_train_path(self, x):
         return any(layer.wants_train_path(x) for layer in self.layers) or A.needs_grad(self.norm, x)
 
-    def run(self, src2d, B, T, pos_embs, kpm_u8, dtype, need_attn):
-        """Fused stack on (B*T, d) fp32 → ((B*T, d) fp32, [attn])."""
+    def run(self, src2d, B, T, pos_embs, kpm_u8, dtype, need_attn, am=None):
+        """Fused stack on (B*T, d) fp32 → ((B*T, d) fp32, [attn]); am: the
+        src_mask as _enc.attn_mask_arg (takes the per-layer path)."""
         if self.wants_train_path(src2d):
-            return self.train_run(src2d, B, T, pos_embs, kpm_u8, dtype)
+            return self.train_run(src2d, B, T, pos_embs, kpm_u8, dtype, am=am)
         d = src2d.shape[1]
         pos = _enc.to_compute(pos_embs.reshape(-1, d), dtype)
         pk_all = _enc.gemm(pos, self.stacked_pos_weight(dtype), out_dtype=dtype)  # (2T-1, L*d)
@@ -347,7 +349,7 @@ class ConformerEncoder(nn.Module):
         u = None
         attns = []
         n = len(self.layers)
-        if USE_LAYER_CHAIN and all(layer.chainable(dtype, d) for layer in self.layers):
+        if USE_LAYER_CHAIN and am is None and all(layer.chainable(dtype, d) for layer in self.layers):
             return self._run_chain(x, B, T, pos, kpm_u8, dtype, need_attn, pk_all)
         for i, layer in enumerate(self.layers):
             nxt = self.layers[i + 1].ffn_module1[0] if i + 1 < n else None
@@ -355,7 +357,7 @@ class ConformerEncoder(nn.Module):
             fn = self.norm.norm
             final_ln = (fn.weight.detach(), fn.bias.detach(), fn.eps) if nxt is None else None
             x, u, a, done = layer.fused(x, B, T, pos, kpm_u8, dtype, need_attn, u_in=u, next_ln=next_ln,
-                                        final_ln=final_ln, pk=pk_all[:, i * d:(i + 1) * d])
+                                        final_ln=final_ln, pk=pk_all[:, i * d:(i + 1) * d], am=am)
             attns.append(a)
             if done:
                 return x, attns
@@ -398,10 +400,9 @@ class ConformerEncoder(nn.Module):
         if self.attention_type == "RelPosMHAXL" and pos_embs is None:
             raise ValueError("The chosen attention type for the Conformer is RelPosMHAXL. For this attention type, "
                              "the positional embeddings are mandatory")
-        if src_mask is not None:
-            raise NotImplementedError("src_mask is not supported by the fused attention kernel")
         B, T, d = src.shape
         kpm = src_key_padding_mask.to(torch.uint8).contiguous() if src_key_padding_mask is not None else None
+        am = _enc.attn_mask_arg(src_mask, B, T, self.layers[0].mha_layer.num_heads, src.device)
         y, attns = self.run(src.float().reshape(B * T, d).contiguous(), B, T, pos_embs, kpm,
-                            _enc.compute_dtype(), True)
+                            _enc.compute_dtype(), True, am=am)
         return y.view(B, T, d), attns

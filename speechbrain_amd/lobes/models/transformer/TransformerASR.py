@@ -8,7 +8,8 @@ encoder checkpoints load with strict=True (positional_encoding,
 positional_encoding_decoder, encoder.*, custom_src_module.layers.0.w.*,
 custom_tgt_module.layers.0.emb.Embedding.weight).  Decoding
 (num_decoder_layers > 0 → TransformerDecoder, forward/decode) is outside the
-accelerated path and raises NotImplementedError.
+accelerated path and raises NotImplementedError.  EncoderWrapper
+(:325-356) makes encode() the forward of a DDP-wrappable module.
 """
 import math
 from typing import Optional
@@ -135,3 +136,16 @@ class TransformerASR(nn.Module):
         pos = self.positional_encoding.table(T, src.device, dtype)  # a constant table: cached in the compute dtype
         y, _ = self.encoder.run(x, B, T, pos, kpm, dtype, False)
         return y.view(B, T, -1)
+
+
+class EncoderWrapper(nn.Module):
+    """TransformerASR.py:325-356: a module whose forward is
+    transformer.encode(x, wav_lens), so the encoder can be wrapped by DDP
+    (Brain._wrap_distributed wraps modules, and DDP only runs forward)."""
+
+    def __init__(self, transformer, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.transformer = transformer
+
+    def forward(self, x, wav_lens=None):
+        return self.transformer.encode(x, wav_lens)

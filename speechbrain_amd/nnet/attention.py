@@ -108,6 +108,19 @@ class RelPosMHAXL(nn.Module):
             return tuple(p.detach() for p in ps)
         return self._wc.get("bf16", ps, lambda: tuple(_enc.cast_bf16(p.detach().contiguous()) for p in ps))
 
+    def in_proj_bias(self):
+        """vbias=True (attention.py:576-579): value + value_bias_weight per
+        head, as a bias of the in_proj GEMM in the head-interleaved [q|k|v]
+        layout (zeros for q and k).  Built from the parameter with torch ops
+        (a 3·d vector), so its gradient reaches value_bias_weight.  None
+        without vbias."""
+        if self.vbias is None:
+            return None
+        H, dh = self.num_heads, self.head_dim
+        vb = self.value_bias_weight.view(H, 1, dh)
+        z = torch.zeros(H, 2, dh, device=vb.device, dtype=vb.dtype)
+        return torch.cat([z, vb], dim=1).reshape(3 * H * dh)
+
     def fused_in_proj(self, dtype):
         """The bf16 in_proj weight when a producer kernel can apply it on chip
         (sbk_ffn_proj: no in_proj bias, 3·d columns in 256-column blocks), else None."""
@@ -116,43 +129,41 @@ class RelPosMHAXL(nn.Module):
         w_in = self.kernel_weights(dtype)[0]
         return w_in if _enc.ffn_proj_supported(self.embed_dim, 256, w_in.shape[0]) else None
 
-    def attend_heads(self, x2d, B, T, pos_embs, kpm_u8, dtype, need_weights, pk=None, qkv=None):
+    def attend_heads(self, x2d, B, T, pos_embs, kpm_u8, dtype, need_weights, pk=None, qkv=None, am=None):
         """attend without the output projection: (o (B*T, d) in dtype, attn,
         (o, out_proj weight, bias)) for a consumer that applies out_proj
         itself (sbk_conv_module_pre)."""
-        if self.vbias is not None:
-            raise NotImplementedError("vbias=True is not on the RelPosMHAXL hot path")
         w_in, w_pos, w_out = self.kernel_weights(dtype)
         if qkv is None:
-            qkv = _enc.gemm(x2d, w_in, out_dtype=dtype)
+            ib = self.in_proj_bias()
+            qkv = _enc.gemm(x2d, w_in, bias=None if ib is None else ib.detach(), out_dtype=dtype)
         if pk is None:
             pos = pos_embs.reshape(-1, self.embed_dim)
             if pos.dtype != dtype:
                 pos = _enc.cast_bf16(pos.float().contiguous()) if dtype == torch.bfloat16 else pos.float()
             pk = _enc.gemm(pos.contiguous(), w_pos, out_dtype=dtype)
         o, probs = _enc.relpos_attention(qkv, pk, self.pos_bias_u.detach(), self.pos_bias_v.detach(), kpm_u8, B, T,
-                                         self.num_heads, self.head_dim, self.scale, need_weights)
+                                         self.num_heads, self.head_dim, self.scale, need_weights, am=am)
         return o, probs, (o, w_out, self.out_proj.bias.detach())
 
     def attend(self, x2d, B, T, pos_embs, kpm_u8, dtype, need_weights, residual=None, post_ln=None, pk=None,
-               qkv=None):
+               qkv=None, am=None):
         """Core used by the fused Conformer layer: x2d (B*T, d) in `dtype`
         (or qkv = x2d · in_proj^T already computed by the producer kernel).
         Returns (out (B*T, d) fp32 [+ residual], attn or None); with post_ln =
         (w, b, eps) also u = LN(out) in `dtype` (fused into the output
         projection when d_model == 256): (out, attn, u)."""
-        if self.vbias is not None:
-            raise NotImplementedError("vbias=True is not on the RelPosMHAXL hot path")
         w_in, w_pos, w_out = self.kernel_weights(dtype)
         if qkv is None:
-            qkv = _enc.gemm(x2d, w_in, out_dtype=dtype)
+            ib = self.in_proj_bias()
+            qkv = _enc.gemm(x2d, w_in, bias=None if ib is None else ib.detach(), out_dtype=dtype)
         if pk is None:  # the encoder passes its one stacked linear_pos GEMM's slice
             pos = pos_embs.reshape(-1, self.embed_dim)
             if pos.dtype != dtype:
                 pos = _enc.cast_bf16(pos.float().contiguous()) if dtype == torch.bfloat16 else pos.float()
             pk = _enc.gemm(pos.contiguous(), w_pos, out_dtype=dtype)
         o, probs = _enc.relpos_attention(qkv, pk, self.pos_bias_u.detach(), self.pos_bias_v.detach(), kpm_u8, B, T,
-                                         self.num_heads, self.head_dim, self.scale, need_weights)
+                                         self.num_heads, self.head_dim, self.scale, need_weights, am=am)
         bias = self.out_proj.bias.detach()
         if post_ln is not None:
             if _enc.gemm_ln_supported(self.embed_dim) and _enc.USE_GEMM_LN:
@@ -164,39 +175,37 @@ class RelPosMHAXL(nn.Module):
         out = _enc.gemm(o, w_out, bias=bias, res=residual, out_dtype=torch.float32)
         return out, probs
 
-    def train_attend(self, x2d, B, T, pos, kpm_u8, dtype, residual=None):
+    def train_attend(self, x2d, B, T, pos, kpm_u8, dtype, residual=None, am=None):
         """Differentiable attention block (training path): x2d (B*T, d) →
         (residual + out_proj(attn(x2d)) fp32, attention probabilities after dropout)."""
-        if self.vbias is not None:
-            raise NotImplementedError("vbias=True is not on the RelPosMHAXL hot path")
-        qkv = A.linear(x2d, self.in_proj_weight, None, dtype, self._wc, "t_in", out_dtype=dtype)
+        qkv = A.linear(x2d, self.in_proj_weight, self.in_proj_bias(), dtype, self._wc, "t_in", out_dtype=dtype)
         pk = A.linear(pos.reshape(-1, self.embed_dim), self.linear_pos.weight, None, dtype, self._wc, "t_pos",
                       out_dtype=dtype)
         p = self.dropout_att.p if self.training else 0.0
         o, attn = A.RelPosAttentionFn.apply(qkv, pk, self.pos_bias_u, self.pos_bias_v, kpm_u8, B, T,
-                                            self.num_heads, self.head_dim, self.scale, float(p))
+                                            self.num_heads, self.head_dim, self.scale, float(p), am)
         out = A.linear(o, self.out_proj.weight, self.out_proj.bias, dtype, self._wc, "t_out", res=residual)
         return out, attn
 
     def forward(self, query, key, value, pos_embs, key_padding_mask=None, attn_mask=None,
                 return_attn_weights=True):
         """attention.py:485-639.  Self-attention only (query, key and value
-        identical, as in every Conformer call site)."""
+        identical, as in every Conformer call site).  attn_mask: (T, T) or
+        (B*H, T, T), bool (True = masked) or additive float (:598-611)."""
         if not self._qkv_same_embed_dim:
             raise NotImplementedError  # the reference raises too (attention.py:558)
         if not ((query is key or torch.equal(query, key)) and (key is value or torch.equal(key, value))):
             raise NotImplementedError("cross-attention RelPosMHAXL is not on the accelerated path")
-        if attn_mask is not None:
-            raise NotImplementedError("attn_mask is not supported by the fused kernel (encoder passes none)")
         B, T, d = query.shape
         dtype = _enc.compute_dtype()
         x2d = query.reshape(B * T, d)
         kpm = key_padding_mask.to(torch.uint8).contiguous() if key_padding_mask is not None else None
+        am = _enc.attn_mask_arg(attn_mask, B, T, self.num_heads, query.device)
         if A.needs_grad(self, query) or (self.training and self.dropout > 0):
-            out, attn = self.train_attend(x2d.float(), B, T, pos_embs.float(), kpm, dtype)
+            out, attn = self.train_attend(x2d.float(), B, T, pos_embs.float(), kpm, dtype, am=am)
         else:
             x2d = _enc.to_compute(x2d, dtype)
-            out, attn = self.attend(x2d, B, T, pos_embs, kpm, dtype, return_attn_weights)
+            out, attn = self.attend(x2d, B, T, pos_embs, kpm, dtype, return_attn_weights, am=am)
         out = out.view(B, T, d)
         if return_attn_weights:
             return out, attn

@@ -39,6 +39,14 @@ Fixture inventory (all float32 unless noted):
   decoder.npz      TransducerBeamSearcher greedy and beam search on a small
                    random one-hot-Embedding / GRU / Linear transducer
                    (decoders/transducer.py:10-519)
+  dropin.npz       constructor coverage beyond the recipe: the default
+                   ConvolutionFrontEnd(input_shape) (3 residual blocks x 5
+                   layers; seeded-init checksums and output), a small
+                   residual / multi-layer / kernel-5 front-end with weights,
+                   output and autograd gradients, RelPosMHAXL with a bool
+                   causal and a float 3-D attn_mask, SpecAugment bilinear
+                   warp (lobes/models/convolution.py:12-175,
+                   nnet/attention.py:598-611, lobes/augment.py:116-148)
   train.npz        gradients of sum(R * encode(cnn(feats), wav_len)) w.r.t.
                    every ConvolutionFrontEnd / TransformerASR parameter and
                    the input features (reference autograd, weights of
@@ -470,7 +478,81 @@ def gen_decoder():
     np.savez_compressed(os.path.join(OUT, "decoder.npz"), **out)
 
 
+def gen_dropin():
+    out = {}
+    g = torch.Generator().manual_seed(21)
+    # 1. ConvolutionFrontEnd with every default (the doctest shape)
+    torch.manual_seed(0)
+    fe = ConvolutionFrontEnd(input_shape=(8, 30, 10))
+    fe.eval()
+    for k, v in fe.state_dict().items():
+        v64 = v.double()
+        out["fe_def_sum." + k] = np.asarray(float(v64.sum()), np.float64)
+        out["fe_def_sq." + k] = np.asarray(float((v64 * v64).sum()), np.float64)
+    x = torch.rand((8, 30, 10), generator=g)
+    with torch.no_grad():
+        y = fe(x)
+    out["fe_def_x"] = t2n(x)
+    out["fe_def_y"] = t2n(y)
+    # 2. residual, 2 layers per block, kernel 5, strides (1, 2): weights,
+    #    output and gradients of sum(R * y)
+    torch.manual_seed(1)
+    fe2 = ConvolutionFrontEnd(input_shape=(3, 37, 20), num_blocks=2, num_layers_per_block=2, out_channels=(8, 16),
+                              kernel_sizes=(3, 5), strides=(1, 2), residuals=(True, True), dropout=0.1)
+    fe2.eval()
+    for k, v in fe2.state_dict().items():
+        out["fe2." + k] = t2n(v)
+    x2 = torch.randn(3, 37, 20, generator=g).requires_grad_(True)
+    y2 = fe2(x2)
+    R = torch.randn(y2.shape, generator=g)
+    (y2 * R).sum().backward()
+    out["fe2_x"], out["fe2_y"], out["fe2_R"] = t2n(x2), t2n(y2), t2n(R)
+    out["fe2_grad_x"] = t2n(x2.grad)
+    for k, p in fe2.named_parameters():
+        out["fe2_grad." + k] = t2n(p.grad)
+    # 3. RelPosMHAXL attn_mask: bool (T, T) causal and float (B*H, T, T) additive
+    torch.manual_seed(2)
+    mha = RelPosMHAXL(embed_dim=64, num_heads=4)
+    mha.eval()
+    for k, v in mha.state_dict().items():
+        out["mha." + k] = t2n(v)
+    T = 29
+    q = torch.randn(2, T, 64, generator=g)
+    pe = RelPosEncXL(64)(q)
+    kpm = torch.arange(T)[None, :] >= torch.tensor([T, 23])[:, None]
+    causal = torch.triu(torch.ones(T, T, dtype=torch.bool), diagonal=1)
+    fmask = 0.5 * torch.randn(2 * 4, T, T, generator=g)
+    out["mha_q"], out["mha_pe"], out["mha_kpm"] = t2n(q), t2n(pe), kpm.numpy()
+    out["mha_fmask"] = t2n(fmask)
+    with torch.no_grad():
+        for tag, am in (("causal", causal), ("float", fmask)):
+            o, a = mha(q, q, q, pe, key_padding_mask=kpm, attn_mask=am)
+            out[f"mha_{tag}_out"], out[f"mha_{tag}_attn"] = t2n(o), t2n(a)
+    # vbias=True (attention.py:576-579), the value bias set away from its zero init
+    torch.manual_seed(3)
+    mhv = RelPosMHAXL(embed_dim=64, num_heads=4, vbias=True)
+    with torch.no_grad():
+        mhv.value_bias_weight.copy_(0.3 * torch.randn(64, generator=g))
+    mhv.eval()
+    for k, v in mhv.state_dict().items():
+        out["mhv." + k] = t2n(v)
+    with torch.no_grad():
+        o, a = mhv(q, q, q, pe, key_padding_mask=kpm)
+    out["mhv_out"], out["mhv_attn"] = t2n(o), t2n(a)
+    # 4. SpecAugment with bilinear time warp (seeds 0..2)
+    feats = torch.randn(3, 120, 40, generator=g)
+    out["warp_feats"] = t2n(feats)
+    aug = SpecAugment(time_warp=True, time_warp_mode="bilinear", freq_mask=False, time_mask=False)
+    for sd in range(3):
+        torch.manual_seed(sd)
+        out[f"warp_bilinear_s{sd}"] = t2n(aug(feats.clone()))
+    np.savez_compressed(os.path.join(OUT, "dropin.npz"), **out)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["dropin"]:
+        gen_dropin()
+        sys.exit(0)
     if sys.argv[1:] == ["decoder"]:
         gen_decoder()
         sys.exit(0)
@@ -491,6 +573,7 @@ if __name__ == "__main__":
     gen_inputnorm()
     gen_wav2vec()
     gen_decoder()
+    gen_dropin()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

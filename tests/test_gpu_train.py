@@ -210,7 +210,8 @@ def test_conv_block_fn_vs_oracle(dev, Ti, Fi, Ci, Co):
     dy = torch.randn(ref.shape, generator=g)
     ref.backward(dy)
     dl = [t.to(dev).requires_grad_(True) for t in (x, w, b, lw, lb)]
-    y = A.ConvBlockFn.apply(dl[0], dl[1], dl[2], dl[3], dl[4], 1e-5, 0.01, torch.float32, torch.float32)
+    y = A.ConvBlockFn.apply(dl[0], dl[1], dl[2], dl[3], dl[4], 1e-5, 0.01, torch.float32, torch.float32,
+                            (3, 3, 2, 2))
     assert_close(y, ref.detach(), rtol=1e-4, name="fwd")
     y.backward(dy.to(dev))
     for n, a, r in zip(("dx", "dw", "db", "dln_w", "dln_b"), dl, leaves):
@@ -320,7 +321,7 @@ def test_relpos_attention_dropout_fwd_bwd(dev, T):
     scale = 1 / math.sqrt(d)
     leaves = [t.to(dev).requires_grad_(True) for t in (qkv, pk, pbu, pbv)]
     torch.manual_seed(3)
-    o, attn = A.RelPosAttentionFn.apply(*leaves, kpm.to(dev).to(torch.uint8), B, T, H, dh, scale, p)
+    o, attn = A.RelPosAttentionFn.apply(*leaves, kpm.to(dev).to(torch.uint8), B, T, H, dh, scale, p, None)
     do = torch.randn(o.shape, generator=g)
     o.backward(do.to(dev))
     attn = attn.cpu().double()
@@ -338,7 +339,7 @@ def test_relpos_attention_dropout_fwd_bwd(dev, T):
     # same seed, bf16: the same mask
     torch.manual_seed(3)
     _, attn_b = A.RelPosAttentionFn.apply(qkv.to(dev).bfloat16(), pk.to(dev).bfloat16(), pbu.to(dev), pbv.to(dev),
-                                          kpm.to(dev).to(torch.uint8), B, T, H, dh, scale, p)
+                                          kpm.to(dev).to(torch.uint8), B, T, H, dh, scale, p, None)
     assert torch.equal(attn_b.cpu() != 0, attn != 0)
 
 
