@@ -56,14 +56,15 @@ def build_model(d_model, dev, layers=12):
 
 
 def make_step(fbank, cnn, tr, wav, wav_len):
-    """The timed step: Fbank (fused spectrum kernel + top_db clamp) → both
-    ConvBlocks in one bf16 kernel → TransformerASR.encode under bf16 autocast
-    (fused FFN / conv-module / LDS-DMA attention kernels).  Also what
+    """The timed step: Fbank (fused spectrum kernel; its top_db floor applied
+    by the front-end as it loads the rows) → both ConvBlocks in one bf16
+    kernel → TransformerASR.encode under bf16 autocast (fused FFN /
+    conv-module / LDS-DMA attention kernels).  Also what
     tests/test_gpu_bench_parity.py runs against the fp32 oracle."""
     def step():
         with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
-            feats = fbank(wav)
-            src = cnn.run(feats, torch.bfloat16)
+            feats, topdb = fbank.forward_deferred(wav)
+            src = cnn.run(feats, torch.bfloat16, topdb=topdb)
             return tr.encode(src, wav_len)
     return step
 

@@ -283,11 +283,15 @@ int sbk_conv_block_mfma(int in_bf16, const void* x, int B, int Tin, int Fin, int
  * 169-175): block 1 (Cin = 1 -> C1 = 64, w1 as sbk_conv_block_c1) feeds block 2
  * (C1 -> C2, wp2 as sbk_conv_block_mfma in the dtype_bf16 type) through LDS;
  * x (B, Tin, Fin) fp32 -> out (B, T2, F2, C2); bf16 compute only (dtype_bf16 = 1), C1 = 64, F1 <= 40, F2 <= 32, C2 <= 32.
- * x == NULL: shape query. */
+ * slot_max (B, nslot) non-null: x is an Fbank output before its top_db floor
+ * (sbk_spectrum mode 2's partial maxima) and the floor max_b - top_db is
+ * applied as the rows are loaded (features.py:706-711; no separate
+ * sbk_topdb_clamp pass).  x == NULL: shape query. */
 int sbk_conv_frontend2(int dtype_bf16, const float* x, int B, int Tin, int Fin, const float* w1, const float* b1,
                        const float* g1, const float* be1, float eps1, float slope1, int C1, const void* wp2,
                        const float* b2, const float* g2, const float* be2, float eps2, float slope2, int C2, void* out,
-                       int out_bf16, int* Tout, int* Fout, void* stream);
+                       int out_bf16, const float* slot_max, int nslot, float top_db, int* Tout, int* Fout,
+                       void* stream);
 
 /* fp32 -> bf16 cast (n elements). */
 int sbk_cast_bf16(const float* x, void* y, long long n, void* stream);

@@ -507,7 +507,8 @@ def conv_block_mfma(x, wperm, bias, ln_w, ln_b, eps, slope, out_dtype):
 @torch.library.custom_op("sbk::conv_frontend2", mutates_args=())
 def _conv_frontend2_op(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, g1: torch.Tensor, be1: torch.Tensor,
                        e1: float, s1: float, wperm2: torch.Tensor, b2: torch.Tensor, g2: torch.Tensor,
-                       be2: torch.Tensor, e2: float, s2: float, out_bf16: bool) -> torch.Tensor:
+                       be2: torch.Tensor, e2: float, s2: float, out_bf16: bool, slot_max: Optional[torch.Tensor],
+                       top_db: float) -> torch.Tensor:
     B, Tin, Fin = x.shape
     C1, C2 = w1.shape[0], wperm2.shape[0]
     T1, F1 = (Tin - 1) // 2 + 1, (Fin - 1) // 2 + 1
@@ -515,27 +516,32 @@ def _conv_frontend2_op(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, g1: 
     out = torch.empty(B, T2, F2, C2, device=x.device, dtype=_bf16 if out_bf16 else _f32)
     rc = lib().sbk_conv_frontend2(int(_is_bf16(wperm2)), ptr(x), B, Tin, Fin, ptr(w1), ptr(b1), ptr(g1), ptr(be1),
                                   float(e1), float(s1), C1, ptr(wperm2), ptr(b2), ptr(g2), ptr(be2), float(e2),
-                                  float(s2), C2, ptr(out), int(out_bf16), None, None, stream_of(x))
+                                  float(s2), C2, ptr(out), int(out_bf16), ptr(slot_max),
+                                  slot_max.shape[1] if slot_max is not None else 0, float(top_db), None, None,
+                                  stream_of(x))
     check(rc, "sbk_conv_frontend2")
     return out
 
 
 @_conv_frontend2_op.register_fake
-def _(x, w1, b1, g1, be1, e1, s1, wperm2, b2, g2, be2, e2, s2, out_bf16):
+def _(x, w1, b1, g1, be1, e1, s1, wperm2, b2, g2, be2, e2, s2, out_bf16, slot_max, top_db):
     B, Tin, Fin = x.shape
     T1, F1 = (Tin - 1) // 2 + 1, (Fin - 1) // 2 + 1
     return x.new_empty(B, (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1, wperm2.shape[0], dtype=_bf16 if out_bf16 else _f32)
 
 
-def conv_frontend2(x, blk1, blk2, wperm2, out_dtype):
+def conv_frontend2(x, blk1, blk2, wperm2, out_dtype, topdb=None):
     """Both ConvBlocks in one kernel: x (B, T, F) fp32 → (B, T2, F2, C2).
     blk*: (conv weight, bias, ln weight, ln bias, ln eps, leaky slope);
-    wperm2: block-2 weights (C2, 3, 3, C1) in the compute dtype."""
+    wperm2: block-2 weights (C2, 3, 3, C1) in the compute dtype; topdb =
+    (slot_max (B, nslot), top_db): x is an Fbank output before its top_db
+    floor, applied on load (ops.fbank_deferred)."""
     require_device(x, wperm2)
     w1, b1, g1, be1, e1, s1 = blk1
     _, b2, g2, be2, e2, s2 = blk2
+    sm, tdb = topdb if topdb is not None else (None, 0.0)
     return torch.ops.sbk.conv_frontend2(x, w1, b1, g1, be1, float(e1), float(s1), wperm2, b2, g2, be2, float(e2),
-                                        float(s2), out_dtype == _bf16)
+                                        float(s2), out_dtype == _bf16, sm, float(tdb))
 
 
 @torch.library.custom_op("sbk::relpos_attention", mutates_args=())

@@ -76,7 +76,7 @@ SIGNATURES = {
     "sbk_conv_block_c1": [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _f, _vp, _i, _vp, _vp, _vp],
     "sbk_conv_block_mfma": [_i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _f, _vp, _i, _vp, _vp, _vp],
     "sbk_conv_frontend2": [_i, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, _vp, _vp, _vp, _f, _f, _i,
-                           _vp, _i, _vp, _vp, _vp],
+                           _vp, _i, _vp, _i, _f, _vp, _vp, _vp],
     "sbk_cast_bf16": [_vp, _vp, _ll, _vp],
     "sbk_swish": [_vp, _vp, _ll, _f, _vp],
     # w2v.hip (config 5 front-end, row LayerNorm / activation / MXFP8 quantisation)

@@ -488,7 +488,8 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
                                                         const T* __restrict__ wp2, int C2,
                                                         const float* __restrict__ b2, const float* __restrict__ g2,
                                                         const float* __restrict__ be2, float eps2, float slope2,
-                                                        void* out, int out_bf16) {
+                                                        void* out, int out_bf16, const float* __restrict__ slot_max,
+                                                        int nslot, float top_db) {
   using Tr = MT<T>;
   constexpr int NT = FE_NT, NW = NT / 64, TT2 = FE_TT2, NJ = 2 * TT2 + 1;
   static_assert(C1 == 64, "block-1 MFMA map: 4 channel tiles");
@@ -547,10 +548,28 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
 #pragma unroll
   for (int u = 0; u < W1V; ++u) w1v[u] = w1[min(tid + u * NT, C1 * 9 - 1)];
   const float b1v = b1 ? b1[tid & (C1 - 1)] : 0.f;
+  // the Fbank's top_db floor (features.py:706-711) applied on load: max over
+  // the utterance's spectrum-kernel partial maxima - top_db (the separate
+  // clamp pass over the features is gone)
+  float floor_db = -INFINITY;
+  if (slot_max) {
+    __shared__ float redm[FE_NT / 64];
+    float m = -INFINITY;
+    for (int i = tid; i < nslot; i += NT) m = fmaxf(m, slot_max[(long long)b * nslot + i]);
+    m = wave_max(m);
+    if (lane == 0) redm[w] = m;
+    __syncthreads();
+    m = redm[0];
+#pragma unroll
+    for (int i = 1; i < FE_NT / 64; ++i) m = fmaxf(m, redm[i]);
+    floor_db = m - top_db;
+  }
 #pragma unroll
   for (int u = 0; u < XV; ++u) {
     const int i = tid + u * NT;
-    if (i < NJ * 3 * fq4) *reinterpret_cast<float4*>(xs + 4 * i) = xin[u];
+    float4 v = xin[u];
+    v.x = fmaxf(v.x, floor_db); v.y = fmaxf(v.y, floor_db); v.z = fmaxf(v.z, floor_db); v.w = fmaxf(v.w, floor_db);
+    if (i < NJ * 3 * fq4) *reinterpret_cast<float4*>(xs + 4 * i) = v;
   }
 #pragma unroll
   for (int u = 0; u < AV; ++u)
@@ -978,8 +997,9 @@ SBK_API int sbk_conv_block_mfma(int in_bf16, const void* x, int B, int Tin, int 
 SBK_API int sbk_conv_frontend2(int dtype_bf16, const float* x, int B, int Tin, int Fin, const float* w1,
                                const float* b1, const float* g1, const float* be1, float eps1, float slope1, int C1,
                                const void* wp2, const float* b2, const float* g2, const float* be2, float eps2,
-                               float slope2, int C2, void* out, int out_bf16, int* Tout_, int* Fout_, void* stream) {
-  if (B <= 0 || Tin < 2 || Fin < 4 || C1 != 64 || C2 % 16 || C2 <= 0) return SBK_ERR_ARG;
+                               float slope2, int C2, void* out, int out_bf16, const float* slot_max, int nslot,
+                               float top_db, int* Tout_, int* Fout_, void* stream) {
+  if (B <= 0 || Tin < 2 || Fin < 4 || C1 != 64 || C2 % 16 || C2 <= 0 || (slot_max && nslot <= 0)) return SBK_ERR_ARG;
   const int T1 = (Tin - 1) / 2 + 1, F1 = (Fin - 1) / 2 + 1;
   const int T2 = (T1 - 1) / 2 + 1, F2 = (F1 - 1) / 2 + 1;
   if (Tout_) *Tout_ = T2;
@@ -1008,7 +1028,8 @@ SBK_API int sbk_conv_frontend2(int dtype_bf16, const float* x, int B, int Tin, i
       attr = true;
     }
     hipLaunchKernelGGL(kern, grid, dim3(FE_NT), lds, s, x, Tin, Fin, T1, F1, T2, F2, w1, b1, g1, be1, eps1, slope1,
-                       reinterpret_cast<const bf16_t*>(wp2), C2, b2, g2, be2, eps2, slope2, out, out_bf16);
+                       reinterpret_cast<const bf16_t*>(wp2), C2, b2, g2, be2, eps2, slope2, out, out_bf16, slot_max,
+                       nslot, top_db);
     return 0;
   };
   static bool attr_max = false, attr_sel = false;

@@ -190,7 +190,7 @@ __device__ __forceinline__ void row_ln(float (&z)[T2][MT][4], float (*red)[FFN_B
 
 #ifdef SBK_PROBE_TL
 // probe build only: s_memtime timeline of 4 waves (wg 0 wave 0, wg 0 last wave, wg 128, wg 250)
-__device__ unsigned long long g_ffn_tl[16][80];
+__device__ unsigned long long g_ffn_tl[16][200];
 #define FFN_TL(i)                                                                 \
   do {                                                                            \
     if (tl_rec >= 0 && lane == 0) g_ffn_tl[tl_rec][i] = __builtin_amdgcn_s_memtime(); \
@@ -346,6 +346,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
       for (int mt = 0; mt < MT; ++mt) xa[r][ks][mt] = ld8(Xn + (mt * 16 + fr) * XS + r * BK + ks * 32 + fk);
   for (int stage = 0; stage < (CHAIN ? 2 : 1); ++stage) {
   if (CHAIN && stage == 1) {
+    FFN_TL(197);
     // ---- between the blocks: A's rows z = x + alpha (acc2 + b2) -> post-LN
     // (norm2) are B's residual (held in xres) and, through B's LN0, its
     // phase-1 operand (Xn -> VGPR fragments); nothing goes to HBM
@@ -395,6 +396,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
           asm volatile("ds_read_b128 %0, %1" : "=v"(xa[r][ks][mt]) : "v"(la) : "memory");
         }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    FFN_TL(198);
   }
   for (int c = 0; c < NCH; ++c)
 #pragma unroll
@@ -404,7 +406,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL * (NB - 1)) : "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (r == K1) __builtin_amdgcn_s_barrier();
-    if (s < 34) FFN_TL(2 + 2 * s);
+    if (s < 96) FFN_TL(2 + 2 * s);
     const bf16_t* tile = ring + (s % NB) * TROWS * BK;
     bf16_t* Hc = Hs + (c & 1) * BM * HS;  // this chunk's hidden activations
     bf16x8 fw[BK / 32][T], fa[BK / 32][MT];
@@ -469,11 +471,11 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
           for (int mt = 0; mt < MT; ++mt)
             acc2[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ks][t], fa[ks][mt], acc2[t][mt], 0, 0, 0);
     }
-    if (s < 34) FFN_TL(3 + 2 * s);
+    if (s < 96) FFN_TL(3 + 2 * s);
   }
   }  // stage
   if (!PROJ) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the tail reloads
-  FFN_TL(70);
+  FFN_TL(194);
 
   // ---- epilogue: lane holds rows m = mt*16 + fr, units d = (w*T + j)*16 + 4g .. +3
   // (CHAIN: the parameters of block B, which has no post-LN)
@@ -494,7 +496,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
       z[j][mt][3] = xr.w + alphaf * (acc2[j][mt][3] + bb.w);
     }
   }
-  FFN_TL(71);
+  FFN_TL(195);
   if (gpf) row_ln<D, T, MT, NW>(z, red, gpf, a.bp, a.epsp, w, g, fr);
   if (PROJ) {
     // u = next-LN(out) -> Xn (bf16, the A operand of the projection), then
@@ -547,6 +549,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     // ---- projection y = u . Wp^T (bf16), 256 output columns per K1 steps
     for (int s = SF; s < ST; s += K1) {
       const int nc = (s - SF) / K1;
+      FFN_TL(199);
 #pragma unroll
       for (int r = 0; r < K1; ++r) {
         // tile s+r landed: younger than it are tile s+r+1 and, on the first
@@ -591,7 +594,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the tail reloads
-    FFN_TL(72);
+    FFN_TL(196);
     return;
   }
   // all residual reads of x are done before out (which may alias x) is written
@@ -627,7 +630,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
       }
     }
   }
-  FFN_TL(72);
+  FFN_TL(196);
 }
 
 template <int D>

@@ -49,6 +49,25 @@ class Fbank(torch.nn.Module):
         self.compute_deltas = Deltas(input_size=n_mels)
         self.context_window = ContextWindow(left_frames=left_frames, right_frames=right_frames)
 
+    def forward_deferred(self, wav):
+        """forward() with the top_db floor left to the consumer: returns
+        (features before the floor, (slot maxima (B, nslot), top_db)) when
+        the fused spectrum kernel applies (log-mel, no deltas / context), else
+        (forward(wav), None).  ConvolutionFrontEnd.run(..., topdb=...) applies
+        the floor as it loads the rows (lobes/features.py:130-147 with
+        processing/features.py:691-712, one pass over the features fewer)."""
+        fb = self.compute_fbanks
+        if (_can_fuse(self.compute_STFT, fb, wav) and fb.log_mel and fb.top_db is not None and not self.deltas
+                and not self.context):
+            st = self.compute_STFT
+            w, tw1, tw2 = st._tables(wav.device)
+            s0, ln, of, mw = fb.csr_tables(wav.device)
+            _, mult, off, amin, top_db = fb._db_args()
+            feats, slot_max = ops.fbank_deferred(wav, w, tw1, tw2, s0, ln, of, mw, st.n_fft, st.hop_length, st.center,
+                                                 ops.PAD_MODES[st.pad_mode], fb.n_mels, mult, off, amin)
+            return feats, (slot_max, float(top_db))
+        return self.forward(wav), None
+
     def forward(self, wav):
         """Returns the FBANK features of a batch of waveforms."""
         if _can_fuse(self.compute_STFT, self.compute_fbanks, wav):

@@ -17,6 +17,7 @@ import torch.nn as nn
 
 from ... import _autograd as A
 from ... import _enc
+from ... import ops
 from ...nnet.CNN import Conv2d
 from ...nnet.normalization import LayerNorm
 
@@ -238,10 +239,16 @@ class ConvolutionFrontEnd(nn.Module):
         return (c1.in_channels == 1 and c1.out_channels == 64 and c2.in_channels == 64
                 and c2.out_channels % 16 == 0 and c2.out_channels <= 32 and (x.shape[2] - 1) // 2 + 1 <= 40)
 
-    def run(self, x, last_dtype):
-        """Intermediate block outputs in the compute dtype, the last in `last_dtype`."""
+    def run(self, x, last_dtype, topdb=None):
+        """Intermediate block outputs in the compute dtype, the last in
+        `last_dtype`.  topdb = (slot maxima, top_db) from
+        Fbank.forward_deferred: x has not had its top_db floor yet; the fused
+        front-end applies it as it loads the rows, the other paths first."""
         dtype = _enc.compute_dtype()
         blocks = [getattr(self, n) for n in self.block_names]
+        if topdb is not None and not (self._fusable2(x, dtype) and not any(b.wants_train_path(x) for b in blocks)):
+            x = ops.topdb_clamp(x, topdb[0], topdb[1])
+            topdb = None
         if any(b.wants_train_path(x) for b in blocks):
             n = len(blocks)
             for i, b in enumerate(blocks):
@@ -251,7 +258,7 @@ class ConvolutionFrontEnd(nn.Module):
             # both blocks in one kernel: the block-1 activation stays in LDS
             b1, b2 = (getattr(self, n) for n in self.block_names)
             return _enc.conv_frontend2(x.float().contiguous(), b1.params(), b2.params(), b2.wperm(dtype),
-                                       last_dtype)
+                                       last_dtype, topdb=topdb)
         n = len(self.block_names)
         for i, name in enumerate(self.block_names):
             x = getattr(self, name).run(x, last_dtype if i == n - 1 else dtype)

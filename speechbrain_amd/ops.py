@@ -127,6 +127,57 @@ def _(x, window, tw_nc, tw_nfft, mel_start, mel_len, mel_off, mel_w, n_fft, hop,
     return x.new_empty(x.shape[0], n_frames(x.shape[1], n_fft, hop, center), n_mels)
 
 
+@torch.library.custom_op("sbk::fbank_deferred", mutates_args=())
+def fbank_deferred(x: torch.Tensor, window: torch.Tensor, tw_nc: torch.Tensor, tw_nfft: torch.Tensor,
+                   mel_start: torch.Tensor, mel_len: torch.Tensor, mel_off: torch.Tensor, mel_w: torch.Tensor,
+                   n_fft: int, hop: int, center: bool, pad_mode: int, n_mels: int, multiplier: float,
+                   db_offset: float, amin: float) -> tuple[torch.Tensor, torch.Tensor]:
+    """fbank (log_mel) WITHOUT the top_db floor: (dB features (B,T,M), the
+    per-workgroup partial maxima (B, nslot)).  The consumer applies
+    max(x, max_b - top_db) as it loads the rows (sbk_conv_frontend2), so the
+    clamp pass over the features never runs; features.py:691-712 otherwise."""
+    require_device(x, window, tw_nc, tw_nfft, mel_start, mel_len, mel_off, mel_w)
+    x = _c(x.to(_f32))
+    B, S = x.shape
+    T = n_frames(S, n_fft, hop, center)
+    out = torch.empty(B, T, n_mels, device=x.device, dtype=_f32)
+    L = _lib.lib()
+    nslot = L.sbk_spectrum_slots(n_fft, hop, T, n_mels, mel_w.numel())
+    slot_max = torch.empty(B, max(nslot, 1), device=x.device, dtype=_f32)
+    rc = L.sbk_spectrum(2, ptr(x), B, S, 1, n_fft, hop, int(center), pad_mode, T, ptr(window), ptr(tw_nc),
+                        ptr(tw_nfft), 1, 1.0, 1.0, 0.0, 0, None, ptr(mel_start), ptr(mel_len), ptr(mel_off),
+                        ptr(mel_w), mel_w.numel(), n_mels, 1, multiplier, db_offset, amin, ptr(out),
+                        ptr(slot_max), stream_of(x))
+    check(rc, "sbk_spectrum(fbank)")
+    return out, slot_max
+
+
+@fbank_deferred.register_fake
+def _(x, window, tw_nc, tw_nfft, mel_start, mel_len, mel_off, mel_w, n_fft, hop, center, pad_mode, n_mels,
+      multiplier, db_offset, amin):
+    B = x.shape[0]
+    T = n_frames(x.shape[1], n_fft, hop, center)
+    nslot = _lib.lib().sbk_spectrum_slots(n_fft, hop, T, n_mels, mel_w.numel())
+    return x.new_empty(B, T, n_mels), x.new_empty(B, max(nslot, 1))
+
+
+@torch.library.custom_op("sbk::topdb_clamp", mutates_args=())
+def topdb_clamp(x: torch.Tensor, slot_max: torch.Tensor, top_db: float) -> torch.Tensor:
+    """max(x, max_b - top_db) per sequence b of fbank_deferred's output
+    (features.py:706-711), into a new tensor."""
+    require_device(x, slot_max)
+    y = _c(x.to(_f32)).clone()
+    B = y.shape[0]
+    check(_lib.lib().sbk_topdb_clamp(ptr(y), ptr(slot_max), slot_max.shape[1], y.numel() // B, B, float(top_db),
+                                     stream_of(y)), "sbk_topdb_clamp")
+    return y
+
+
+@topdb_clamp.register_fake
+def _(x, slot_max, top_db):
+    return torch.empty_like(x, dtype=_f32)
+
+
 @torch.library.custom_op("sbk::filterbank", mutates_args=())
 def filterbank(spec: torch.Tensor, mel_start: torch.Tensor, mel_len: torch.Tensor, mel_off: torch.Tensor,
                mel_w: torch.Tensor, n_mels: int, log_mel: bool, multiplier: float, db_offset: float,
