@@ -199,6 +199,140 @@ __global__ void __launch_bounds__(256) apply_kernel(const float* src, float* x, 
   }
 }
 
+// ---- 4-wide path (F % 4 == 0, 16-B aligned x / scratch): the kernels
+// above move one float per thread and every apply block re-reduced all the
+// warp blocks' partial sums (3,008 blocks x 24 KB of L2 reads at config 2).
+// Here a thread moves one float4 (its four frequency columns' mask bits
+// computed once), a block covers TT4 = 64 rows, and the two fills are
+// reduced once by a one-block kernel.
+constexpr int TT4 = 64;
+
+__device__ __forceinline__ unsigned col_mask4(const int* m, int n, int nm, int f0) {
+  unsigned cm = 0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (nm && in_masks(m, n, nm, f0 + e)) cm |= 1u << e;
+  return cm;
+}
+
+// y = warp(x) (bicubic / bilinear as warp_kernel; c < 0: no warp, y unused)
+// and the block's partial sums [all, freq-masked cells] of the warped values.
+template <bool CUBIC, bool WARP>
+__global__ void __launch_bounds__(256) warp4_kernel(const float* __restrict__ x, float* __restrict__ y, int N, int T,
+                                                    int F, int c, int w, const int* __restrict__ fmask, int n_fmask,
+                                                    float* __restrict__ partial) {
+  __shared__ float red[16];
+  const int F4 = F >> 2, rpp = 256 / F4;  // float4 columns per row, rows per pass
+  const int ntile = (T + TT4 - 1) / TT4;
+  const int n = blockIdx.x / ntile;
+  const int t0 = (blockIdx.x - n * ntile) * TT4, t1 = min(T, t0 + TT4);
+  const int q = threadIdx.x % F4, tr = threadIdx.x / F4;
+  const float* xn = x + (long long)n * T * F;
+  float* yn = y + (long long)n * T * F;
+  float s_all = 0.f, s_msk = 0.f;
+  if (tr < rpp) {
+    const unsigned cm = col_mask4(fmask, n, n_fmask, 4 * q);
+    for (int t = t0 + tr; t < t1; t += rpp) {
+      float4 v;
+      if (WARP) {
+        const bool left = t < w;
+        const int in_rows = left ? c : T - c, out_rows = left ? w : T - w;
+        const int src0 = left ? 0 : c, dst = left ? t : t - w;
+        if (in_rows == out_rows) {
+          v = *reinterpret_cast<const float4*>(xn + (long long)(src0 + dst) * F + 4 * q);
+        } else {
+          const float scale = out_rows > 1 ? (float)((double)(in_rows - 1) / (double)(out_rows - 1)) : 0.f;
+          const float real = scale * (float)dst;
+          const float fl = floorf(real);
+          const float tt = real - fl;
+          const int i0 = (int)fl;
+          if (CUBIC) {
+            const float wt[4] = {cubic2(tt + 1.f), cubic1(tt), cubic1(1.f - tt), cubic2(2.f - tt)};
+            float4 a[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              a[k] = *reinterpret_cast<const float4*>(xn + (long long)(src0 + min(max(i0 - 1 + k, 0), in_rows - 1)) * F + 4 * q);
+            v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              v.x += wt[k] * a[k].x; v.y += wt[k] * a[k].y; v.z += wt[k] * a[k].z; v.w += wt[k] * a[k].w;
+            }
+          } else {
+            const float l1 = fminf(fmaxf(tt, 0.f), 1.f), l0 = 1.f - l1;
+            const int i1 = i0 + (i0 < in_rows - 1 ? 1 : 0);
+            const float4 a0 = *reinterpret_cast<const float4*>(xn + (long long)(src0 + i0) * F + 4 * q);
+            const float4 a1 = *reinterpret_cast<const float4*>(xn + (long long)(src0 + i1) * F + 4 * q);
+            v = make_float4(l0 * a0.x + l1 * a1.x, l0 * a0.y + l1 * a1.y, l0 * a0.z + l1 * a1.z, l0 * a0.w + l1 * a1.w);
+          }
+        }
+        *reinterpret_cast<float4*>(yn + (long long)t * F + 4 * q) = v;
+      } else {
+        v = *reinterpret_cast<const float4*>(xn + (long long)t * F + 4 * q);
+      }
+      s_all += v.x + v.y + v.z + v.w;
+      s_msk += ((cm & 1) ? v.x : 0.f) + ((cm & 2) ? v.y : 0.f) + ((cm & 4) ? v.z : 0.f) + ((cm & 8) ? v.w : 0.f);
+    }
+  }
+  if (partial) {
+    const float a = block_sum(s_all, red);
+    const float m = block_sum(s_msk, red);
+    if (threadIdx.x == 0) {
+      partial[2 * blockIdx.x] = a;
+      partial[2 * blockIdx.x + 1] = m;
+    }
+  }
+}
+
+// the two fills from the partial sums, once (fixed order: deterministic)
+__global__ void __launch_bounds__(256) fills_kernel(const float* __restrict__ partial, int nparts, int N, int T, int F,
+                                                    long long n_fcells, float* __restrict__ fills) {
+  __shared__ float red[16];
+  float a = 0.f, m = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
+    a += partial[2 * i];
+    m += partial[2 * i + 1];
+  }
+  a = block_sum(a, red);
+  m = block_sum(m, red);
+  if (threadIdx.x == 0) {
+    const double total = (double)N * T * F;
+    const float mean1 = (float)(a / total);
+    fills[0] = mean1;
+    fills[1] = (float)(((double)a - (double)m + (double)mean1 * (double)n_fcells) / total);
+  }
+}
+
+// x = time-masked ? fill_t : freq-masked ? fill_f : src, one float4 per thread
+__global__ void __launch_bounds__(256) apply4_kernel(const float* src, float* x, int N, int T, int F,
+                                                     const int* __restrict__ fmask, int n_fmask,
+                                                     const int* __restrict__ tmask, int n_tmask,
+                                                     const float* __restrict__ fills) {
+  const int F4 = F >> 2, rpp = 256 / F4;
+  const int ntile = (T + TT4 - 1) / TT4;
+  const int n = blockIdx.x / ntile;
+  const int t0 = (blockIdx.x - n * ntile) * TT4, t1 = min(T, t0 + TT4);
+  const int q = threadIdx.x % F4, tr = threadIdx.x / F4;
+  if (tr >= rpp) return;
+  const float fill_f = fills ? fills[0] : 0.f, fill_t = fills ? fills[1] : 0.f;
+  const unsigned cm = col_mask4(fmask, n, n_fmask, 4 * q);
+  for (int t = t0 + tr; t < t1; t += rpp) {
+    const long long i = ((long long)n * T + t) * F + 4 * q;
+    float4 v;
+    if (n_tmask && in_masks(tmask, n, n_tmask, t)) {
+      v = make_float4(fill_t, fill_t, fill_t, fill_t);
+    } else {
+      v = *reinterpret_cast<const float4*>(src + i);
+      if (cm) {
+        if (cm & 1) v.x = fill_f;
+        if (cm & 2) v.y = fill_f;
+        if (cm & 4) v.z = fill_f;
+        if (cm & 8) v.w = fill_f;
+      }
+    }
+    *reinterpret_cast<float4*>(x + i) = v;
+  }
+}
+
 }  // namespace
 
 // Full SpecAugment application on x (N, T, F) fp32, in place.
@@ -213,6 +347,38 @@ SBK_API int sbk_specaugment(float* x, int N, int T, int F, int c, int w, int war
                             const int* tmask, int n_tmask, int use_mean, float* partial, long long n_fcells,
                             void* stream) {
   if (N <= 0 || T <= 0 || F <= 0 || warp_mode < 0 || warp_mode > 1) return SBK_ERR_ARG;
+  hipStream_t s4 = (hipStream_t)stream;
+  if (F % 4 == 0 && F <= 1024 &&
+      ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(tmp) | reinterpret_cast<uintptr_t>(partial)) & 15) == 0) {
+    // 4-wide path; `partial` must hold 2 * N * ceil(T/16) + 2 floats (the fills at its end)
+    const int nblk4 = N * ((T + TT4 - 1) / TT4);
+    float* fills = use_mean ? partial + 2 * N * ((T + 15) / 16) : nullptr;
+    const float* src = x;
+    if (c >= 0) {
+      if (!tmp || c <= 0 || c >= T || w <= 0 || w >= T) return SBK_ERR_ARG;
+      if (warp_mode == 0)
+        hipLaunchKernelGGL((warp4_kernel<true, true>), dim3(nblk4), dim3(256), 0, s4, x, tmp, N, T, F, c, w, fmask,
+                           n_fmask, use_mean ? partial : nullptr);
+      else
+        hipLaunchKernelGGL((warp4_kernel<false, true>), dim3(nblk4), dim3(256), 0, s4, x, tmp, N, T, F, c, w, fmask,
+                           n_fmask, use_mean ? partial : nullptr);
+      SBK_CHECK_LAUNCH();
+      src = tmp;
+    } else if (use_mean) {
+      hipLaunchKernelGGL((warp4_kernel<true, false>), dim3(nblk4), dim3(256), 0, s4, x, nullptr, N, T, F, c, w, fmask,
+                         n_fmask, partial);
+      SBK_CHECK_LAUNCH();
+    }
+    if (c < 0 && n_fmask == 0 && n_tmask == 0) return 0;
+    if (use_mean) {
+      hipLaunchKernelGGL(fills_kernel, dim3(1), dim3(256), 0, s4, partial, nblk4, N, T, F, n_fcells, fills);
+      SBK_CHECK_LAUNCH();
+    }
+    hipLaunchKernelGGL(apply4_kernel, dim3(nblk4), dim3(256), 0, s4, src, x, N, T, F, fmask, n_fmask, tmask, n_tmask,
+                       fills);
+    SBK_CHECK_LAUNCH();
+    return 0;
+  }
   const int TT = 16;
   const int nblk = N * ((T + TT - 1) / TT);
   hipStream_t s = (hipStream_t)stream;
