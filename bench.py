@@ -39,6 +39,12 @@ SR = 16000
 SECONDS = 15.0
 BATCH = 32
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+_T0 = time.perf_counter()
+
+
+def progress(msg):
+    """One line per phase on stderr (stdout carries only the JSON line)."""
+    print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
 def build_model(d_model, dev, layers=12):
@@ -97,23 +103,33 @@ def pick_threads(probe):
     on the host's cores (torch.set_num_threads(os.cpu_count())).  A GPU box's
     process may hold only a share of the machine (OMP_NUM_THREADS is set to
     it), where os.cpu_count() threads oversubscribe; so one short probe pass
-    runs at each candidate — OMP_NUM_THREADS, the affinity mask, os.cpu_count()
-    — and the fastest is used.  Returns (threads, {threads: probe seconds})."""
-    cands = {max(1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0)), _usable_cpus(), os.cpu_count() or 1}
-    cands = sorted(c for c in cands if c >= 1)
+    runs at each candidate — OMP_NUM_THREADS, the affinity mask, os.cpu_count(),
+    those beyond 4x OMP_NUM_THREADS skipped — and the fastest is used.  Returns (threads, {threads: probe seconds})."""
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    cands = {c for c in (omp, _usable_cpus(), os.cpu_count() or 1) if c >= 1}
+    if omp >= 1:  # a share is set: far beyond it only oversubscribes (minutes per pass)
+        cands = {c for c in cands if c <= 4 * omp}
     times = {}
-    for c in cands:
+    for c in sorted(cands):
         torch.set_num_threads(c)
-        probe()  # warm-up at this thread count
         t0 = time.perf_counter()
-        probe()
-        times[c] = round(time.perf_counter() - t0, 4)
+        probe()  # warm-up at this thread count
+        warm = time.perf_counter() - t0
+        if times and warm > 4 * min(times.values()) + 2.0:
+            # oversubscribed (the machine's cores, not this process's share):
+            # a second pass would only spend minutes confirming it
+            times[c] = round(warm, 4)
+        else:
+            t0 = time.perf_counter()
+            probe()
+            times[c] = round(time.perf_counter() - t0, 4)
+        progress(f"thread probe: {c} threads {times[c]:.3f} s")
     best = min(times, key=times.get)
     torch.set_num_threads(best)
     return best, times
 
 
-def cpu_baseline(d_model, n_utt=16, reps=4):
+def cpu_baseline(d_model, n_utt=64, reps=3):
     """Oracle (PyTorch CPU fp32 restatement) on n_utt x 15 s, median of `reps`."""
     import oracle.conformer as OC
     fbank, cnn, tr = build_model(d_model, "cpu")
@@ -125,11 +141,13 @@ def cpu_baseline(d_model, n_utt=16, reps=4):
     with torch.no_grad():
         threads, tried = pick_threads(lambda: OC.fbank_to_encoder(wav[:2], sd_cnn, sd_tr, 12, 4, n_mels=80,
                                                                   wav_len=lens[:2]))
+    progress(f"cpu baseline: {threads} threads (probe {tried})")
     times = []
     with torch.no_grad():
         for r in range(reps + 1):
             t0 = time.perf_counter()
             OC.fbank_to_encoder(wav, sd_cnn, sd_tr, 12, 4, n_mels=80, wav_len=lens)
+            progress(f"cpu baseline rep {r}: {time.perf_counter() - t0:.2f} s")
             if r:
                 times.append(time.perf_counter() - t0)
     med = statistics.median(times)
@@ -422,6 +440,7 @@ def cpu_baseline_c2(batch, n_utt=4, reps=3):
         torch.manual_seed(1234)
         OA.spec_augment(d, time_warp_window=5, freq_mask_width=(0, 30), time_mask_width=(0, 40),
                         replace_with_zero=False)
+        progress(f"cpu baseline rep {r}: {time.perf_counter() - t0:.2f} s")
         if r:
             times.append(time.perf_counter() - t0)
     med = statistics.median(times)
@@ -496,6 +515,7 @@ def cpu_baseline_c5(n_utt=1, reps=2):
         for r in range(reps + 1):
             t0 = time.perf_counter()
             OW.wav2vec_encode(wav, sde, sdw, C5_LAYERS, C5_H, wav_lens=torch.ones(n_utt))
+            progress(f"cpu baseline rep {r}: {time.perf_counter() - t0:.2f} s")
             if r:
                 times.append(time.perf_counter() - t0)
     med = statistics.median(times)
@@ -657,6 +677,7 @@ def main():
     wav_len = torch.ones(args.batch, device=dev)
 
     step = make_step(fbank, cnn, tr, wav, wav_len)
+    progress("model built")
 
     out = step()
     T_e = out.shape[1]
@@ -673,6 +694,7 @@ def main():
         with torch.cuda.graph(graph):
             out = step()
         torch.cuda.synchronize()
+        progress("graph captured")
 
     run = graph.replay if graph is not None else step
     for _ in range(args.warmup):
@@ -691,6 +713,7 @@ def main():
     elapsed = max_over_ranks(mine, world, dev)
     rank_ms = [round(1000.0 * t / args.steps, 4) for t in per_rank(mine, world, dev)]
     ms_per_step = 1000.0 * elapsed / args.steps
+    progress(f"timed {args.steps} steps: {ms_per_step:.3f} ms/step")
     audio = world * args.batch * SECONDS * args.steps
     value = audio / elapsed
 
@@ -728,6 +751,7 @@ def main():
                                 "avg_launch_us": round(1000.0 * ms / n, 3),
                                 "achieved": round(fl / (ms * 1e-3) / 1e12, 2),
                                 "step_share_ms": round(ms, 4)}
+        progress("per-kernel launch timing done")
         dom = max(kern.values(), key=lambda k: k["step_share_ms"]) if kern else None
         traffic = load_traffic()
         res = {

@@ -12,12 +12,23 @@ head's weight gradient and gradient_as_bucket_view buckets all pass through
 DDP.  Each rank takes half of a 4-utterance batch; with accumulation 2 the
 first micro-batch runs under no_sync.
 
-Checks (after two optimizer steps): both ranks end with bit-identical
-parameters, and the all-reduced gradients of the last step equal a
-single-process run on the concatenated batches.  Every
-per-row computation of the path is independent of the other rows of the
-batch, so the two differ only in the fp32 summation order of the weight /
-bias reductions (split-K atomics): normwise 1e-4 per tensor."""
+Checks (two optimizer steps, SGD lr 1e-4; gradients recorded at each step):
+  * both ranks end with bit-identical parameters;
+  * the all-reduced gradients equal one process accumulating the same
+    per-rank micro-batches (grad_accumulation_factor = ranks x accum).  Step 1
+    starts from identical parameters, so only the order of the final fp32
+    sums differs: normwise 1e-5 per tensor in bf16 (5e-4 for the library
+    GRU, whose bf16 solver is chosen per process); 1e-4 in fp32, whose
+    weight-gradient GEMMs split K over fp32 atomics (a rerun of the same
+    process differs by up to 2e-5).  Step 2 starts from parameters that
+    differ in the last fp32 bit: 2e-4 (measured 6.5e-5, the library GRU);
+  * a single-process run on the concatenated batch: in bf16 a gradient that
+    is reduced over the batch INSIDE the step and stored in bf16 — the shared
+    positional projection p_k's (a bf16 activation under autocast, as in the
+    reference) — is rounded once per batch split, bounded by the bf16 step
+    2^-8 (normwise 1e-2; measured 8.5e-3 for linear_pos.weight); in fp32 the
+    rel-pos bias / linear_pos gradients are batch sums that cancel to ~1e-3
+    of their terms, 1e-3 (measured 3e-4)."""
 import os
 import socket
 
@@ -58,7 +69,7 @@ def _brain(dev, fused, run_opts):
     base = BT.brain_class(fused)
 
     class DDPTestBrain(base):
-        grads = None
+        grads = None  # one {name: gradient} per optimizer step
 
         def compute_forward(self, batch, stage):
             hp = self.hparams
@@ -70,17 +81,18 @@ def _brain(dev, fused, run_opts):
                 self.hparams = hp
 
         def check_gradients(self, loss):
-            self.grads = {}
+            g = {}
             for mname, m in self.modules.items():
                 inner = m.module if hasattr(m, "module") else m
                 for n, p in inner.named_parameters():
                     if p.grad is not None:
-                        self.grads[f"{mname}.{n}"] = p.grad.detach().float().cpu().clone()
+                        g[f"{mname}.{n}"] = p.grad.detach().float().cpu().clone()
+            self.grads = (self.grads or []) + [g]
             return super().check_gradients(loss)
 
     mods, hp = BT.build_modules(layers=2, dropout=0.0, fused_head=fused)
     hp = {k: (v.to(dev) if hasattr(v, "to") else v) for k, v in hp.items()}
-    b = DDPTestBrain(modules=mods, opt_class=lambda p: torch.optim.SGD(p, lr=0.05), hparams=hp, run_opts=run_opts)
+    b = DDPTestBrain(modules=mods, opt_class=lambda p: torch.optim.SGD(p, lr=1e-4), hparams=hp, run_opts=run_opts)
     for m in b.modules.values():
         m.train()
     return b
@@ -95,15 +107,23 @@ def _params(brain):
     return out
 
 
-def _run(brain, dev, accum, half=None, steps=2):
+def _run(brain, dev, accum, half=None, steps=2, split=None):
     """`steps` optimizer steps of `accum` micro-batches (a second step also
     catches parameters that never receive a gradient: DDP without
-    find_unused_parameters raises on the next forward)."""
+    find_unused_parameters raises on the next forward).  split = world: the
+    single-process reference of a DDP run — every micro-batch cut into the
+    ranks' parts, fed one after another (grad_accumulation_factor = world x
+    accum)."""
     for micro in range(steps * accum):
         batch = _batch(dev, micro)
         if half is not None:
             batch = [t[half] for t in batch]
-        brain.fit_batch(batch)
+        if split:
+            per = B_ALL // split
+            for r in range(split):
+                brain.fit_batch([t[r * per:(r + 1) * per] for t in batch])
+        else:
+            brain.fit_batch(batch)
 
 
 def _worker(rank, world, port, out, fused, accum):
@@ -140,22 +160,51 @@ def test_brain_ddp_real_modules(dev, fused, accum):
     mp.start_processes(_worker, args=(world, _free_port(), out, fused, accum), nprocs=world, join=True,
                        start_method="spawn")
     (p0, g0), (p1, g1) = out[0], out[1]
-    assert set(p0) == set(p1) and set(g0) == set(g1)
+    assert set(p0) == set(p1) and len(g0) == len(g1) == 2
+    for a, b in zip(g0, g1):  # the all-reduced gradients are the same on both ranks
+        assert set(a) == set(b) and all(torch.equal(a[k], b[k]) for k in a)
     for k in p0:
         assert torch.equal(p0[k], p1[k]), f"ranks differ: {k}"
-    run_opts = {"device": str(dev), "auto_mix_prec": "bf16" if fused else False, "max_grad_norm": 0.0,
-                "grad_accumulation_factor": accum}
-    single = _brain(dev, fused, run_opts)
-    _run(single, dev, accum)
-    gs, ps = single.grads, _params(single)
-    assert set(gs) == set(g0), set(gs) ^ set(g0)
-    assert len(gs) > 50
-    worst = []
-    for k, ref in gs.items():
-        e = ((g0[k].double() - ref.double()).norm() / ref.double().norm().clamp_min(1e-30)).item()
-        worst.append((e, k))
-        assert e <= 1e-4, f"{k}: DDP vs single-process gradient {e:.2e}"
-    print("worst DDP-vs-single gradients:", sorted(worst)[-4:])
-    for k in ps:
-        d = (p0[k] - ps[k]).abs().max().item()
-        assert d <= 1e-4 * max(ps[k].abs().max().item(), 1e-3), f"{k}: parameters {d:.2e}"
+    def single_run(accum_factor, split):
+        ro = {"device": str(dev), "auto_mix_prec": "bf16" if fused else False, "max_grad_norm": 0.0,
+              "grad_accumulation_factor": accum_factor}
+        b = _brain(dev, fused, ro)
+        _run(b, dev, accum, split=split)
+        return b.grads, _params(b)
+
+    def rel(a, b):
+        return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
+
+    def compare(ref_grads, ref_params, tols, what):
+        assert len(ref_grads) == len(g0) == 2
+        for step, (gs, gr, tol) in enumerate(zip(g0, ref_grads, tols)):
+            assert set(gr) == set(gs), set(gr) ^ set(gs)
+            assert len(gr) > 50
+            worst = sorted((rel(gs[k], gr[k]), k) for k in gr)
+            print(f"step {step + 1} worst DDP vs {what}:", worst[-3:])
+            # the library GRU (MIOpen, bf16 under autocast) picks its solver per
+            # process: its bf16 gradients differ across processes at the bf16
+            # rounding level (measured 9.4e-5) though a rerun in one process is
+            # bit-stable
+            bad = [(e, k) for e, k in worst if e > (max(tol, 5e-4) if fused and k.startswith("dec.") else tol)]
+            assert not bad, f"step {step + 1}: DDP vs {what}: gradients beyond {tol}: {bad}"
+        for k in ref_params:
+            d = (p0[k] - ref_params[k]).abs().max().item()
+            assert d <= 1e-4 * max(ref_params[k].abs().max().item(), 1e-3), f"{k}: parameters {d:.2e}"
+
+    # the same per-rank micro-batches accumulated in one process
+    ga, pa = single_run(world * accum, world)
+    gb, _ = single_run(world * accum, world)
+    print("single-process rerun noise, step 1 / 2:",
+          [max(rel(x[k], y[k]) for k in x) for x, y in zip(ga, gb)])
+    # step 1 starts from identical parameters: only the order of the final
+    # fp32 sums differs (plus, fp32, the split-K atomics of the weight-gradient
+    # GEMMs).  Step 2 starts from parameters that differ in the last fp32 bit,
+    # which the bf16 casts (the library GRU's input projection most) turn into
+    # an occasional flipped bf16 rounding: measured <= 6.5e-5.
+    compare(ga, pa, (1e-5 if fused else 1e-4, 2e-4), "single-process accumulation of the ranks' micro-batches")
+    # the concatenated batch: the bf16 batch-reduced p_k gradient as above
+    # (1e-2); fp32, the rel-pos bias and linear_pos gradients are batch sums
+    # that cancel to ~1e-3 of their terms, so 2+2 vs 4-row ordering shows at
+    # ~3e-4 normwise
+    compare(*single_run(accum, None), (1e-2, 1e-2) if fused else (1e-3, 1e-3), "single-process concatenated batch")
