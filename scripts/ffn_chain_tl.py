@@ -35,18 +35,19 @@ x = torch.randn(M, D, device=dev)
 for _ in range(5):
     _enc.ffn_chain(x, la, lb, "swish", 0.0, nl, wp)
 torch.cuda.synchronize()
-buf = (ctypes.c_ulonglong * (16 * 200))()
+buf = (ctypes.c_ulonglong * (16 * 256))()
 lib = ctypes.CDLL(_L.LIB_PATH)
 assert lib.sbk_probe_ffn_tl(buf) == 0
-tl = np.array(buf, dtype=np.int64).reshape(16, 200)
+tl = np.array(buf, dtype=np.int64).reshape(16, 256)
 t0 = tl[:8, 0].min()
 rel = tl[:8] - t0
 for w in range(8):
     r = rel[w]
     st = [r[3 + 2 * s] - r[2 + 2 * s] for s in range(76)]
     gaps = [r[2 + 2 * (s + 1)] - r[3 + 2 * s] for s in range(75)]
-    print(f"w{w}: start {r[0]} loop {r[1]} | A steps {r[2]}..{r[3 + 2 * 31]} | between {r[197]}->{r[198]} | "
-          f"B steps {r[2 + 64]}..{r[3 + 2 * 63]} | epi {r[194]} {r[195]} | proj {r[199]} | end {r[196]}")
+    print(f"w{w}: start {r[0]} loop {r[1]} | A steps {r[2]}..{r[3 + 2 * 31]} | between {r[197]} z {r[200]} "
+          f"postLN {r[201]} LN0b {r[202]} bar {r[203]} ->{r[198]} | B steps {r[2 + 64]}..{r[3 + 2 * 63]} | "
+          f"epi {r[194]} z {r[195]} nextLN {r[204]} xa {r[205]} proj-end {r[206]} | end {r[196]}")
     print(f"   step body  mean A {np.mean(st[:32]):.0f} B {np.mean(st[32:64]):.0f}; "
           f"gap mean {np.mean(gaps):.0f}; phase1/2 bodies {np.mean([st[s] for s in range(32) if s % 8 < 4]):.0f}"
           f"/{np.mean([st[s] for s in range(32) if s % 8 >= 4]):.0f}")

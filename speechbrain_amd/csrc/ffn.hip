@@ -53,6 +53,19 @@
 // VGPR load (30.3 us), a tile-contiguous weight image (29.3 us).
 // Round 2 (layer chain, 58 us): a single-pass row LayerNorm (sum and sum of
 // squares in one LDS exchange, affine prefetched) was no faster (58.4 us).
+// Round 3: no s_waitcnt vmcnt(0) left outside the last step.  The compiler
+// guards a visible LDS access or the first use of a visible global load
+// with vmcnt(0) (it does not count LDS-DMA in order), and __syncthreads()
+// waits for vmcnt(0): each drained the two weight tiles in flight (and, in
+// the tail, the stores).  Hence asm LDS accesses, asm prologue loads with
+// one counted wait, LDS-only barriers, the epilogue vectors copied to LDS in
+// the prologue, lane offsets recomputed instead of hoisted (spills 13 -> 4),
+// and the out / projection stores interleaved into the projection steps
+// with counted waits.  s_memtime timeline: 129.5k -> 128.5k cycles, the
+// steps unchanged at ~1,030 cycles: a step issues 32 KB of LDS-DMA per CU,
+// ~40 B/clk, the per-CU LDS-DMA issue rate (MI355X_MICROARCH ldsdma-fill:
+// 16 KiB per 0.154 us), while its 12 MFMAs per wave fill 384 of them.
+// Fewer weight bytes per CU need more rows per CU than M / 256 = 47.
 #include "mfma.h"
 
 using namespace sbk;
@@ -112,42 +125,84 @@ __device__ __forceinline__ float act_fn(float v, float slope) {
   return v;
 }
 
+// LDS read the compiler cannot see (it would guard a visible one with
+// s_waitcnt vmcnt(0) against the in-flight LDS-DMA tiles, draining stores too)
+__device__ __forceinline__ f32x4 lds_f4(const float* p) {
+  f32x4 v;
+  const uint32_t la = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)p);
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(la) : "memory");
+  return v;
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
+}
+__device__ __forceinline__ float lds_f1(const float* p) {
+  float v;
+  asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+  return v;
+}
+__device__ __forceinline__ void lds_st1(float* p, float v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_st4(float* p, f32x4 v) {
+  asm volatile("ds_write_b128 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_st2(void* p, uint2 v) {
+  const unsigned long long u = (unsigned long long)v.x | ((unsigned long long)v.y << 32);
+  asm volatile("ds_write_b64 %0, %1" ::"v"(lds_addr(p)), "v"(u) : "memory");
+}
+// s_waitcnt lgkmcnt(0) that a value read by the asm LDS loads above depends
+// on: its uses cannot be scheduled before the wait (the first tie waits, the
+// others retire at once)
+template <typename V>
+__device__ __forceinline__ void tie(V& v) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v));
+}
+// workgroup barrier on LDS traffic only: __syncthreads() also waits for
+// vmcnt(0), i.e. for every LDS-DMA tile and store in flight
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+// global load the compiler cannot see: it would follow a visible one's first
+// use with s_waitcnt vmcnt(0) (it does not count LDS-DMA in order), draining
+// the weight tiles issued after it.  The caller waits (asm) and then vtie()s.
+__device__ __forceinline__ f32x4 gld4(const float* p) {
+  f32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ void vtie(f32x4& v) { asm volatile("" : "+v"(v)); }
+
+// s_waitcnt vmcnt(n) for a wave-uniform n known only at run time
+__device__ __forceinline__ void vm_wait(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+  }
+}
+
 // Full-row LayerNorm of the epilogue values z (in place).  Lane (w, g, fr)
 // holds rows mt*16 + fr, units (w*T2 + j)*16 + 4g + e; row statistics are
-// reduced over g by shuffles and over the NW waves through red[NW][BM].
+// reduced over g by shuffles and over the NW waves through red[BM][NW]; gam /
+// bet are LDS copies.  Every LDS access is explicit (asm) and the barriers
+// wait on LDS only, so the weight tiles and stores in flight stay in flight.
 template <int D, int T2, int MT, int NW>
-__device__ __forceinline__ void row_ln(float (&z)[T2][MT][4], float (*red)[FFN_BM], const float* gam,
-                                       const float* bet, float eps, int w, int g, int fr) {
+__device__ __forceinline__ void row_ln(float (&z)[T2][MT][4], float* red, const float* gam, const float* bet, float eps,
+                                       int w, int g, int fr) {
+  static_assert(NW == 8, "two b128 reads per row");
   float mean[MT], rstd[MT];
-  // pass 1: mean
-  {
-    float part[MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      float s = 0.f;
-#pragma unroll
-      for (int j = 0; j < T2; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) s += z[j][mt][e];
-      s = col4_sum(s);
-      part[mt] = s;
-    }
-    __syncthreads();
-    if (g == 0) {
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) red[w][mt * 16 + fr] = part[mt];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      float t = 0.f;
-#pragma unroll
-      for (int k = 0; k < NW; ++k) t += red[k][mt * 16 + fr];
-      mean[mt] = t / D;
-    }
-  }
-  // pass 2: variance about the mean
-  {
+  for (int pass = 0; pass < 2; ++pass) {
     float part[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -156,41 +211,78 @@ __device__ __forceinline__ void row_ln(float (&z)[T2][MT][4], float (*red)[FFN_B
       for (int j = 0; j < T2; ++j)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float dv = z[j][mt][e] - mean[mt];
-          s += dv * dv;
+          const float dv = pass ? z[j][mt][e] - mean[mt] : z[j][mt][e];
+          s += pass ? dv * dv : dv;
         }
-      s = col4_sum(s);
-      part[mt] = s;
+      part[mt] = col4_sum(s);
     }
-    __syncthreads();
+    lds_barrier();  // the previous readers of red are done
     if (g == 0) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) red[w][mt * 16 + fr] = part[mt];
+      for (int mt = 0; mt < MT; ++mt) lds_st1(red + (mt * 16 + fr) * NW + w, part[mt]);
     }
-    __syncthreads();
+    lds_barrier();
+    f32x4 rv[MT][2];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      float t = 0.f;
+      rv[mt][0] = lds_f4(red + (mt * 16 + fr) * NW);
+      rv[mt][1] = lds_f4(red + (mt * 16 + fr) * NW + 4);
+    }
 #pragma unroll
-      for (int k = 0; k < NW; ++k) t += red[k][mt * 16 + fr];
-      rstd[mt] = 1.0f / sqrtf(t / D + eps);
+    for (int mt = 0; mt < MT; ++mt) {
+      tie(rv[mt][0]);
+      tie(rv[mt][1]);
+      const float t = (rv[mt][0][0] + rv[mt][0][1]) + (rv[mt][0][2] + rv[mt][0][3]) + (rv[mt][1][0] + rv[mt][1][1]) +
+                      (rv[mt][1][2] + rv[mt][1][3]);
+      if (pass)
+        rstd[mt] = 1.0f / sqrtf(t / D + eps);
+      else
+        mean[mt] = t / D;
     }
   }
+  f32x4 gv[T2], bv[T2];
 #pragma unroll
   for (int j = 0; j < T2; ++j) {
     const int d = (w * T2 + j) * 16 + 4 * g;
-    const float4 g4 = *reinterpret_cast<const float4*>(gam + d), b4 = *reinterpret_cast<const float4*>(bet + d);
-    const float gm[4] = {g4.x, g4.y, g4.z, g4.w}, bt[4] = {b4.x, b4.y, b4.z, b4.w};
+    gv[j] = lds_f4(gam + d);
+    bv[j] = lds_f4(bet + d);
+  }
+#pragma unroll
+  for (int j = 0; j < T2; ++j) {
+    tie(gv[j]);
+    tie(bv[j]);
 #pragma unroll
     for (int e = 0; e < 4; ++e)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) z[j][mt][e] = (z[j][mt][e] - mean[mt]) * rstd[mt] * gm[e] + bt[e];
+      for (int mt = 0; mt < MT; ++mt) z[j][mt][e] = (z[j][mt][e] - mean[mt]) * rstd[mt] * gv[j][e] + bv[j][e];
   }
+}
+
+// A-operand fragments of the LayerNorm'd rows (Xn, bf16, row stride XS)
+// into VGPRs for every K-step of a block
+template <int K1, int KS, int MT, int XS, int BK>
+__device__ __forceinline__ void load_frags(bf16x8 (&xa)[K1][KS][MT], const bf16_t* Xn, int fr, int fk) {
+#pragma unroll
+  for (int r = 0; r < K1; ++r)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        asm volatile("ds_read_b128 %0, %1"
+                     : "=v"(xa[r][ks][mt])
+                     : "v"(lds_addr(Xn + (mt * 16 + fr) * XS + r * BK + ks * 32 + fk))
+                     : "memory");
+#pragma unroll
+  for (int r = 0; r < K1; ++r)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) tie(xa[r][ks][mt]);
 }
 
 #ifdef SBK_PROBE_TL
 // probe build only: s_memtime timeline of 4 waves (wg 0 wave 0, wg 0 last wave, wg 128, wg 250)
-__device__ unsigned long long g_ffn_tl[16][200];
+__device__ unsigned long long g_ffn_tl[16][256];
 #define FFN_TL(i)                                                                 \
   do {                                                                            \
     if (tl_rec >= 0 && lane == 0) g_ffn_tl[tl_rec][i] = __builtin_amdgcn_s_memtime(); \
@@ -221,7 +313,12 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   bf16_t* Xn = ring + NB * TROWS * BK;                      // BM x XS
   bf16_t* Hs = Xn + BM * XS;                                // 2 x BM x HS
   float* b1s = reinterpret_cast<float*>(Hs + 2 * BM * HS);  // H (CHAIN: 2 H, block A then B)
-  float (*red)[BM] = reinterpret_cast<float (*)[BM]>(b1s + (CHAIN ? 2 : 1) * a.H);  // NW x BM
+  float* red = b1s + (CHAIN ? 2 : 1) * a.H;                 // BM x NW row partials
+  // epilogue vectors, copied to LDS in the prologue so that no global load
+  // (and its in-order vmcnt wait behind the weight tiles) sits between blocks
+  float* prm = red + BM * NW;                               // P_* x D
+  enum { P_B2 = 0, P_GP, P_BP, P_G0B, P_B0B, P_B2B, P_GN, P_BN, P_N };
+  static_assert(P_N == NW, "one parameter row per wave");
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int fr = lane & 15, g = lane >> 4, fk = 8 * g;
@@ -242,28 +339,34 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   // the x rows of the LayerNorm, so their latency overlaps the first weight
   // tiles instead of being paid again after the last MFMA.
   constexpr int NRW = (BM + NW - 1) / NW;    // LN rows per wave
-  float4 xres[T][MT];
+  f32x4 xres[T][MT];
 #pragma unroll
   for (int j = 0; j < T; ++j)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int row = min(m0 + mt * 16 + fr, a.M - 1);
-      xres[j][mt] = *reinterpret_cast<const float4*>(a.x + (long long)row * D + (w * T + j) * 16 + 4 * g);
+      xres[j][mt] = gld4(a.x + (long long)row * D + (w * T + j) * 16 + 4 * g);
     }
-  float4 xv[NRW];
+  f32x4 xv[NRW];
 #pragma unroll
   for (int i = 0; i < NRW; ++i) {
     const int rr = w + i * NW, row = min(m0 + rr, a.M - 1);
-    xv[i] = *reinterpret_cast<const float4*>(a.x + (long long)row * D + lane * PER);
+    xv[i] = gld4(a.x + (long long)row * D + lane * PER);
   }
-  const float4 g04 = *reinterpret_cast<const float4*>(a.g0 + lane * PER);
-  const float4 b04 = *reinterpret_cast<const float4*>(a.b0 + lane * PER);
+  f32x4 g04 = gld4(a.g0 + lane * PER), b04 = gld4(a.b0 + lane * PER);
+  // wave w loads parameter row w (null rows are never read); lane-quads of b1 / b1b
+  const float* psrc = w == P_B2 ? a.b2 : w == P_GP ? a.gp : w == P_BP ? a.bp : w == P_G0B ? a.g0b
+                    : w == P_B0B ? a.b0b : w == P_B2B ? a.b2b : w == P_GN ? a.gn : a.bn;
+  f32x4 pv = f32x4{0.f, 0.f, 0.f, 0.f}, b1v = pv, b1bv = pv;
+  if (psrc) pv = gld4(psrc + lane * PER);
+  const bool b1t = tid * 4 < a.H;
+  if (b1t) b1v = gld4(a.b1 + tid * 4);
+  if (CHAIN && b1t) b1bv = gld4(a.b1b + tid * 4);
   // ---- weight tile s -> ring slot (LDS-DMA, 1 KB = 8 rows per wave-instruction)
   // lane L of instruction i writes row R0 + L/8, 16-B chunk L%8 (linear image)
   // and fetches source chunk (L%8) ^ ((row >> 1) & 7): the read side applies
   // the same involution.  Steps S.. are the projection's (256 columns of Wp
   // by 64 k per tile, column block after column block).
-  const int lrow = lane >> 3, lchk = lane & 7;
   auto issue = [&](int s, int slot) __attribute__((always_inline)) {
     const bf16_t* base;
     int ld;
@@ -282,17 +385,34 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
       ld = p1 ? D : a.H;
     }
     bf16_t* dst = ring + slot * TROWS * BK;
+    // the lane's source offsets are recomputed per issue from an opaque lane
+    // id: hoisted, they would hold 2 x GL 64-bit addresses through the launch
+    int ln;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
 #pragma unroll
     for (int i = 0; i < GL; ++i) {
       const int r0 = w * (T * 16) + i * 8;  // the wave's own rows: it is their only reader
-      const int row = r0 + lrow;
-      const bf16_t* src = base + (long long)row * ld + ((lchk ^ ((row >> 1) & 7)) << 3);
+      const int row = r0 + (ln >> 3);
+      const bf16_t* src = base + (row * ld + (((ln & 7) ^ ((row >> 1) & 7)) << 3));
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(dst + r0 * BK), 16, 0, 0);
     }
   };
   issue(0, 0);
   issue(1, 1);
+  // every load above has landed; the two tiles stay in flight
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB * GL) : "memory");
+#pragma unroll
+  for (int j = 0; j < T; ++j)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) vtie(xres[j][mt]);
+#pragma unroll
+  for (int i = 0; i < NRW; ++i) vtie(xv[i]);
+  vtie(g04);
+  vtie(b04);
+  vtie(pv);
+  vtie(b1v);
+  vtie(b1bv);
 
   // LayerNorm of the workgroup's rows -> Xn (bf16); b1 -> LDS
 #pragma unroll
@@ -300,20 +420,21 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     const int rr = w + i * NW;
     if (rr >= BM) break;
     const bool live = m0 + rr < a.M;
-    const float v[4] = {live ? xv[i].x : 0.f, live ? xv[i].y : 0.f, live ? xv[i].z : 0.f, live ? xv[i].w : 0.f};
+    const float v[4] = {live ? xv[i][0] : 0.f, live ? xv[i][1] : 0.f, live ? xv[i][2] : 0.f, live ? xv[i][3] : 0.f};
     const float mean = wave_sum_v(v[0] + v[1] + v[2] + v[3]) / D;
     float q = 0.f;
 #pragma unroll
     for (int e = 0; e < 4; ++e) q += (v[e] - mean) * (v[e] - mean);
     const float rstd = 1.0f / sqrtf(wave_sum_v(q) / D + a.eps0);
     uint2 pk;
-    pk.x = pack_bf16x2((v[0] - mean) * rstd * g04.x + b04.x, (v[1] - mean) * rstd * g04.y + b04.y);
-    pk.y = pack_bf16x2((v[2] - mean) * rstd * g04.z + b04.z, (v[3] - mean) * rstd * g04.w + b04.w);
-    *reinterpret_cast<uint2*>(Xn + rr * XS + lane * PER) = pk;
+    pk.x = pack_bf16x2((v[0] - mean) * rstd * g04[0] + b04[0], (v[1] - mean) * rstd * g04[1] + b04[1]);
+    pk.y = pack_bf16x2((v[2] - mean) * rstd * g04[2] + b04[2], (v[3] - mean) * rstd * g04[3] + b04[3]);
+    lds_st2(Xn + rr * XS + lane * PER, pk);
   }
-  for (int i = tid; i < a.H; i += NT) b1s[i] = a.b1[i];
-  if (CHAIN)
-    for (int i = tid; i < a.H; i += NT) b1s[a.H + i] = a.b1b[i];
+  static_assert(2048 <= NT * 4, "b1 in one float4 per thread");
+  if (psrc) lds_st4(prm + w * D + lane * PER, pv);
+  if (b1t) lds_st4(b1s + tid * 4, b1v);
+  if (CHAIN && b1t) lds_st4(b1s + a.H + tid * 4, b1bv);
 
   f32x4 acc1[T][MT], acc2[T][MT];
 #pragma unroll
@@ -335,15 +456,9 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   // 8 waves 40.8 us, 16 waves spill; weights streamed straight into VGPRs
   // with 4 steps in flight instead of LDS-DMA — 45 us at 8 or 16 waves.)
   FFN_TL(1);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
+  lds_barrier();
   bf16x8 xa[K1][BK / 32][MT];
-#pragma unroll
-  for (int r = 0; r < K1; ++r)
-#pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks)
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) xa[r][ks][mt] = ld8(Xn + (mt * 16 + fr) * XS + r * BK + ks * 32 + fk);
+  load_frags<K1, BK / 32, MT, XS, BK>(xa, Xn, fr, fk);
   for (int stage = 0; stage < (CHAIN ? 2 : 1); ++stage) {
   if (CHAIN && stage == 1) {
     FFN_TL(197);
@@ -354,24 +469,28 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
 #pragma unroll
     for (int j = 0; j < T; ++j) {
       const int d = (w * T + j) * 16 + 4 * g;
-      const float4 bb = *reinterpret_cast<const float4*>(a.b2 + d);
+      f32x4 bb = lds_f4(prm + P_B2 * D + d);
+      tie(bb);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const float4 xr = xres[j][mt];
-        z[j][mt][0] = xr.x + a.alpha * (acc2[j][mt][0] + bb.x);
-        z[j][mt][1] = xr.y + a.alpha * (acc2[j][mt][1] + bb.y);
-        z[j][mt][2] = xr.z + a.alpha * (acc2[j][mt][2] + bb.z);
-        z[j][mt][3] = xr.w + a.alpha * (acc2[j][mt][3] + bb.w);
+        const f32x4 xr = xres[j][mt];
+        z[j][mt][0] = xr[0] + a.alpha * (acc2[j][mt][0] + bb[0]);
+        z[j][mt][1] = xr[1] + a.alpha * (acc2[j][mt][1] + bb[1]);
+        z[j][mt][2] = xr[2] + a.alpha * (acc2[j][mt][2] + bb[2]);
+        z[j][mt][3] = xr[3] + a.alpha * (acc2[j][mt][3] + bb[3]);
         acc1[j][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
         acc2[j][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
-    if (a.gp) row_ln<D, T, MT, NW>(z, red, a.gp, a.bp, a.epsp, w, g, fr);
+    FFN_TL(200);
+    if (a.gp) row_ln<D, T, MT, NW>(z, red, prm + P_GP * D, prm + P_BP * D, a.epsp, w, g, fr);
+    FFN_TL(201);
 #pragma unroll
     for (int j = 0; j < T; ++j)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) xres[j][mt] = make_float4(z[j][mt][0], z[j][mt][1], z[j][mt][2], z[j][mt][3]);
-    row_ln<D, T, MT, NW>(z, red, a.g0b, a.b0b, a.eps0b, w, g, fr);
+      for (int mt = 0; mt < MT; ++mt) xres[j][mt] = f32x4{z[j][mt][0], z[j][mt][1], z[j][mt][2], z[j][mt][3]};
+    row_ln<D, T, MT, NW>(z, red, prm + P_G0B * D, prm + P_B0B * D, a.eps0b, w, g, fr);
+    FFN_TL(202);
 #pragma unroll
     for (int j = 0; j < T; ++j) {
       const int d = (w * T + j) * 16 + 4 * g;
@@ -380,22 +499,12 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
         uint2 pk;
         pk.x = pack_bf16x2(z[j][mt][0], z[j][mt][1]);
         pk.y = pack_bf16x2(z[j][mt][2], z[j][mt][3]);
-        *reinterpret_cast<uint2*>(Xn + (mt * 16 + fr) * XS + d) = pk;
+        lds_st2(Xn + (mt * 16 + fr) * XS + d, pk);
       }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-#pragma unroll
-    for (int r = 0; r < K1; ++r)
-#pragma unroll
-      for (int ks = 0; ks < BK / 32; ++ks)
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const uint32_t la =
-              (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) bf16_t*)(Xn + (mt * 16 + fr) * XS + r * BK + ks * 32 + fk));
-          asm volatile("ds_read_b128 %0, %1" : "=v"(xa[r][ks][mt]) : "v"(la) : "memory");
-        }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    lds_barrier();
+    FFN_TL(203);
+    load_frags<K1, BK / 32, MT, XS, BK>(xa, Xn, fr, fk);
     FFN_TL(198);
   }
   for (int c = 0; c < NCH; ++c)
@@ -479,121 +588,165 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
 
   // ---- epilogue: lane holds rows m = mt*16 + fr, units d = (w*T + j)*16 + 4g .. +3
   // (CHAIN: the parameters of block B, which has no post-LN)
-  const float* b2f = CHAIN ? a.b2b : a.b2;
+  const float* b2f = prm + (CHAIN ? P_B2B : P_B2) * D;
   const float alphaf = CHAIN ? a.alphab : a.alpha;
-  const float* gpf = CHAIN ? nullptr : a.gp;
+  const bool postln = !CHAIN && a.gp;
   float z[T][MT][4];
 #pragma unroll
   for (int j = 0; j < T; ++j) {
     const int d = (w * T + j) * 16 + 4 * g;
-    const float4 bb = *reinterpret_cast<const float4*>(b2f + d);
+    f32x4 bb = lds_f4(b2f + d);
+    tie(bb);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      const float4 xr = xres[j][mt];
-      z[j][mt][0] = xr.x + alphaf * (acc2[j][mt][0] + bb.x);
-      z[j][mt][1] = xr.y + alphaf * (acc2[j][mt][1] + bb.y);
-      z[j][mt][2] = xr.z + alphaf * (acc2[j][mt][2] + bb.z);
-      z[j][mt][3] = xr.w + alphaf * (acc2[j][mt][3] + bb.w);
+      const f32x4 xr = xres[j][mt];
+      z[j][mt][0] = xr[0] + alphaf * (acc2[j][mt][0] + bb[0]);
+      z[j][mt][1] = xr[1] + alphaf * (acc2[j][mt][1] + bb[1]);
+      z[j][mt][2] = xr[2] + alphaf * (acc2[j][mt][2] + bb[2]);
+      z[j][mt][3] = xr[3] + alphaf * (acc2[j][mt][3] + bb[3]);
     }
   }
   FFN_TL(195);
-  if (gpf) row_ln<D, T, MT, NW>(z, red, gpf, a.bp, a.epsp, w, g, fr);
+  if (postln) row_ln<D, T, MT, NW>(z, red, prm + P_GP * D, prm + P_BP * D, a.epsp, w, g, fr);
   if (PROJ) {
-    // u = next-LN(out) -> Xn (bf16, the A operand of the projection), then
-    // the out stores: every compiler-visible LDS access precedes them, so no
-    // alias-guard wait drains them before the projection steps
-    float zo[T][MT][4];
+    // the out rows wait in LDS (over the hidden-chunk buffers, free once the
+    // row_ln barriers have passed) until the last weight tile has landed: a
+    // store is counted by vmcnt like the LDS-DMA tiles, so a store issued
+    // before a tile wait would hold that wait for its HBM write
+    float* Zo = reinterpret_cast<float*>(Hs);  // BM x ZS fp32
+    constexpr int ZS = D + 4;
+    static_assert(BM * ZS * 4 <= 2 * BM * HS * 2, "out rows fit over Hs");
 #pragma unroll
     for (int j = 0; j < T; ++j)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) zo[j][mt][e] = z[j][mt][e];
-    row_ln<D, T, MT, NW>(z, red, a.gn, a.bn, a.epsn, w, g, fr);
+      for (int mt = 0; mt < MT; ++mt) xres[j][mt] = f32x4{z[j][mt][0], z[j][mt][1], z[j][mt][2], z[j][mt][3]};
+    // u = next-LN(out) -> Xn (bf16) -> VGPR fragments, the A operand of the projection
+    row_ln<D, T, MT, NW>(z, red, prm + P_GN * D, prm + P_BN * D, a.epsn, w, g, fr);
+    FFN_TL(204);
 #pragma unroll
     for (int j = 0; j < T; ++j) {
       const int d = (w * T + j) * 16 + 4 * g;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
+        lds_st4(Zo + (mt * 16 + fr) * ZS + d, xres[j][mt]);
         uint2 pk;
         pk.x = pack_bf16x2(z[j][mt][0], z[j][mt][1]);
         pk.y = pack_bf16x2(z[j][mt][2], z[j][mt][3]);
-        *reinterpret_cast<uint2*>(Xn + (mt * 16 + fr) * XS + d) = pk;
+        lds_st2(Xn + (mt * 16 + fr) * XS + d, pk);
       }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-#pragma unroll
-    for (int r = 0; r < K1; ++r)
-#pragma unroll
-      for (int ks = 0; ks < BK / 32; ++ks)
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const uint32_t la =
-              (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) bf16_t*)(Xn + (mt * 16 + fr) * XS + r * BK + ks * 32 + fk));
-          asm volatile("ds_read_b128 %0, %1" : "=v"(xa[r][ks][mt]) : "v"(la) : "memory");
-        }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const bool full = m0 + BM <= a.M;  // every out / projection store of this workgroup is issued
-#pragma unroll
-    for (int j = 0; j < T; ++j) {
-      const int d = (w * T + j) * 16 + 4 * g;
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int row = m0 + mt * 16 + fr;
-        if (row < a.M)
-          *reinterpret_cast<float4*>(a.out + (long long)row * D + d) =
-              make_float4(zo[j][mt][0], zo[j][mt][1], zo[j][mt][2], zo[j][mt][3]);
-      }
-    }
-    // ---- projection y = u . Wp^T (bf16), 256 output columns per K1 steps
-    for (int s = SF; s < ST; s += K1) {
-      const int nc = (s - SF) / K1;
-      FFN_TL(199);
+    lds_barrier();
+    FFN_TL(205);
+    // ---- projection y = u . Wp^T (bf16), 256 output columns per K1 steps.
+    // Stores go out T per step during the first MT steps of every column
+    // block, each right after that step's DMA issue: the out rows in block 0,
+    // block nc-1's y rows in block nc (the last block's after the loop).  A
+    // tile wait counts the stores younger than its tile, so a store only has
+    // to land before the wait two steps on instead of holding the next one
+    // (a store counts in vmcnt like the LDS-DMA tiles).  Workgroups with rows
+    // past M store unconditionally-counted nothing: their stores come at the
+    // block ends / the end and their waits assume none younger.  No reloads
+    // past ST-1.
+    static_assert(MT <= K1, "stores of a column block fit in its steps");
+    const int ncp = a.np / TROWS;
+    const bool full = m0 + BM <= a.M;
+    uint2 yq[T][MT];  // the previous column block's y (bf16)
+    for (int nc = 0; nc < ncp; ++nc) {
 #pragma unroll
       for (int r = 0; r < K1; ++r) {
-        // tile s+r landed: younger than it are tile s+r+1 and, on the first
-        // step after a store burst (T*MT stores per lane, all issued only in
-        // full workgroups), those stores
-        if (r == 0 && full)
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL * (NB - 1) + T * MT) : "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL * (NB - 1)) : "memory");
-        const bf16_t* tile = ring + ((s + r) % NB) * TROWS * BK;
+        const int s = SF + nc * K1 + r;
+        // stores of the two steps before (k(x) = T if step x stored)
+        const int kprev1 = (r >= 1 ? (r - 1 < MT) : (K1 - 1 < MT)) ? T : 0;
+        const int kprev2 = (r >= 2 ? (r - 2 < MT) : (K1 + r - 2 < MT)) ? T : 0;
+        const int k1 = (r >= 1 || nc > 0) ? kprev1 : 0, k2 = (r >= 2 || nc > 0) ? kprev2 : 0;
+        vm_wait((s + 1 < ST ? GL : 0) + (full ? k1 + k2 : 0));
+        const bf16_t* tile = ring + (s % NB) * TROWS * BK;
+        // fragment offsets from an opaque lane id (hoisted, they spill)
+        int ln;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+        const int lfr = ln & 15, lg = ln >> 4;
         bf16x8 fw[BK / 32][T];
 #pragma unroll
         for (int ks = 0; ks < BK / 32; ++ks)
 #pragma unroll
           for (int t = 0; t < T; ++t) {
-            const int row = w * (T * 16) + t * 16 + fr;
-            fw[ks][t] = ld8(tile + row * BK + (((ks * 4 + g) ^ ((row >> 1) & 7)) << 3));
+            const int row = w * (T * 16) + t * 16 + lfr;
+            fw[ks][t] = ld8(tile + row * BK + (((ks * 4 + lg) ^ ((row >> 1) & 7)) << 3));
           }
+        // the A operand from Xn each step (not held in VGPRs here: the
+        // registers go to the deferred stores instead)
+        bf16x8 fx[BK / 32][MT];
+#pragma unroll
+        for (int ks = 0; ks < BK / 32; ++ks)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const uint32_t la = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) bf16_t*)(
+                Xn + (mt * 16 + fr) * XS + r * BK + ks * 32 + fk));
+            asm volatile("ds_read_b128 %0, %1" : "=v"(fx[ks][mt]) : "v"(la) : "memory");
+          }
+        f32x4 ov[T];
+        if (r < MT && full && nc == 0) {
+#pragma unroll
+          for (int j = 0; j < T; ++j) ov[j] = lds_f4(Zo + (r * 16 + lfr) * ZS + (w * T + j) * 16 + 4 * lg);
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        issue(min(s + r + NB, ST - 1), (s + r) % NB);
+        if (s + NB < ST) issue(s + NB, s % NB);
+        asm volatile("" ::: "memory");  // the stores stay behind the DMA issue (the counts above)
+        if (r < MT && full) {
+          const long long row = m0 + r * 16 + lfr;
+          if (nc == 0) {
+#pragma unroll
+            for (int j = 0; j < T; ++j)
+              *reinterpret_cast<f32x4*>(a.out + row * D + (w * T + j) * 16 + 4 * lg) = ov[j];
+          } else {
+#pragma unroll
+            for (int t = 0; t < T; ++t)
+              *reinterpret_cast<uint2*>(a.yp + row * a.np + (nc - 1) * TROWS + w * (T * 16) + t * 16 + 4 * lg) = yq[t][r];
+          }
+        }
 #pragma unroll
         for (int ks = 0; ks < BK / 32; ++ks)
 #pragma unroll
           for (int t = 0; t < T; ++t)
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
-              acc1[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ks][t], xa[r][ks][mt], acc1[t][mt], 0, 0, 0);
+              acc1[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ks][t], fx[ks][mt], acc1[t][mt], 0, 0, 0);
       }
+      int ln;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
 #pragma unroll
-      for (int t = 0; t < T; ++t) {
-        const int n = nc * TROWS + w * (T * 16) + t * 16 + 4 * g;
+      for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const f32x4 v = acc1[t][mt];
+          yq[t][mt].x = pack_bf16x2(v[0], v[1]);
+          yq[t][mt].y = pack_bf16x2(v[2], v[3]);
+          acc1[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+          const int row = m0 + mt * 16 + (ln & 15);
+          if ((!full || nc == ncp - 1) && row < a.M)
+            *reinterpret_cast<uint2*>(a.yp + (long long)row * a.np + nc * TROWS + w * (T * 16) + t * 16 + 4 * (ln >> 4)) =
+                yq[t][mt];
+        }
+    }
+    FFN_TL(206);
+    if (!full) {
+      f32x4 ov[T][MT];
+#pragma unroll
+      for (int j = 0; j < T; ++j)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) ov[j][mt] = lds_f4(Zo + (mt * 16 + fr) * ZS + (w * T + j) * 16 + 4 * g);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < T; ++j)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const int row = m0 + mt * 16 + fr;
-          const f32x4 v = acc1[t][mt];
-          uint2 pk;
-          pk.x = pack_bf16x2(v[0], v[1]);
-          pk.y = pack_bf16x2(v[2], v[3]);
-          if (row < a.M) *reinterpret_cast<uint2*>(a.yp + (long long)row * a.np + n) = pk;
-          acc1[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (row < a.M) *reinterpret_cast<f32x4*>(a.out + (long long)row * D + (w * T + j) * 16 + 4 * g) = ov[j][mt];
         }
-      }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the tail reloads
+#ifdef SBK_PROBE_TL
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // probe: the end marker includes the store drain
+#endif
     FFN_TL(196);
     return;
   }
@@ -610,7 +763,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     }
   }
   if (a.gn) {
-    row_ln<D, T, MT, NW>(z, red, a.gn, a.bn, a.epsn, w, g, fr);
+    row_ln<D, T, MT, NW>(z, red, prm + P_GN * D, prm + P_BN * D, a.epsn, w, g, fr);
 #pragma unroll
     for (int j = 0; j < T; ++j) {
       const int d = (w * T + j) * 16 + 4 * g;
@@ -635,9 +788,10 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
 
 template <int D>
 size_t ffn_lds(int H, bool chain) {
-  // 2-slot weight ring, Xn, two hidden-chunk buffers, b1 (two with CHAIN), the row-reduction scratch
+  // 2-slot weight ring, Xn, two hidden-chunk buffers, b1 (two with CHAIN), the row-reduction scratch,
+  // the epilogue parameter rows
   return ((size_t)2 * 256 * 64 + (size_t)FFN_BM * (D + 16) + (size_t)2 * FFN_BM * (256 + 16)) * sizeof(bf16_t) +
-         (size_t)(chain ? 2 : 1) * H * 4 + (size_t)FFN_NW * FFN_BM * 4;
+         (size_t)(chain ? 2 : 1) * H * 4 + (size_t)FFN_NW * FFN_BM * 4 + (size_t)FFN_NW * D * 4;
 }
 
 template <int D, int ACT, bool PROJ, bool CHAIN>

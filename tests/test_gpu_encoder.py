@@ -159,7 +159,8 @@ def test_fused_ffn_vs_unfused(dev, D, H, M):
     assert_close(out2, z, rtol=2e-2, name="ffn no post-LN")
 
 
-@pytest.mark.parametrize("H,M,NP", [(1024, 12032, 768), (1024, 1000, 768), (512, 48, 256), (2048, 333, 512)])
+@pytest.mark.parametrize("H,M,NP", [(1024, 12032, 768), (1024, 1000, 768), (512, 48, 256), (2048, 333, 512),
+                                    (1024, 500, 1024)])
 def test_fused_ffn_proj_vs_unfused(dev, H, M, NP):
     """sbk_ffn_proj (the FFN block + next-LN + the MHSA in_proj, one kernel)
     vs sbk_ffn's u output through the separate sbk_gemm: the same rounding
