@@ -99,7 +99,7 @@ int sbk_context_window(const float* x, float* y, int N, int T, int F, int left, 
  * 1 bilinear — the align_corners interpolate modes of :134-148) through
  * `tmp`, then frequency / time masks given as device int32 (N, n, 2)
  * [len, pos] arrays drawn on the host, filled with 0 or the running means
- * (use_mean; `partial` scratch of 2*N*ceil(T/16) + 2 floats, 16-B aligned;
+ * (use_mean; `partial` scratch of 2*N*ceil(T/4) + 2 floats, 16-B aligned;
  * n_fcells = number of frequency-masked cells).  F % 4 == 0 with 16-B
  * aligned x / tmp takes the float4 kernels. */
 int sbk_specaugment(float* x, int N, int T, int F, int c, int w, int warp_mode, float* tmp, const int* fmask,

@@ -31,9 +31,7 @@ using namespace sbk;
 
 namespace {
 
-#ifndef SBK_ATT_MINW
-#define SBK_ATT_MINW 2  // waves per SIMD the register budget must allow
-#endif
+
 constexpr int QB = 64;        // queries per workgroup
 constexpr int KC = 64;        // keys per chunk
 constexpr int PBR = KC + QB;  // positional band rows staged per chunk (127 used)
@@ -94,21 +92,14 @@ __device__ __forceinline__ bf16x8 vt_frag_tr(const bf16_t* V, int KR, int k0, in
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-#ifdef SBK_PROBE_TL
-__device__ unsigned long long g_att_tl[4][64];
-__device__ unsigned long long g_att_wg[4096][4];  // per workgroup: memtime / memrealtime at start and end, HW_ID
-#define ATT_TL(i)                                                                        \
-  do {                                                                                   \
-    if (tl_on && lane == 0 && (i) < 64) g_att_tl[w][i] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-#else
-#define ATT_TL(i) \
-  do {            \
-  } while (0)
-#endif
+// s_memtime marks of the waves of one workgroup, and per workgroup its
+// memrealtime / memtime at start and end (probe builds only)
+SBK_PROBE_BUFFER(g_att_tl, 4, 64)
+SBK_PROBE_BUFFER(g_att_wg, 4096, 4)
+#define ATT_TL(i) SBK_PROBE(if (tl_on && lane == 0 && (i) < 64) g_att_tl[w][i] = __builtin_amdgcn_s_memtime();)
 
 template <typename T, int DHP, bool PROBS>
-__global__ void __launch_bounds__(256, SBK_ATT_MINW) relpos_flash_kernel(const T* __restrict__ qkv, const T* __restrict__ pk,
+__global__ void __launch_bounds__(256, 2) relpos_flash_kernel(const T* __restrict__ qkv, const T* __restrict__ pk,
                                                            const float* __restrict__ pbu,
                                                            const float* __restrict__ pbv,
                                                            const uint8_t* __restrict__ kpm, int B, int Tn, int H,
@@ -147,9 +138,7 @@ __global__ void __launch_bounds__(256, SBK_ATT_MINW) relpos_flash_kernel(const T
   const int bh = tile / nqb;
   const int h = bh % H, b = bh / H;
   const int i0 = qb * QB;
-#ifdef SBK_PROBE_TL
-  const bool tl_on = tile == 200 && sizeof(T) == 2 && !PROBS;
-#endif
+  SBK_PROBE(const bool tl_on = tile == 200 && sizeof(T) == 2 && !PROBS;)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c16 = lane & 15, g = lane >> 4;
   const int i0w = i0 + 16 * w;
@@ -586,9 +575,7 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c16 = lane & 15, g = lane >> 4;
   const int my_i = i0 + 16 * w + c16;
-#ifdef SBK_PROBE_TL
-  const bool tl_on = tile == 200;
-#endif
+  SBK_PROBE(const bool tl_on = tile == 200;)
   const bf16_t* qkv_b = qkv + (long long)b * Tn * row3 + h * 3 * dh;
   const bf16_t* pk_h = pk + h * dh;
   float* gq = Gs + w * 16 * G2 + c16 * G2 + GO;  // this lane's query row of the G scratch, at key 0
@@ -648,12 +635,10 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
     }
   };
   ATT_TL(0);
-#ifdef SBK_PROBE_TL
-  if (tid == 0 && orig < 4096) {
+  SBK_PROBE(if (tid == 0 && orig < 4096) {
     g_att_wg[orig][0] = __builtin_amdgcn_s_memrealtime();
     g_att_wg[orig][2] = __builtin_amdgcn_s_memtime();
-  }
-#endif
+  })
   dma_kp(0);
   const int nchunk = (Tn + KC - 1) / KC;  // <= 64 (launcher)
   // Key padding: which chunks hold a padded key, as a 64-bit chunk bitmap
@@ -836,13 +821,10 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
     }
   }
   ATT_TL(62);
-#ifdef SBK_PROBE_TL
-  __syncthreads();
-  if (tid == 0 && orig < 4096) {
+  SBK_PROBE(__syncthreads(); if (tid == 0 && orig < 4096) {
     g_att_wg[orig][1] = __builtin_amdgcn_s_memrealtime();
     g_att_wg[orig][3] = __builtin_amdgcn_s_memtime();
-  }
-#endif
+  })
 }
 
 int launch_dma(const void* qkv, const void* pk, int ldp, const float* pbu, const float* pbv, const uint8_t* kpm, int B,
@@ -928,14 +910,8 @@ SBK_API int sbk_relpos_attention_mask(int dtype_bf16, const void* qkv, const voi
                                        am_sh);
 }
 
-#ifdef SBK_PROBE_TL
-SBK_API int sbk_probe_att_tl(unsigned long long* out) {
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_att_tl), sizeof(g_att_tl), 0, hipMemcpyDeviceToHost);
-}
-SBK_API int sbk_probe_att_wg(unsigned long long* out) {
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_att_wg), sizeof(g_att_wg), 0, hipMemcpyDeviceToHost);
-}
-#endif
+SBK_PROBE_EXPORT(sbk_probe_att_tl, g_att_tl)
+SBK_PROBE_EXPORT(sbk_probe_att_wg, g_att_wg)
 
 SBK_API long long sbk_relpos_attention_lds(int dtype_bf16, int Tn, int dh) {
   (void)Tn;

@@ -203,9 +203,12 @@ __global__ void __launch_bounds__(256) apply_kernel(const float* src, float* x, 
 // above move one float per thread and every apply block re-reduced all the
 // warp blocks' partial sums (3,008 blocks x 24 KB of L2 reads at config 2).
 // Here a thread moves one float4 (its four frequency columns' mask bits
-// computed once), a block covers TT4 = 64 rows, and the two fills are
-// reduced once by a one-block kernel.
-constexpr int TT4 = 64;
+// computed once) for UR rows whose loads (all taps) are issued together, a
+// block covers UR x (256 / (F/4)) rows (16 at F = 240: 3,008 blocks at
+// config 2, ~12 per CU), and the two fills are reduced once by a one-block
+// kernel.  (A first version walked 64 rows per block one row at a time:
+// 752 blocks, each thread's 16 dependent-latency iterations; 104 us.)
+constexpr int UR = 4;
 
 __device__ __forceinline__ unsigned col_mask4(const int* m, int n, int nm, int f0) {
   unsigned cm = 0;
@@ -215,60 +218,88 @@ __device__ __forceinline__ unsigned col_mask4(const int* m, int n, int nm, int f
   return cm;
 }
 
+__host__ __device__ __forceinline__ int rows_per_block4(int F) { return UR * (256 / (F >> 2)); }
+
 // y = warp(x) (bicubic / bilinear as warp_kernel; c < 0: no warp, y unused)
 // and the block's partial sums [all, freq-masked cells] of the warped values.
 template <bool CUBIC, bool WARP>
 __global__ void __launch_bounds__(256) warp4_kernel(const float* __restrict__ x, float* __restrict__ y, int N, int T,
                                                     int F, int c, int w, const int* __restrict__ fmask, int n_fmask,
                                                     float* __restrict__ partial) {
+  constexpr int NTAP = WARP ? (CUBIC ? 4 : 2) : 1;
   __shared__ float red[16];
-  const int F4 = F >> 2, rpp = 256 / F4;  // float4 columns per row, rows per pass
-  const int ntile = (T + TT4 - 1) / TT4;
+  const int F4 = F >> 2, rpp = 256 / F4, RB = UR * rpp;
+  const int ntile = (T + RB - 1) / RB;
   const int n = blockIdx.x / ntile;
-  const int t0 = (blockIdx.x - n * ntile) * TT4, t1 = min(T, t0 + TT4);
+  const int t0 = (blockIdx.x - n * ntile) * RB;
   const int q = threadIdx.x % F4, tr = threadIdx.x / F4;
   const float* xn = x + (long long)n * T * F;
   float* yn = y + (long long)n * T * F;
   float s_all = 0.f, s_msk = 0.f;
   if (tr < rpp) {
     const unsigned cm = col_mask4(fmask, n, n_fmask, 4 * q);
-    for (int t = t0 + tr; t < t1; t += rpp) {
-      float4 v;
-      if (WARP) {
+    float4 a[UR][NTAP];
+    float wt[UR][NTAP];
+    bool ident[UR];
+    // every tap of the UR rows first
+#pragma unroll
+    for (int u = 0; u < UR; ++u) {
+      const int t = min(t0 + tr + u * rpp, T - 1);
+      if constexpr (WARP) {
         const bool left = t < w;
         const int in_rows = left ? c : T - c, out_rows = left ? w : T - w;
         const int src0 = left ? 0 : c, dst = left ? t : t - w;
-        if (in_rows == out_rows) {
-          v = *reinterpret_cast<const float4*>(xn + (long long)(src0 + dst) * F + 4 * q);
-        } else {
-          const float scale = out_rows > 1 ? (float)((double)(in_rows - 1) / (double)(out_rows - 1)) : 0.f;
-          const float real = scale * (float)dst;
-          const float fl = floorf(real);
-          const float tt = real - fl;
-          const int i0 = (int)fl;
-          if (CUBIC) {
-            const float wt[4] = {cubic2(tt + 1.f), cubic1(tt), cubic1(1.f - tt), cubic2(2.f - tt)};
-            float4 a[4];
+        ident[u] = in_rows == out_rows;
+        const float scale = out_rows > 1 ? (float)((double)(in_rows - 1) / (double)(out_rows - 1)) : 0.f;
+        const float real = scale * (float)dst;
+        const float fl = floorf(real);
+        const float tt = real - fl;
+        const int i0 = (int)fl;
+        if constexpr (CUBIC) {
+          wt[u][0] = cubic2(tt + 1.f);
+          wt[u][1] = cubic1(tt);
+          wt[u][2] = cubic1(1.f - tt);
+          wt[u][3] = cubic2(2.f - tt);
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-              a[k] = *reinterpret_cast<const float4*>(xn + (long long)(src0 + min(max(i0 - 1 + k, 0), in_rows - 1)) * F + 4 * q);
-            v = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              v.x += wt[k] * a[k].x; v.y += wt[k] * a[k].y; v.z += wt[k] * a[k].z; v.w += wt[k] * a[k].w;
-            }
-          } else {
-            const float l1 = fminf(fmaxf(tt, 0.f), 1.f), l0 = 1.f - l1;
-            const int i1 = i0 + (i0 < in_rows - 1 ? 1 : 0);
-            const float4 a0 = *reinterpret_cast<const float4*>(xn + (long long)(src0 + i0) * F + 4 * q);
-            const float4 a1 = *reinterpret_cast<const float4*>(xn + (long long)(src0 + i1) * F + 4 * q);
-            v = make_float4(l0 * a0.x + l1 * a1.x, l0 * a0.y + l1 * a1.y, l0 * a0.z + l1 * a1.z, l0 * a0.w + l1 * a1.w);
+          for (int k = 0; k < NTAP; ++k) {
+            const int r = ident[u] ? dst : min(max(i0 - 1 + k, 0), in_rows - 1);
+            a[u][k] = *reinterpret_cast<const float4*>(xn + (long long)(src0 + r) * F + 4 * q);
           }
+        } else {
+          const float l1 = fminf(fmaxf(tt, 0.f), 1.f);
+          wt[u][0] = 1.f - l1;
+          wt[u][NTAP - 1] = l1;
+          const int i1 = i0 + (i0 < in_rows - 1 ? 1 : 0);
+          a[u][0] = *reinterpret_cast<const float4*>(xn + (long long)(src0 + (ident[u] ? dst : i0)) * F + 4 * q);
+          a[u][NTAP - 1] = *reinterpret_cast<const float4*>(xn + (long long)(src0 + (ident[u] ? dst : i1)) * F + 4 * q);
         }
-        *reinterpret_cast<float4*>(yn + (long long)t * F + 4 * q) = v;
       } else {
-        v = *reinterpret_cast<const float4*>(xn + (long long)t * F + 4 * q);
+        ident[u] = true;
+        a[u][0] = *reinterpret_cast<const float4*>(xn + (long long)t * F + 4 * q);
       }
+    }
+#pragma unroll
+    for (int u = 0; u < UR; ++u) {
+      const int t = t0 + tr + u * rpp;
+      if (t >= T) continue;
+      float4 v;
+      if (ident[u]) {
+        v = a[u][WARP && CUBIC ? 1 : 0];
+      } else {
+        v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (CUBIC) {
+#pragma unroll
+          for (int k = 0; k < NTAP; ++k) {
+            v.x += wt[u][k] * a[u][k].x; v.y += wt[u][k] * a[u][k].y;
+            v.z += wt[u][k] * a[u][k].z; v.w += wt[u][k] * a[u][k].w;
+          }
+        } else {
+          const float l0 = wt[u][0], l1 = wt[u][NTAP - 1];
+          const float4 a0 = a[u][0], a1 = a[u][NTAP - 1];
+          v = make_float4(l0 * a0.x + l1 * a1.x, l0 * a0.y + l1 * a1.y, l0 * a0.z + l1 * a1.z, l0 * a0.w + l1 * a1.w);
+        }
+      }
+      if (WARP) *reinterpret_cast<float4*>(yn + (long long)t * F + 4 * q) = v;
       s_all += v.x + v.y + v.z + v.w;
       s_msk += ((cm & 1) ? v.x : 0.f) + ((cm & 2) ? v.y : 0.f) + ((cm & 4) ? v.z : 0.f) + ((cm & 8) ? v.w : 0.f);
     }
@@ -283,14 +314,24 @@ __global__ void __launch_bounds__(256) warp4_kernel(const float* __restrict__ x,
   }
 }
 
-// the two fills from the partial sums, once (fixed order: deterministic)
-__global__ void __launch_bounds__(256) fills_kernel(const float* __restrict__ partial, int nparts, int N, int T, int F,
-                                                    long long n_fcells, float* __restrict__ fills) {
+// the two fills from the partial sums, once (fixed order: deterministic);
+// 1024 threads, four independent pair loads in flight per thread
+__global__ void __launch_bounds__(1024) fills_kernel(const float* __restrict__ partial, int nparts, int N, int T,
+                                                     int F, long long n_fcells, float* __restrict__ fills) {
   __shared__ float red[16];
   float a = 0.f, m = 0.f;
-  for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
-    a += partial[2 * i];
-    m += partial[2 * i + 1];
+  for (int i0 = threadIdx.x; i0 < nparts; i0 += 4 * blockDim.x) {
+    float2 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = i0 + k * blockDim.x;
+      v[k] = i < nparts ? *reinterpret_cast<const float2*>(partial + 2 * i) : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      a += v[k].x;
+      m += v[k].y;
+    }
   }
   a = block_sum(a, red);
   m = block_sum(m, red);
@@ -302,34 +343,40 @@ __global__ void __launch_bounds__(256) fills_kernel(const float* __restrict__ pa
   }
 }
 
-// x = time-masked ? fill_t : freq-masked ? fill_f : src, one float4 per thread
+// x = time-masked ? fill_t : freq-masked ? fill_f : src, one float4 per
+// thread and row, UR rows per thread loaded together
 __global__ void __launch_bounds__(256) apply4_kernel(const float* src, float* x, int N, int T, int F,
                                                      const int* __restrict__ fmask, int n_fmask,
                                                      const int* __restrict__ tmask, int n_tmask,
                                                      const float* __restrict__ fills) {
-  const int F4 = F >> 2, rpp = 256 / F4;
-  const int ntile = (T + TT4 - 1) / TT4;
+  const int F4 = F >> 2, rpp = 256 / F4, RB = UR * rpp;
+  const int ntile = (T + RB - 1) / RB;
   const int n = blockIdx.x / ntile;
-  const int t0 = (blockIdx.x - n * ntile) * TT4, t1 = min(T, t0 + TT4);
+  const int t0 = (blockIdx.x - n * ntile) * RB;
   const int q = threadIdx.x % F4, tr = threadIdx.x / F4;
   if (tr >= rpp) return;
   const float fill_f = fills ? fills[0] : 0.f, fill_t = fills ? fills[1] : 0.f;
   const unsigned cm = col_mask4(fmask, n, n_fmask, 4 * q);
-  for (int t = t0 + tr; t < t1; t += rpp) {
-    const long long i = ((long long)n * T + t) * F + 4 * q;
-    float4 v;
+  float4 v[UR];
+#pragma unroll
+  for (int u = 0; u < UR; ++u) {
+    const int t = min(t0 + tr + u * rpp, T - 1);
+    v[u] = *reinterpret_cast<const float4*>(src + ((long long)n * T + t) * F + 4 * q);
+  }
+#pragma unroll
+  for (int u = 0; u < UR; ++u) {
+    const int t = t0 + tr + u * rpp;
+    if (t >= T) continue;
+    float4 o = v[u];
     if (n_tmask && in_masks(tmask, n, n_tmask, t)) {
-      v = make_float4(fill_t, fill_t, fill_t, fill_t);
-    } else {
-      v = *reinterpret_cast<const float4*>(src + i);
-      if (cm) {
-        if (cm & 1) v.x = fill_f;
-        if (cm & 2) v.y = fill_f;
-        if (cm & 4) v.z = fill_f;
-        if (cm & 8) v.w = fill_f;
-      }
+      o = make_float4(fill_t, fill_t, fill_t, fill_t);
+    } else if (cm) {
+      if (cm & 1) o.x = fill_f;
+      if (cm & 2) o.y = fill_f;
+      if (cm & 4) o.z = fill_f;
+      if (cm & 8) o.w = fill_f;
     }
-    *reinterpret_cast<float4*>(x + i) = v;
+    *reinterpret_cast<float4*>(x + ((long long)n * T + t) * F + 4 * q) = o;
   }
 }
 
@@ -340,7 +387,7 @@ __global__ void __launch_bounds__(256) apply4_kernel(const float* src, float* x,
 //   tmp: (N, T, F) scratch, required when warping;
 //   fmask (N, n_fmask, 2) / tmask (N, n_tmask, 2) int32 [len, pos] device arrays (or n_* = 0);
 //   use_mean: fill with the running means (replace_with_zero=False), else 0;
-//   partial: scratch of 2 * N * ceil(T/16) floats (when use_mean);
+//   partial: scratch of 2 * N * ceil(T/4) + 2 floats (when use_mean);
 //   n_fcells: number of frequency-masked cells (host-computed, for the second mean).
 SBK_API int sbk_specaugment(float* x, int N, int T, int F, int c, int w, int warp_mode, float* tmp, const int* fmask,
                             int n_fmask,
@@ -350,9 +397,10 @@ SBK_API int sbk_specaugment(float* x, int N, int T, int F, int c, int w, int war
   hipStream_t s4 = (hipStream_t)stream;
   if (F % 4 == 0 && F <= 1024 &&
       ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(tmp) | reinterpret_cast<uintptr_t>(partial)) & 15) == 0) {
-    // 4-wide path; `partial` must hold 2 * N * ceil(T/16) + 2 floats (the fills at its end)
-    const int nblk4 = N * ((T + TT4 - 1) / TT4);
-    float* fills = use_mean ? partial + 2 * N * ((T + 15) / 16) : nullptr;
+    // 4-wide path; `partial` must hold 2 * N * ceil(T/4) + 2 floats (the fills at its end)
+    const int rb = rows_per_block4(F);  // >= UR = 4
+    const int nblk4 = N * ((T + rb - 1) / rb);
+    float* fills = use_mean ? partial + 2 * N * ((T + 3) / 4) : nullptr;
     const float* src = x;
     if (c >= 0) {
       if (!tmp || c <= 0 || c >= T || w <= 0 || w >= T) return SBK_ERR_ARG;
@@ -371,7 +419,7 @@ SBK_API int sbk_specaugment(float* x, int N, int T, int F, int c, int w, int war
     }
     if (c < 0 && n_fmask == 0 && n_tmask == 0) return 0;
     if (use_mean) {
-      hipLaunchKernelGGL(fills_kernel, dim3(1), dim3(256), 0, s4, partial, nblk4, N, T, F, n_fcells, fills);
+      hipLaunchKernelGGL(fills_kernel, dim3(1), dim3(1024), 0, s4, partial, nblk4, N, T, F, n_fcells, fills);
       SBK_CHECK_LAUNCH();
     }
     hipLaunchKernelGGL(apply4_kernel, dim3(nblk4), dim3(256), 0, s4, src, x, N, T, F, fmask, n_fmask, tmask, n_tmask,

@@ -454,17 +454,9 @@ __global__ void __launch_bounds__(256) conv_block_mfma_kernel(const T* __restric
 // LN statistics as wave reductions (no workgroup barrier per row).
 // (Tried: two rows per pass over all 10 waves with cross-wave LN reductions
 // and VALU FMAs: 188 us; one row per wave on VALU FMAs: 130 us.)
-#ifdef SBK_PROBE_TL
-__device__ unsigned long long g_fe_tl[10][16];
-#define FE_TL(i)                                                                   \
-  do {                                                                             \
-    if (blockIdx.x == 700 && lane == 0) g_fe_tl[w][i] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-#else
-#define FE_TL(i) \
-  do {           \
-  } while (0)
-#endif
+// s_memtime marks of the waves of workgroup 700 (probe builds only)
+SBK_PROBE_BUFFER(g_fe_tl, 10, 16)
+#define FE_TL(i) SBK_PROBE(if (blockIdx.x == 700 && lane == 0) g_fe_tl[w][i] = __builtin_amdgcn_s_memtime();)
 
 // 10 waves x 8 output rows (17 block-1 rows: passes of 10 and 7 rows).
 // (8 waves x 7 rows with the block-1 LN affine held in VGPRs: 133 us.)
@@ -883,11 +875,7 @@ inline int grid_for(long long n, int block) {
 
 }  // namespace
 
-#ifdef SBK_PROBE_TL
-SBK_API int sbk_probe_fe_tl(unsigned long long* out) {
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fe_tl), sizeof(g_fe_tl), 0, hipMemcpyDeviceToHost);
-}
-#endif
+SBK_PROBE_EXPORT(sbk_probe_fe_tl, g_fe_tl)
 
 SBK_API int sbk_layernorm(const float* x, int M, int D, const float* g1, const float* b1, float eps1, void* out1,
                           int out1_bf16, const float* g2, const float* b2, float eps2, void* out2, int out2_bf16,

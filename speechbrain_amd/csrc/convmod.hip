@@ -69,18 +69,10 @@ struct ConvModArgs {
   const float* bo;   // (D) or null
 };
 
-#ifdef SBK_PROBE_TL
-__device__ unsigned long long g_cm_tl[16][8];
-#define CM_TL(i)                                                                   \
-  do {                                                                             \
-    if (blockIdx.x == 100 && (threadIdx.x & 63) == 0)                              \
-      g_cm_tl[threadIdx.x >> 6][i] = __builtin_amdgcn_s_memtime();                 \
-  } while (0)
-#else
+// s_memtime phase marks of the waves of workgroup 100 (probe builds only)
+SBK_PROBE_BUFFER(g_cm_tl, 16, 8)
 #define CM_TL(i) \
-  do {           \
-  } while (0)
-#endif
+  SBK_PROBE(if (blockIdx.x == 100 && (threadIdx.x & 63) == 0) g_cm_tl[threadIdx.x >> 6][i] = __builtin_amdgcn_s_memtime();)
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
 // operations, not for its outstanding global loads (a __syncthreads() fence
@@ -510,11 +502,7 @@ constexpr size_t conv_module_lds() {
 
 }  // namespace
 
-#ifdef SBK_PROBE_TL
-SBK_API int sbk_probe_cm_tl(unsigned long long* out) {
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cm_tl), sizeof(g_cm_tl), 0, hipMemcpyDeviceToHost);
-}
-#endif
+SBK_PROBE_EXPORT(sbk_probe_cm_tl, g_cm_tl)
 
 SBK_API int sbk_conv_module_supported(int D, int K) { return D == CM_D && K >= 1 && K <= CM_KMAX; }
 

@@ -280,18 +280,9 @@ __device__ __forceinline__ void load_frags(bf16x8 (&xa)[K1][KS][MT], const bf16_
       for (int mt = 0; mt < MT; ++mt) tie(xa[r][ks][mt]);
 }
 
-#ifdef SBK_PROBE_TL
-// probe build only: s_memtime timeline of 4 waves (wg 0 wave 0, wg 0 last wave, wg 128, wg 250)
-__device__ unsigned long long g_ffn_tl[16][256];
-#define FFN_TL(i)                                                                 \
-  do {                                                                            \
-    if (tl_rec >= 0 && lane == 0) g_ffn_tl[tl_rec][i] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-#else
-#define FFN_TL(i) \
-  do {            \
-  } while (0)
-#endif
+// s_memtime timeline of the waves of workgroup 128 (probe builds only)
+SBK_PROBE_BUFFER(g_ffn_tl, 16, 256)
+#define FFN_TL(i) SBK_PROBE(if (tl_rec >= 0 && lane == 0) g_ffn_tl[tl_rec][i] = __builtin_amdgcn_s_memtime();)
 
 template <int D, int ACT, bool PROJ, bool CHAIN>
 __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
@@ -328,9 +319,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   const int SF = CHAIN ? 2 * S : S;                     // FFN K-steps (blocks A, B)
   const int SP = PROJ ? (a.np / TROWS) * K1 : 0;        // projection K-steps
   const int ST = SF + SP;
-#ifdef SBK_PROBE_TL
-  const int tl_rec = blockIdx.x == 128 ? w : -1;
-#endif
+  SBK_PROBE(const int tl_rec = blockIdx.x == 128 ? w : -1;)
   FFN_TL(0);
 
   // ---- prologue.  Every HBM read of the launch is issued here, before the
@@ -744,9 +733,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
           if (row < a.M) *reinterpret_cast<f32x4*>(a.out + (long long)row * D + (w * T + j) * 16 + 4 * g) = ov[j][mt];
         }
     }
-#ifdef SBK_PROBE_TL
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // probe: the end marker includes the store drain
-#endif
+    SBK_PROBE(asm volatile("s_waitcnt vmcnt(0)" ::: "memory");)  // the end mark includes the store drain
     FFN_TL(196);
     return;
   }
@@ -828,11 +815,7 @@ int ffn_dispatch(const FfnArgs& a, hipStream_t s) {
 
 }  // namespace
 
-#ifdef SBK_PROBE_TL
-SBK_API int sbk_probe_ffn_tl(unsigned long long* out) {
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ffn_tl), sizeof(g_ffn_tl), 0, hipMemcpyDeviceToHost);
-}
-#endif
+SBK_PROBE_EXPORT(sbk_probe_ffn_tl, g_ffn_tl)
 
 SBK_API int sbk_ffn_supported(int D, int H) { return D == 256 && H > 0 && H % 256 == 0 && H <= 2048; }
 

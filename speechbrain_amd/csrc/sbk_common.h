@@ -15,6 +15,22 @@
 
 #define SBK_ERR_ARG 1001  // invalid argument (shape/config) detected on host
 
+// Timeline probes: s_memtime marks compiled only into the probe builds of
+// scripts/probe_build.sh (-DSBK_PROBE_TL, never the product library, which
+// the probe scripts then load in its place); in the product every
+// SBK_PROBE(...) expands to nothing.
+#ifdef SBK_PROBE_TL
+#define SBK_PROBE(...) __VA_ARGS__
+#else
+#define SBK_PROBE(...)
+#endif
+// a device buffer of probe marks and its host read-back entry
+#define SBK_PROBE_BUFFER(name, rows, cols) SBK_PROBE(__device__ unsigned long long name[rows][cols];)
+#define SBK_PROBE_EXPORT(fn, name)                                                                     \
+  SBK_PROBE(SBK_API int fn(unsigned long long* out) {                                                  \
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(name), sizeof(name), 0, hipMemcpyDeviceToHost);    \
+  })
+
 namespace sbk {
 
 constexpr int kWave = 64;

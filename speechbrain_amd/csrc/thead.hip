@@ -31,11 +31,8 @@ using namespace sbk;
 
 namespace {
 
-#ifndef SBK_TH_BN
-#define SBK_TH_BN 128
-#endif
-// 96 KB of W ring in either tile width: 12 x 8 KB or 6 x 16 KB
-constexpr int TH_BM = 128, TH_BN = SBK_TH_BN, TH_BK = 64, TH_NT = 512, TH_NB = 12 * 64 / TH_BN;
+// 96 KB of W ring: 6 slots of 128 vocabulary rows x 64 k (16 KB)
+constexpr int TH_BM = 128, TH_BN = 128, TH_BK = 64, TH_NT = 512, TH_NB = 12 * 64 / TH_BN;
 
 struct TheadArgs {
   const float* tn;    // (B, T, J) fp32

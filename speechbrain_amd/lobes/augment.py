@@ -28,7 +28,7 @@ def specaugment_(x: torch.Tensor, N: int, T: int, F: int, c: int, w: int, fm: Op
     the batch-mean fill when use_mean (augment.py:116-201)."""
     tmp = torch.empty_like(x) if c >= 0 else None
     # partial sums (+ the two fills of the 4-wide path at the end)
-    partial = torch.empty(2 * N * ((T + 15) // 16) + 4, device=x.device, dtype=torch.float32) if use_mean else None
+    partial = torch.empty(2 * N * ((T + 3) // 4) + 4, device=x.device, dtype=torch.float32) if use_mean else None
     n_f = fm.shape[1] if fm is not None else 0
     n_t = tm.shape[1] if tm is not None else 0
     rc = lib().sbk_specaugment(ptr(x), N, T, F, c, w, int(warp_mode), ptr(tmp), ptr(fm), n_f, ptr(tm), n_t,
