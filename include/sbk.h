@@ -90,6 +90,12 @@ int sbk_dct(const float* x, const float* D, float* y, long long rows, int n_in, 
 /* Deltas.forward (features.py:829-852) along time of (N, T, F); concat=1
  * writes [x | d1 | d2] (N, T, 3F) in one pass (lobes/features.py:141-144). */
 int sbk_deltas(const float* x, float* y, int N, int T, int F, int window_length, int concat, void* stream);
+/* processing/features.py:706-711 + lobes/features.py:141-144: the
+ * [x | Δx | ΔΔx] concat of a log-mel fbank whose top_db floor was deferred
+ * (sbk_spectrum's per-workgroup maxima slot_max (N, nslot)); x is floored
+ * at max_b - top_db as it loads.  F % 4 == 0, 16-B aligned. */
+int sbk_deltas_floor(const float* x, float* y, int N, int T, int F, int window_length, const float* slot_max,
+                     int nslot, float top_db, void* stream);
 
 /* ContextWindow.forward (features.py:917-937): (N, T, F) -> (N, T, F*(l+r+1)). */
 int sbk_context_window(const float* x, float* y, int N, int T, int F, int left, int right, void* stream);

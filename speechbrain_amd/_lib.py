@@ -37,6 +37,7 @@ SIGNATURES = {
     "sbk_magnitude": [_vp, _vp, _ll, _i, _f, _f, _i, _vp],
     "sbk_dct": [_vp, _vp, _vp, _ll, _i, _i, _vp],
     "sbk_deltas": [_vp, _vp, _i, _i, _i, _i, _i, _vp],
+    "sbk_deltas_floor": [_vp, _vp, _i, _i, _i, _i, _vp, _i, _f, _vp],
     "sbk_context_window": [_vp, _vp, _i, _i, _i, _i, _i, _vp],
     # gemm.hip
     "sbk_gemm_glu_group": [_i],

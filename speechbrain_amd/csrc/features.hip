@@ -583,6 +583,92 @@ __global__ void __launch_bounds__(256) deltas_kernel(const float* __restrict__ x
   }
 }
 
+// The [x | d1 | d2] concat with float4 columns (F % 4 == 0, 16-B aligned):
+// the scalar kernel above moved one float per thread with an integer divide
+// per element (30.6 us at config 2, 2.0 TB/s).  Here each thread moves
+// float4s, the tile load issues four independent loads per thread before
+// any LDS store, and each output row leaves as 3 x F/4 float4 stores.  Same
+// arithmetic order per element as deltas_kernel<true>.
+// slot_max (optional): the fbank's per-workgroup maxima of sequence b
+// (sbk_spectrum with the floor deferred): x is floored at max_b - top_db as
+// it loads (features.py:706-711, the separate clamp pass folded in).
+__global__ void __launch_bounds__(256) deltas4_concat_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                             int N, int T, int F, int n, float denom, int ttile,
+                                                             const float* __restrict__ slot_max, int nslot,
+                                                             float top_db) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ float red[4];
+  const int F4 = F >> 2, halo = 2 * n;
+  const int ntile = (T + ttile - 1) / ttile;
+  const int b = blockIdx.x / ntile;
+  const int t0 = (blockIdx.x - b * ntile) * ttile;
+  const int nt = min(ttile, T - t0);
+  const int rows = nt + 2 * halo;
+  float4* xs = reinterpret_cast<float4*>(smem);
+  float4* d1s = xs + rows * F4;
+  const float4* xb = reinterpret_cast<const float4*>(x + (long long)b * T * F);
+  const int nld = rows * F4;
+  float fl = -INFINITY;
+  if (slot_max) {
+    float m = -INFINITY;
+    for (int i = threadIdx.x; i < nslot; i += 256) m = fmaxf(m, slot_max[(long long)b * nslot + i]);
+    fl = block_max(m, red) - top_db;
+  }
+  for (int base = threadIdx.x; base < nld; base += 4 * 256) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = min(base + u * 256, nld - 1), r = i / F4, q = i - r * F4;
+      const int t = min(max(t0 - halo + r, 0), T - 1);
+      v[u] = xb[(long long)t * F4 + q];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (base + u * 256 < nld) {
+        float4 w = v[u];
+        if (slot_max) w = make_float4(fmaxf(w.x, fl), fmaxf(w.y, fl), fmaxf(w.z, fl), fmaxf(w.w, fl));
+        xs[base + u * 256] = w;
+      }
+  }
+  __syncthreads();
+  // d1 over rows [halo - n, halo + nt + n), replicate padding applied to d1
+  const int r1lo = halo - n, r1hi = halo + nt + n;
+  for (int i = threadIdx.x; i < (r1hi - r1lo) * F4; i += 256) {
+    const int rr = i / F4 + r1lo, q = i % F4;
+    const int t = min(max(t0 - halo + rr, 0), T - 1);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 1; k <= n; ++k) {
+      const float4 p = xs[(min(t + k, T - 1) - (t0 - halo)) * F4 + q];
+      const float4 m = xs[(max(t - k, 0) - (t0 - halo)) * F4 + q];
+      const float kf = (float)k;
+      acc.x = fmaf(kf, p.x - m.x, acc.x);
+      acc.y = fmaf(kf, p.y - m.y, acc.y);
+      acc.z = fmaf(kf, p.z - m.z, acc.z);
+      acc.w = fmaf(kf, p.w - m.w, acc.w);
+    }
+    d1s[rr * F4 + q] = make_float4(acc.x / denom, acc.y / denom, acc.z / denom, acc.w / denom);
+  }
+  __syncthreads();
+  float4* yb = reinterpret_cast<float4*>(y + ((long long)b * T + t0) * 3 * F);
+  for (int i = threadIdx.x; i < nt * F4; i += 256) {
+    const int lr = i / F4, q = i - lr * F4;
+    const int r = lr + halo;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 1; k <= n; ++k) {
+      const float4 p = d1s[(r + k) * F4 + q], m = d1s[(r - k) * F4 + q];
+      const float kf = (float)k;
+      acc.x = fmaf(kf, p.x - m.x, acc.x);
+      acc.y = fmaf(kf, p.y - m.y, acc.y);
+      acc.z = fmaf(kf, p.z - m.z, acc.z);
+      acc.w = fmaf(kf, p.w - m.w, acc.w);
+    }
+    float4* o = yb + (long long)lr * 3 * F4;
+    o[q] = xs[r * F4 + q];
+    o[F4 + q] = d1s[r * F4 + q];
+    o[2 * F4 + q] = make_float4(acc.x / denom, acc.y / denom, acc.z / denom, acc.w / denom);
+  }
+}
+
 // ContextWindow: y[b, t, c*L + k] = x[b, t + k - left, c] (zero outside).
 __global__ void context_kernel(const float* __restrict__ x, float* __restrict__ y, int N, int T, int F,
                                int left, int L) {
@@ -1110,6 +1196,26 @@ SBK_API int sbk_dct(const float* x, const float* D, float* y, long long rows, in
   return 0;
 }
 
+// y = [max(x, max_b - top_db) | d1 | d2] (N,T,3F): the concat deltas of an
+// fbank whose top_db floor was deferred (slot_max: (N, nslot) maxima from
+// sbk_spectrum).  F % 4 == 0, 16-B aligned x / y.
+SBK_API int sbk_deltas_floor(const float* x, float* y, int N, int T, int F, int window_length, const float* slot_max,
+                             int nslot, float top_db, void* stream) {
+  if (N <= 0 || T <= 0 || F <= 0 || F % 4 || window_length < 3 || !slot_max || nslot <= 0) return SBK_ERR_ARG;
+  if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) return SBK_ERR_ARG;
+  const int n = (window_length - 1) / 2;
+  const float denom = (float)(n * (n + 1) * (2 * n + 1)) / 3.0f;
+  int ttile = 64;
+  auto lds = [&](int tt) { return (size_t)(tt + 4 * n) * F * 4 * 2; };
+  while (ttile > 4 && lds(ttile) > 64 * 1024) ttile >>= 1;
+  if (lds(ttile) > 160 * 1024) return SBK_ERR_ARG;
+  const int nblk = N * ((T + ttile - 1) / ttile);
+  hipLaunchKernelGGL(deltas4_concat_kernel, dim3(nblk), dim3(256), lds(ttile), (hipStream_t)stream, x, y, N, T, F, n,
+                     denom, ttile, slot_max, nslot, top_db);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
 // concat=0: y = deltas(x) (N,T,F); concat=1: y = [x | d1 | d2] (N,T,3F)
 SBK_API int sbk_deltas(const float* x, float* y, int N, int T, int F, int window_length, int concat, void* stream) {
   if (N <= 0 || T <= 0 || F <= 0 || window_length < 3) return SBK_ERR_ARG;
@@ -1121,7 +1227,10 @@ SBK_API int sbk_deltas(const float* x, float* y, int N, int T, int F, int window
   while (ttile > 4 && lds(ttile) > 64 * 1024) ttile >>= 1;
   if (lds(ttile) > 160 * 1024) return SBK_ERR_ARG;
   const int nblk = N * ((T + ttile - 1) / ttile);
-  if (concat)
+  if (concat && F % 4 == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0)
+    hipLaunchKernelGGL(deltas4_concat_kernel, dim3(nblk), dim3(256), lds(ttile), (hipStream_t)stream, x, y, N, T, F,
+                       n, denom, ttile, nullptr, 0, 0.f);
+  else if (concat)
     hipLaunchKernelGGL(deltas_kernel<true>, dim3(nblk), dim3(256), lds(ttile), (hipStream_t)stream, x, y, N, T, F,
                        n, denom, ttile);
   else

@@ -42,6 +42,22 @@ def _(x, N, T, F, c, w, fm, tm, use_mean, n_fcells, warp_mode=0):
     return None
 
 
+def _masked_cells(fm, F):
+    """Number of (sequence, frequency) cells covered by a frequency mask —
+    pos <= f < pos + len, the kernels' test — from the host draws (N, n, 2)
+    [len, pos], by interval union (the second running mean's cell count)."""
+    total = 0
+    for row in fm.tolist():
+        iv = sorted((max(ps, 0), min(ps + ln, F)) for ln, ps in row)
+        end = 0
+        for a, b in iv:
+            a = max(a, end)
+            if b > a:
+                total += b - a
+                end = b
+    return total
+
+
 class SpecAugment(torch.nn.Module):
     def __init__(self, time_warp=True, time_warp_window=5, time_warp_mode="bicubic", freq_mask=True,
                  freq_mask_width=(0, 20), n_freq_mask=2, time_mask=True, time_mask_width=(0, 100), n_time_mask=2,
@@ -104,15 +120,16 @@ class SpecAugment(torch.nn.Module):
         if c == w:
             c = w = -1  # identical segment sizes: the resize is the identity
         self.last_draws = (c, w, fm, tm)
-        dev = x.device
-        fm_d = fm.to(dev, non_blocking=True) if fm is not None else None
-        tm_d = tm.to(dev, non_blocking=True) if tm is not None else None
-        n_fcells = 0
-        if fm is not None:
-            # number of masked (sequence, freq) cells x T, for the second running mean
-            ar = torch.arange(F).view(1, 1, -1)
-            cov = ((fm[..., 1:2] <= ar) & (ar < fm[..., 1:2] + fm[..., 0:1])).any(1)
-            n_fcells = int(cov.sum()) * T
+        # both mask tables in one host -> device copy (the per-step host work
+        # is this module's cost at config 2, not its kernels)
+        parts = [m.reshape(-1) for m in (fm, tm) if m is not None]
+        fm_d = tm_d = None
+        if parts:
+            buf = (torch.cat(parts) if len(parts) > 1 else parts[0]).to(x.device, non_blocking=True)
+            nf = fm.numel() if fm is not None else 0
+            fm_d = buf[:nf] if fm is not None else None
+            tm_d = buf[nf:] if tm is not None else None
+        n_fcells = _masked_cells(fm, F) * T if fm is not None else 0
         torch.ops.sbk.specaugment_(x, N, T, F, c, w, fm_d, tm_d, not self.replace_with_zero, n_fcells,
                                    _WARP_MODES.get(self.time_warp_mode, 0))
         return x

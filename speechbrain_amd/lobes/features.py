@@ -2,7 +2,8 @@
 
 Fbank on a mono (B,S) waveform with frozen filters is ONE fused kernel
 (frame → window → FFT → |X|² → mel → dB, plus per-utterance max) followed by
-the top_db clamp; with deltas the [x | Δ | ΔΔ] concat is one stencil kernel.
+the top_db clamp; with deltas the [x | Δ | ΔΔ] concat is one stencil kernel
+that also applies the top_db floor as it loads (no clamp pass).
 Module structure and state_dict keys match speechbrain/lobes/features.py:22-281.
 """
 import torch
@@ -59,18 +60,29 @@ class Fbank(torch.nn.Module):
         fb = self.compute_fbanks
         if (_can_fuse(self.compute_STFT, fb, wav) and fb.log_mel and fb.top_db is not None and not self.deltas
                 and not self.context):
-            st = self.compute_STFT
-            w, tw1, tw2 = st._tables(wav.device)
-            s0, ln, of, mw = fb.csr_tables(wav.device)
-            _, mult, off, amin, top_db = fb._db_args()
-            feats, slot_max = ops.fbank_deferred(wav, w, tw1, tw2, s0, ln, of, mw, st.n_fft, st.hop_length, st.center,
-                                                 ops.PAD_MODES[st.pad_mode], fb.n_mels, mult, off, amin)
-            return feats, (slot_max, float(top_db))
+            return self._deferred(wav)
         return self.forward(wav), None
+
+    def _deferred(self, wav):
+        st, fb = self.compute_STFT, self.compute_fbanks
+        w, tw1, tw2 = st._tables(wav.device)
+        s0, ln, of, mw = fb.csr_tables(wav.device)
+        _, mult, off, amin, top_db = fb._db_args()
+        feats, slot_max = ops.fbank_deferred(wav, w, tw1, tw2, s0, ln, of, mw, st.n_fft, st.hop_length, st.center,
+                                             ops.PAD_MODES[st.pad_mode], fb.n_mels, mult, off, amin)
+        return feats, (slot_max, float(top_db))
 
     def forward(self, wav):
         """Returns the FBANK features of a batch of waveforms."""
-        if _can_fuse(self.compute_STFT, self.compute_fbanks, wav):
+        fb = self.compute_fbanks
+        if (self.deltas and _can_fuse(self.compute_STFT, fb, wav) and fb.log_mel and fb.top_db is not None
+                and fb.n_mels % 4 == 0):
+            # the top_db floor applied by the concat deltas kernel as it loads
+            # the rows (one pass over the features fewer)
+            feats, (slot_max, top_db) = self._deferred(wav)
+            fbanks = ops.deltas_floor(feats, 2 * self.compute_deltas.n + 1, slot_max, top_db)
+            return self.context_window(fbanks) if self.context else fbanks
+        if _can_fuse(self.compute_STFT, fb, wav):
             fbanks = _fused_fbank(self.compute_STFT, self.compute_fbanks, wav)
         else:
             fbanks = self.compute_fbanks(spectral_magnitude(self.compute_STFT(wav)))

@@ -285,6 +285,25 @@ def _(x, window_length, concat):
     return x.new_empty(x.shape[0], x.shape[1], 3 * x.shape[2] if concat else x.shape[2])
 
 
+@torch.library.custom_op("sbk::deltas_floor", mutates_args=())
+def deltas_floor(x: torch.Tensor, window_length: int, slot_max: torch.Tensor, top_db: float) -> torch.Tensor:
+    """[max(x, max_b - top_db) | Δ | ΔΔ] of fbank_deferred's output: the
+    top_db floor (features.py:706-711) applied as the concat deltas kernel
+    loads its rows (lobes/features.py:141-144), no clamp pass."""
+    require_device(x, slot_max)
+    x = _c(x.to(_f32))
+    N, T, Fd = x.shape
+    out = torch.empty(N, T, 3 * Fd, device=x.device, dtype=_f32)
+    check(_lib.lib().sbk_deltas_floor(ptr(x), ptr(out), N, T, Fd, window_length, ptr(slot_max), slot_max.shape[1],
+                                      float(top_db), stream_of(x)), "sbk_deltas_floor")
+    return out
+
+
+@deltas_floor.register_fake
+def _(x, window_length, slot_max, top_db):
+    return x.new_empty(x.shape[0], x.shape[1], 3 * x.shape[2])
+
+
 @torch.library.custom_op("sbk::context_window", mutates_args=())
 def context_window(x: torch.Tensor, left: int, right: int) -> torch.Tensor:
     """ContextWindow on (N,T,F) → (N,T,F·(l+r+1)) (features.py:917-937)."""

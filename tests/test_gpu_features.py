@@ -268,3 +268,24 @@ def test_fbank_deferred_topdb_into_frontend2(dev):
         a = cnn.run(ref, torch.bfloat16)
         b = cnn.run(raw, torch.bfloat16, topdb=topdb)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n_mels", [80, 42])
+def test_fbank_deltas_floor_on_load(dev, n_mels):
+    """Fbank(deltas=True): the concat deltas kernel applies the deferred
+    top_db floor as it loads (sbk_deltas_floor) — bit-identical to the
+    clamped fbank followed by the concat deltas; n_mels % 4 != 0 keeps the
+    clamp pass (scalar kernel).  The floor binds in every utterance."""
+    from speechbrain_amd import ops
+    from speechbrain_amd.lobes.features import Fbank
+    g = torch.Generator().manual_seed(9)
+    wav = 0.1 * torch.randn(3, 48000, generator=g)
+    wav[:, 16000:20000] *= 1e-6
+    wav = wav.to(dev)
+    plain = Fbank(n_mels=n_mels).to(dev)(wav)
+    ref = ops.deltas(plain, 5, True)
+    out = Fbank(n_mels=n_mels, deltas=True).to(dev)(wav)
+    assert out.shape == (3, plain.shape[1], 3 * n_mels)
+    assert torch.equal(out, ref)
+    raw, _ = Fbank(n_mels=n_mels).to(dev).forward_deferred(wav)
+    assert (raw < plain).any(), "the floor must bind somewhere for this test to mean anything"

@@ -196,15 +196,21 @@ def _c5_oracle(wav, lens, ext, wrap, layers, mm=None, act=None):
         OW.set_rounding(None, None)
 
 
+_C5_REF = {}
+
+
 @pytest.mark.parametrize("prec", ["mxfp8", "bf16"])
 def test_config5_full_size_vs_oracle(dev, prec):
-    """Two 15 s utterances (one ragged) through W2VLatentExtractor (512 ch)
-    and a 4-layer d=1024 / 16-head / ffn 4096 GELU pre-norm encoder.  The
-    tolerance is the deviation of an oracle run whose GEMM operands carry the
-    same rounding (MXFP8 blocks for the MXFP8 path, bf16 activations between
-    kernels) from the fp32 oracle, times 1.5; observed values are printed."""
+    """BASELINE config 5 at full size: two 15 s utterances (one ragged)
+    through W2VLatentExtractor (512 ch) and the 24-layer d=1024 / 16-head /
+    ffn 4096 GELU pre-norm encoder.  The tolerance is the deviation of an
+    oracle run whose GEMM operands carry the same rounding (MXFP8 blocks for
+    the MXFP8 path, bf16 activations between kernels) from the fp32 oracle:
+    the mean error within 1.02x of it and the max within 1.25x (the kernels'
+    fp32 summation order differs from the oracle's, so the two roundings of
+    one product land on different elements); the ratios are printed."""
     import speechbrain_amd as sba
-    layers = 4
+    layers = 24
     ext, wrap = _c5_model(dev, layers)
     g = torch.Generator().manual_seed(5)
     wav = 0.1 * torch.randn(2, 240000, generator=g)
@@ -220,14 +226,17 @@ def test_config5_full_size_vs_oracle(dev, prec):
                 y = wrap.embed(lat, 2, T, lens.to(dev))
     y = y.view(2, T, 1024).cpu()
     assert T == 748
-    ref = _c5_oracle(wav, lens, ext, wrap, layers)
+    if "ref" not in _C5_REF:
+        _C5_REF["ref"] = _c5_oracle(wav, lens, ext, wrap, layers)
+    ref = _C5_REF["ref"]
     if prec == "mxfp8":
         emu = _c5_oracle(wav, lens, ext, wrap, layers, mm=OW.mx_round, act=OW.bf16_round)
     else:
         emu = _c5_oracle(wav, lens, ext, wrap, layers, mm=OW.bf16_round, act=OW.bf16_round)
     e_gpu, e_emu = (y - ref).abs(), (emu - ref).abs()
-    print(f"\nconfig5 {prec}: GPU vs fp32 oracle max {e_gpu.max():.4e} mean {e_gpu.mean():.4e}; "
-          f"rounded-operand oracle max {e_emu.max():.4e} mean {e_emu.mean():.4e}")
+    rmean, rmax = float(e_gpu.mean()) / float(e_emu.mean()), float(e_gpu.max()) / float(e_emu.max())
+    print(f"\nconfig5 {prec} ({layers} layers): GPU vs fp32 oracle max {e_gpu.max():.4e} mean {e_gpu.mean():.4e}; "
+          f"rounded-operand oracle max {e_emu.max():.4e} mean {e_emu.mean():.4e}; ratios mean {rmean:.3f} max {rmax:.3f}")
     assert torch.isfinite(y).all()
-    assert float(e_gpu.mean()) <= 1.5 * float(e_emu.mean())
-    assert float(e_gpu.max()) <= 1.5 * float(e_emu.max())
+    assert rmean <= 1.02  # measured 1.0005 (both precisions)
+    assert rmax <= 1.25  # measured 1.028 (mxfp8), 1.046 (bf16)
