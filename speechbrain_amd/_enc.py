@@ -627,9 +627,12 @@ def cast_bf16(x):
 
 
 def to_compute(x, dtype):
-    """Row-contiguous copy of x in the compute dtype (bf16 via the cast kernel)."""
+    """Row-contiguous copy of x in the compute dtype (bf16 via the cast kernel;
+    fp16 / bf16 activations of library ops under fp16 autocast -> fp32)."""
     if dtype == _bf16:
         return x.contiguous() if x.dtype == _bf16 else cast_bf16(x.float().contiguous())
+    if x.dtype in (torch.float16, _bf16):
+        return x.float().contiguous()
     if x.dtype != _f32:
         raise TypeError(f"fp32 compute path got {x.dtype}")
     return x.contiguous()
@@ -637,16 +640,17 @@ def to_compute(x, dtype):
 
 def compute_dtype():
     """bf16 MFMA under torch.autocast(device_type='cuda', dtype=bf16),
-    exact-f32 MFMA otherwise.  fp16 autocast (the reference's
-    `--auto_mix_prec`, core.py:905-919) has no kernels here and raises rather
-    than silently computing in bf16."""
+    exact-f32 MFMA otherwise — including fp16 autocast (the reference's
+    `--auto_mix_prec`, core.py:905-919): there are no fp16 kernels, and the
+    fp32 ones are at least as precise as the fp16 GEMMs the request stands
+    for (computing bf16 instead would lose precision without telling the
+    caller).  Library ops around these modules still run in fp16."""
     if torch.is_autocast_enabled("cuda"):
         dt = torch.get_autocast_dtype("cuda")
-        if dt != _bf16:
-            raise NotImplementedError(
-                f"speechbrain_amd kernels compute in bf16 or fp32; torch.autocast(dtype={dt}) is not supported. "
-                "Use torch.autocast('cuda', dtype=torch.bfloat16) (Brain: auto_mix_prec='bf16') or no autocast.")
-        return _bf16
+        if dt == _bf16:
+            return _bf16
+        if dt != torch.float16:
+            raise NotImplementedError(f"speechbrain_amd kernels compute in bf16 or fp32; torch.autocast(dtype={dt})")
     return _f32
 
 

@@ -15,8 +15,9 @@ unchanged).  MI355X choices:
   * mixed precision is bf16 autocast (same exponent range as fp32, so no
     GradScaler).  The reference's `--auto_mix_prec` (True) means fp16
     autocast + GradScaler; here True selects bf16 and says so in the log,
-    and "fp16" raises — the kernels have no fp16 path, and computing bf16
-    under an fp16 request would change numerics without telling the caller;
+    and "fp16" is the reference's step exactly (fp16 autocast, GradScaler
+    scale / unscale_ / step / update) with these modules computing in fp32
+    (no fp16 kernels; _enc.compute_dtype) and library ops in fp16;
   * everything the modules compute runs on libsbk.so HIP kernels.
 """
 import contextlib
@@ -40,7 +41,7 @@ class Brain:
 
     modules: dict of nn.Modules; opt_class: callable(params) -> optimizer;
     run_opts: device, distributed_launch, distributed_backend,
-    auto_mix_prec (False | True/"bf16"; "fp16" raises), max_grad_norm (5.0),
+    auto_mix_prec (False | True/"bf16" | "fp16" + GradScaler), max_grad_norm (5.0),
     grad_accumulation_factor (1), nonfinite_patience (3),
     find_unused_parameters (False), bucket_cap_mb (64).
     """
@@ -51,12 +52,15 @@ class Brain:
         self.distributed_launch = bool(run_opts.get("distributed_launch", False))
         self.distributed_backend = run_opts.get("distributed_backend", "nccl")
         amp = run_opts.get("auto_mix_prec", False)
-        if amp in ("fp16", torch.float16):
-            raise NotImplementedError("auto_mix_prec='fp16': the speechbrain_amd kernels compute in bf16 or fp32; "
-                                      "use auto_mix_prec='bf16' (no GradScaler needed) or False")
         if amp is True:
-            logger.warning("auto_mix_prec=True runs bf16 autocast on MI355X (the reference uses fp16 + GradScaler)")
-        self.amp_dtype = {False: None, None: None, True: torch.bfloat16, "bf16": torch.bfloat16}[amp]
+            logger.warning("auto_mix_prec=True runs bf16 autocast on MI355X (the reference uses fp16 + GradScaler; "
+                           "auto_mix_prec='fp16' runs that)")
+        if amp == torch.float16:
+            amp = "fp16"
+        self.amp_dtype = {False: None, None: None, True: torch.bfloat16, "bf16": torch.bfloat16,
+                          "fp16": torch.float16}[amp]
+        # core.py:558 (GradScaler for the fp16 step)
+        self.scaler = torch.amp.GradScaler("cuda") if self.amp_dtype == torch.float16 else None
         self.max_grad_norm = float(run_opts.get("max_grad_norm", 5.0))
         self.grad_accumulation_factor = int(run_opts.get("grad_accumulation_factor", 1))
         self.nonfinite_patience = int(run_opts.get("nonfinite_patience", 3))
@@ -133,13 +137,24 @@ class Brain:
         with self._autocast():
             outputs = self.compute_forward(batch, Stage.TRAIN)
             loss = self.compute_objectives(outputs, batch, Stage.TRAIN)
-        with self.no_sync(not should_step):
-            (loss / self.grad_accumulation_factor).backward()
-        if should_step:
-            if self.check_gradients(loss):
-                self.optimizer.step()
-            self.zero_grad()
-            self.optimizer_step += 1
+        if self.scaler is not None:  # core.py:906-919: the fp16 step
+            with self.no_sync(not should_step):
+                self.scaler.scale(loss / self.grad_accumulation_factor).backward()
+            if should_step:
+                self.scaler.unscale_(self.optimizer)
+                if self.check_gradients(loss):
+                    self.scaler.step(self.optimizer)
+                self.scaler.update()
+                self.zero_grad()
+                self.optimizer_step += 1
+        else:
+            with self.no_sync(not should_step):
+                (loss / self.grad_accumulation_factor).backward()
+            if should_step:
+                if self.check_gradients(loss):
+                    self.optimizer.step()
+                self.zero_grad()
+                self.optimizer_step += 1
         self.on_fit_batch_end(batch, outputs, loss, should_step)
         return loss.detach()
 

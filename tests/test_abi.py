@@ -104,18 +104,17 @@ def test_feature_module_attributes():
     assert ContextWindow(2, 3).context_len == 6
 
 
-def test_fp16_autocast_raises_not_bf16():
-    """fp16 autocast (the reference's --auto_mix_prec) has no kernels: the
-    modules raise instead of silently computing in bf16."""
-    import pytest
+def test_fp16_autocast_computes_fp32_not_bf16():
+    """fp16 autocast (the reference's --auto_mix_prec) has no fp16 kernels:
+    the modules compute in fp32 (at least as precise as the fp16 request),
+    never silently in bf16; bf16 autocast selects bf16."""
     import torch
     from speechbrain_amd import _enc
     prev = (torch.is_autocast_enabled("cuda"), torch.get_autocast_dtype("cuda"))
     try:
         torch.set_autocast_enabled("cuda", True)
         torch.set_autocast_dtype("cuda", torch.float16)
-        with pytest.raises(NotImplementedError):
-            _enc.compute_dtype()
+        assert _enc.compute_dtype() == torch.float32
         torch.set_autocast_dtype("cuda", torch.bfloat16)
         assert _enc.compute_dtype() == torch.bfloat16
     finally:
@@ -124,9 +123,9 @@ def test_fp16_autocast_raises_not_bf16():
     assert _enc.compute_dtype() == torch.float32
 
 
-def test_brain_rejects_fp16_amp():
-    import pytest
+def test_brain_fp16_amp_uses_grad_scaler():
+    import torch
     from speechbrain_amd.core import Brain
-    with pytest.raises(NotImplementedError):
-        Brain(modules={}, run_opts={"device": "cpu", "auto_mix_prec": "fp16"})
+    b = Brain(modules={}, run_opts={"device": "cpu", "auto_mix_prec": "fp16"})
+    assert b.amp_dtype == torch.float16 and b.scaler is not None
     assert Brain(modules={}, run_opts={"device": "cpu", "auto_mix_prec": True}).amp_dtype is not None

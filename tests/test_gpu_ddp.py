@@ -21,7 +21,9 @@ Checks (two optimizer steps, SGD lr 1e-4; gradients recorded at each step):
     GRU, whose bf16 solver is chosen per process); 1e-4 in fp32, whose
     weight-gradient GEMMs split K over fp32 atomics (a rerun of the same
     process differs by up to 2e-5).  Step 2 starts from parameters that
-    differ in the last fp32 bit: 2e-4 (measured 6.5e-5, the library GRU);
+    differ in the last fp32 bit: 2e-4 in bf16 (measured 6.5e-5, the library
+    GRU); 1e-3 in fp32, where the rel-pos bias / linear_pos gradients are
+    batch sums cancelling to ~1e-3 of their terms (measured 2.9e-4);
   * a single-process run on the concatenated batch: in bf16 a gradient that
     is reduced over the batch INSIDE the step and stored in bf16 — the shared
     positional projection p_k's (a bf16 activation under autocast, as in the
@@ -202,7 +204,7 @@ def test_brain_ddp_real_modules(dev, fused, accum):
     # GEMMs).  Step 2 starts from parameters that differ in the last fp32 bit,
     # which the bf16 casts (the library GRU's input projection most) turn into
     # an occasional flipped bf16 rounding: measured <= 6.5e-5.
-    compare(ga, pa, (1e-5 if fused else 1e-4, 2e-4), "single-process accumulation of the ranks' micro-batches")
+    compare(ga, pa, (1e-5, 2e-4) if fused else (1e-4, 1e-3), "single-process accumulation of the ranks' micro-batches")
     # the concatenated batch: the bf16 batch-reduced p_k gradient as above
     # (1e-2); fp32, the rel-pos bias and linear_pos gradients are batch sums
     # that cancel to ~1e-3 of their terms, so 2+2 vs 4-row ordering shows at
