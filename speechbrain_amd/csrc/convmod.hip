@@ -29,8 +29,22 @@
 //            dependent cross-lane reductions per wave)
 //   phase 3: Y = V W2^T (wave w: 16 output units x 48 frames) + b2, row mask,
 //            + x (fp32), float4 stores
-// Weight fragments are loaded straight from global (L2-resident: every
-// workgroup reads the same 384 KB) one K-step ahead of the MFMAs.
+// Phase -1's out_proj fragments are loaded straight from global (L2-resident)
+// into VGPRs up front; the phase-1 (256 KB) and phase-3 (128 KB) weights
+// stream L2 -> LDS by LDS-DMA through a 4-slot ring of 16-row x 32-k pieces
+// (one per wave and slice, each wave staging only the rows it multiplies)
+// in the buffers the phase does not use, three slices in flight.
+// Round 3 (s_memtime, profiles/r03_convmod_pre_timeline.log): 67k -> 55k
+// cycles per workgroup, 33.4 -> 28.5 us per launch.  Phase 1 went 17k ->
+// 11.5k (the register prefetch one K-step ahead waited on L2 latency every
+// step); phase 3 8-10k -> 3-5k (its bias / key-mask bytes now load ahead of
+// the ring instead of after it); the bf16-output sigmoids use the hardware
+// reciprocal (an IEEE divide per element before, and the GLU's branches).
+// What remains: phase -1 (all 251 workgroups pull 120 KB of o / x rows —
+// 1.67x the output rows for the conv halo — plus 128 KB of out_proj weights
+// at once: ~15k cycles to the last wave's data) and phase 1 at ~22 B/clk of
+// weights with every wave re-reading all 80 U rows from LDS (LDS bound:
+// 144 KB of LDS traffic per K-slice).
 #include "mfma.h"
 
 using namespace sbk;
@@ -85,6 +99,57 @@ __device__ __forceinline__ void lds_barrier() {
 
 __device__ __forceinline__ bf16x8 ld8g(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
+// Weight streams (phases 1 and 3) go L2 -> LDS by LDS-DMA pieces (64 lanes x
+// 16 B) issued from inline asm: the compiler sees no LDS write in flight (no
+// alias-guard waits on the LDS reads) and the ring waits are explicit
+// counted vmcnt.  A wave stages exactly the weight rows it multiplies, so a
+// slot needs no workgroup barrier.  A row of a K-slice is 32 bf16 = 64 B, its
+// four 16-B chunks XOR-swizzled by (row >> 2) & 3: the 16 lanes of a
+// fragment read (rows fr, chunk g) then cover all 64 banks.
+// (m0 is a reserved register: the clobber is advisory.  This kernel has no
+// other m0 user — every m0 write in its ISA is this one — so nothing the
+// compiler keeps in m0 can be overwritten.)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void cm_dma(const bf16_t* src, bf16_t* lds) {
+  const uint32_t la = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)((__attribute__((address_space(3))) bf16_t*)lds));
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(la) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+// 16 rows of a row-major (., CM_D) bf16 weight (src: the first row at k0), k0 ..
+// k0 + 31, into 16 slot rows of 64 B at dst (one piece)
+__device__ __forceinline__ void cm_dma16(const bf16_t* src, bf16_t* dst, int lane) {
+  const int r = lane >> 2, lc = (lane & 3) ^ ((r >> 2) & 3);
+  cm_dma(src + (long long)r * CM_D + 8 * lc, dst);
+}
+// fragment of slot row `row`, logical chunk g (8 consecutive k)
+__device__ __forceinline__ bf16x8 cm_frag(const bf16_t* slot, int row, int g) {
+  return *reinterpret_cast<const bf16x8*>(slot + row * 32 + 8 * (g ^ ((row >> 2) & 3)));
+}
+// s_waitcnt vmcnt(n), n = 0, 1, 2 known only at run time (wave-uniform)
+__device__ __forceinline__ void cm_vmwait(int n) {
+  if (n >= 2)
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if (n == 1)
+    asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+// global load the compiler cannot see (so its first use gets no vmcnt(0)
+// behind the DMA pieces issued after it); the caller waits (asm) and ties
+__device__ __forceinline__ f32x4 cm_gld4(const float* p) {
+  f32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ void cm_tie(f32x4& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ int cm_gldu8(const uint8_t* p) {
+  int v;
+  asm volatile("global_load_ubyte %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
 template <bool PRE>
 __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -104,16 +169,21 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
   // residual rows are issued up front: their latency overlaps phases 0-2
   constexpr int T1 = 2;                  // phase-1 tiles per wave: (value, gate) of GLU group w
   constexpr int T3 = CM_D / 16 / CM_NW;  // phase-3 output tiles per wave (1)
-  const bf16_t* wrow1 = a.w1 + (long long)(w * 32 + fr) * CM_D + fk;
-  const bf16_t* wrow3 = a.w2 + (long long)(w * 16 * T3 + fr) * CM_D + fk;
-  bf16x8 fw1[2][T1][2];  // [buffer][tile][ks]
-  auto load_fw1 = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int t = 0; t < T1; ++t)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) fw1[0][t][ks] = ld8g(wrow1 + t * 16 * CM_D + ks * 32);
+  // Weight rings.  A slot holds one 16-row x 32-k piece per wave (16 KB).
+  // Phase 1 streams 16 slices (8 K-slices x the value / gate tile) through
+  // four slots — two in Gs, two in the front of Cv, all free while the GLU
+  // GEMM runs — three slices in flight; phase 3 streams 8 K-slices through
+  // the same four (Gs is free after phase 2a, Cv after phase 2b).
+  constexpr int KSL = CM_D / 32, P1S = KSL * T1, SLOT = CM_NW * 16 * 32;
+  bf16_t* p1slot[4] = {Gs, Gs + SLOT, reinterpret_cast<bf16_t*>(Cv), reinterpret_cast<bf16_t*>(Cv) + SLOT};
+  bf16_t* const* p3slot = p1slot;  // Gs slots from phase 2b on, the Cv ones from phase 3 on
+  static_assert(2 * SLOT * 2 <= CM_ROWS * CM_S * 2 && 2 * SLOT * 2 <= CM_BM * CM_D * 4, "ring slots fit");
+  auto issue_p1 = [&](int q) __attribute__((always_inline)) {  // slice q: K-slice q / 2, tile q % 2
+    cm_dma16(a.w1 + (long long)(w * 32 + 16 * (q & 1)) * CM_D + 32 * (q >> 1), p1slot[q & 3] + w * 16 * 32, lane);
   };
-  if constexpr (!PRE) load_fw1();  // (PRE: once phase -1's own fragments are dead)
+  auto issue_p3 = [&](int ks) __attribute__((always_inline)) {
+    cm_dma16(a.w2 + (long long)(w * 16) * CM_D + 32 * ks, p3slot[ks & 3] + w * 16 * 32, lane);
+  };
 
   // PRE: x_att of this lane's phase-3 outputs (units w*16 + 4g .., frames
   // t0 + mt*16 + fr), moved across lanes from phase -1's staged-row layout
@@ -132,7 +202,12 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       ov[i] = *reinterpret_cast<const uint4*>(a.o + (ubase + fc) * CM_D + ch * 8);
     }
     // LN0 affine -> LDS (threads < 128, one float4 each; read after LN0's barrier)
-    float* gb0s = Cv + 2 * CM_ROWS * (CM_NW + 4) + 2 * CM_ROWS;  // [g0 | b0], past LN0's partials / statistics
+    // LN0's scratch (partials, statistics, affine) sits past the phase-1
+    // ring slot that Cv also holds, so that slot can fill during LN0
+    float* lnscr = Cv + CM_NW * 32 * 32 / 2;  // 32 KB in (bf16 slot -> float offset)
+    static_assert(CM_NW * 32 * 32 / 2 + 2 * CM_ROWS * (CM_NW + 4) + 2 * CM_ROWS + 2 * CM_D <= CM_BM * CM_D,
+                  "LN0 scratch fits beside the ring slot");
+    float* gb0s = lnscr + 2 * CM_ROWS * (CM_NW + 4) + 2 * CM_ROWS;  // [g0 | b0], past LN0's partials / statistics
     const float4 gbv = tid < CM_D / 2 ? *reinterpret_cast<const float4*>((tid < CM_D / 4 ? a.g0 : a.b0) +
                                                                          4 * (tid % (CM_D / 4)))
                                       : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -211,7 +286,7 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
     // four 16-B reads: with [wave][row] every wave issued 160 ds_read_b32
     // here, and the CU's LDS pipe spent ~11k cycles on them.
     constexpr int RS = CM_NW + 4;  // row stride (floats), 16-B aligned
-    float* red = Cv;               // [CM_ROWS][RS] sums, then [CM_ROWS][RS] squares
+    float* red = lnscr;            // [CM_ROWS][RS] sums, then [CM_ROWS][RS] squares
     float mean[CM_MT1], rstd[CM_MT1];
 #pragma unroll
     for (int mt = 0; mt < CM_MT1; ++mt) {
@@ -223,11 +298,13 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
         red[CM_ROWS * RS + (mt * 16 + fr) * RS + w] = pq;
       }
     }
-    // phase-1 weights issued here: their latency overlaps the statistics
-    // exchange (issued before x_att, the spill reloads of this phase waited
-    // for them: vmcnt is in order)
-    load_fw1();
     lds_barrier();
+    // every wave is past its phase -1 reads of Gs: the phase-1 weight ring's
+    // first three slices land (Gs, the free front of Cv) under the statistics
+    // exchange and the LN0 application
+    issue_p1(0);
+    issue_p1(1);
+    issue_p1(2);
     // final statistics once per row (lanes of waves 0-1: row = 64 w + lane),
     // not redundantly in all 16 waves: the LN0 phase is VALU-issue bound
     // (4 waves per SIMD), and the 16-way sums were a third of its VALU work
@@ -300,6 +377,11 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
     }
   }
   }
+  if constexpr (!PRE) {  // phase 0's loads are consumed: no wait for them lands behind these
+    issue_p1(0);
+    issue_p1(1);
+    issue_p1(2);
+  }
   lds_barrier();
   CM_TL(1);
 
@@ -310,33 +392,25 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
     for (int t = 0; t < T1; ++t)
 #pragma unroll
       for (int mt = 0; mt < CM_MT1; ++mt) acc[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const bf16_t* wrow = wrow1;
-    auto& fw = fw1;
+    bf16x8 fa[CM_MT1];  // U fragments of the K-slice, shared by its two tiles
 #pragma unroll
-    for (int kk = 0; kk < CM_D / 64; ++kk) {
-      const int cur = kk & 1;
-      if (kk + 1 < CM_D / 64) {
-#pragma unroll
-        for (int t = 0; t < T1; ++t)
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks) fw[cur ^ 1][t][ks] = ld8g(wrow + t * 16 * CM_D + (kk + 1) * 64 + ks * 32);
-      }
-      // keep the prefetch here: left alone the scheduler sank every fragment
-      // load onto its MFMAs (load -> vmcnt(0) -> MFMA, one L2 round trip each)
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 fa[CM_MT1];
+    for (int q = 0; q < P1S; ++q) {
+      const int ks = q >> 1, t = q & 1;
+      // this slice landed; the (up to two) slices issued after it stay in flight
+      cm_vmwait(P1S - 1 - q < 2 ? P1S - 1 - q : 2);
+      const bf16x8 fw = cm_frag(p1slot[q & 3], w * 16 + fr, g);
+      if (t == 0) {
 #pragma unroll
         for (int mt = 0; mt < CM_MT1; ++mt)
-          fa[mt] = *reinterpret_cast<const bf16x8*>(Us + (mt * 16 + fr) * CM_S + kk * 64 + ks * 32 + fk);
-#pragma unroll
-        for (int t = 0; t < T1; ++t)
-#pragma unroll
-          for (int mt = 0; mt < CM_MT1; ++mt)
-            acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[cur][t][ks], fa[mt], acc[t][mt], 0, 0, 0);
+          fa[mt] = *reinterpret_cast<const bf16x8*>(Us + (mt * 16 + fr) * CM_S + ks * 32 + fk);
       }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (q + 3 < P1S) issue_p1(q + 3);  // into the slot of slice q - 1, whose fragment is in VGPRs
+#pragma unroll
+      for (int mt = 0; mt < CM_MT1; ++mt)
+        acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw, fa[mt], acc[t][mt], 0, 0, 0);
     }
+    lds_barrier();  // every wave's ring reads are done before G overwrites Gs
     // GLU epilogue: lane holds frames mt*16 + fr, units 4g..4g+3 of each
     // tile; tiles (0, 1) = (value, gate) of channel group w
     {
@@ -353,7 +427,9 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float va = acc[0][mt][e] + bav[e], vg = acc[1][mt][e] + bgv[e];
-          o[e] = live ? va * (1.0f / (1.0f + __expf(-vg))) : 0.f;
+          // bf16 output: the approximate reciprocal (1 ulp) is far below its rounding
+          const float sg = va * __builtin_amdgcn_rcpf(1.0f + __expf(-vg));
+          o[e] = live ? sg : 0.f;
         }
         uint2 pk;
         pk.x = pack_bf16x2(o[0], o[1]);
@@ -365,11 +441,6 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
   lds_barrier();
   CM_TL(2);
 
-  bf16x8 fw3[2][T3][2];
-#pragma unroll
-  for (int t = 0; t < T3; ++t)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) fw3[0][t][ks] = ld8g(wrow3 + t * 16 * CM_D + ks * 32);
   float4 xr[T3][CM_MT3];
   static_assert(T3 == 1, "phase 3: one 16-unit tile per wave (the units of phase -1)");
 #pragma unroll
@@ -413,11 +484,29 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
   }
   lds_barrier();
   CM_TL(3);
+  f32x4 bb2 = f32x4{0.f, 0.f, 0.f, 0.f};
+  int km[CM_MT3] = {};
   {
-    // 2b: one wave per frame, 4 channels per lane
-    const float4 g14 = *reinterpret_cast<const float4*>(a.g1 + lane * 4);
-    const float4 b14 = *reinterpret_cast<const float4*>(a.b1n + lane * 4);
-    const float gm[4] = {g14.x, g14.y, g14.z, g14.w}, bt[4] = {b14.x, b14.y, b14.z, b14.w};
+    // 2b: one wave per frame, 4 channels per lane.  Gs is free: the phase-3
+    // weight ring's first two slices land under this phase (the LN1 affine
+    // is loaded first and waited for by count, ahead of them)
+    f32x4 g14 = cm_gld4(a.g1 + lane * 4), b14 = cm_gld4(a.b1n + lane * 4);
+    // and phase 3's epilogue operands (its bias and key-padding bytes), which
+    // after the ring would each cost a dependent global round trip
+    if (a.b2) bb2 = cm_gld4(a.b2 + w * 16 * T3 + 4 * g);
+    if (a.kpm) {
+#pragma unroll
+      for (int mt = 0; mt < CM_MT3; ++mt) km[mt] = cm_gldu8(a.kpm + ubase + min(t0 + mt * 16 + fr, a.T - 1));
+    }
+    issue_p3(0);
+    issue_p3(1);
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    cm_tie(g14);
+    cm_tie(b14);
+    cm_tie(bb2);
+#pragma unroll
+    for (int mt = 0; mt < CM_MT3; ++mt) asm volatile("" : "+v"(km[mt]));
+    const float gm[4] = {g14[0], g14[1], g14[2], g14[3]}, bt[4] = {b14[0], b14[1], b14[2], b14[3]};
     for (int fi = w; fi < CM_BM; fi += CM_NW) {
       const float4 v4 = *reinterpret_cast<const float4*>(Cv + fi * CM_D + lane * 4);
       float v[4] = {v4.x, v4.y, v4.z, v4.w};
@@ -429,7 +518,7 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float z = (v[e] - mean) * rstd * gm[e] + bt[e];
-        v[e] = z * (1.0f / (1.0f + __expf(-z)));
+        v[e] = z * __builtin_amdgcn_rcpf(1.0f + __expf(-z));  // bf16 output (as the GLU above)
       }
       uint2 pk;
       pk.x = pack_bf16x2(v[0], v[1]);
@@ -447,48 +536,36 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
     for (int t = 0; t < T3; ++t)
 #pragma unroll
       for (int mt = 0; mt < CM_MT3; ++mt) acc[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const bf16_t* wrow = wrow3;
-    auto& fw = fw3;
+    issue_p3(2);  // Cv is free: the LN1 statistics are read
 #pragma unroll
-    for (int kk = 0; kk < CM_D / 64; ++kk) {
-      const int cur = kk & 1;
-      if (kk + 1 < CM_D / 64) {
+    for (int ks = 0; ks < KSL; ++ks) {
+      cm_vmwait(KSL - 1 - ks < 2 ? KSL - 1 - ks : 2);  // this slice landed (up to two after it in flight)
+      const bf16x8 fw = cm_frag(p3slot[ks & 3], w * 16 + fr, g);
+      bf16x8 fa[CM_MT3];
 #pragma unroll
-        for (int t = 0; t < T3; ++t)
+      for (int mt = 0; mt < CM_MT3; ++mt)
+        fa[mt] = *reinterpret_cast<const bf16x8*>(Us + (mt * 16 + fr) * CM_S + ks * 32 + fk);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (ks + 3 < KSL) issue_p3(ks + 3);
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks) fw[cur ^ 1][t][ks] = ld8g(wrow + t * 16 * CM_D + (kk + 1) * 64 + ks * 32);
-      }
-      // keep the prefetch here: left alone the scheduler sank every fragment
-      // load onto its MFMAs (load -> vmcnt(0) -> MFMA, one L2 round trip each)
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 fa[CM_MT3];
-#pragma unroll
-        for (int mt = 0; mt < CM_MT3; ++mt)
-          fa[mt] = *reinterpret_cast<const bf16x8*>(Us + (mt * 16 + fr) * CM_S + kk * 64 + ks * 32 + fk);
-#pragma unroll
-        for (int t = 0; t < T3; ++t)
-#pragma unroll
-          for (int mt = 0; mt < CM_MT3; ++mt)
-            acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[cur][t][ks], fa[mt], acc[t][mt], 0, 0, 0);
-      }
+      for (int mt = 0; mt < CM_MT3; ++mt)
+        acc[0][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw, fa[mt], acc[0][mt], 0, 0, 0);
     }
 #pragma unroll
     for (int t = 0; t < T3; ++t) {
       const int d = w * 16 * T3 + t * 16 + 4 * g;
-      const float4 bb = a.b2 ? *reinterpret_cast<const float4*>(a.b2 + d) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const f32x4 bb = bb2;
 #pragma unroll
       for (int mt = 0; mt < CM_MT3; ++mt) {
         const int f = t0 + mt * 16 + fr;
         if (f >= a.T) continue;
-        const bool m = a.kpm && a.kpm[ubase + f];
+        const bool m = km[mt] != 0;
         const float4 xv = xr[t][mt];
         float4 o;
-        o.x = xv.x + (m ? 0.f : acc[t][mt][0] + bb.x);
-        o.y = xv.y + (m ? 0.f : acc[t][mt][1] + bb.y);
-        o.z = xv.z + (m ? 0.f : acc[t][mt][2] + bb.z);
-        o.w = xv.w + (m ? 0.f : acc[t][mt][3] + bb.w);
+        o.x = xv.x + (m ? 0.f : acc[t][mt][0] + bb[0]);
+        o.y = xv.y + (m ? 0.f : acc[t][mt][1] + bb[1]);
+        o.z = xv.z + (m ? 0.f : acc[t][mt][2] + bb[2]);
+        o.w = xv.w + (m ? 0.f : acc[t][mt][3] + bb[3]);
         *reinterpret_cast<float4*>(a.out + (ubase + f) * CM_D + d) = o;
       }
     }
