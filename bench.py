@@ -308,8 +308,27 @@ def launch_ranks(script, argv, n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, script, *argv], env=env))
-    codes = [p.wait() for p in procs]
-    return max(codes, key=abs)
+    # poll every rank: the first one that fails ends the others (its peers
+    # would otherwise block in a collective until the process-group timeout)
+    codes = {}
+    while len(codes) < n:
+        for r, p in enumerate(procs):
+            if r not in codes and p.poll() is not None:
+                codes[r] = p.returncode
+                if p.returncode != 0:
+                    for q in procs:
+                        if q.poll() is None:
+                            q.terminate()
+                    for q in procs:
+                        try:
+                            q.wait(timeout=30)
+                        except subprocess.TimeoutExpired:
+                            q.kill()
+                            q.wait()
+                    for r2, q in enumerate(procs):
+                        codes.setdefault(r2, q.returncode)
+        time.sleep(0.05)
+    return max(codes.values(), key=abs)
 
 
 def rank_env(gpus):
@@ -328,6 +347,8 @@ def launch_plumbing(args):
     (gloo), a fixed sleep per rank instead of the GPU step.  Used by the CPU
     test of the multi-rank contract."""
     world, rank, _ = rank_env(args.gpus)
+    if os.environ.get("SBK_PLUMBING_FAIL_RANK") == str(rank):
+        sys.exit(3)  # the launcher test's crashing rank: its peer must not wait for it
     if world > 1:
         dist.init_process_group("gloo")
         assert dist.get_world_size() == args.gpus

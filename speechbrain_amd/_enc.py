@@ -373,6 +373,10 @@ def ffn_chain(x, a, b, act, slope, next_ln, wp):
     returns (b's output fp32, next_ln(out) · wp^T bf16).  The Conformer's
     FFN2 + norm2 of layer i with FFN1 + norm1 + in_proj of layer i+1."""
     require_device(x, a[1], b[1], wp)
+    # one H and activation for both blocks (the kernel takes H from block a)
+    if b[1].shape != a[1].shape or b[3].shape != a[3].shape:
+        raise ValueError(f"ffn_chain: block shapes differ ({tuple(a[1].shape)}/{tuple(a[3].shape)} vs "
+                         f"{tuple(b[1].shape)}/{tuple(b[3].shape)})")
     gp, bp, ep = a[6] if a[6] is not None else (None, None, 0.0)
     return torch.ops.sbk.ffn_chain(x, ACT[act], float(slope), a[0][0], a[0][1], float(a[0][2]), a[1], a[2], a[3],
                                    a[4], float(a[5]), gp, bp, float(ep), b[0][0], b[0][1], float(b[0][2]), b[1], b[2],

@@ -349,7 +349,8 @@ class ConformerEncoder(nn.Module):
         u = None
         attns = []
         n = len(self.layers)
-        if USE_LAYER_CHAIN and am is None and all(layer.chainable(dtype, d) for layer in self.layers):
+        if (USE_LAYER_CHAIN and am is None and all(layer.chainable(dtype, d) for layer in self.layers)
+                and self._uniform_ffns()):
             return self._run_chain(x, B, T, pos, kpm_u8, dtype, need_attn, pk_all)
         for i, layer in enumerate(self.layers):
             nxt = self.layers[i + 1].ffn_module1[0] if i + 1 < n else None
@@ -364,6 +365,12 @@ class ConformerEncoder(nn.Module):
         fn = self.norm.norm
         y, _ = _enc.layernorm(x, fn.weight.detach(), fn.bias.detach(), fn.eps, out1_dtype=_f32)
         return y, attns
+
+    def _uniform_ffns(self):
+        """The chain kernel runs layer i's FFN2 with layer i+1's FFN1 under one
+        activation and hidden size: every layer's FFNs must agree."""
+        f = [m[1] for layer in self.layers for m in (layer.ffn_module1, layer.ffn_module2)]
+        return all(x.act_name() == f[0].act_name() and x.ffn[0].out_features == f[0].ffn[0].out_features for x in f)
 
     def _run_chain(self, x, B, T, pos, kpm_u8, dtype, need_attn, pk_all):
         """The fused stack as 3 launches per layer: [FFN2_i + norm2_i +

@@ -67,3 +67,20 @@ def test_bench_rejects_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--plumbing"],
                        capture_output=True, text=True, env=env, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_bench_launcher_stops_peers_of_a_failed_rank():
+    """A rank that dies (here: exit 3 before the rendezvous) makes the
+    launcher stop its peers — rank 0 would otherwise wait in the gloo
+    rendezvous until its timeout — and return the failing exit code."""
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["SBK_PLUMBING_FAIL_RANK"] = "1"
+    t0 = time.perf_counter()
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--plumbing"],
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode != 0
+    assert time.perf_counter() - t0 < 90
