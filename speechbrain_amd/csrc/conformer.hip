@@ -13,6 +13,7 @@
 #include "mfma.h"
 
 #include <algorithm>
+#include <utility>
 
 using namespace sbk;
 
@@ -462,6 +463,19 @@ SBK_PROBE_BUFFER(g_fe_tl, 10, 16)
 // (8 waves x 7 rows with the block-1 LN affine held in VGPRs: 133 us.)
 constexpr int FE_NT = 640, FE_TT2 = 8;
 
+// f(std::integral_constant<int, I>) for I = 0 .. N-1: register arrays indexed
+// inside get compile-time indices.  (The staged weights / affine used to sit
+// in HIP uint4 / float4 struct arrays that were left in scratch: 96 B per
+// thread through HBM, 86 MB of writes per launch; now native vectors.)
+template <int... I, class F>
+__device__ __forceinline__ void static_for_impl(std::integer_sequence<int, I...>, F&& f) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(std::make_integer_sequence<int, N>{}, f);
+}
+
 // LeakyReLU on a packed pair: max(t, s t) for slopes <= 1 (2 packed-rate ops)
 template <bool LMAX>
 __device__ __forceinline__ float __attribute__((ext_vector_type(2)))
@@ -516,8 +530,12 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
   // rows reflect(2*t1 - 1 + kt)
   constexpr int XV = (NJ * 3 * 20 + NT - 1) / NT, WV = (32 * 9 * 64 / 8 + NT - 1) / NT;  // vectors per thread (Fin <= 80, C2 <= 32)
   const int fq4 = Fin / 4;        // Fin % 4 == 0, Fin <= 80 (host-checked)
+  // native vectors: the HIP float4 / uint4 structs (a union inside) held in
+  // a register array are not always split into registers
+  typedef float nf4 __attribute__((ext_vector_type(4)));
+  typedef uint32_t nu4 __attribute__((ext_vector_type(4)));
   float4 xin[XV];
-  uint4 wvin[WV];
+  nu4 wvin[WV];
   const int nwv = C2 * K / Tr::VEC;
 #pragma unroll
   for (int u = 0; u < XV; ++u) {
@@ -529,12 +547,12 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
   }
   constexpr int AV = (2 * 40 * 64 / 4 + NT - 1) / NT;  // block-1 affine float4s per thread (F1 <= 40)
   const int nav = F1 * C1 / 4;
-  float4 afin[AV];
-#pragma unroll
-  for (int u = 0; u < AV; ++u) {
-    const int i = min(tid + u * NT, 2 * nav - 1);
-    afin[u] = i < nav ? reinterpret_cast<const float4*>(g1)[i] : reinterpret_cast<const float4*>(be1)[i - nav];
-  }
+  nf4 afin[AV];
+  static_for<AV>([&](auto U) {
+    const int i = min(tid + U * NT, 2 * nav - 1);
+    const nf4* src = i < nav ? reinterpret_cast<const nf4*>(g1) + i : reinterpret_cast<const nf4*>(be1) + (i - nav);
+    afin[U] = *src;
+  });
   constexpr int W1V = (C1 * 9 + NT - 1) / NT;  // block-1 taps per thread
   float w1v[W1V];
 #pragma unroll
@@ -563,9 +581,9 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
     v.x = fmaxf(v.x, floor_db); v.y = fmaxf(v.y, floor_db); v.z = fmaxf(v.z, floor_db); v.w = fmaxf(v.w, floor_db);
     if (i < NJ * 3 * fq4) *reinterpret_cast<float4*>(xs + 4 * i) = v;
   }
-#pragma unroll
-  for (int u = 0; u < AV; ++u)
-    if (tid + u * NT < 2 * nav) reinterpret_cast<float4*>(g1s)[tid + u * NT] = afin[u];
+  static_for<AV>([&](auto U) {
+    if (tid + U * NT < 2 * nav) reinterpret_cast<nf4*>(g1s)[tid + U * NT] = afin[U];
+  });
 #pragma unroll
   for (int u = 0; u < W1V; ++u)
     if (tid + u * NT < C1 * 9) w1s[tid + u * NT] = w1v[u];
@@ -678,17 +696,15 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
   // block-2 weights (L2-resident: every workgroup reads the same 37 KB) into
   // region 0 once every wave is done with the block-1 affine (loading them
   // with the stage instead delays the stage's LDS stores more than it saves)
-#pragma unroll
-  for (int u = 0; u < WV; ++u) wvin[u] = reinterpret_cast<const uint4*>(wp2)[min(tid + u * NT, nwv - 1)];
+  static_for<WV>([&](auto U) { wvin[U] = reinterpret_cast<const nu4*>(wp2)[min(tid + U * NT, nwv - 1)]; });
   __syncthreads();
-#pragma unroll
-  for (int u = 0; u < WV; ++u) {
-    const int i = tid + u * NT;
+  static_for<WV>([&](auto U) {
+    const int i = tid + U * NT;
     if (i < nwv) {
       const int co = (i * Tr::VEC) / K, kk = i * Tr::VEC - co * K;
-      *reinterpret_cast<uint4*>(wl + co * KP + kk) = wvin[u];
+      *reinterpret_cast<nu4*>(wl + co * KP + kk) = wvin[U];
     }
-  }
+  });
   __syncthreads();
   FE_TL(11);
 

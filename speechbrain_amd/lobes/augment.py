@@ -127,8 +127,8 @@ class SpecAugment(torch.nn.Module):
         if parts:
             buf = (torch.cat(parts) if len(parts) > 1 else parts[0]).to(x.device, non_blocking=True)
             nf = fm.numel() if fm is not None else 0
-            fm_d = buf[:nf] if fm is not None else None
-            tm_d = buf[nf:] if tm is not None else None
+            fm_d = buf[:nf].view(fm.shape) if fm is not None else None
+            tm_d = buf[nf:].view(tm.shape) if tm is not None else None
         n_fcells = _masked_cells(fm, F) * T if fm is not None else 0
         torch.ops.sbk.specaugment_(x, N, T, F, c, w, fm_d, tm_d, not self.replace_with_zero, n_fcells,
                                    _WARP_MODES.get(self.time_warp_mode, 0))
