@@ -779,8 +779,17 @@ __device__ __forceinline__ void static_stage(float2* __restrict__ buf, const flo
   }
 }
 
+// s_memtime marks of wave 0 of every workgroup (probe builds only): start,
+// stage 0 done, FFT done, split done, mel done, end, hardware / XCC id
+SBK_PROBE_BUFFER(g_spec_tl, 8192, 8)
+#define SPEC_TL(i) SBK_PROBE(if (threadIdx.x == 0 && blockIdx.x < 8192) g_spec_tl[blockIdx.x][i] = __builtin_amdgcn_s_memtime();)
+
 template <int MODE, int NC, int FPB, int NT>
 __global__ void __launch_bounds__(NT) spec_static_kernel(SpecArgs a) {
+  SPEC_TL(0);
+  SBK_PROBE(if (threadIdx.x == 0 && blockIdx.x < 8192) g_spec_tl[blockIdx.x][6] =
+                (unsigned long long)__builtin_amdgcn_s_getreg(63492) |
+                ((unsigned long long)__builtin_amdgcn_s_getreg(30740) << 32) | ((unsigned long long)blockIdx.x << 40);)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ float red[NT / 64];
   constexpr int NCP = frame_stride(NC), NBINS = NC + 1;
@@ -907,8 +916,10 @@ __global__ void __launch_bounds__(NT) spec_static_kernel(SpecArgs a) {
     }
     __syncthreads();
   }
+  SPEC_TL(1);
   // ---- remaining stages in place
   static_stage<NC, FPB, NT, 1>(buf, tw);
+  SPEC_TL(2);
 
   // ---- real split: bins k and NC-k per task
   constexpr int NPAIR = NC / 2 + 1, TASKS = FPB * NPAIR, TPT = (TASKS + NT - 1) / NT;
@@ -957,6 +968,7 @@ __global__ void __launch_bounds__(NT) spec_static_kernel(SpecArgs a) {
       }
     }
   }
+  SPEC_TL(3);
   if constexpr (MODE == MODE_FBANK) {
     __syncthreads();
     float lmax = -INFINITY;
@@ -977,11 +989,13 @@ __global__ void __launch_bounds__(NT) spec_static_kernel(SpecArgs a) {
       }
       orow[f * a.M + j] = acc;
     }
+    SPEC_TL(4);
     if (a.log_mel) {
       const float m = block_max(lmax, red);
       if (tid == 0) a.slot_max[blockIdx.x] = m;
     }
   }
+  SPEC_TL(5);
 }
 
 template <int NC> struct StaticCfg;
@@ -1059,6 +1073,8 @@ inline int grid_for(long long n, int block) {
 }
 
 }  // namespace
+
+SBK_PROBE_EXPORT(sbk_probe_spec_tl, g_spec_tl)
 
 // ---------------------------------------------------------------------------
 // C ABI (declared in include/sbk.h)
