@@ -331,6 +331,13 @@ int sbk_relpos_attention_mask(int dtype_bf16, const void* qkv, const void* pk, i
                               const float* pbv, const unsigned char* kpm, const float* am, long long am_sb,
                               long long am_sh, int B, int T, int H, int dh, float scale, void* out, float* probs,
                               void* stream);
+/* Plain scaled dot-product attention over the same head-interleaved qkv
+ * (MultiheadAttention, attention.py:642-779: no positional term, no u / v
+ * biases): bf16, dh == 64, T <= 4096, 16-B aligned qkv / out; kpm (B, T)
+ * uint8 or null; no probabilities.  Equal to sbk_relpos_attention_ld with a
+ * zero band and zero biases; SBK_ERR_ARG outside that envelope. */
+int sbk_mha_attention(const void* qkv, const unsigned char* kpm, int B, int T, int H, int dh, float scale, void* out,
+                      void* stream);
 /* LDS bytes one attention workgroup needs (host-side capacity check). */
 long long sbk_relpos_attention_lds(int dtype_bf16, int T, int dh);
 

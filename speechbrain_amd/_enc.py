@@ -608,6 +608,31 @@ def relpos_attention(qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale, need_probs=Fals
     return out, (probs if need_probs else None)
 
 
+@torch.library.custom_op("sbk::mha_attention", mutates_args=())
+def _mha_attention_op(qkv: torch.Tensor, kpm: Optional[torch.Tensor], B: int, T: int, H: int, dh: int,
+                      scale: float) -> torch.Tensor:
+    out = torch.empty(B * T, H * dh, device=qkv.device, dtype=qkv.dtype)
+    check(lib().sbk_mha_attention(ptr(qkv), ptr(kpm), B, T, H, dh, float(scale), ptr(out), stream_of(qkv)),
+          "sbk_mha_attention")
+    return out
+
+
+@_mha_attention_op.register_fake
+def _(qkv, kpm, B, T, H, dh, scale):
+    return qkv.new_empty(B * T, H * dh)
+
+
+def mha_fast_ok(qkv, T, dh):
+    """The band-free kernel's envelope (sbk_mha_attention)."""
+    return qkv.dtype == _bf16 and dh == 64 and T <= 4096 and qkv.is_contiguous() and qkv.data_ptr() % 16 == 0
+
+
+def mha_attention(qkv, kpm, B, T, H, dh, scale):
+    """Plain attention core (no positional band): qkv (B*T, 3d) head-interleaved
+    bf16 -> out (B*T, d) bf16.  Inside mha_fast_ok's envelope only."""
+    return torch.ops.sbk.mha_attention(qkv, kpm, int(B), int(T), int(H), int(dh), float(scale))
+
+
 def glu_group():
     """Channels per GLU pairing group (weights row-permuted in [a | gate] groups)."""
     return int(lib().sbk_gemm_glu_group(1))

@@ -102,6 +102,7 @@ SIGNATURES = {
     "sbk_relpos_attention_lds": [_i, _i, _i],
     "sbk_relpos_attention_mask": [_i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _ll, _ll, _i, _i, _i, _i, _f, _vp, _vp, _vp],
     "sbk_relpos_attention_ld": [_i, _vp, _vp, _i, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _vp],
+    "sbk_mha_attention": [_vp, _vp, _i, _i, _i, _i, _f, _vp, _vp],
     # norm.hip
     "sbk_inorm_slices": [_i],
     "sbk_inorm_partials": [_vp, _vp, _i, _i, _i, _vp, _vp],

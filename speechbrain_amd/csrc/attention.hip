@@ -549,6 +549,11 @@ __device__ __forceinline__ bf16x8 vt_frag_swz(const bf16_t* V, int k0, int dbase
 }
 }  // namespace dmak
 
+// BAND = false: plain scaled dot-product attention (MultiheadAttention of the
+// TransformerEncoder, attention.py:642-779 over nn.MultiheadAttention): no
+// positional band, no u / v biases — no band DMA, no G tiles, no scatter,
+// 16 KB of LDS; otherwise the same chunk loop.
+template <bool BAND>
 __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* __restrict__ qkv,
                                                                   const bf16_t* __restrict__ pk, int ldp,
                                                                   const float* __restrict__ pbu,
@@ -558,9 +563,9 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
   using namespace dmak;
   constexpr int dh = 64;
   __shared__ __attribute__((aligned(16))) bf16_t Ks[KC * RB];
-  __shared__ __attribute__((aligned(16))) bf16_t Ps[PB * RB];
+  __shared__ __attribute__((aligned(16))) bf16_t Ps[BAND ? PB * RB : 8];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[KC * RB];
-  __shared__ __attribute__((aligned(16))) float Gs[4 * 16 * G2];
+  __shared__ __attribute__((aligned(16))) float Gs[BAND ? 4 * 16 * G2 : 4];
   __shared__ unsigned long long Mb[4];  // per-wave partial bitmaps of the chunks holding a padded key
 
   const int d_model = H * dh;
@@ -595,18 +600,20 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r0 = 32 * w + 8 * i, rr = r0 + lrow;
-    offp[i] = (uint32_t)(rr * ldp + ((lchk ^ swz_kp(rr)) << 3)) * 2u;
-    lap[i] = lds_addr(Ps + r0 * RB);
+    offp[i] = BAND ? (uint32_t)(rr * ldp + ((lchk ^ swz_kp(rr)) << 3)) * 2u : 0u;
+    lap[i] = BAND ? lds_addr(Ps + r0 * RB) : 0u;
   }
   auto dma_kp = [&](int j0) {
     const int rbase = Tn - QB - i0 + j0;  // band row 0
-    if (j0 + KC <= Tn && rbase >= 0 && rbase + PB <= 2 * Tn - 1) {  // no row clamped
+    if (j0 + KC <= Tn && (!BAND || (rbase >= 0 && rbase + PB <= 2 * Tn - 1))) {  // no row clamped
       const bf16_t* sk = qkv_b + (long long)j0 * row3 + dh;
-      const bf16_t* sp = pk_h + (long long)rbase * ldp;
 #pragma unroll
       for (int i = 0; i < 2; ++i) dma16s(sk, offk[i], lak[i]);
+      if constexpr (BAND) {
+        const bf16_t* sp = pk_h + (long long)rbase * ldp;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) dma16s(sp, offp[i], lap[i]);
+        for (int i = 0; i < 4; ++i) dma16s(sp, offp[i], lap[i]);
+      }
       return;
     }
 #pragma unroll
@@ -614,6 +621,7 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
       const int r0 = 16 * w + 8 * i, row = r0 + lrow;
       dma16(qkv_b + (long long)min(j0 + row, Tn - 1) * row3 + dh + ((lchk ^ swz_kp(row)) << 3), Ks + r0 * RB);
     }
+    if constexpr (BAND)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {  // band rows 32w .. 32w+31
       const int r0 = 32 * w + 8 * i, rr = r0 + lrow;
@@ -672,10 +680,11 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
     const uint32_t wv[4] = {q4.x, q4.y, q4.z, q4.w};
     // biases by unconditional vector loads (guarded scalar loads each became
     // a branch and a full wait)
-    const f32x4 bu0 = *reinterpret_cast<const f32x4*>(pbu + h * dh + d0);
-    const f32x4 bu1 = *reinterpret_cast<const f32x4*>(pbu + h * dh + d0 + 4);
-    const f32x4 bv0 = *reinterpret_cast<const f32x4*>(pbv + h * dh + d0);
-    const f32x4 bv1 = *reinterpret_cast<const f32x4*>(pbv + h * dh + d0 + 4);
+    const f32x4 z4 = f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 bu0 = BAND ? *reinterpret_cast<const f32x4*>(pbu + h * dh + d0) : z4;
+    const f32x4 bu1 = BAND ? *reinterpret_cast<const f32x4*>(pbu + h * dh + d0 + 4) : z4;
+    const f32x4 bv0 = BAND ? *reinterpret_cast<const f32x4*>(pbv + h * dh + d0) : z4;
+    const f32x4 bv1 = BAND ? *reinterpret_cast<const f32x4*>(pbv + h * dh + d0 + 4) : z4;
     float qu[8], qv[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -720,26 +729,29 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
         const int row = 16 * t + c16;
         fk[t] = *reinterpret_cast<const bf16x8*>(Ks + row * RB + (((4 * s + g) ^ swz_kp(row)) << 3));
       }
+      if constexpr (BAND)
 #pragma unroll
-      for (int t = 0; t < 5; ++t) {
-        const int row = pofs + 16 * t + c16;
-        fpb[t] = *reinterpret_cast<const bf16x8*>(Ps + row * RB + (((4 * s + g) ^ swz_kp(row)) << 3));
-      }
+        for (int t = 0; t < 5; ++t) {
+          const int row = pofs + 16 * t + c16;
+          fpb[t] = *reinterpret_cast<const bf16x8*>(Ps + row * RB + (((4 * s + g) ^ swz_kp(row)) << 3));
+        }
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc_s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fk[t], fqu[s], acc_s[t], 0, 0, 0);
+      if constexpr (BAND)
 #pragma unroll
-      for (int t = 0; t < 5; ++t) acc_g[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fpb[t], fqv[s], acc_g[t], 0, 0, 0);
+        for (int t = 0; t < 5; ++t) acc_g[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fpb[t], fqv[s], acc_g[t], 0, 0, 0);
     }
     // rel_shift on the write: row R = 16t + 4g + r -> position R - (15 - c16)
+    if constexpr (BAND)
 #pragma unroll
-    for (int t = 0; t < 5; ++t)
+      for (int t = 0; t < 5; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int p = 16 * t + 4 * g + r + c16 - 15;
-        if (t == 0) p = max(p, -1);
-        if (t == 4) p = min(p, KC);
-        gq[p] = acc_g[t][r];
-      }
+        for (int r = 0; r < 4; ++r) {
+          int p = 16 * t + 4 * g + r + c16 - 15;
+          if (t == 0) p = max(p, -1);
+          if (t == 4) p = min(p, KC);
+          gq[p] = acc_g[t][r];
+        }
     ATT_TL(2 + 5 * ch);
     dma_barrier();  // B
     ATT_TL(3 + 5 * ch);
@@ -747,7 +759,8 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
     // scores for this lane's query, keys jj = 16t + 4g + r (log2 domain)
     f32x4 gv[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) gv[t] = *reinterpret_cast<const f32x4*>(gq + 16 * t + 4 * g);
+    for (int t = 0; t < 4; ++t)
+      gv[t] = BAND ? *reinterpret_cast<const f32x4*>(gq + 16 * t + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
     const bool chunk_padded = ((ch < 32 ? mlo >> ch : mhi >> (ch - 32)) & 1u) != 0u;
     __builtin_amdgcn_sched_barrier(0);
     if (more) dma_kp(j0 + KC);
@@ -756,7 +769,7 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) p[t][r] = acc_s[t][r] + gv[t][r];
+      for (int r = 0; r < 4; ++r) p[t][r] = BAND ? acc_s[t][r] + gv[t][r] : acc_s[t][r];
     if (chunk_padded) {  // uniform branch, only in chunks holding a padded key
       const uint8_t* kb = kpm + (long long)b * Tn;
 #pragma unroll
@@ -830,9 +843,13 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
 int launch_dma(const void* qkv, const void* pk, int ldp, const float* pbu, const float* pbv, const uint8_t* kpm, int B,
                int Tn, int H, float scale, void* out, hipStream_t s) {
   const int grid = B * H * ((Tn + QB - 1) / QB);
-  hipLaunchKernelGGL(relpos_flash_dma_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<const bf16_t*>(qkv),
-                     reinterpret_cast<const bf16_t*>(pk), ldp, pbu, pbv, kpm, Tn, H, scale,
-                     reinterpret_cast<bf16_t*>(out));
+  if (pk)
+    hipLaunchKernelGGL(relpos_flash_dma_kernel<true>, dim3(grid), dim3(256), 0, s, reinterpret_cast<const bf16_t*>(qkv),
+                       reinterpret_cast<const bf16_t*>(pk), ldp, pbu, pbv, kpm, Tn, H, scale,
+                       reinterpret_cast<bf16_t*>(out));
+  else
+    hipLaunchKernelGGL(relpos_flash_dma_kernel<false>, dim3(grid), dim3(256), 0, s, reinterpret_cast<const bf16_t*>(qkv),
+                       nullptr, 0, nullptr, nullptr, kpm, Tn, H, scale, reinterpret_cast<bf16_t*>(out));
   SBK_CHECK_LAUNCH();
   return 0;
 }
@@ -868,7 +885,7 @@ int launch(const void* qkv, const void* pk, int ldp, const float* pbu, const flo
 SBK_API int sbk_relpos_attention_ld(int dtype_bf16, const void* qkv, const void* pk, int ldp, const float* pbu,
                                     const float* pbv, const uint8_t* kpm, int B, int Tn, int H, int dh, float scale,
                                     void* out, float* probs, void* stream) {
-  if (B <= 0 || Tn <= 0 || H <= 0 || dh <= 0 || dh > 128 || ldp < H * dh) return SBK_ERR_ARG;
+  if (B <= 0 || Tn <= 0 || H <= 0 || dh <= 0 || dh > 128 || ldp < H * dh || !pk) return SBK_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   // the encoder's inference path: bf16, dh = 64, no probabilities
   if (dtype_bf16 && dh == 64 && !probs && ldp % 8 == 0 && Tn <= 64 * 64 &&
@@ -879,6 +896,18 @@ SBK_API int sbk_relpos_attention_ld(int dtype_bf16, const void* qkv, const void*
                     : launch<bf16_t, 128>(qkv, pk, ldp, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s);
   return dh <= 64 ? launch<float, 64>(qkv, pk, ldp, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s)
                   : launch<float, 128>(qkv, pk, ldp, pbu, pbv, kpm, B, Tn, H, dh, scale, out, probs, s);
+}
+
+// Plain scaled dot-product attention over the same head-interleaved qkv
+// (no positional band, no biases): the band-free LDS-DMA kernel; bf16,
+// dh = 64, T <= 4096, 16-B aligned operands (else SBK_ERR_ARG: the caller
+// takes sbk_relpos_attention_ld with a zero band).
+SBK_API int sbk_mha_attention(const void* qkv, const uint8_t* kpm, int B, int Tn, int H, int dh, float scale, void* out,
+                              void* stream) {
+  if (B <= 0 || Tn <= 0 || H <= 0 || dh != 64 || Tn > 64 * 64 ||
+      ((reinterpret_cast<uintptr_t>(qkv) | reinterpret_cast<uintptr_t>(out)) % 16) != 0)
+    return SBK_ERR_ARG;
+  return launch_dma(qkv, nullptr, 0, nullptr, nullptr, kpm, B, Tn, H, scale, out, (hipStream_t)stream);
 }
 
 SBK_API int sbk_relpos_attention(int dtype_bf16, const void* qkv, const void* pk, const float* pbu, const float* pbv,

@@ -371,6 +371,9 @@ class MultiheadAttention(nn.Module):
         """qkv (B*T, 3E) per-head layout (bf16 or fp32) → (o (B*T, E), probs (B, H, T, T) or None)."""
         E, H = self.d_model, self.nhead
         dh = E // H
+        if not need_weights and _enc.mha_fast_ok(qkv, T, dh):
+            # band-free kernel: no zero positional band through the MFMAs
+            return _enc.mha_attention(qkv, kpm_u8, B, T, H, dh, 1.0 / math.sqrt(dh)), None
         band, zb = self.zero_band(T, qkv.device, qkv.dtype)
         return _enc.relpos_attention(qkv, band, zb, zb, kpm_u8, B, T, H, dh, 1.0 / math.sqrt(dh),
                                      need_probs=need_weights)

@@ -123,6 +123,37 @@ def _load(mod, sd):
     return mod
 
 
+@pytest.mark.parametrize("B,T,H,lens", [(2, 748, 16, [748, 601]), (3, 40, 4, [40, 33, 7]), (1, 130, 16, None)])
+def test_mha_band_free_kernel_equals_zero_band(dev, B, T, H, lens):
+    """sbk_mha_attention (the band-free LDS-DMA kernel of MultiheadAttention)
+    against sbk_relpos_attention_ld with a zero positional band and zero u / v
+    biases on the same qkv: the band term adds exact zeros, so the two must
+    agree bit for bit (ragged key padding, partial last chunk)."""
+    from speechbrain_amd import _enc
+    dh = 64
+    torch.manual_seed(T)
+    qkv = (torch.randn(B * T, 3 * H * dh, device=dev) * 0.5).to(torch.bfloat16)
+    kpm = None
+    if lens is not None:
+        kpm = (torch.arange(T)[None] >= torch.tensor(lens)[:, None]).to(torch.uint8).to(dev)
+    scale = 1.0 / math.sqrt(dh)
+    assert _enc.mha_fast_ok(qkv, T, dh)
+    o = _enc.mha_attention(qkv, kpm, B, T, H, dh, scale)
+    band = torch.zeros(2 * T - 1, H * dh, device=dev, dtype=torch.bfloat16)
+    zb = torch.zeros(dh, H, device=dev)
+    ref, _ = _enc.relpos_attention(qkv, band, zb, zb, kpm, B, T, H, dh, scale)
+    torch.cuda.synchronize()
+    assert torch.equal(o, ref)
+    # and against plain softmax attention in fp32 (bf16 output rounding)
+    q, k, v = qkv.float().view(B, T, H, 3, dh).unbind(3)
+    sc = torch.einsum("bihd,bjhd->bhij", q, k) * scale
+    if kpm is not None:
+        sc = sc.masked_fill(kpm.bool()[:, None, None, :], float("-inf"))
+    want = torch.einsum("bhij,bjhd->bihd", sc.softmax(-1), v).reshape(B * T, H * dh)
+    err = (o.float() - want).abs().max().item()
+    assert err <= 2e-2, err
+
+
 def test_latent_extractor_vs_golden(golden, dev):
     from speechbrain_amd.lobes.models.wav2vec import W2VLatentExtractor
     g = golden("wav2vec")
