@@ -502,6 +502,7 @@ __global__ void __launch_bounds__(256, 2) relpos_flash_kernel(const T* __restric
 // before an LDS access it cannot tell apart from a DMA in flight) has little
 // to wait for.  50 KB of LDS and <= 168 VGPRs: three workgroups per CU.
 namespace dmak {
+typedef float v2f __attribute__((ext_vector_type(2)));
 constexpr int RB = 64;   // bf16 per staged row (dh = 64): 128 B
 constexpr int PB = 128;  // band rows staged per chunk (127 used)
 constexpr int G2 = 72;   // G scratch row (floats): 18 16-B slots, ≡ 2 mod 4
@@ -766,10 +767,17 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
     if (more) dma_kp(j0 + KC);
     float p[4][4];
     float cmax = -INFINITY;
+    // S + G as packed fp32 pairs (v_pk_add_f32: half the instructions of the
+    // per-element adds; the chunk loop is VALU-issue bound)
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) p[t][r] = BAND ? acc_s[t][r] + gv[t][r] : acc_s[t][r];
+      for (int r = 0; r < 4; r += 2) {
+        const v2f sg = BAND ? v2f{acc_s[t][r], acc_s[t][r + 1]} + v2f{gv[t][r], gv[t][r + 1]}
+                            : v2f{acc_s[t][r], acc_s[t][r + 1]};
+        p[t][r] = sg[0];
+        p[t][r + 1] = sg[1];
+      }
     if (chunk_padded) {  // uniform branch, only in chunks holding a padded key
       const uint8_t* kb = kpm + (long long)b * Tn;
 #pragma unroll
@@ -793,15 +801,23 @@ __global__ void __launch_bounds__(256, 3) relpos_flash_dma_kernel(const bf16_t* 
     const float m_new = fmaxf(m_run, cmax);
     const float mref = m_new == -INFINITY ? 0.f : m_new;
     const float alpha = __builtin_amdgcn_exp2f(m_run - mref);
-    float ls = 0.f;
+    // p - m as packed pairs; the row sum as a tree of packed pairs (one
+    // serial chain of 16 dependent adds before)
+    v2f ls2[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 4; ++t) {
+      v2f e[2];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        p[t][r] = __builtin_amdgcn_exp2f(p[t][r] - mref);
-        ls += p[t][r];
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const v2f d = v2f{p[t][2 * h2], p[t][2 * h2 + 1]} - v2f{mref, mref};
+        e[h2] = v2f{__builtin_amdgcn_exp2f(d[0]), __builtin_amdgcn_exp2f(d[1])};
+        p[t][2 * h2] = e[h2][0];
+        p[t][2 * h2 + 1] = e[h2][1];
       }
-    l_run = l_run * alpha + col4_sum(ls);
+      ls2[t] = e[0] + e[1];
+    }
+    const v2f lsv = (ls2[0] + ls2[1]) + (ls2[2] + ls2[3]);
+    l_run = l_run * alpha + col4_sum(lsv[0] + lsv[1]);
     m_run = m_new;
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc_o[t] *= alpha;
