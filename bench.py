@@ -420,8 +420,8 @@ def run_c2(args, world, rank, dev):
     kern = []
     traffic = load_traffic()
     for name, fn, nbytes, pmc in (
-            ("spec_static_kernel (Fbank, top_db floor deferred)", lambda: fb._deferred(wav),
-             4.0 * B * S + 4.0 * B * T * 80, ("spec_static_kernel<2, 200, 8, 320>",)),
+            ("spec_reg_kernel (Fbank, register FFT, top_db floor deferred)", lambda: fb._deferred(wav),
+             4.0 * B * S + 4.0 * B * T * 80, ("spec_reg_kernel<2, false>",)),
             ("deltas4_concat_kernel (floor(x)|Δ|ΔΔ)", lambda: ops.deltas_floor(f80, 5, smax, topdb),
              4.0 * B * T * 80 + 4.0 * B * T * 240, ("deltas4_concat_kernel",)),
             ("specaugment (warp + masks + mean fill)", sa_kernels, 2 * 4.0 * B * T * 240,

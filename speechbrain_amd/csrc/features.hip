@@ -998,6 +998,400 @@ __global__ void __launch_bounds__(NT) spec_static_kernel(SpecArgs a) {
   SPEC_TL(5);
 }
 
+// ---------------------------------------------------------------------------
+// Register-FFT spectrum kernel, n_fft = 400 (nc = 200 = 8 x 25), mono, power
+// spectrum or fused Fbank.  Eight lanes own one frame and a wave eight
+// frames; the complex FFT is a 25 x 8 decomposition and a wave never waits
+// on another after the table stage (persistent workgroups, tables once):
+//   * the wave's 8 frames are one contiguous span of samples: LDS-DMA puts it
+//     in the wave's frame regions (6 x 16 B per lane); lane n1 (0..7) then
+//     reads z[8 n2 + n1], n2 = 0..24 (window from LDS) and runs a DFT-25
+//     (5 x 5, compile-time twiddles) in registers;
+//   * twiddle by W_200^(n1 k2), then a wave-private LDS transposition: lane
+//     n1 writes Y[k2][n1]; each lane reads back the eight Y[k2][.] of a
+//     unit {m, 25 - m} (m = 1..12, unit 0 = {0}) and runs two radix-8 DFTs,
+//     which gives Z[k2 + 25 k1] for both k2 of the unit, k1 = 0..7 (two
+//     passes of 13 / 12 rows, so a frame region is 848 B, not 1.6 KB);
+//   * the real split X[k] = E + W_400^k O pairs bin k with 200 - k, which
+//     lives in the same unit, so no second exchange: |X|^2 goes to the
+//     frame's LDS region (over its consumed Y), then the mel filters as dense
+//     16-B rows from each filter's aligned first bin (zero weights outside),
+//     dB, and one partial max per wave (= per 8 frames: the slot layout of
+//     the static kernel).
+// Fbank at config 3: 53.2 us (static kernel, ~18k cycles per 8 frames, half
+// of it behind its prologue loads, most of the rest at in-place stage
+// barriers) -> 42.8 us.  Measured on the way: the first version (strided
+// 8-B waveform loads, a 1.6 KB region per frame, 2 workgroups of 4 waves per
+// CU) 42.9 us; window / twiddles read from their global tables per use
+// 75 us (the vector-memory address rate); without the span staging 55.6 us;
+// non-persistent 52.4 us.  s_memtime per wave (scripts/rf_tl.py): the load
+// phase (all waves of a round fetching at once) and the mel phase dominate.
+// ---------------------------------------------------------------------------
+#ifndef SBK_RF_NW
+#define SBK_RF_NW 4
+#define SBK_RF_MINW 3
+#endif
+// 4 waves x 8 frames, three workgroups per CU (LDS), <= 168 VGPRs (no spills):
+// 42.8 us against 45.9 us for 8-wave workgroups at 128 VGPRs (spills) and
+// 44.3 us for one 8-wave workgroup per CU
+constexpr int RF_NW = SBK_RF_NW, RF_NT = RF_NW * 64;
+constexpr int RF_FS = 13 * 8 + 2;              // float2 per frame region (13 rows of Y[k2][8] / P[201]);
+                                               // 212 floats = 20 mod 64 banks: frames on distinct banks
+constexpr int RF_PAD = 24;                     // float2 of zeros after a wave's 8 regions
+constexpr int RF_WS = 8 * RF_FS + RF_PAD;      // float2 per wave
+constexpr int RF_SPAN = 1536;                  // staged samples per wave (6 KB: 8 frames at hop <= 162)
+static_assert(RF_SPAN <= 2 * RF_WS, "the span fits the wave's regions");
+constexpr int RF_LW = 36;                      // dense mel row: 16-B aligned start + up to 33 bins
+typedef float rf4 __attribute__((ext_vector_type(4)));
+#ifndef SBK_RF_WGS_PER_CU
+#define SBK_RF_WGS_PER_CU 3                    // persistent grid: workgroups per CU (LDS: three fit)
+#endif
+
+// compile-time W_25^m for the DFT-25 (Taylor series in double, |x| <= pi)
+__host__ __device__ constexpr double cx_sin(double x) {
+  double t = x, s = x;
+  for (int n = 1; n < 16; ++n) { t *= -x * x / ((2.0 * n) * (2.0 * n + 1.0)); s += t; }
+  return s;
+}
+__host__ __device__ constexpr double cx_cos(double x) {
+  double t = 1.0, s = 1.0;
+  for (int n = 1; n < 16; ++n) { t *= -x * x / ((2.0 * n - 1.0) * (2.0 * n)); s += t; }
+  return s;
+}
+struct Tw25 {
+  float re[25], im[25];
+};
+__host__ __device__ constexpr Tw25 make_tw25() {
+  Tw25 t{};
+  for (int m = 0; m < 25; ++m) {
+    double th = 2.0 * 3.14159265358979323846 * m / 25.0;
+    if (th > 3.14159265358979323846) th -= 2.0 * 3.14159265358979323846;
+    t.re[m] = (float)cx_cos(th);
+    t.im[m] = (float)-cx_sin(th);
+  }
+  return t;
+}
+__device__ constexpr Tw25 kTw25 = make_tw25();
+
+// DFT-25 in registers, natural order in and out: n = 5a + b, U_b = DFT5_a,
+// U_b[c] *= W_25^(bc), X[c + 5d] = DFT5_b U_b[c]
+__device__ __forceinline__ void dft25(float2 (&x)[25]) {
+  float2 u[5][5];
+#pragma unroll
+  for (int b = 0; b < 5; ++b) {
+#pragma unroll
+    for (int a = 0; a < 5; ++a) u[b][a] = x[5 * a + b];
+    dft_small<5>(u[b]);
+  }
+#pragma unroll
+  for (int b = 1; b < 5; ++b)
+#pragma unroll
+    for (int c = 1; c < 5; ++c) {
+      const int m = (b * c) % 25;
+      u[b][c] = cmul(u[b][c], make_float2(kTw25.re[m], kTw25.im[m]));
+    }
+#pragma unroll
+  for (int c = 0; c < 5; ++c) {
+    float2 t[5];
+#pragma unroll
+    for (int b = 0; b < 5; ++b) t[b] = u[b][c];
+    dft_small<5>(t);
+#pragma unroll
+    for (int d = 0; d < 5; ++d) x[c + 5 * d] = t[d];
+  }
+}
+
+// real-FFT split of bin k from Z[k] (za) and Z[nc - k] (zb), w = W_nfft^k
+__device__ __forceinline__ float2 rsplit(float2 za, float2 zb, float2 w) {
+  const float2 zc = make_float2(zb.x, -zb.y);
+  const float2 E = make_float2(0.5f * (za.x + zc.x), 0.5f * (za.y + zc.y));
+  const float2 O = mul_mi(make_float2(0.5f * (za.x - zc.x), 0.5f * (za.y - zc.y)));
+  return cadd(E, cmul(w, O));
+}
+
+template <int MODE, bool GP>
+__device__ __forceinline__ float rf_power(float2 x, const SpecArgs& a) {
+  x.x *= a.norm_scale;
+  x.y *= a.norm_scale;
+  float p = x.x * x.x + x.y * x.y;
+  if (GP && a.power != 1.0f) {
+    if (a.power < 1.0f) p += a.eps;
+    p = powf(p, a.power);
+  }
+  if (GP && MODE == MODE_POWER && a.log_mag) p = logf(p + a.eps);
+  return p;
+}
+
+// one unit's 16 bins (m + 25 k1 and 200 - m - 25 k1, k1 = 0..7) from the
+// radix-8 outputs A = Z[m + 25 .], B = Z[25 - m + 25 .]; unit 0 passes B =
+// A rotated by one (Z[200 - 25 k1] = A[(8 - k1) % 8])
+template <int MODE, bool GP>
+__device__ __forceinline__ void rf_unit(int m, const float2 (&A)[8], const float2 (&B)[8], const float2* t2,
+                                        const SpecArgs& a, float (&pw)[16]) {
+#pragma unroll
+  for (int k1 = 0; k1 < 8; ++k1) {
+    const float2 wk = t2[m + 25 * k1];
+    const float2 wr = make_float2(-wk.x, wk.y);  // W_400^(200-k) = -conj(W_400^k)
+    pw[2 * k1] = rf_power<MODE, GP>(rsplit(A[k1], B[7 - k1], wk), a);
+    pw[2 * k1 + 1] = rf_power<MODE, GP>(rsplit(B[7 - k1], A[k1], wr), a);
+  }
+}
+
+// s_memtime marks of lane 0 of every wave (probe builds only): entry, tables,
+// frames loaded, DFT-25 + twiddle, pass A, pass B, P written, end
+SBK_PROBE_BUFFER(g_rf_tl, 16384, 8)
+#define RF_TL(i) SBK_PROBE(if (lane == 0 && tl_row < 16384) g_rf_tl[tl_row][i] = __builtin_amdgcn_s_memtime();)
+
+// GP: a power other than 1 or a log magnitude (the Fbank path has neither)
+template <int MODE, bool GP>
+__global__ void __launch_bounds__(RF_NT, SBK_RF_MINW) spec_reg_kernel(SpecArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NC = 200;
+  float2* win = reinterpret_cast<float2*>(smem);  // (window[2n], window[2n+1]), n < 200
+  float2* t1 = win + NC;                           // W_200^(n1 k2): [8][25]
+  float2* t2 = t1 + NC;                            // W_400^k, k <= 200
+  float2* fr = t2 + NC + 2;                        // per wave: 8 frame regions + a zero pad
+  float* wd = reinterpret_cast<float*>(fr + RF_NW * RF_WS);   // mel weights, dense [M][RF_LW] from a 16-B aligned bin
+  int* mstart = reinterpret_cast<int*>(wd + (MODE == MODE_FBANK ? a.M * RF_LW : 0));  // that aligned bin
+  __shared__ int lmax_s;
+  const int tid = threadIdx.x, lane = tid & 63;
+  SBK_PROBE(int tl_row = blockIdx.x * RF_NW + (tid >> 6); unsigned long long tl0 = __builtin_amdgcn_s_memtime();)
+  // ---- tables, once per workgroup (the only workgroup barriers; tables read
+  // from global memory per use measured 75 against 47 us)
+  if (tid < NC) {
+    win[tid] = reinterpret_cast<const float2*>(a.window)[tid];
+    const int n1 = tid / 25, k2 = tid - n1 * 25;
+    t1[tid] = a.tw[n1 * k2];  // n1 k2 <= 168
+  }
+  for (int i = tid; i <= NC; i += RF_NT) t2[i] = a.tw2[i];
+  int lw = 0;  // dense mel width (multiple of 4, <= RF_LW); 0 = a filter is wider (CSR loop from global)
+  if constexpr (MODE == MODE_FBANK) {
+    if (tid == 0) lmax_s = 0;
+    __syncthreads();
+    for (int i = tid; i < a.M; i += RF_NT) atomicMax(&lmax_s, (a.mel_start[i] & 3) + a.mel_len[i]);
+    __syncthreads();
+    const int lm = lmax_s;
+    lw = lm <= RF_LW ? (lm + 3) & ~3 : 0;
+    if (lw) {
+      for (int i = tid; i < a.M * RF_LW; i += RF_NT) {
+        const int jm = i / RF_LW, c = i - jm * RF_LW, L = a.mel_len[jm];
+        const int sh = a.mel_start[jm] & 3;
+        wd[i] = c >= sh && c - sh < L ? a.mel_w[a.mel_off[jm] + c - sh] : 0.f;
+      }
+      for (int i = tid; i < a.M; i += RF_NT) mstart[i] = a.mel_start[i] & ~3;
+    }
+  }
+  __syncthreads();
+  SBK_PROBE(const unsigned long long tl1 = __builtin_amdgcn_s_memtime();)
+  const int w = tid >> 6;
+  const int nwb = (a.T + 7) >> 3;                   // 8-frame slots per utterance
+  const int nblk_t = (nwb + RF_NW - 1) / RF_NW;
+  // persistent: workgroup-sized blocks of 64 frames strided over the grid
+  // (the mel table is built once per workgroup)
+  for (int blk = blockIdx.x; blk < a.Bfold * nblk_t; blk += gridDim.x) {
+  const int bf = blk / nblk_t;
+  const int slot = (blk - bf * nblk_t) * RF_NW + w;
+  if (slot >= nwb) continue;
+  // the lane's frame / column from an opaque lane id, per block: hoisted out
+  // of the block loop, every lane-dependent LDS address would stay live
+  // through it (spills)
+  int ln;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+  const int q = ln >> 3, j = ln & 7;
+  const int t0 = slot * 8;
+  SBK_PROBE(tl_row = blk * RF_NW + w; if (lane == 0 && tl_row < 16384) { g_rf_tl[tl_row][0] = tl0; g_rf_tl[tl_row][1] = tl1; })
+  SBK_PROBE(tl0 = __builtin_amdgcn_s_memtime();)
+  const int tf = min(t0 + q, a.T - 1);              // frames past T recompute the last one
+  const float* wrow = a.wav + (long long)bf * a.S;
+
+  // ---- z[n2] = windowed (x[2n], x[2n+1]), n = 8 n2 + j
+  float2 z[25];
+  {
+    const int pad = a.center ? NC : 0;
+    const int s0 = tf * a.hop - pad + 2 * j;
+    const int span0 = t0 * a.hop - pad;  // first sample of the wave's 8 frames
+    if (span0 >= 0 && span0 + RF_SPAN <= a.S && 7 * a.hop + 2 * NC <= RF_SPAN && ((span0 | a.S | a.hop) & 3) == 0) {
+      // the wave's samples (one contiguous span) -> its frame regions by
+      // LDS-DMA: RF_SPAN / 256 16-B pieces per lane instead of 25 strided
+      // 8-B loads per lane (the vector-memory address rate, not HBM, set the
+      // load phase); the frames then read their z pairs from LDS
+      float* stage = reinterpret_cast<float*>(fr + w * RF_WS);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the last block's LDS reads are done
+#pragma unroll
+      for (int c = 0; c < RF_SPAN / 256; ++c)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(wrow + span0 + c * 256 + lane * 4),
+            (__attribute__((address_space(3))) void*)(stage + c * 256), 16, 0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const float2* src = reinterpret_cast<const float2*>(stage + (tf - t0) * a.hop + 2 * j);
+#pragma unroll
+      for (int n2 = 0; n2 < 25; ++n2) z[n2] = src[8 * n2];
+    } else {  // utterance ends (padding), other geometries
+#pragma unroll
+      for (int n2 = 0; n2 < 25; ++n2) {
+        bool ok0, ok1;
+        const int p0 = map_pos(s0 + 16 * n2, a.S, a.pad_mode, &ok0);
+        const int p1 = map_pos(s0 + 16 * n2 + 1, a.S, a.pad_mode, &ok1);
+        z[n2] = make_float2(ok0 ? wrow[p0] : 0.f, ok1 ? wrow[p1] : 0.f);
+      }
+    }
+#pragma unroll
+    for (int n2 = 0; n2 < 25; ++n2) {
+      const float2 wv = win[8 * n2 + j];
+      z[n2] = make_float2(z[n2].x * wv.x, z[n2].y * wv.y);
+    }
+  }
+  SBK_PROBE(asm volatile("s_waitcnt vmcnt(0)" ::: "memory");)
+  RF_TL(2);
+  dft25(z);
+#pragma unroll
+  for (int k2 = 1; k2 < 25; ++k2) z[k2] = cmul(z[k2], t1[j * 25 + k2]);
+  RF_TL(3);
+
+  // ---- transposition through the frame's LDS region in two passes of
+  // 13 / 12 k2 rows: pass A holds k2 0..6 and 19..24 (units 0..6 on lanes
+  // 0..6), pass B k2 7..18 (units 7..12 on lanes 0..5).  Each pass reads all
+  // its rows before anything overwrites them; the powers wait in VGPRs.
+  float2* reg = fr + w * RF_WS + q * RF_FS;
+  float pa[16], pb[16];
+  const int ma = min(j, 6), mb = 7 + min(j, 5);
+  {
+#pragma unroll
+    for (int k2 = 0; k2 < 7; ++k2) reg[k2 * 8 + j] = z[k2];
+#pragma unroll
+    for (int k2 = 19; k2 < 25; ++k2) reg[(k2 - 12) * 8 + j] = z[k2];
+    float2 A[8], B[8];
+    const int rb = ma ? 13 - ma : 0;  // row of k2 = 25 - ma
+#pragma unroll
+    for (int n1 = 0; n1 < 8; ++n1) {
+      A[n1] = reg[ma * 8 + n1];
+      B[n1] = reg[rb * 8 + n1];
+    }
+    asm volatile("" ::: "memory");  // pass B's row writes stay behind these reads
+    dft_small<8>(A);
+    dft_small<8>(B);
+    if (ma == 0) {
+#pragma unroll
+      for (int n = 0; n < 8; ++n) B[n] = A[(n + 1) & 7];
+    }
+    rf_unit<MODE, GP>(ma, A, B, t2, a, pa);
+  }
+  RF_TL(4);
+  {
+#pragma unroll
+    for (int k2 = 7; k2 < 19; ++k2) reg[(k2 - 7) * 8 + j] = z[k2];
+    float2 A[8], B[8];
+#pragma unroll
+    for (int n1 = 0; n1 < 8; ++n1) {
+      A[n1] = reg[(mb - 7) * 8 + n1];
+      B[n1] = reg[(18 - mb) * 8 + n1];
+    }
+    asm volatile("" ::: "memory");  // the P writes stay behind these reads
+    dft_small<8>(A);
+    dft_small<8>(B);
+    rf_unit<MODE, GP>(mb, A, B, t2, a, pb);
+  }
+  RF_TL(5);
+  const bool wa = j <= 6, wb = j <= 5;  // lanes with a unit of their own in pass A / B
+  if constexpr (MODE == MODE_POWER) {
+    if (t0 + q < a.T) {
+      float* orow = a.out + bf * a.os_b + (long long)(t0 + q) * a.os_t;
+#pragma unroll
+      for (int k1 = 0; k1 < 8; ++k1) {
+        if (wa) {
+          orow[(ma + 25 * k1) * a.os_k] = pa[2 * k1];
+          orow[(NC - ma - 25 * k1) * a.os_k] = pa[2 * k1 + 1];
+        }
+        if (wb) {
+          orow[(mb + 25 * k1) * a.os_k] = pb[2 * k1];
+          orow[(NC - mb - 25 * k1) * a.os_k] = pb[2 * k1 + 1];
+        }
+      }
+    }
+  } else {
+    // |X|^2 -> P (the frame's region, over its consumed rows)
+    float* P = reinterpret_cast<float*>(reg);
+#pragma unroll
+    for (int k1 = 0; k1 < 8; ++k1) {
+      if (wa) {
+        P[ma + 25 * k1] = pa[2 * k1];
+        P[NC - ma - 25 * k1] = pa[2 * k1 + 1];
+      }
+      if (wb) {
+        P[mb + 25 * k1] = pb[2 * k1];
+        P[NC - mb - 25 * k1] = pb[2 * k1 + 1];
+      }
+    }
+    // the wave's pad (the dense mel reads run up to RF_LW - 1 bins past a
+    // filter's start): finite zeros
+    if (lane < 2 * RF_PAD) reinterpret_cast<float*>(fr + w * RF_WS + 8 * RF_FS)[lane] = 0.f;
+    RF_TL(6);
+    // ---- mel + dB: lane -> (filter jm, frame f) of this wave's frames
+    float lmax = -INFINITY;
+    const float* P0 = reinterpret_cast<const float*>(fr + w * RF_WS);
+    float* obase = a.out + ((long long)bf * a.T + t0) * a.M;
+    const int f = lane & 7;  // the lane's frame; filters jm = lane / 8 + 8 i
+    auto mel = [&](int jm) __attribute__((always_inline)) {
+      float acc = 0.f;
+      if (lw) {
+        // dense rows from the filter's 16-B aligned first bin, zero weights
+        // outside it: 16-B reads of P and weights, lw / 4 of each
+        const rf4* pf = reinterpret_cast<const rf4*>(P0 + f * (2 * RF_FS) + mstart[jm]);
+        const rf4* wq = reinterpret_cast<const rf4*>(wd + jm * RF_LW);
+#pragma unroll
+        for (int c = 0; c < RF_LW / 4; ++c) {
+          if (4 * c < lw) {
+            const rf4 pv = pf[c], wv = wq[c];
+            acc = fmaf(pv[0], wv[0], acc);
+            acc = fmaf(pv[1], wv[1], acc);
+            acc = fmaf(pv[2], wv[2], acc);
+            acc = fmaf(pv[3], wv[3], acc);
+          }
+        }
+      } else {
+        const float* pf = P0 + f * (2 * RF_FS) + a.mel_start[jm];
+        const float* wq = a.mel_w + a.mel_off[jm];
+        const int L = a.mel_len[jm];
+        for (int i = 0; i < L; ++i) acc = fmaf(pf[i], wq[i], acc);
+      }
+      return acc;
+    };
+    auto emit = [&](int jm, float acc) __attribute__((always_inline)) {
+      if (t0 + f < a.T) {
+        if (a.log_mel) {
+          acc = to_db(acc, a.amin, a.amin_db, a.multiplier, a.db_offset);
+          lmax = fmaxf(lmax, acc);
+        }
+        obase[f * a.M + jm] = acc;
+      }
+    };
+    // two filters per trip: their LDS round trips overlap
+    int jm = lane >> 3;
+    for (; jm + 8 < a.M; jm += 16) {
+      const float a0 = mel(jm), a1 = mel(jm + 8);
+      emit(jm, a0);
+      emit(jm + 8, a1);
+    }
+    if (jm < a.M) emit(jm, mel(jm));
+    if (a.log_mel) {
+      lmax = wave_max(lmax);
+      if (lane == 0) a.slot_max[(long long)bf * nwb + slot] = lmax;
+    }
+  }
+  SBK_PROBE(asm volatile("s_waitcnt vmcnt(0)" ::: "memory");)
+  RF_TL(7);
+  }  // blk
+}
+
+size_t reg_lds(int mode, int M) {
+  return (size_t)(3 * 200 + 2 + RF_NW * RF_WS) * sizeof(float2) +
+         (mode == MODE_FBANK ? (size_t)M * (RF_LW + 1) * 4 : 0);
+}
+// the register-FFT kernel takes n_fft 400 mono power / Fbank
+bool use_reg(int nc, int mode, int C, int M) {
+  return nc == 200 && C == 1 && (mode == MODE_POWER || (mode == MODE_FBANK && M <= 128));
+}
+
 template <int NC> struct StaticCfg;
 template <> struct StaticCfg<200> { static constexpr int FPB = 8, NT = 320; };
 template <> struct StaticCfg<256> { static constexpr int FPB = 8, NT = 256; };
@@ -1052,6 +1446,36 @@ void launch_static_m(int nc, int rows, hipStream_t s, const SpecArgs& a) {
 }
 
 void launch_spec(int mode, int nc, int rows, size_t lds, hipStream_t s, const SpecArgs& a, const FftPlan& plan) {
+  if (use_reg(nc, mode, a.C, a.M)) {
+    const int nwb = (a.T + 7) / 8;
+    static int ncu = 0;
+    if (!ncu) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+        ncu = 256;
+    }
+    const dim3 grid(std::min(rows * ((nwb + RF_NW - 1) / RF_NW), SBK_RF_WGS_PER_CU * ncu));
+    const size_t rl = reg_lds(mode, a.M);
+    static bool attr = false;  // > 64 KB of dynamic LDS: opt in once
+    if (!attr) {
+      for (const void* k : {reinterpret_cast<const void*>(&spec_reg_kernel<MODE_POWER, true>),
+                            reinterpret_cast<const void*>(&spec_reg_kernel<MODE_POWER, false>),
+                            reinterpret_cast<const void*>(&spec_reg_kernel<MODE_FBANK, true>),
+                            reinterpret_cast<const void*>(&spec_reg_kernel<MODE_FBANK, false>)})
+        (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024);
+      attr = true;
+    }
+    const bool gp = a.power != 1.0f || (mode == MODE_POWER && a.log_mag);
+    if (mode == MODE_POWER) {
+      if (gp) hipLaunchKernelGGL((spec_reg_kernel<MODE_POWER, true>), grid, dim3(RF_NT), rl, s, a);
+      else hipLaunchKernelGGL((spec_reg_kernel<MODE_POWER, false>), grid, dim3(RF_NT), rl, s, a);
+    } else {
+      if (gp) hipLaunchKernelGGL((spec_reg_kernel<MODE_FBANK, true>), grid, dim3(RF_NT), rl, s, a);
+      else hipLaunchKernelGGL((spec_reg_kernel<MODE_FBANK, false>), grid, dim3(RF_NT), rl, s, a);
+    }
+    return;
+  }
   const int snc = static_nc(nc, mode, a.onesided);
   if (snc) {
     if (mode == MODE_STFT) launch_static_m<MODE_STFT>(snc, rows, s, a);
@@ -1075,6 +1499,7 @@ inline int grid_for(long long n, int block) {
 }  // namespace
 
 SBK_PROBE_EXPORT(sbk_probe_spec_tl, g_spec_tl)
+SBK_PROBE_EXPORT(sbk_probe_rf_tl, g_rf_tl)
 
 // ---------------------------------------------------------------------------
 // C ABI (declared in include/sbk.h)
