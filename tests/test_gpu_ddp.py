@@ -202,9 +202,13 @@ def test_brain_ddp_real_modules(dev, fused, accum):
     # step 1 starts from identical parameters: only the order of the final
     # fp32 sums differs (plus, fp32, the split-K atomics of the weight-gradient
     # GEMMs).  Step 2 starts from parameters that differ in the last fp32 bit,
-    # which the bf16 casts (the library GRU's input projection most) turn into
-    # an occasional flipped bf16 rounding: measured <= 6.5e-5.
-    compare(ga, pa, (1e-5, 2e-4) if fused else (1e-4, 1e-3), "single-process accumulation of the ranks' micro-batches")
+    # which the bf16 casts turn into occasional flipped bf16 roundings; the
+    # rel-pos bias and linear_pos gradients are batch sums that cancel to
+    # ~1e-3 of their terms and amplify those flips (as in the concatenated-
+    # batch comparison below): measured 6.5e-5 .. 2.3e-3 from one Fbank
+    # kernel's rounding to the next, while a single-process rerun is
+    # bit-stable (~5e-8)
+    compare(ga, pa, (1e-5, 5e-3) if fused else (1e-4, 1e-3), "single-process accumulation of the ranks' micro-batches")
     # the concatenated batch: the bf16 batch-reduced p_k gradient as above
     # (1e-2); fp32, the rel-pos bias and linear_pos gradients are batch sums
     # that cancel to ~1e-3 of their terms, so 2+2 vs 4-row ordering shows at
