@@ -1,4 +1,5 @@
-"""A/B of TransformerASR.encode's side stream (positional keys + key mask
+"""(Round-3 record; the SIDE_STREAM switch it toggled was removed with the
+rejected variant.)  A/B of TransformerASR.encode's side stream (positional keys + key mask
 beside the src Linear): graph replays of the bench's config-3 step with the
 switch on and off, alternating, same process and box."""
 import os
