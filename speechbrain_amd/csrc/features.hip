@@ -1153,9 +1153,37 @@ __global__ void __launch_bounds__(RF_NT, SBK_RF_MINW) spec_reg_kernel(SpecArgs a
   float2* fr = t2 + NC + 2;                        // per wave: 8 frame regions + a zero pad
   float* wd = reinterpret_cast<float*>(fr + RF_NW * RF_WS);   // mel weights, dense [M][RF_LW] from a 16-B aligned bin
   int* mstart = reinterpret_cast<int*>(wd + (MODE == MODE_FBANK ? a.M * RF_LW : 0));  // that aligned bin
+  int* mlen_s = mstart + (MODE == MODE_FBANK ? a.M : 0);  // table stage only: mel_len, mel_off
+  int* moff_s = mlen_s + (MODE == MODE_FBANK ? a.M : 0);
   __shared__ int lmax_s;
   const int tid = threadIdx.x, lane = tid & 63;
   SBK_PROBE(int tl_row = blockIdx.x * RF_NW + (tid >> 6); unsigned long long tl0 = __builtin_amdgcn_s_memtime();)
+  const int w = tid >> 6;
+  const int nwb = (a.T + 7) >> 3;                   // 8-frame slots per utterance
+  const int nblk_t = (nwb + RF_NW - 1) / RF_NW;
+  const int pad = a.center ? NC : 0;
+  // span of block bk for this wave: its first sample, or -1 (not staged:
+  // utterance ends, other geometries, or no valid slot)
+  auto span_of = [&](int bk) __attribute__((always_inline)) {
+    const int bf_ = bk / nblk_t, sl = (bk - bf_ * nblk_t) * RF_NW + w;
+    const int sp = sl * 8 * a.hop - pad;
+    const bool ok = sl < nwb && sp >= 0 && sp + RF_SPAN <= a.S && 7 * a.hop + 2 * NC <= RF_SPAN &&
+                    ((sp | a.S | a.hop) & 3) == 0;
+    return ok ? sp : -1;
+  };
+  auto fetch = [&](int bk, int sp) __attribute__((always_inline)) {
+    const float* src = a.wav + (long long)(bk / nblk_t) * a.S + sp;
+    float* stage = reinterpret_cast<float*>(fr + w * RF_WS);
+#pragma unroll
+    for (int c = 0; c < RF_SPAN / 256; ++c)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + c * 256 + lane * 4),
+                                       (__attribute__((address_space(3))) void*)(stage + c * 256), 16, 0, 0);
+  };
+  // the first block's span is in flight under the table stage
+  if (blockIdx.x < a.Bfold * nblk_t) {
+    const int sp = span_of(blockIdx.x);
+    if (sp >= 0) fetch(blockIdx.x, sp);
+  }
   // ---- tables, once per workgroup (the only workgroup barriers; tables read
   // from global memory per use measured 75 against 47 us)
   if (tid < NC) {
@@ -1168,24 +1196,30 @@ __global__ void __launch_bounds__(RF_NT, SBK_RF_MINW) spec_reg_kernel(SpecArgs a
   if constexpr (MODE == MODE_FBANK) {
     if (tid == 0) lmax_s = 0;
     __syncthreads();
-    for (int i = tid; i < a.M; i += RF_NT) atomicMax(&lmax_s, (a.mel_start[i] & 3) + a.mel_len[i]);
+    // the CSR index arrays go to LDS on the way (the dense rows then need
+    // one dependent global round trip, not two)
+    for (int i = tid; i < a.M; i += RF_NT) {
+      const int st = a.mel_start[i], ln = a.mel_len[i];
+      atomicMax(&lmax_s, (st & 3) + ln);
+      mstart[i] = st;
+      mlen_s[i] = ln;
+      moff_s[i] = a.mel_off[i];
+    }
     __syncthreads();
     const int lm = lmax_s;
     lw = lm <= RF_LW ? (lm + 3) & ~3 : 0;
     if (lw) {
       for (int i = tid; i < a.M * RF_LW; i += RF_NT) {
-        const int jm = i / RF_LW, c = i - jm * RF_LW, L = a.mel_len[jm];
-        const int sh = a.mel_start[jm] & 3;
-        wd[i] = c >= sh && c - sh < L ? a.mel_w[a.mel_off[jm] + c - sh] : 0.f;
+        const int jm = i / RF_LW, c = i - jm * RF_LW, L = mlen_s[jm];
+        const int sh = mstart[jm] & 3;
+        wd[i] = c >= sh && c - sh < L ? a.mel_w[moff_s[jm] + c - sh] : 0.f;
       }
-      for (int i = tid; i < a.M; i += RF_NT) mstart[i] = a.mel_start[i] & ~3;
+      __syncthreads();  // every read of mstart above is done
+      for (int i = tid; i < a.M; i += RF_NT) mstart[i] &= ~3;
     }
   }
   __syncthreads();
   SBK_PROBE(const unsigned long long tl1 = __builtin_amdgcn_s_memtime();)
-  const int w = tid >> 6;
-  const int nwb = (a.T + 7) >> 3;                   // 8-frame slots per utterance
-  const int nblk_t = (nwb + RF_NW - 1) / RF_NW;
   // persistent: workgroup-sized blocks of 64 frames strided over the grid
   // (the mel table is built once per workgroup)
   for (int blk = blockIdx.x; blk < a.Bfold * nblk_t; blk += gridDim.x) {
@@ -1207,21 +1241,19 @@ __global__ void __launch_bounds__(RF_NT, SBK_RF_MINW) spec_reg_kernel(SpecArgs a
   // ---- z[n2] = windowed (x[2n], x[2n+1]), n = 8 n2 + j
   float2 z[25];
   {
-    const int pad = a.center ? NC : 0;
     const int s0 = tf * a.hop - pad + 2 * j;
-    const int span0 = t0 * a.hop - pad;  // first sample of the wave's 8 frames
-    if (span0 >= 0 && span0 + RF_SPAN <= a.S && 7 * a.hop + 2 * NC <= RF_SPAN && ((span0 | a.S | a.hop) & 3) == 0) {
+    const int span0 = span_of(blk);  // first sample of the wave's 8 frames, or -1
+    if (span0 >= 0) {
       // the wave's samples (one contiguous span) -> its frame regions by
       // LDS-DMA: RF_SPAN / 256 16-B pieces per lane instead of 25 strided
       // 8-B loads per lane (the vector-memory address rate, not HBM, set the
-      // load phase); the frames then read their z pairs from LDS
-      float* stage = reinterpret_cast<float*>(fr + w * RF_WS);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the last block's LDS reads are done
-#pragma unroll
-      for (int c = 0; c < RF_SPAN / 256; ++c)
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(wrow + span0 + c * 256 + lane * 4),
-            (__attribute__((address_space(3))) void*)(stage + c * 256), 16, 0, 0);
+      // load phase); the frames then read their z pairs from LDS.  The first
+      // block's span was issued before the table stage.
+      const float* stage = reinterpret_cast<const float*>(fr + w * RF_WS);
+      if (blk != blockIdx.x) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the last block's LDS reads are done
+        fetch(blk, span0);
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const float2* src = reinterpret_cast<const float2*>(stage + (tf - t0) * a.hop + 2 * j);
 #pragma unroll
@@ -1385,7 +1417,7 @@ __global__ void __launch_bounds__(RF_NT, SBK_RF_MINW) spec_reg_kernel(SpecArgs a
 
 size_t reg_lds(int mode, int M) {
   return (size_t)(3 * 200 + 2 + RF_NW * RF_WS) * sizeof(float2) +
-         (mode == MODE_FBANK ? (size_t)M * (RF_LW + 1) * 4 : 0);
+         (mode == MODE_FBANK ? (size_t)M * (RF_LW + 3) * 4 : 0);
 }
 // the register-FFT kernel takes n_fft 400 mono power / Fbank
 bool use_reg(int nc, int mode, int C, int M) {
