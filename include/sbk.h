@@ -35,7 +35,10 @@ int sbk_fft_supported(int n_fft);
  *   mode 0: STFT  -> out[bo*os_b + c*os_c + t*os_t + k*os_k + ri*os_ri]
  *   mode 1: power -> out[bo*os_b + c*os_c + t*os_t + k*os_k]  (power, eps, log_mag)
  *   mode 2: Fbank -> out (Bo, T, M) dB; slot_max (Bo, sbk_spectrum_slots(..)) receives one
- *           partial max per workgroup (input of sbk_topdb_clamp; no atomics, deterministic)
+ *           partial max per 8 frames (input of sbk_topdb_clamp; no atomics, deterministic)
+ * n_fft 400 with C == 1 in modes 1 / 2 (M <= 128) runs the register-FFT kernel (8 lanes per
+ * frame, LDS-DMA staged waveform); other sizes / modes the LDS Stockham kernels.  Both write
+ * the same slot layout, so consumers of slot_max see no difference. 
  * wav: (Bo, S, C) fp32; window: n_fft fp32 (win centred, zero padded);
  * twiddle_nc: n_fft/2 complex W_{n_fft/2}^m; twiddle_nfft: n_fft/2+1 complex W_{n_fft}^k;
  * out_strides: HOST array of 5 int64 (modes 0/1); mel_*: per-filter CSR of the

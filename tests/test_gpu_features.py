@@ -289,3 +289,35 @@ def test_fbank_deltas_floor_on_load(dev, n_mels):
     assert torch.equal(out, ref)
     raw, _ = Fbank(n_mels=n_mels).to(dev).forward_deferred(wav)
     assert (raw < plain).any(), "the floor must bind somewhere for this test to mean anything"
+
+
+@pytest.mark.parametrize("S,hop_ms,center,pad,power,log", [
+    (16000, 10, True, "constant", 1, False),    # staged spans (hop 160), utterance ends on the map_pos path
+    (3001, 10, True, "constant", 1, False),     # T = 19: a partial 8-frame wave, frames past T recomputed
+    (1200, 10, True, "constant", 1, False),     # T = 8: one wave, every frame near an end
+    (16000, 6.25, True, "reflect", 1, False),   # hop 100 (staged), reflect padding at the ends
+    (16000, 10.125, True, "constant", 1, False),  # hop 162: spans not 16-B aligned -> unstaged path
+    (16000, 10, False, "constant", 0.5, True),  # center=False, generic power + log magnitude
+])
+def test_register_fft_geometries_vs_oracle(dev, S, hop_ms, center, pad, power, log):
+    """The n_fft = 400 power / Fbank path (spec_reg_kernel, features.hip): its
+    LDS-DMA span staging, unstaged edge path, partial waves and generic
+    power, against the float64 oracle (features.py:101-188, 327-356)."""
+    F, _ = _mods()
+    g = torch.Generator().manual_seed(S + int(100 * hop_ms))
+    x = 0.2 * torch.randn(3, S, generator=g)
+    st = F.STFT(16000, hop_length=hop_ms, center=center, pad_mode=pad)
+    ref = OF.spectral_magnitude(OF.stft(x, 16000, 25, hop_ms, 400, center=center, pad_mode=pad,
+                                        compute_dtype=torch.float64), power=power, log=log)
+    out = st.power_spectrum(x.to(dev), power=power, log=log)
+    assert out.shape == ref.shape
+    if log:
+        assert_close(out, ref, rtol=2e-4, name="log power")
+    else:
+        scale = float(ref.abs().max())
+        assert_close(out / scale, ref / scale, rtol=2e-6, name="power")
+    if center and pad == "constant" and power == 1:
+        # the fused Fbank (mel + dB in the same kernel) at this geometry
+        _, LF = _mods()
+        fbk = LF.Fbank(n_mels=80, hop_length=hop_ms)(x.to(dev))
+        assert_close(fbk, OF.fbank(x, n_mels=80, hop_length=hop_ms), name="fbank")
