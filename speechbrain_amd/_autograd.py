@@ -414,16 +414,17 @@ class ConvBlockFn(Function):
     """One ConvBlock layer (convolution.py:112-175): Conv2d with "same"
     reflect padding (CNN.py:616-700) -> [LayerNorm over (freq, chan)] ->
     [LeakyReLU], as im2col (HIP) + MFMA GEMM + wide LayerNorm + activation.
-    geom = (kT, kF, sT, sF): time / freq kernel and stride (odd kernels;
-    padding (k - 1) / 2, get_padding_elem :1459-1481).  ln_w None: no norm
+    geom = (kT, kF, sT, sF[, pT, pF]): time / freq kernel and stride, and
+    the reflect padding per side (default (k - 1) / 2 for odd kernels,
+    get_padding_elem :1459-1481; 0 = "valid").  ln_w None: no norm
     (ln_b, eps ignored); slope None: no activation (the residual branch's
     1x1 conv + norm).  x (B, Ti, Fi, Ci) -> (B, To, Fo, Co)."""
 
     @staticmethod
     def forward(ctx, x, w, bias, ln_w, ln_b, eps, slope, dtype, out_dtype, geom):
         x = _cont(x)
-        kt, kf, st, sf = geom
-        pt, pf = (kt - 1) // 2, (kf - 1) // 2
+        kt, kf, st, sf = geom[:4]
+        pt, pf = geom[4:] if len(geom) == 6 else ((kt - 1) // 2, (kf - 1) // 2)
         B, Ti, Fi, Ci = x.shape
         Co = w.shape[0]
         To, Fo = (Ti + 2 * pt - kt) // st + 1, (Fi + 2 * pf - kf) // sf + 1

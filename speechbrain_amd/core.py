@@ -92,7 +92,8 @@ class Brain:
     def init_optimizers(self):
         self.optimizer = self.opt_class(self.modules.parameters())
 
-    def zero_grad(self, set_to_none=True):
+    def zero_grad(self, set_to_none=False):
+        """core.py:848-856 (zeros by default, as the reference)."""
         self.optimizer.zero_grad(set_to_none)
 
     @contextlib.contextmanager

@@ -1079,7 +1079,10 @@ SBK_API int sbk_layernorm_bwd(const float* x, const void* dy, int dy_bf16, int M
 
 SBK_API int sbk_layernorm_wide(const float* x, int M, int D, const float* g, const float* b, float eps, void* y,
                                int y_bf16, void* stream) {
-  if (M <= 0 || D <= 0) return SBK_ERR_ARG;
+  // the same row limit as sbk_layernorm_bwd (its workgroup-per-row kernel
+  // keeps 2 x D fp32 partials in LDS): a row the backward cannot take is
+  // refused here, before any forward work
+  if (M <= 0 || D <= 0 || D > 16384) return SBK_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   if (D > 2560) {
     ln_fwd_row_kernel<<<grid_for(M, 1, 4096), 256, 0, s>>>(x, M, D, g, b, eps, y, y_bf16);

@@ -378,6 +378,26 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     // id: hoisted, they would hold 2 x GL 64-bit addresses through the launch
     int ln;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+#ifdef SBK_PROBE_CONTIG
+    // probe (wrong results, timing only): tile t of a matrix read as the
+    // contiguous 32 KB block t, inside the same allocation
+    {
+      const bf16_t* mat;
+      int ti;
+      if (PROJ && s >= SF) {
+        mat = a.wp;
+        ti = s - SF;
+      } else {
+        const bool sb = CHAIN && s >= S;
+        const int sl = sb ? s - S : s;
+        const int c = sl / SPC, r = sl - c * SPC;
+        mat = r < K1 ? (sb ? a.w1b : a.w1) : (sb ? a.w2b : a.w2);
+        ti = r < K1 ? c * K1 + r : c * K2 + r - K1;
+      }
+      base = mat + (long long)ti * TROWS * BK;
+      ld = BK;
+    }
+#endif
 #pragma unroll
     for (int i = 0; i < GL; ++i) {
       const int r0 = w * (T * 16) + i * 8;  // the wave's own rows: it is their only reader

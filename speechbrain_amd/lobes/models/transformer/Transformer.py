@@ -31,7 +31,8 @@ from .... import _autograd as A
 from ....nnet.attention import MultiheadAttention, PositionalwiseFeedForward, RelPosMHAXL, _mode_weight
 from ....nnet.normalization import LayerNorm
 
-__all__ = ["PositionalEncoding", "TransformerEncoderLayer", "TransformerEncoder"]
+__all__ = ["PositionalEncoding", "TransformerEncoderLayer", "TransformerEncoder", "TransformerDecoderLayer",
+           "TransformerDecoder", "NormalizedEmbedding", "get_key_padding_mask", "get_lookahead_mask"]
 
 _f32, _bf16 = torch.float32, torch.bfloat16
 
@@ -211,3 +212,146 @@ class TransformerEncoder(nn.Module):
         kpm = src_key_padding_mask.to(torch.uint8).contiguous() if src_key_padding_mask is not None else None
         y, attns = self.run(src.float().reshape(B * T, d).contiguous(), B, T, kpm, True)
         return y.view(B, T, d), attns
+
+
+# ---------------------------------------------------------------------------
+# Decoder side (Transformer.py:489-797): TransformerDecoderLayer,
+# TransformerDecoder, NormalizedEmbedding.  The decoder is outside the
+# accelerated path (attention decoders OUT); it exists so that a
+# recipe's TransformerASR(num_decoder_layers > 0) constructs with the
+# reference's module tree and state_dict keys, loads its checkpoint with
+# strict=True, and runs forward()/decode() with the reference's semantics.
+# Its LayerNorms and FFNs are the HIP drop-ins (nnet.normalization.LayerNorm,
+# nnet.attention.PositionalwiseFeedForward); the masked self- and cross-
+# attention use the wrapped torch.nn.MultiheadAttention on the device (the
+# reference's own call, attention.py:752-769), since the HIP attention
+# kernels cover the encoder's self-attention only.
+# ---------------------------------------------------------------------------
+def _ref_mha(mod, query, key, value, attn_mask=None, key_padding_mask=None, need_weights=True):
+    """sb.nnet.attention.MultiheadAttention.forward (attention.py:749-778)
+    on the wrapped nn.MultiheadAttention: (B, L, E) in and out."""
+    out = mod.att(query.permute(1, 0, 2), key.permute(1, 0, 2), value.permute(1, 0, 2), attn_mask=attn_mask,
+                  key_padding_mask=key_padding_mask, need_weights=need_weights)
+    if need_weights:
+        o, w = out
+        return o.permute(1, 0, 2), w
+    return out[0].permute(1, 0, 2), None
+
+
+class TransformerDecoderLayer(nn.Module):
+    """Transformer.py:489-654 (regularMHA; the decoder TransformerASR builds)."""
+
+    def __init__(self, d_ffn, nhead, d_model, kdim=None, vdim=None, dropout=0.0, activation=nn.ReLU,
+                 normalize_before=False, attention_type="regularMHA", causal=None):
+        super().__init__()
+        if attention_type != "regularMHA":
+            raise NotImplementedError("TransformerDecoderLayer: attention_type='regularMHA' (what TransformerASR "
+                                      "builds, Transformer.py:180-192)")
+        self.nhead = nhead
+        self.self_attn = MultiheadAttention(nhead=nhead, d_model=d_model, kdim=kdim, vdim=vdim, dropout=dropout)
+        self.mutihead_attn = MultiheadAttention(nhead=nhead, d_model=d_model, kdim=kdim, vdim=vdim, dropout=dropout)
+        self.pos_ffn = PositionalwiseFeedForward(d_ffn=d_ffn, input_size=d_model, dropout=dropout,
+                                                 activation=activation)
+        self.norm1 = LayerNorm(d_model, eps=1e-6)
+        self.norm2 = LayerNorm(d_model, eps=1e-6)
+        self.norm3 = LayerNorm(d_model, eps=1e-6)
+        self.dropout1 = nn.Dropout(dropout)
+        self.dropout2 = nn.Dropout(dropout)
+        self.dropout3 = nn.Dropout(dropout)
+        self.normalize_before = normalize_before
+
+    def forward(self, tgt, memory, tgt_mask=None, memory_mask=None, tgt_key_padding_mask=None,
+                memory_key_padding_mask=None, pos_embs_tgt=None, pos_embs_src=None):
+        if pos_embs_tgt is not None or pos_embs_src is not None:
+            raise NotImplementedError("regularMHA decoder: pos_embs are added by the caller (TransformerASR)")
+        tgt1 = self.norm1(tgt) if self.normalize_before else tgt
+        tgt2, self_attn = _ref_mha(self.self_attn, tgt1, tgt1, tgt1, attn_mask=tgt_mask,
+                                   key_padding_mask=tgt_key_padding_mask)
+        tgt = tgt + self.dropout1(tgt2)
+        if not self.normalize_before:
+            tgt = self.norm1(tgt)
+        tgt1 = self.norm2(tgt) if self.normalize_before else tgt
+        tgt2, multihead_attention = _ref_mha(self.mutihead_attn, tgt1, memory, memory, attn_mask=memory_mask,
+                                             key_padding_mask=memory_key_padding_mask)
+        tgt = tgt + self.dropout2(tgt2)
+        if not self.normalize_before:
+            tgt = self.norm2(tgt)
+        tgt1 = self.norm3(tgt) if self.normalize_before else tgt
+        tgt2 = self.pos_ffn(tgt1)
+        tgt = tgt + self.dropout3(tgt2)
+        if not self.normalize_before:
+            tgt = self.norm3(tgt)
+        return tgt, self_attn, multihead_attention
+
+
+class TransformerDecoder(nn.Module):
+    """Transformer.py:657-763 (layers.N.*, norm.norm.*)."""
+
+    def __init__(self, num_layers, nhead, d_ffn, d_model, kdim=None, vdim=None, dropout=0.0, activation=nn.ReLU,
+                 normalize_before=False, causal=False, attention_type="regularMHA"):
+        super().__init__()
+        self.layers = nn.ModuleList([
+            TransformerDecoderLayer(d_ffn=d_ffn, nhead=nhead, d_model=d_model, kdim=kdim, vdim=vdim, dropout=dropout,
+                                    activation=activation, normalize_before=normalize_before, causal=causal,
+                                    attention_type=attention_type) for _ in range(num_layers)])
+        self.norm = LayerNorm(d_model, eps=1e-6)
+
+    def forward(self, tgt, memory, tgt_mask=None, memory_mask=None, tgt_key_padding_mask=None,
+                memory_key_padding_mask=None, pos_embs_tgt=None, pos_embs_src=None):
+        output = tgt
+        self_attns, multihead_attns = [], []
+        for dec_layer in self.layers:
+            output, self_attn, multihead_attn = dec_layer(
+                output, memory, tgt_mask=tgt_mask, memory_mask=memory_mask, tgt_key_padding_mask=tgt_key_padding_mask,
+                memory_key_padding_mask=memory_key_padding_mask, pos_embs_tgt=pos_embs_tgt, pos_embs_src=pos_embs_src)
+            self_attns.append(self_attn)
+            multihead_attns.append(multihead_attn)
+        return self.norm(output), self_attns, multihead_attns
+
+
+class _Embedding(nn.Module):
+    """nnet/embedding.py:13-114 Embedding (one-hot off): nn.Embedding under
+    `.Embedding`, indices cast to long."""
+
+    def __init__(self, num_embeddings, embedding_dim=128, consider_as_one_hot=False, blank_id=0):
+        super().__init__()
+        if consider_as_one_hot:
+            raise NotImplementedError("one-hot Embedding is not on the accelerated path")
+        self.num_embeddings = num_embeddings
+        self.embedding_dim = embedding_dim
+        self.blank_id = blank_id
+        self.Embedding = nn.Embedding(num_embeddings, embedding_dim)
+
+    def forward(self, x):
+        return self.Embedding(x.long())
+
+
+class NormalizedEmbedding(nn.Module):
+    """Transformer.py:766-797: emb(x) * sqrt(d_model)."""
+
+    def __init__(self, d_model, vocab):
+        super().__init__()
+        self.emb = _Embedding(num_embeddings=vocab, embedding_dim=d_model, blank_id=0)
+        self.d_model = d_model
+
+    def forward(self, x):
+        return self.emb(x) * math.sqrt(self.d_model)
+
+
+def get_key_padding_mask(padded_input, pad_idx):
+    """Transformer.py:800-830."""
+    if len(padded_input.shape) == 4:
+        bz, time, ch1, ch2 = padded_input.shape
+        padded_input = padded_input.reshape(bz, time, ch1 * ch2)
+    key_padded_mask = padded_input.eq(pad_idx).to(padded_input.device)
+    if len(padded_input.shape) > 2:
+        return key_padded_mask.float().prod(dim=-1).bool().detach()
+    return key_padded_mask.detach()
+
+
+def get_lookahead_mask(padded_input):
+    """Transformer.py:833-858: (L, L) float mask, -inf above the diagonal."""
+    seq_len = padded_input.shape[1]
+    mask = (torch.triu(torch.ones((seq_len, seq_len), device=padded_input.device)) == 1).transpose(0, 1)
+    mask = mask.float().masked_fill(mask == 0, float("-inf")).masked_fill(mask == 1, float(0.0))
+    return mask.detach().to(padded_input.device)

@@ -1,12 +1,18 @@
 """Drop-in for the Conv2d wrapper of speechbrain.nnet.CNN (CNN.py:504-722):
 same constructor and state_dict key (conv.weight / conv.bias).  Inside a
 ConvBlock the convolution runs fused with its LayerNorm and LeakyReLU
-(lobes.models.convolution); this module carries the parameters and the
-"same"/reflect geometry (CNN.py:659-700, get_padding_elem :1459-1481)."""
+(lobes.models.convolution); standalone, forward() is the reference's
+(B, T, F[, C]) → (B, T', F', C_out) convolution (CNN.py:616-657) on the HIP
+im2col kernel + the MFMA GEMM (_autograd.ConvBlockFn without norm and
+activation, so it is differentiable), with the "same"/reflect padding
+(get_padding_elem :1459-1481) or "valid"."""
 import math
 
 import torch
 import torch.nn as nn
+
+from .. import _autograd as A
+from .. import _enc
 
 
 def get_padding_elem(L_in: int, stride: int, kernel_size: int, dilation: int):
@@ -78,5 +84,38 @@ class Conv2d(nn.Module):
                 and not self.skip_transpose)
 
     def forward(self, x):
-        raise NotImplementedError("standalone Conv2d runs inside the fused ConvBlock "
-                                  "(speechbrain_amd.lobes.models.convolution)")
+        """CNN.py:616-657: x (B, T, F, C) — or (B, T, F) for a 3-D input_shape —
+        → (B, T', F', C_out) ((B, T', F') when C_out = 1 and the input was 3-D,
+        the reference's squeeze(1))."""
+        if self.skip_transpose:
+            raise NotImplementedError("Conv2d(skip_transpose=True): the accelerated path takes (B, T, F, C)")
+        if self.groups != 1 or self.dilation != (1, 1):
+            raise NotImplementedError("Conv2d: groups=1 and dilation 1 are on the accelerated path")
+        (kf, kt), (sf, st) = self.kernel_size, self.stride
+        if self.padding == "same":
+            if self.padding_mode != "reflect":
+                raise NotImplementedError("Conv2d 'same' padding: padding_mode='reflect' is on the accelerated path")
+            # get_padding_elem: floor(k / 2) per side for stride > 1, (k - 1) / 2 at stride 1 (odd k)
+            pt, pf = kt // 2 if st > 1 else (kt - 1) // 2, kf // 2 if sf > 1 else (kf - 1) // 2
+        elif self.padding == "valid":
+            pt = pf = 0
+        else:
+            raise NotImplementedError(f"Conv2d padding={self.padding!r}: 'same' (reflect) and 'valid' are on the "
+                                      "accelerated path")
+        squeeze = x.dim() == 3
+        if squeeze:
+            x = x.unsqueeze(-1)
+        if x.shape[-1] != self.in_channels:
+            raise ValueError(f"Conv2d: {x.shape[-1]} input channels, expected {self.in_channels}")
+        if self.padding == "same" and (pt >= x.shape[1] or pf >= x.shape[2]):
+            raise ValueError("Conv2d: reflect padding needs more frames / bins than the padding")
+        dtype = _enc.compute_dtype()
+        cv = self.conv
+        xin = x if (x.dtype == dtype or self.in_channels == 1) else A.to_dtype(x, dtype)
+        if xin.dtype not in (torch.float32, torch.bfloat16):
+            xin = xin.float()
+        y = A.ConvBlockFn.apply(xin, cv.weight, cv.bias, None, None, 1e-5, None, dtype, torch.float32,
+                                (kt, kf, st, sf, pt, pf))
+        if squeeze and y.shape[-1] == 1:
+            y = y.squeeze(-1)
+        return y

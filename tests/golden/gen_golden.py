@@ -47,6 +47,17 @@ Fixture inventory (all float32 unless noted):
                    causal and a float 3-D attn_mask, SpecAugment bilinear
                    warp (lobes/models/convolution.py:12-175,
                    nnet/attention.py:598-611, lobes/augment.py:116-148)
+  recipe.npz       Fbank(80) on all 12 tests/samples/ASR WAVs; Filterbank
+                   param_rand_factor jitter (training mode, seeds 0-2);
+                   standalone Conv2d (same / strided / valid / 3-D input,
+                   outputs and gradients); TransformerASR with a 2-layer
+                   decoder (seeded init, state_dict, forward, encode,
+                   decode); six reference Brain.fit_batch steps (SGD,
+                   grad accumulation 2, clip 5.0, a NaN loss on a stepping
+                   batch) with every parameter after each step
+                   (lobes/features.py:82-147, processing/features.py:525-532,
+                   nnet/CNN.py:504-700, lobes/models/transformer/*,
+                   core.py:882-994)
   train.npz        gradients of sum(R * encode(cnn(feats), wav_len)) w.r.t.
                    every ConvolutionFrontEnd / TransformerASR parameter and
                    the input features (reference autograd, weights of
@@ -549,7 +560,140 @@ def gen_dropin():
     np.savez_compressed(os.path.join(OUT, "dropin.npz"), **out)
 
 
+def gen_recipe():
+    """recipe.npz: the recipe-level drop-ins beyond the encoder fixtures."""
+    out = {}
+    g = torch.Generator().manual_seed(41)
+    # 1. Fbank(n_mels=80) on every tests/samples/ASR WAV (dataio.py:216-250 scaling)
+    names = sorted(f[:-4] for f in os.listdir(os.path.join(REF, "tests/samples/ASR")) if f.endswith(".wav"))
+    fb = LF.Fbank(n_mels=80)
+    fb.eval()
+    out["wav_names"] = np.array(names)
+    with torch.no_grad():
+        for n in names:
+            pcm = read_wav(n)
+            out[f"pcm.{n}"] = pcm.astype(np.int16)
+            out[f"fbank80.{n}"] = t2n(fb(torch.from_numpy(pcm.astype(np.float32) / 32768.0)[None]))
+    # 2. Filterbank(param_rand_factor=0.1) in training mode: the per-call
+    #    torch.rand(2) jitter of central frequencies and bands
+    #    (processing/features.py:525-532), seeds 0..2, and eval mode (no jitter)
+    spec = torch.rand(2, 37, 201, generator=g) * 3
+    out["fbj_spec"] = t2n(spec)
+    fbj = F.Filterbank(n_mels=40, param_rand_factor=0.1)
+    fbj.train()
+    with torch.no_grad():
+        for sd in range(3):
+            torch.manual_seed(sd)
+            out[f"fbj_train_s{sd}"] = t2n(fbj(spec))
+        fbj.eval()
+        out["fbj_eval"] = t2n(fbj(spec))
+    # 3. standalone Conv2d (nnet/CNN.py:504-700): "same" reflect padding
+    #    (stride 1 and 2, non-square kernels), "valid", a 3-D input
+    from speechbrain.nnet.CNN import Conv2d
+    convs = {
+        "c33": dict(out_channels=5, kernel_size=(3, 3), input_shape=(2, 21, 13, 3)),
+        "c53s21": dict(out_channels=6, kernel_size=(5, 3), stride=(2, 1), input_shape=(2, 19, 16, 4)),
+        "cvalid": dict(out_channels=4, kernel_size=(3, 5), padding="valid", input_shape=(2, 17, 12, 2)),
+        "c3d": dict(out_channels=3, kernel_size=(3, 3), input_shape=(2, 15, 11)),
+    }
+    for tag, kw in convs.items():
+        torch.manual_seed(5)
+        conv = Conv2d(**kw)
+        for k, v in conv.state_dict().items():
+            out[f"{tag}.{k}"] = t2n(v)
+        x = torch.randn(*kw["input_shape"], generator=g).requires_grad_(True)
+        y = conv(x)
+        R = torch.randn(y.shape, generator=g)
+        (y * R).sum().backward()
+        out[f"{tag}_x"], out[f"{tag}_y"], out[f"{tag}_R"] = t2n(x), t2n(y), t2n(R)
+        out[f"{tag}_grad_x"] = t2n(x.grad)
+        for k, p in conv.named_parameters():
+            out[f"{tag}_grad.{k}"] = t2n(p.grad)
+    # 4. TransformerASR with the decoder (conformer_small.yaml's shape of
+    #    model at a small size): seeded-init checksums, state_dict, forward
+    #    (encoder + decoder), encode and decode
+    torch.manual_seed(9)
+    asr = TransformerASR(tgt_vocab=31, input_size=40, d_model=64, nhead=4, num_encoder_layers=2,
+                         num_decoder_layers=2, d_ffn=128, dropout=0.1, activation=torch.nn.GELU,
+                         encoder_module="conformer", attention_type="RelPosMHAXL", normalize_before=True,
+                         causal=False)
+    asr.eval()
+    params = dict(asr.named_parameters())
+    for k, v in asr.state_dict().items():
+        if k in params:  # buffers (the sine tables) are checked by their checksums only
+            out[f"asr.{k}"] = t2n(v)
+        v64 = v.double()
+        out[f"asr_sum.{k}"] = np.asarray(float(v64.sum()), np.float64)
+    src = torch.randn(3, 23, 40, generator=g)
+    tgt = torch.randint(1, 31, (3, 9), generator=g)
+    tgt[1, 6:] = 0  # padding (pad_idx 0)
+    tgt[2, 4:] = 0
+    wav_len = torch.tensor([1.0, 0.7, 0.45])
+    with torch.no_grad():
+        enc_out, dec_out = asr(src, tgt, wav_len)
+        enc = asr.encode(src, wav_len)
+        enc_len = torch.round(wav_len * 23).long()
+        pred, att = asr.decode(tgt, enc, enc_len)
+    out["asr_src"], out["asr_tgt"], out["asr_wav_len"] = t2n(src), tgt.numpy(), t2n(wav_len)
+    out["asr_fwd_enc"], out["asr_fwd_dec"], out["asr_enc"] = t2n(enc_out), t2n(dec_out), t2n(enc)
+    out["asr_enc_len"] = enc_len.numpy()
+    out["asr_dec_pred"], out["asr_dec_att"] = t2n(pred), t2n(att)
+    # 5. the reference Brain step (core.py:882-994) on CPU: ConvolutionFrontEnd +
+    #    2-layer TransformerASR encoder (weights of conformer.npz), SGD,
+    #    grad_accumulation_factor 2, max_grad_norm 5.0, a NaN loss on the
+    #    4th batch (an optimizer step: skipped, nonfinite_count 1)
+    from speechbrain.core import Brain, Stage  # noqa: F401
+    g0 = np.load(os.path.join(OUT, "conformer.npz"))
+    cnn = ConvolutionFrontEnd(input_shape=(8, 10, 80), num_blocks=2, num_layers_per_block=1,
+                              out_channels=(64, 32), kernel_sizes=(3, 3), strides=(2, 2),
+                              residuals=(False, False), dropout=0.0)
+    tr = TransformerASR(tgt_vocab=10, input_size=640, d_model=64, nhead=4, num_encoder_layers=2,
+                        num_decoder_layers=0, d_ffn=128, dropout=0.0, encoder_module="conformer",
+                        attention_type="RelPosMHAXL", normalize_before=True, causal=False)
+    for pre, m in (("cnn.", cnn), ("tr.", tr)):
+        m.load_state_dict({k[len(pre):]: torch.from_numpy(g0[k]) for k in g0.files if k.startswith(pre)})
+
+    class StepBrain(Brain):
+        def compute_forward(self, batch, stage):
+            feats, wl, _, _ = batch
+            return self.modules.tr.encode(self.modules.cnn(feats), wl)
+
+        def compute_objectives(self, y, batch, stage):
+            _, _, tgt, bad = batch
+            loss = 0.5 * ((y - tgt) ** 2).sum()
+            return loss * float("nan") if bad else loss
+
+    brain = StepBrain(modules={"cnn": cnn, "tr": tr}, opt_class=lambda ps: torch.optim.SGD(ps, lr=0.01),
+                      run_opts={"device": "cpu", "grad_accumulation_factor": 2, "max_grad_norm": 5.0})
+    brain.modules.train()
+    brain.init_optimizers()
+    brain.nonfinite_count = 0
+    wl = torch.tensor([1.0, 0.8])
+    for i in range(6):
+        feats = torch.randn(2, 40, 80, generator=g)
+        tgt = torch.randn(2, 10, 64, generator=g)
+        bad = i == 3
+        out[f"brain_feats{i}"], out[f"brain_tgt{i}"] = t2n(feats), t2n(tgt)
+        brain.step += 1
+        loss = brain.fit_batch((feats, wl, tgt, bad))
+        out[f"brain_loss{i}"] = np.asarray(float(loss), np.float64)
+        # parameters after the two optimizer steps that run (batches 1 and 5;
+        # batch 3's step is the skipped one), a float64 checksum after each batch
+        for name, m in (("cnn.", cnn), ("tr.", tr)):
+            for k, p in m.named_parameters():
+                if i in (1, 5):
+                    out[f"brain_p{i}.{name}{k}"] = t2n(p)
+        out[f"brain_psum{i}"] = np.asarray(sum(float((p.double() ** 2).sum()) for p in brain.modules.parameters()),
+                                           np.float64)
+        out[f"brain_state{i}"] = np.array([brain.step, brain.optimizer_step, brain.nonfinite_count], np.int64)
+    out["brain_wav_len"] = t2n(wl)
+    np.savez_compressed(os.path.join(OUT, "recipe.npz"), **out)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["recipe"]:
+        gen_recipe()
+        sys.exit(0)
     if sys.argv[1:] == ["dropin"]:
         gen_dropin()
         sys.exit(0)
@@ -574,6 +718,7 @@ if __name__ == "__main__":
     gen_wav2vec()
     gen_decoder()
     gen_dropin()
+    gen_recipe()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

@@ -36,6 +36,15 @@ def test_library_exports_header_symbols():
     assert lib.sbk_fft_supported(400) == 1
     assert lib.sbk_fft_supported(512) == 1
     assert lib.sbk_fft_supported(402) == 0  # 201 = 3 * 67: no plan
+    # wide-row LayerNorm: the forward refuses the rows its backward cannot
+    # take (D > 16384), before any launch (argument check only, no GPU)
+    lib.sbk_layernorm_wide.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_float, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    lib.sbk_layernorm_bwd.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_void_p]
+    assert lib.sbk_layernorm_wide(None, 4, 16385, None, None, 1e-5, None, 0, None) == 1001
+    assert lib.sbk_layernorm_bwd(None, None, 0, 4, 16385, None, 1e-5, None, None, None, None) == 1001
 
 
 def test_no_cpu_fallback():

@@ -147,6 +147,39 @@ def test_layernorm_bwd(dev, D, dy_bf16):
     assert_grad(lnd.bias.grad, ln.bias.grad, name="dbeta")
 
 
+@pytest.mark.parametrize("D", [10240, 16384])  # the default 80-mel front-end's (F·C) rows; the kernels' limit
+@pytest.mark.parametrize("with_dres", [False, True])
+def test_layernorm_wide_rows(dev, D, with_dres):
+    """Workgroup-per-row LayerNorm kernels (D > 2560: ln_fwd_row_kernel /
+    ln_bwd_row_kernel) through the C ABI, incl. the residual-gradient input
+    dres (dx = LN backward + dres, ConvBlockFn's use), against torch autograd."""
+    from speechbrain_amd._lib import lib, ptr, stream_of
+    g = torch.Generator().manual_seed(D + with_dres)
+    M = 37
+    x = torch.randn(M, D, generator=g) * 2 + 0.3
+    w = 1 + 0.2 * torch.randn(D, generator=g)
+    b = 0.1 * torch.randn(D, generator=g)
+    dy = torch.randn(M, D, generator=g)
+    dres = torch.randn(M, D, generator=g)
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
+    yr = F.layer_norm(xr, (D,), wr, br, 1e-5)
+    yr.backward(dy)
+    xd, wd, bd, dyd, dresd = (t.to(dev) for t in (x, w, b, dy, dres))
+    y = torch.empty(M, D, device=dev)
+    L = lib()
+    assert L.sbk_layernorm_wide(ptr(xd), M, D, ptr(wd), ptr(bd), 1e-5, ptr(y), 0, stream_of(xd)) == 0
+    assert_close(y, yr.detach(), rtol=1e-5, name="fwd")
+    nblk = int(L.sbk_layernorm_bwd_blocks(M))
+    part = torch.empty(nblk * 2 * D, device=dev)
+    dx = torch.empty(M, D, device=dev)
+    assert L.sbk_layernorm_bwd(ptr(xd), ptr(dyd), 0, M, D, ptr(wd), 1e-5, ptr(dresd) if with_dres else None, ptr(dx),
+                               ptr(part), stream_of(xd)) == 0
+    gb = part.view(nblk, 2 * D).sum(0)
+    assert_grad(dx, xr.grad + (dres if with_dres else 0), name="dx")
+    assert_grad(gb[:D], wr.grad, name="dgamma")
+    assert_grad(gb[D:], br.grad, name="dbeta")
+
+
 @pytest.mark.parametrize("cols", [96, 98])  # 4-wide kernels / per-element kernels (GLU halves 49)
 @pytest.mark.parametrize("name", ["swish", "glu", "leaky_relu"])
 def test_act_bwd(dev, name, cols):
