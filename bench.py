@@ -298,7 +298,8 @@ def _free_port():
 def launch_ranks(script, argv, n):
     """`--gpus N` without a torchrun launcher: start N child processes of
     `script` (one per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set as torchrun
-    would, rendezvous on 127.0.0.1) and return the worst exit code.  Called
+    would, rendezvous on 127.0.0.1) and return the first failing rank's exit code (0
+    when every rank succeeds).  Called
     before this process touches the GPU, so the parent never initialises HIP;
     the children are started (not exec'd) and the parent waits for all."""
     import subprocess
@@ -311,11 +312,14 @@ def launch_ranks(script, argv, n):
     # poll every rank: the first one that fails ends the others (its peers
     # would otherwise block in a collective until the process-group timeout)
     codes = {}
+    first_fail = None  # the exit code of the first rank that failed on its own
     while len(codes) < n:
         for r, p in enumerate(procs):
             if r not in codes and p.poll() is not None:
                 codes[r] = p.returncode
                 if p.returncode != 0:
+                    if first_fail is None:
+                        first_fail = p.returncode
                     for q in procs:
                         if q.poll() is None:
                             q.terminate()
@@ -328,7 +332,9 @@ def launch_ranks(script, argv, n):
                     for r2, q in enumerate(procs):
                         codes.setdefault(r2, q.returncode)
         time.sleep(0.05)
-    return max(codes.values(), key=abs)
+    # the peers this function terminated report -15: the failing rank's own
+    # code is the one to return
+    return first_fail if first_fail is not None else max(codes.values(), key=abs)
 
 
 def rank_env(gpus):

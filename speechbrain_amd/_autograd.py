@@ -90,8 +90,10 @@ def wgrad(g, a):
         a = a if a.dtype == _bf16 else _as(a, _bf16)
         if (N % 8 or K % 8 or g.stride(0) % 8 or a.stride(0) % 8 or (g.data_ptr() | a.data_ptr()) % 16
                 or g.stride(1) != 1 or a.stride(1) != 1):
-            gp = torch.nn.functional.pad(g, (0, -N % 8))
-            ap = torch.nn.functional.pad(a, (0, -K % 8))
+            # F.pad with a zero pad returns a clone that keeps the input's
+            # strides: .contiguous() makes the rows dense in every case
+            gp = torch.nn.functional.pad(g, (0, -N % 8)).contiguous()
+            ap = torch.nn.functional.pad(a, (0, -K % 8)).contiguous()
             return _enc.gemm_tn(gp, ap)[:N, :K]
         return _enc.gemm_tn(g, a)
     return _enc.gemm_tn(_cont(g), _cont(_as(a, _f32)))

@@ -217,6 +217,7 @@ __device__ __forceinline__ int map_pos(int p, int S, int mode, bool* valid) {
 struct SpecArgs {
   const float* wav;  // (Bo, S, C) contiguous; folded row b' = bo*C + c
   int S, C, Bfold;   // Bfold = Bo*C
+  int wav16;         // wav is 16-B aligned (the register-FFT kernel's LDS-DMA span staging needs it)
   int n_fft, hop, center, pad_mode, T;
   const float* window;  // n_fft floats (win centred, zero padded)
   const float2* tw;     // W_nc^m, m in [0, nc)
@@ -1168,7 +1169,7 @@ __global__ void __launch_bounds__(RF_NT, SBK_RF_MINW) spec_reg_kernel(SpecArgs a
     const int bf_ = bk / nblk_t, sl = (bk - bf_ * nblk_t) * RF_NW + w;
     const int sp = sl * 8 * a.hop - pad;
     const bool ok = sl < nwb && sp >= 0 && sp + RF_SPAN <= a.S && 7 * a.hop + 2 * NC <= RF_SPAN &&
-                    ((sp | a.S | a.hop) & 3) == 0;
+                    ((sp | a.S | a.hop) & 3) == 0 && a.wav16;
     return ok ? sp : -1;
   };
   auto fetch = [&](int bk, int sp) __attribute__((always_inline)) {
@@ -1592,6 +1593,7 @@ SBK_API int sbk_spectrum(int mode, const float* wav, int Bo, int S, int C, int n
   if ((n_fft & 1) || fill_plan(&plan, n_fft / 2)) return SBK_ERR_ARG;
   SpecArgs a;
   a.wav = wav; a.S = S; a.C = C; a.Bfold = Bo * C;
+  a.wav16 = (reinterpret_cast<uintptr_t>(wav) & 15) == 0;  // a view at a 4-B offset takes the unstaged path
   a.n_fft = n_fft; a.hop = hop; a.center = center; a.pad_mode = pad_mode; a.T = T;
   a.window = window;
   a.tw = reinterpret_cast<const float2*>(twiddle_nc);

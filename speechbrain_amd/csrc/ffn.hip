@@ -117,8 +117,20 @@ struct IntC {
 constexpr int FFN_BM = 48;
 constexpr int FFN_NW = 8, FFN_NT = FFN_NW * 64;  // 8 waves: LN'd rows fit in VGPRs (2 waves/SIMD)
 
+// Phase-removal probes (timing only, wrong results; scripts/probe_build.sh):
+// NOACT identity activation, NOLN no row LayerNorms, NOMFMA no FFN-step MFMAs
+// (the fragment reads stay, consumed by one add), NODMA no weight DMA.
+#ifdef SBK_PROBE_NOMFMA
+#define FFN_MFMA(A, B, C) ((C) + f32x4{(float)(A)[0], (float)(B)[1], 0.f, 0.f})
+#else
+#define FFN_MFMA(A, B, C) __builtin_amdgcn_mfma_f32_16x16x32_bf16((A), (B), (C), 0, 0, 0)
+#endif
+
 template <int ACT>
 __device__ __forceinline__ float act_fn(float v, float slope) {
+#ifdef SBK_PROBE_NOACT
+  return v;
+#endif
   if (ACT == ACT_SWISH) return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));  // bf16 hidden: approx rcp
   if (ACT == ACT_LRELU) return v >= 0.f ? v : v * slope;
   if (ACT == ACT_GELU) return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
@@ -200,6 +212,9 @@ template <int D, int T2, int MT, int NW>
 __device__ __forceinline__ void row_ln(float (&z)[T2][MT][4], float* red, const float* gam, const float* bet, float eps,
                                        int w, int g, int fr) {
   static_assert(NW == 8, "two b128 reads per row");
+#ifdef SBK_PROBE_NOLN
+  return;
+#endif
   float mean[MT], rstd[MT];
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
@@ -403,8 +418,10 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
       const int r0 = w * (T * 16) + i * 8;  // the wave's own rows: it is their only reader
       const int row = r0 + (ln >> 3);
       const bf16_t* src = base + (row * ld + (((ln & 7) ^ ((row >> 1) & 7)) << 3));
+#ifndef SBK_PROBE_NODMA
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(dst + r0 * BK), 16, 0, 0);
+#endif
     }
   };
   issue(0, 0);
@@ -550,7 +567,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
         for (int t = 0; t < T; ++t)
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
-            acc1[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ks][t], fa[ks][mt], acc1[t][mt], 0, 0, 0);
+            acc1[t][mt] = FFN_MFMA(fw[ks][t], fa[ks][mt], acc1[t][mt]);
       if (r == K1 - 1) {
         // hidden chunk -> +b1, act -> Hc (4 consecutive units per lane, one
         // 8-B store); phase 2 reads it after the next step's barrier.  The
@@ -587,7 +604,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
         for (int t = 0; t < T; ++t)
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
-            acc2[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ks][t], fa[ks][mt], acc2[t][mt], 0, 0, 0);
+            acc2[t][mt] = FFN_MFMA(fw[ks][t], fa[ks][mt], acc2[t][mt]);
     }
     if (s < 96) FFN_TL(3 + 2 * s);
   }

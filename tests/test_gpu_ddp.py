@@ -21,9 +21,12 @@ Checks (two optimizer steps, SGD lr 1e-4; gradients recorded at each step):
     GRU, whose bf16 solver is chosen per process); 1e-4 in fp32, whose
     weight-gradient GEMMs split K over fp32 atomics (a rerun of the same
     process differs by up to 2e-5).  Step 2 starts from parameters that
-    differ in the last fp32 bit: 2e-4 in bf16 (measured 6.5e-5, the library
-    GRU); 1e-3 in fp32, where the rel-pos bias / linear_pos gradients are
-    batch sums cancelling to ~1e-3 of their terms (measured 2.9e-4);
+    differ in the last fp32 bit: 5e-4 in bf16 (measured up to 2.1e-4, the
+    first ConvBlock's weight, a sum over every (frame, bin) position) for
+    every gradient except the rel-pos biases and linear_pos, batch
+    sums cancelling to ~1e-3 of their terms that amplify flipped bf16
+    roundings of their inputs (5e-3; measured 6.5e-5 .. 2.3e-3); 1e-3 in
+    fp32, where those gradients measured 2.9e-4;
   * a single-process run on the concatenated batch: in bf16 a gradient that
     is reduced over the batch INSIDE the step and stored in bf16 — the shared
     positional projection p_k's (a bf16 activation under autocast, as in the
@@ -177,9 +180,14 @@ def test_brain_ddp_real_modules(dev, fused, accum):
     def rel(a, b):
         return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
 
-    def compare(ref_grads, ref_params, tols, what):
+    # gradients that are batch sums cancelling to ~1e-3 of their terms (the
+    # rel-pos biases, the shared positional projection): they amplify
+    # last-bit differences of their inputs, and only they get `loose`
+    cancelling = ("pos_bias_u", "pos_bias_v", "linear_pos")
+
+    def compare(ref_grads, ref_params, tols, what, loose=None):
         assert len(ref_grads) == len(g0) == 2
-        for step, (gs, gr, tol) in enumerate(zip(g0, ref_grads, tols)):
+        for step, (gs, gr, tol0) in enumerate(zip(g0, ref_grads, tols)):
             assert set(gr) == set(gs), set(gr) ^ set(gs)
             assert len(gr) > 50
             worst = sorted((rel(gs[k], gr[k]), k) for k in gr)
@@ -188,8 +196,13 @@ def test_brain_ddp_real_modules(dev, fused, accum):
             # process: its bf16 gradients differ across processes at the bf16
             # rounding level (measured 9.4e-5) though a rerun in one process is
             # bit-stable
-            bad = [(e, k) for e, k in worst if e > (max(tol, 5e-4) if fused and k.startswith("dec.") else tol)]
-            assert not bad, f"step {step + 1}: DDP vs {what}: gradients beyond {tol}: {bad}"
+            def tol_of(k):
+                tol = tol0
+                if loose is not None and loose[step] is not None and any(c in k for c in cancelling):
+                    tol = loose[step]
+                return max(tol, 5e-4) if fused and k.startswith("dec.") else tol
+            bad = [(e, k, tol_of(k)) for e, k in worst if e > tol_of(k)]
+            assert not bad, f"step {step + 1}: DDP vs {what}: gradients beyond their bound: {bad}"
         for k in ref_params:
             d = (p0[k] - ref_params[k]).abs().max().item()
             assert d <= 1e-4 * max(ref_params[k].abs().max().item(), 1e-3), f"{k}: parameters {d:.2e}"
@@ -208,7 +221,8 @@ def test_brain_ddp_real_modules(dev, fused, accum):
     # batch comparison below): measured 6.5e-5 .. 2.3e-3 from one Fbank
     # kernel's rounding to the next, while a single-process rerun is
     # bit-stable (~5e-8)
-    compare(ga, pa, (1e-5, 5e-3) if fused else (1e-4, 1e-3), "single-process accumulation of the ranks' micro-batches")
+    compare(ga, pa, (1e-5, 5e-4) if fused else (1e-4, 1e-3), "single-process accumulation of the ranks' micro-batches",
+            loose=(None, 5e-3) if fused else None)
     # the concatenated batch: the bf16 batch-reduced p_k gradient as above
     # (1e-2); fp32, the rel-pos bias and linear_pos gradients are batch sums
     # that cancel to ~1e-3 of their terms, so 2+2 vs 4-row ordering shows at

@@ -321,3 +321,19 @@ def test_register_fft_geometries_vs_oracle(dev, S, hop_ms, center, pad, power, l
         _, LF = _mods()
         fbk = LF.Fbank(n_mels=80, hop_length=hop_ms)(x.to(dev))
         assert_close(fbk, OF.fbank(x, n_mels=80, hop_length=hop_ms), name="fbank")
+
+
+def test_fbank_misaligned_view(dev):
+    """A contiguous waveform view at a 4-B storage offset (not 16-B aligned):
+    the register-FFT kernel's LDS-DMA span staging needs a 16-B aligned base,
+    so such a view must take the unstaged load path (features.hip span_of),
+    with the same result as an aligned copy and the oracle."""
+    _, LF = _mods()
+    g = torch.Generator().manual_seed(11)
+    flat = 0.2 * torch.randn(3 * 16000 + 1, generator=g)
+    xd = flat.to(dev)[1:].view(3, 16000)
+    assert xd.is_contiguous() and xd.data_ptr() % 16 == 4
+    fb = LF.Fbank(n_mels=80)
+    out = fb(xd)
+    assert_close(out, OF.fbank(flat[1:].view(3, 16000), n_mels=80), name="fbank of a 4-B offset view")
+    assert torch.equal(out, fb(xd.clone()))

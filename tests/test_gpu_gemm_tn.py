@@ -138,3 +138,20 @@ def test_linear_backward_fp32_on_sbk(dev):
         for name, got, want in (("dX", xd.grad, xr.grad), ("dW", wd.grad, wr.grad), ("db", bd.grad, br.grad)):
             e = ((got.cpu().double() - want).norm() / want.norm()).item()
             assert e <= 1e-5, (M, name, e)
+
+
+def test_wgrad_bf16_strided_operands(dev):
+    """_autograd.wgrad's bf16 fallback with operands that are not row-dense
+    (a transposed g: stride(1) != 1) at N, K already multiples of 8 — the pad
+    is zero there, and F.pad's clone keeps the strides, so the fallback must
+    make them contiguous itself."""
+    from speechbrain_amd import _autograd as A
+    g0 = torch.Generator().manual_seed(5)
+    M, N, K = 96, 64, 40
+    gt = torch.randn(N, M, generator=g0).to(torch.bfloat16).to(dev)
+    g = gt.t()  # (M, N), stride (1, M)
+    a = torch.randn(M, K, generator=g0).to(torch.bfloat16).to(dev)
+    assert g.stride(1) != 1
+    dw = A.wgrad(g, a)
+    ref = g.float().t() @ a.float()
+    assert torch.allclose(dw.float(), ref, rtol=1e-3, atol=1e-3), float((dw.float() - ref).abs().max())

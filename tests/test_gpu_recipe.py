@@ -18,7 +18,8 @@ itself (tests/golden/recipe.npz, made by tests/golden/gen_golden.py):
 
 fp32 tolerance as everywhere: |a - b| <= 1e-4 * max(1, |b|); gradients within
 1e-4 of the tensor's largest reference gradient; Brain parameters within 1e-4
-of the largest parameter change the reference made."""
+of the largest parameter change the reference made (plus 2 fp32 ulp of the
+parameter)."""
 import numpy as np
 import pytest
 import torch
@@ -170,4 +171,7 @@ def test_brain_step_matches_reference(golden, dev):
                     ref = torch.from_numpy(g[f"brain_p{i}.{pre}{k}"])
                     step = (ref - init[pre + k].cpu()).abs().max().item()
                     err = (p.detach().cpu() - ref).abs().max().item()
-                    assert err <= 1e-4 * max(step, 1e-6), f"after batch {i}: {pre}{k} err {err:.3e} step {step:.3e}"
+                    # 1e-4 of the update the reference made, plus the fp32 rounding
+                    # of the parameter itself (2 ulp of its largest element)
+                    tol = 1e-4 * step + 2.4e-7 * ref.abs().max().item()
+                    assert err <= tol, f"after batch {i}: {pre}{k} err {err:.3e} step {step:.3e}"
