@@ -103,10 +103,13 @@ def pick_threads(probe):
     on the host's cores (torch.set_num_threads(os.cpu_count())).  A GPU box's
     process may hold only a share of the machine (OMP_NUM_THREADS is set to
     it), where os.cpu_count() threads oversubscribe; so one short probe pass
-    runs at each candidate — OMP_NUM_THREADS, the affinity mask, os.cpu_count(),
-    those beyond 4x OMP_NUM_THREADS skipped — and the fastest is used.  Returns (threads, {threads: probe seconds})."""
+    runs at each candidate — OMP_NUM_THREADS and 2x / 4x it (16 / 32 / 64 on
+    the GPU box), the affinity mask, os.cpu_count(), those beyond 4x
+    OMP_NUM_THREADS skipped — and the fastest is used.  Returns (threads,
+    {threads: probe seconds})."""
     omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    cands = {c for c in (omp, _usable_cpus(), os.cpu_count() or 1) if c >= 1}
+    cpus = os.cpu_count() or 1
+    cands = {c for c in (omp, 2 * omp, 4 * omp, _usable_cpus(), cpus) if 1 <= c <= cpus}
     if omp >= 1:  # a share is set: far beyond it only oversubscribes (minutes per pass)
         cands = {c for c in cands if c <= 4 * omp}
     times = {}
@@ -418,11 +421,9 @@ def run_c2(args, world, rank, dev):
     if c == w:
         c = w = -1
     fm_d, tm_d = fm.to(dev), tm.to(dev)
-    ar = torch.arange(F3).view(1, 1, -1)
-    n_fcells = int(((fm[..., 1:2] <= ar) & (ar < fm[..., 1:2] + fm[..., 0:1])).any(1).sum()) * T
 
-    def sa_kernels():
-        torch.ops.sbk.specaugment_(d240, B, T, F3, c, w, fm_d, tm_d, True, n_fcells, 0)
+    def sa_kernels():  # the masked-cell count on the device (-1), as the module does
+        torch.ops.sbk.specaugment_(d240, B, T, F3, c, w, fm_d, tm_d, True, -1, 0)
     kern = []
     traffic = load_traffic()
     for name, fn, nbytes, pmc in (

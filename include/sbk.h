@@ -108,9 +108,10 @@ int sbk_context_window(const float* x, float* y, int N, int T, int F, int left, 
  * 1 bilinear — the align_corners interpolate modes of :134-148) through
  * `tmp`, then frequency / time masks given as device int32 (N, n, 2)
  * [len, pos] arrays drawn on the host, filled with 0 or the running means
- * (use_mean; `partial` scratch of 2*N*ceil(T/4) + 2 floats, 16-B aligned;
- * n_fcells = number of frequency-masked cells).  F % 4 == 0 with 16-B
- * aligned x / tmp takes the float4 kernels. */
+ * (use_mean; `partial` scratch of 2*N*ceil(T/4) + 4 floats, 16-B aligned;
+ * n_fcells = number of frequency-masked cells, or < 0 to count them on the
+ * device from the mask table).  F % 4 == 0 with 16-B aligned x / tmp takes
+ * the float4 kernels. */
 int sbk_specaugment(float* x, int N, int T, int F, int c, int w, int warp_mode, float* tmp, const int* fmask,
                     int n_fmask, const int* tmask, int n_tmask, int use_mean, float* partial, long long n_fcells,
                     void* stream);
@@ -229,39 +230,54 @@ int sbk_gemm_tn_cfg(const void* A, long long lda, long long sA, const void* B, l
 int sbk_gemm_tn_f32(const float* A, long long lda, long long sA, const float* B, long long ldb, long long sB, int M,
                     int N, int K, int batch, float* C, long long ldc, long long sC, int nsplit, void* stream);
 
+/* Weight-stream image of the fused FFN kernels: the launch's bf16 weights as
+ * 32-KB tiles (256 rows x 64 k) in the order the kernel streams them — per
+ * FFN block (w1 (H, D), w2 (D, H); a chain's second block w1b, w2b) and
+ * hidden chunk of 256 units: D/64 tiles of w1, then 4 of w2; then the
+ * projection wp (np, D), D/64 tiles per 256 output columns — with the LDS
+ * bank swizzle applied (row r's 16-B chunk j' holds chunk j' ^ ((r >> 1) & 7)),
+ * so every wave streams one contiguous 4 KB per tile.  Built once per weight
+ * version by the caller (a cache), read by sbk_ffn / sbk_ffn_proj /
+ * sbk_ffn_chain.  sbk_ffn_image_elems: its size in bf16 elements (host only;
+ * -1 for an unsupported shape); chain != 0 counts the second block. */
+long long sbk_ffn_image_elems(int D, int H, int np, int chain);
+int sbk_ffn_image(const void* w1, const void* w2, const void* w1b, const void* w2b, const void* wp, int D, int H,
+                  int np, void* img, void* stream);
+
 /* Fused macaron feed-forward block, bf16 MFMA (Conformer.py:239-260 with
  * attention.py:823-839):
  *   z = x + alpha * (act(LN0(x) W1^T + b1) W2^T + b2);  out = LNp(z) if gp;
  *   u = LNn(out) if gn (bf16 when u_bf16, else fp32).
- * x, out (M, D) fp32 (out may alias x); w1 (H, D), w2 (D, H) bf16; b1, b2 required (zeros when the
- * Linear has no bias); act as sbk_gemm (not GLU). */
-int sbk_ffn(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0, const void* w1,
-            const float* b1, int act, float slope, const void* w2, const float* b2, float alpha, const float* gp,
-            const float* bp, float epsp, float* out, const float* gn, const float* bn, float epsn, void* u,
-            int u_bf16, void* stream);
+ * x, out (M, D) fp32 (out may alias x); img = sbk_ffn_image(w1, w2) of
+ * w1 (H, D), w2 (D, H) bf16; b1, b2 required (zeros when the Linear has no
+ * bias); act as sbk_gemm (not GLU). */
+int sbk_ffn(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0, const void* img,
+            const float* b1, int act, float slope, const float* b2, float alpha, const float* gp, const float* bp,
+            float epsp, float* out, const float* gn, const float* bn, float epsn, void* u, int u_bf16, void* stream);
 
-/* sbk_ffn with a projection tail: with wp (np, D) bf16, np % 256 == 0, the
- * next-LN output is not written (u must be null) but projected on chip:
- * yp (M, np) bf16 = LNn(out) wp^T — the following MHSA's in_proj
- * (attention.py:549-553, Conformer.py:186-197), replacing its QKV GEMM
- * launch.  wp == null behaves as sbk_ffn. */
-int sbk_ffn_proj(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0, const void* w1,
-                 const float* b1, int act, float slope, const void* w2, const float* b2, float alpha,
-                 const float* gp, const float* bp, float epsp, float* out, const float* gn, const float* bn,
-                 float epsn, void* u, int u_bf16, const void* wp, int np, void* yp, void* stream);
+/* sbk_ffn with a projection tail: with np > 0 (np % 256 == 0; img =
+ * sbk_ffn_image(w1, w2, null, null, wp), wp (np, D) bf16) the next-LN output
+ * is not written (u must be null) but projected on chip: yp (M, np) bf16 =
+ * LNn(out) wp^T — the following MHSA's in_proj (attention.py:549-553,
+ * Conformer.py:186-197), replacing its QKV GEMM launch.  np == 0 behaves as
+ * sbk_ffn. */
+int sbk_ffn_proj(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0, const void* img,
+                 const float* b1, int act, float slope, const float* b2, float alpha, const float* gp,
+                 const float* bp, float epsp, float* out, const float* gn, const float* bn, float epsn, void* u,
+                 int u_bf16, int np, void* yp, void* stream);
 
 /* Two consecutive FFN blocks in one launch: block A (g0 .. epsp, as
- * sbk_ffn with its post-LN) then block B (g0b .. alphab: LN0, weights and
+ * sbk_ffn with its post-LN) then block B (g0b .. alphab: LN0, biases and
  * alpha, no post-LN) on A's output, which never leaves the CU; then next-LN
- * and the projection tail as sbk_ffn_proj.  out receives B's output.  The
- * Conformer's FFN2 + norm2 of layer i with FFN1 + norm1 + in_proj of layer
- * i+1 (Conformer.py:239-260, attention.py:549-553); H is common to both. */
+ * and the projection tail as sbk_ffn_proj.  out receives B's output.  img =
+ * sbk_ffn_image(w1, w2, w1b, w2b, wp).  The Conformer's FFN2 + norm2 of
+ * layer i with FFN1 + norm1 + in_proj of layer i+1 (Conformer.py:239-260,
+ * attention.py:549-553); H is common to both. */
 int sbk_ffn_chain(const float* x, int M, int D, int H, int act, float slope, const float* g0, const float* b0,
-                  float eps0, const void* w1, const float* b1, const void* w2, const float* b2, float alpha,
-                  const float* gp, const float* bp, float epsp, const float* g0b, const float* b0b, float eps0b,
-                  const void* w1b, const float* b1b, const void* w2b, const float* b2b, float alphab, float* out,
-                  const float* gn, const float* bn, float epsn, void* u, int u_bf16, const void* wp, int np,
-                  void* yp, void* stream);
+                  float eps0, const float* b1, const float* b2, float alpha, const float* gp, const float* bp,
+                  float epsp, const float* g0b, const float* b0b, float eps0b, const float* b1b, const float* b2b,
+                  float alphab, float* out, const float* gn, const float* bn, float epsn, void* u, int u_bf16,
+                  const void* img, int np, void* yp, void* stream);
 
 /* LayerNorm (normalization.py:172-223; Conformer.py:178,194,340): one or two
  * chained LayerNorms over rows of x (M, D) fp32, D <= 1024. */

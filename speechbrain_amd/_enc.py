@@ -8,7 +8,7 @@ from typing import Optional
 
 import torch
 
-from ._lib import check, lib, ptr, require_device, stream_of
+from ._lib import SbkError, check, lib, ptr, require_device, stream_of
 
 ACT = {None: 0, "none": 0, "swish": 1, "glu": 2, "leaky_relu": 3, "relu": 3, "gelu": 4}
 _bf16 = torch.bfloat16
@@ -284,6 +284,48 @@ def ffn_supported(D, H):
     return bool(lib().sbk_ffn_supported(int(D), int(H)))
 
 
+class _ImageCache:
+    """The fused FFN kernels stream their weights from one pre-laid-out image
+    (sbk_ffn_image: 32-KB tiles in stream order, bank swizzle applied), built
+    once per set of weight tensors and reused while none of them changes.  An
+    entry keeps its source tensors referenced, so their storage cannot be
+    recycled into a false hit while it lives; LRU-bounded."""
+
+    def __init__(self, cap=64):
+        self.cap = cap
+        self._d = {}
+
+    def get(self, ws, np_):
+        key = tuple((w.data_ptr(), w._version) if w is not None else None for w in ws) + (np_,)
+        hit = self._d.pop(key, None)
+        if hit is None:
+            w1, w2, w1b, w2b, wp = ws
+            D, H = w1.shape[1], w1.shape[0]
+            n = int(lib().sbk_ffn_image_elems(D, H, np_, int(w1b is not None)))
+            if n <= 0:
+                raise SbkError(f"sbk_ffn_image_elems: unsupported shape D={D} H={H} np={np_}")
+            img = torch.empty(n, device=w1.device, dtype=_bf16)
+            check(lib().sbk_ffn_image(ptr(w1), ptr(w2), ptr(w1b), ptr(w2b), ptr(wp), D, H, np_, ptr(img),
+                                      stream_of(w1)), "sbk_ffn_image")
+            hit = (img, ws)
+            if len(self._d) >= self.cap:
+                self._d.pop(next(iter(self._d)))
+        self._d[key] = hit
+        return hit[0]
+
+
+_FFN_IMAGES = _ImageCache()
+
+
+def ffn_image(w1, w2, w1b=None, w2b=None, wp=None):
+    """The weight-stream image of one FFN block (w1 (H, D), w2 (D, H) bf16),
+    or of a chain (w1b, w2b), with the projection wp (np, D) bf16 appended."""
+    for t in (w1, w2, w1b, w2b, wp):
+        if t is not None and (t.dtype != _bf16 or not t.is_contiguous()):
+            raise TypeError("ffn_image: contiguous bf16 weights")
+    return _FFN_IMAGES.get((w1, w2, w1b, w2b, wp), 0 if wp is None else wp.shape[0])
+
+
 @torch.library.custom_op("sbk::ffn", mutates_args=())
 def _ffn_op(x: torch.Tensor, g0: torch.Tensor, b0: torch.Tensor, e0: float, w1: torch.Tensor, b1: torch.Tensor,
             act: int, slope: float, w2: torch.Tensor, b2: torch.Tensor, alpha: float, gp: Optional[torch.Tensor],
@@ -291,10 +333,11 @@ def _ffn_op(x: torch.Tensor, g0: torch.Tensor, b0: torch.Tensor, e0: float, w1: 
             next_bf16: bool) -> tuple[torch.Tensor, torch.Tensor]:
     M, D = x.shape
     H = w1.shape[0]
+    img = ffn_image(w1, w2)
     out = torch.empty_like(x)
     u = torch.empty(M, D, device=x.device, dtype=_bf16 if next_bf16 else _f32) if gn is not None else None
-    rc = lib().sbk_ffn(ptr(x), M, D, H, ptr(g0), ptr(b0), float(e0), ptr(w1), ptr(b1), act, float(slope), ptr(w2),
-                       ptr(b2), float(alpha), ptr(gp), ptr(bp), float(ep), ptr(out), ptr(gn), ptr(bn), float(en),
+    rc = lib().sbk_ffn(ptr(x), M, D, H, ptr(g0), ptr(b0), float(e0), ptr(img), ptr(b1), act, float(slope), ptr(b2),
+                       float(alpha), ptr(gp), ptr(bp), float(ep), ptr(out), ptr(gn), ptr(bn), float(en),
                        ptr(u), int(next_bf16), stream_of(x))
     check(rc, "sbk_ffn")
     return out, (u if u is not None else x.new_empty(0))
@@ -313,11 +356,12 @@ def _ffn_proj_op(x: torch.Tensor, g0: torch.Tensor, b0: torch.Tensor, e0: float,
                  bn: torch.Tensor, en: float, wp: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     M, D = x.shape
     H, NP = w1.shape[0], wp.shape[0]
+    img = ffn_image(w1, w2, wp=wp)
     out = torch.empty_like(x)
     y = torch.empty(M, NP, device=x.device, dtype=_bf16)
-    rc = lib().sbk_ffn_proj(ptr(x), M, D, H, ptr(g0), ptr(b0), float(e0), ptr(w1), ptr(b1), act, float(slope),
-                            ptr(w2), ptr(b2), float(alpha), ptr(gp), ptr(bp), float(ep), ptr(out), ptr(gn), ptr(bn),
-                            float(en), None, 1, ptr(wp), NP, ptr(y), stream_of(x))
+    rc = lib().sbk_ffn_proj(ptr(x), M, D, H, ptr(g0), ptr(b0), float(e0), ptr(img), ptr(b1), act, float(slope),
+                            ptr(b2), float(alpha), ptr(gp), ptr(bp), float(ep), ptr(out), ptr(gn), ptr(bn),
+                            float(en), None, 1, NP, ptr(y), stream_of(x))
     check(rc, "sbk_ffn_proj")
     return out, y
 
@@ -350,12 +394,13 @@ def _ffn_chain_op(x: torch.Tensor, act: int, slope: float, g0: torch.Tensor, b0:
                   wp: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     M, D = x.shape
     H, NP = w1.shape[0], wp.shape[0]
+    img = ffn_image(w1, w2, w1b, w2b, wp)
     out = torch.empty_like(x)
     y = torch.empty(M, NP, device=x.device, dtype=_bf16)
-    rc = lib().sbk_ffn_chain(ptr(x), M, D, H, act, float(slope), ptr(g0), ptr(b0), float(e0), ptr(w1), ptr(b1),
-                             ptr(w2), ptr(b2), float(alpha), ptr(gp), ptr(bp), float(ep), ptr(g0b), ptr(b0b),
-                             float(e0b), ptr(w1b), ptr(b1b), ptr(w2b), ptr(b2b), float(alphab), ptr(out), ptr(gn),
-                             ptr(bn), float(en), None, 1, ptr(wp), NP, ptr(y), stream_of(x))
+    rc = lib().sbk_ffn_chain(ptr(x), M, D, H, act, float(slope), ptr(g0), ptr(b0), float(e0), ptr(b1), ptr(b2),
+                             float(alpha), ptr(gp), ptr(bp), float(ep), ptr(g0b), ptr(b0b), float(e0b), ptr(b1b),
+                             ptr(b2b), float(alphab), ptr(out), ptr(gn), ptr(bn), float(en), None, 1, ptr(img), NP,
+                             ptr(y), stream_of(x))
     check(rc, "sbk_ffn_chain")
     return out, y
 

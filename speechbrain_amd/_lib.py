@@ -65,12 +65,14 @@ SIGNATURES = {
                                    _vp],
     # ffn.hip
     "sbk_ffn_supported": [_i, _i],
-    "sbk_ffn": [_vp, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _i, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _vp, _f,
-                _vp, _i, _vp],
-    "sbk_ffn_chain": [_vp, _i, _i, _i, _i, _f, _vp, _vp, _f, _vp, _vp, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _f,
-                      _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _f, _vp, _i, _vp, _i, _vp, _vp],
-    "sbk_ffn_proj": [_vp, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _i, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _vp,
-                     _f, _vp, _i, _vp, _i, _vp, _vp],
+    "sbk_ffn": [_vp, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _i, _f, _vp, _f, _vp, _vp, _f, _vp, _vp, _vp, _f, _vp, _i,
+                _vp],
+    "sbk_ffn_chain": [_vp, _i, _i, _i, _i, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _f,
+                      _vp, _vp, _vp, _f, _vp, _i, _vp, _i, _vp, _vp],
+    "sbk_ffn_proj": [_vp, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _i, _f, _vp, _f, _vp, _vp, _f, _vp, _vp, _vp, _f, _vp,
+                     _i, _i, _vp, _vp],
+    "sbk_ffn_image_elems": [_i, _i, _i, _i],
+    "sbk_ffn_image": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp],
     # conformer.hip
     "sbk_layernorm": [_vp, _i, _i, _vp, _vp, _f, _vp, _i, _vp, _vp, _f, _vp, _i, _vp],
     "sbk_dwconv_ln_swish": [_i, _vp, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _f, _vp, _i, _vp],
@@ -134,7 +136,7 @@ SIGNATURES = {
     "sbk_joint_bwd": [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp],
     "sbk_joint_bwd_workspace_floats": [_i, _i, _i, _i],
 }
-RESTYPES = {"sbk_relpos_attention_lds": ctypes.c_longlong, "sbk_joint_bwd_workspace_floats": ctypes.c_longlong, "sbk_rnnt_workspace_floats": ctypes.c_longlong}
+RESTYPES = {"sbk_relpos_attention_lds": ctypes.c_longlong, "sbk_ffn_image_elems": ctypes.c_longlong, "sbk_joint_bwd_workspace_floats": ctypes.c_longlong, "sbk_rnnt_workspace_floats": ctypes.c_longlong}
 
 _lib = None
 _load_error = None

@@ -46,6 +46,25 @@ __device__ __forceinline__ bool in_masks(const int* m, int n, int nm, int i) {
   return false;
 }
 
+// number of (sequence, frequency) cells covered by a frequency mask
+// (pos <= f < pos + len), over all sequences — reduced by the block.  The
+// table is read through LDS (mlds, FM_LDS ints) when it fits: the checks of
+// the (n, f) cells then cost no global round trip each.
+constexpr int FM_LDS = 2048;
+__device__ __forceinline__ long long fmask_cells(const int* fmask, int n_fmask, int N, int F, float* red, int* mlds,
+                                                 bool prestaged = false) {
+  const int nm = N * n_fmask * 2;
+  const bool staged = nm <= FM_LDS;
+  if (staged && !prestaged) {
+    for (int i = threadIdx.x; i < nm; i += blockDim.x) mlds[i] = fmask[i];
+    __syncthreads();
+  }
+  const int* m = staged ? mlds : fmask;
+  float cnt = 0.f;  // exact: < 2^24 cells
+  for (int i = threadIdx.x; i < N * F; i += blockDim.x) cnt += in_masks(m, i / F, n_fmask, i % F) ? 1.f : 0.f;
+  return (long long)block_sum(cnt, red);
+}
+
 // One block per (n, tile of TT output rows); threads over F.  CUBIC: the
 // bicubic resize (A = -0.75, border-clamped taps); else bilinear
 // (time_warp_mode="bilinear": two taps, lambda0 = 1 - lambda1, the upper
@@ -159,7 +178,9 @@ __global__ void __launch_bounds__(256) apply_kernel(const float* src, float* x, 
                                                     long long n_fcells, int use_mean) {
   __shared__ float red[16];
   __shared__ float fills[2];
+  __shared__ int mlds[FM_LDS];
   if (use_mean) {
+    if (n_fcells < 0) n_fcells = n_fmask ? fmask_cells(fmask, n_fmask, N, F, red, mlds) * T : 0;
     // deterministic reduction of the per-block partial sums, same order in every block
     float a = 0.f, m = 0.f;
     for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
@@ -317,8 +338,21 @@ __global__ void __launch_bounds__(256) warp4_kernel(const float* __restrict__ x,
 // the two fills from the partial sums, once (fixed order: deterministic);
 // 1024 threads, four independent pair loads in flight per thread
 __global__ void __launch_bounds__(1024) fills_kernel(const float* __restrict__ partial, int nparts, int N, int T,
-                                                     int F, long long n_fcells, float* __restrict__ fills) {
+                                                     int F, long long n_fcells, const int* __restrict__ fmask,
+                                                     int n_fmask, float* __restrict__ fills) {
   __shared__ float red[16];
+  __shared__ int mlds[FM_LDS];
+  // n_fcells < 0: count the frequency-masked cells here from the device mask
+  // table (no host pass over the draws); its loads go out ahead of the
+  // partial sums'
+  static_assert(FM_LDS == 2 * 1024, "two table entries per thread");
+  const int nm = N * n_fmask * 2;
+  const bool count = n_fcells < 0 && n_fmask > 0, staged = count && nm <= FM_LDS;
+  int e0 = 0, e1 = 0;
+  if (staged) {
+    if ((int)threadIdx.x < nm) e0 = fmask[threadIdx.x];
+    if ((int)threadIdx.x + 1024 < nm) e1 = fmask[threadIdx.x + 1024];
+  }
   float a = 0.f, m = 0.f;
   for (int i0 = threadIdx.x; i0 < nparts; i0 += 4 * blockDim.x) {
     float2 v[4];
@@ -335,6 +369,12 @@ __global__ void __launch_bounds__(1024) fills_kernel(const float* __restrict__ p
   }
   a = block_sum(a, red);
   m = block_sum(m, red);
+  if (staged) {
+    mlds[threadIdx.x] = e0;
+    mlds[threadIdx.x + 1024] = e1;
+    __syncthreads();
+  }
+  if (n_fcells < 0) n_fcells = count ? fmask_cells(fmask, n_fmask, N, F, red, mlds, staged) * T : 0;
   if (threadIdx.x == 0) {
     const double total = (double)N * T * F;
     const float mean1 = (float)(a / total);
@@ -388,7 +428,8 @@ __global__ void __launch_bounds__(256) apply4_kernel(const float* src, float* x,
 //   fmask (N, n_fmask, 2) / tmask (N, n_tmask, 2) int32 [len, pos] device arrays (or n_* = 0);
 //   use_mean: fill with the running means (replace_with_zero=False), else 0;
 //   partial: scratch of 2 * N * ceil(T/4) + 2 floats (when use_mean);
-//   n_fcells: number of frequency-masked cells (host-computed, for the second mean).
+//   n_fcells: number of frequency-masked cells (the second mean's count); < 0: counted on the device
+//             from fmask.
 SBK_API int sbk_specaugment(float* x, int N, int T, int F, int c, int w, int warp_mode, float* tmp, const int* fmask,
                             int n_fmask,
                             const int* tmask, int n_tmask, int use_mean, float* partial, long long n_fcells,
@@ -419,7 +460,8 @@ SBK_API int sbk_specaugment(float* x, int N, int T, int F, int c, int w, int war
     }
     if (c < 0 && n_fmask == 0 && n_tmask == 0) return 0;
     if (use_mean) {
-      hipLaunchKernelGGL(fills_kernel, dim3(1), dim3(1024), 0, s4, partial, nblk4, N, T, F, n_fcells, fills);
+      hipLaunchKernelGGL(fills_kernel, dim3(1), dim3(1024), 0, s4, partial, nblk4, N, T, F, n_fcells, fmask, n_fmask,
+                         fills);
       SBK_CHECK_LAUNCH();
     }
     hipLaunchKernelGGL(apply4_kernel, dim3(nblk4), dim3(256), 0, s4, src, x, N, T, F, fmask, n_fmask, tmask, n_tmask,

@@ -79,11 +79,13 @@ struct FfnArgs {
   int M, H;
   const float *g0, *b0;
   float eps0;
-  const bf16_t* w1;  // (H, D)
+  // the launch's weight stream: ST tiles of 256 rows x 64 k (32 KB) in
+  // stream order, each row's 16-B chunks pre-swizzled (sbk_ffn_image), so a
+  // wave's share of a tile is one contiguous 4 KB run
+  const bf16_t* img;
   const float* b1;
   int act;
   float slope;
-  const bf16_t* w2;  // (D, H)
   const float* b2;
   float alpha;
   const float *gp, *bp;  // post-LN (or null)
@@ -93,16 +95,14 @@ struct FfnArgs {
   float epsn;
   void* u;
   int u_bf16;
-  const bf16_t* wp;  // (np, D) projection of next-LN(out), or null
-  int np;
+  int np;      // projection of next-LN(out): np output columns (0: none)
   bf16_t* yp;  // (M, np) bf16
   // CHAIN: a second FFN block on the first one's output, which stays on chip
   // (the first block's `out` is not written): FFN2 + norm2 of layer i, then
   // FFN1 of layer i+1 with its own LN0, alpha, w1/b1/w2/b2; its result goes
   // to `out`, next-LN and the projection tail as for a single block
-  const float *g0b, *b0b;
+  const float *g0b, *b0b;  // null: one block
   float eps0b;
-  const bf16_t *w1b, *w2b;
   const float *b1b, *b2b;
   float alphab;
 };
@@ -205,9 +205,12 @@ __device__ __forceinline__ void vm_wait(int n) {
 
 // Full-row LayerNorm of the epilogue values z (in place).  Lane (w, g, fr)
 // holds rows mt*16 + fr, units (w*T2 + j)*16 + 4g + e; row statistics are
-// reduced over g by shuffles and over the NW waves through red[BM][NW]; gam /
-// bet are LDS copies.  Every LDS access is explicit (asm) and the barriers
-// wait on LDS only, so the weight tiles and stores in flight stay in flight.
+// reduced over g by shuffles and over the NW waves through red[2][BM][NW]
+// (mean, then variance: one buffer each, so a pass needs only the barrier
+// between its writes and its reads — a buffer's previous readers passed the
+// other pass's barrier since); gam / bet are LDS copies.  Every LDS access is
+// explicit (asm) and the barriers wait on LDS only, so the weight tiles and
+// stores in flight stay in flight.
 template <int D, int T2, int MT, int NW>
 __device__ __forceinline__ void row_ln(float (&z)[T2][MT][4], float* red, const float* gam, const float* bet, float eps,
                                        int w, int g, int fr) {
@@ -231,17 +234,17 @@ __device__ __forceinline__ void row_ln(float (&z)[T2][MT][4], float* red, const 
         }
       part[mt] = col4_sum(s);
     }
-    lds_barrier();  // the previous readers of red are done
+    float* rb = red + pass * (MT * 16 * NW);
     if (g == 0) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) lds_st1(red + (mt * 16 + fr) * NW + w, part[mt]);
+      for (int mt = 0; mt < MT; ++mt) lds_st1(rb + (mt * 16 + fr) * NW + w, part[mt]);
     }
     lds_barrier();
     f32x4 rv[MT][2];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      rv[mt][0] = lds_f4(red + (mt * 16 + fr) * NW);
-      rv[mt][1] = lds_f4(red + (mt * 16 + fr) * NW + 4);
+      rv[mt][0] = lds_f4(rb + (mt * 16 + fr) * NW);
+      rv[mt][1] = lds_f4(rb + (mt * 16 + fr) * NW + 4);
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -319,10 +322,10 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   bf16_t* Xn = ring + NB * TROWS * BK;                      // BM x XS
   bf16_t* Hs = Xn + BM * XS;                                // 2 x BM x HS
   float* b1s = reinterpret_cast<float*>(Hs + 2 * BM * HS);  // H (CHAIN: 2 H, block A then B)
-  float* red = b1s + (CHAIN ? 2 : 1) * a.H;                 // BM x NW row partials
+  float* red = b1s + (CHAIN ? 2 : 1) * a.H;                 // 2 x BM x NW row partials
   // epilogue vectors, copied to LDS in the prologue so that no global load
   // (and its in-order vmcnt wait behind the weight tiles) sits between blocks
-  float* prm = red + BM * NW;                               // P_* x D
+  float* prm = red + 2 * BM * NW;                           // P_* x D
   enum { P_B2 = 0, P_GP, P_BP, P_G0B, P_B0B, P_B2B, P_GN, P_BN, P_N };
   static_assert(P_N == NW, "one parameter row per wave");
 
@@ -332,7 +335,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   const int NCH = a.H / HC;
   const int S = NCH * SPC;                              // K-steps of one FFN block
   const int SF = CHAIN ? 2 * S : S;                     // FFN K-steps (blocks A, B)
-  const int SP = PROJ ? (a.np / TROWS) * K1 : 0;        // projection K-steps
+  const int SP = PROJ ? (a.np / TROWS) * K1 : 0;        // projection K-steps (image tiles after the FFN ones)
   const int ST = SF + SP;
   SBK_PROBE(const int tl_rec = blockIdx.x == 128 ? w : -1;)
   FFN_TL(0);
@@ -372,57 +375,22 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   // the same involution.  Steps S.. are the projection's (256 columns of Wp
   // by 64 k per tile, column block after column block).
   auto issue = [&](int s, int slot) __attribute__((always_inline)) {
-    const bf16_t* base;
-    int ld;
-    if (PROJ && s >= SF) {
-      const int pj = s - SF, nc = pj / K1, r = pj - nc * K1;
-      base = a.wp + (long long)nc * TROWS * D + r * BK;
-      ld = D;
-    } else {
-      const bool sb = CHAIN && s >= S;  // block B
-      const int sl = sb ? s - S : s;
-      const int c = sl / SPC, r = sl - c * SPC;
-      const bool p1 = r < K1;
-      const bf16_t* w1 = sb ? a.w1b : a.w1;
-      const bf16_t* w2 = sb ? a.w2b : a.w2;
-      base = p1 ? w1 + (long long)c * HC * D + r * BK : w2 + c * HC + (r - K1) * BK;
-      ld = p1 ? D : a.H;
-    }
-    bf16_t* dst = ring + slot * TROWS * BK;
-    // the lane's source offsets are recomputed per issue from an opaque lane
-    // id: hoisted, they would hold 2 x GL 64-bit addresses through the launch
-    int ln;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-#ifdef SBK_PROBE_CONTIG
-    // probe (wrong results, timing only): tile t of a matrix read as the
-    // contiguous 32 KB block t, inside the same allocation
-    {
-      const bf16_t* mat;
-      int ti;
-      if (PROJ && s >= SF) {
-        mat = a.wp;
-        ti = s - SF;
-      } else {
-        const bool sb = CHAIN && s >= S;
-        const int sl = sb ? s - S : s;
-        const int c = sl / SPC, r = sl - c * SPC;
-        mat = r < K1 ? (sb ? a.w1b : a.w1) : (sb ? a.w2b : a.w2);
-        ti = r < K1 ? c * K1 + r : c * K2 + r - K1;
-      }
-      base = mat + (long long)ti * TROWS * BK;
-      ld = BK;
-    }
-#endif
-#pragma unroll
-    for (int i = 0; i < GL; ++i) {
-      const int r0 = w * (T * 16) + i * 8;  // the wave's own rows: it is their only reader
-      const int row = r0 + (ln >> 3);
-      const bf16_t* src = base + (row * ld + (((ln & 7) ^ ((row >> 1) & 7)) << 3));
+    // tile s of the image: wave w's 4 KB (its 32 rows, lane-linear) by GL
+    // pieces of 1 KB from one base address and immediate offsets, which the
+    // instruction applies to the global and the LDS address alike (one m0
+    // per tile; the per-piece address arithmetic and tile-index logic of a
+    // strided source cost ~100 scalar and vector instructions per step)
+    const bf16_t* src = a.img + (long long)s * (TROWS * BK) + w * (GL * 512) + lane * 8;
+    bf16_t* dst = ring + slot * (TROWS * BK) + w * (GL * 512);
+    const auto gs = (const __attribute__((address_space(1))) void*)src;
+    const auto ls = (__attribute__((address_space(3))) void*)dst;
+    static_assert(GL == 4, "four 1-KB pieces per wave and tile");
 #ifndef SBK_PROBE_NODMA
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(dst + r0 * BK), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(gs, ls, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(gs, ls, 16, 1024, 0);
+    __builtin_amdgcn_global_load_lds(gs, ls, 16, 2048, 0);
+    __builtin_amdgcn_global_load_lds(gs, ls, 16, 3072, 0);
 #endif
-    }
   };
   issue(0, 0);
   issue(1, 1);
@@ -485,6 +453,73 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   lds_barrier();
   bf16x8 xa[K1][BK / 32][MT];
   load_frags<K1, BK / 32, MT, XS, BK>(xa, Xn, fr, fk);
+  // one K-step: tile s landed -> this wave's fragments (phase 1: the held Xn
+  // fragments of k-step r; phase 2: the hidden chunk Hc at k-step r) -> the
+  // slot takes tile s+NB -> 12 MFMAs into acc1 / acc2
+  auto step = [&](int s, int r, bool ph2, const bf16_t* Hc, bool bar, auto&& post) __attribute__((always_inline)) {
+    // this wave's rows of tile s landed (tile s+1 stays in flight)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL * (NB - 1)) : "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (bar) __builtin_amdgcn_s_barrier();
+    if (s < 96) FFN_TL(2 + 2 * s);
+    const bf16_t* tile = ring + (s % NB) * TROWS * BK;
+    bf16x8 fw[BK / 32][T], fa[BK / 32][MT];
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const int row = w * (T * 16) + t * 16 + fr;
+        fw[ks][t] = ld8(tile + row * BK + (((ks * 4 + g) ^ ((row >> 1) & 7)) << 3));
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        fa[ks][mt] = ph2 ? ld8(Hc + (mt * 16 + fr) * HS + r * BK + ks * 32 + fk) : xa[ph2 ? 0 : r][ks][mt];
+    }
+    // once this step's fragments are in VGPRs its slot takes tile s+2 (tail:
+    // the projection's first tiles, or a harmless reload of the last tile)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    issue(min(s + NB, ST - 1), s % NB);
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks)
+#pragma unroll
+      for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          if (ph2)
+            acc2[t][mt] = FFN_MFMA(fw[ks][t], fa[ks][mt], acc2[t][mt]);
+          else
+            acc1[t][mt] = FFN_MFMA(fw[ks][t], fa[ks][mt], acc1[t][mt]);
+        }
+    post();  // VALU work that rides under this step's MFMAs (after its DMA issue)
+    if (s < 96) FFN_TL(3 + 2 * s);
+  };
+  auto none = []() __attribute__((always_inline)) {};
+  // hidden tiles i = t*MT + mt in [i0, i1) of acc1 -> +b1, act -> Hn (4
+  // consecutive units per lane, one 8-B store); acc1 tiles zeroed.  b1 and Hn
+  // by explicit ds_read / ds_write: compiler-visible LDS accesses here get an
+  // s_waitcnt vmcnt(0) (alias guard against the in-flight LDS-DMA tiles),
+  // draining the weight stream
+  auto act_tiles = [&](int i0, int i1, const float* b1c, bf16_t* Hn) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      if ((t + 1) * MT <= i0 || t * MT >= i1) continue;
+      const int n = w * (T * 16) + t * 16 + 4 * g;
+      f32x4 bb;
+      asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(bb) : "v"(lds_addr(b1c + n)) : "memory");
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int i = t * MT + mt;
+        if (i < i0 || i >= i1) continue;
+        const f32x4 v = acc1[t][mt];
+        uint2 pk;
+        pk.x = pack_bf16x2(act_fn<ACT>(v[0] + bb[0], a.slope), act_fn<ACT>(v[1] + bb[1], a.slope));
+        pk.y = pack_bf16x2(act_fn<ACT>(v[2] + bb[2], a.slope), act_fn<ACT>(v[3] + bb[3], a.slope));
+        const unsigned long long pv = (unsigned long long)pk.x | ((unsigned long long)pk.y << 32);
+        asm volatile("ds_write_b64 %0, %1" ::"v"(lds_addr(Hn + (mt * 16 + fr) * HS + n)), "v"(pv) : "memory");
+        acc1[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
   for (int stage = 0; stage < (CHAIN ? 2 : 1); ++stage) {
   if (CHAIN && stage == 1) {
     FFN_TL(197);
@@ -533,81 +568,46 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     load_frags<K1, BK / 32, MT, XS, BK>(xa, Xn, fr, fk);
     FFN_TL(198);
   }
-  for (int c = 0; c < NCH; ++c)
+  const float* b1st = b1s + stage * a.H;  // this block's b1 (LDS)
+#ifdef FFN_ACTPIPE
+  // probe: phase 1 of chunk 0, then per chunk c: phase 1 of chunk c+1 (acc1),
+  // then phase 2 of chunk c (acc2) with chunk c+1's activation issued after
+  // each step's DMA and MFMAs (image in the matching order)
+  int s = stage * S;
 #pragma unroll
-  for (int r = 0; r < SPC; ++r) {
-    const int s = stage * S + c * SPC + r;
-    // this wave's rows of tile s landed (tile s+1 stays in flight)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL * (NB - 1)) : "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (r == K1) __builtin_amdgcn_s_barrier();
-    if (s < 96) FFN_TL(2 + 2 * s);
-    const bf16_t* tile = ring + (s % NB) * TROWS * BK;
-    bf16_t* Hc = Hs + (c & 1) * BM * HS;  // this chunk's hidden activations
-    bf16x8 fw[BK / 32][T], fa[BK / 32][MT];
+  for (int r = 0; r < K1; ++r) step(s + r, r, false, nullptr, false, none);
+  s += K1;
+  act_tiles(0, T * MT, b1st, Hs);
+  for (int c = 0; c < NCH; ++c) {
+    const bool more = c + 1 < NCH;
+    if (more) {
 #pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-#pragma unroll
-      for (int t = 0; t < T; ++t) {
-        const int row = w * (T * 16) + t * 16 + fr;
-        fw[ks][t] = ld8(tile + row * BK + (((ks * 4 + g) ^ ((row >> 1) & 7)) << 3));
-      }
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-        fa[ks][mt] = r < K1 ? xa[r < K1 ? r : 0][ks][mt] : ld8(Hc + (mt * 16 + fr) * HS + (r - K1) * BK + ks * 32 + fk);
+      for (int r = 0; r < K1; ++r) step(s + r, r, false, nullptr, false, none);
+      s += K1;
     }
-    // once this step's fragments are in VGPRs its slot takes tile s+2 (tail:
-    // the projection's first tiles, or a harmless reload of the last tile)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    issue(min(s + NB, ST - 1), s % NB);
-    if (r < K1) {
+    const bf16_t* Hc = Hs + (c & 1) * BM * HS;
+    bf16_t* Hn = Hs + ((c + 1) & 1) * BM * HS;
 #pragma unroll
-      for (int ks = 0; ks < BK / 32; ++ks)
-#pragma unroll
-        for (int t = 0; t < T; ++t)
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-            acc1[t][mt] = FFN_MFMA(fw[ks][t], fa[ks][mt], acc1[t][mt]);
-      if (r == K1 - 1) {
-        // hidden chunk -> +b1, act -> Hc (4 consecutive units per lane, one
-        // 8-B store); phase 2 reads it after the next step's barrier.  The
-        // buffer written here was last read in chunk c-2, before every wave
-        // passed chunk c-1's r == K1 barrier.
-#pragma unroll
-        for (int t = 0; t < T; ++t) {
-          const int n = w * (T * 16) + t * 16 + 4 * g;
-          // b1 and Hs by explicit ds_read / ds_write: compiler-visible LDS
-          // accesses here get an s_waitcnt vmcnt(0) (alias guard against the
-          // in-flight LDS-DMA tiles), draining the weight stream
-          f32x4 bb;
-          {
-            const uint32_t la = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)(b1s + stage * a.H + c * HC + n));
-            asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(bb) : "v"(la) : "memory");
-          }
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            const f32x4 v = acc1[t][mt];
-            uint2 pk;
-            pk.x = pack_bf16x2(act_fn<ACT>(v[0] + bb[0], a.slope), act_fn<ACT>(v[1] + bb[1], a.slope));
-            pk.y = pack_bf16x2(act_fn<ACT>(v[2] + bb[2], a.slope), act_fn<ACT>(v[3] + bb[3], a.slope));
-            const uint32_t la = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) bf16_t*)(Hc + (mt * 16 + fr) * HS + n));
-            const unsigned long long pv = (unsigned long long)pk.x | ((unsigned long long)pk.y << 32);
-            asm volatile("ds_write_b64 %0, %1" ::"v"(la), "v"(pv) : "memory");
-            acc1[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-          }
-        }
-      }
-    } else {
-#pragma unroll
-      for (int ks = 0; ks < BK / 32; ++ks)
-#pragma unroll
-        for (int t = 0; t < T; ++t)
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-            acc2[t][mt] = FFN_MFMA(fw[ks][t], fa[ks][mt], acc2[t][mt]);
-    }
-    if (s < 96) FFN_TL(3 + 2 * s);
+    for (int p = 0; p < K2; ++p)
+      step(s + p, p, true, Hc, p == 0, [&]() __attribute__((always_inline)) {
+        if (more) act_tiles(p * T * MT / K2, (p + 1) * T * MT / K2, b1st + (c + 1) * HC, Hn);
+      });
+    s += K2;
   }
+#else
+  for (int c = 0; c < NCH; ++c) {
+    const int s0 = stage * S + c * SPC;
+#pragma unroll
+    for (int r = 0; r < K1; ++r) step(s0 + r, r, false, nullptr, false, none);
+    // hidden chunk -> +b1, act -> Hc; phase 2 reads it after the next step's
+    // barrier.  The buffer written here was last read in chunk c-2, before
+    // every wave passed chunk c-1's first phase-2 barrier.
+    bf16_t* Hc = Hs + (c & 1) * BM * HS;
+    act_tiles(0, T * MT, b1st + c * HC, Hc);
+#pragma unroll
+    for (int p = 0; p < K2; ++p) step(s0 + K1 + p, p, true, Hc, p == 0, none);
+  }
+#endif
   }  // stage
   if (!PROJ) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the tail reloads
   FFN_TL(194);
@@ -812,10 +812,10 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
 
 template <int D>
 size_t ffn_lds(int H, bool chain) {
-  // 2-slot weight ring, Xn, two hidden-chunk buffers, b1 (two with CHAIN), the row-reduction scratch,
-  // the epilogue parameter rows
+  // 2-slot weight ring, Xn, two hidden-chunk buffers, b1 (two with CHAIN), the row-reduction scratch
+  // (two buffers), the epilogue parameter rows
   return ((size_t)2 * 256 * 64 + (size_t)FFN_BM * (D + 16) + (size_t)2 * FFN_BM * (256 + 16)) * sizeof(bf16_t) +
-         (size_t)(chain ? 2 : 1) * H * 4 + (size_t)FFN_NW * FFN_BM * 4 + (size_t)FFN_NW * D * 4;
+         (size_t)(chain ? 2 : 1) * H * 4 + (size_t)2 * FFN_NW * FFN_BM * 4 + (size_t)FFN_NW * D * 4;
 }
 
 template <int D, int ACT, bool PROJ, bool CHAIN>
@@ -845,9 +845,70 @@ int launch_ffn(const FfnArgs& a, hipStream_t s) {
 }
 
 int ffn_dispatch(const FfnArgs& a, hipStream_t s) {
-  const bool proj = a.wp != nullptr, chain = a.w1b != nullptr;
+  const bool proj = a.np > 0, chain = a.g0b != nullptr;
   if (chain) return proj ? launch_ffn<256, true, true>(a, s) : launch_ffn<256, false, true>(a, s);
   return proj ? launch_ffn<256, true, false>(a, s) : launch_ffn<256, false, false>(a, s);
+}
+
+// ---- the weight-stream image.  Tile s (256 rows x 64 k, 32 KB) in the order
+// ffn_kernel streams them: per FFN block (A, then B for a chain) and hidden
+// chunk c of 256 units: K1 = D / 64 tiles of W1 rows c*256.. (k over D), then
+// 4 tiles of W2 (all D rows, k over the chunk's units); then the projection:
+// per 256 output columns nc, K1 tiles of Wp rows nc*256.. .  Row r of a tile
+// holds its 8 chunks of 8 k in the order j' -> source chunk j' ^ ((r >> 1) & 7)
+// (the ring's bank swizzle, applied here once instead of on every load).
+struct ImgSrc {
+  const bf16_t *w1, *w2, *w1b, *w2b, *wp;
+  int D, H, ntile_blk, ntile_ffn, chain;
+};
+
+__device__ __forceinline__ void img_tile_src(const ImgSrc& q, int s, const bf16_t** mat, int* ld, int* row0,
+                                             int* k0) {
+  const int K1 = q.D / 64, SPC = K1 + 4;
+  if (s >= q.ntile_ffn) {  // projection
+    const int pj = s - q.ntile_ffn, nc = pj / K1, r = pj - nc * K1;
+    *mat = q.wp; *ld = q.D; *row0 = nc * 256; *k0 = r * 64;
+    return;
+  }
+  const bool sb = s >= q.ntile_blk;
+#ifdef FFN_ACTPIPE
+  const int sl = sb ? s - q.ntile_blk : s, nch = q.H / 256;
+  int c, r;
+  bool w1t;
+  if (sl < K1) {
+    w1t = true; c = 0; r = sl;
+  } else {
+    const int qq = sl - K1, seg = qq / SPC, p = qq - seg * SPC;
+    w1t = seg + 1 < nch && p < K1;
+    c = w1t ? seg + 1 : seg;
+    r = w1t ? p : (seg + 1 < nch ? p - K1 : p) + K1;
+  }
+#else
+  const int sl = sb ? s - q.ntile_blk : s, c = sl / SPC, r = sl - c * SPC;
+#endif
+  if (r < K1) {
+    *mat = sb ? q.w1b : q.w1; *ld = q.D; *row0 = c * 256; *k0 = r * 64;
+  } else {
+    *mat = sb ? q.w2b : q.w2; *ld = q.H; *row0 = 0; *k0 = c * 256 + (r - K1) * 64;
+  }
+}
+
+__global__ void __launch_bounds__(256) ffn_image_kernel(ImgSrc q, int ntile, bf16_t* __restrict__ img) {
+  const long long n = (long long)ntile * 256 * 8;  // 16-B chunks
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int s = (int)(i >> 11), rem = (int)(i & 2047), r = rem >> 3, jp = rem & 7;
+    const bf16_t* mat;
+    int ld, row0, k0;
+    img_tile_src(q, s, &mat, &ld, &row0, &k0);
+    const int j = jp ^ ((r >> 1) & 7);
+    *reinterpret_cast<uint4*>(img + i * 8) =
+        *reinterpret_cast<const uint4*>(mat + (long long)(row0 + r) * ld + k0 + 8 * j);
+  }
+}
+
+int ffn_tiles(int D, int H, int np, int chain) {
+  const int per_blk = (H / 256) * (D / 64 + 4);
+  return (chain ? 2 : 1) * per_blk + (np / 256) * (D / 64);
 }
 
 }  // namespace
@@ -856,36 +917,69 @@ SBK_PROBE_EXPORT(sbk_probe_ffn_tl, g_ffn_tl)
 
 SBK_API int sbk_ffn_supported(int D, int H) { return D == 256 && H > 0 && H % 256 == 0 && H <= 2048; }
 
-SBK_API int sbk_ffn_proj(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0,
-                         const void* w1, const float* b1, int act, float slope, const void* w2, const float* b2,
-                         float alpha, const float* gp, const float* bp, float epsp, float* out, const float* gn,
-                         const float* bn, float epsn, void* u, int u_bf16, const void* wp, int np, void* yp,
-                         void* stream) {
-  if (M <= 0 || !sbk_ffn_supported(D, H) || !g0 || !b0 || !w1 || !b1 || !w2 || !b2 || !out) return SBK_ERR_ARG;
-  if (act == ACT_GLU || (gn && !u && !wp)) return SBK_ERR_ARG;
+SBK_API long long sbk_ffn_image_elems(int D, int H, int np, int chain) {
+  if (!sbk_ffn_supported(D, H) || np < 0 || np % 256) return -1;
+  return (long long)ffn_tiles(D, H, np, chain) * 256 * 64;
+}
+
+SBK_API int sbk_ffn_image(const void* w1, const void* w2, const void* w1b, const void* w2b, const void* wp, int D,
+                          int H, int np, void* img, void* stream) {
+  const int chain = w1b != nullptr;
+  if (!sbk_ffn_supported(D, H) || !w1 || !w2 || !img || (chain && !w2b) || np < 0 || np % 256 || (np > 0) != (wp != nullptr))
+    return SBK_ERR_ARG;
+  if ((reinterpret_cast<uintptr_t>(w1) | reinterpret_cast<uintptr_t>(w2) | reinterpret_cast<uintptr_t>(w1b) |
+       reinterpret_cast<uintptr_t>(w2b) | reinterpret_cast<uintptr_t>(wp) | reinterpret_cast<uintptr_t>(img)) & 15)
+    return SBK_ERR_ARG;
+  ImgSrc q;
+  q.w1 = reinterpret_cast<const bf16_t*>(w1); q.w2 = reinterpret_cast<const bf16_t*>(w2);
+  q.w1b = reinterpret_cast<const bf16_t*>(w1b); q.w2b = reinterpret_cast<const bf16_t*>(w2b);
+  q.wp = reinterpret_cast<const bf16_t*>(wp);
+  q.D = D; q.H = H; q.chain = chain;
+  q.ntile_blk = (H / 256) * (D / 64 + 4);
+  q.ntile_ffn = (chain ? 2 : 1) * q.ntile_blk;
+  const int nt = ffn_tiles(D, H, np, chain);
+  const long long chunks = (long long)nt * 2048;
+  hipLaunchKernelGGL(ffn_image_kernel, dim3((unsigned)std::min<long long>((chunks + 255) / 256, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, q, nt, reinterpret_cast<bf16_t*>(img));
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+namespace {
+int ffn_check(const float* x, int M, int D, int H, const float* g0, const float* b0, const void* img,
+              const float* b1, int act, const float* b2, const float* gp, const float* bp, float* out,
+              const float* gn, const float* bn, void* u, int np, void* yp) {
+  if (M <= 0 || !sbk_ffn_supported(D, H) || !g0 || !b0 || !img || !b1 || !b2 || !out) return SBK_ERR_ARG;
+  if (act == ACT_GLU || act < 0 || act > ACT_GELU || (gn && !u && np == 0)) return SBK_ERR_ARG;
   // projection tail: y = next-LN(out) . Wp^T, whole 256-column blocks; it
   // replaces the u output
-  if (wp && (!gn || !bn || u || !yp || np <= 0 || np % 256)) return SBK_ERR_ARG;
-  // float4 loads of rows and LayerNorm parameters
+  if (np < 0 || np % 256 || (np > 0 && (!gn || !bn || u || !yp))) return SBK_ERR_ARG;
+  // float4 loads of rows and LayerNorm parameters, 16-B image pieces
   const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(g0) |
                        reinterpret_cast<uintptr_t>(b0) | reinterpret_cast<uintptr_t>(b1) |
                        reinterpret_cast<uintptr_t>(b2) | reinterpret_cast<uintptr_t>(gp) |
                        reinterpret_cast<uintptr_t>(bp) | reinterpret_cast<uintptr_t>(out) |
                        reinterpret_cast<uintptr_t>(gn) | reinterpret_cast<uintptr_t>(bn) |
-                       reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(w1) | reinterpret_cast<uintptr_t>(w2) |
-                       reinterpret_cast<uintptr_t>(wp) | reinterpret_cast<uintptr_t>(yp);
-  if (al & 15) return SBK_ERR_ARG;
+                       reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(img) | reinterpret_cast<uintptr_t>(yp);
+  return (al & 15) ? SBK_ERR_ARG : 0;
+}
+}  // namespace
+
+SBK_API int sbk_ffn_proj(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0,
+                         const void* img, const float* b1, int act, float slope, const float* b2, float alpha,
+                         const float* gp, const float* bp, float epsp, float* out, const float* gn, const float* bn,
+                         float epsn, void* u, int u_bf16, int np, void* yp, void* stream) {
+  if (ffn_check(x, M, D, H, g0, b0, img, b1, act, b2, gp, bp, out, gn, bn, u, np, yp)) return SBK_ERR_ARG;
   FfnArgs a;
   a.x = x; a.M = M; a.H = H;
   a.g0 = g0; a.b0 = b0; a.eps0 = eps0;
-  a.w1 = reinterpret_cast<const bf16_t*>(w1); a.b1 = b1; a.act = act; a.slope = slope;
-  a.w2 = reinterpret_cast<const bf16_t*>(w2); a.b2 = b2; a.alpha = alpha;
+  a.img = reinterpret_cast<const bf16_t*>(img); a.b1 = b1; a.act = act; a.slope = slope;
+  a.b2 = b2; a.alpha = alpha;
   a.gp = gp; a.bp = bp; a.epsp = epsp;
   a.out = out;
   a.gn = gn; a.bn = bn; a.epsn = epsn; a.u = u; a.u_bf16 = u_bf16;
-  a.wp = reinterpret_cast<const bf16_t*>(wp); a.np = np; a.yp = reinterpret_cast<bf16_t*>(yp);
-  a.g0b = nullptr; a.b0b = nullptr; a.eps0b = 0.f; a.w1b = nullptr; a.w2b = nullptr; a.b1b = nullptr;
-  a.b2b = nullptr; a.alphab = 0.f;
+  a.np = np; a.yp = reinterpret_cast<bf16_t*>(yp);
+  a.g0b = nullptr; a.b0b = nullptr; a.eps0b = 0.f; a.b1b = nullptr; a.b2b = nullptr; a.alphab = 0.f;
   const int rc = ffn_dispatch(a, (hipStream_t)stream);
   if (rc) return rc;
   SBK_CHECK_LAUNCH();
@@ -896,39 +990,27 @@ SBK_API int sbk_ffn_proj(const float* x, int M, int D, int H, const float* g0, c
 // output, which never leaves the CU): block A (g0 .. gp: e.g. FFN2 + norm2 of
 // Conformer layer i) then block B (g0b .. alphab: FFN1 of layer i+1, no
 // post-LN), then next-LN / projection tail as sbk_ffn_proj.  out receives
-// block B's output only.
+// block B's output only.  img: sbk_ffn_image of (w1, w2, w1b, w2b, wp).
 SBK_API int sbk_ffn_chain(const float* x, int M, int D, int H, int act, float slope, const float* g0, const float* b0,
-                          float eps0, const void* w1, const float* b1, const void* w2, const float* b2, float alpha,
-                          const float* gp, const float* bp, float epsp, const float* g0b, const float* b0b,
-                          float eps0b, const void* w1b, const float* b1b, const void* w2b, const float* b2b,
-                          float alphab, float* out, const float* gn, const float* bn, float epsn, void* u,
-                          int u_bf16, const void* wp, int np, void* yp, void* stream) {
-  if (!g0b || !b0b || !w1b || !b1b || !w2b || !b2b) return SBK_ERR_ARG;
-  if ((reinterpret_cast<uintptr_t>(g0b) | reinterpret_cast<uintptr_t>(b0b) | reinterpret_cast<uintptr_t>(w1b) |
-       reinterpret_cast<uintptr_t>(b1b) | reinterpret_cast<uintptr_t>(w2b) | reinterpret_cast<uintptr_t>(b2b)) & 15)
+                          float eps0, const float* b1, const float* b2, float alpha, const float* gp, const float* bp,
+                          float epsp, const float* g0b, const float* b0b, float eps0b, const float* b1b,
+                          const float* b2b, float alphab, float* out, const float* gn, const float* bn, float epsn,
+                          void* u, int u_bf16, const void* img, int np, void* yp, void* stream) {
+  if (!g0b || !b0b || !b1b || !b2b) return SBK_ERR_ARG;
+  if ((reinterpret_cast<uintptr_t>(g0b) | reinterpret_cast<uintptr_t>(b0b) | reinterpret_cast<uintptr_t>(b1b) |
+       reinterpret_cast<uintptr_t>(b2b)) & 15)
     return SBK_ERR_ARG;
-  if (M <= 0 || !sbk_ffn_supported(D, H) || !g0 || !b0 || !w1 || !b1 || !w2 || !b2 || !out) return SBK_ERR_ARG;
-  if (act == ACT_GLU || (gn && !u && !wp)) return SBK_ERR_ARG;
-  if (wp && (!gn || !bn || u || !yp || np <= 0 || np % 256)) return SBK_ERR_ARG;
-  const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(g0) |
-                       reinterpret_cast<uintptr_t>(b0) | reinterpret_cast<uintptr_t>(b1) |
-                       reinterpret_cast<uintptr_t>(b2) | reinterpret_cast<uintptr_t>(gp) |
-                       reinterpret_cast<uintptr_t>(bp) | reinterpret_cast<uintptr_t>(out) |
-                       reinterpret_cast<uintptr_t>(gn) | reinterpret_cast<uintptr_t>(bn) |
-                       reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(w1) | reinterpret_cast<uintptr_t>(w2) |
-                       reinterpret_cast<uintptr_t>(wp) | reinterpret_cast<uintptr_t>(yp);
-  if (al & 15) return SBK_ERR_ARG;
+  if (ffn_check(x, M, D, H, g0, b0, img, b1, act, b2, gp, bp, out, gn, bn, u, np, yp)) return SBK_ERR_ARG;
   FfnArgs a;
   a.x = x; a.M = M; a.H = H;
   a.g0 = g0; a.b0 = b0; a.eps0 = eps0;
-  a.w1 = reinterpret_cast<const bf16_t*>(w1); a.b1 = b1; a.act = act; a.slope = slope;
-  a.w2 = reinterpret_cast<const bf16_t*>(w2); a.b2 = b2; a.alpha = alpha;
+  a.img = reinterpret_cast<const bf16_t*>(img); a.b1 = b1; a.act = act; a.slope = slope;
+  a.b2 = b2; a.alpha = alpha;
   a.gp = gp; a.bp = bp; a.epsp = epsp;
   a.out = out;
   a.gn = gn; a.bn = bn; a.epsn = epsn; a.u = u; a.u_bf16 = u_bf16;
-  a.wp = reinterpret_cast<const bf16_t*>(wp); a.np = np; a.yp = reinterpret_cast<bf16_t*>(yp);
+  a.np = np; a.yp = reinterpret_cast<bf16_t*>(yp);
   a.g0b = g0b; a.b0b = b0b; a.eps0b = eps0b;
-  a.w1b = reinterpret_cast<const bf16_t*>(w1b); a.w2b = reinterpret_cast<const bf16_t*>(w2b);
   a.b1b = b1b; a.b2b = b2b; a.alphab = alphab;
   const int rc = ffn_dispatch(a, (hipStream_t)stream);
   if (rc) return rc;
@@ -937,9 +1019,9 @@ SBK_API int sbk_ffn_chain(const float* x, int M, int D, int H, int act, float sl
 }
 
 SBK_API int sbk_ffn(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0,
-                    const void* w1, const float* b1, int act, float slope, const void* w2, const float* b2,
-                    float alpha, const float* gp, const float* bp, float epsp, float* out, const float* gn,
-                    const float* bn, float epsn, void* u, int u_bf16, void* stream) {
-  return sbk_ffn_proj(x, M, D, H, g0, b0, eps0, w1, b1, act, slope, w2, b2, alpha, gp, bp, epsp, out, gn, bn, epsn,
-                      u, u_bf16, nullptr, 0, nullptr, stream);
+                    const void* img, const float* b1, int act, float slope, const float* b2, float alpha,
+                    const float* gp, const float* bp, float epsp, float* out, const float* gn, const float* bn,
+                    float epsn, void* u, int u_bf16, void* stream) {
+  return sbk_ffn_proj(x, M, D, H, g0, b0, eps0, img, b1, act, slope, b2, alpha, gp, bp, epsp, out, gn, bn, epsn, u,
+                      u_bf16, 0, nullptr, stream);
 }

@@ -26,11 +26,11 @@ def specaugment_(x: torch.Tensor, N: int, T: int, F: int, c: int, w: int, fm: Op
     bilinear) and freq / time masks
     (fm, tm: (N, n, 2) int32 [len, pos]) to x (N, T, F) fp32 in place, with
     the batch-mean fill when use_mean (augment.py:116-201)."""
+    n_f = fm.shape[1] if fm is not None else 0
+    n_t = tm.shape[1] if tm is not None else 0
     tmp = torch.empty_like(x) if c >= 0 else None
     # partial sums (+ the two fills of the 4-wide path at the end)
     partial = torch.empty(2 * N * ((T + 3) // 4) + 4, device=x.device, dtype=torch.float32) if use_mean else None
-    n_f = fm.shape[1] if fm is not None else 0
-    n_t = tm.shape[1] if tm is not None else 0
     rc = lib().sbk_specaugment(ptr(x), N, T, F, c, w, int(warp_mode), ptr(tmp), ptr(fm), n_f, ptr(tm), n_t,
                                int(use_mean),
                                ptr(partial), n_fcells, stream_of(x))
@@ -40,22 +40,6 @@ def specaugment_(x: torch.Tensor, N: int, T: int, F: int, c: int, w: int, fm: Op
 @specaugment_.register_fake
 def _(x, N, T, F, c, w, fm, tm, use_mean, n_fcells, warp_mode=0):
     return None
-
-
-def _masked_cells(fm, F):
-    """Number of (sequence, frequency) cells covered by a frequency mask —
-    pos <= f < pos + len, the kernels' test — from the host draws (N, n, 2)
-    [len, pos], by interval union (the second running mean's cell count)."""
-    total = 0
-    for row in fm.tolist():
-        iv = sorted((max(ps, 0), min(ps + ln, F)) for ln, ps in row)
-        end = 0
-        for a, b in iv:
-            a = max(a, end)
-            if b > a:
-                total += b - a
-                end = b
-    return total
 
 
 class SpecAugment(torch.nn.Module):
@@ -85,6 +69,23 @@ class SpecAugment(torch.nn.Module):
         self.n_time_mask = n_time_mask
         self.replace_with_zero = replace_with_zero
         self.last_draws = None
+        self._pin = None     # pinned staging of the mask draws (reused; see _upload)
+        self._pin_ev = None  # completion of the last upload out of it
+
+    def _upload(self, host, device):
+        """int32 host draws -> device, asynchronously from a reused pinned
+        buffer (a pageable copy would block the host for the transfer)."""
+        n = host.numel()
+        if self._pin is None or self._pin.numel() < n:
+            self._pin = torch.empty(max(n, 1024), dtype=torch.int32).pin_memory()
+            self._pin_ev = None
+        if self._pin_ev is not None:
+            self._pin_ev.synchronize()  # the previous copy out of the buffer is done
+        self._pin[:n].copy_(host)
+        dev = self._pin[:n].to(device, non_blocking=True)
+        self._pin_ev = torch.cuda.Event()
+        self._pin_ev.record(torch.cuda.current_stream(device))
+        return dev
 
     def draws(self, N, T, F):
         """Host draws in the reference order (augment.py:131-133, :175-186)."""
@@ -120,16 +121,17 @@ class SpecAugment(torch.nn.Module):
         if c == w:
             c = w = -1  # identical segment sizes: the resize is the identity
         self.last_draws = (c, w, fm, tm)
-        # both mask tables in one host -> device copy (the per-step host work
-        # is this module's cost at config 2, not its kernels)
+        # both mask tables in one asynchronous pinned host -> device copy (the
+        # per-step host work is this module's cost at config 2, not its
+        # kernels); the second mean's masked-cell count is taken on the
+        # device from the table (n_fcells = -1)
         parts = [m.reshape(-1) for m in (fm, tm) if m is not None]
         fm_d = tm_d = None
         if parts:
-            buf = (torch.cat(parts) if len(parts) > 1 else parts[0]).to(x.device, non_blocking=True)
+            buf = self._upload(torch.cat(parts) if len(parts) > 1 else parts[0], x.device)
             nf = fm.numel() if fm is not None else 0
             fm_d = buf[:nf].view(fm.shape) if fm is not None else None
             tm_d = buf[nf:].view(tm.shape) if tm is not None else None
-        n_fcells = _masked_cells(fm, F) * T if fm is not None else 0
-        torch.ops.sbk.specaugment_(x, N, T, F, c, w, fm_d, tm_d, not self.replace_with_zero, n_fcells,
+        torch.ops.sbk.specaugment_(x, N, T, F, c, w, fm_d, tm_d, not self.replace_with_zero, -1,
                                    _WARP_MODES.get(self.time_warp_mode, 0))
         return x

@@ -91,3 +91,27 @@ def test_specaugment_4d_and_short(dev):
     torch.manual_seed(6)
     ref = OA.spec_augment(x.clone(), freq_mask_width=(0, 5), time_mask_width=(0, 3))
     assert_close(y, ref, rtol=1e-5, name="short")
+
+
+@pytest.mark.parametrize("N,T,F,win,zero", [
+    (32, 1501, 240, 5, False),   # config 2 (Δ/ΔΔ features), the float4 kernels
+    (3, 200, 240, 5, True),      # zero fill
+    (2, 300, 80, 40, False),     # a wide warp window
+    (2, 120, 42, 5, False),      # F % 4 != 0: the scalar kernels
+])
+def test_specaugment_paths_vs_oracle(dev, N, T, F, win, zero):
+    """The float4 and scalar routes of sbk_specaugment, with the second mean's
+    masked-cell count taken on the device from the mask table, against the
+    oracle."""
+    from speechbrain_amd.lobes.augment import SpecAugment
+    x = torch.randn(N, T, F, generator=torch.Generator().manual_seed(T + F)) * 10 - 40
+    kw = dict(time_warp=True, time_warp_window=win, freq_mask=True, n_freq_mask=2, time_mask=True, n_time_mask=2,
+              replace_with_zero=zero, freq_mask_width=min(30, F // 2), time_mask_width=40)
+    for seed in (11, 12):
+        torch.manual_seed(seed)
+        y = SpecAugment(**kw)(x.clone().to(dev))
+        torch.manual_seed(seed)
+        ref = OA.spec_augment(x.clone(), time_warp_on=True, time_warp_window=win, freq_mask=True, n_freq_mask=2,
+                              time_mask=True, n_time_mask=2, replace_with_zero=zero,
+                              freq_mask_width=kw["freq_mask_width"], time_mask_width=40)
+        assert_close(y, ref, rtol=1e-5, name=f"N{N} T{T} F{F} win{win} seed{seed}")

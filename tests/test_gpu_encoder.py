@@ -504,3 +504,37 @@ def test_encoder_chain_vs_per_layer(dev):
         finally:
             C.USE_LAYER_CHAIN = True
     assert_close(y_chain, y_ref, rtol=2e-2, name="chain vs per-layer")
+
+
+def test_ffn_weight_image_layout(dev):
+    """sbk_ffn_image: the fused FFN kernels' weight stream — 32-KB tiles in
+    stream order (per block and 256-unit hidden chunk: D/64 tiles of W1, 4 of
+    W2; then D/64 per 256 projection columns), each row's 16-B chunks in the
+    ring's swizzled order j' -> j' ^ ((row >> 1) & 7) — bit-exact against the
+    same layout built with torch indexing."""
+    from speechbrain_amd import _enc
+    g = torch.Generator().manual_seed(3)
+    D, H, NP = 256, 512, 768
+    ws = [torch.randn(*shp, generator=g).to(torch.bfloat16).to(dev)
+          for shp in ((H, D), (D, H), (H, D), (D, H), (NP, D))]
+    perm = torch.tensor([[jp ^ ((r >> 1) & 7) for jp in range(8)] for r in range(256)])
+
+    def tile(mat, r0, k0):
+        t = mat[r0:r0 + 256, k0:k0 + 64].cpu().reshape(256, 8, 8)
+        return torch.gather(t, 1, perm[:, :, None].expand(256, 8, 8)).reshape(-1)
+
+    def blocks(w1, w2):
+        out = []
+        for c in range(H // 256):
+            out += [tile(w1, c * 256, r * 64) for r in range(D // 64)]
+            out += [tile(w2, 0, c * 256 + r * 64) for r in range(4)]
+        return out
+
+    proj = [tile(ws[4], nc * 256, r * 64) for nc in range(NP // 256) for r in range(D // 64)]
+    single = _enc.ffn_image(ws[0], ws[1])
+    assert torch.equal(single.cpu(), torch.cat(blocks(ws[0], ws[1])))
+    chain = _enc.ffn_image(*ws)
+    assert torch.equal(chain.cpu(), torch.cat(blocks(ws[0], ws[1]) + blocks(ws[2], ws[3]) + proj))
+    assert _enc.ffn_image(*ws) is chain  # cached while no weight changes
+    ws[4].add_(1)  # an in-place update (new version) rebuilds it
+    assert _enc.ffn_image(*ws) is not chain
