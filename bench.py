@@ -66,7 +66,10 @@ def make_step(fbank, cnn, tr, wav, wav_len):
     by the front-end as it loads the rows) → both ConvBlocks in one bf16
     kernel → TransformerASR.encode under bf16 autocast (fused FFN /
     conv-module / LDS-DMA attention kernels).  Also what
-    tests/test_gpu_bench_parity.py runs against the fp32 oracle."""
+    tests/test_gpu_bench_parity.py runs against the fp32 oracle.  (The
+    batch as 2 or 4 utterance groups on concurrent streams in one graph
+    measured no faster in rounds 2 and 4: 1.339 / 1.355 vs 1.333 ms,
+    profiles/r04i_bench_s*.log — the kernels already fill the chip.)"""
     def step():
         with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
             feats, topdb = fbank.forward_deferred(wav)
@@ -397,7 +400,10 @@ def run_c2(args, world, rank, dev):
     it = [0]
 
     def step():
-        torch.manual_seed(1234 + it[0])
+        # the draws come from the CPU generator (the reference's); seeding only
+        # it (torch.manual_seed also seeds every GPU generator: ~57 us of host
+        # time per step, more than a third of the step's kernels)
+        torch.default_generator.manual_seed(1234 + it[0])
         it[0] += 1
         with torch.no_grad():
             return sa(fb(wav))  # Fbank(deltas=True): [fbank | Δ | ΔΔ], the top_db floor applied on load

@@ -8,7 +8,7 @@ from typing import Optional
 
 import torch
 
-from ._lib import SbkError, check, lib, ptr, require_device, stream_of
+from ._lib import OPS, SbkError, check, custom_op, lib, ptr, require_device, stream_of
 
 ACT = {None: 0, "none": 0, "swish": 1, "glu": 2, "leaky_relu": 3, "relu": 3, "gelu": 4}
 _bf16 = torch.bfloat16
@@ -27,7 +27,7 @@ def _is_bf16(t):
 # signatures the modules use.  Optional outputs are returned as 0-element
 # tensors by the ops and mapped back to None by the wrappers.
 # ---------------------------------------------------------------------------
-@torch.library.custom_op("sbk::gemm", mutates_args=())
+@custom_op("sbk::gemm", mutates_args=())
 def _gemm_op(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], act: int, slope: float,
              res: Optional[torch.Tensor], alpha: float, rowmask: Optional[torch.Tensor], out_bf16: bool,
              tile: int) -> torch.Tensor:
@@ -69,11 +69,11 @@ def gemm(a, w, bias=None, act=None, slope=0.0, res=None, alpha=1.0, rowmask=None
         Kp = -(-a.shape[1] // vec) * vec
         a = torch.nn.functional.pad(a, (0, Kp - a.shape[1]))
         w = torch.nn.functional.pad(w, (0, Kp - w.shape[1]))
-    return torch.ops.sbk.gemm(a, w, bias, ACT[act], float(slope), res, float(alpha), rowmask,
+    return OPS.gemm(a, w, bias, ACT[act], float(slope), res, float(alpha), rowmask,
                               out_dtype == _bf16, int(tile))
 
 
-@torch.library.custom_op("sbk::gemm_tn", mutates_args=())
+@custom_op("sbk::gemm_tn", mutates_args=())
 def _gemm_tn_op(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     K, M = a.shape[-2], a.shape[-1]
     N = b.shape[-1]
@@ -114,7 +114,7 @@ def gemm_tn(a, b):
         raise TypeError(f"gemm_tn takes two bf16 or two fp32 operands (got {a.dtype}, {b.dtype})")
     if a.stride(-1) != 1 or b.stride(-1) != 1:
         raise ValueError("gemm_tn operands must be column-contiguous")
-    return torch.ops.sbk.gemm_tn(a, b)
+    return OPS.gemm_tn(a, b)
 
 
 def gemm_tn_into(a, b, out, ldc, sC):
@@ -132,7 +132,7 @@ def gemm_tn_into(a, b, out, ldc, sC):
     return out
 
 
-@torch.library.custom_op("sbk::gemm_batched", mutates_args=())
+@custom_op("sbk::gemm_batched", mutates_args=())
 def _gemm_batched_op(a: torch.Tensor, w: torch.Tensor, out_bf16: bool, M: int, zdiv: int, ldc: int, sC: int,
                      sCo: int, rows: int) -> torch.Tensor:
     Bt, _, K = a.shape
@@ -176,11 +176,11 @@ def gemm_batched(a, w, out_dtype=_f32, M=None, heads=None):
         H = int(heads)
         if Bt % H:
             raise ValueError("gemm_batched: batch not a multiple of heads")
-        return torch.ops.sbk.gemm_batched(a, w, out_dtype == _bf16, M, H, H * N, N, M * H * N, Bt // H * M)
-    return torch.ops.sbk.gemm_batched(a, w, out_dtype == _bf16, M, 0, 0, 0, 0, 0)
+        return OPS.gemm_batched(a, w, out_dtype == _bf16, M, H, H * N, N, M * H * N, Bt // H * M)
+    return OPS.gemm_batched(a, w, out_dtype == _bf16, M, 0, 0, 0, 0, 0)
 
 
-@torch.library.custom_op("sbk::length_mask", mutates_args=())
+@custom_op("sbk::length_mask", mutates_args=())
 def _length_mask_op(rel_len: torch.Tensor, T: int) -> torch.Tensor:
     B = rel_len.shape[0]
     out = torch.empty(B, T, device=rel_len.device, dtype=torch.uint8)
@@ -197,10 +197,10 @@ def length_mask(rel_len, T):
     """(B, T) uint8: t > floor(rel_len[b] * T) — one launch."""
     require_device(rel_len)
     rl = rel_len if (rel_len.dtype == _f32 and rel_len.is_contiguous()) else rel_len.float().contiguous()
-    return torch.ops.sbk.length_mask(rl, int(T))
+    return OPS.length_mask(rl, int(T))
 
 
-@torch.library.custom_op("sbk::gemm_ln", mutates_args=())
+@custom_op("sbk::gemm_ln", mutates_args=())
 def _gemm_ln_op(a: torch.Tensor, w: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float,
                 bias: Optional[torch.Tensor], res: Optional[torch.Tensor], alpha: float,
                 rowmask: Optional[torch.Tensor], u_bf16: bool, tile: int) -> tuple[torch.Tensor, torch.Tensor]:
@@ -233,7 +233,7 @@ def gemm_ln(a, w, ln, bias=None, res=None, alpha=1.0, rowmask=None, out=None, u_
     if res is not None and (res.dtype != _f32 or res.stride(-1) != 1):
         raise ValueError("residual must be fp32, row-contiguous")
     g, b, eps = ln
-    return torch.ops.sbk.gemm_ln(a, w, g, b, float(eps), bias, res, float(alpha), rowmask, u_dtype == _bf16,
+    return OPS.gemm_ln(a, w, g, b, float(eps), bias, res, float(alpha), rowmask, u_dtype == _bf16,
                                  int(tile))
 
 
@@ -246,7 +246,7 @@ def gemm_ln_supported(N):
     return int(N) == 256
 
 
-@torch.library.custom_op("sbk::layernorm", mutates_args=())
+@custom_op("sbk::layernorm", mutates_args=())
 def _layernorm_op(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, eps1: float, out1_mode: int,
                   w2: Optional[torch.Tensor], b2: Optional[torch.Tensor], eps2: float,
                   out2_bf16: bool) -> tuple[torch.Tensor, torch.Tensor]:
@@ -276,7 +276,7 @@ def layernorm(x, w1, b1, eps1, out1_dtype=_f32, w2=None, b2=None, eps2=1e-5, out
     if out1 is not None:
         raise ValueError("layernorm allocates its output (out1= is not supported)")
     mode = 0 if out1_dtype is None else (2 if out1_dtype == _bf16 else 1)
-    y1, y2 = torch.ops.sbk.layernorm(x, w1, b1, float(eps1), mode, w2, b2, float(eps2), out2_dtype == _bf16)
+    y1, y2 = OPS.layernorm(x, w1, b1, float(eps1), mode, w2, b2, float(eps2), out2_dtype == _bf16)
     return (y1 if mode else None), (y2 if w2 is not None else None)
 
 
@@ -326,7 +326,7 @@ def ffn_image(w1, w2, w1b=None, w2b=None, wp=None):
     return _FFN_IMAGES.get((w1, w2, w1b, w2b, wp), 0 if wp is None else wp.shape[0])
 
 
-@torch.library.custom_op("sbk::ffn", mutates_args=())
+@custom_op("sbk::ffn", mutates_args=())
 def _ffn_op(x: torch.Tensor, g0: torch.Tensor, b0: torch.Tensor, e0: float, w1: torch.Tensor, b1: torch.Tensor,
             act: int, slope: float, w2: torch.Tensor, b2: torch.Tensor, alpha: float, gp: Optional[torch.Tensor],
             bp: Optional[torch.Tensor], ep: float, gn: Optional[torch.Tensor], bn: Optional[torch.Tensor], en: float,
@@ -349,7 +349,7 @@ def _(x, g0, b0, e0, w1, b1, act, slope, w2, b2, alpha, gp, bp, ep, gn, bn, en, 
             x.new_empty(x.shape, dtype=_bf16 if next_bf16 else _f32) if gn is not None else x.new_empty(0))
 
 
-@torch.library.custom_op("sbk::ffn_proj", mutates_args=())
+@custom_op("sbk::ffn_proj", mutates_args=())
 def _ffn_proj_op(x: torch.Tensor, g0: torch.Tensor, b0: torch.Tensor, e0: float, w1: torch.Tensor,
                  b1: torch.Tensor, act: int, slope: float, w2: torch.Tensor, b2: torch.Tensor, alpha: float,
                  gp: Optional[torch.Tensor], bp: Optional[torch.Tensor], ep: float, gn: torch.Tensor,
@@ -381,11 +381,11 @@ def ffn_proj(x, ln0, w1, b1, act, slope, w2, b2, alpha, next_ln, wp, post_ln=Non
     bias (RelPosMHAXL's in_proj)."""
     require_device(x, w1, w2, wp)
     gp, bp, ep = post_ln if post_ln is not None else (None, None, 0.0)
-    return torch.ops.sbk.ffn_proj(x, ln0[0], ln0[1], float(ln0[2]), w1, b1, ACT[act], float(slope), w2, b2,
+    return OPS.ffn_proj(x, ln0[0], ln0[1], float(ln0[2]), w1, b1, ACT[act], float(slope), w2, b2,
                                   float(alpha), gp, bp, float(ep), next_ln[0], next_ln[1], float(next_ln[2]), wp)
 
 
-@torch.library.custom_op("sbk::ffn_chain", mutates_args=())
+@custom_op("sbk::ffn_chain", mutates_args=())
 def _ffn_chain_op(x: torch.Tensor, act: int, slope: float, g0: torch.Tensor, b0: torch.Tensor, e0: float,
                   w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor, alpha: float,
                   gp: Optional[torch.Tensor], bp: Optional[torch.Tensor], ep: float, g0b: torch.Tensor,
@@ -423,7 +423,7 @@ def ffn_chain(x, a, b, act, slope, next_ln, wp):
         raise ValueError(f"ffn_chain: block shapes differ ({tuple(a[1].shape)}/{tuple(a[3].shape)} vs "
                          f"{tuple(b[1].shape)}/{tuple(b[3].shape)})")
     gp, bp, ep = a[6] if a[6] is not None else (None, None, 0.0)
-    return torch.ops.sbk.ffn_chain(x, ACT[act], float(slope), a[0][0], a[0][1], float(a[0][2]), a[1], a[2], a[3],
+    return OPS.ffn_chain(x, ACT[act], float(slope), a[0][0], a[0][1], float(a[0][2]), a[1], a[2], a[3],
                                    a[4], float(a[5]), gp, bp, float(ep), b[0][0], b[0][1], float(b[0][2]), b[1], b[2],
                                    b[3], b[4], float(b[5]), next_ln[0], next_ln[1], float(next_ln[2]), wp)
 
@@ -437,12 +437,12 @@ def ffn(x, ln0, w1, b1, act, slope, w2, b2, alpha, post_ln=None, next_ln=None, n
     require_device(x, w1, w2)
     gp, bp, ep = post_ln if post_ln is not None else (None, None, 0.0)
     gn, bn, en = next_ln if next_ln is not None else (None, None, 0.0)
-    y, u = torch.ops.sbk.ffn(x, ln0[0], ln0[1], float(ln0[2]), w1, b1, ACT[act], float(slope), w2, b2, float(alpha),
+    y, u = OPS.ffn(x, ln0[0], ln0[1], float(ln0[2]), w1, b1, ACT[act], float(slope), w2, b2, float(alpha),
                              gp, bp, float(ep), gn, bn, float(en), next_dtype == _bf16)
     return y, (u if next_ln is not None else None)
 
 
-@torch.library.custom_op("sbk::dwconv_ln_swish", mutates_args=())
+@custom_op("sbk::dwconv_ln_swish", mutates_args=())
 def _dwconv_op(x: torch.Tensor, B: int, T: int, w: torch.Tensor, bias: Optional[torch.Tensor], causal: bool,
                ln_w: torch.Tensor, ln_b: torch.Tensor, eps: float, out_bf16: bool) -> torch.Tensor:
     C = x.shape[-1]
@@ -461,7 +461,7 @@ def _(x, B, T, w, bias, causal, ln_w, ln_b, eps, out_bf16):
 
 def dwconv_ln_swish(x, B, T, w, bias, causal, ln_w, ln_b, eps, out_dtype):
     """Depthwise Conv1d over time + LayerNorm(C) + Swish.  x: (B*T, C)."""
-    return torch.ops.sbk.dwconv_ln_swish(x, int(B), int(T), w, bias, bool(causal), ln_w, ln_b, float(eps),
+    return OPS.dwconv_ln_swish(x, int(B), int(T), w, bias, bool(causal), ln_w, ln_b, float(eps),
                                          out_dtype == _bf16)
 
 
@@ -469,7 +469,7 @@ def conv_module_supported(D, K):
     return bool(lib().sbk_conv_module_supported(int(D), int(K)))
 
 
-@torch.library.custom_op("sbk::conv_module", mutates_args=())
+@custom_op("sbk::conv_module", mutates_args=())
 def _conv_module_op(x: torch.Tensor, B: int, T: int, g0: torch.Tensor, b0: torch.Tensor, e0: float,
                     w1p: torch.Tensor, b1p: torch.Tensor, wc: torch.Tensor, bc: Optional[torch.Tensor], causal: bool,
                     g1: torch.Tensor, b1: torch.Tensor, e1: float, w2: torch.Tensor, b2: Optional[torch.Tensor],
@@ -496,11 +496,11 @@ def conv_module(x, B, T, ln0, w1p, b1p, wc, bc, causal, ln1, w2, b2, kpm=None, p
     projection and residual fused in; o (B*T, 256) bf16)."""
     require_device(x, w1p, w2)
     o, wo, bo = pre if pre is not None else (None, None, None)
-    return torch.ops.sbk.conv_module(x, int(B), int(T), ln0[0], ln0[1], float(ln0[2]), w1p, b1p, wc, bc,
+    return OPS.conv_module(x, int(B), int(T), ln0[0], ln0[1], float(ln0[2]), w1p, b1p, wc, bc,
                                      bool(causal), ln1[0], ln1[1], float(ln1[2]), w2, b2, kpm, o, wo, bo)
 
 
-@torch.library.custom_op("sbk::conv_block_c1", mutates_args=())
+@custom_op("sbk::conv_block_c1", mutates_args=())
 def _conv_block_c1_op(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, ln_w: torch.Tensor, ln_b: torch.Tensor,
                       eps: float, slope: float, out_bf16: bool) -> torch.Tensor:
     B, Tin, Fin = x.shape
@@ -522,10 +522,10 @@ def _(x, w, bias, ln_w, ln_b, eps, slope, out_bf16):
 def conv_block_c1(x, w, bias, ln_w, ln_b, eps, slope, out_dtype):
     """ConvBlock with one input channel: x (B, T, F) fp32 → (B, T', F', C)."""
     require_device(x)
-    return torch.ops.sbk.conv_block_c1(x, w, bias, ln_w, ln_b, float(eps), float(slope), out_dtype == _bf16)
+    return OPS.conv_block_c1(x, w, bias, ln_w, ln_b, float(eps), float(slope), out_dtype == _bf16)
 
 
-@torch.library.custom_op("sbk::conv_block_mfma", mutates_args=())
+@custom_op("sbk::conv_block_mfma", mutates_args=())
 def _conv_block_mfma_op(x: torch.Tensor, wperm: torch.Tensor, bias: torch.Tensor, ln_w: torch.Tensor,
                         ln_b: torch.Tensor, eps: float, slope: float, out_bf16: bool) -> torch.Tensor:
     B, Tin, Fin, Cin = x.shape
@@ -550,10 +550,10 @@ def conv_block_mfma(x, wperm, bias, ln_w, ln_b, eps, slope, out_dtype):
     """ConvBlock implicit GEMM: x (B, T, F, Cin) → (B, T', F', Cout);
     wperm: (Cout, 3, 3, Cin) [time, freq] in x.dtype."""
     require_device(x, wperm)
-    return torch.ops.sbk.conv_block_mfma(x, wperm, bias, ln_w, ln_b, float(eps), float(slope), out_dtype == _bf16)
+    return OPS.conv_block_mfma(x, wperm, bias, ln_w, ln_b, float(eps), float(slope), out_dtype == _bf16)
 
 
-@torch.library.custom_op("sbk::conv_frontend2", mutates_args=())
+@custom_op("sbk::conv_frontend2", mutates_args=())
 def _conv_frontend2_op(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, g1: torch.Tensor, be1: torch.Tensor,
                        e1: float, s1: float, wperm2: torch.Tensor, b2: torch.Tensor, g2: torch.Tensor,
                        be2: torch.Tensor, e2: float, s2: float, out_bf16: bool, slot_max: Optional[torch.Tensor],
@@ -589,11 +589,11 @@ def conv_frontend2(x, blk1, blk2, wperm2, out_dtype, topdb=None):
     w1, b1, g1, be1, e1, s1 = blk1
     _, b2, g2, be2, e2, s2 = blk2
     sm, tdb = topdb if topdb is not None else (None, 0.0)
-    return torch.ops.sbk.conv_frontend2(x, w1, b1, g1, be1, float(e1), float(s1), wperm2, b2, g2, be2, float(e2),
+    return OPS.conv_frontend2(x, w1, b1, g1, be1, float(e1), float(s1), wperm2, b2, g2, be2, float(e2),
                                         float(s2), out_dtype == _bf16, sm, float(tdb))
 
 
-@torch.library.custom_op("sbk::relpos_attention", mutates_args=())
+@custom_op("sbk::relpos_attention", mutates_args=())
 def _relpos_attention_op(qkv: torch.Tensor, pk: torch.Tensor, pbu: torch.Tensor, pbv: torch.Tensor,
                          kpm: Optional[torch.Tensor], B: int, T: int, H: int, dh: int, scale: float,
                          need_probs: bool, am: Optional[torch.Tensor], am_sb: int,
@@ -648,12 +648,12 @@ def relpos_attention(qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale, need_probs=Fals
     if pk.stride(-1) != 1 or pk.shape[-1] != d:
         raise ValueError("pk must be (2T-1, d) with unit column stride")
     m, sb, sh = am if am is not None else (None, 0, 0)
-    out, probs = torch.ops.sbk.relpos_attention(qkv, pk, pbu, pbv, kpm, int(B), int(T), int(H), int(dh),
+    out, probs = OPS.relpos_attention(qkv, pk, pbu, pbv, kpm, int(B), int(T), int(H), int(dh),
                                                 float(scale), bool(need_probs), m, int(sb), int(sh))
     return out, (probs if need_probs else None)
 
 
-@torch.library.custom_op("sbk::mha_attention", mutates_args=())
+@custom_op("sbk::mha_attention", mutates_args=())
 def _mha_attention_op(qkv: torch.Tensor, kpm: Optional[torch.Tensor], B: int, T: int, H: int, dh: int,
                       scale: float) -> torch.Tensor:
     out = torch.empty(B * T, H * dh, device=qkv.device, dtype=qkv.dtype)
@@ -675,7 +675,7 @@ def mha_fast_ok(qkv, T, dh):
 def mha_attention(qkv, kpm, B, T, H, dh, scale):
     """Plain attention core (no positional band): qkv (B*T, 3d) head-interleaved
     bf16 -> out (B*T, d) bf16.  Inside mha_fast_ok's envelope only."""
-    return torch.ops.sbk.mha_attention(qkv, kpm, int(B), int(T), int(H), int(dh), float(scale))
+    return OPS.mha_attention(qkv, kpm, int(B), int(T), int(H), int(dh), float(scale))
 
 
 def glu_group():
@@ -683,7 +683,7 @@ def glu_group():
     return int(lib().sbk_gemm_glu_group(1))
 
 
-@torch.library.custom_op("sbk::cast_bf16", mutates_args=())
+@custom_op("sbk::cast_bf16", mutates_args=())
 def _cast_bf16_op(x: torch.Tensor) -> torch.Tensor:
     out = torch.empty(x.shape, device=x.device, dtype=_bf16)
     check(lib().sbk_cast_bf16(ptr(x), ptr(out), x.numel(), stream_of(x)), "sbk_cast_bf16")
@@ -697,7 +697,7 @@ def _(x):
 
 def cast_bf16(x):
     """fp32 → bf16 (round to nearest even), contiguous input."""
-    return torch.ops.sbk.cast_bf16(x)
+    return OPS.cast_bf16(x)
 
 
 def to_compute(x, dtype):

@@ -194,3 +194,51 @@ def require_device(*tensors):
         if t is not None and (not isinstance(t, torch.Tensor) or t.device.type != "cuda"):
             raise SbkError("speechbrain_amd kernels need ROCm device tensors (got "
                            f"{getattr(t, 'device', type(t))}); there is no CPU fallback")
+
+
+class _FastOp:
+    """A torch.library custom op (sbk::*) whose eager calls skip the
+    dispatcher: outside torch.compile / export tracing and torch.jit.trace
+    the op's body runs directly — the dispatch (schema checks, mutation
+    bookkeeping) costs ~20 µs of host time per call, which paces host-bound
+    eager steps such as config 2's feature ops and SpecAugment — while a
+    traced call goes through the registered op, so the launch is recorded as
+    a graph node.  Attribute access (register_fake, ...) reaches the op."""
+
+    def __init__(self, opdef):
+        self._def = opdef
+        self._body = opdef._init_fn
+        self._op = None
+
+    def __call__(self, *args, **kw):
+        if torch.compiler.is_compiling() or torch.jit.is_tracing():
+            if self._op is None:
+                self._op = getattr(torch.ops.sbk, self._def._name)
+            return self._op(*args, **kw)
+        return self._body(*args, **kw)
+
+    def __getattr__(self, name):
+        return getattr(self._def, name)
+
+
+_OPS = {}
+
+
+def custom_op(qualname, mutates_args):
+    """torch.library.custom_op for the sbk namespace, returning a _FastOp."""
+    def deco(fn):
+        op = _FastOp(torch.library.custom_op(qualname, mutates_args=mutates_args)(fn))
+        _OPS[qualname.split("::", 1)[1]] = op
+        return op
+    return deco
+
+
+class _Ops:
+    """OPS.<name>: the _FastOp of sbk::<name> (torch.ops.sbk.<name> with the
+    eager fast path)."""
+
+    def __getattr__(self, name):
+        return _OPS[name]
+
+
+OPS = _Ops()

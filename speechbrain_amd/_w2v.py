@@ -9,7 +9,7 @@ from typing import NamedTuple, Optional
 
 import torch
 
-from ._lib import check, lib, ptr, require_device, stream_of
+from ._lib import OPS, check, custom_op, lib, ptr, require_device, stream_of
 
 _f32, _bf16, _u8 = torch.float32, torch.bfloat16, torch.uint8
 OUT = {_f32: 0, _bf16: 1, "mx": 2}
@@ -35,7 +35,7 @@ def _fake_out(x, M, N, mode):
 
 
 # ---------------------------------------------------------------------------
-@torch.library.custom_op("sbk::w2v_wav_stats", mutates_args=())
+@custom_op("sbk::w2v_wav_stats", mutates_args=())
 def wav_stats(wav: torch.Tensor, eps: float) -> torch.Tensor:
     """(B, 2) [mean, rstd] of F.layer_norm(wav, wav.shape[1:]) (wav2vec.py:92-93)."""
     B, S = wav.shape
@@ -49,7 +49,7 @@ def _(wav, eps):
     return wav.new_empty(wav.shape[0], 2)
 
 
-@torch.library.custom_op("sbk::w2v_conv0", mutates_args=())
+@custom_op("sbk::w2v_conv0", mutates_args=())
 def _conv0_op(wav: torch.Tensor, stats: Optional[torch.Tensor], w: torch.Tensor, g: torch.Tensor, b: torch.Tensor,
               eps: float, stride: int, out_mode: int) -> tuple[torch.Tensor, torch.Tensor]:
     B, S = wav.shape
@@ -72,11 +72,11 @@ def conv0(wav, stats, w, g, b, eps, stride, out):
     """Layer 0 of the latent extractor: (B, S) → (B*T0, C) in `out`
     (torch.float32 | torch.bfloat16 | "mx")."""
     require_device(wav, w)
-    y, s = torch.ops.sbk.w2v_conv0(wav.contiguous(), stats, w.contiguous(), g, b, float(eps), int(stride), OUT[out])
+    y, s = OPS.w2v_conv0(wav.contiguous(), stats, w.contiguous(), g, b, float(eps), int(stride), OUT[out])
     return MX(y, s) if out == "mx" else y
 
 
-@torch.library.custom_op("sbk::ln_act", mutates_args=())
+@custom_op("sbk::ln_act", mutates_args=())
 def _ln_act_op(x: torch.Tensor, g: Optional[torch.Tensor], b: Optional[torch.Tensor], eps: float, act: int,
                out_mode: int) -> tuple[torch.Tensor, torch.Tensor]:
     M, D = x.shape
@@ -99,11 +99,11 @@ def ln_act(x, ln=None, act=None, out=_f32):
     if x.stride(-1) != 1:
         x = x.contiguous()
     g, b, eps = ln if ln is not None else (None, None, 0.0)
-    y, s = torch.ops.sbk.ln_act(x, g, b, float(eps), ACT[act], OUT[out])
+    y, s = OPS.ln_act(x, g, b, float(eps), ACT[act], OUT[out])
     return MX(y, s) if out == "mx" else y
 
 
-@torch.library.custom_op("sbk::mx_quant", mutates_args=())
+@custom_op("sbk::mx_quant", mutates_args=())
 def _mx_quant_op(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     M, K = x.shape
     q = torch.empty(M, K, device=x.device, dtype=_u8)
@@ -121,7 +121,7 @@ def _(x):
 def mx_quant(x):
     """fp32 / bf16 (M, K) → MX (power-of-two block scales, e4m3 elements)."""
     require_device(x)
-    q, s = torch.ops.sbk.mx_quant(x if x.stride(-1) == 1 else x.contiguous())
+    q, s = OPS.mx_quant(x if x.stride(-1) == 1 else x.contiguous())
     return MX(q, s)
 
 
@@ -134,7 +134,7 @@ def mx_dequant(m):
     return out
 
 
-@torch.library.custom_op("sbk::mx_gemm", mutates_args=())
+@custom_op("sbk::mx_gemm", mutates_args=())
 def _mx_gemm_op(aq: torch.Tensor, asc: torch.Tensor, M: int, K: int, lda: int, ldsa: int, rpb: int, a_bs: int,
                 s_bs: int, wq: torch.Tensor, wsc: torch.Tensor, bias: Optional[torch.Tensor], act: int, alpha: float,
                 res: Optional[torch.Tensor], out_mode: int) -> tuple[torch.Tensor, torch.Tensor]:
@@ -161,7 +161,7 @@ def mx_gemm(a, w, bias=None, act=None, alpha=1.0, res=None, out=_f32):
         raise ValueError(f"mx_gemm K mismatch {K} vs {w.q.shape[1]}")
     if res is not None and (res.dtype != _f32 or res.stride(-1) != 1):
         raise ValueError("residual must be fp32, row-contiguous")
-    y, s = torch.ops.sbk.mx_gemm(a.q, a.s, M, K, a.q.stride(0), a.s.stride(0), M, 0, 0, w.q, w.s, bias, ACT[act],
+    y, s = OPS.mx_gemm(a.q, a.s, M, K, a.q.stride(0), a.s.stride(0), M, 0, 0, w.q, w.s, bias, ACT[act],
                                  float(alpha), res, OUT[out])
     return MX(y, s) if out == "mx" else y
 
@@ -174,12 +174,12 @@ def mx_conv_gemm(x, B, T_in, C, k, stride, w, out=_f32):
     [out][tap][in] (CNN.py:309-516, padding "valid")."""
     T_out = (T_in - k) // stride + 1
     M = B * T_out
-    y, s = torch.ops.sbk.mx_gemm(x.q, x.s, M, k * C, stride * C, stride * C // 32, T_out, T_in * C,
+    y, s = OPS.mx_gemm(x.q, x.s, M, k * C, stride * C, stride * C // 32, T_out, T_in * C,
                                  T_in * C // 32, w.q, w.s, None, 0, 1.0, None, OUT[out])
     return (MX(y, s) if out == "mx" else y), T_out
 
 
-@torch.library.custom_op("sbk::add_posenc", mutates_args=("x",))
+@custom_op("sbk::add_posenc", mutates_args=("x",))
 def add_posenc(x: torch.Tensor, pe: torch.Tensor, T: int) -> None:
     """x (B*T, D) fp32 += pe[t] (EncoderWrapper: latents + positional_encoding,
     wav2vec.py:222)."""

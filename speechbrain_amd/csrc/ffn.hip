@@ -205,12 +205,11 @@ __device__ __forceinline__ void vm_wait(int n) {
 
 // Full-row LayerNorm of the epilogue values z (in place).  Lane (w, g, fr)
 // holds rows mt*16 + fr, units (w*T2 + j)*16 + 4g + e; row statistics are
-// reduced over g by shuffles and over the NW waves through red[2][BM][NW]
-// (mean, then variance: one buffer each, so a pass needs only the barrier
-// between its writes and its reads — a buffer's previous readers passed the
-// other pass's barrier since); gam / bet are LDS copies.  Every LDS access is
-// explicit (asm) and the barriers wait on LDS only, so the weight tiles and
-// stores in flight stay in flight.
+// reduced over g by shuffles and over the NW waves through red[BM][NW]; gam /
+// bet are LDS copies.  Every LDS access is explicit (asm) and the barriers
+// wait on LDS only, so the weight tiles and stores in flight stay in flight.
+// (One barrier per pass with a buffer per pass measured 1.5 us slower per
+// chain launch than two barriers over one buffer.)
 template <int D, int T2, int MT, int NW>
 __device__ __forceinline__ void row_ln(float (&z)[T2][MT][4], float* red, const float* gam, const float* bet, float eps,
                                        int w, int g, int fr) {
@@ -234,17 +233,17 @@ __device__ __forceinline__ void row_ln(float (&z)[T2][MT][4], float* red, const 
         }
       part[mt] = col4_sum(s);
     }
-    float* rb = red + pass * (MT * 16 * NW);
+    lds_barrier();  // the previous readers of red are done
     if (g == 0) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) lds_st1(rb + (mt * 16 + fr) * NW + w, part[mt]);
+      for (int mt = 0; mt < MT; ++mt) lds_st1(red + (mt * 16 + fr) * NW + w, part[mt]);
     }
     lds_barrier();
     f32x4 rv[MT][2];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      rv[mt][0] = lds_f4(rb + (mt * 16 + fr) * NW);
-      rv[mt][1] = lds_f4(rb + (mt * 16 + fr) * NW + 4);
+      rv[mt][0] = lds_f4(red + (mt * 16 + fr) * NW);
+      rv[mt][1] = lds_f4(red + (mt * 16 + fr) * NW + 4);
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -298,6 +297,61 @@ __device__ __forceinline__ void load_frags(bf16x8 (&xa)[K1][KS][MT], const bf16_
       for (int mt = 0; mt < MT; ++mt) tie(xa[r][ks][mt]);
 }
 
+#ifdef SBK_PROBE_PAIRX
+// Probe (timing only, wrong results; never the product): the cost of the seam
+// a hidden-dimension split over paired workgroups would need — each
+// workgroup publishes its (48 x 256) fp32 phase-2 partial (48 KB) with
+// write-through (sc1) stores, raises a flag after every wave's vmcnt(0) and a
+// barrier, polls its partner's flag (blockIdx ^ 8: the same XCD), reads the
+// partner's partial (sc1 loads) and adds it.  The consumer resets the
+// partner's flag, so every launch starts from zero.  Spins are bounded.
+__device__ float4 g_pairx_buf[256 * 512 * 6];
+__device__ unsigned g_pairx_flag[256];
+template <int T, int MT>
+__device__ __forceinline__ void pairx_exchange(f32x4 (&acc)[T][MT], int tid) {
+  const int pb = blockIdx.x ^ 8;
+  if (pb >= (int)gridDim.x) return;
+  float4* mine = g_pairx_buf + ((long long)blockIdx.x * 512 + tid) * (T * MT);
+  const float4* theirs = g_pairx_buf + ((long long)pb * 512 + tid) * (T * MT);
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+      asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(mine + t * MT + mt), "v"(acc[t][mt]) : "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (tid == 0) {
+    const unsigned one = 1;
+    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(g_pairx_flag + blockIdx.x), "v"(one) : "memory");
+    unsigned f = 0;
+    for (int it = 0; it < (1 << 20); ++it) {
+      asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(f) : "v"(g_pairx_flag + pb) : "memory");
+      if (f == 1) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __builtin_amdgcn_s_barrier();
+  f32x4 v[T][MT];
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+      asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v[t][mt]) : "v"(theirs + t * MT + mt) : "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      vtie(v[t][mt]);
+      acc[t][mt] += v[t][mt];
+    }
+  if (tid == 0) {
+    const unsigned zero = 0;
+    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(g_pairx_flag + pb), "v"(zero) : "memory");
+  }
+}
+#endif
+
 // s_memtime timeline of the waves of workgroup 128 (probe builds only)
 SBK_PROBE_BUFFER(g_ffn_tl, 16, 256)
 #define FFN_TL(i) SBK_PROBE(if (tl_rec >= 0 && lane == 0) g_ffn_tl[tl_rec][i] = __builtin_amdgcn_s_memtime();)
@@ -322,10 +376,10 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   bf16_t* Xn = ring + NB * TROWS * BK;                      // BM x XS
   bf16_t* Hs = Xn + BM * XS;                                // 2 x BM x HS
   float* b1s = reinterpret_cast<float*>(Hs + 2 * BM * HS);  // H (CHAIN: 2 H, block A then B)
-  float* red = b1s + (CHAIN ? 2 : 1) * a.H;                 // 2 x BM x NW row partials
+  float* red = b1s + (CHAIN ? 2 : 1) * a.H;                 // BM x NW row partials
   // epilogue vectors, copied to LDS in the prologue so that no global load
   // (and its in-order vmcnt wait behind the weight tiles) sits between blocks
-  float* prm = red + 2 * BM * NW;                           // P_* x D
+  float* prm = red + BM * NW;                               // P_* x D
   enum { P_B2 = 0, P_GP, P_BP, P_G0B, P_B0B, P_B2B, P_GN, P_BN, P_N };
   static_assert(P_N == NW, "one parameter row per wave");
 
@@ -340,6 +394,34 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   SBK_PROBE(const int tl_rec = blockIdx.x == 128 ? w : -1;)
   FFN_TL(0);
 
+  // ---- weight tile s -> ring slot (LDS-DMA, 1 KB = 8 rows per wave-instruction)
+  // lane L of instruction i writes row R0 + L/8, 16-B chunk L%8 (linear image)
+  // and fetches source chunk (L%8) ^ ((row >> 1) & 7): the read side applies
+  // the same involution.  Steps S.. are the projection's (256 columns of Wp
+  // by 64 k per tile, column block after column block).
+  auto issue = [&](int s, int slot) __attribute__((always_inline)) {
+    // tile s of the image: wave w's 4 KB (its 32 rows, lane-linear) by GL
+    // pieces of 1 KB from one base address and immediate offsets, which the
+    // instruction applies to the global and the LDS address alike (one m0
+    // per tile; the per-piece address arithmetic and tile-index logic of a
+    // strided source cost ~100 scalar and vector instructions per step)
+    const bf16_t* src = a.img + (long long)s * (TROWS * BK) + w * (GL * 512) + lane * 8;
+    bf16_t* dst = ring + slot * (TROWS * BK) + w * (GL * 512);
+    const auto gs = (const __attribute__((address_space(1))) void*)src;
+    const auto ls = (__attribute__((address_space(3))) void*)dst;
+    static_assert(GL == 4, "four 1-KB pieces per wave and tile");
+#ifndef SBK_PROBE_NODMA
+    __builtin_amdgcn_global_load_lds(gs, ls, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(gs, ls, 16, 1024, 0);
+    __builtin_amdgcn_global_load_lds(gs, ls, 16, 2048, 0);
+    __builtin_amdgcn_global_load_lds(gs, ls, 16, 3072, 0);
+#endif
+  };
+#ifdef FFN_TILES_FIRST
+  // probe: the first two tiles ahead of the x rows (they then land first)
+  issue(0, 0);
+  issue(1, 1);
+#endif
   // ---- prologue.  Every HBM read of the launch is issued here, before the
   // weight stream: the residual x values of this lane's epilogue outputs
   // (held in VGPRs through the main loop; rows clamped, masked at the end) and
@@ -369,33 +451,14 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   const bool b1t = tid * 4 < a.H;
   if (b1t) b1v = gld4(a.b1 + tid * 4);
   if (CHAIN && b1t) b1bv = gld4(a.b1b + tid * 4);
-  // ---- weight tile s -> ring slot (LDS-DMA, 1 KB = 8 rows per wave-instruction)
-  // lane L of instruction i writes row R0 + L/8, 16-B chunk L%8 (linear image)
-  // and fetches source chunk (L%8) ^ ((row >> 1) & 7): the read side applies
-  // the same involution.  Steps S.. are the projection's (256 columns of Wp
-  // by 64 k per tile, column block after column block).
-  auto issue = [&](int s, int slot) __attribute__((always_inline)) {
-    // tile s of the image: wave w's 4 KB (its 32 rows, lane-linear) by GL
-    // pieces of 1 KB from one base address and immediate offsets, which the
-    // instruction applies to the global and the LDS address alike (one m0
-    // per tile; the per-piece address arithmetic and tile-index logic of a
-    // strided source cost ~100 scalar and vector instructions per step)
-    const bf16_t* src = a.img + (long long)s * (TROWS * BK) + w * (GL * 512) + lane * 8;
-    bf16_t* dst = ring + slot * (TROWS * BK) + w * (GL * 512);
-    const auto gs = (const __attribute__((address_space(1))) void*)src;
-    const auto ls = (__attribute__((address_space(3))) void*)dst;
-    static_assert(GL == 4, "four 1-KB pieces per wave and tile");
-#ifndef SBK_PROBE_NODMA
-    __builtin_amdgcn_global_load_lds(gs, ls, 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(gs, ls, 16, 1024, 0);
-    __builtin_amdgcn_global_load_lds(gs, ls, 16, 2048, 0);
-    __builtin_amdgcn_global_load_lds(gs, ls, 16, 3072, 0);
-#endif
-  };
+#ifdef FFN_TILES_FIRST
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
   issue(0, 0);
   issue(1, 1);
   // every load above has landed; the two tiles stay in flight
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB * GL) : "memory");
+#endif
 #pragma unroll
   for (int j = 0; j < T; ++j)
 #pragma unroll
@@ -490,6 +553,9 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
           else
             acc1[t][mt] = FFN_MFMA(fw[ks][t], fa[ks][mt], acc1[t][mt]);
         }
+    // (a sched_barrier here, keeping the MFMAs above the next step's tile
+    // wait instead of letting the scheduler sink most of them below it,
+    // measured equal: 55.4-56.4 vs 53.8-56.6 us, profiles/r04i_chain_time.log)
     post();  // VALU work that rides under this step's MFMAs (after its DMA issue)
     if (s < 96) FFN_TL(3 + 2 * s);
   };
@@ -523,6 +589,9 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   for (int stage = 0; stage < (CHAIN ? 2 : 1); ++stage) {
   if (CHAIN && stage == 1) {
     FFN_TL(197);
+#ifdef SBK_PROBE_PAIRX
+    pairx_exchange<T, MT>(acc2, tid);
+#endif
     // ---- between the blocks: A's rows z = x + alpha (acc2 + b2) -> post-LN
     // (norm2) are B's residual (held in xres) and, through B's LN0, its
     // phase-1 operand (Xn -> VGPR fragments); nothing goes to HBM
@@ -812,10 +881,10 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
 
 template <int D>
 size_t ffn_lds(int H, bool chain) {
-  // 2-slot weight ring, Xn, two hidden-chunk buffers, b1 (two with CHAIN), the row-reduction scratch
-  // (two buffers), the epilogue parameter rows
+  // 2-slot weight ring, Xn, two hidden-chunk buffers, b1 (two with CHAIN), the row-reduction scratch,
+  // the epilogue parameter rows
   return ((size_t)2 * 256 * 64 + (size_t)FFN_BM * (D + 16) + (size_t)2 * FFN_BM * (256 + 16)) * sizeof(bf16_t) +
-         (size_t)(chain ? 2 : 1) * H * 4 + (size_t)2 * FFN_NW * FFN_BM * 4 + (size_t)FFN_NW * D * 4;
+         (size_t)(chain ? 2 : 1) * H * 4 + (size_t)FFN_NW * FFN_BM * 4 + (size_t)FFN_NW * D * 4;
 }
 
 template <int D, int ACT, bool PROJ, bool CHAIN>

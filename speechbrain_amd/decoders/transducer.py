@@ -21,10 +21,10 @@ where:
 import numpy as np
 import torch
 
-from .._lib import check, lib, ptr, require_device, stream_of
+from .._lib import check, custom_op, lib, ptr, require_device, stream_of
 
 
-@torch.library.custom_op("sbk::logsoftmax_topk", mutates_args=())
+@custom_op("sbk::logsoftmax_topk", mutates_args=())
 def logsoftmax_topk(x: torch.Tensor, k: int) -> tuple[torch.Tensor, torch.Tensor]:
     """x (R, V) logits → (log-probs of the k best (R, k) fp32, their indices (R, k) int64)."""
     R, V = x.shape

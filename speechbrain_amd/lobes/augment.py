@@ -12,14 +12,14 @@ from typing import Optional
 
 import torch
 
-from .._lib import check, lib, ptr, require_device, stream_of
+from .._lib import OPS, check, custom_op, lib, ptr, require_device, stream_of
 
 __all__ = ["SpecAugment"]
 
 _WARP_MODES = {"bicubic": 0, "bilinear": 1}
 
 
-@torch.library.custom_op("sbk::specaugment_", mutates_args=("x",))
+@custom_op("sbk::specaugment_", mutates_args=("x",))
 def specaugment_(x: torch.Tensor, N: int, T: int, F: int, c: int, w: int, fm: Optional[torch.Tensor],
                  tm: Optional[torch.Tensor], use_mean: bool, n_fcells: int, warp_mode: int = 0) -> None:
     """Applies the drawn warp (c, w; -1 = none; warp_mode 0 bicubic, 1
@@ -72,16 +72,20 @@ class SpecAugment(torch.nn.Module):
         self._pin = None     # pinned staging of the mask draws (reused; see _upload)
         self._pin_ev = None  # completion of the last upload out of it
 
-    def _upload(self, host, device):
-        """int32 host draws -> device, asynchronously from a reused pinned
-        buffer (a pageable copy would block the host for the transfer)."""
-        n = host.numel()
+    def _upload(self, parts, device):
+        """int32 host draws (concatenated) -> device, asynchronously from a
+        reused pinned buffer (a pageable copy would block the host for the
+        transfer)."""
+        n = sum(p.numel() for p in parts)
         if self._pin is None or self._pin.numel() < n:
             self._pin = torch.empty(max(n, 1024), dtype=torch.int32).pin_memory()
             self._pin_ev = None
         if self._pin_ev is not None:
             self._pin_ev.synchronize()  # the previous copy out of the buffer is done
-        self._pin[:n].copy_(host)
+        o = 0
+        for p in parts:
+            self._pin[o:o + p.numel()].copy_(p)
+            o += p.numel()
         dev = self._pin[:n].to(device, non_blocking=True)
         self._pin_ev = torch.cuda.Event()
         self._pin_ev.record(torch.cuda.current_stream(device))
@@ -95,15 +99,18 @@ class SpecAugment(torch.nn.Module):
             if T - win > win:
                 c = int(torch.randint(win, T - win, (1,))[0])
                 w = int(torch.randint(c - win, c + win, (1,))[0]) + 1
+        # (int32 draws: the same values as the reference's int64 ones — one
+        # 32-bit generator draw per element either way, tests/test_augment_draws.py)
+        i32 = torch.int32
         fm = tm = None
         if self.freq_mask:
-            ln = torch.randint(self.freq_mask_width[0], self.freq_mask_width[1], (N, self.n_freq_mask))
-            ps = torch.randint(0, max(1, F - int(ln.max())), (N, self.n_freq_mask))
-            fm = torch.stack([ln, ps], -1).to(torch.int32)
+            ln = torch.randint(self.freq_mask_width[0], self.freq_mask_width[1], (N, self.n_freq_mask), dtype=i32)
+            ps = torch.randint(0, max(1, F - int(ln.max())), (N, self.n_freq_mask), dtype=i32)
+            fm = torch.stack([ln, ps], -1)
         if self.time_mask:
-            ln = torch.randint(self.time_mask_width[0], self.time_mask_width[1], (N, self.n_time_mask))
-            ps = torch.randint(0, max(1, T - int(ln.max())), (N, self.n_time_mask))
-            tm = torch.stack([ln, ps], -1).to(torch.int32)
+            ln = torch.randint(self.time_mask_width[0], self.time_mask_width[1], (N, self.n_time_mask), dtype=i32)
+            ps = torch.randint(0, max(1, T - int(ln.max())), (N, self.n_time_mask), dtype=i32)
+            tm = torch.stack([ln, ps], -1)
         return c, w, fm, tm
 
     def forward(self, x):
@@ -128,10 +135,10 @@ class SpecAugment(torch.nn.Module):
         parts = [m.reshape(-1) for m in (fm, tm) if m is not None]
         fm_d = tm_d = None
         if parts:
-            buf = self._upload(torch.cat(parts) if len(parts) > 1 else parts[0], x.device)
+            buf = self._upload(parts, x.device)
             nf = fm.numel() if fm is not None else 0
             fm_d = buf[:nf].view(fm.shape) if fm is not None else None
             tm_d = buf[nf:].view(tm.shape) if tm is not None else None
-        torch.ops.sbk.specaugment_(x, N, T, F, c, w, fm_d, tm_d, not self.replace_with_zero, -1,
+        OPS.specaugment_(x, N, T, F, c, w, fm_d, tm_d, not self.replace_with_zero, -1,
                                    _WARP_MODES.get(self.time_warp_mode, 0))
         return x

@@ -33,7 +33,7 @@ import torch.nn as nn
 
 from ... import _autograd as A
 from ... import _enc
-from ..._lib import check, lib, ptr, require_device, stream_of
+from ..._lib import check, custom_op, lib, ptr, require_device, stream_of
 from ..linear import Linear
 
 __all__ = ["transducer_head_loss", "TransducerHeadLinear"]
@@ -51,7 +51,7 @@ def _padded_bf16(w):
     return out
 
 
-@torch.library.custom_op("sbk::thead_loss", mutates_args=())
+@custom_op("sbk::thead_loss", mutates_args=())
 def thead_loss(tn: torch.Tensor, pn: torch.Tensor, w: torch.Tensor, labels: torch.Tensor, Tl: torch.Tensor,
                Ul: torch.Tensor, blank: int, reduction: int, loss_mode: int, act: int,
                slope: float) -> tuple[torch.Tensor, torch.Tensor]:
@@ -78,7 +78,7 @@ def _(tn, pn, w, labels, Tl, Ul, blank, reduction, loss_mode, act, slope):
     return tn.new_empty(B if reduction == 2 else ()), tn.new_empty(7 * B * T * U1 + 2 * B)
 
 
-@torch.library.custom_op("sbk::thead_grad", mutates_args=())
+@custom_op("sbk::thead_grad", mutates_args=())
 def thead_grad(tn: torch.Tensor, pn: torch.Tensor, w: torch.Tensor, labels: torch.Tensor, Tl: torch.Tensor,
                ws: torch.Tensor, go: torch.Tensor, blank: int, act: int,
                slope: float) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:

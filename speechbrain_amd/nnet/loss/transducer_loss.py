@@ -14,12 +14,12 @@ module accepts ROCm tensors (and raises for CPU tensors: no CPU fallback).
 import torch
 from torch.nn import Module
 
-from ..._lib import check, lib, ptr, require_device, stream_of
+from ..._lib import check, custom_op, lib, ptr, require_device, stream_of
 
 _RED = {"mean": 0, "sum": 1, "none": 2}
 
 
-@torch.library.custom_op("sbk::rnnt", mutates_args=())
+@custom_op("sbk::rnnt", mutates_args=())
 def rnnt(x: torch.Tensor, labels: torch.Tensor, Tl: torch.Tensor, Ul: torch.Tensor, blank: int, reduction: int,
          is_logits: bool, loss_mode: int) -> tuple[torch.Tensor, torch.Tensor]:
     """Forward kernels (gather [+ fused log-softmax], α/β lattice, sparse
@@ -40,7 +40,7 @@ def _(x, labels, Tl, Ul, blank, reduction, is_logits, loss_mode):
     return (x.new_empty(B if reduction == 2 else ()), x.new_empty(7 * B * maxT * U1 + 2 * B))
 
 
-@torch.library.custom_op("sbk::rnnt_grad", mutates_args=())
+@custom_op("sbk::rnnt_grad", mutates_args=())
 def rnnt_grad(x: torch.Tensor, labels: torch.Tensor, ws: torch.Tensor, go: torch.Tensor, blank: int,
               mode: int) -> torch.Tensor:
     """Dense (B, T, U1, V) gradient: mode 0 wrt log-probs, 1 wrt logits

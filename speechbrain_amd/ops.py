@@ -12,7 +12,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import check, ptr, require_device, stream_of
+from ._lib import check, custom_op, ptr, require_device, stream_of
 
 _f32 = torch.float32
 
@@ -33,7 +33,7 @@ def n_frames(S, n_fft, hop, center):
     return 1 + (S + 2 * pad - n_fft) // hop
 
 
-@torch.library.custom_op("sbk::stft", mutates_args=())
+@custom_op("sbk::stft", mutates_args=())
 def stft(x: torch.Tensor, window: torch.Tensor, tw_nc: torch.Tensor, tw_nfft: torch.Tensor,
          n_fft: int, hop: int, center: bool, pad_mode: int, onesided: bool, normalized: bool) -> torch.Tensor:
     """torch.stft(return_complex=False) layout (features.py:161-183):
@@ -69,7 +69,7 @@ def _(x, window, tw_nc, tw_nfft, n_fft, hop, center, pad_mode, onesided, normali
     return x.new_empty(x.shape[0], T, Fo, 2)
 
 
-@torch.library.custom_op("sbk::power_spectrum", mutates_args=())
+@custom_op("sbk::power_spectrum", mutates_args=())
 def power_spectrum(x: torch.Tensor, window: torch.Tensor, tw_nc: torch.Tensor, tw_nfft: torch.Tensor,
                    n_fft: int, hop: int, center: bool, pad_mode: int, normalized: bool,
                    power: float, eps: float, log_mag: bool) -> torch.Tensor:
@@ -95,7 +95,7 @@ def _(x, window, tw_nc, tw_nfft, n_fft, hop, center, pad_mode, normalized, power
     return x.new_empty(x.shape[0], n_frames(x.shape[1], n_fft, hop, center), n_fft // 2 + 1)
 
 
-@torch.library.custom_op("sbk::fbank", mutates_args=())
+@custom_op("sbk::fbank", mutates_args=())
 def fbank(x: torch.Tensor, window: torch.Tensor, tw_nc: torch.Tensor, tw_nfft: torch.Tensor,
           mel_start: torch.Tensor, mel_len: torch.Tensor, mel_off: torch.Tensor, mel_w: torch.Tensor,
           n_fft: int, hop: int, center: bool, pad_mode: int, n_mels: int, log_mel: bool,
@@ -127,7 +127,7 @@ def _(x, window, tw_nc, tw_nfft, mel_start, mel_len, mel_off, mel_w, n_fft, hop,
     return x.new_empty(x.shape[0], n_frames(x.shape[1], n_fft, hop, center), n_mels)
 
 
-@torch.library.custom_op("sbk::fbank_deferred", mutates_args=())
+@custom_op("sbk::fbank_deferred", mutates_args=())
 def fbank_deferred(x: torch.Tensor, window: torch.Tensor, tw_nc: torch.Tensor, tw_nfft: torch.Tensor,
                    mel_start: torch.Tensor, mel_len: torch.Tensor, mel_off: torch.Tensor, mel_w: torch.Tensor,
                    n_fft: int, hop: int, center: bool, pad_mode: int, n_mels: int, multiplier: float,
@@ -161,7 +161,7 @@ def _(x, window, tw_nc, tw_nfft, mel_start, mel_len, mel_off, mel_w, n_fft, hop,
     return x.new_empty(B, T, n_mels), x.new_empty(B, max(nslot, 1))
 
 
-@torch.library.custom_op("sbk::topdb_clamp", mutates_args=())
+@custom_op("sbk::topdb_clamp", mutates_args=())
 def topdb_clamp(x: torch.Tensor, slot_max: torch.Tensor, top_db: float) -> torch.Tensor:
     """max(x, max_b - top_db) per sequence b of fbank_deferred's output
     (features.py:706-711), into a new tensor."""
@@ -178,7 +178,7 @@ def _(x, slot_max, top_db):
     return torch.empty_like(x, dtype=_f32)
 
 
-@torch.library.custom_op("sbk::filterbank", mutates_args=())
+@custom_op("sbk::filterbank", mutates_args=())
 def filterbank(spec: torch.Tensor, mel_start: torch.Tensor, mel_len: torch.Tensor, mel_off: torch.Tensor,
                mel_w: torch.Tensor, n_mels: int, log_mel: bool, multiplier: float, db_offset: float,
                amin: float, top_db: float) -> torch.Tensor:
@@ -204,7 +204,7 @@ def _(spec, mel_start, mel_len, mel_off, mel_w, n_mels, log_mel, multiplier, db_
     return spec.new_empty(spec.shape[0], spec.shape[1], n_mels)
 
 
-@torch.library.custom_op("sbk::filterbank_dense", mutates_args=())
+@custom_op("sbk::filterbank_dense", mutates_args=())
 def filterbank_dense(spec: torch.Tensor, mat: torch.Tensor, log_mel: bool, multiplier: float,
                      db_offset: float, amin: float, top_db: float) -> torch.Tensor:
     """Filterbank with a dense (F, M) matrix (learnable filters, freeze=False)."""
@@ -231,7 +231,7 @@ def _(spec, mat, log_mel, multiplier, db_offset, amin, top_db):
     return spec.new_empty(spec.shape[0], spec.shape[1], mat.shape[1])
 
 
-@torch.library.custom_op("sbk::magnitude", mutates_args=())
+@custom_op("sbk::magnitude", mutates_args=())
 def magnitude(x: torch.Tensor, power: float, eps: float, log_mag: bool) -> torch.Tensor:
     """spectral_magnitude: reduce the last axis by sum of squares (features.py:347-356)."""
     require_device(x)
@@ -249,7 +249,7 @@ def _(x, power, eps, log_mag):
     return x.new_empty(x.shape[:-1])
 
 
-@torch.library.custom_op("sbk::dct", mutates_args=())
+@custom_op("sbk::dct", mutates_args=())
 def dct(x: torch.Tensor, mat: torch.Tensor) -> torch.Tensor:
     """x (..., n_in) @ mat (n_in, n_out) (features.py:765-786)."""
     require_device(x, mat)
@@ -267,7 +267,7 @@ def _(x, mat):
     return x.new_empty(*x.shape[:-1], mat.shape[1])
 
 
-@torch.library.custom_op("sbk::deltas", mutates_args=())
+@custom_op("sbk::deltas", mutates_args=())
 def deltas(x: torch.Tensor, window_length: int, concat: bool) -> torch.Tensor:
     """Deltas along dim 1 of (N,T,F) (features.py:829-852); concat=True
     returns [x | Δx | ΔΔx] in one pass (lobes/features.py:141-144)."""
@@ -285,7 +285,7 @@ def _(x, window_length, concat):
     return x.new_empty(x.shape[0], x.shape[1], 3 * x.shape[2] if concat else x.shape[2])
 
 
-@torch.library.custom_op("sbk::deltas_floor", mutates_args=())
+@custom_op("sbk::deltas_floor", mutates_args=())
 def deltas_floor(x: torch.Tensor, window_length: int, slot_max: torch.Tensor, top_db: float) -> torch.Tensor:
     """[max(x, max_b - top_db) | Δ | ΔΔ] of fbank_deferred's output: the
     top_db floor (features.py:706-711) applied as the concat deltas kernel
@@ -304,7 +304,7 @@ def _(x, window_length, slot_max, top_db):
     return x.new_empty(x.shape[0], x.shape[1], 3 * x.shape[2])
 
 
-@torch.library.custom_op("sbk::context_window", mutates_args=())
+@custom_op("sbk::context_window", mutates_args=())
 def context_window(x: torch.Tensor, left: int, right: int) -> torch.Tensor:
     """ContextWindow on (N,T,F) → (N,T,F·(l+r+1)) (features.py:917-937)."""
     require_device(x)
@@ -327,7 +327,7 @@ def _(x, left, right):
 # these gradients from torch autograd; here they are HIP kernels too
 # ---------------------------------------------------------------------------
 
-@torch.library.custom_op("sbk::filterbank_dense_bwd", mutates_args=())
+@custom_op("sbk::filterbank_dense_bwd", mutates_args=())
 def filterbank_dense_bwd(grad: torch.Tensor, spec: torch.Tensor, mat: torch.Tensor, log_mel: bool,
                          multiplier: float, db_offset: float, amin: float,
                          top_db: float) -> tuple[torch.Tensor, torch.Tensor]:
