@@ -105,16 +105,20 @@ int sbk_context_window(const float* x, float* y, int N, int T, int F, int left, 
 
 /* SpecAugment.forward (speechbrain/lobes/augment.py:106-201) on x (N, T, F)
  * fp32, in place: time warp (c, w; c < 0 = none; warp_mode 0 bicubic,
- * 1 bilinear — the align_corners interpolate modes of :134-148) through
- * `tmp`, then frequency / time masks given as device int32 (N, n, 2)
- * [len, pos] arrays drawn on the host, filled with 0 or the running means
- * (use_mean; `partial` scratch of 2*N*ceil(T/4) + 4 floats, 16-B aligned;
+ * 1 bilinear — the align_corners interpolate modes of :134-148), then
+ * frequency / time masks given as device int32 (N, n, 2) [len, pos] arrays
+ * drawn on the host, filled with 0 or the running means (use_mean; `partial`
+ * scratch of max(2*N*ceil(T/4), 3*N*(F/4)) + 4 floats, 16-B aligned;
  * n_fcells = number of frequency-masked cells, or < 0 to count them on the
- * device from the mask table).  F % 4 == 0 with 16-B aligned x / tmp takes
- * the float4 kernels. */
+ * device from the mask table).  F % 4 == 0 with 16-B aligned x, |c - w| <= 61
+ * and <= 32 masks of each kind runs in place with no copy (x read once, the
+ * unmasked cells written once, the masked cells written after the means);
+ * otherwise the warp goes through `tmp` (a copy of x) —
+ * sbk_specaugment_needs_scratch says which. */
 int sbk_specaugment(float* x, int N, int T, int F, int c, int w, int warp_mode, float* tmp, const int* fmask,
                     int n_fmask, const int* tmask, int n_tmask, int use_mean, float* partial, long long n_fcells,
                     void* stream);
+int sbk_specaugment_needs_scratch(int N, int T, int F, int c, int w, int n_fmask, int n_tmask, int x_aligned);
 
 /* ------------------------------------------------------------ RNN-T loss */
 

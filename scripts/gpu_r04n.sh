@@ -1,0 +1,11 @@
+# SpecAugment in place, 512-row windows (roll4) + masked-cells-only fixup4: parity on every route, the C2 bench,
+# its kernel stats and PMC traffic.
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp && \
+timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_augment.py > gpurun_out/r04n_aug.log 2>&1 && \
+timeout -k 10 300 python bench.py --config c2 --no-cpu-baseline > gpurun_out/r04n_bench_c2.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04n_prof_c2 -o run -- python bench.py --config c2 --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/r04n_prof_c2.log 2>&1 && \
+bash scripts/pmc_traffic.sh r04n_pmc_c2 --config c2
+rc=$?
+grep -E "passed|failed|FAILED|Error" gpurun_out/r04n_aug.log | tail -4
+tail -1 gpurun_out/r04n_bench_c2.log | cut -c1-700
+exit $rc

@@ -94,6 +94,7 @@ SIGNATURES = {
     "sbk_mx_dequant": [_vp, _ll, _vp, _ll, _i, _i, _vp, _vp],
     # augment.hip
     "sbk_specaugment": [_vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _i, _vp, _ll, _vp],
+    "sbk_specaugment_needs_scratch": [_i, _i, _i, _i, _i, _i, _i, _i],
     # rnnt.hip
     "sbk_rnnt_forward": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp],
     "sbk_rnnt_workspace_floats": [_i, _i, _i],
@@ -203,7 +204,9 @@ class _FastOp:
     bookkeeping) costs ~20 µs of host time per call, which paces host-bound
     eager steps such as config 2's feature ops and SpecAugment — while a
     traced call goes through the registered op, so the launch is recorded as
-    a graph node.  Attribute access (register_fake, ...) reaches the op."""
+    a graph node, and so does a call of an op with a registered backward on
+    inputs that require grad (its autograd edge).  Attribute access
+    (register_fake, register_autograd, ...) reaches the op."""
 
     def __init__(self, opdef):
         self._def = opdef
@@ -211,7 +214,11 @@ class _FastOp:
         self._op = None
 
     def __call__(self, *args, **kw):
-        if torch.compiler.is_compiling() or torch.jit.is_tracing():
+        if (torch.compiler.is_compiling() or torch.jit.is_tracing()
+                or (self._def._backward_fn is not None and torch.is_grad_enabled()
+                    and any(isinstance(t, torch.Tensor) and t.requires_grad for t in (*args, *kw.values())))):
+            # traced, or a differentiable call of an op with a registered
+            # backward: through the dispatcher (graph node / autograd edge)
             if self._op is None:
                 self._op = getattr(torch.ops.sbk, self._def._name)
             return self._op(*args, **kw)

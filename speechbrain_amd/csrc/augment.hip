@@ -335,6 +335,232 @@ __global__ void __launch_bounds__(256) warp4_kernel(const float* __restrict__ x,
   }
 }
 
+// ---- In place, 1R + ~1.1W (x read once, unmasked cells written once, the
+// masked cells written by fixup4_kernel after the means are known).
+// roll4_kernel: one workgroup per (utterance n, slab of J float4 columns),
+// all T rows in order through a 1024-row LDS ring: window after window of WR
+// = 512 output rows (32 KB of loads in flight per workgroup at J = 4, two or
+// more workgroups per CU), each output row's taps (|p(t) - t| <= |c - w|, so rows
+// t - H .. t + H with H = |c - w| + 3) read from the ring.  The next window's
+// new input rows are loaded into registers while this window computes — they
+// lie above every row this window writes — and stored into the ring after
+// it, so an input row is read from HBM before the workgroup overwrites it and
+// never again (the in-place hazard is confined to the workgroup that owns the
+// column slab).  Per workgroup partials [sum, freq-masked sum, freq-masked
+// columns of the slab] feed the means.
+#ifndef SBK_RL_JMAX
+#define SBK_RL_JMAX 4  // (probe builds vary the slab width)
+#endif
+constexpr int RL_RING = 1024, RL_WR = 512, RL_HMAX = (RL_RING - RL_WR) / 2, RL_MAXM = 32, RL_JMAX = SBK_RL_JMAX;
+template <bool CUBIC, bool WARP, bool MEAN>
+__global__ void __launch_bounds__(256) roll4_kernel(float* __restrict__ x, int N, int T, int F, int J, int c, int w,
+                                                    const int* __restrict__ fmask, int n_fmask,
+                                                    const int* __restrict__ tmask, int n_tmask,
+                                                    float* __restrict__ partial) {
+  constexpr int NTAP = WARP ? (CUBIC ? 4 : 2) : 1;
+  constexpr int PF = RL_WR * RL_JMAX / 256;  // prefetch float4 per thread at the widest slab
+  // (HIP's float4 struct arrays stay in scratch; ext_vector_type ones are registers)
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  extern __shared__ v4f ring[];         // RL_RING x J
+  __shared__ float red[16];
+  __shared__ int tms[2 * RL_MAXM];      // utterance n's time masks: no global load inside the row loop
+  const int F4 = F >> 2, nslab = F4 / J;
+  // XCD-aware bijective remap (workgroup i runs on XCD i % 8): the slabs of
+  // an utterance — J * 16 B of every 128-B row line — go to one XCD, whose L2
+  // then fetches each line once
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int slab = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int n = slab / nslab, j0 = (slab - n * nslab) * J;
+  if ((int)threadIdx.x < 2 * n_tmask) tms[threadIdx.x] = tmask[2 * n * n_tmask + threadIdx.x];
+  const int RP = 256 / J;               // rows per pass
+  const int q = threadIdx.x % J, rp = threadIdx.x / J;
+  const bool act = rp < RP;
+  float* xn = x + (long long)n * T * F + 4 * (j0 + q);
+  const int H = WARP ? abs(c - w) + 3 : 0;
+  // the two segments' source scales (align_corners), once per workgroup
+  float scl[2] = {0.f, 0.f};
+  if constexpr (WARP) {
+#pragma unroll
+    for (int sg = 0; sg < 2; ++sg) {
+      const int in_rows = sg == 0 ? c : T - c, out_rows = sg == 0 ? w : T - w;
+      scl[sg] = out_rows > 1 ? (float)((double)(in_rows - 1) / (double)(out_rows - 1)) : 0.f;
+    }
+  }
+  const unsigned cm = act ? col_mask4(fmask, n, n_fmask, 4 * (j0 + q)) : 0u;
+  float s_all = 0.f, s_msk = 0.f;
+  // rows [lo, hi) -> registers pf (row lo + rp + k * RP), then -> ring.
+  // Unconditional loads (rows past the range clamp onto row T - 1 and are not
+  // stashed): a conditional load per row compiled to a branch with a full
+  // vmcnt wait after each, serialising the prefetch.
+  v4f pf[PF];
+#define RL_FETCH(lo)                                                                  \
+  _Pragma("unroll") for (int k = 0; k < PF; ++k) {                                    \
+    const int r_ = min((lo) + rp + k * RP, T - 1);                                    \
+    pf[k] = *reinterpret_cast<const v4f*>(xn + (long long)r_ * F);                  \
+  }
+#define RL_STASH(lo, hi)                                                              \
+  _Pragma("unroll") for (int k = 0; k < PF; ++k) {                                    \
+    const int r_ = (lo) + rp + k * RP;                                                \
+    if (act && r_ < (hi)) ring[(r_ & (RL_RING - 1)) * J + q] = pf[k];                 \
+  }
+  int have = min(T, RL_WR + H);  // rows [0, have) staged
+  for (int lo = 0; lo < have; lo += RL_WR) {
+    RL_FETCH(lo);
+    RL_STASH(lo, min(have, lo + RL_WR));
+  }
+  __syncthreads();
+  for (int t0 = 0; t0 < T; t0 += RL_WR) {
+    // the next window's new rows, in flight under this window's compute
+    const int nlo = have, nhi = min(T, t0 + 2 * RL_WR + H);
+    RL_FETCH(nlo);
+    if (act) {
+      for (int t = t0 + rp; t < min(T, t0 + RL_WR); t += RP) {
+        v4f v;
+        if constexpr (WARP) {
+          const bool left = t < w;
+          const int in_rows = left ? c : T - c, out_rows = left ? w : T - w;
+          const int src0 = left ? 0 : c, dst = left ? t : t - w;
+          if (in_rows == out_rows) {
+            v = ring[((src0 + dst) & (RL_RING - 1)) * J + q];
+          } else {
+            const float real = scl[left ? 0 : 1] * (float)dst;
+            const float fl = floorf(real);
+            const float tt = real - fl;
+            const int i0 = (int)fl;
+            if constexpr (CUBIC) {
+              const float wt[4] = {cubic2(tt + 1.f), cubic1(tt), cubic1(1.f - tt), cubic2(2.f - tt)};
+              v = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+              for (int k = 0; k < NTAP; ++k) {
+                const int r = src0 + min(max(i0 - 1 + k, 0), in_rows - 1);
+                const v4f a = ring[(r & (RL_RING - 1)) * J + q];
+                v.x += wt[k] * a.x; v.y += wt[k] * a.y; v.z += wt[k] * a.z; v.w += wt[k] * a.w;
+              }
+            } else {
+              const float l1 = fminf(fmaxf(tt, 0.f), 1.f), l0 = 1.f - l1;
+              const int i1 = i0 + (i0 < in_rows - 1 ? 1 : 0);
+              const v4f a0 = ring[((src0 + i0) & (RL_RING - 1)) * J + q];
+              const v4f a1 = ring[((src0 + i1) & (RL_RING - 1)) * J + q];
+              v = v4f{l0 * a0.x + l1 * a1.x, l0 * a0.y + l1 * a1.y, l0 * a0.z + l1 * a1.z, l0 * a0.w + l1 * a1.w};
+            }
+          }
+        } else {
+          v = ring[(t & (RL_RING - 1)) * J + q];
+        }
+        if constexpr (MEAN) {
+          s_all += v.x + v.y + v.z + v.w;
+          s_msk += ((cm & 1) ? v.x : 0.f) + ((cm & 2) ? v.y : 0.f) + ((cm & 4) ? v.z : 0.f) + ((cm & 8) ? v.w : 0.f);
+        }
+        // masked cells are fixup4_kernel's: a time-masked row or a fully
+        // frequency-masked float4 is not written here
+        if (WARP && cm != 15u && !(n_tmask && in_masks(tms, 0, n_tmask, t)))
+          *reinterpret_cast<v4f*>(xn + (long long)t * F) = v;
+      }
+    }
+    __syncthreads();  // every read of the ring for this window is done
+    RL_STASH(nlo, nhi);
+    have = max(have, nhi);
+    __syncthreads();
+  }
+  if constexpr (MEAN) {
+    const float sa = block_sum(s_all, red);
+    const float sm = block_sum(s_msk, red);
+    const float nc = block_sum(act && rp == 0 ? (float)__builtin_popcount(cm) : 0.f, red);
+    if (threadIdx.x == 0) {
+      partial[3 * slab] = sa;
+      partial[3 * slab + 1] = sm;
+      partial[3 * slab + 2] = nc;
+    }
+  }
+#undef RL_FETCH
+#undef RL_STASH
+}
+
+// The masked cells after roll4_kernel: time-masked rows -> fill_t, the
+// frequency-masked cells of the other rows -> fill_f (0 without the mean
+// fill).  One workgroup per (utterance, FX_TR rows): the utterance's masked
+// columns are listed in LDS, then only masked cells are touched (a pass over
+// every cell checking the masks measured 40 us at config 2).  Every workgroup
+// reduces the roll partials in the same fixed order (deterministic, no
+// cross-workgroup hand-off).
+constexpr int FX_TR = 64, FX_FMAX = 1024;
+__global__ void __launch_bounds__(256) fixup4_kernel(float* __restrict__ x, int N, int T, int F,
+                                                     const int* __restrict__ fmask, int n_fmask,
+                                                     const int* __restrict__ tmask, int n_tmask,
+                                                     const float* __restrict__ partial, int nparts, int use_mean,
+                                                     long long n_fcells) {
+  __shared__ float fl[2];
+  __shared__ int fms[2 * RL_MAXM], tms[2 * RL_MAXM];
+  __shared__ short cols[FX_FMAX];
+  __shared__ unsigned char trow[FX_TR];
+  __shared__ int ncol;
+  const int ntile = (T + FX_TR - 1) / FX_TR;
+  const int n = blockIdx.x / ntile, r0 = (blockIdx.x - n * ntile) * FX_TR;
+  if ((int)threadIdx.x < 2 * n_fmask) fms[threadIdx.x] = fmask[2 * n * n_fmask + threadIdx.x];
+  if ((int)threadIdx.x < 2 * n_tmask) tms[threadIdx.x] = tmask[2 * n * n_tmask + threadIdx.x];
+  __syncthreads();  // the mask tables
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  if (wv == 0 && use_mean) {
+    // the roll partials, one wave, fixed order (deterministic; every
+    // workgroup computes the same fills)
+    float a = 0.f, m = 0.f, nc = 0.f;
+    for (int i = ln; i < nparts; i += 64) {
+      a += partial[3 * i];
+      m += partial[3 * i + 1];
+      nc += partial[3 * i + 2];
+    }
+    a = wave_sum_v(a);
+    m = wave_sum_v(m);
+    nc = wave_sum_v(nc);
+    if (ln == 0) {
+      const double total = (double)N * T * F;
+      const double cells = n_fcells >= 0 ? (double)n_fcells : (double)nc * T;
+      const float mean1 = (float)(a / total);
+      fl[0] = mean1;
+      fl[1] = (float)(((double)a - (double)m + (double)mean1 * cells) / total);
+    }
+  } else if (wv == 1) {
+    // this utterance's masked columns, ascending; the running count stays in
+    // wave-uniform registers
+    int base = 0;
+    for (int f0 = 0; f0 < F; f0 += 64) {
+      const int f = f0 + ln;
+      const bool m = f < F && n_fmask && in_masks(fms, 0, n_fmask, f);
+      const unsigned long long bal = __ballot(m);
+      if (m) cols[base + __builtin_popcountll(bal & ((1ull << ln) - 1))] = (short)f;
+      base += __builtin_popcountll(bal);
+    }
+    if (ln == 0) ncol = base;
+  } else if (wv == 2) {
+    for (int i = ln; i < FX_TR; i += 64)
+      trow[i] = (unsigned char)(r0 + i < T && n_tmask && in_masks(tms, 0, n_tmask, r0 + i));
+  }
+  __syncthreads();
+  const float fill_f = use_mean ? fl[0] : 0.f, fill_t = use_mean ? fl[1] : 0.f;
+  const int F4 = F >> 2, nc = ncol, nr = min(FX_TR, T - r0);
+  float* xt = x + ((long long)n * T + r0) * F;
+  // time-masked rows: whole rows
+  for (int i = threadIdx.x; i < nr * F4; i += blockDim.x) {
+    const int r = i / F4;
+    if (trow[r]) *reinterpret_cast<float4*>(xt + (long long)r * F + 4 * (i - r * F4)) = make_float4(fill_t, fill_t, fill_t, fill_t);
+  }
+  // the masked columns of the other rows
+  for (int i = threadIdx.x; i < nr * nc; i += blockDim.x) {
+    const int r = i / nc;
+    if (!trow[r]) xt[(long long)r * F + cols[i - r * nc]] = fill_f;
+  }
+}
+
+// slab width (float4 columns) of roll4_kernel: the widest divisor of F4 up to
+// RL_JMAX (the ring is RL_RING x J x 16 B of LDS: 64 KB at J = 4)
+__host__ __forceinline__ int roll_slab(int N, int F4) {
+  (void)N;
+  for (int J = RL_JMAX; J >= 1; --J)
+    if (F4 % J == 0) return J;
+  return 0;
+}
+
 // the two fills from the partial sums, once (fixed order: deterministic);
 // 1024 threads, four independent pair loads in flight per thread
 __global__ void __launch_bounds__(1024) fills_kernel(const float* __restrict__ partial, int nparts, int N, int T,
@@ -430,12 +656,65 @@ __global__ void __launch_bounds__(256) apply4_kernel(const float* src, float* x,
 //   partial: scratch of 2 * N * ceil(T/4) + 2 floats (when use_mean);
 //   n_fcells: number of frequency-masked cells (the second mean's count); < 0: counted on the device
 //             from fmask.
+namespace {
+bool roll_route(int N, int F, int c, int w, int n_fmask, int n_tmask, bool x_aligned) {
+  return F % 4 == 0 && F <= FX_FMAX && x_aligned && (c < 0 || abs(c - w) + 3 <= RL_HMAX) && roll_slab(N, F >> 2) > 0 &&
+         n_fmask <= RL_MAXM && n_tmask <= RL_MAXM;
+}
+}  // namespace
+
+// 1 when sbk_specaugment needs its `tmp` scratch for these arguments (the
+// warp of the copy path), 0 when it runs in place without one
+SBK_API int sbk_specaugment_needs_scratch(int N, int T, int F, int c, int w, int n_fmask, int n_tmask, int x_aligned) {
+  (void)T;
+  return c >= 0 && !roll_route(N, F, c, w, n_fmask, n_tmask, x_aligned != 0);
+}
+
 SBK_API int sbk_specaugment(float* x, int N, int T, int F, int c, int w, int warp_mode, float* tmp, const int* fmask,
                             int n_fmask,
                             const int* tmask, int n_tmask, int use_mean, float* partial, long long n_fcells,
                             void* stream) {
   if (N <= 0 || T <= 0 || F <= 0 || warp_mode < 0 || warp_mode > 1) return SBK_ERR_ARG;
   hipStream_t s4 = (hipStream_t)stream;
+  if (roll_route(N, F, c, w, n_fmask, n_tmask, (reinterpret_cast<uintptr_t>(x) & 15) == 0)) {
+    // in place: roll4_kernel (x read once, unmasked cells written once) +
+    // fixup4_kernel (the masked cells); `partial`: 3 * N * (F/4) / J floats
+    const int J = roll_slab(N, F >> 2), nblk = N * ((F >> 2) / J);
+    if (c >= 0 && (c <= 0 || c >= T || w <= 0 || w >= T)) return SBK_ERR_ARG;
+    if (use_mean && !partial) return SBK_ERR_ARG;
+    const size_t lds = (size_t)RL_RING * J * 16;
+    float* pp = use_mean ? partial : nullptr;
+#define SBK_ROLL(CU, WA, ME)                                                                                        \
+  do {                                                                                                              \
+    static bool attr = false; /* > 64 KB of LDS with the static arrays: opt in once */                              \
+    if (!attr) {                                                                                                    \
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&roll4_kernel<CU, WA, ME>),           \
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);               \
+      if (e != hipSuccess) return (int)e;                                                                           \
+      attr = true;                                                                                                  \
+    }                                                                                                               \
+    hipLaunchKernelGGL((roll4_kernel<CU, WA, ME>), dim3(nblk), dim3(256), lds, s4, x, N, T, F, J, c, w, fmask,      \
+                       n_fmask, tmask, n_tmask, pp);                                                                \
+  } while (0)
+    if (c >= 0) {
+      if (warp_mode == 0) {
+        if (use_mean) SBK_ROLL(true, true, true); else SBK_ROLL(true, true, false);
+      } else {
+        if (use_mean) SBK_ROLL(false, true, true); else SBK_ROLL(false, true, false);
+      }
+      SBK_CHECK_LAUNCH();
+    } else if (use_mean) {
+      SBK_ROLL(true, false, true);
+      SBK_CHECK_LAUNCH();
+    }
+#undef SBK_ROLL
+    if (n_fmask == 0 && n_tmask == 0) return 0;
+    const int fblk = N * ((T + FX_TR - 1) / FX_TR);
+    hipLaunchKernelGGL(fixup4_kernel, dim3(fblk), dim3(256), 0, s4, x, N, T, F, fmask, n_fmask, tmask, n_tmask,
+                       pp, nblk, use_mean, n_fcells);
+    SBK_CHECK_LAUNCH();
+    return 0;
+  }
   if (F % 4 == 0 && F <= 1024 &&
       ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(tmp) | reinterpret_cast<uintptr_t>(partial)) & 15) == 0) {
     // 4-wide path; `partial` must hold 2 * N * ceil(T/4) + 2 floats (the fills at its end)

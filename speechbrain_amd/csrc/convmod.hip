@@ -160,7 +160,11 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int fr = lane & 15, g = lane >> 4, fk = 8 * g;
   const int nblk = (a.T + CM_BM - 1) / CM_BM;
-  const int b = blockIdx.x / nblk, t0 = (blockIdx.x % nblk) * CM_BM;
+  // (an XCD-aware remap that put an utterance's consecutive tiles — which
+  // share halo rows — on one XCD measured equal: 30.4-30.5 vs 30.4-30.8 us,
+  // profiles/r04m_conv_xcd.log)
+  const int tile = blockIdx.x;
+  const int b = tile / nblk, t0 = (tile % nblk) * CM_BM;
   const int f0 = t0 - a.padL;  // frame of staged row 0
   const int nrows = CM_BM + a.K - 1;
   const long long ubase = (long long)b * a.T;

@@ -417,11 +417,6 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     __builtin_amdgcn_global_load_lds(gs, ls, 16, 3072, 0);
 #endif
   };
-#ifdef FFN_TILES_FIRST
-  // probe: the first two tiles ahead of the x rows (they then land first)
-  issue(0, 0);
-  issue(1, 1);
-#endif
   // ---- prologue.  Every HBM read of the launch is issued here, before the
   // weight stream: the residual x values of this lane's epilogue outputs
   // (held in VGPRs through the main loop; rows clamped, masked at the end) and
@@ -451,14 +446,10 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   const bool b1t = tid * 4 < a.H;
   if (b1t) b1v = gld4(a.b1 + tid * 4);
   if (CHAIN && b1t) b1bv = gld4(a.b1b + tid * 4);
-#ifdef FFN_TILES_FIRST
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#else
   issue(0, 0);
   issue(1, 1);
   // every load above has landed; the two tiles stay in flight
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB * GL) : "memory");
-#endif
 #pragma unroll
   for (int j = 0; j < T; ++j)
 #pragma unroll

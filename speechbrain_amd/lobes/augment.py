@@ -28,9 +28,13 @@ def specaugment_(x: torch.Tensor, N: int, T: int, F: int, c: int, w: int, fm: Op
     the batch-mean fill when use_mean (augment.py:116-201)."""
     n_f = fm.shape[1] if fm is not None else 0
     n_t = tm.shape[1] if tm is not None else 0
-    tmp = torch.empty_like(x) if c >= 0 else None
-    # partial sums (+ the two fills of the 4-wide path at the end)
-    partial = torch.empty(2 * N * ((T + 3) // 4) + 4, device=x.device, dtype=torch.float32) if use_mean else None
+    # the in-place path (the float4 shapes of the recipe) needs no scratch copy
+    tmp = (torch.empty_like(x) if lib().sbk_specaugment_needs_scratch(N, T, F, c, w, n_f, n_t,
+                                                                       int(x.data_ptr() % 16 == 0)) else None)
+    # partial sums: the copy path's 2 per 4 rows (+ its two fills), the
+    # in-place path's 3 per column slab
+    npart = max(2 * N * ((T + 3) // 4), 3 * N * (F // 4))
+    partial = torch.empty(npart + 4, device=x.device, dtype=torch.float32) if use_mean else None
     rc = lib().sbk_specaugment(ptr(x), N, T, F, c, w, int(warp_mode), ptr(tmp), ptr(fm), n_f, ptr(tm), n_t,
                                int(use_mean),
                                ptr(partial), n_fcells, stream_of(x))

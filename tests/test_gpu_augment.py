@@ -93,25 +93,34 @@ def test_specaugment_4d_and_short(dev):
     assert_close(y, ref, rtol=1e-5, name="short")
 
 
-@pytest.mark.parametrize("N,T,F,win,zero", [
-    (32, 1501, 240, 5, False),   # config 2 (Δ/ΔΔ features), the float4 kernels
-    (3, 200, 240, 5, True),      # zero fill
-    (2, 300, 80, 40, False),     # a wide warp window
-    (2, 120, 42, 5, False),      # F % 4 != 0: the scalar kernels
+@pytest.mark.parametrize("N,T,F,win,zero,warp", [
+    (32, 1501, 240, 5, False, True),   # config 2 (Δ/ΔΔ features): in place, no scratch
+    (3, 200, 240, 5, True, True),      # zero fill, in place
+    (2, 300, 80, 40, False, True),     # a wide warp window (|c - w| <= 40: still in place)
+    (2, 400, 80, 90, False, True),     # a wider window, still in place
+    (2, 1200, 40, 300, False, True),   # |c - w| may pass the in-place halo (253): the copy path
+    (2, 700, 240, 5, False, False),    # no warp: sums only, then the masked cells
+    (1, 97, 40, 5, False, True),       # one utterance, narrow slabs
+    (2, 120, 42, 5, False, True),      # F % 4 != 0: the scalar kernels
 ])
-def test_specaugment_paths_vs_oracle(dev, N, T, F, win, zero):
-    """The float4 and scalar routes of sbk_specaugment, with the second mean's
-    masked-cell count taken on the device from the mask table, against the
-    oracle."""
+def test_specaugment_paths_vs_oracle(dev, N, T, F, win, zero, warp):
+    """The in-place (x read once, masked cells written after the means), copy
+    and scalar routes of sbk_specaugment, with the second mean's masked-cell
+    count taken on the device, against the oracle."""
+    from speechbrain_amd._lib import lib
     from speechbrain_amd.lobes.augment import SpecAugment
     x = torch.randn(N, T, F, generator=torch.Generator().manual_seed(T + F)) * 10 - 40
-    kw = dict(time_warp=True, time_warp_window=win, freq_mask=True, n_freq_mask=2, time_mask=True, n_time_mask=2,
+    kw = dict(time_warp=warp, time_warp_window=win, freq_mask=True, n_freq_mask=2, time_mask=True, n_time_mask=2,
               replace_with_zero=zero, freq_mask_width=min(30, F // 2), time_mask_width=40)
-    for seed in (11, 12):
+    for seed in (11, 12, 13):
         torch.manual_seed(seed)
-        y = SpecAugment(**kw)(x.clone().to(dev))
+        aug = SpecAugment(**kw)
+        y = aug(x.clone().to(dev))
+        c, w, _, _ = aug.last_draws
+        in_place = F % 4 == 0 and (c < 0 or abs(c - w) + 3 <= 256)
+        assert lib().sbk_specaugment_needs_scratch(N, T, F, c, w, 2, 2, 1) == int(c >= 0 and not in_place)
         torch.manual_seed(seed)
-        ref = OA.spec_augment(x.clone(), time_warp_on=True, time_warp_window=win, freq_mask=True, n_freq_mask=2,
+        ref = OA.spec_augment(x.clone(), time_warp_on=warp, time_warp_window=win, freq_mask=True, n_freq_mask=2,
                               time_mask=True, n_time_mask=2, replace_with_zero=zero,
                               freq_mask_width=kw["freq_mask_width"], time_mask_width=40)
         assert_close(y, ref, rtol=1e-5, name=f"N{N} T{T} F{F} win{win} seed{seed}")
