@@ -349,7 +349,7 @@ __global__ void __launch_bounds__(256) warp4_kernel(const float* __restrict__ x,
 // column slab).  Per workgroup partials [sum, freq-masked sum, freq-masked
 // columns of the slab] feed the means.
 #ifndef SBK_RL_JMAX
-#define SBK_RL_JMAX 4  // (probe builds vary the slab width)
+#define SBK_RL_JMAX 2  // (probe builds vary the slab width: 2 measured 39.2-39.7 us, 4 41.3-41.4, 1 48.6-49.2 per call)
 #endif
 constexpr int RL_RING = 1024, RL_WR = 512, RL_HMAX = (RL_RING - RL_WR) / 2, RL_MAXM = 32, RL_JMAX = SBK_RL_JMAX;
 template <bool CUBIC, bool WARP, bool MEAN>
@@ -404,18 +404,20 @@ __global__ void __launch_bounds__(256) roll4_kernel(float* __restrict__ x, int N
     const int r_ = (lo) + rp + k * RP;                                                \
     if (act && r_ < (hi)) ring[(r_ & (RL_RING - 1)) * J + q] = pf[k];                 \
   }
-  int have = min(T, RL_WR + H);  // rows [0, have) staged
-  for (int lo = 0; lo < have; lo += RL_WR) {
-    RL_FETCH(lo);
-    RL_STASH(lo, min(have, lo + RL_WR));
-  }
+  // rows [0, have) are staged; a window computes the output rows whose taps
+  // are all staged, [t0, have - H) (all remaining rows once have = T), while
+  // the next RL_WR input rows are in flight; a stash overwrites ring rows
+  // below have - RL_RING + RL_WR <= have - 2H, which no later window reads
+  int have = min(T, RL_WR);
+  RL_FETCH(0);
+  RL_STASH(0, have);
   __syncthreads();
-  for (int t0 = 0; t0 < T; t0 += RL_WR) {
-    // the next window's new rows, in flight under this window's compute
-    const int nlo = have, nhi = min(T, t0 + 2 * RL_WR + H);
-    RL_FETCH(nlo);
+  for (int t0 = 0; t0 < T;) {
+    const int t1 = have >= T ? T : have - H;
+    const int nlo = have, nhi = min(T, have + RL_WR);
+    RL_FETCH(nlo);  // in flight under this window's compute
     if (act) {
-      for (int t = t0 + rp; t < min(T, t0 + RL_WR); t += RP) {
+      for (int t = t0 + rp; t < t1; t += RP) {
         v4f v;
         if constexpr (WARP) {
           const bool left = t < w;
@@ -460,7 +462,8 @@ __global__ void __launch_bounds__(256) roll4_kernel(float* __restrict__ x, int N
     }
     __syncthreads();  // every read of the ring for this window is done
     RL_STASH(nlo, nhi);
-    have = max(have, nhi);
+    have = nhi;
+    t0 = t1;
     __syncthreads();
   }
   if constexpr (MEAN) {
@@ -492,9 +495,10 @@ __global__ void __launch_bounds__(256) fixup4_kernel(float* __restrict__ x, int 
                                                      long long n_fcells) {
   __shared__ float fl[2];
   __shared__ int fms[2 * RL_MAXM], tms[2 * RL_MAXM];
-  __shared__ short cols[FX_FMAX];
+  __shared__ short cols[FX_FMAX];    // masked columns of partly masked float4s (scalar stores)
+  __shared__ short quads[FX_FMAX / 4];  // fully masked float4s (16-B stores)
   __shared__ unsigned char trow[FX_TR];
-  __shared__ int ncol;
+  __shared__ int ncol, nquad;
   const int ntile = (T + FX_TR - 1) / FX_TR;
   const int n = blockIdx.x / ntile, r0 = (blockIdx.x - n * ntile) * FX_TR;
   if ((int)threadIdx.x < 2 * n_fmask) fms[threadIdx.x] = fmask[2 * n * n_fmask + threadIdx.x];
@@ -521,31 +525,48 @@ __global__ void __launch_bounds__(256) fixup4_kernel(float* __restrict__ x, int 
       fl[1] = (float)(((double)a - (double)m + (double)mean1 * cells) / total);
     }
   } else if (wv == 1) {
-    // this utterance's masked columns, ascending; the running count stays in
-    // wave-uniform registers
-    int base = 0;
-    for (int f0 = 0; f0 < F; f0 += 64) {
-      const int f = f0 + ln;
-      const bool m = f < F && n_fmask && in_masks(fms, 0, n_fmask, f);
-      const unsigned long long bal = __ballot(m);
-      if (m) cols[base + __builtin_popcountll(bal & ((1ull << ln) - 1))] = (short)f;
-      base += __builtin_popcountll(bal);
+    // this utterance's masked float4s: fully masked ones (one 16-B store per
+    // row) and the masked columns of partly masked ones (4-B stores); the
+    // running counts stay in wave-uniform registers
+    int b4 = 0, b1 = 0;
+    const int F4 = F >> 2;
+    for (int q0 = 0; q0 < F4; q0 += 64) {
+      const int q = q0 + ln;
+      const unsigned cm = q < F4 ? col_mask4(fms, 0, n_fmask, 4 * q) : 0u;
+      const unsigned long long full = __ballot(cm == 15u);
+      if (cm == 15u) quads[b4 + __builtin_popcountll(full & ((1ull << ln) - 1))] = (short)q;
+      b4 += __builtin_popcountll(full);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool m = cm != 15u && (cm >> e & 1u);
+        const unsigned long long bal = __ballot(m);
+        if (m) cols[b1 + __builtin_popcountll(bal & ((1ull << ln) - 1))] = (short)(4 * q + e);
+        b1 += __builtin_popcountll(bal);
+      }
     }
-    if (ln == 0) ncol = base;
+    if (ln == 0) {
+      ncol = b1;
+      nquad = b4;
+    }
   } else if (wv == 2) {
     for (int i = ln; i < FX_TR; i += 64)
       trow[i] = (unsigned char)(r0 + i < T && n_tmask && in_masks(tms, 0, n_tmask, r0 + i));
   }
   __syncthreads();
   const float fill_f = use_mean ? fl[0] : 0.f, fill_t = use_mean ? fl[1] : 0.f;
-  const int F4 = F >> 2, nc = ncol, nr = min(FX_TR, T - r0);
+  const int F4 = F >> 2, nc = ncol, nq = nquad, nr = min(FX_TR, T - r0);
   float* xt = x + ((long long)n * T + r0) * F;
   // time-masked rows: whole rows
   for (int i = threadIdx.x; i < nr * F4; i += blockDim.x) {
     const int r = i / F4;
     if (trow[r]) *reinterpret_cast<float4*>(xt + (long long)r * F + 4 * (i - r * F4)) = make_float4(fill_t, fill_t, fill_t, fill_t);
   }
-  // the masked columns of the other rows
+  // the frequency-masked cells of the other rows
+  for (int i = threadIdx.x; i < nr * nq; i += blockDim.x) {
+    const int r = i / nq;
+    if (!trow[r])
+      *reinterpret_cast<float4*>(xt + (long long)r * F + 4 * quads[i - r * nq]) = make_float4(fill_f, fill_f, fill_f, fill_f);
+  }
   for (int i = threadIdx.x; i < nr * nc; i += blockDim.x) {
     const int r = i / nc;
     if (!trow[r]) xt[(long long)r * F + cols[i - r * nc]] = fill_f;
