@@ -208,10 +208,15 @@ class _FastOp:
     inputs that require grad (its autograd edge).  Attribute access
     (register_fake, register_autograd, ...) reaches the op."""
 
-    def __init__(self, opdef):
+    def __init__(self, opdef, mutates_args=()):
+        import inspect
         self._def = opdef
         self._body = opdef._init_fn
         self._op = None
+        # positions of the mutated arguments: their version counters are
+        # bumped as the dispatcher would (autograd's saved-tensor checks)
+        names = list(inspect.signature(opdef._init_fn).parameters)
+        self._mut = tuple((names.index(m), m) for m in mutates_args)
 
     def __call__(self, *args, **kw):
         if (torch.compiler.is_compiling() or torch.jit.is_tracing()
@@ -222,7 +227,12 @@ class _FastOp:
             if self._op is None:
                 self._op = getattr(torch.ops.sbk, self._def._name)
             return self._op(*args, **kw)
-        return self._body(*args, **kw)
+        out = self._body(*args, **kw)
+        for i, m in self._mut:
+            t = args[i] if i < len(args) else kw.get(m)
+            if isinstance(t, torch.Tensor):
+                torch.autograd.graph.increment_version(t)
+        return out
 
     def __getattr__(self, name):
         return getattr(self._def, name)
@@ -234,7 +244,7 @@ _OPS = {}
 def custom_op(qualname, mutates_args):
     """torch.library.custom_op for the sbk namespace, returning a _FastOp."""
     def deco(fn):
-        op = _FastOp(torch.library.custom_op(qualname, mutates_args=mutates_args)(fn))
+        op = _FastOp(torch.library.custom_op(qualname, mutates_args=mutates_args)(fn), mutates_args)
         _OPS[qualname.split("::", 1)[1]] = op
         return op
     return deco
