@@ -7,6 +7,9 @@ import os
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import speechbrain_amd._lib as _L  # noqa: E402
+if os.environ.get("SBK_PROBE_LIB"):
+    _L.LIB_PATH = os.path.abspath(os.environ["SBK_PROBE_LIB"])  # A/B of a probe build (never the product)
 from speechbrain_amd import _w2v, _enc  # noqa: E402
 
 
