@@ -508,11 +508,25 @@ __global__ void __launch_bounds__(256) fixup4_kernel(float* __restrict__ x, int 
   if (wv == 0 && use_mean) {
     // the roll partials, one wave, fixed order (deterministic; every
     // workgroup computes the same fills)
+    // eight triples in flight per lane (a loop of one dependent load round
+    // per 64 triples paid ~10 us of L2 latency at config 2's 960 partials)
     float a = 0.f, m = 0.f, nc = 0.f;
-    for (int i = ln; i < nparts; i += 64) {
-      a += partial[3 * i];
-      m += partial[3 * i + 1];
-      nc += partial[3 * i + 2];
+    for (int i0 = ln; i0 < nparts; i0 += 64 * 8) {
+      float pa[8], pm[8], pn[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = min(i0 + 64 * u, nparts - 1);
+        pa[u] = partial[3 * i];
+        pm[u] = partial[3 * i + 1];
+        pn[u] = partial[3 * i + 2];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (i0 + 64 * u < nparts) {
+          a += pa[u];
+          m += pm[u];
+          nc += pn[u];
+        }
     }
     a = wave_sum_v(a);
     m = wave_sum_v(m);

@@ -359,7 +359,10 @@ SBK_PROBE_BUFFER(g_ffn_tl, 16, 256)
 template <int D, int ACT, bool PROJ, bool CHAIN>
 __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   constexpr int BM = FFN_BM, HC = 256, NW = FFN_NW, NT = FFN_NT;
-  constexpr int XS = D + 16, HS = HC + 16;   // LDS row strides (elements), +32 B pad: conflict-free b128 reads
+#ifndef SBK_FFN_PAD
+#define SBK_FFN_PAD 16  // (probe builds vary the row pad)
+#endif
+  constexpr int XS = D + SBK_FFN_PAD, HS = HC + SBK_FFN_PAD;   // LDS row strides (elements), +32 B pad: conflict-free b128 reads
   constexpr int MT = BM / 16;                // m-tiles (3)
   constexpr int T = 256 / 16 / FFN_NW;       // 16-row weight tiles per wave (HC/16/NW = D/16/NW)
   constexpr int BK = 64;                     // K per step: one 128-B line per weight row
@@ -874,7 +877,8 @@ template <int D>
 size_t ffn_lds(int H, bool chain) {
   // 2-slot weight ring, Xn, two hidden-chunk buffers, b1 (two with CHAIN), the row-reduction scratch,
   // the epilogue parameter rows
-  return ((size_t)2 * 256 * 64 + (size_t)FFN_BM * (D + 16) + (size_t)2 * FFN_BM * (256 + 16)) * sizeof(bf16_t) +
+  return ((size_t)2 * 256 * 64 + (size_t)FFN_BM * (D + SBK_FFN_PAD) + (size_t)2 * FFN_BM * (256 + SBK_FFN_PAD)) *
+             sizeof(bf16_t) +
          (size_t)(chain ? 2 : 1) * H * 4 + (size_t)FFN_NW * FFN_BM * 4 + (size_t)FFN_NW * D * 4;
 }
 
