@@ -1044,6 +1044,9 @@ constexpr int RF_SPAN = 1536;                  // staged samples per wave (6 KB:
 static_assert(RF_SPAN <= 2 * RF_WS, "the span fits the wave's regions");
 constexpr int RF_LW = 36;                      // dense mel row: 16-B aligned start + up to 33 bins
 typedef float rf4 __attribute__((ext_vector_type(4)));
+#ifndef SBK_RF_TRIPCH
+#define SBK_RF_TRIPCH 0                        // per-trip mel chunk counts (probe)
+#endif
 #ifndef SBK_RF_WGS_PER_CU
 #define SBK_RF_WGS_PER_CU 3                    // persistent grid: workgroups per CU (LDS: three fit)
 #endif
@@ -1217,6 +1220,17 @@ __global__ void __launch_bounds__(RF_NT, SBK_RF_MINW) spec_reg_kernel(SpecArgs a
       }
       __syncthreads();  // every read of mstart above is done
       for (int i = tid; i < a.M; i += RF_NT) mstart[i] &= ~3;
+#if SBK_RF_TRIPCH
+      // 16-B chunks per mel trip (filters 16 t .. 16 t + 15): the largest of
+      // its filters' own counts, so a trip skips the trailing all-zero chunks
+      // of the dense rows (wave-uniform; mel_off's table slots are free now)
+      for (int t = tid; 16 * t < a.M; t += RF_NT) {
+        int c = 0;
+        for (int jm = 16 * t; jm < min(16 * t + 16, a.M); ++jm)
+          c = max(c, ((a.mel_start[jm] & 3) + a.mel_len[jm] + 3) >> 2);
+        moff_s[t] = c;
+      }
+#endif
     }
   }
   __syncthreads();
@@ -1364,7 +1378,7 @@ __global__ void __launch_bounds__(RF_NT, SBK_RF_MINW) spec_reg_kernel(SpecArgs a
     const float* P0 = reinterpret_cast<const float*>(fr + w * RF_WS);
     float* obase = a.out + ((long long)bf * a.T + t0) * a.M;
     const int f = lane & 7;  // the lane's frame; filters jm = lane / 8 + 8 i
-    auto mel = [&](int jm) __attribute__((always_inline)) {
+    auto mel = [&](int jm, int nch) __attribute__((always_inline)) {
       float acc = 0.f;
       if (lw) {
         // dense rows from the filter's 16-B aligned first bin, zero weights
@@ -1373,7 +1387,7 @@ __global__ void __launch_bounds__(RF_NT, SBK_RF_MINW) spec_reg_kernel(SpecArgs a
         const rf4* wq = reinterpret_cast<const rf4*>(wd + jm * RF_LW);
 #pragma unroll
         for (int c = 0; c < RF_LW / 4; ++c) {
-          if (4 * c < lw) {
+          if (c < nch) {
             const rf4 pv = pf[c], wv = wq[c];
             acc = fmaf(pv[0], wv[0], acc);
             acc = fmaf(pv[1], wv[1], acc);
@@ -1399,13 +1413,22 @@ __global__ void __launch_bounds__(RF_NT, SBK_RF_MINW) spec_reg_kernel(SpecArgs a
       }
     };
     // two filters per trip: their LDS round trips overlap
+    // (SBK_RF_TRIPCH: chunk count per trip from the table stage, else lw / 4)
+    auto trip_ch = [&](int t) __attribute__((always_inline)) {
+#if SBK_RF_TRIPCH
+      return lw ? __builtin_amdgcn_readfirstlane(moff_s[t]) : 0;
+#else
+      return lw >> 2;
+#endif
+    };
     int jm = lane >> 3;
     for (; jm + 8 < a.M; jm += 16) {
-      const float a0 = mel(jm), a1 = mel(jm + 8);
+      const int nch = trip_ch(jm >> 4);
+      const float a0 = mel(jm, nch), a1 = mel(jm + 8, nch);
       emit(jm, a0);
       emit(jm + 8, a1);
     }
-    if (jm < a.M) emit(jm, mel(jm));
+    if (jm < a.M) emit(jm, mel(jm, trip_ch(jm >> 4)));
     if (a.log_mel) {
       lmax = wave_max(lmax);
       if (lane == 0) a.slot_max[(long long)bf * nwb + slot] = lmax;
