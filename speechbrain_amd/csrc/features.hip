@@ -1045,7 +1045,7 @@ static_assert(RF_SPAN <= 2 * RF_WS, "the span fits the wave's regions");
 constexpr int RF_LW = 36;                      // dense mel row: 16-B aligned start + up to 33 bins
 typedef float rf4 __attribute__((ext_vector_type(4)));
 #ifndef SBK_RF_TRIPCH
-#define SBK_RF_TRIPCH 0                        // per-trip mel chunk counts (probe)
+#define SBK_RF_TRIPCH 1                        // per-trip mel chunk counts (0: the dense width for every trip)
 #endif
 #ifndef SBK_RF_WGS_PER_CU
 #define SBK_RF_WGS_PER_CU 3                    // persistent grid: workgroups per CU (LDS: three fit)
