@@ -110,8 +110,8 @@ int sbk_context_window(const float* x, float* y, int N, int T, int F, int left, 
  * drawn on the host, filled with 0 or the running means (use_mean; `partial`
  * scratch of max(2*N*ceil(T/4), 3*N*(F/4)) + 4 floats, 16-B aligned;
  * n_fcells = number of frequency-masked cells, or < 0 to count them on the
- * device from the mask table).  F % 4 == 0 with 16-B aligned x, |c - w| <= 61
- * and <= 32 masks of each kind runs in place with no copy (x read once, the
+ * device from the mask table).  F % 4 == 0, F <= 1024 with 16-B aligned x,
+ * |c - w| <= 253 and <= 32 masks of each kind runs in place with no copy (x read once, the
  * unmasked cells written once, the masked cells written after the means);
  * otherwise the warp goes through `tmp` (a copy of x) —
  * sbk_specaugment_needs_scratch says which. */
@@ -254,9 +254,12 @@ int sbk_ffn_image(const void* w1, const void* w2, const void* w1b, const void* w
  *   u = LNn(out) if gn (bf16 when u_bf16, else fp32).
  * x, out (M, D) fp32 (out may alias x); img = sbk_ffn_image(w1, w2) of
  * w1 (H, D), w2 (D, H) bf16; b1, b2 required (zeros when the Linear has no
- * bias); act as sbk_gemm (not GLU). */
+ * bias); act as sbk_gemm (not GLU).  img_elems: the image's size in bf16
+ * elements, which must equal sbk_ffn_image_elems(D, H, np, chain) of this
+ * call (SBK_ERR_ARG otherwise: an image built for another shape or for one
+ * block instead of a chain is refused, never read out of bounds). */
 int sbk_ffn(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0, const void* img,
-            const float* b1, int act, float slope, const float* b2, float alpha, const float* gp, const float* bp,
+            long long img_elems, const float* b1, int act, float slope, const float* b2, float alpha, const float* gp, const float* bp,
             float epsp, float* out, const float* gn, const float* bn, float epsn, void* u, int u_bf16, void* stream);
 
 /* sbk_ffn with a projection tail: with np > 0 (np % 256 == 0; img =
@@ -266,7 +269,7 @@ int sbk_ffn(const float* x, int M, int D, int H, const float* g0, const float* b
  * Conformer.py:186-197), replacing its QKV GEMM launch.  np == 0 behaves as
  * sbk_ffn. */
 int sbk_ffn_proj(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0, const void* img,
-                 const float* b1, int act, float slope, const float* b2, float alpha, const float* gp,
+                 long long img_elems, const float* b1, int act, float slope, const float* b2, float alpha, const float* gp,
                  const float* bp, float epsp, float* out, const float* gn, const float* bn, float epsn, void* u,
                  int u_bf16, int np, void* yp, void* stream);
 
@@ -281,7 +284,7 @@ int sbk_ffn_chain(const float* x, int M, int D, int H, int act, float slope, con
                   float eps0, const float* b1, const float* b2, float alpha, const float* gp, const float* bp,
                   float epsp, const float* g0b, const float* b0b, float eps0b, const float* b1b, const float* b2b,
                   float alphab, float* out, const float* gn, const float* bn, float epsn, void* u, int u_bf16,
-                  const void* img, int np, void* yp, void* stream);
+                  const void* img, long long img_elems, int np, void* yp, void* stream);
 
 /* LayerNorm (normalization.py:172-223; Conformer.py:178,194,340): one or two
  * chained LayerNorms over rows of x (M, D) fp32, D <= 1024. */
@@ -363,6 +366,33 @@ int sbk_mha_attention(const void* qkv, const unsigned char* kpm, int B, int T, i
                       void* stream);
 /* LDS bytes one attention workgroup needs (host-side capacity check). */
 long long sbk_relpos_attention_lds(int dtype_bf16, int T, int dh);
+
+/* RelPosMHAXL with query != key/value and q_len != k_len (csrc/xattn.hip):
+ * the attention core of attention.py:554-639 after the separate q / k / v
+ * projections (:554-564), with the reference's rel_shift (:468-483) of a
+ * (Lq, P) band (P = pos_embs rows, P//2 + 1 == Lk) and its mask_pos_future
+ * tril (:479-481).  q (B*Lq, ldq), k / v (B*Lk, ldk / ldv), pk (P, ldp), head
+ * h at columns h*dh; fp32 or bf16 (dtype_bf16).  pbu / pbv (H*dh) fp32; kpm
+ * (B, Lk) uint8 or null; am additive fp32 or null, element (b, h, i, j) at
+ * am[b*am_sb + h*am_sh + i*Lk + j].  out (B*Lq, ldo) in the input dtype;
+ * probs (B, H, Lq, Lk) fp32, the softmax; with p_drop > 0 attn receives the
+ * dropped probabilities (the reference's returned weights) and out = attn·V.
+ * dh <= 256; Lk, Lq, P within one workgroup's LDS. */
+int sbk_relpos_xattn_fwd(int dtype_bf16, const void* q, int ldq, const void* k, int ldk, const void* v, int ldv,
+                         const void* pk, int ldp, int P, const float* pbu, const float* pbv, const unsigned char* kpm,
+                         const float* am, long long am_sb, long long am_sh, int B, int Lq, int Lk, int H, int dh,
+                         float scale, int mask_pos_future, float p_drop, unsigned long long seed, void* out, int ldo,
+                         float* probs, float* attn, void* stream);
+/* Its backward from dO (B*Lq, lddo) in the input dtype and the forward's
+ * probs / seed: dq (B*Lq, H*dh), dk, dv (B*Lk, H*dh), dpk (P, H*dh) fp32;
+ * workspace G (B*H*Lq*Lk) fp32 (score gradients), dqu / dqv (B*Lq, H*dh)
+ * fp32 — the content and positional parts of dq, whose column sums are the
+ * pos_bias_u / pos_bias_v gradients. */
+int sbk_relpos_xattn_bwd(int dtype_bf16, const void* q, int ldq, const void* k, int ldk, const void* v, int ldv,
+                         const void* pk, int ldp, int P, const float* pbu, const float* pbv, const float* probs,
+                         const void* dO, int lddo, int B, int Lq, int Lk, int H, int dh, float scale,
+                         int mask_pos_future, float p_drop, unsigned long long seed, float* G, float* dqu, float* dqv,
+                         float* dq, float* dk, float* dv, float* dpk, void* stream);
 
 /* Whole Conformer convolution module in one launch (csrc/convmod.hip; Conformer.py:54-115,254-255),
  * bf16 MFMA: out = x + rowmask0(Linear2(Swish(LN1(dwconv_K(GLU(Linear1(LN0(x))))))));

@@ -96,6 +96,58 @@ def rel_pos_mha(x, pos_embs, sd, prefix, num_heads, key_padding_mask=None,
     return out, attn
 
 
+def rel_shift_cross(bd, mask_pos_future=False):
+    """attention.py:468-483 for any (q_len, P) band, in closed form.  The pad /
+    view / drop-row trick maps output element (i, j) to flat position
+    p = i*P + j + q_len of the left-padded (q_len, P+1) band: row r = p // (P+1),
+    column c = p % (P+1); c == 0 is the pad (0), else bd[r, c-1].  For
+    q_len == k_len, r == i always; for q_len > k_len some elements read the
+    next row(s), as the reference's view does.  mask_pos_future multiplies by
+    tril(ones, P - q_len) before the slice to j < P//2 + 1."""
+    Lq, P = bd.shape[-2], bd.shape[-1]
+    Lk = P // 2 + 1
+    i = torch.arange(Lq).view(-1, 1)
+    j = torch.arange(Lk).view(1, -1)
+    p = i * P + j + Lq
+    r, c = p // (P + 1), p % (P + 1)
+    padded = F.pad(bd, (1, 0))  # (..., Lq, P+1)
+    out = padded[..., r, c]
+    if mask_pos_future:
+        out = out * ((j - i) <= (P - Lq)).to(out.dtype)
+    return out
+
+
+def rel_pos_mha_cross(query, key, value, pos_embs, sd, prefix, num_heads, vbias=False, mask_pos_future=False,
+                      key_padding_mask=None, attn_mask=None):
+    """attention.py:485-639 with query != key/value (the separate q/k/v
+    projections of :554-564) and q_len != k_len.  Returns (out (B, Lq, E),
+    attn (B, H, Lq, Lk))."""
+    B, Lq, E = query.shape
+    Lk = key.shape[1]
+    dh = E // num_heads
+    wq, wk, wv = _p(sd, prefix + "in_proj_weight").chunk(3, dim=0)
+    q = F.linear(query, wq).view(B, Lq, num_heads, dh)
+    k = F.linear(key, wk).view(B, Lk, num_heads, dh)
+    v = F.linear(value, wv).view(B, Lk, num_heads, dh)
+    if vbias:
+        v = v + _p(sd, prefix + "value_bias_weight").view(1, 1, num_heads, dh)
+    p_k = F.linear(pos_embs, _p(sd, prefix + "linear_pos.weight")).view(1, -1, num_heads, dh)
+    u = _p(sd, prefix + "pos_bias_u").reshape(1, 1, num_heads, dh)
+    vb = _p(sd, prefix + "pos_bias_v").reshape(1, 1, num_heads, dh)
+    ac = torch.matmul((q + u).transpose(1, 2), k.permute(0, 2, 3, 1))
+    bd = rel_shift_cross(torch.matmul((q + vb).transpose(1, 2), p_k.permute(0, 2, 3, 1)), mask_pos_future)
+    score = (ac + bd) * (1.0 / math.sqrt(E))
+    if attn_mask is not None:
+        am = attn_mask.view(1, 1, Lq, Lk) if attn_mask.ndim == 2 else attn_mask.view(-1, num_heads, Lq, Lk)
+        score = score.masked_fill(am, -float("inf")) if am.dtype == torch.bool else score + am
+    if key_padding_mask is not None:
+        score = score.masked_fill(key_padding_mask.view(B, 1, 1, Lk), -float("inf"))
+    attn = F.softmax(score, dim=-1)
+    o = torch.matmul(attn, v.transpose(1, 2)).transpose(1, 2).reshape(B, Lq, E)
+    out = F.linear(o, _p(sd, prefix + "out_proj.weight"), _p(sd, prefix + "out_proj.bias"))
+    return out, attn
+
+
 def swish(x):
     return x * torch.sigmoid(x)  # activations.py:111-142 (beta=1)
 

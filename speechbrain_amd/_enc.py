@@ -3,7 +3,9 @@ conformer.hip, attention.hip).  Direct ctypes calls — no Python compute, no
 fallback; used by the nn.Module drop-ins and capturable into HIP graphs
 (no host sync, no allocation outside torch's caching allocator)."""
 import contextlib
+import ctypes
 import threading
+import weakref
 from typing import Optional
 
 import torch
@@ -287,15 +289,25 @@ def ffn_supported(D, H):
 class _ImageCache:
     """The fused FFN kernels stream their weights from one pre-laid-out image
     (sbk_ffn_image: 32-KB tiles in stream order, bank swizzle applied), built
-    once per set of weight tensors and reused while none of them changes.  An
-    entry keeps its source tensors referenced, so their storage cannot be
-    recycled into a false hit while it lives; LRU-bounded."""
+    once per set of weight tensors and reused while none of them changes.
+
+    An entry is keyed on its source tensors' (data_ptr, version) and holds
+    them only weakly: the bf16 copies a module's WeightCache replaces after
+    an optimizer step die with their last strong reference, and the entry
+    (image included) is dropped with them by the weakref callback — before
+    their storage can be recycled into a false hit, and without keeping dead
+    images alive across a train / validate loop.  An image is built on the
+    requesting stream; a hit from another stream waits on the event recorded
+    after the build.  LRU-bounded as a backstop."""
 
     def __init__(self, cap=64):
         self.cap = cap
         self._d = {}
 
-    def get(self, ws, np_):
+    def _drop(self, key):
+        self._d.pop(key, None)
+
+    def get(self, ws, np_, stream):
         key = tuple((w.data_ptr(), w._version) if w is not None else None for w in ws) + (np_,)
         hit = self._d.pop(key, None)
         if hit is None:
@@ -306,10 +318,15 @@ class _ImageCache:
                 raise SbkError(f"sbk_ffn_image_elems: unsupported shape D={D} H={H} np={np_}")
             img = torch.empty(n, device=w1.device, dtype=_bf16)
             check(lib().sbk_ffn_image(ptr(w1), ptr(w2), ptr(w1b), ptr(w2b), ptr(wp), D, H, np_, ptr(img),
-                                      stream_of(w1)), "sbk_ffn_image")
-            hit = (img, ws)
+                                      ctypes.c_void_p(stream.cuda_stream)), "sbk_ffn_image")
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            refs = tuple(weakref.ref(w, lambda _r, k=key: self._drop(k)) for w in ws if w is not None)
+            hit = (img, refs, ev, stream.cuda_stream)
             if len(self._d) >= self.cap:
                 self._d.pop(next(iter(self._d)))
+        elif hit[3] != stream.cuda_stream:
+            stream.wait_event(hit[2])
         self._d[key] = hit
         return hit[0]
 
@@ -323,7 +340,8 @@ def ffn_image(w1, w2, w1b=None, w2b=None, wp=None):
     for t in (w1, w2, w1b, w2b, wp):
         if t is not None and (t.dtype != _bf16 or not t.is_contiguous()):
             raise TypeError("ffn_image: contiguous bf16 weights")
-    return _FFN_IMAGES.get((w1, w2, w1b, w2b, wp), 0 if wp is None else wp.shape[0])
+    img = _FFN_IMAGES.get((w1, w2, w1b, w2b, wp), 0 if wp is None else wp.shape[0], torch.cuda.current_stream(w1.device))
+    return img
 
 
 @custom_op("sbk::ffn", mutates_args=())
@@ -336,8 +354,8 @@ def _ffn_op(x: torch.Tensor, g0: torch.Tensor, b0: torch.Tensor, e0: float, w1: 
     img = ffn_image(w1, w2)
     out = torch.empty_like(x)
     u = torch.empty(M, D, device=x.device, dtype=_bf16 if next_bf16 else _f32) if gn is not None else None
-    rc = lib().sbk_ffn(ptr(x), M, D, H, ptr(g0), ptr(b0), float(e0), ptr(img), ptr(b1), act, float(slope), ptr(b2),
-                       float(alpha), ptr(gp), ptr(bp), float(ep), ptr(out), ptr(gn), ptr(bn), float(en),
+    rc = lib().sbk_ffn(ptr(x), M, D, H, ptr(g0), ptr(b0), float(e0), ptr(img), img.numel(), ptr(b1), act,
+                       float(slope), ptr(b2), float(alpha), ptr(gp), ptr(bp), float(ep), ptr(out), ptr(gn), ptr(bn), float(en),
                        ptr(u), int(next_bf16), stream_of(x))
     check(rc, "sbk_ffn")
     return out, (u if u is not None else x.new_empty(0))
@@ -359,8 +377,8 @@ def _ffn_proj_op(x: torch.Tensor, g0: torch.Tensor, b0: torch.Tensor, e0: float,
     img = ffn_image(w1, w2, wp=wp)
     out = torch.empty_like(x)
     y = torch.empty(M, NP, device=x.device, dtype=_bf16)
-    rc = lib().sbk_ffn_proj(ptr(x), M, D, H, ptr(g0), ptr(b0), float(e0), ptr(img), ptr(b1), act, float(slope),
-                            ptr(b2), float(alpha), ptr(gp), ptr(bp), float(ep), ptr(out), ptr(gn), ptr(bn),
+    rc = lib().sbk_ffn_proj(ptr(x), M, D, H, ptr(g0), ptr(b0), float(e0), ptr(img), img.numel(), ptr(b1), act,
+                            float(slope), ptr(b2), float(alpha), ptr(gp), ptr(bp), float(ep), ptr(out), ptr(gn), ptr(bn),
                             float(en), None, 1, NP, ptr(y), stream_of(x))
     check(rc, "sbk_ffn_proj")
     return out, y
@@ -399,7 +417,7 @@ def _ffn_chain_op(x: torch.Tensor, act: int, slope: float, g0: torch.Tensor, b0:
     y = torch.empty(M, NP, device=x.device, dtype=_bf16)
     rc = lib().sbk_ffn_chain(ptr(x), M, D, H, act, float(slope), ptr(g0), ptr(b0), float(e0), ptr(b1), ptr(b2),
                              float(alpha), ptr(gp), ptr(bp), float(ep), ptr(g0b), ptr(b0b), float(e0b), ptr(b1b),
-                             ptr(b2b), float(alphab), ptr(out), ptr(gn), ptr(bn), float(en), None, 1, ptr(img), NP,
+                             ptr(b2b), float(alphab), ptr(out), ptr(gn), ptr(bn), float(en), None, 1, ptr(img), img.numel(), NP,
                              ptr(y), stream_of(x))
     check(rc, "sbk_ffn_chain")
     return out, y
@@ -619,25 +637,27 @@ def _(qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale, need_probs, am, am_sb, am_sh):
             qkv.new_empty(B, H, T, T, dtype=_f32) if need_probs else qkv.new_empty(0, dtype=_f32))
 
 
-def attn_mask_arg(attn_mask, B, T, H, device):
+def attn_mask_arg(attn_mask, B, T, H, device, Lk=None):
     """RelPosMHAXL's attn_mask (attention.py:598-611) as the kernel's additive
-    fp32 mask: (mask (T, T) or (B|1, H, T, T), batch stride, head stride),
-    bool masks as 0 / -inf (masked_fill(-inf) == adding -inf); None -> None."""
+    fp32 mask: (mask (Lq, Lk) or (B|1, H, Lq, Lk), batch stride, head stride),
+    bool masks as 0 / -inf (masked_fill(-inf) == adding -inf); None -> None.
+    Lq = T; Lk defaults to T (self-attention)."""
     if attn_mask is None:
         return None
+    Lk = T if Lk is None else Lk
     m = attn_mask.to(device)
     if m.dtype == torch.bool:
         m = torch.zeros(m.shape, device=device, dtype=_f32).masked_fill_(m, -float("inf"))
     else:
         m = m.to(_f32)
     if m.dim() == 2:
-        if tuple(m.shape) != (T, T):
-            raise ValueError(f"attn_mask {tuple(m.shape)} != ({T}, {T})")
+        if tuple(m.shape) != (T, Lk):
+            raise ValueError(f"attn_mask {tuple(m.shape)} != ({T}, {Lk})")
         return m.contiguous(), 0, 0
-    m = m.reshape(-1, H, T, T).contiguous()  # the reference's view(-1, num_heads, qlen, klen)
+    m = m.reshape(-1, H, T, Lk).contiguous()  # the reference's view(-1, num_heads, qlen, klen)
     if m.shape[0] not in (1, B):
         raise ValueError(f"attn_mask batch {m.shape[0]} does not broadcast to {B}")
-    return m, (H * T * T if m.shape[0] == B else 0), T * T
+    return m, (H * T * Lk if m.shape[0] == B else 0), T * Lk
 
 
 def relpos_attention(qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale, need_probs=False, am=None):
@@ -651,6 +671,48 @@ def relpos_attention(qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale, need_probs=Fals
     out, probs = OPS.relpos_attention(qkv, pk, pbu, pbv, kpm, int(B), int(T), int(H), int(dh),
                                                 float(scale), bool(need_probs), m, int(sb), int(sh))
     return out, (probs if need_probs else None)
+
+
+@custom_op("sbk::relpos_xattn", mutates_args=())
+def _relpos_xattn_op(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, pk: torch.Tensor, pbu: torch.Tensor,
+                     pbv: torch.Tensor, kpm: Optional[torch.Tensor], am: Optional[torch.Tensor], am_sb: int,
+                     am_sh: int, B: int, Lq: int, Lk: int, H: int, dh: int, scale: float, mpf: bool, p: float,
+                     seed: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    out = torch.empty(B * Lq, H * dh, device=q.device, dtype=q.dtype)
+    probs = torch.empty(B, H, Lq, Lk, device=q.device, dtype=_f32)
+    attn = torch.empty_like(probs) if p > 0 else probs.new_empty(0)
+    rc = lib().sbk_relpos_xattn_fwd(int(_is_bf16(q)), ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0),
+                                    ptr(pk), pk.stride(0), pk.shape[0], ptr(pbu), ptr(pbv), ptr(kpm), ptr(am),
+                                    int(am_sb), int(am_sh), B, Lq, Lk, H, dh, float(scale), int(mpf), float(p),
+                                    int(seed), ptr(out), out.stride(0), ptr(probs), ptr(attn) if p > 0 else None,
+                                    stream_of(q))
+    check(rc, "sbk_relpos_xattn_fwd")
+    return out, probs, attn
+
+
+@_relpos_xattn_op.register_fake
+def _(q, k, v, pk, pbu, pbv, kpm, am, am_sb, am_sh, B, Lq, Lk, H, dh, scale, mpf, p, seed):
+    probs = q.new_empty(B, H, Lq, Lk, dtype=_f32)
+    return q.new_empty(B * Lq, H * dh), probs, (q.new_empty(B, H, Lq, Lk, dtype=_f32) if p > 0 else
+                                                  q.new_empty(0, dtype=_f32))
+
+
+def relpos_xattn(q, k, v, pk, pbu, pbv, kpm, B, Lq, Lk, H, dh, scale, mask_pos_future=False, am=None, p=0.0,
+                 seed=0):
+    """RelPosMHAXL core for query != key/value (sbk_relpos_xattn_fwd): q
+    (B*Lq, d), k / v (B*Lk, d), pk (P, d) with P // 2 + 1 == Lk, unit
+    column stride, bf16 or fp32 alike; pbu / pbv fp32 (H*dh); am:
+    attn_mask_arg(..., Lk=Lk) or None.  Returns (out (B*Lq, d) in q.dtype,
+    probs (B, H, Lq, Lk) fp32, attention weights after dropout)."""
+    for t in (q, k, v, pk):
+        if t.stride(-1) != 1 or t.shape[-1] != H * dh or t.dtype != q.dtype:
+            raise ValueError("relpos_xattn: q / k / v / pk must be (rows, H*dh), unit column stride, one dtype")
+    if pk.shape[0] // 2 + 1 != Lk:
+        raise ValueError(f"pos_embs has {pk.shape[0]} rows: rel_shift keeps {pk.shape[0] // 2 + 1} != k_len {Lk}")
+    m, sb, sh = am if am is not None else (None, 0, 0)
+    out, probs, attn = OPS.relpos_xattn(q, k, v, pk, pbu, pbv, kpm, m, int(sb), int(sh), int(B), int(Lq), int(Lk),
+                                        int(H), int(dh), float(scale), bool(mask_pos_future), float(p), int(seed))
+    return out, probs, (attn if p > 0 else probs)
 
 
 @custom_op("sbk::mha_attention", mutates_args=())

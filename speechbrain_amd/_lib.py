@@ -65,12 +65,12 @@ SIGNATURES = {
                                    _vp],
     # ffn.hip
     "sbk_ffn_supported": [_i, _i],
-    "sbk_ffn": [_vp, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _i, _f, _vp, _f, _vp, _vp, _f, _vp, _vp, _vp, _f, _vp, _i,
-                _vp],
+    "sbk_ffn": [_vp, _i, _i, _i, _vp, _vp, _f, _vp, _ll, _vp, _i, _f, _vp, _f, _vp, _vp, _f, _vp, _vp, _vp, _f, _vp,
+                _i, _vp],
     "sbk_ffn_chain": [_vp, _i, _i, _i, _i, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _f,
-                      _vp, _vp, _vp, _f, _vp, _i, _vp, _i, _vp, _vp],
-    "sbk_ffn_proj": [_vp, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _i, _f, _vp, _f, _vp, _vp, _f, _vp, _vp, _vp, _f, _vp,
-                     _i, _i, _vp, _vp],
+                      _vp, _vp, _vp, _f, _vp, _i, _vp, _ll, _i, _vp, _vp],
+    "sbk_ffn_proj": [_vp, _i, _i, _i, _vp, _vp, _f, _vp, _ll, _vp, _i, _f, _vp, _f, _vp, _vp, _f, _vp, _vp, _vp, _f,
+                     _vp, _i, _i, _vp, _vp],
     "sbk_ffn_image_elems": [_i, _i, _i, _i],
     "sbk_ffn_image": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp],
     # conformer.hip
@@ -106,6 +106,11 @@ SIGNATURES = {
     "sbk_relpos_attention_mask": [_i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _ll, _ll, _i, _i, _i, _i, _f, _vp, _vp, _vp],
     "sbk_relpos_attention_ld": [_i, _vp, _vp, _i, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _vp],
     "sbk_mha_attention": [_vp, _vp, _i, _i, _i, _i, _f, _vp, _vp],
+    # xattn.hip (RelPosMHAXL with query != key/value, q_len != k_len)
+    "sbk_relpos_xattn_fwd": [_i, _vp, _i, _vp, _i, _vp, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _ll, _ll, _i, _i, _i, _i,
+                             _i, _f, _i, _f, ctypes.c_ulonglong, _vp, _i, _vp, _vp, _vp],
+    "sbk_relpos_xattn_bwd": [_i, _vp, _i, _vp, _i, _vp, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i,
+                             _f, _i, _f, ctypes.c_ulonglong, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     # norm.hip
     "sbk_inorm_slices": [_i],
     "sbk_inorm_partials": [_vp, _vp, _i, _i, _i, _vp, _vp],
@@ -220,10 +225,16 @@ class _FastOp:
 
     def __call__(self, *args, **kw):
         if (torch.compiler.is_compiling() or torch.jit.is_tracing()
-                or (self._def._backward_fn is not None and torch.is_grad_enabled()
+                or torch._C._get_dispatch_mode(torch._C._TorchDispatchModeKey.FAKE) is not None
+                or torch._C._len_torch_dispatch_stack() > 0 or torch._C._are_functorch_transforms_active()
+                or (torch.is_grad_enabled()
                     and any(isinstance(t, torch.Tensor) and t.requires_grad for t in (*args, *kw.values())))):
-            # traced, or a differentiable call of an op with a registered
-            # backward: through the dispatcher (graph node / autograd edge)
+            # traced, under a dispatch mode / functorch transform, or a call
+            # on inputs that require grad: through the dispatcher (graph
+            # node, fake / mode handling, and the autograd edge — or, for an
+            # op with no registered backward, the dispatcher's "autograd not
+            # implemented" error instead of a silently non-differentiable
+            # result)
             if self._op is None:
                 self._op = getattr(torch.ops.sbk, self._def._name)
             return self._op(*args, **kw)

@@ -1044,9 +1044,6 @@ constexpr int RF_SPAN = 1536;                  // staged samples per wave (6 KB:
 static_assert(RF_SPAN <= 2 * RF_WS, "the span fits the wave's regions");
 constexpr int RF_LW = 36;                      // dense mel row: 16-B aligned start + up to 33 bins
 typedef float rf4 __attribute__((ext_vector_type(4)));
-#ifndef SBK_RF_TRIPCH
-#define SBK_RF_TRIPCH 1                        // per-trip mel chunk counts (0: the dense width for every trip)
-#endif
 #ifndef SBK_RF_WGS_PER_CU
 #define SBK_RF_WGS_PER_CU 3                    // persistent grid: workgroups per CU (LDS: three fit)
 #endif
@@ -1220,7 +1217,6 @@ __global__ void __launch_bounds__(RF_NT, SBK_RF_MINW) spec_reg_kernel(SpecArgs a
       }
       __syncthreads();  // every read of mstart above is done
       for (int i = tid; i < a.M; i += RF_NT) mstart[i] &= ~3;
-#if SBK_RF_TRIPCH
       // 16-B chunks per mel trip (filters 16 t .. 16 t + 15): the largest of
       // its filters' own counts, so a trip skips the trailing all-zero chunks
       // of the dense rows (wave-uniform; mel_off's table slots are free now)
@@ -1230,7 +1226,6 @@ __global__ void __launch_bounds__(RF_NT, SBK_RF_MINW) spec_reg_kernel(SpecArgs a
           c = max(c, ((a.mel_start[jm] & 3) + a.mel_len[jm] + 3) >> 2);
         moff_s[t] = c;
       }
-#endif
     }
   }
   __syncthreads();
@@ -1413,13 +1408,9 @@ __global__ void __launch_bounds__(RF_NT, SBK_RF_MINW) spec_reg_kernel(SpecArgs a
       }
     };
     // two filters per trip: their LDS round trips overlap
-    // (SBK_RF_TRIPCH: chunk count per trip from the table stage, else lw / 4)
+    // (chunk count per trip from the table stage)
     auto trip_ch = [&](int t) __attribute__((always_inline)) {
-#if SBK_RF_TRIPCH
       return lw ? __builtin_amdgcn_readfirstlane(moff_s[t]) : 0;
-#else
-      return lw >> 2;
-#endif
     };
     int jm = lane >> 3;
     for (; jm + 8 < a.M; jm += 16) {

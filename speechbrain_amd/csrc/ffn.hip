@@ -115,22 +115,13 @@ struct IntC {
 };
 
 constexpr int FFN_BM = 48;
+constexpr int FFN_PAD = 16;  // LDS row pad (elements): conflict-free b128 reads (8 measured slower)
 constexpr int FFN_NW = 8, FFN_NT = FFN_NW * 64;  // 8 waves: LN'd rows fit in VGPRs (2 waves/SIMD)
 
-// Phase-removal probes (timing only, wrong results; scripts/probe_build.sh):
-// NOACT identity activation, NOLN no row LayerNorms, NOMFMA no FFN-step MFMAs
-// (the fragment reads stay, consumed by one add), NODMA no weight DMA.
-#ifdef SBK_PROBE_NOMFMA
-#define FFN_MFMA(A, B, C) ((C) + f32x4{(float)(A)[0], (float)(B)[1], 0.f, 0.f})
-#else
 #define FFN_MFMA(A, B, C) __builtin_amdgcn_mfma_f32_16x16x32_bf16((A), (B), (C), 0, 0, 0)
-#endif
 
 template <int ACT>
 __device__ __forceinline__ float act_fn(float v, float slope) {
-#ifdef SBK_PROBE_NOACT
-  return v;
-#endif
   if (ACT == ACT_SWISH) return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));  // bf16 hidden: approx rcp
   if (ACT == ACT_LRELU) return v >= 0.f ? v : v * slope;
   if (ACT == ACT_GELU) return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
@@ -214,9 +205,6 @@ template <int D, int T2, int MT, int NW>
 __device__ __forceinline__ void row_ln(float (&z)[T2][MT][4], float* red, const float* gam, const float* bet, float eps,
                                        int w, int g, int fr) {
   static_assert(NW == 8, "two b128 reads per row");
-#ifdef SBK_PROBE_NOLN
-  return;
-#endif
   float mean[MT], rstd[MT];
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
@@ -297,60 +285,6 @@ __device__ __forceinline__ void load_frags(bf16x8 (&xa)[K1][KS][MT], const bf16_
       for (int mt = 0; mt < MT; ++mt) tie(xa[r][ks][mt]);
 }
 
-#ifdef SBK_PROBE_PAIRX
-// Probe (timing only, wrong results; never the product): the cost of the seam
-// a hidden-dimension split over paired workgroups would need — each
-// workgroup publishes its (48 x 256) fp32 phase-2 partial (48 KB) with
-// write-through (sc1) stores, raises a flag after every wave's vmcnt(0) and a
-// barrier, polls its partner's flag (blockIdx ^ 8: the same XCD), reads the
-// partner's partial (sc1 loads) and adds it.  The consumer resets the
-// partner's flag, so every launch starts from zero.  Spins are bounded.
-__device__ float4 g_pairx_buf[256 * 512 * 6];
-__device__ unsigned g_pairx_flag[256];
-template <int T, int MT>
-__device__ __forceinline__ void pairx_exchange(f32x4 (&acc)[T][MT], int tid) {
-  const int pb = blockIdx.x ^ 8;
-  if (pb >= (int)gridDim.x) return;
-  float4* mine = g_pairx_buf + ((long long)blockIdx.x * 512 + tid) * (T * MT);
-  const float4* theirs = g_pairx_buf + ((long long)pb * 512 + tid) * (T * MT);
-#pragma unroll
-  for (int t = 0; t < T; ++t)
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-      asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(mine + t * MT + mt), "v"(acc[t][mt]) : "memory");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  if (tid == 0) {
-    const unsigned one = 1;
-    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(g_pairx_flag + blockIdx.x), "v"(one) : "memory");
-    unsigned f = 0;
-    for (int it = 0; it < (1 << 20); ++it) {
-      asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(f) : "v"(g_pairx_flag + pb) : "memory");
-      if (f == 1) break;
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  __builtin_amdgcn_s_barrier();
-  f32x4 v[T][MT];
-#pragma unroll
-  for (int t = 0; t < T; ++t)
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-      asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v[t][mt]) : "v"(theirs + t * MT + mt) : "memory");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int t = 0; t < T; ++t)
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      vtie(v[t][mt]);
-      acc[t][mt] += v[t][mt];
-    }
-  if (tid == 0) {
-    const unsigned zero = 0;
-    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(g_pairx_flag + pb), "v"(zero) : "memory");
-  }
-}
-#endif
 
 // s_memtime timeline of the waves of workgroup 128 (probe builds only)
 SBK_PROBE_BUFFER(g_ffn_tl, 16, 256)
@@ -359,10 +293,7 @@ SBK_PROBE_BUFFER(g_ffn_tl, 16, 256)
 template <int D, int ACT, bool PROJ, bool CHAIN>
 __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   constexpr int BM = FFN_BM, HC = 256, NW = FFN_NW, NT = FFN_NT;
-#ifndef SBK_FFN_PAD
-#define SBK_FFN_PAD 16  // (probe builds vary the row pad)
-#endif
-  constexpr int XS = D + SBK_FFN_PAD, HS = HC + SBK_FFN_PAD;   // LDS row strides (elements), +32 B pad: conflict-free b128 reads
+  constexpr int XS = D + FFN_PAD, HS = HC + FFN_PAD;   // LDS row strides (elements), +32 B pad: conflict-free b128 reads
   constexpr int MT = BM / 16;                // m-tiles (3)
   constexpr int T = 256 / 16 / FFN_NW;       // 16-row weight tiles per wave (HC/16/NW = D/16/NW)
   constexpr int BK = 64;                     // K per step: one 128-B line per weight row
@@ -413,12 +344,10 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     const auto gs = (const __attribute__((address_space(1))) void*)src;
     const auto ls = (__attribute__((address_space(3))) void*)dst;
     static_assert(GL == 4, "four 1-KB pieces per wave and tile");
-#ifndef SBK_PROBE_NODMA
     __builtin_amdgcn_global_load_lds(gs, ls, 16, 0, 0);
     __builtin_amdgcn_global_load_lds(gs, ls, 16, 1024, 0);
     __builtin_amdgcn_global_load_lds(gs, ls, 16, 2048, 0);
     __builtin_amdgcn_global_load_lds(gs, ls, 16, 3072, 0);
-#endif
   };
   // ---- prologue.  Every HBM read of the launch is issued here, before the
   // weight stream: the residual x values of this lane's epilogue outputs
@@ -583,9 +512,6 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   for (int stage = 0; stage < (CHAIN ? 2 : 1); ++stage) {
   if (CHAIN && stage == 1) {
     FFN_TL(197);
-#ifdef SBK_PROBE_PAIRX
-    pairx_exchange<T, MT>(acc2, tid);
-#endif
     // ---- between the blocks: A's rows z = x + alpha (acc2 + b2) -> post-LN
     // (norm2) are B's residual (held in xres) and, through B's LN0, its
     // phase-1 operand (Xn -> VGPR fragments); nothing goes to HBM
@@ -632,32 +558,6 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     FFN_TL(198);
   }
   const float* b1st = b1s + stage * a.H;  // this block's b1 (LDS)
-#ifdef FFN_ACTPIPE
-  // probe: phase 1 of chunk 0, then per chunk c: phase 1 of chunk c+1 (acc1),
-  // then phase 2 of chunk c (acc2) with chunk c+1's activation issued after
-  // each step's DMA and MFMAs (image in the matching order)
-  int s = stage * S;
-#pragma unroll
-  for (int r = 0; r < K1; ++r) step(s + r, r, false, nullptr, false, none);
-  s += K1;
-  act_tiles(0, T * MT, b1st, Hs);
-  for (int c = 0; c < NCH; ++c) {
-    const bool more = c + 1 < NCH;
-    if (more) {
-#pragma unroll
-      for (int r = 0; r < K1; ++r) step(s + r, r, false, nullptr, false, none);
-      s += K1;
-    }
-    const bf16_t* Hc = Hs + (c & 1) * BM * HS;
-    bf16_t* Hn = Hs + ((c + 1) & 1) * BM * HS;
-#pragma unroll
-    for (int p = 0; p < K2; ++p)
-      step(s + p, p, true, Hc, p == 0, [&]() __attribute__((always_inline)) {
-        if (more) act_tiles(p * T * MT / K2, (p + 1) * T * MT / K2, b1st + (c + 1) * HC, Hn);
-      });
-    s += K2;
-  }
-#else
   for (int c = 0; c < NCH; ++c) {
     const int s0 = stage * S + c * SPC;
 #pragma unroll
@@ -670,7 +570,6 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
 #pragma unroll
     for (int p = 0; p < K2; ++p) step(s0 + K1 + p, p, true, Hc, p == 0, none);
   }
-#endif
   }  // stage
   if (!PROJ) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the tail reloads
   FFN_TL(194);
@@ -877,7 +776,7 @@ template <int D>
 size_t ffn_lds(int H, bool chain) {
   // 2-slot weight ring, Xn, two hidden-chunk buffers, b1 (two with CHAIN), the row-reduction scratch,
   // the epilogue parameter rows
-  return ((size_t)2 * 256 * 64 + (size_t)FFN_BM * (D + SBK_FFN_PAD) + (size_t)2 * FFN_BM * (256 + SBK_FFN_PAD)) *
+  return ((size_t)2 * 256 * 64 + (size_t)FFN_BM * (D + FFN_PAD) + (size_t)2 * FFN_BM * (256 + FFN_PAD)) *
              sizeof(bf16_t) +
          (size_t)(chain ? 2 : 1) * H * 4 + (size_t)FFN_NW * FFN_BM * 4 + (size_t)FFN_NW * D * 4;
 }
@@ -935,21 +834,7 @@ __device__ __forceinline__ void img_tile_src(const ImgSrc& q, int s, const bf16_
     return;
   }
   const bool sb = s >= q.ntile_blk;
-#ifdef FFN_ACTPIPE
-  const int sl = sb ? s - q.ntile_blk : s, nch = q.H / 256;
-  int c, r;
-  bool w1t;
-  if (sl < K1) {
-    w1t = true; c = 0; r = sl;
-  } else {
-    const int qq = sl - K1, seg = qq / SPC, p = qq - seg * SPC;
-    w1t = seg + 1 < nch && p < K1;
-    c = w1t ? seg + 1 : seg;
-    r = w1t ? p : (seg + 1 < nch ? p - K1 : p) + K1;
-  }
-#else
   const int sl = sb ? s - q.ntile_blk : s, c = sl / SPC, r = sl - c * SPC;
-#endif
   if (r < K1) {
     *mat = sb ? q.w1b : q.w1; *ld = q.D; *row0 = c * 256; *k0 = r * 64;
   } else {
@@ -1011,9 +896,12 @@ SBK_API int sbk_ffn_image(const void* w1, const void* w2, const void* w1b, const
 
 namespace {
 int ffn_check(const float* x, int M, int D, int H, const float* g0, const float* b0, const void* img,
-              const float* b1, int act, const float* b2, const float* gp, const float* bp, float* out,
-              const float* gn, const float* bn, void* u, int np, void* yp) {
+              long long img_elems, int chain, const float* b1, int act, const float* b2, const float* gp,
+              const float* bp, float* out, const float* gn, const float* bn, void* u, int np, void* yp) {
   if (M <= 0 || !sbk_ffn_supported(D, H) || !g0 || !b0 || !img || !b1 || !b2 || !out) return SBK_ERR_ARG;
+  // the image must be the one sbk_ffn_image built for this (D, H, np, chain):
+  // the kernel streams exactly that many tiles from it
+  if (np < 0 || np % 256 || img_elems != sbk_ffn_image_elems(D, H, np, chain)) return SBK_ERR_ARG;
   if (act == ACT_GLU || act < 0 || act > ACT_GELU || (gn && !u && np == 0)) return SBK_ERR_ARG;
   // projection tail: y = next-LN(out) . Wp^T, whole 256-column blocks; it
   // replaces the u output
@@ -1030,10 +918,11 @@ int ffn_check(const float* x, int M, int D, int H, const float* g0, const float*
 }  // namespace
 
 SBK_API int sbk_ffn_proj(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0,
-                         const void* img, const float* b1, int act, float slope, const float* b2, float alpha,
-                         const float* gp, const float* bp, float epsp, float* out, const float* gn, const float* bn,
-                         float epsn, void* u, int u_bf16, int np, void* yp, void* stream) {
-  if (ffn_check(x, M, D, H, g0, b0, img, b1, act, b2, gp, bp, out, gn, bn, u, np, yp)) return SBK_ERR_ARG;
+                         const void* img, long long img_elems, const float* b1, int act, float slope, const float* b2,
+                         float alpha, const float* gp, const float* bp, float epsp, float* out, const float* gn,
+                         const float* bn, float epsn, void* u, int u_bf16, int np, void* yp, void* stream) {
+  if (ffn_check(x, M, D, H, g0, b0, img, img_elems, 0, b1, act, b2, gp, bp, out, gn, bn, u, np, yp))
+    return SBK_ERR_ARG;
   FfnArgs a;
   a.x = x; a.M = M; a.H = H;
   a.g0 = g0; a.b0 = b0; a.eps0 = eps0;
@@ -1059,12 +948,14 @@ SBK_API int sbk_ffn_chain(const float* x, int M, int D, int H, int act, float sl
                           float eps0, const float* b1, const float* b2, float alpha, const float* gp, const float* bp,
                           float epsp, const float* g0b, const float* b0b, float eps0b, const float* b1b,
                           const float* b2b, float alphab, float* out, const float* gn, const float* bn, float epsn,
-                          void* u, int u_bf16, const void* img, int np, void* yp, void* stream) {
+                          void* u, int u_bf16, const void* img, long long img_elems, int np, void* yp,
+                          void* stream) {
   if (!g0b || !b0b || !b1b || !b2b) return SBK_ERR_ARG;
   if ((reinterpret_cast<uintptr_t>(g0b) | reinterpret_cast<uintptr_t>(b0b) | reinterpret_cast<uintptr_t>(b1b) |
        reinterpret_cast<uintptr_t>(b2b)) & 15)
     return SBK_ERR_ARG;
-  if (ffn_check(x, M, D, H, g0, b0, img, b1, act, b2, gp, bp, out, gn, bn, u, np, yp)) return SBK_ERR_ARG;
+  if (ffn_check(x, M, D, H, g0, b0, img, img_elems, 1, b1, act, b2, gp, bp, out, gn, bn, u, np, yp))
+    return SBK_ERR_ARG;
   FfnArgs a;
   a.x = x; a.M = M; a.H = H;
   a.g0 = g0; a.b0 = b0; a.eps0 = eps0;
@@ -1083,9 +974,9 @@ SBK_API int sbk_ffn_chain(const float* x, int M, int D, int H, int act, float sl
 }
 
 SBK_API int sbk_ffn(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0,
-                    const void* img, const float* b1, int act, float slope, const float* b2, float alpha,
-                    const float* gp, const float* bp, float epsp, float* out, const float* gn, const float* bn,
-                    float epsn, void* u, int u_bf16, void* stream) {
-  return sbk_ffn_proj(x, M, D, H, g0, b0, eps0, img, b1, act, slope, b2, alpha, gp, bp, epsp, out, gn, bn, epsn, u,
-                      u_bf16, 0, nullptr, stream);
+                    const void* img, long long img_elems, const float* b1, int act, float slope, const float* b2,
+                    float alpha, const float* gp, const float* bp, float epsp, float* out, const float* gn,
+                    const float* bn, float epsn, void* u, int u_bf16, void* stream) {
+  return sbk_ffn_proj(x, M, D, H, g0, b0, eps0, img, img_elems, b1, act, slope, b2, alpha, gp, bp, epsp, out, gn, bn,
+                      epsn, u, u_bf16, 0, nullptr, stream);
 }

@@ -4,7 +4,9 @@ PositionalwiseFeedForward (speechbrain/nnet/attention.py:312-839).
 Parameter names and shapes match the reference so checkpoints load with
 strict=True.  RelPosMHAXL self-attention runs as: in_proj GEMM (MFMA) →
 linear_pos GEMM → one fused rel-pos attention kernel (scores, closed-form
-rel_shift, mask, softmax, P·V) → out_proj GEMM.
+rel_shift, mask, softmax, P·V) → out_proj GEMM.  With query != key / value
+(any q_len, k_len) it runs separate q / k / v GEMMs → the cross-length
+rel-pos core of csrc/xattn.hip → out_proj, forward and backward.
 """
 import math
 
@@ -53,7 +55,8 @@ class RelPosEncXL(nn.Module):
 
 
 class RelPosMHAXL(nn.Module):
-    """attention.py:362-639 (self-attention path)."""
+    """attention.py:362-639: self-attention on the fused rel-pos flash
+    kernels; query != key / value (and q_len != k_len) on cross_forward."""
 
     def __init__(self, embed_dim, num_heads, dropout=0.0, vbias=False, vdim=None, mask_pos_future=False):
         super().__init__()
@@ -187,15 +190,47 @@ class RelPosMHAXL(nn.Module):
         out = A.linear(o, self.out_proj.weight, self.out_proj.bias, dtype, self._wc, "t_out", res=residual)
         return out, attn
 
+    def cross_forward(self, query, key, value, pos_embs, key_padding_mask=None, attn_mask=None):
+        """attention.py:554-639 for query != key / value: separate q / k / v
+        projections on the MFMA GEMM (the row chunks of in_proj_weight,
+        :555-564; vbias as the v projection's bias, :576-579), linear_pos, the
+        cross-length rel-pos core (csrc/xattn.hip: rel_shift of the
+        (q_len, 2*k_len-1) band incl. mask_pos_future) and out_proj, each
+        differentiable.  Returns (out (B, Lq, E), attention weights)."""
+        B, Lq, E = query.shape
+        Lk = key.shape[1]
+        if value.shape[:2] != key.shape[:2]:
+            raise ValueError(f"key {tuple(key.shape)} and value {tuple(value.shape)} lengths differ")
+        dtype = _enc.compute_dtype()
+        H, dh = self.num_heads, self.head_dim
+        wq, wk, wv = self.in_proj_weight.chunk(3, dim=0)
+        vb = self.value_bias_weight if self.vbias is not None else None
+        q = A.linear(query.reshape(B * Lq, E), wq, None, dtype, self._wc, "x_q", out_dtype=dtype)
+        k = A.linear(key.reshape(B * Lk, E), wk, None, dtype, self._wc, "x_k", out_dtype=dtype)
+        v = A.linear(value.reshape(B * Lk, E), wv, vb, dtype, self._wc, "x_v", out_dtype=dtype)
+        pk = A.linear(pos_embs.reshape(-1, E), self.linear_pos.weight, None, dtype, self._wc, "x_pos",
+                      out_dtype=dtype)
+        kpm = key_padding_mask.to(query.device, torch.uint8).contiguous() if key_padding_mask is not None else None
+        am = _enc.attn_mask_arg(attn_mask, B, Lq, H, query.device, Lk=Lk)
+        p = self.dropout_att.p if self.training else 0.0
+        o, attn = A.RelPosCrossAttnFn.apply(q, k, v, pk, self.pos_bias_u, self.pos_bias_v, kpm, am, B, Lq, Lk, H, dh,
+                                            self.scale, bool(self.mask_pos_future), float(p))
+        out = A.linear(o, self.out_proj.weight, self.out_proj.bias, dtype, self._wc, "x_out")
+        return out.view(B, Lq, E), attn
+
     def forward(self, query, key, value, pos_embs, key_padding_mask=None, attn_mask=None,
                 return_attn_weights=True):
-        """attention.py:485-639.  Self-attention only (query, key and value
-        identical, as in every Conformer call site).  attn_mask: (T, T) or
-        (B*H, T, T), bool (True = masked) or additive float (:598-611)."""
+        """attention.py:485-639.  Self-attention (query, key and value
+        identical, every Conformer call site) runs the fused kernels;
+        anything else — key or value != query, q_len != k_len — takes
+        cross_forward.  attn_mask: (Lq, Lk) or (B*H, Lq, Lk), bool (True =
+        masked) or additive float (:598-611)."""
         if not self._qkv_same_embed_dim:
-            raise NotImplementedError  # the reference raises too (attention.py:558)
-        if not ((query is key or torch.equal(query, key)) and (key is value or torch.equal(key, value))):
-            raise NotImplementedError("cross-attention RelPosMHAXL is not on the accelerated path")
+            raise NotImplementedError  # the reference raises too (attention.py:566)
+        if not ((query is key or (query.shape == key.shape and torch.equal(query, key)))
+                and (key is value or (key.shape == value.shape and torch.equal(key, value)))):
+            out, attn = self.cross_forward(query, key, value, pos_embs, key_padding_mask, attn_mask)
+            return (out, attn) if return_attn_weights else out
         B, T, d = query.shape
         dtype = _enc.compute_dtype()
         x2d = query.reshape(B * T, d)

@@ -690,7 +690,83 @@ def gen_recipe():
     np.savez_compressed(os.path.join(OUT, "recipe.npz"), **out)
 
 
+def gen_xattn():
+    """xattn.npz: RelPosMHAXL with query != key/value and q_len != k_len
+    (nnet/attention.py:554-564 separate projections, rel_shift :468-483 on a
+    (q_len, 2*k_len-1) band, mask_pos_future's tril).  Cases "u*": the 16
+    combinations of tests/unittests/test_attention.py:4-27 (emb 4, 2 heads,
+    k_len 12|10 x q_len 10|12 x vbias x vdim 4|None), seeded; "c*": wider
+    cases (emb 64, 4 heads) with mask_pos_future, key padding, a bool and a
+    float attn_mask, key != value.  Every case records the state_dict, the
+    inputs, out and attention weights, and the autograd gradients of
+    sum(R * out) w.r.t. the parameters, query, key and value."""
+    out = {}
+    g = torch.Generator().manual_seed(61)
+    cases = []
+    n = 0
+    for kl in (12, 10):
+        for ql in (10, 12):
+            for b in (True, False):
+                for h in (4, None):
+                    cases.append(dict(tag=f"u{n}", E=4, H=2, vbias=b, vdim=h, ql=ql, kl=kl, same_kv=True))
+                    n += 1
+    cases += [
+        dict(tag="c0", E=64, H=4, vbias=False, vdim=None, ql=37, kl=23, same_kv=True, mpf=True),
+        dict(tag="c1", E=64, H=4, vbias=True, vdim=None, ql=19, kl=41, same_kv=False, mpf=True, kpm=True),
+        dict(tag="c2", E=64, H=4, vbias=False, vdim=None, ql=29, kl=17, same_kv=False, kpm=True, bmask=True),
+        dict(tag="c3", E=64, H=4, vbias=True, vdim=None, ql=16, kl=33, same_kv=True, fmask=True),
+        dict(tag="c4", E=32, H=2, vbias=False, vdim=None, ql=21, kl=21, same_kv=False, mpf=True),
+        dict(tag="c5", E=64, H=4, vbias=False, vdim=None, ql=50, kl=7, same_kv=True, mpf=True),
+    ]
+    out["cases"] = np.array([c["tag"] for c in cases])
+    for i, c in enumerate(cases):
+        t, E, H, ql, kl = c["tag"], c["E"], c["H"], c["ql"], c["kl"]
+        torch.manual_seed(100 + i)
+        m = RelPosMHAXL(E, num_heads=H, vbias=c["vbias"], vdim=c["vdim"], mask_pos_future=c.get("mpf", False))
+        if c["vbias"]:
+            with torch.no_grad():
+                m.value_bias_weight.copy_(0.3 * torch.randn(E, generator=g))
+        B = 2
+        q = torch.rand((B, ql, E), generator=g).requires_grad_(True)
+        k = torch.rand((B, kl, E), generator=g).requires_grad_(True)
+        v = k if c["same_kv"] else torch.rand((B, kl, E), generator=g).requires_grad_(True)
+        pe = torch.rand((1, 2 * kl - 1, E), generator=g)
+        kpm = None
+        if c.get("kpm"):
+            kpm = torch.arange(kl)[None, :] >= torch.tensor([kl, kl - 5])[:, None]
+        am = None
+        if c.get("bmask"):
+            am = torch.rand((ql, kl), generator=g) < 0.25
+            am[:, 0] = False  # no fully masked row
+        if c.get("fmask"):
+            am = 0.5 * torch.randn(B * H, ql, kl, generator=g)
+        o, a = m(q, k, v, pos_embs=pe, key_padding_mask=kpm, attn_mask=am)
+        R = torch.randn(o.shape, generator=g)
+        (o * R).sum().backward()
+        meta = np.array([E, H, int(c["vbias"]), ql, kl, int(c["same_kv"]), int(c.get("mpf", False)),
+                         int(kpm is not None), 0 if am is None else (1 if am.dtype == torch.bool else 2)], np.int64)
+        out[f"{t}.meta"] = meta
+        for kk, vv in m.state_dict().items():
+            out[f"{t}.sd.{kk}"] = t2n(vv)
+        out[f"{t}.q"], out[f"{t}.k"], out[f"{t}.pe"], out[f"{t}.R"] = t2n(q), t2n(k), t2n(pe), t2n(R)
+        if not c["same_kv"]:
+            out[f"{t}.v"] = t2n(v)
+            out[f"{t}.grad_v"] = t2n(v.grad)
+        if kpm is not None:
+            out[f"{t}.kpm"] = kpm.numpy()
+        if am is not None:
+            out[f"{t}.am"] = am.numpy() if am.dtype == torch.bool else t2n(am)
+        out[f"{t}.out"], out[f"{t}.attn"] = t2n(o), t2n(a)
+        out[f"{t}.grad_q"], out[f"{t}.grad_k"] = t2n(q.grad), t2n(k.grad)
+        for kk, p in m.named_parameters():
+            out[f"{t}.grad.{kk}"] = t2n(p.grad)
+    np.savez_compressed(os.path.join(OUT, "xattn.npz"), **out)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["xattn"]:
+        gen_xattn()
+        sys.exit(0)
     if sys.argv[1:] == ["recipe"]:
         gen_recipe()
         sys.exit(0)
@@ -719,6 +795,7 @@ if __name__ == "__main__":
     gen_decoder()
     gen_dropin()
     gen_recipe()
+    gen_xattn()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

@@ -294,3 +294,40 @@ def test_wav2vec_encoder_wrapper_and_transformer(golden):
     o, w = OW.mha(torch.from_numpy(g["mha_q"]), kv, kv, sdm, "", 4, torch.from_numpy(g["mha_kpm"]))
     assert_close(o, g["mha_out"], rtol=1e-5, name="mha out")
     assert_close(w, g["mha_w"], rtol=1e-5, name="mha weights")
+
+
+def _xattn_case(g, t):
+    """Inputs of one xattn.npz case (gen_golden.gen_xattn) as torch tensors."""
+    E, H, vbias, ql, kl, same_kv, mpf, has_kpm, am_kind = (int(x) for x in g[f"{t}.meta"])
+    pre = f"{t}.sd."
+    sd = {k[len(pre):]: torch.from_numpy(g[k]) for k in g.files if k.startswith(pre)}
+    q, k = torch.from_numpy(g[f"{t}.q"]), torch.from_numpy(g[f"{t}.k"])
+    v = k if same_kv else torch.from_numpy(g[f"{t}.v"])
+    kpm = torch.from_numpy(g[f"{t}.kpm"]) if has_kpm else None
+    am = torch.from_numpy(g[f"{t}.am"]) if am_kind else None
+    return dict(E=E, H=H, vbias=bool(vbias), mpf=bool(mpf), sd=sd, q=q, k=k, v=v, same_kv=bool(same_kv),
+                pe=torch.from_numpy(g[f"{t}.pe"]), kpm=kpm, am=am, R=torch.from_numpy(g[f"{t}.R"]))
+
+
+def test_relpos_cross_attention_oracle(golden):
+    """The cross-length RelPosMHAXL restatement (oracle.conformer.rel_pos_mha_cross)
+    against the reference on test_attention.py's 16 combinations and the
+    masked / causal / key != value cases, outputs, attention maps and
+    gradients."""
+    g = golden("xattn")
+    for t in g["cases"]:
+        c = _xattn_case(g, t)
+        sd = {k: v.clone().requires_grad_(True) for k, v in c["sd"].items()}
+        q, k = c["q"].clone().requires_grad_(True), c["k"].clone().requires_grad_(True)
+        v = k if c["same_kv"] else c["v"].clone().requires_grad_(True)
+        o, a = OC.rel_pos_mha_cross(q, k, v, c["pe"], sd, "", c["H"], c["vbias"], c["mpf"], c["kpm"], c["am"])
+        assert_close(o, g[f"{t}.out"], rtol=1e-5, name=f"{t} out")
+        assert_close(a, g[f"{t}.attn"], rtol=1e-5, name=f"{t} attn")
+        (o * c["R"]).sum().backward()
+        assert_close(q.grad, g[f"{t}.grad_q"], rtol=1e-5, name=f"{t} grad_q")
+        assert_close(k.grad, g[f"{t}.grad_k"], rtol=1e-5, name=f"{t} grad_k")
+        if not c["same_kv"]:
+            assert_close(v.grad, g[f"{t}.grad_v"], rtol=1e-5, name=f"{t} grad_v")
+        for name, p in sd.items():
+            if f"{t}.grad.{name}" in g.files:
+                assert_close(p.grad, g[f"{t}.grad.{name}"], rtol=1e-5, name=f"{t} grad {name}")
