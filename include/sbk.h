@@ -580,6 +580,15 @@ int sbk_mx_gemm(const uint8_t* A, const uint8_t* SA, long long lda, long long ld
                 int K, const float* bias, int act, float alpha, const float* res, long long ldr, void* out,
                 long long ldc, int out_mode, uint8_t* out_scales, long long ldso, void* stream);
 
+/* sbk_mx_gemm on the 256 x 256-tile multi-phase kernel (csrc/gemm256.hip):
+ * same arguments; N % 256 == 0, K % 128 == 0 (SBK_ERR_ARG otherwise).
+ * sbk_mx_gemm takes this kernel by itself when the shape allows and M is
+ * large; this entry point forces it. */
+int sbk_mx_gemm256(const uint8_t* A, const uint8_t* SA, long long lda, long long ldsa, long long rpb, long long a_bs,
+                   long long s_bs, const uint8_t* W, const uint8_t* SW, long long ldw, long long ldsw, int M, int N,
+                   int K, const float* bias, int act, float alpha, const float* res, long long ldr, void* out,
+                   long long ldc, int out_mode, uint8_t* out_scales, long long ldso, void* stream);
+
 /* x[m, :] += pe[m % T, :] in place, x (M, D) fp32 (EncoderWrapper positional table). */
 int sbk_add_rows_periodic(float* x, int M, int D, const float* pe, int T, void* stream);
 

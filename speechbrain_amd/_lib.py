@@ -90,6 +90,8 @@ SIGNATURES = {
     # mxgemm.hip (MXFP8 block-scaled MFMA GEMM)
     "sbk_mx_gemm": [_vp, _vp, _ll, _ll, _ll, _ll, _ll, _vp, _vp, _ll, _ll, _i, _i, _i, _vp, _i, _f, _vp, _ll, _vp,
                     _ll, _i, _vp, _ll, _vp],
+    "sbk_mx_gemm256": [_vp, _vp, _ll, _ll, _ll, _ll, _ll, _vp, _vp, _ll, _ll, _i, _i, _i, _vp, _i, _f, _vp, _ll,
+                       _vp, _ll, _i, _vp, _ll, _vp],
     "sbk_mx_quant": [_vp, _i, _ll, _i, _i, _vp, _ll, _vp, _ll, _vp],
     "sbk_mx_dequant": [_vp, _ll, _vp, _ll, _i, _i, _vp, _vp],
     # augment.hip

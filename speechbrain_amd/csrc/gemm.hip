@@ -18,6 +18,7 @@
 //   conv + GLU), :87-92 (after_conv Linear), :243,:259 (0.5-scaled residuals),
 //   TransformerASR.py:127-135 (custom_src_module Linear).
 #include "mfma.h"
+#include "gemm256.h"
 
 using namespace sbk;
 
@@ -756,6 +757,17 @@ SBK_API int sbk_gemm(int dtype_bf16, const void* A, int lda, const void* W, int 
   if (act == ACT_GLU && (N % 32)) return SBK_ERR_ARG;  // whole [a16|gate16] groups
   Epi ep{bias, act, slope, res, ldr, alpha, rowmask, out, ldc, out_bf16};
   hipStream_t s = (hipStream_t)stream;
+  // tile 30: the 256 x 256 multi-phase kernel (gemm256.hip), N % 256 == 0,
+  // K % 64 == 0; taken by default when it fills the chip (>= 180 tiles) at
+  // K >= 256 — config 5's projections: 0.97-1.03 PF/s against 0.67-0.82 for
+  // the best of the other tiles (profiles/r05c_g256.log)
+  if (dtype_bf16 && (tile == 30 || tile == 0)) {
+    const Gemm256Epi e{bias, act, slope, res, ldr, alpha, rowmask, out, ldc, out_bf16};
+    const bool ok = gemm256_supported(M, N, K, lda, ldw, A, W, e);
+    if (tile == 30 && !ok) return SBK_ERR_ARG;
+    if (ok && (tile == 30 || (K >= 256 && (long long)((M + 255) / 256) * (N / 256) >= 180)))
+      return gemm256_launch(A, lda, W, ldw, M, N, K, e, s);
+  }
   // tile 2 (64x64x64) measured best for every encoder shape (M = B*T = 12032,
   // scripts/kbench.py gemm); the joint-output projection of the transducer
   // (M = B*T*U1 = 782080, N = 1000, K = 1024) runs 1.5x faster on 128x128x128

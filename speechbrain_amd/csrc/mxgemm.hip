@@ -30,6 +30,7 @@
 // Epilogue: bias, GELU / ReLU, alpha * val + fp32 residual, output fp32,
 // bf16 or MXFP8 (+ scales, amax over the 32 lanes of a tile row).
 #include "mx.h"
+#include "gemm256.h"
 
 using namespace sbk;
 
@@ -489,6 +490,14 @@ SBK_API int sbk_mx_gemm(const uint8_t* A, const uint8_t* SA, long long lda, long
   MxArgs p{A, SA, lda, ldsa, rpb, a_bs, s_bs, W, SW, ldw, ldsw, M, N, K, bias, act, alpha, res, ldr,
            out, ldc, out_mode, out_scales, ldso};
   hipStream_t s = (hipStream_t)stream;
+  // the 256 x 256 multi-phase kernel (gemm256.hip) when it fills the chip:
+  // 1.1-1.5x these kernels on config 5's shapes (profiles/r05c_mx256.log)
+  if (ldr <= 0x7fffffffLL && ldc <= 0x7fffffffLL && (long long)((M + 255) / 256) * (N / 256) >= 180) {
+    const Gemm256Epi ep{bias, act, 0.f, res, (int)ldr, alpha, nullptr, out, (int)ldc, out_mode == 1};
+    if (mx256_supported(M, N, K, lda, ldsa, rpb, a_bs, s_bs, ldw, ldsw, A, SA, W, SW, ep, out_mode, out_scales))
+      return mx256_launch(A, SA, lda, ldsa, rpb, a_bs, s_bs, W, SW, ldw, ldsw, M, N, K, ep, out_mode, out_scales, ldso,
+                          s);
+  }
   if (act == 4) return launch_act<4>(p, s);
   if (act == 3) return launch_act<3>(p, s);
   return launch_act<0>(p, s);
