@@ -39,6 +39,7 @@ SR = 16000
 SECONDS = 15.0
 BATCH = 32
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3  # MI355X exact-f32 MFMA = the f32 vector rate (MI355X_MICROARCH.md)
 _T0 = time.perf_counter()
 
 
@@ -61,7 +62,7 @@ def build_model(d_model, dev, layers=12):
     return fbank.to(dev).eval(), cnn.to(dev).eval(), tr.to(dev).eval()
 
 
-def make_step(fbank, cnn, tr, wav, wav_len):
+def make_step(fbank, cnn, tr, wav, wav_len, precision="bf16"):
     """The timed step: Fbank (fused spectrum kernel; its top_db floor applied
     by the front-end as it loads the rows) → both ConvBlocks in one bf16
     kernel → TransformerASR.encode under bf16 autocast (fused FFN /
@@ -70,6 +71,16 @@ def make_step(fbank, cnn, tr, wav, wav_len):
     batch as 2 or 4 utterance groups on concurrent streams in one graph
     measured no faster in rounds 2 and 4: 1.339 / 1.355 vs 1.333 ms,
     profiles/r04i_bench_s*.log — the kernels already fill the chip.)"""
+    if precision == "fp32":
+        # the parity precision: no autocast, every GEMM / attention product on
+        # the exact-f32 MFMA path (the 1e-4 parity of tests/test_gpu_encoder.py)
+        def step():
+            with torch.no_grad():
+                feats, topdb = fbank.forward_deferred(wav)
+                src = cnn.run(feats, torch.float32, topdb=topdb)
+                return tr.encode(src, wav_len)
+        return step
+
     def step():
         with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
             feats, topdb = fbank.forward_deferred(wav)
@@ -173,8 +184,8 @@ def cpu_baseline(d_model, n_utt=64, reps=3):
 
 
 class _LaunchProbe:
-    """Wraps one speechbrain_amd._enc entry point and records every bf16 call
-    of one eager step (arguments kept alive) with its algorithmic FLOPs
+    """Wraps one speechbrain_amd._enc entry point and records every call of
+    the timed precision (is_bf16: the selector, bf16 or fp32 operands) in one eager step (arguments kept alive) with its algorithmic FLOPs
     (`flops_of(*args, **kw)`).  `replay_time()` then captures exactly those
     calls, back to back, `reps` times into one HIP graph on the launch stream
     (torch's current stream, the one the ctypes kernels use) and times the
@@ -702,9 +713,15 @@ def main():
     ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c3",
                     help="c3: Fbank→Conformer (the BASELINE metric, default); c2: feature kernels "
                          "(Fbank, Δ/ΔΔ, SpecAugment); c5: wav2vec2 + 24L TransformerEncoder")
-    ap.add_argument("--precision", choices=["mxfp8", "bf16"], default="mxfp8", help="config 5 GEMM precision")
+    ap.add_argument("--precision", choices=["mxfp8", "bf16", "fp32"], default=None,
+                    help="c3: bf16 (default, the BASELINE config) or fp32 (the 1e-4 parity path); "
+                         "c5: mxfp8 (default) or bf16")
     ap.add_argument("--plumbing", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.precision is None:
+        args.precision = "mxfp8" if args.config == "c5" else "bf16"
+    if (args.config == "c5" and args.precision == "fp32") or (args.config == "c3" and args.precision == "mxfp8"):
+        ap.error(f"--precision {args.precision} is not offered for --config {args.config}")
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(os.path.abspath(__file__), sys.argv[1:], args.gpus))
@@ -729,7 +746,8 @@ def main():
     wav = (0.1 * torch.randn(args.batch, int(SR * SECONDS), generator=g)).to(dev)
     wav_len = torch.ones(args.batch, device=dev)
 
-    step = make_step(fbank, cnn, tr, wav, wav_len)
+    fp32 = args.precision == "fp32"
+    step = make_step(fbank, cnn, tr, wav, wav_len, args.precision)
     progress("model built")
 
     out = step()
@@ -774,7 +792,9 @@ def main():
         total_flops = encoder_flops(args.batch, T_e, args.d_model)
         # per-kernel timing: the dominant kernels' launches of one step,
         # replayed back to back from a HIP graph and timed with HIP events
-        bf = lambda t: t.dtype == torch.bfloat16  # noqa: E731
+        # the calls of the timed precision (bf16 operands, or fp32 ones on the parity path)
+        sel_dt = torch.float32 if fp32 else torch.bfloat16
+        bf = lambda t: t.dtype == sel_dt  # noqa: E731
         probes = [_LaunchProbe("ffn_chain", _ffn_chain_flops, lambda x, a, *r, **k: bf(a[1])),
                   _LaunchProbe("ffn_proj", _ffn_proj_flops, lambda x, ln0, w1, *a, **k: bf(w1)),
                   _LaunchProbe("ffn", _ffn_flops, lambda x, ln0, w1, *a, **k: bf(w1)),
@@ -795,8 +815,12 @@ def main():
                   ("ffn_kernel<256, 1, false, false> (final FFN2 + final LayerNorm)",
                    "ffn_kernel<256, 1, false, false>"),
                   ("conv_module_kernel<true> (out_proj + residual + conv module)", "conv_module_kernel<true>"),
-                  ("gemm_kernel<bf16> (projections, all tiles)", "gemm_kernel<unsigned short, 64, 64, 64, 2>"),
-                  ("relpos_flash_dma_kernel (rel-pos attention)", "relpos_flash_dma_kernel"))
+                  ("gemm_kernel<float> (exact-f32 projections, all tiles)" if fp32 else
+                   "gemm_kernel<bf16> (projections, all tiles)",
+                   "gemm_kernel<float" if fp32 else "gemm_kernel<unsigned short, 64, 64, 64, 2>"),
+                  ("relpos_flash_kernel<float> (rel-pos attention, exact f32)" if fp32 else
+                   "relpos_flash_dma_kernel (rel-pos attention)",
+                   "relpos_flash_kernel<float" if fp32 else "relpos_flash_dma_kernel"))
         for p, (label, pmc_key) in zip(probes, labels):
             ms, n, fl = p.replay_time()
             if n:
@@ -807,6 +831,7 @@ def main():
         progress("per-kernel launch timing done")
         dom = max(kern.values(), key=lambda k: k["step_share_ms"]) if kern else None
         traffic = load_traffic()
+        peak = PEAK_F32_TFLOPS if fp32 else PEAK_BF16_TFLOPS
         res = {
             "metric": "audio-sec/sec Fbank→Conformer fwd (16kHz, B=32×15s) at 1/2/4/8 GPU",
             "value": round(value, 1),
@@ -819,16 +844,17 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "fp32" if fp32 else "bf16",
             "data": "synthetic (0.1·N(0,1) 16 kHz, random-init weights)",
             "config": {"workload": f"Fbank(80)→ConvFrontEnd(64,32)→Conformer 12L d={args.d_model} H=4 ffn=1024 "
-                                   f"k=31 encode, B={args.batch}×15s per GPU",
+                                   f"k=31 encode, B={args.batch}×15s per GPU" +
+                                   (" (fp32: exact-f32 MFMA, the parity path)" if fp32 else ""),
                        "global_batch": world * args.batch, "seq_len": T_e, "parallelism": f"replicas{world}",
                        "hip_graph": graph is not None},
             "roofline": None if dom is None else {
-                "bound": "mfma", "kernel": dom["kernel"], "achieved": dom["achieved"], "peak": PEAK_BF16_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(dom["achieved"] / PEAK_BF16_TFLOPS, 4),
-                "traffic": traffic.get(dom["pmc_key"]),
+                "bound": "mfma", "kernel": dom["kernel"], "achieved": dom["achieved"], "peak": peak,
+                "unit": "TFLOP/s", "frac": round(dom["achieved"] / peak, 4),
+                "traffic": None if fp32 else traffic.get(dom["pmc_key"]),
                 "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch)",
                 "launches_per_step": dom["launches_per_step"], "avg_launch_us": dom["avg_launch_us"],
                 "step_algorithmic_tflop": round(total_flops / 1e12, 4),

@@ -337,3 +337,27 @@ def test_fbank_misaligned_view(dev):
     out = fb(xd)
     assert_close(out, OF.fbank(flat[1:].view(3, 16000), n_mels=80), name="fbank of a 4-B offset view")
     assert torch.equal(out, fb(xd.clone()))
+
+
+@pytest.mark.parametrize("T", [1, 3, 5, 8, 9, 12, 17, 100, 1501])
+@pytest.mark.parametrize("F", [4, 40, 80, 240])
+def test_concat_deltas_edges_vs_oracle(dev, T, F):
+    """The concat deltas (window 5) against the oracle's
+    Δ / ΔΔ restatement (features.py:806-852) for T around the run length
+    and the utterance edges; the top_db-floor form against clamp + deltas
+    bit for bit."""
+    import oracle.features as OF
+    from speechbrain_amd import ops
+    g = torch.Generator().manual_seed(T * 1000 + F)
+    x = torch.randn(3, T, F, generator=g)
+    out = ops.deltas(x.to(dev), 5, True)
+    d1 = OF.deltas(x)
+    d2 = OF.deltas(d1)
+    ref = torch.cat([x, d1, d2], dim=-1)
+    assert_close(out, ref, rtol=1e-5, name=f"deltas T={T} F={F}")
+    slots = torch.randn(3, 7, generator=g).to(dev)
+    top_db = 1.5
+    floored = ops.deltas_floor(x.to(dev), 5, slots, top_db)
+    fl = slots.max(dim=1).values - top_db
+    ref2 = ops.deltas(torch.maximum(x.to(dev), fl[:, None, None]), 5, True)
+    assert torch.equal(floored, ref2)

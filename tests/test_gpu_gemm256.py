@@ -1,0 +1,99 @@
+"""The 256 x 256-tile GEMMs (csrc/gemm256.hip) on the GPU: bf16 (sbk_gemm
+tile 30, and the automatic dispatch on a config-5 shape) against an fp32
+matmul of the same bf16 operands, every epilogue (bias, Swish / GELU,
+row mask, alpha, residual; fp32 / bf16 out), M tails; MXFP8
+(sbk_mx_gemm256) against the dequantised operands' product, fp32 / bf16 /
+MXFP8 outputs, and equal to sbk_mx_gemm's small-tile kernel where both run."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rnd(dev, *s):
+    return torch.rand(*s, device=dev) * 2 - 1
+
+
+def _epi(x, b, act, mask, alpha, r):
+    x = x + b
+    if act == "swish":
+        x = x * torch.sigmoid(x)
+    elif act == "gelu":
+        x = torch.nn.functional.gelu(x)
+    x = torch.where(mask.bool()[:, None], torch.zeros_like(x), alpha * x)
+    return x + r
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 512, 128), (1000, 768, 256), (777, 256, 1024)])
+def test_gemm256_bf16_epilogues(dev, M, N, K):
+    from speechbrain_amd import _enc
+    torch.manual_seed(M)
+    a, w = _rnd(dev, M, K).to(torch.bfloat16), _rnd(dev, N, K).to(torch.bfloat16)
+    b, r = _rnd(dev, N), _rnd(dev, M, N)
+    mask = (torch.rand(M, device=dev) < 0.1).to(torch.uint8)
+    ref = (a.double().cpu() @ w.double().cpu().t()).float().to(dev)  # exact-enough reference
+    for act in (None, "swish", "gelu"):
+        x = _epi(ref, b, act, mask, 0.5, r)
+        for odt in (torch.float32, torch.bfloat16):
+            o = _enc.gemm(a, w, bias=b, act=act, res=r, alpha=0.5, rowmask=mask, out_dtype=odt, tile=30)
+            tol = (1e-5 * math.sqrt(K) + (3e-6 if act == "gelu" else 0.0)) if odt == torch.float32 else 8e-3
+            err = float(((o.float() - x).abs() / x.abs().clamp(min=1.0)).max())
+            assert err <= tol, (act, odt, err)
+
+
+def test_gemm256_auto_dispatch_config5_shape(dev):
+    """(M, N, K) = (4096, 4096, 1024) takes the 256 tile by default: the
+    result equals tile 30 bit for bit and the fp32 product within 1e-5 rel."""
+    from speechbrain_amd import _enc
+    torch.manual_seed(1)
+    a, w = _rnd(dev, 4096, 1024).to(torch.bfloat16), _rnd(dev, 4096, 1024).to(torch.bfloat16)
+    o0 = _enc.gemm(a, w, out_dtype=torch.float32)
+    o30 = _enc.gemm(a, w, out_dtype=torch.float32, tile=30)
+    assert torch.equal(o0, o30)
+    ref = (a.double().cpu() @ w.double().cpu().t()).float().to(dev)
+    assert float(((o0 - ref).abs() / ref.abs().clamp(min=1.0)).max()) < 1e-5 * 32
+
+
+def _mx_call(fn, a, w, M, N, K, mode, bias=None, act=0, res=None):
+    from speechbrain_amd import _w2v
+    from speechbrain_amd._lib import ptr, stream_of
+    out, sc = _w2v._empty_out(M, N, mode, a.q.device)
+    rc = fn(ptr(a.q), ptr(a.s), a.q.stride(0), a.s.stride(0), M, 0, 0, ptr(w.q), ptr(w.s), w.q.stride(0),
+            w.s.stride(0), M, N, K, ptr(bias), act, 1.0, ptr(res), res.stride(0) if res is not None else 0,
+            ptr(out), out.stride(0), mode, ptr(sc) if mode == 2 else None, sc.stride(0) if mode == 2 else 0,
+            stream_of(a.q))
+    assert rc == 0, rc
+    return out, sc
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 256, 128), (1000, 512, 256), (2048, 768, 1024)])
+def test_mx256_vs_dequantised_and_small_tile(dev, M, N, K):
+    from speechbrain_amd import _w2v
+    from speechbrain_amd._lib import lib
+    L = lib()
+    torch.manual_seed(K)
+    a = _w2v.mx_quant(_rnd(dev, M, K))
+    w = _w2v.mx_quant(_rnd(dev, N, K))
+    ref = (_w2v.mx_dequant(a).double().cpu() @ _w2v.mx_dequant(w).double().cpu().t()).float().to(dev)
+    bias, res = _rnd(dev, N), _rnd(dev, M, N)
+    o, _ = _mx_call(L.sbk_mx_gemm256, a, w, M, N, K, 0, bias, 0, res)
+    # the block-scaled MFMA's own accumulation is coarser than an fp32 sum of
+    # the exact e4m3 products (measured 1.7e-4 .. 4.7e-4 of max(1, |ref|) at
+    # K = 128 .. 1024, identical in the small-tile kernel): bound it, and
+    # equality with that kernel below pins this one bit for bit
+    err = float(((o - (ref + bias + res)).abs() / (ref + bias + res).abs().clamp(min=1.0)).max())
+    assert err < 4e-5 * math.sqrt(K), err
+    # fp32 / bf16 / MXFP8 outputs equal the 128-tile kernel's (same MFMA, same K order;
+    # at these M sbk_mx_gemm runs its small-tile kernel)
+    for mode, act in ((0, 4), (1, 4), (2, 4), (2, 0)):
+        o0, s0 = _mx_call(L.sbk_mx_gemm, a, w, M, N, K, mode, bias, act)
+        o1, s1 = _mx_call(L.sbk_mx_gemm256, a, w, M, N, K, mode, bias, act)
+        if act == 4:  # the 256 tile's GELU is the 1.5e-7 erf approximation: compare values
+            d0 = o0.float() if mode < 2 else _w2v.mx_dequant(_w2v.MX(o0, s0))
+            d1 = o1.float() if mode < 2 else _w2v.mx_dequant(_w2v.MX(o1, s1))
+            tol = 1e-5 if mode == 0 else (8e-3 if mode == 1 else 0.13)
+            assert float(((d0 - d1).abs() / d0.abs().clamp(min=1.0)).max()) <= tol, mode
+        else:
+            assert torch.equal(o0, o1) and torch.equal(s0, s1), mode
