@@ -760,7 +760,7 @@ SBK_API int sbk_gemm(int dtype_bf16, const void* A, int lda, const void* W, int 
   // tile 30: the 256 x 256 multi-phase kernel (gemm256.hip), N % 256 == 0,
   // K % 64 == 0; taken by default when it fills the chip (>= 180 tiles) at
   // K >= 256 — config 5's projections: 0.97-1.03 PF/s against 0.67-0.82 for
-  // the best of the other tiles (profiles/r05c_g256.log)
+  // the best of the other tiles (profiles/r05c_g256_shapes.log)
   if (dtype_bf16 && (tile == 30 || tile == 0)) {
     const Gemm256Epi e{bias, act, slope, res, ldr, alpha, rowmask, out, ldc, out_bf16};
     const bool ok = gemm256_supported(M, N, K, lda, ldw, A, W, e);
