@@ -454,15 +454,35 @@ def run_c2(args, world, rank, dev):
              4.0 * B * T * 80 + 4.0 * B * T * 240, ("deltas4_concat_kernel",)),
             ("specaugment (in place: roll4 warp + sums, fixup4 masked cells)", sa_kernels, 2 * 4.0 * B * T * 240,
              ("roll4_kernel<true, true, true>", "fixup4_kernel"))):
+        # device time per call: `reps` calls captured in one HIP graph and
+        # replayed (host dispatch excluded, kernels back to back)
         for _ in range(2):
             fn()
         torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         reps = 20
-        e0.record()
-        for _ in range(reps):
-            fn()
-        e1.record()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        try:
+            gs = torch.cuda.Stream()
+            gs.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(gs):
+                fn()
+            torch.cuda.current_stream().wait_stream(gs)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(reps):
+                    fn()
+            g.replay()
+            torch.cuda.synchronize()
+            e0.record()
+            g.replay()
+            e1.record()
+        except RuntimeError as exc:  # not capturable: eager back-to-back calls
+            progress(f"probe {name}: eager timing ({exc})")
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(reps):
+                fn()
+            e1.record()
         torch.cuda.synchronize()
         us = 1000.0 * e0.elapsed_time(e1) / reps
         tr = [traffic.get(k) for k in pmc]

@@ -1,10 +1,13 @@
-# chain vs GEMM-FFN A/B; fresh s_memtime timelines of the C3 layer kernels and the Fbank kernel (probe builds, never the product)
+# augment parity on the roll route (new long / narrow / bilinear cases); then the r05g timelines
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp && \
-timeout -k 10 240 python -u scripts/chain_gemm_ab.py > gpurun_out/r05g_chain_gemm_ab.log 2>&1 && \
+timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_augment.py > gpurun_out/r05i_aug.log 2>&1
+rc=$?
+grep -E "passed|failed|FAILED|Error" gpurun_out/r05i_aug.log | tail -5
+[ $rc -ne 0 ] && exit $rc
 CM_PRE=1 SBK_PROBE_LIB=gpurun_probe_CMTL.so timeout -k 10 120 python -u scripts/cm_tl.py > gpurun_out/r05g_cm_tl.log 2>&1 && \
 SBK_PROBE_LIB=gpurun_probe_FFTL.so timeout -k 10 120 python -u scripts/ffn_chain_tl.py > gpurun_out/r05g_chain_tl.log 2>&1 && \
 SBK_PROBE_LIB=gpurun_probe_ATTL.so timeout -k 10 120 python -u scripts/att_dma_tl.py > gpurun_out/r05g_att_tl.log 2>&1 && \
 SBK_PROBE_LIB=gpurun_probe_RFTL.so timeout -k 10 120 python -u scripts/rf_tl.py > gpurun_out/r05g_rf_tl.log 2>&1
 rc=$?
-cat gpurun_out/r05g_chain_gemm_ab.log gpurun_out/r05g_cm_tl.log
+cat gpurun_out/r05g_cm_tl.log
 exit $rc

@@ -461,28 +461,50 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
 
   // ---- phase 2: depthwise conv (register window) -> fp32 tile; LN1 -> Swish -> V (over U) ----
   {
-    // 2a: thread (channel c, quarter h) slides the taps down its channel for 12 frames
+    // 2a: thread (channel c, quarter h) slides the taps down its channel for
+    // 12 frames, two taps per v_dot2c_f32_bf16 (bf16 operands, fp32
+    // accumulation: Conv1d under bf16 autocast, which this kernel serves):
+    // tap pair j = (2j, 2j+1) against the window pair (g[i+2j], g[i+2j+1]),
+    // an even-aligned pair E for even frames i and an odd-aligned one O for
+    // odd frames.  (fp32 FMAs, one tap per instruction: 8.5k cycles of the
+    // 58k per workgroup, VALU-bound at 4 waves per SIMD.)
     const int c = tid & (CM_D - 1), h = tid >> 8;  // channel, quarter of the frames
     constexpr int NF = CM_BM / (CM_NT / CM_D);
-    float wk[CM_KMAX];
+    constexpr int NP = (CM_KMAX + 1) / 2;          // tap pairs (tap 31 is zero)
+    float wk[2 * NP];
 #pragma unroll
     // unconditional loads (clamped address + select): a guarded load compiled
     // to a branch and a full wait per element, serialising the 31 tap loads
-    // and the 42 window reads
-    for (int k = 0; k < CM_KMAX; ++k) {  // (K, D): coalesced
+    // and the 43 window reads
+    for (int k = 0; k < 2 * NP; ++k) {  // (K, D): coalesced
       const float v = a.wc[min(k, a.K - 1) * CM_D + c];
       wk[k] = k < a.K ? v : 0.f;
     }
     const float bias = a.bc ? a.bc[c] : 0.f;
-    static_assert((CM_NT / CM_D) * NF + CM_KMAX - 1 <= CM_ROWS, "every window row is staged");
-    float win[NF + CM_KMAX - 1];
+    static_assert((CM_NT / CM_D) * NF + 2 * NP - 1 <= CM_ROWS, "every window row is staged");
+    static_assert(NF % 2 == 0, "frame pairs");
+    typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+    bf2 tp[NP], ev[NF / 2 + NP - 1], od[NF / 2 + NP - 1];
+    // the tap pairs first (the fp32 taps die here: 128 VGPRs at 4 waves per SIMD)
 #pragma unroll
-    for (int r = 0; r < NF + CM_KMAX - 1; ++r) win[r] = bf16_to_f32(Gs[(h * NF + r) * CM_S + c]);
+    for (int j = 0; j < NP; ++j) {
+      tp[j] = __builtin_bit_cast(bf2, pack_bf16x2(wk[2 * j], wk[2 * j + 1]));
+      asm volatile("" : "+v"(tp[j]));
+    }
+    const unsigned short* Gu = reinterpret_cast<const unsigned short*>(Gs) + h * NF * CM_S + c;
+    uint32_t g0 = Gu[0];
+#pragma unroll
+    for (int r = 0; r < NF / 2 + NP - 1; ++r) {
+      const uint32_t g1 = Gu[(2 * r + 1) * CM_S], g2 = Gu[(2 * r + 2) * CM_S];
+      ev[r] = __builtin_bit_cast(bf2, g0 | (g1 << 16));
+      od[r] = __builtin_bit_cast(bf2, g1 | (g2 << 16));
+      g0 = g2;
+    }
 #pragma unroll
     for (int i = 0; i < NF; ++i) {
       float s = bias;
 #pragma unroll
-      for (int k = 0; k < CM_KMAX; ++k) s = fmaf(wk[k], win[i + k], s);
+      for (int j = 0; j < NP; ++j) s = __builtin_amdgcn_fdot2_f32_bf16(tp[j], (i & 1) ? od[i / 2 + j] : ev[i / 2 + j], s, false);
       Cv[(h * NF + i) * CM_D + c] = s;
     }
   }
@@ -511,23 +533,37 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
 #pragma unroll
     for (int mt = 0; mt < CM_MT3; ++mt) asm volatile("" : "+v"(km[mt]));
     const float gm[4] = {g14[0], g14[1], g14[2], g14[3]}, bt[4] = {b14[0], b14[1], b14[2], b14[3]};
-    for (int fi = w; fi < CM_BM; fi += CM_NW) {
-      const float4 v4 = *reinterpret_cast<const float4*>(Cv + fi * CM_D + lane * 4);
-      float v[4] = {v4.x, v4.y, v4.z, v4.w};
-      const float mean = wave_sum_v((v[0] + v[1]) + (v[2] + v[3])) * (1.0f / CM_D);
+    // the wave's CM_BM / CM_NW frames side by side: their four cross-lane
+    // reduction chains interleave instead of running back to back
+    constexpr int FPW = CM_BM / CM_NW;
+    float v[FPW][4], mean[FPW], rstd[FPW];
+#pragma unroll
+    for (int u = 0; u < FPW; ++u) {
+      const float4 v4 = *reinterpret_cast<const float4*>(Cv + (w + u * CM_NW) * CM_D + lane * 4);
+      v[u][0] = v4.x; v[u][1] = v4.y; v[u][2] = v4.z; v[u][3] = v4.w;
+    }
+#pragma unroll
+    for (int u = 0; u < FPW; ++u) mean[u] = wave_sum_v((v[u][0] + v[u][1]) + (v[u][2] + v[u][3])) * (1.0f / CM_D);
+#pragma unroll
+    for (int u = 0; u < FPW; ++u) {
       float q = 0.f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) q += (v[e] - mean) * (v[e] - mean);
-      const float rstd = 1.0f / sqrtf(wave_sum_v(q) * (1.0f / CM_D) + a.eps1);
+      for (int e = 0; e < 4; ++e) q += (v[u][e] - mean[u]) * (v[u][e] - mean[u]);
+      rstd[u] = q;
+    }
+#pragma unroll
+    for (int u = 0; u < FPW; ++u) rstd[u] = 1.0f / sqrtf(wave_sum_v(rstd[u]) * (1.0f / CM_D) + a.eps1);
+#pragma unroll
+    for (int u = 0; u < FPW; ++u) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float z = (v[e] - mean) * rstd * gm[e] + bt[e];
-        v[e] = z * __builtin_amdgcn_rcpf(1.0f + __expf(-z));  // bf16 output (as the GLU above)
+        const float z = (v[u][e] - mean[u]) * rstd[u] * gm[e] + bt[e];
+        v[u][e] = z * __builtin_amdgcn_rcpf(1.0f + __expf(-z));  // bf16 output (as the GLU above)
       }
       uint2 pk;
-      pk.x = pack_bf16x2(v[0], v[1]);
-      pk.y = pack_bf16x2(v[2], v[3]);
-      *reinterpret_cast<uint2*>(Us + fi * CM_S + lane * 4) = pk;
+      pk.x = pack_bf16x2(v[u][0], v[u][1]);
+      pk.y = pack_bf16x2(v[u][2], v[u][3]);
+      *reinterpret_cast<uint2*>(Us + (w + u * CM_NW) * CM_S + lane * 4) = pk;
     }
   }
   lds_barrier();

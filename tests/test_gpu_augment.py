@@ -124,3 +124,53 @@ def test_specaugment_paths_vs_oracle(dev, N, T, F, win, zero, warp):
                               time_mask=True, n_time_mask=2, replace_with_zero=zero,
                               freq_mask_width=kw["freq_mask_width"], time_mask_width=40)
         assert_close(y, ref, rtol=1e-5, name=f"N{N} T{T} F{F} win{win} seed{seed}")
+
+
+@pytest.mark.parametrize("N,T,F,win,zero", [
+    (2, 257, 240, 5, False),
+    (2, 512, 80, 10, False),   # |c - w| + 3 up to 13
+    (3, 769, 40, 10, True),    # zero fill
+    (2, 1000, 24, 5, False),   # F / 4 = 6: two-column slabs
+    (2, 600, 20, 5, False),    # F / 4 = 5: one-column slabs
+])
+def test_specaugment_long_and_narrow_vs_oracle(dev, N, T, F, win, zero):
+    """The in-place route on longer utterances (T around multiples of 256,
+    up to three windows of the roll kernel's ring) and on 1- / 2-column
+    slabs (F / 4 odd or 6) against the oracle, masks and mean fills
+    included."""
+    from speechbrain_amd.lobes.augment import SpecAugment
+    x = torch.randn(N, T, F, generator=torch.Generator().manual_seed(3 * T + F)) * 10 - 40
+    kw = dict(time_warp=True, time_warp_window=win, freq_mask=True, n_freq_mask=2, time_mask=True, n_time_mask=2,
+              replace_with_zero=zero, freq_mask_width=min(30, F // 2), time_mask_width=40)
+    for seed in (21, 22, 23, 24):
+        torch.manual_seed(seed)
+        aug = SpecAugment(**kw)
+        y = aug(x.clone().to(dev))
+        torch.manual_seed(seed)
+        ref = OA.spec_augment(x.clone(), time_warp_on=True, time_warp_window=win, freq_mask=True, n_freq_mask=2,
+                              time_mask=True, n_time_mask=2, replace_with_zero=zero,
+                              freq_mask_width=kw["freq_mask_width"], time_mask_width=40)
+        assert_close(y, ref, rtol=1e-5, name=f"N{N} T{T} F{F} win{win} seed{seed}")
+
+
+@pytest.mark.parametrize("T", [300, 1501])
+def test_specaugment_bilinear_warp_in_place(dev, T):
+    """The bilinear warp in place: torch's align_corners bilinear
+    resize of the two segments (augment.py:134-148) at the drawn c, w."""
+    import torch.nn.functional as Fn
+    from speechbrain_amd.lobes.augment import SpecAugment
+    x = torch.randn(3, T, 80, generator=torch.Generator().manual_seed(T)) * 10 - 40
+    for seed in (31, 32, 33):
+        torch.manual_seed(seed)
+        aug = SpecAugment(time_warp=True, time_warp_window=8, time_warp_mode="bilinear", freq_mask=False,
+                          time_mask=False)
+        y = aug(x.clone().to(dev))
+        c, w, _, _ = aug.last_draws
+        if c < 0:
+            assert_close(y, x, rtol=0, name="identity")
+            continue
+        x4 = x.unsqueeze(1)
+        left = Fn.interpolate(x4[:, :, :c], size=(w, 80), mode="bilinear", align_corners=True)
+        right = Fn.interpolate(x4[:, :, c:], size=(T - w, 80), mode="bilinear", align_corners=True)
+        ref = torch.cat([left, right], dim=2).squeeze(1)
+        assert_close(y, ref, rtol=1e-5, name=f"bilinear T{T} seed{seed}")
