@@ -521,6 +521,19 @@ int sbk_im2col(const void* x, int x_bf16, int B, int Ti, int Fi, int Ci, int kt,
 int sbk_col2im(const void* dcol, int dcol_bf16, int B, int Ti, int Fi, int Ci, int kt, int kf, int st, int sf, int pt,
                int pf, int ldcol, void* dx, int dx_bf16, void* stream);
 
+/* The general Conv2d geometry of the standalone drop-in (CNN.py:556-700):
+ * dilation (dt, df), leading pads (pt, pf; the trailing ones follow from the
+ * given To, Fo), pad mode 0 reflect, 1 zeros, 2 replicate, 3 circular
+ * (F.pad; "same" with any padding_mode, "valid", "causal").  Same col layout
+ * as sbk_im2col.  sbk_col2im_x: its adjoint through dxpad, fp32 scratch of
+ * B*Tp*Fp*Ci with Tp = (To-1) st + (kt-1) dt + 1, Fp alike (gathered onto
+ * the padded grid, then folded onto x in a fixed order: deterministic). */
+int sbk_im2col_x(const void* x, int x_bf16, int B, int Ti, int Fi, int Ci, int kt, int kf, int st, int sf, int dt,
+                 int df, int pt, int pf, int To, int Fo, int mode, int ldcol, void* col, int col_bf16, void* stream);
+int sbk_col2im_x(const void* dcol, int dcol_bf16, int B, int Ti, int Fi, int Ci, int kt, int kf, int st, int sf,
+                 int dt, int df, int pt, int pf, int To, int Fo, int mode, int ldcol, float* dxpad, void* dx,
+                 int dx_bf16, void* stream);
+
 /* Transducer_joint "sum" (transducer_joint.py:57-95): z[b,t,u,:] = act(tn[b,t,:] + pn[b,u,:]),
  * act 0 none, 3 LeakyReLU(slope), 5 tanh, 6 ReLU; tn (B, T, J), pn (B, U1, J) fp32, z fp32/bf16.
  * Backward: dtn = sum_u dz act', dpn = sum_t dz act' — one pass over dz (block per

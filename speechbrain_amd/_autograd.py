@@ -541,6 +541,56 @@ class ConvBlockFn(Function):
         return dx, dw, db, dlw, dlb, None, None, None, None, None
 
 
+class Conv2dXFn(Function):
+    """The standalone Conv2d's general geometry (CNN.py:616-700): dilation,
+    per-side padding and the F.pad modes, as sbk_im2col_x + the MFMA GEMM.
+    geom = (kT, kF, sT, sF, dT, dF, pT, pF, To, Fo, mode) with pT / pF the
+    leading pads and mode 0 reflect, 1 zeros, 2 replicate, 3 circular.
+    x (B, Ti, Fi, Ci) -> (B, To, Fo, Co); w (Co, Ci, kF, kT)."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, dtype, out_dtype, geom):
+        x = _cont(x)
+        kt, kf, st, sf, dt, df, pt, pf, To, Fo, mode = geom
+        B, Ti, Fi, Ci = x.shape
+        Co = w.shape[0]
+        vec = 8 if dtype == _bf16 else 4
+        K = kt * kf * Ci
+        ldcol = -(-K // vec) * vec
+        L = lib()
+        s = stream_of(x)
+        col = torch.empty(B * To * Fo, ldcol, device=x.device, dtype=dtype)
+        check(L.sbk_im2col_x(ptr(x), _bf(x), B, Ti, Fi, Ci, kt, kf, st, sf, dt, df, pt, pf, To, Fo, mode, ldcol,
+                             ptr(col), _bf(col), s), "sbk_im2col_x")
+        wp = torch.zeros(Co, ldcol, device=x.device, dtype=_f32)
+        wp[:, :K] = w.detach().permute(0, 3, 2, 1).reshape(Co, K)
+        wk = _as(wp, dtype)
+        c = _enc.gemm(col, wk, bias=None if bias is None else bias.detach(), out_dtype=out_dtype)
+        ctx.save_for_backward(col, wk)
+        ctx.dims = (B, Ti, Fi, Ci, Co, ldcol, bias is not None, tuple(w.shape), x.dtype, geom)
+        return c.view(B, To, Fo, Co)
+
+    @staticmethod
+    def backward(ctx, dy):
+        col, wk = ctx.saved_tensors
+        B, Ti, Fi, Ci, Co, ldcol, has_bias, wshape, xdt, geom = ctx.dims
+        kt, kf, st, sf, dt, df, pt, pf, To, Fo, mode = geom
+        dc = _cont(dy).view(B * To * Fo, Co)
+        g = _as(dc, col.dtype)
+        K = kt * kf * Ci
+        dw = wgrad(g, col)[:, :K].reshape(Co, kt, kf, Ci).permute(0, 3, 2, 1).reshape(wshape)
+        db = rowsum(dc) if has_bias else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dcol = dgrad(g, wk)
+            Tp, Fp = (To - 1) * st + (kt - 1) * dt + 1, (Fo - 1) * sf + (kf - 1) * df + 1
+            dxpad = torch.empty(B * Tp * Fp * Ci, device=col.device, dtype=_f32)
+            dx = torch.empty(B, Ti, Fi, Ci, device=col.device, dtype=xdt)
+            check(lib().sbk_col2im_x(ptr(dcol), _bf(dcol), B, Ti, Fi, Ci, kt, kf, st, sf, dt, df, pt, pf, To, Fo,
+                                     mode, ldcol, ptr(dxpad), ptr(dx), _bf(dx), stream_of(col)), "sbk_col2im_x")
+        return dx, dw, db, None, None, None
+
+
 # ---------------------------------------------------------- transducer joint
 class JointFn(Function):
     """Transducer_joint "sum" + nonlinearity (transducer_joint.py:57-95):

@@ -59,7 +59,7 @@ def gemm(a, w, bias=None, act=None, slope=0.0, res=None, alpha=1.0, rowmask=None
         raise ValueError("gemm allocates its output (out= is not supported)")
     if a.dtype != w.dtype:
         raise TypeError(f"gemm operand dtypes differ: {a.dtype} vs {w.dtype}")
-    if a.stride(-1) != 1 or w.stride(-1) != 1:
+    if (a.stride(-1) != 1 and a.shape[-1] > 1) or (w.stride(-1) != 1 and w.shape[-1] > 1):
         raise ValueError("gemm operands must be K-contiguous")
     if res is not None and (res.dtype != _f32 or res.stride(-1) != 1):
         raise ValueError("residual must be fp32, row-contiguous")

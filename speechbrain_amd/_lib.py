@@ -139,6 +139,8 @@ SIGNATURES = {
     "sbk_dwconv_bwd": [_vp, _i, _vp, _i, _i, _i, _vp, _i, _i, _vp, _i, _vp, _vp],
     "sbk_im2col": [_vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _vp],
     "sbk_col2im": [_vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _vp],
+    "sbk_im2col_x": [_vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _vp],
+    "sbk_col2im_x": [_vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp],
     "sbk_joint_fwd": [_vp, _vp, _i, _i, _i, _i, _i, _f, _vp, _i, _vp],
     "sbk_dropout_add": [_vp, _i, _vp, _ll, _i, _vp, _f, _f, ctypes.c_ulonglong, _vp, _i, _vp],
     "sbk_joint_bwd": [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp],

@@ -1248,6 +1248,145 @@ SBK_API int sbk_col2im(const void* dcol, int dcol_bf16, int B, int Ti, int Fi, i
   return 0;
 }
 
+// ---- general Conv2d geometry: dilation, leading / trailing padding per
+// axis and the F.pad modes (0 reflect, 1 zeros, 2 replicate, 3 circular):
+// the standalone Conv2d drop-in (CNN.py:556-700: "same" with any
+// padding_mode, "valid", "causal", dilation; groups and skip_transpose by
+// the host).  col (B*To*Fo, ldcol), column order (time tap, freq tap, ci).
+struct ConvGeomX {
+  int kt, kf, st, sf, dt, df, pt, pf, mode;
+};
+
+// input index of padded-minus-lead position s, or -1 for a zero
+__device__ __forceinline__ int pad_map(int s, int n, int mode) {
+  if (s >= 0 && s < n) return s;
+  if (mode == 1) return -1;
+  if (mode == 2) return s < 0 ? 0 : n - 1;
+  if (mode == 3) return ((s % n) + n) % n;
+  return reflect_idx(s, n);  // one reflection (host: pad < n)
+}
+
+__global__ void im2colx_kernel(const void* __restrict__ x, int x_bf16, int B, int Ti, int Fi, int Ci, int To, int Fo,
+                               ConvGeomX gm, int ldcol, void* __restrict__ col, int col_bf16) {
+  const long long n = (long long)B * To * Fo * ldcol;
+  const int kcols = gm.kt * gm.kf * Ci;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int kk = (int)(i % ldcol);
+    long long q = i / ldcol;
+    if (kk >= kcols) {
+      stv(col, i, 0.f, col_bf16);
+      continue;
+    }
+    const int ci = kk % Ci;
+    const int kf = (kk / Ci) % gm.kf;
+    const int kt = kk / (gm.kf * Ci);
+    const int fo = (int)(q % Fo); q /= Fo;
+    const int to = (int)(q % To);
+    const int b = (int)(q / To);
+    const int ti = pad_map(to * gm.st + kt * gm.dt - gm.pt, Ti, gm.mode);
+    const int fi = pad_map(fo * gm.sf + kf * gm.df - gm.pf, Fi, gm.mode);
+    const float v = (ti < 0 || fi < 0) ? 0.f : ldv(x, (((long long)b * Ti + ti) * Fi + fi) * Ci + ci, x_bf16);
+    stv(col, i, v, col_bf16);
+  }
+}
+
+// the adjoint, first onto the padded grid (Tp x Fp, fp32): every padded
+// position gathers the (output position, tap) pairs that read it
+__global__ void col2padx_kernel(const void* __restrict__ dcol, int dcol_bf16, int B, int Tp, int Fp, int Ci, int To,
+                                int Fo, ConvGeomX gm, int ldcol, float* __restrict__ dxp) {
+  const long long n = (long long)B * Tp * Fp * Ci;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % Ci);
+    long long q = i / Ci;
+    const int fp = (int)(q % Fp); q /= Fp;
+    const int tp = (int)(q % Tp);
+    const int b = (int)(q / Tp);
+    float s = 0.f;
+    for (int kt = 0; kt < gm.kt; ++kt) {
+      const int d = tp - kt * gm.dt;
+      if (d < 0 || d % gm.st) continue;
+      const int to = d / gm.st;
+      if (to >= To) continue;
+      for (int kf = 0; kf < gm.kf; ++kf) {
+        const int df = fp - kf * gm.df;
+        if (df < 0 || df % gm.sf) continue;
+        const int fo = df / gm.sf;
+        if (fo >= Fo) continue;
+        s += ldv(dcol, (((long long)b * To + to) * Fo + fo) * ldcol + (kt * gm.kf + kf) * Ci + ci, dcol_bf16);
+      }
+    }
+    dxp[i] = s;
+  }
+}
+
+// then folded onto the input: dx[ti, fi] = sum of the padded positions that
+// map onto it (the direct one and, in the pad zones, its reflections /
+// replications / wraps), in a fixed order (deterministic)
+__global__ void foldx_kernel(const float* __restrict__ dxp, int B, int Tp, int Fp, int Ti, int Fi, int Ci, int pt,
+                             int pf, int mode, void* __restrict__ dx, int dx_bf16) {
+  const long long n = (long long)B * Ti * Fi * Ci;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % Ci);
+    long long q = i / Ci;
+    const int fi = (int)(q % Fi); q /= Fi;
+    const int ti = (int)(q % Ti);
+    const int b = (int)(q / Ti);
+    // candidates per axis: the leading pad zone, the direct position, the
+    // trailing pad zone (the interior maps 1:1)
+    const int zt = max(0, Tp - pt - Ti), zf = max(0, Fp - pf - Fi);
+    float s = 0.f;
+    for (int u = 0; u < pt + 1 + zt; ++u) {
+      const int tp = u < pt ? u : (u == pt ? ti + pt : pt + Ti + (u - pt - 1));
+      if (tp >= Tp || pad_map(tp - pt, Ti, mode) != ti) continue;
+      for (int v = 0; v < pf + 1 + zf; ++v) {
+        const int fp = v < pf ? v : (v == pf ? fi + pf : pf + Fi + (v - pf - 1));
+        if (fp >= Fp || pad_map(fp - pf, Fi, mode) != fi) continue;
+        s += dxp[(((long long)b * Tp + tp) * Fp + fp) * Ci + ci];
+      }
+    }
+    stv(dx, i, s, dx_bf16);
+  }
+}
+
+namespace {
+bool convx_ok(int B, int Ti, int Fi, int Ci, int kt, int kf, int st, int sf, int dt, int df, int pt, int pf, int To,
+              int Fo, int mode, int ldcol) {
+  return B > 0 && Ti > 0 && Fi > 0 && Ci > 0 && kt > 0 && kf > 0 && st > 0 && sf > 0 && dt > 0 && df > 0 && pt >= 0 &&
+         pf >= 0 && To > 0 && Fo > 0 && mode >= 0 && mode <= 3 && ldcol >= kt * kf * Ci &&
+         (mode != 0 || (pt < Ti && pf < Fi)) &&
+         // every tap of the last output lies within one pad of the input
+         (To - 1) * st + (kt - 1) * dt - pt < Ti + (mode == 0 ? Ti - 1 : 1 << 30) &&
+         (Fo - 1) * sf + (kf - 1) * df - pf < Fi + (mode == 0 ? Fi - 1 : 1 << 30);
+}
+}  // namespace
+
+SBK_API int sbk_im2col_x(const void* x, int x_bf16, int B, int Ti, int Fi, int Ci, int kt, int kf, int st, int sf,
+                         int dt, int df, int pt, int pf, int To, int Fo, int mode, int ldcol, void* col, int col_bf16,
+                         void* stream) {
+  if (!convx_ok(B, Ti, Fi, Ci, kt, kf, st, sf, dt, df, pt, pf, To, Fo, mode, ldcol)) return SBK_ERR_ARG;
+  im2colx_kernel<<<grid_for((long long)B * To * Fo * ldcol, 256), 256, 0, (hipStream_t)stream>>>(
+      x, x_bf16, B, Ti, Fi, Ci, To, Fo, ConvGeomX{kt, kf, st, sf, dt, df, pt, pf, mode}, ldcol, col, col_bf16);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
+// dxpad: fp32 scratch of B*Tp*Fp*Ci, Tp = (To-1) st + (kt-1) dt + 1 (and Fp
+// alike): the padded extent the outputs read
+SBK_API int sbk_col2im_x(const void* dcol, int dcol_bf16, int B, int Ti, int Fi, int Ci, int kt, int kf, int st,
+                         int sf, int dt, int df, int pt, int pf, int To, int Fo, int mode, int ldcol, float* dxpad,
+                         void* dx, int dx_bf16, void* stream) {
+  if (!convx_ok(B, Ti, Fi, Ci, kt, kf, st, sf, dt, df, pt, pf, To, Fo, mode, ldcol) || !dxpad) return SBK_ERR_ARG;
+  const int Tp = (To - 1) * st + (kt - 1) * dt + 1, Fp = (Fo - 1) * sf + (kf - 1) * df + 1;
+  const ConvGeomX gm{kt, kf, st, sf, dt, df, pt, pf, mode};
+  col2padx_kernel<<<grid_for((long long)B * Tp * Fp * Ci, 256), 256, 0, (hipStream_t)stream>>>(
+      dcol, dcol_bf16, B, Tp, Fp, Ci, To, Fo, gm, ldcol, dxpad);
+  SBK_CHECK_LAUNCH();
+  foldx_kernel<<<grid_for((long long)B * Ti * Fi * Ci, 256), 256, 0, (hipStream_t)stream>>>(
+      dxpad, B, Tp, Fp, Ti, Fi, Ci, pt, pf, mode, dx, dx_bf16);
+  SBK_CHECK_LAUNCH();
+  return 0;
+}
+
 SBK_API int sbk_joint_fwd(const float* tn, const float* pn, int B, int T, int U1, int J, int act, float slope, void* z,
                           int z_bf16, void* stream) {
   if (B <= 0 || T <= 0 || U1 <= 0 || J <= 0) return SBK_ERR_ARG;
