@@ -466,7 +466,8 @@ int sbk_rowsum(const void* x, int x_bf16, long long rows, int cols, float* part,
 
 /* Activations and their backward: mode 1 Swish (activations.py:111-142),
  * 2 GLU over [a | gate] halves of 2*cols inputs (Conformer.py:73-79, nn.GLU(dim=1)),
- * 3 LeakyReLU(slope) (convolution.py:169-175).  dx has the shape of x. */
+ * 3 LeakyReLU(slope) (convolution.py:169-175), 4 GELU with the exact erf
+ * (torch.nn.GELU, Transformer.py's FFN).  dx has the shape of x. */
 int sbk_act_fwd(int mode, const void* x, int x_bf16, long long rows, int cols, void* y, int y_bf16, float slope,
                 void* stream);
 int sbk_act_bwd(int mode, const void* x, int x_bf16, const void* dy, int dy_bf16, long long rows, int cols, void* dx,

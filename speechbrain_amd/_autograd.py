@@ -27,7 +27,7 @@ from ._lib import check, lib, ptr, stream_of
 _f32 = torch.float32
 _bf16 = torch.bfloat16
 
-ACT_CODE = {"swish": 1, "glu": 2, "leaky_relu": 3}
+ACT_CODE = {"swish": 1, "glu": 2, "leaky_relu": 3, "gelu": 4}
 
 
 def _bf(t):

@@ -288,7 +288,13 @@ __global__ void __launch_bounds__(1024) colsum_kernel(const float* __restrict__ 
 
 // ------------------------------------------------------------- activations
 // mode 1 Swish y = x sigmoid(x); 2 GLU y = a sigmoid(b), x = [a | b] (2 cols);
-// 3 LeakyReLU(slope).  rows x cols outputs.
+// 3 LeakyReLU(slope); 4 GELU y = x Φ(x) with the exact erf (torch.nn.GELU,
+// the TransformerEncoder FFN's activation).  rows x cols outputs.
+__device__ __forceinline__ float gelu_f(float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)); }
+// d/dx x Φ(x) = Φ(x) + x φ(x)
+__device__ __forceinline__ float gelu_d(float v) {
+  return 0.5f * (1.0f + erff(v * 0.70710678118654752f)) + v * 0.39894228040143268f * expf(-0.5f * v * v);
+}
 __global__ void act_fwd_kernel(int mode, const void* __restrict__ x, int x_bf16, long long rows, int cols,
                                void* __restrict__ y, int y_bf16, float slope) {
   const long long n = rows * cols;
@@ -300,7 +306,7 @@ __global__ void act_fwd_kernel(int mode, const void* __restrict__ x, int x_bf16,
       r = a * (1.0f / (1.0f + expf(-b)));
     } else {
       const float v = ldv(x, i, x_bf16);
-      r = mode == 1 ? v * (1.0f / (1.0f + expf(-v))) : (v >= 0.f ? v : v * slope);
+      r = mode == 1 ? v * (1.0f / (1.0f + expf(-v))) : mode == 4 ? gelu_f(v) : (v >= 0.f ? v : v * slope);
     }
     stv(y, i, r, y_bf16);
   }
@@ -324,6 +330,8 @@ __global__ void act_bwd_kernel(int mode, const void* __restrict__ x, int x_bf16,
       const float v = ldv(x, i, x_bf16);
       const float s = 1.0f / (1.0f + expf(-v));
       stv(dx, i, g * (s + v * s * (1.0f - s)), dx_bf16);
+    } else if (mode == 4) {
+      stv(dx, i, g * gelu_d(ldv(x, i, x_bf16)), dx_bf16);
     } else {
       const float v = ldv(x, i, x_bf16);
       stv(dx, i, v > 0.f ? g : g * slope, dx_bf16);
@@ -1134,9 +1142,9 @@ SBK_API int sbk_colsum(const float* part, int rows, int cols, float* out, int ac
 
 SBK_API int sbk_act_fwd(int mode, const void* x, int x_bf16, long long rows, int cols, void* y, int y_bf16,
                         float slope, void* stream) {
-  if (mode < 1 || mode > 3 || rows < 0 || cols <= 0) return SBK_ERR_ARG;
+  if (mode < 1 || mode > 4 || rows < 0 || cols <= 0) return SBK_ERR_ARG;
   if (rows == 0) return 0;
-  if (vec4_ok(rows, cols, mode, {x, y})) {
+  if (mode != 4 && vec4_ok(rows, cols, mode, {x, y})) {
     const int g4 = grid_for(rows * cols / 4, 256);
     hipStream_t st = (hipStream_t)stream;
     if (mode == 1) act_fwd4_kernel<1><<<g4, 256, 0, st>>>(x, x_bf16, rows, cols, y, y_bf16, slope);
@@ -1153,9 +1161,9 @@ SBK_API int sbk_act_fwd(int mode, const void* x, int x_bf16, long long rows, int
 
 SBK_API int sbk_act_bwd(int mode, const void* x, int x_bf16, const void* dy, int dy_bf16, long long rows, int cols,
                         void* dx, int dx_bf16, float slope, void* stream) {
-  if (mode < 1 || mode > 3 || rows < 0 || cols <= 0) return SBK_ERR_ARG;
+  if (mode < 1 || mode > 4 || rows < 0 || cols <= 0) return SBK_ERR_ARG;
   if (rows == 0) return 0;
-  if (vec4_ok(rows, cols, mode, {x, dy, dx})) {
+  if (mode != 4 && vec4_ok(rows, cols, mode, {x, dy, dx})) {
     const int g4 = grid_for(rows * cols / 4, 256);
     hipStream_t st = (hipStream_t)stream;
     if (mode == 1) act_bwd4_kernel<1><<<g4, 256, 0, st>>>(x, x_bf16, dy, dy_bf16, rows, cols, dx, dx_bf16, slope);

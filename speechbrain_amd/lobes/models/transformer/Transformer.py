@@ -165,12 +165,35 @@ class TransformerEncoderLayer(nn.Module):
             x = _enc.layernorm(x, *self._ln(self.norm2), out1_dtype=_f32)[0]
         return x, (probs.mean(dim=1) if probs is not None else None)
 
+    def module_forward(self, src, src_mask=None, src_key_padding_mask=None, pos_embs=None):
+        """Transformer.py:343-376 step by step on the drop-in submodules — the
+        attention's differentiable path (masks, pos_embs, dropout,
+        gradients), the HIP LayerNorm / FFN autograd Functions — for
+        everything the fused inference step does not take."""
+        src1 = self.norm1(src) if self.normalize_before else src
+        if self.attention_type == "RelPosMHAXL":
+            output, self_attn = self.self_att(src1, src1, src1, pos_embs, key_padding_mask=src_key_padding_mask,
+                                              attn_mask=src_mask)
+        else:
+            output, self_attn = self.self_att(src1, src1, src1, attn_mask=src_mask,
+                                              key_padding_mask=src_key_padding_mask, pos_embs=pos_embs)
+        src = src + self.dropout1(output)
+        if not self.normalize_before:
+            src = self.norm1(src)
+        src1 = self.norm2(src) if self.normalize_before else src
+        output = src + self.dropout2(self.pos_ffn(src1))
+        if not self.normalize_before:
+            output = self.norm2(output)
+        return output, self_attn
+
+    def _fused_ok(self, src, src_mask, pos_embs):
+        return (src_mask is None and pos_embs is None and self.attention_type == "regularMHA"
+                and not A.needs_grad(self, src) and not (self.training and self.dropout1.p > 0))
+
     def forward(self, src, src_mask: Optional[torch.Tensor] = None,
                 src_key_padding_mask: Optional[torch.Tensor] = None, pos_embs: Optional[torch.Tensor] = None):
-        if src_mask is not None or pos_embs is not None:
-            raise NotImplementedError("src_mask / pos_embs are not on the HIP TransformerEncoderLayer path")
-        if A.needs_grad(self, src) or (self.training and self.dropout1.p > 0):
-            raise NotImplementedError("TransformerEncoderLayer has no training path yet (inference only)")
+        if not self._fused_ok(src, src_mask, pos_embs):
+            return self.module_forward(src, src_mask, src_key_padding_mask, pos_embs)
         B, T, d = src.shape
         kpm = src_key_padding_mask.to(torch.uint8).contiguous() if src_key_padding_mask is not None else None
         y, attn = self.run(src.float().reshape(B * T, d).contiguous(), B, T, kpm, _mode(), True)
@@ -204,10 +227,16 @@ class TransformerEncoder(nn.Module):
 
     def forward(self, src, src_mask: Optional[torch.Tensor] = None,
                 src_key_padding_mask: Optional[torch.Tensor] = None, pos_embs: Optional[torch.Tensor] = None):
-        if src_mask is not None or pos_embs is not None:
-            raise NotImplementedError("src_mask / pos_embs are not on the HIP TransformerEncoder path")
-        if A.needs_grad(self, src) or (self.training and any(l.dropout1.p > 0 for l in self.layers)):
-            raise NotImplementedError("TransformerEncoder has no training path yet (inference only)")
+        if not all(l._fused_ok(src, src_mask, pos_embs) for l in self.layers):
+            # Transformer.py:448-486 with the layers' module path
+            keep = self.rng.random(len(self.layers)) if self.layerdrop_prob > 0.0 else None
+            out, attns = src, []
+            for i, layer in enumerate(self.layers):
+                if not self.training or self.layerdrop_prob == 0.0 or keep[i] > self.layerdrop_prob:
+                    out, a = layer(out, src_mask=src_mask, src_key_padding_mask=src_key_padding_mask,
+                                   pos_embs=pos_embs)
+                    attns.append(a)
+            return self.norm(out), attns
         B, T, d = src.shape
         kpm = src_key_padding_mask.to(torch.uint8).contiguous() if src_key_padding_mask is not None else None
         y, attns = self.run(src.float().reshape(B * T, d).contiguous(), B, T, kpm, True)
@@ -221,21 +250,11 @@ class TransformerEncoder(nn.Module):
 # recipe's TransformerASR(num_decoder_layers > 0) constructs with the
 # reference's module tree and state_dict keys, loads its checkpoint with
 # strict=True, and runs forward()/decode() with the reference's semantics.
-# Its LayerNorms and FFNs are the HIP drop-ins (nnet.normalization.LayerNorm,
-# nnet.attention.PositionalwiseFeedForward); the masked self- and cross-
-# attention use the wrapped torch.nn.MultiheadAttention on the device (the
-# reference's own call, attention.py:752-769), since the HIP attention
-# kernels cover the encoder's self-attention only.
+# Its LayerNorms, FFNs and its masked self- and cross-attention are the HIP
+# drop-ins (nnet.normalization.LayerNorm, nnet.attention
+# .PositionalwiseFeedForward, the MultiheadAttention's general path on
+# csrc/xattn.hip: attn_mask, key padding, pos_embs, S != L).
 # ---------------------------------------------------------------------------
-def _ref_mha(mod, query, key, value, attn_mask=None, key_padding_mask=None, need_weights=True):
-    """sb.nnet.attention.MultiheadAttention.forward (attention.py:749-778)
-    on the wrapped nn.MultiheadAttention: (B, L, E) in and out."""
-    out = mod.att(query.permute(1, 0, 2), key.permute(1, 0, 2), value.permute(1, 0, 2), attn_mask=attn_mask,
-                  key_padding_mask=key_padding_mask, need_weights=need_weights)
-    if need_weights:
-        o, w = out
-        return o.permute(1, 0, 2), w
-    return out[0].permute(1, 0, 2), None
 
 
 class TransformerDecoderLayer(nn.Module):
@@ -262,17 +281,15 @@ class TransformerDecoderLayer(nn.Module):
 
     def forward(self, tgt, memory, tgt_mask=None, memory_mask=None, tgt_key_padding_mask=None,
                 memory_key_padding_mask=None, pos_embs_tgt=None, pos_embs_src=None):
-        if pos_embs_tgt is not None or pos_embs_src is not None:
-            raise NotImplementedError("regularMHA decoder: pos_embs are added by the caller (TransformerASR)")
         tgt1 = self.norm1(tgt) if self.normalize_before else tgt
-        tgt2, self_attn = _ref_mha(self.self_attn, tgt1, tgt1, tgt1, attn_mask=tgt_mask,
-                                   key_padding_mask=tgt_key_padding_mask)
+        tgt2, self_attn = self.self_attn(tgt1, tgt1, tgt1, attn_mask=tgt_mask, key_padding_mask=tgt_key_padding_mask,
+                                         pos_embs=pos_embs_tgt)
         tgt = tgt + self.dropout1(tgt2)
         if not self.normalize_before:
             tgt = self.norm1(tgt)
         tgt1 = self.norm2(tgt) if self.normalize_before else tgt
-        tgt2, multihead_attention = _ref_mha(self.mutihead_attn, tgt1, memory, memory, attn_mask=memory_mask,
-                                             key_padding_mask=memory_key_padding_mask)
+        tgt2, multihead_attention = self.mutihead_attn(tgt1, memory, memory, attn_mask=memory_mask,
+                                                       key_padding_mask=memory_key_padding_mask, pos_embs=pos_embs_src)
         tgt = tgt + self.dropout2(tgt2)
         if not self.normalize_before:
             tgt = self.norm2(tgt)

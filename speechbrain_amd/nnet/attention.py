@@ -293,7 +293,7 @@ class PositionalwiseFeedForward(nn.Module):
         act, slope = self.act_name()
         if act == "relu":
             act, slope = "leaky_relu", 0.0  # ReLU = LeakyReLU(0), same backward
-        if act not in ("swish", "leaky_relu"):
+        if act not in ("swish", "leaky_relu", "gelu"):
             raise NotImplementedError(f"activation {act} has no backward kernel yet")
         l1, l2 = self.ffn[0], self.ffn[3]
         h = A.linear(u2d, l1.weight, l1.bias, dtype, self._wc, "t1", out_dtype=dtype)
@@ -349,12 +349,18 @@ class PositionalwiseFeedForward(nn.Module):
 class MultiheadAttention(nn.Module):
     """attention.py:642-778: the wrapper of torch.nn.MultiheadAttention
     (state_dict keys att.in_proj_weight / att.in_proj_bias /
-    att.out_proj.{weight,bias}).  Self-attention (query is key is value,
-    the TransformerEncoderLayer case) runs as one in_proj GEMM (rows
-    permuted per head to [q_h | k_h | v_h]) → the fused attention kernel
-    (scores·1/√d_head, key padding mask, softmax, P·V; the positional band of
-    the rel-pos kernel is fed zeros) → out_proj GEMM.  Returns
-    (output (B, L, E), head-averaged weights (B, L, S)) like the reference."""
+    att.out_proj.{weight,bias}, or att.{q,k,v}_proj_weight with kdim / vdim).
+    Inference self-attention without attn_mask (query is key is value, the
+    TransformerEncoderLayer case) runs as one in_proj GEMM (rows permuted per
+    head to [q_h | k_h | v_h]) → the fused attention kernel (scores·1/√d_head,
+    key padding mask, softmax, P·V) → out_proj GEMM.  Everything else —
+    cross-attention (key / value ≠ query, S ≠ L), attn_mask (2-D or
+    (B·H, L, S), bool / byte / additive), pos_embs (added to attn_mask,
+    :756-761), a float key_padding_mask, training with attention dropout, or
+    gradients — runs the differentiable path: q / k / v projections on the
+    MFMA GEMM, the attention core of csrc/xattn.hip (its positional band and
+    biases zero), out_proj.  Returns (output (B, L, E), head-averaged
+    weights (B, L, S)) like the reference."""
 
     def __init__(self, nhead, d_model, dropout=0.0, bias=True, add_bias_kv=False, add_zero_attn=False, kdim=None,
                  vdim=None):
@@ -413,15 +419,87 @@ class MultiheadAttention(nn.Module):
         return _enc.relpos_attention(qkv, band, zb, zb, kpm_u8, B, T, H, dh, 1.0 / math.sqrt(dh),
                                      need_probs=need_weights)
 
+    def general_forward(self, query, key, value, attn_mask=None, key_padding_mask=None, pos_embs=None):
+        """The differentiable path (see the class docstring).  Returns
+        (out (B, L, E), weights (B, L, S) averaged over heads)."""
+        a = self.att
+        if a.bias_k is not None or a.add_zero_attn:
+            raise NotImplementedError("MultiheadAttention: add_bias_kv / add_zero_attn are not on the HIP path")
+        B, L, E = query.shape
+        S = key.shape[1]
+        if value.shape[:2] != key.shape[:2]:
+            raise ValueError(f"key {tuple(key.shape)} and value {tuple(value.shape)} lengths differ")
+        H = self.nhead
+        dh = E // H
+        dtype = _enc.compute_dtype()
+        if a._qkv_same_embed_dim:
+            wq, wk, wv = a.in_proj_weight.chunk(3, dim=0)
+        else:
+            wq, wk, wv = a.q_proj_weight, a.k_proj_weight, a.v_proj_weight
+        bq = bk = bv = None
+        if a.in_proj_bias is not None:
+            bq, bk, bv = a.in_proj_bias.chunk(3, dim=0)
+        q = A.linear(query.reshape(B * L, -1), wq, bq, dtype, self._wc, "g_q", out_dtype=dtype)
+        k = A.linear(key.reshape(B * S, -1), wk, bk, dtype, self._wc, "g_k", out_dtype=dtype)
+        v = A.linear(value.reshape(B * S, -1), wv, bv, dtype, self._wc, "g_v", out_dtype=dtype)
+        # attn_mask (+ pos_embs, the reference's in-place add without the
+        # mutation of the caller's tensor) and a float key padding mask as one
+        # additive fp32 mask; bool / byte masks: True (non-zero) = masked
+        if pos_embs is not None:
+            # attention.py:756-761, in place on the caller's mask as there (a
+            # mask shared by a stack of layers accumulates every layer's add;
+            # a bool / byte mask raises, as in the reference)
+            if attn_mask is not None:
+                attn_mask += pos_embs
+            else:
+                attn_mask = pos_embs
+        m = attn_mask
+        if m is not None and m.dim() == 3 and m.shape[-1] == 1:
+            m = m.reshape(m.shape[0], m.shape[1])  # (L, S, 1) pos_embs
+        if m is not None and m.dtype == torch.uint8:
+            m = m.bool()
+        kpm = None
+        if key_padding_mask is not None:
+            if key_padding_mask.dtype in (torch.bool, torch.uint8):
+                kpm = key_padding_mask.to(query.device, torch.uint8).contiguous()
+            else:  # additive (B, S): folded into a (B*H, L, S) mask
+                add = key_padding_mask.to(query.device, torch.float32).view(B, 1, 1, S).expand(B, H, L, S)
+                if m is None:
+                    m = add.reshape(B * H, L, S)
+                else:
+                    mf = (torch.zeros(m.shape, device=query.device).masked_fill(m.to(query.device), -float("inf"))
+                          if m.dtype == torch.bool else m.to(query.device, torch.float32))
+                    mf = mf.view(1, 1, L, S) if mf.dim() == 2 else mf.view(-1, H, L, S)
+                    m = (mf + add).reshape(B * H, L, S)
+        am = _enc.attn_mask_arg(m, B, L, H, query.device, Lk=S)
+        z = self._zero_core(S, E, H, dh, query.device, dtype)
+        p = a.dropout if self.training else 0.0
+        o, attn = A.RelPosCrossAttnFn.apply(q, k, v, z[0], z[1], z[1], kpm, am, B, L, S, H, dh, 1.0 / math.sqrt(dh),
+                                            False, float(p))
+        out = A.linear(o, a.out_proj.weight, a.out_proj.bias, dtype, self._wc, "g_out")
+        return out.view(B, L, E), attn.mean(dim=1)
+
+    def _zero_core(self, S, E, H, dh, dev, dtype):
+        """A zero (2S-1, E) positional band and zero (dh, H) biases: the
+        xattn core is then plain scaled dot-product attention."""
+        key = ("core", S, str(dev), dtype)
+        z = self._zeros.get(key)
+        if z is None:
+            z = (torch.zeros(2 * S - 1, E, device=dev, dtype=dtype), torch.zeros(dh, H, device=dev))
+            self._zeros = {key: z}
+        return z
+
     def forward(self, query, key, value, attn_mask=None, key_padding_mask=None, return_attn_weights=True,
                 pos_embs=None):
+        fast = (query is key and key is value and attn_mask is None and pos_embs is None
+                and (key_padding_mask is None or key_padding_mask.dtype in (torch.bool, torch.uint8))
+                and not A.needs_grad(self, query) and not (self.training and self.att.dropout > 0)
+                and self.att._qkv_same_embed_dim and self.att.bias_k is None and not self.att.add_zero_attn
+                and self.att.in_proj_bias is not None)
+        if not fast:
+            out, w = self.general_forward(query, key, value, attn_mask, key_padding_mask, pos_embs)
+            return (out, w) if return_attn_weights else out
         self._check()
-        if attn_mask is not None or pos_embs is not None:
-            raise NotImplementedError("attn_mask / pos_embs are not on the HIP attention path")
-        if not (query is key and key is value):
-            raise NotImplementedError("MultiheadAttention: the HIP path is self-attention (query is key is value)")
-        if A.needs_grad(self, query) or (self.training and self.att.dropout > 0):
-            raise NotImplementedError("MultiheadAttention has no training path yet (inference only)")
         B, T, E = query.shape
         mode = _enc.compute_dtype()
         x2d = _enc.to_compute(query.reshape(B * T, E), mode)
