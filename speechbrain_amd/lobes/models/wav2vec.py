@@ -140,10 +140,40 @@ class W2VLatentExtractor(nn.Module):
                         "mx" if out_dtype == "mx" else out_dtype)
         return x, T
 
+    def module_forward(self, x, normalize_signal=True):
+        """wav2vec.py:88-95 layer by layer, differentiable (training, conv
+        dropout, gradients): F.layer_norm of the waveform (HIP LayerNorm with
+        unit affine), then per block the valid strided Conv1d as a (k x 1)
+        Conv2d on sbk_im2col_x + the MFMA GEMM, LayerNorm over channels,
+        GELU and dropout (HIP kernels with backward), the closing LayerNorm."""
+        B, S = x.shape
+        dtype = _enc.compute_dtype()
+        x = x.float().contiguous()
+        if normalize_signal:
+            ones = torch.ones(S, device=x.device)
+            x = A.LayerNormFn.apply(x, ones, torch.zeros_like(ones), 1e-5, _f32)
+        h = x.view(B, S, 1, 1)  # (B, T, F = 1, C) for the 2-D im2col
+        T = S
+        for i in range(len(self.kernel_sizes)):
+            conv, ln = self._block(i)
+            drop = getattr(self.extractor, f"convblock_{i}").convs.dropout_0
+            k, s = self.kernel_sizes[i], self.strides[i]
+            To = (T - k) // s + 1
+            hin = h if h.dtype == dtype else A.to_dtype(h, dtype)
+            y = A.Conv2dXFn.apply(hin, conv.weight.unsqueeze(2), None, dtype, _f32,
+                                  (k, 1, s, 1, 1, 1, 0, 0, To, 1, 1))  # (B, To, 1, Cout)
+            C = y.shape[-1]
+            y = A.layer_norm(y.reshape(B * To, C), ln)
+            y = A.act(y, "gelu")
+            y = A.dropout(y, drop.p, self.training)
+            h, T = y.view(B, To, 1, C), To
+        return A.layer_norm(h.reshape(B * T, -1), self.norm).view(B, T, -1)
+
     def forward(self, x, normalize_signal=True):
         """(B, S) waveform → (B, T', C) latents (fp32)."""
-        if A.needs_grad(self, x):
-            raise NotImplementedError("W2VLatentExtractor has no training path yet (inference only)")
+        if A.needs_grad(self, x) or (self.training and any(isinstance(m, nn.Dropout) and m.p > 0
+                                                           for m in self.modules())):
+            return self.module_forward(x, normalize_signal)
         B = x.shape[0]
         y, T = self.run(x, normalize_signal, _f32)
         return y.view(B, T, -1)
@@ -209,11 +239,37 @@ class EncoderWrapper(nn.Module):
         y, _ = self.latent_encoder.run(h, B, T, kpm, need_weights)
         return y
 
-    def forward(self, latents, wav_lens=None, padding_mask=None, mask=None):
+    def module_forward(self, latents, wav_lens=None, padding_mask=None, mask=None):
+        """wav2vec.py:199-227 step by step (training, gradients, masked
+        pre-training): projector on the MFMA GEMM, HIP dropout, mask_emb on
+        the masked frames, the positional table, the latent encoder's module
+        path with the key padding of round(wav_lens·T)."""
+        results = {}
+        B, T, C = latents.shape
+        dtype = _enc.compute_dtype()
+        lin = self.input_projector
+        h = A.linear(latents.reshape(B * T, C), lin.weight, lin.bias, dtype, self._wc, "t_proj")
+        h = A.dropout(h, self.dropout_encoder_input.p, self.training).view(B, T, -1)
         if mask is not None:
-            raise NotImplementedError("EncoderWrapper: masked pre-training (mask=...) is not on the HIP path")
-        if A.needs_grad(self, latents):
-            raise NotImplementedError("EncoderWrapper has no training path yet (inference only)")
+            h = h.clone()
+            h[mask] = self.mask_emb.to(h.dtype)
+            num_masked = mask.sum()
+            results["num_masked"] = num_masked
+            results["ratio_masked"] = num_masked / mask.numel()
+        if wav_lens is not None:
+            n = torch.round(wav_lens.to(h.device).float() * T)
+            padding_mask = torch.arange(T, device=h.device)[None, :] >= n[:, None]
+        h = h + self.positional_encoding(h)
+        feats, _ = self.latent_encoder(h, src_key_padding_mask=padding_mask)
+        results["embeddings"] = feats
+        return results
+
+    def forward(self, latents, wav_lens=None, padding_mask=None, mask=None):
+        if (mask is not None or A.needs_grad(self, latents)
+                or (self.training and (self.dropout_encoder_input.p > 0
+                                       or any(isinstance(m, nn.Dropout) and m.p > 0
+                                              for m in self.latent_encoder.modules())))):
+            return self.module_forward(latents, wav_lens, padding_mask, mask)
         B, T, C = latents.shape
         y = self.embed(latents.float().reshape(B * T, C).contiguous(), B, T, wav_lens, padding_mask)
         return {"embeddings": y.view(B, T, -1)}
