@@ -88,6 +88,25 @@ __device__ __forceinline__ float gelu_fast(float x) {
   return x * (x >= 0.f ? 1.0f - h : h);
 }
 
+// the same on a pair (v_pk_fma / v_pk_mul for everything but the two
+// transcendentals): the FFN1 epilogue's GELU ran on scalar VALU at a cost of
+// ~29 us of config 5's 217-us MXFP8 up-projection
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v gelu_fast2(f2v x) {
+  const f2v z = __builtin_elementwise_abs(x) * 0.70710678118654752f;
+  const f2v d = z * 0.3275911f + 1.0f;
+  const f2v t = f2v{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+  f2v y = t * 1.061405429f - 1.453152027f;
+  y = y * t + 1.421413741f;
+  y = y * t - 0.284496736f;
+  y = y * t + 0.254829592f;
+  y = y * t;
+  const f2v q = (z * z) * -1.4426950408889634f;
+  const f2v h = (0.5f * y) * f2v{__builtin_amdgcn_exp2f(q[0]), __builtin_amdgcn_exp2f(q[1])};
+  const f2v one_h = 1.0f - h;
+  return x * f2v{x[0] >= 0.f ? one_h[0] : h[0], x[1] >= 0.f ? one_h[1] : h[1]};
+}
+
 template <int ACT>
 __device__ __forceinline__ float act_f(float x, float slope) {
   if (ACT == G_SWISH) return x * (1.0f / (1.0f + __expf(-x)));
@@ -378,8 +397,14 @@ __global__ void __launch_bounds__(NT, 1) gemm256_kernel(G256 p) {
         const int row = m0 + wm * 128 + hm * 64 + rl;
         const float4 a = *reinterpret_cast<const float4*>(cs + rl * CS_STRIDE + ocol);
         const float sc = scv[q];
-        float v0 = act_f<ACT>(a.x + bv.x, p.ep.slope) * sc, v1 = act_f<ACT>(a.y + bv.y, p.ep.slope) * sc;
-        float v2 = act_f<ACT>(a.z + bv.z, p.ep.slope) * sc, v3 = act_f<ACT>(a.w + bv.w, p.ep.slope) * sc;
+        float v0, v1, v2, v3;
+        if constexpr (ACT == G_GELU) {
+          const f2v g0 = gelu_fast2(f2v{a.x + bv.x, a.y + bv.y}) * sc, g1 = gelu_fast2(f2v{a.z + bv.z, a.w + bv.w}) * sc;
+          v0 = g0[0]; v1 = g0[1]; v2 = g1[0]; v3 = g1[1];
+        } else {
+          v0 = act_f<ACT>(a.x + bv.x, p.ep.slope) * sc; v1 = act_f<ACT>(a.y + bv.y, p.ep.slope) * sc;
+          v2 = act_f<ACT>(a.z + bv.z, p.ep.slope) * sc; v3 = act_f<ACT>(a.w + bv.w, p.ep.slope) * sc;
+        }
         if (p.ep.res) {  // (no +0 when there is none: a -0 stays -0, as in the other kernels)
           v0 += rv[q].x;
           v1 += rv[q].y;
