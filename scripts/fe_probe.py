@@ -24,11 +24,11 @@ if os.environ.get("SBK_PROBE_TL"):
     import ctypes
     import numpy as np
     torch.cuda.synchronize()
-    buf = (ctypes.c_ulonglong * 160)()
+    buf = (ctypes.c_ulonglong * (12 * 16))()
     assert ctypes.CDLL(_L.LIB_PATH).sbk_probe_fe_tl(buf) == 0
-    tl = np.array(buf, dtype=np.int64).reshape(10, 16)
-    t0 = tl[:, 0].min()
-    for w in range(10):
+    tl = np.array(buf, dtype=np.int64).reshape(12, 16)
+    for w in range(12):
         r = tl[w]
-        last = r[3] if r[3] else r[2]
-        print(f"w{w}: stage {r[1]-r[0]} block1 rows {r[2]-r[1]} {r[3]-r[2] if r[3] else 0} final-bar {r[11]-last} mfma {r[12]-r[11]} epi {r[13]-r[12]} total {r[13]-r[0]}")
+        print(f"w{w}: stage {r[1]-r[0]} block1 mfma+stats {r[2]-r[1]} block1 writes {r[3]-r[2]} "
+              f"w2-stage {r[11]-r[3]} mfma {r[12]-r[11]} epi {r[13]-r[12] if r[13] else 0} "
+              f"total {(r[13] if r[13] else r[12])-r[0]}")

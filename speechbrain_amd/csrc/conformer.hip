@@ -456,12 +456,12 @@ __global__ void __launch_bounds__(256) conv_block_mfma_kernel(const T* __restric
 // (Tried: two rows per pass over all 10 waves with cross-wave LN reductions
 // and VALU FMAs: 188 us; one row per wave on VALU FMAs: 130 us.)
 // s_memtime marks of the waves of workgroup 700 (probe builds only)
-SBK_PROBE_BUFFER(g_fe_tl, 10, 16)
 #define FE_TL(i) SBK_PROBE(if (blockIdx.x == 700 && lane == 0) g_fe_tl[w][i] = __builtin_amdgcn_s_memtime();)
 
-// 10 waves x 8 output rows (17 block-1 rows: passes of 10 and 7 rows).
+// 12 waves x 8 output rows (17 block-1 rows over 4 row groups x 3 frequency tiles).
 // (8 waves x 7 rows with the block-1 LN affine held in VGPRs: 133 us.)
-constexpr int FE_NT = 640, FE_TT2 = 8;
+constexpr int FE_NT = 768, FE_TT2 = 8;
+SBK_PROBE_BUFFER(g_fe_tl, FE_NT / 64, 16)
 
 // f(std::integral_constant<int, I>) for I = 0 .. N-1: register arrays indexed
 // inside get compile-time indices.  (The staged weights / affine used to sit
@@ -621,78 +621,101 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
   f32x4 bias4[4];
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) bias4[mt] = *reinterpret_cast<const f32x4*>(b1s + 16 * mt + 4 * g4);
-  // this lane's B-fragment taps k = 4 g4 + e of output frequency 16 nt + fr,
-  // as row-relative LDS offsets (k >= 9 and frequencies >= F1 read a valid
-  // element: the matching A entries are zero / the column is masked below)
-  int goff[3][4];
+  // Block 1, work split (round 5): wave w takes frequency tile nt = w % 3 of
+  // the rows j = w / 3 + 4 i (12 waves: 4 row groups x 3 tiles), all four
+  // channel tiles, which share each gathered B fragment.  The LN affine of
+  // the wave's 16 frequencies x 64 channels comes from LDS once, into VGPRs
+  // (one row per wave re-read it per row: 24 of the 33 KB of LDS traffic per
+  // wave and row, the block's bound at ~6.5-12k cycles a row); the rows'
+  // accumulators stay in VGPRs while the row statistics combine over the
+  // three tile waves through LDS — two workgroup barriers for the 17 rows.
+  static_assert(NW == 12, "block 1: 4 row groups x 3 frequency tiles");
+  constexpr int RG = 4, RPW = (NJ + RG - 1) / RG;  // rows per wave (5)
+  __shared__ float lnred[2][NJ][4];                 // [pass][row][tile] partial sums
+  const int nt = w % 3, grp = w / 3;
+  const int f1 = 16 * nt + fr;
+  const int f1c = min(f1, F1 - 1);
+  const float colm = f1 < F1 ? 1.f : 0.f;
+  // this lane's B-fragment taps k = 4 g4 + e of output frequency f1, as
+  // row-relative LDS offsets (k >= 9 and frequencies >= F1 read a valid
+  // element: the matching A entries are zero / the column is masked)
+  int goff[4];
 #pragma unroll
-  for (int nt = 0; nt < 3; ++nt) {
-    const int f1c = min(16 * nt + fr, F1 - 1);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int k = min(4 * g4 + e, 8);
-      goff[nt][e] = (k % 3) * Fin + reflect_idx(2 * f1c + k / 3 - 1, Fin);
-    }
+  for (int e = 0; e < 4; ++e) {
+    const int k = min(4 * g4 + e, 8);
+    goff[e] = (k % 3) * Fin + reflect_idx(2 * f1c + k / 3 - 1, Fin);
   }
-  float colm[3];  // 1 for output frequencies < F1
+  f32x4 gam[4], bet[4];
 #pragma unroll
-  for (int nt = 0; nt < 3; ++nt) colm[nt] = 16 * nt + fr < F1 ? 1.f : 0.f;
+  for (int mt = 0; mt < 4; ++mt) {
+    gam[mt] = *reinterpret_cast<const f32x4*>(g1s + f1c * C1 + 16 * mt + 4 * g4);
+    bet[mt] = *reinterpret_cast<const f32x4*>(be1s + f1c * C1 + 16 * mt + 4 * g4);
+  }
   const float inv_n1 = 1.0f / (float)(F1 * C1);
   FE_TL(1);
-  for (int j = w; j < NJ; j += NW) {
+  f32x4 acc[RPW][4];
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int j = min(grp + RG * i, NJ - 1);  // (a group's missing row recomputes the last: discarded)
     const float* r = xs + (j * 3) * Fin;
-    f32x4 acc[4][3];
+    const s16x4 xb4 =
+        __builtin_bit_cast(s16x4, uint2{pack2(f32x2{r[goff[0]], r[goff[1]]}), pack2(f32x2{r[goff[2]], r[goff[3]]})});
 #pragma unroll
-    for (int nt = 0; nt < 3; ++nt) {
-      const s16x4 xb4 = __builtin_bit_cast(
-          s16x4, uint2{pack2(f32x2{r[goff[nt][0]], r[goff[nt][1]]}), pack2(f32x2{r[goff[nt][2]], r[goff[nt][3]]})});
+    for (int mt = 0; mt < 4; ++mt) acc[i][mt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wa[mt], xb4, bias4[mt], 0, 0, 0);
+  }
+  // LayerNorm over each row's F1 x C1 values, two-pass: the tile partials of
+  // every row, then the squared deviations
+  float mean[RPW], rstd[RPW];
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wa[mt], xb4, bias4[mt], 0, 0, 0);
-    }
-    // LayerNorm over the row's F1 x C1 values (two-pass, packed pairs)
-    f32x2 s2 = {0.f, 0.f};
+  for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
-    for (int nt = 0; nt < 3; ++nt) {
+    for (int i = 0; i < RPW; ++i) {
+      const int j = grp + RG * i;
       f32x2 sn = {0.f, 0.f};
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) sn += f32x2{acc[mt][nt][0], acc[mt][nt][1]} + f32x2{acc[mt][nt][2], acc[mt][nt][3]};
-      s2 += sn * colm[nt];
-    }
-    const float mean = wave_sum_v(s2.x + s2.y) * inv_n1;
-    const f32x2 mv = {mean, mean};
-    f32x2 q2 = {0.f, 0.f};
-#pragma unroll
-    for (int nt = 0; nt < 3; ++nt) {
-      f32x2 qn = {0.f, 0.f};
-#pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
-        const f32x2 d0 = f32x2{acc[mt][nt][0], acc[mt][nt][1]} - mv, d1 = f32x2{acc[mt][nt][2], acc[mt][nt][3]} - mv;
-        qn += d0 * d0;
-        qn += d1 * d1;
+        f32x2 a0 = f32x2{acc[i][mt][0], acc[i][mt][1]}, a1 = f32x2{acc[i][mt][2], acc[i][mt][3]};
+        if (pass) {
+          a0 -= f32x2{mean[i], mean[i]};
+          a1 -= f32x2{mean[i], mean[i]};
+          sn += a0 * a0 + a1 * a1;
+        } else {
+          sn += a0 + a1;
+        }
       }
-      q2 += qn * colm[nt];
+      const float t = wave_sum_v((sn.x + sn.y) * colm);
+      if (j < NJ && lane == 0) lnred[pass][j][nt] = t;
     }
-    const float rstd = 1.0f / sqrtf(wave_sum_v(q2.x + q2.y) * inv_n1 + eps1);
-    const f32x2 rv = {rstd, rstd};
+    __syncthreads();
 #pragma unroll
-    for (int nt = 0; nt < 3; ++nt) {
-      const int f1 = 16 * nt + fr;
-      if (f1 >= F1) continue;
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const int c = 16 * mt + 4 * g4;
-        const f32x4 ga = *reinterpret_cast<const f32x4*>(g1s + f1 * C1 + c);
-        const f32x4 ba = *reinterpret_cast<const f32x4*>(be1s + f1 * C1 + c);
-        f32x2 y0 = (f32x2{acc[mt][nt][0], acc[mt][nt][1]} - mv) * rv * f32x2{ga[0], ga[1]} + f32x2{ba[0], ba[1]};
-        f32x2 y1 = (f32x2{acc[mt][nt][2], acc[mt][nt][3]} - mv) * rv * f32x2{ga[2], ga[3]} + f32x2{ba[2], ba[3]};
-        y0 = lrelu2<LMAX>(y0, slope1);
-        y1 = lrelu2<LMAX>(y1, slope1);
-        *reinterpret_cast<uint2*>(b1r + (j * F1 + f1) * C1P + c) = uint2{pack2(y0), pack2(y1)};
-      }
+    for (int i = 0; i < RPW; ++i) {
+      const int j = min(grp + RG * i, NJ - 1);
+      const float t = (lnred[pass][j][0] + lnred[pass][j][1]) + lnred[pass][j][2];
+      if (pass)
+        rstd[i] = 1.0f / sqrtf(t * inv_n1 + eps1);
+      else
+        mean[i] = t * inv_n1;
     }
-    FE_TL(2 + j / NW);
   }
+  FE_TL(2);
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int j = grp + RG * i;
+    if (j >= NJ || f1 >= F1) continue;
+    const f32x2 mv = {mean[i], mean[i]}, rv = {rstd[i], rstd[i]};
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int c = 16 * mt + 4 * g4;
+      f32x2 y0 = (f32x2{acc[i][mt][0], acc[i][mt][1]} - mv) * rv * f32x2{gam[mt][0], gam[mt][1]} +
+                 f32x2{bet[mt][0], bet[mt][1]};
+      f32x2 y1 = (f32x2{acc[i][mt][2], acc[i][mt][3]} - mv) * rv * f32x2{gam[mt][2], gam[mt][3]} +
+                 f32x2{bet[mt][2], bet[mt][3]};
+      y0 = lrelu2<LMAX>(y0, slope1);
+      y1 = lrelu2<LMAX>(y1, slope1);
+      *reinterpret_cast<uint2*>(b1r + (j * F1 + f1) * C1P + c) = uint2{pack2(y0), pack2(y1)};
+    }
+  }
+  FE_TL(3);
   // block-2 weights (L2-resident: every workgroup reads the same 37 KB) into
   // region 0 once every wave is done with the block-1 affine (loading them
   // with the stage instead delays the stage's LDS stores more than it saves)
@@ -710,13 +733,15 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
 
   // block 2 as one implicit GEMM over the workgroup's output positions:
   // rows m = t2_local * F2 + f2 (8 x 20 = 160 = 10 tiles of 16 at config 3, no
-  // padded rows), columns the C2 channels, K = (kt, kf, ci).  Wave w < NMW
-  // owns m-tiles 2w, 2w + 1 against both channel tiles, so each K step issues
-  // 4 MFMAs behind 4 fragment reads, and the LDS operand traffic (the bound of
-  // this phase) is 5 waves' worth instead of one padded row per wave.
+  // padded rows), columns the C2 channels, K = (kt, kf, ci).  Wave w < nmw
+  // owns m-tiles TMW w .. TMW w + TMW - 1 against both channel tiles, so each
+  // K step issues 2 TMW MFMAs behind TMW + 2 fragment reads.  (One m-tile per
+  // wave — ten multiplying waves instead of five — measured equal, 74.4 vs
+  // 74.6 us: the phase is LDS-read bound, profiles/r05t_fe_tl.log.)
   const int nrow = min(TT2, T2 - t20);  // valid output rows of this workgroup
   const int Mv = nrow * F2, ntl = C2 / 16;
-  const int nmw = (Mv + 31) / 32;       // waves with MFMA work (<= NW: host-checked F2 <= 32, TT2 = 8)
+  constexpr int TMW = 2;                // m-tiles per wave
+  const int nmw = (Mv + 16 * TMW - 1) / (16 * TMW);  // waves with MFMA work (<= NW: F1 <= 40, F2 <= 20, TT2 = 8)
   const int fk = 8 * (lane >> 4);
   // the epilogue's LN affine and bias, loaded ahead of the MFMA loop (their
   // latency hides behind it)
@@ -737,11 +762,11 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
     }
   }
   if (w < nmw) {
-    int aoff[2][3];  // A-row (m = 32 w + 16 tm + fr) offsets into b1r per kf, kt = 0
-    bool arow[2];
+    int aoff[TMW][3];  // A-row (m = 16 TMW w + 16 tm + fr) offsets into b1r per kf, kt = 0
+    bool arow[TMW];
 #pragma unroll
-    for (int tm = 0; tm < 2; ++tm) {
-      const int m = 32 * w + 16 * tm + fr;
+    for (int tm = 0; tm < TMW; ++tm) {
+      const int m = 16 * TMW * w + 16 * tm + fr;
       arow[tm] = m < Mv;
       const int mc = arow[tm] ? m : 0;
       const int tl = mc / F2, fo = mc - tl * F2;
@@ -751,9 +776,9 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
     float cb[2];
 #pragma unroll
     for (int tn = 0; tn < 2; ++tn) cb[tn] = b2 && tn < ntl ? b2[tn * 16 + fr] : 0.f;
-    f32x4 acc[2][2];
+    f32x4 acc[TMW][2];
 #pragma unroll
-    for (int tm = 0; tm < 2; ++tm)
+    for (int tm = 0; tm < TMW; ++tm)
 #pragma unroll
       for (int tn = 0; tn < 2; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
     // unconditional fragment reads (rows past Mv / channel tiles past C2 read
@@ -768,28 +793,28 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
 #pragma unroll
         for (int c0 = 0; c0 < C1; c0 += 32) {
           const int k = (kt * 3 + kf) * C1 + c0;
-          typename Tr::frag fa[2], fbw[2];
+          typename Tr::frag fa[TMW], fbw[2];
 #pragma unroll
-          for (int tm = 0; tm < 2; ++tm) fa[tm] = Tr::load(brow + aoff[tm][kf] + c0);
+          for (int tm = 0; tm < TMW; ++tm) fa[tm] = Tr::load(brow + aoff[tm][kf] + c0);
 #pragma unroll
           for (int tn = 0; tn < 2; ++tn) fbw[tn] = Tr::load(wrow[tn] + k);
 #pragma unroll
-          for (int tm = 0; tm < 2; ++tm)
+          for (int tm = 0; tm < TMW; ++tm)
 #pragma unroll
             for (int tn = 0; tn < 2; ++tn) Tr::mma(acc[tm][tn], fa[tm], fbw[tn]);
         }
     }
-    // D rows m = 32 w + 16 tm + 4 (lane >> 4) + r -> yv[m][co] (rows of one
-    // output time step are contiguous: yv[t2_local][f2][co])
+    // D rows m = 16 TMW w + 16 tm + 4 (lane >> 4) + r -> yv[m][co] (rows of
+    // one output time step are contiguous: yv[t2_local][f2][co])
 #pragma unroll
-    for (int tm = 0; tm < 2; ++tm)
+    for (int tm = 0; tm < TMW; ++tm)
 #pragma unroll
       for (int tn = 0; tn < 2; ++tn) {
         if (tn >= ntl) continue;
         const int co = tn * 16 + fr;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int m = 32 * w + 16 * tm + 4 * (lane >> 4) + r;
+          const int m = 16 * TMW * w + 16 * tm + 4 * (lane >> 4) + r;
           if (m < Mv) yv[m * C2 + co] = acc[tm][tn][r] + cb[tn];
         }
       }
