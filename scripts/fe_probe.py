@@ -29,6 +29,7 @@ if os.environ.get("SBK_PROBE_TL"):
     tl = np.array(buf, dtype=np.int64).reshape(12, 16)
     for w in range(12):
         r = tl[w]
-        print(f"w{w}: stage {r[1]-r[0]} block1 mfma+stats {r[2]-r[1]} block1 writes {r[3]-r[2]} "
-              f"w2-stage {r[11]-r[3]} mfma {r[12]-r[11]} epi {r[13]-r[12] if r[13] else 0} "
-              f"total {(r[13] if r[13] else r[12])-r[0]}")
+        # persistent kernel (marks of workgroup 100's last tile): 0 tile top, 1 after the xs barrier,
+        # 2 block-1 MFMA + LN statistics, 3 block-1 writes, 12 block 2 (+ next-tile fetch issue), 13 epilogue
+        print(f"w{w}: xs-stage {r[1]-r[0]} block1 mfma+stats {r[2]-r[1]} block1 writes {r[3]-r[2]} "
+              f"block2 {r[12]-r[3]} epi {r[13]-r[12]} total {r[13]-r[0]}; kernel (all tiles) {r[15]-r[14]}")

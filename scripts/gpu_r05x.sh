@@ -1,0 +1,6 @@
+# frontend2 persistent (no K split, folded LN apply): timing, probe timeline, SQ counters
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && \
+timeout -k 10 120 python scripts/fe_probe.py > gpurun_out/r05x_fe.log 2>&1 && \
+SBK_PROBE_TL=1 SBK_PROBE_LIB=gpurun_probe_FETL.so timeout -k 10 120 python scripts/fe_probe.py > gpurun_out/r05x_fe_tl.log 2>&1 && \
+bash scripts/fe_pmc.sh
+rc=$?; cat gpurun_out/r05x_fe.log gpurun_out/r05x_fe_tl.log | grep -v amdgpu.ids; exit $rc

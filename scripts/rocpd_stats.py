@@ -1,27 +1,15 @@
-"""Per-kernel summary of a rocprofv3 run (its SQLite output, the default
-format) in the layout of rocprofv3's own kernel_stats.csv:
-
-    python scripts/rocpd_stats.py gpurun_out/<dir>/run_results.db > profiles/<name>_kernel_stats.csv
-"""
-import csv
+"""Per-kernel stats (calls, average / total duration, share) from a rocprofv3
+sqlite result (rocpd `kernels` view), printed as CSV like --stats' kernel_stats.
+usage: python scripts/rocpd_stats.py <results.db> [name-filter]"""
 import sqlite3
-import statistics
 import sys
 
-
-def main(path):
-    con = sqlite3.connect(path)
-    per = {}
-    for name, dur in con.execute("select name, duration from kernels"):
-        per.setdefault(name, []).append(int(dur))
-    total = sum(sum(v) for v in per.values()) or 1
-    w = csv.writer(sys.stdout, quoting=csv.QUOTE_NONNUMERIC, lineterminator="\n")
-    w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs", "StdDev"])
-    for name, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
-        s = sum(v)
-        w.writerow([name, len(v), s, round(s / len(v), 6), round(100.0 * s / total, 2), min(v), max(v),
-                    round(statistics.pstdev(v), 6) if len(v) > 1 else 0.0])
-
-
-if __name__ == "__main__":
-    main(sys.argv[1])
+c = sqlite3.connect(sys.argv[1])
+rows = c.execute("select name, count(*), avg(duration), sum(duration), min(duration), max(duration) "
+                 "from kernels group by name order by sum(duration) desc").fetchall()
+tot = sum(r[3] for r in rows)
+flt = sys.argv[2] if len(sys.argv) > 2 else ""
+print('"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs"')
+for n, k, a, s, lo, hi in rows:
+    if flt in n:
+        print(f'"{n}",{k},{s},{a:.1f},{100.0 * s / tot:.3f},{lo},{hi}')

@@ -444,21 +444,25 @@ __global__ void __launch_bounds__(256) conv_block_mfma_kernel(const T* __restric
 // Both ConvBlocks of the ConvolutionFrontEnd in one kernel (convolution.py
 // :12-84,169-175): conv3x3/s2 reflect (Cin=1) -> LN(F1*C1) -> LeakyReLU ->
 // conv3x3/s2 reflect (C1 -> C2, MFMA implicit GEMM) -> LN(F2*C2) -> LeakyReLU.
-// A 640-thread workgroup owns TT2 = 8 output time rows of one utterance: it
-// computes the 2*TT2+1 block-1 rows they read (reflect-padded) straight into
-// LDS (the (B, T1, F1, C1) intermediate never reaches HBM), stages the block-2
-// weights in LDS once, then waves 0..7 convolve output row t2_0 + w and
-// normalise it on their own.
+// A tile is TT2 = 8 output time rows of one utterance: the 2*TT2+1 block-1
+// rows they read (reflect-padded) are computed straight into LDS (the
+// (B, T1, F1, C1) intermediate never reaches HBM), then block 2 runs as an
+// implicit GEMM on MFMA and waves 0..7 normalise one output row each.
+// Persistent (round 5): one 768-thread workgroup per CU walks a contiguous
+// run of tiles with the block-2 weights resident in LDS; a tile continuing
+// the previous one reuses its last block-1 row as row 0 (16 rows computed,
+// not 17), and the next tile's input rows are fetched during the epilogue.
 //   x (B, Tin, Fin) fp32; w1 (C1, 3, 3) fp32 in conv_block_c1's tap order;
 //   wp2 (C2, 3 time, 3 freq, C1) T; out (B, T2, F2*C2).
-// Block 1, one row per wave, on MFMA (the 9 taps padded to one bf16 K step),
-// LN statistics as wave reductions (no workgroup barrier per row).
 // (Tried: two rows per pass over all 10 waves with cross-wave LN reductions
-// and VALU FMAs: 188 us; one row per wave on VALU FMAs: 130 us.)
-// s_memtime marks of the waves of workgroup 700 (probe builds only)
-#define FE_TL(i) SBK_PROBE(if (blockIdx.x == 700 && lane == 0) g_fe_tl[w][i] = __builtin_amdgcn_s_memtime();)
+// and VALU FMAs: 188 us; one row per wave on VALU FMAs: 130 us; one
+// workgroup per tile with per-tile weight staging: 74.6 us; block 2 with its
+// K loop split over wave pairs: +1k cycles per tile; a chunk-pair swizzle of
+// the block-1 rows: more LDS bank conflicts, not fewer.)
+// s_memtime marks of the waves of workgroup 100, its last tile (probe builds only)
+#define FE_TL(i) SBK_PROBE(if (blockIdx.x == 100 && lane == 0) g_fe_tl[w][i] = __builtin_amdgcn_s_memtime();)
 
-// 12 waves x 8 output rows (17 block-1 rows over 4 row groups x 3 frequency tiles).
+// 12 waves x 8 output rows (16-17 block-1 rows over 4 row groups x 3 frequency tiles).
 // (8 waves x 7 rows with the block-1 LN affine held in VGPRs: 133 us.)
 constexpr int FE_NT = 768, FE_TT2 = 8;
 SBK_PROBE_BUFFER(g_fe_tl, FE_NT / 64, 16)
@@ -487,8 +491,8 @@ lrelu2(float __attribute__((ext_vector_type(2))) t, float s) {
 }
 
 template <typename T, int C1, bool LMAX>
-__global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restrict__ x, int Tin, int Fin, int T1, int F1,
-                                                        int T2, int F2, const float* __restrict__ w1,
+__global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restrict__ x, int ntile, int Tin, int Fin,
+                                                        int T1, int F1, int T2, int F2, const float* __restrict__ w1,
                                                         const float* __restrict__ b1, const float* __restrict__ g1,
                                                         const float* __restrict__ be1, float eps1, float slope1,
                                                         const T* __restrict__ wp2, int C2,
@@ -505,101 +509,80 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
   // then spread over the banks instead of hitting one 16-B slot column
   constexpr int C1P = C1 + 8;
   const int K = 9 * C1, KP = K + 8;
-  // region 0: the block-1 LN affine (F1 x C1 gamma, beta; fp32) during block
-  // 1, then the block-2 weights (staged after block 1)
+  // region 0: the block-2 weights, staged once and resident for all of the
+  // workgroup's tiles
   T* wl = reinterpret_cast<T*>(smem);                                   // C2 x KP block-2 weights
-  float* g1s = reinterpret_cast<float*>(smem);                          // F1 x C1
-  float* be1s = g1s + F1 * C1;                                          // F1 x C1
-  const int r0 = (max(C2 * KP * (int)sizeof(T), 2 * F1 * C1 * 4) + 15) & ~15;
+  const int r0 = (C2 * KP * (int)sizeof(T) + 15) & ~15;
   float* yv = reinterpret_cast<float*>(smem + r0);                      // TT2 x F2*C2 (block 2)
   float* xs = yv;                                                       // NJ x 3 x Fin (block 1, same space)
   const int xsz = max(TT2 * F2 * C2, (NJ * 3 * Fin + 3) & ~3);
   T* b1r = reinterpret_cast<T*>(yv + xsz);                              // NJ x F1 x C1P
-  float* w1s = reinterpret_cast<float*>(b1r + NJ * F1 * C1P);           // C1 x 9 block-1 taps
-  float* b1s = w1s + C1 * 9;                                            // C1
+  uint2* wal = reinterpret_cast<uint2*>(b1r + NJ * F1 * C1P);           // 4 x 64 block-1 A fragments (bf16 taps)
+  float* b1s = reinterpret_cast<float*>(wal + 4 * 64);                  // C1 block-1 bias
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nblk = (T2 + TT2 - 1) / TT2;
-  const int b = blockIdx.x / nblk, t20 = (blockIdx.x - b * nblk) * TT2;
-  const float* xb = x + (long long)b * Tin * Fin;
-  FE_TL(0);
+  // contiguous tile runs: a tile that continues the previous one (same
+  // utterance) takes its block-1 row 0 from the previous tile's row 16
+  const int tbeg = (int)(((long long)blockIdx.x * ntile) / gridDim.x);
+  const int tend = (int)(((long long)(blockIdx.x + 1) * ntile) / gridDim.x);
+  int tile = tbeg;
+  FE_TL(14);
 
-  // stage the input rows, the block-2 weights and the block-1 taps / bias,
-  // every load issued before the first LDS store (one latency instead of one
-  // per loop trip): block-1 row j is t1 = reflect(2*t20 - 1 + j) and reads x
-  // rows reflect(2*t1 - 1 + kt)
+  // Persistent workgroups (round 5): one per CU, each walks the tiles
+  // blockIdx.x, + gridDim.x, ...  The per-tile constants — block-2 weights
+  // (37 KB, LDS), block-1 taps / bias / LN affine (VGPRs) — load once per
+  // workgroup instead of once per tile (57 KB of L2 reads and a staging
+  // barrier pair per tile before), and the next tile's input rows and
+  // top_db partial maxima are fetched into registers during this tile's
+  // block 2 and epilogue.  Block-1 row j is t1 = reflect(2*t20 - 1 + j) and
+  // reads x rows reflect(2*t1 - 1 + kt).
   constexpr int XV = (NJ * 3 * 20 + NT - 1) / NT, WV = (32 * 9 * 64 / 8 + NT - 1) / NT;  // vectors per thread (Fin <= 80, C2 <= 32)
   const int fq4 = Fin / 4;        // Fin % 4 == 0, Fin <= 80 (host-checked)
+  const float inv_fq4 = 1.0f / (float)fq4;
   // native vectors: the HIP float4 / uint4 structs (a union inside) held in
   // a register array are not always split into registers
   typedef float nf4 __attribute__((ext_vector_type(4)));
   typedef uint32_t nu4 __attribute__((ext_vector_type(4)));
-  float4 xin[XV];
-  nu4 wvin[WV];
+  nf4 xin[XV];
+  float smx = -INFINITY;  // this thread's top_db partial maximum (slot tid) of the tile's utterance
+  auto fetch = [&](int tl, int tid) __attribute__((always_inline)) {
+    const int b = tl / nblk, t20 = (tl - b * nblk) * TT2;
+    const float* xb = x + (long long)b * Tin * Fin;
+#pragma unroll
+    for (int u = 0; u < XV; ++u) {
+      const int i = tid + u * NT;
+      const int q = (int)(((float)i + 0.5f) * inv_fq4);  // i / fq4 (exact: i < 2^11, fq4 <= 20)
+      const int jk = min(q, NJ * 3 - 1), f4 = i - q * fq4;
+      const int j = jk / 3, kt = jk - 3 * j;
+      const int t1 = reflect_idx(2 * t20 - 1 + j, T1);
+      xin[u] = *reinterpret_cast<const nf4*>(xb + (long long)reflect_idx(2 * t1 - 1 + kt, Tin) * Fin + 4 * f4);
+    }
+    smx = -INFINITY;
+    if (slot_max && tid < nslot) smx = slot_max[(long long)b * nslot + tid];
+  };
+  fetch(tile, tid);
   const int nwv = C2 * K / Tr::VEC;
-#pragma unroll
-  for (int u = 0; u < XV; ++u) {
-    const int i = tid + u * NT;
-    const int jk = min(i / fq4, NJ * 3 - 1), f4 = i - (i / fq4) * fq4;
-    const int j = jk / 3, kt = jk - 3 * j;
-    const int t1 = reflect_idx(2 * t20 - 1 + j, T1);
-    xin[u] = *reinterpret_cast<const float4*>(xb + (long long)reflect_idx(2 * t1 - 1 + kt, Tin) * Fin + 4 * f4);
+  {
+    nu4 wvin[WV];
+    static_for<WV>([&](auto U) { wvin[U] = reinterpret_cast<const nu4*>(wp2)[min(tid + U * NT, nwv - 1)]; });
+    static_for<WV>([&](auto U) {
+      const int i = tid + U * NT;
+      if (i < nwv) {
+        const int co = (i * Tr::VEC) / K, kk = i * Tr::VEC - co * K;
+        *reinterpret_cast<nu4*>(wl + co * KP + kk) = wvin[U];
+      }
+    });
   }
-  constexpr int AV = (2 * 40 * 64 / 4 + NT - 1) / NT;  // block-1 affine float4s per thread (F1 <= 40)
-  const int nav = F1 * C1 / 4;
-  nf4 afin[AV];
-  static_for<AV>([&](auto U) {
-    const int i = min(tid + U * NT, 2 * nav - 1);
-    const nf4* src = i < nav ? reinterpret_cast<const nf4*>(g1) + i : reinterpret_cast<const nf4*>(be1) + (i - nav);
-    afin[U] = *src;
-  });
-  constexpr int W1V = (C1 * 9 + NT - 1) / NT;  // block-1 taps per thread
-  float w1v[W1V];
-#pragma unroll
-  for (int u = 0; u < W1V; ++u) w1v[u] = w1[min(tid + u * NT, C1 * 9 - 1)];
-  const float b1v = b1 ? b1[tid & (C1 - 1)] : 0.f;
-  // the Fbank's top_db floor (features.py:706-711) applied on load: max over
-  // the utterance's spectrum-kernel partial maxima - top_db (the separate
-  // clamp pass over the features is gone)
-  float floor_db = -INFINITY;
-  if (slot_max) {
-    __shared__ float redm[FE_NT / 64];
-    float m = -INFINITY;
-    for (int i = tid; i < nslot; i += NT) m = fmaxf(m, slot_max[(long long)b * nslot + i]);
-    m = wave_max(m);
-    if (lane == 0) redm[w] = m;
-    __syncthreads();
-    m = redm[0];
-#pragma unroll
-    for (int i = 1; i < FE_NT / 64; ++i) m = fmaxf(m, redm[i]);
-    floor_db = m - top_db;
-  }
-#pragma unroll
-  for (int u = 0; u < XV; ++u) {
-    const int i = tid + u * NT;
-    float4 v = xin[u];
-    v.x = fmaxf(v.x, floor_db); v.y = fmaxf(v.y, floor_db); v.z = fmaxf(v.z, floor_db); v.w = fmaxf(v.w, floor_db);
-    if (i < NJ * 3 * fq4) *reinterpret_cast<float4*>(xs + 4 * i) = v;
-  }
-  static_for<AV>([&](auto U) {
-    if (tid + U * NT < 2 * nav) reinterpret_cast<nf4*>(g1s)[tid + U * NT] = afin[U];
-  });
-#pragma unroll
-  for (int u = 0; u < W1V; ++u)
-    if (tid + u * NT < C1 * 9) w1s[tid + u * NT] = w1v[u];
-  if (tid < C1) b1s[tid] = b1v;
-  __syncthreads();  // xs, w1s, b1s staged
-  // block 1 on MFMA, one row per wave (rows w and w + 10): the 3x3 / stride-2
-  // convolution of a row is C^T[c][f1] = W^T[c][tap] · X^T[tap][f1] with the 9
-  // taps zero-padded to one 16-deep bf16 step (v_mfma_f32_16x16x16_bf16; conv
-  // inputs and taps in bf16, fp32 accumulation — what the reference computes
-  // under autocast): 4 x 3 tiles of 16x16 per row.  A lane then holds 4
-  // consecutive channels of one frequency per tile, so the row's LayerNorm is
-  // two wave reductions (no workgroup barrier) and each tile leaves as one
-  // 8-B LDS store.  VALU budget per row (the phase's bound): the B-fragment
-  // gathers use row-invariant LDS offsets computed once, the LN statistics
-  // and affine run as packed fp32 pairs, bf16 packing is v_cvt_pk_bf16_f32.
-  // tap order k = kf * 3 + kt (conv_block_c1's layout of w1)
+  // block 1 on MFMA: the 3x3 / stride-2 convolution of a row is
+  // C^T[c][f1] = W^T[c][tap] · X^T[tap][f1] with the 9 taps zero-padded to
+  // one 16-deep bf16 step (v_mfma_f32_16x16x16_bf16; conv inputs and taps in
+  // bf16, fp32 accumulation — what the reference computes under autocast):
+  // 4 x 3 tiles of 16x16 per row.  A lane then holds 4 consecutive channels
+  // of one frequency per tile; each tile leaves as one 8-B LDS store.  The
+  // B-fragment gathers use row-invariant LDS offsets computed once, the LN
+  // statistics and affine run as packed fp32 pairs, bf16 packing is
+  // v_cvt_pk_bf16_f32.  Tap order k = kf * 3 + kt (conv_block_c1's layout of w1)
   typedef short s16x4 __attribute__((ext_vector_type(4)));
   typedef float f32x2 __attribute__((ext_vector_type(2)));
   typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
@@ -607,152 +590,261 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
     return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));
   };
   const int fr = lane & 15, g4 = lane >> 4;
-  s16x4 wa[4];  // A fragments: W^T rows c = 16 mt + fr, taps 4 g4 .. 4 g4 + 3 (k >= 9: zero)
+  // A fragments (W^T rows c = 16 mt + fr, taps 4 g4 .. 4 g4 + 3, k >= 9
+  // zero) packed once by wave 0 into LDS with the bias; each tile re-reads
+  // them (held in VGPRs across the tile loop they pushed block 2 into spills)
+  if (w == 0) {
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    float t4[4];
+    for (int mt = 0; mt < 4; ++mt) {
+      float t4[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int k = 4 * g4 + e;
-      t4[e] = k < 9 ? w1s[(16 * mt + fr) * 9 + min(k, 8)] : 0.f;
+      for (int e = 0; e < 4; ++e) {
+        const int k = 4 * g4 + e;
+        t4[e] = k < 9 ? w1[(16 * mt + fr) * 9 + min(k, 8)] : 0.f;
+      }
+      wal[mt * 64 + lane] = uint2{pack2(f32x2{t4[0], t4[1]}), pack2(f32x2{t4[2], t4[3]})};
     }
-    wa[mt] = __builtin_bit_cast(s16x4, uint2{pack2(f32x2{t4[0], t4[1]}), pack2(f32x2{t4[2], t4[3]})});
+    b1s[lane] = b1 ? b1[lane] : 0.f;
   }
-  f32x4 bias4[4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) bias4[mt] = *reinterpret_cast<const f32x4*>(b1s + 16 * mt + 4 * g4);
-  // Block 1, work split (round 5): wave w takes frequency tile nt = w % 3 of
-  // the rows j = w / 3 + 4 i (12 waves: 4 row groups x 3 tiles), all four
-  // channel tiles, which share each gathered B fragment.  The LN affine of
-  // the wave's 16 frequencies x 64 channels comes from LDS once, into VGPRs
-  // (one row per wave re-read it per row: 24 of the 33 KB of LDS traffic per
-  // wave and row, the block's bound at ~6.5-12k cycles a row); the rows'
+  // Block 1, work split: wave w takes frequency tile nt = w % 3 of the rows
+  // j = w / 3 + 4 i (12 waves: 4 row groups x 3 tiles), all four channel
+  // tiles, which share each gathered B fragment.  The LN affine of the
+  // wave's 16 frequencies x 64 channels sits in VGPRs; the rows'
   // accumulators stay in VGPRs while the row statistics combine over the
   // three tile waves through LDS — two workgroup barriers for the 17 rows.
   static_assert(NW == 12, "block 1: 4 row groups x 3 frequency tiles");
   constexpr int RG = 4, RPW = (NJ + RG - 1) / RG;  // rows per wave (5)
   __shared__ float lnred[2][NJ][4];                 // [pass][row][tile] partial sums
+  __shared__ float redm[FE_NT / 64];                // top_db: per-wave maxima
   const int nt = w % 3, grp = w / 3;
-  const int f1 = 16 * nt + fr;
-  const int f1c = min(f1, F1 - 1);
-  const float colm = f1 < F1 ? 1.f : 0.f;
-  // this lane's B-fragment taps k = 4 g4 + e of output frequency f1, as
-  // row-relative LDS offsets (k >= 9 and frequencies >= F1 read a valid
-  // element: the matching A entries are zero / the column is masked)
-  int goff[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int k = min(4 * g4 + e, 8);
-    goff[e] = (k % 3) * Fin + reflect_idx(2 * f1c + k / 3 - 1, Fin);
-  }
-  f32x4 gam[4], bet[4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    gam[mt] = *reinterpret_cast<const f32x4*>(g1s + f1c * C1 + 16 * mt + 4 * g4);
-    bet[mt] = *reinterpret_cast<const f32x4*>(be1s + f1c * C1 + 16 * mt + 4 * g4);
-  }
   const float inv_n1 = 1.0f / (float)(F1 * C1);
-  FE_TL(1);
-  f32x4 acc[RPW][4];
+  // block 2 (tile-invariant part): rows m = t2_local * F2 + f2, columns the C2
+  // channels, K = (kt, kf, ci); wave w < nmw owns m-tiles TMW w .. TMW w + TMW - 1
+  const int ntl = C2 / 16;
+  constexpr int TMW = 2;  // m-tiles per wave
+  const int nout = F2 * C2;  // multiple of 16 (C2 % 16 == 0)
+  const float inv_f2 = 1.0f / (float)F2, inv_nout = 1.0f / (float)nout;
+  const int nch = nout / 8;
+  constexpr int NCH = (32 * 32 / 8 + 63) / 64;  // epilogue chunks per lane (F2, C2 <= 32)
+
+  float floor_db = -INFINITY;
+  for (; tile < tend; ++tile) {
+    const int b = tile / nblk, t20 = (tile - b * nblk) * TT2;
+    const int carry = tile > tbeg && t20 > 0 ? 1 : 0;  // row 0 already in b1r
+    FE_TL(0);
+    // lane-derived addressing recomputed per tile from an opaque copy of the
+    // lane id: hoisted out of the loop, the tile-invariant LDS addresses of
+    // every gather / store occupied ~170 VGPRs (scratch spills)
+    int tdl = tid;
+    asm volatile("" : "+v"(tdl));
+    const int ln = tdl & 63;
+    const int frl = ln & 15, g4l = ln >> 4;
+    const int f1 = 16 * nt + frl;
+    const int f1c = min(f1, F1 - 1);
+    const float colm = f1 < F1 ? 1.f : 0.f;
+    // this lane's B-fragment taps k = 4 g4 + e of output frequency f1, as
+    // row-relative LDS offsets (k >= 9 and frequencies >= F1 read a valid
+    // element: the matching A entries are zero / the column is masked)
+    int goff[4];
 #pragma unroll
-  for (int i = 0; i < RPW; ++i) {
-    const int j = min(grp + RG * i, NJ - 1);  // (a group's missing row recomputes the last: discarded)
-    const float* r = xs + (j * 3) * Fin;
-    const s16x4 xb4 =
-        __builtin_bit_cast(s16x4, uint2{pack2(f32x2{r[goff[0]], r[goff[1]]}), pack2(f32x2{r[goff[2]], r[goff[3]]})});
+    for (int e = 0; e < 4; ++e) {
+      const int k = min(4 * g4l + e, 8);
+      goff[e] = (k % 3) * Fin + reflect_idx(2 * f1c + k / 3 - 1, Fin);
+    }
+    const int fk = 8 * g4l;
+
+    // the Fbank's top_db floor (features.py:706-711), max over the
+    // utterance's spectrum-kernel partial maxima - top_db, applied at the
+    // block-1 gathers (the separate clamp pass over the features is gone)
+    // (once per utterance: the floor stays in a register across its tiles)
+    const bool newutt = tile == tbeg || t20 == 0;
+    if (slot_max && newutt) {
+      float m = smx;
+      for (int i = tdl + NT; i < nslot; i += NT) m = fmaxf(m, slot_max[(long long)b * nslot + i]);
+      m = wave_max(m);
+      if (lane == 0) redm[w] = m;
+    }
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) acc[i][mt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wa[mt], xb4, bias4[mt], 0, 0, 0);
-  }
-  // LayerNorm over each row's F1 x C1 values, two-pass: the tile partials of
-  // every row, then the squared deviations
-  float mean[RPW], rstd[RPW];
+    for (int u = 0; u < XV; ++u) {
+      const int i = tdl + u * NT;
+      if (i < NJ * 3 * fq4) *reinterpret_cast<nf4*>(xs + 4 * i) = xin[u];
+    }
+    __syncthreads();  // xs, redm (and, first tile, wl) staged
+    if (slot_max && newutt) {
+      float m = redm[0];
 #pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
+      for (int i = 1; i < FE_NT / 64; ++i) m = fmaxf(m, redm[i]);
+      floor_db = m - top_db;
+    }
+    FE_TL(1);
+    // max(v, floor) as one v_max_f32 (fmaxf of a loaded value adds a NaN-quieting max)
+    auto flo = [floor_db](float v) __attribute__((always_inline)) {
+      float r;
+      asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(v), "v"(floor_db));
+      return r;
+    };
+    s16x4 wa[4];  // (after the barrier: wave 0 staged them before the first tile)
+    f32x4 bias4[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      wa[mt] = __builtin_bit_cast(s16x4, wal[mt * 64 + ln]);
+      bias4[mt] = *reinterpret_cast<const f32x4*>(b1s + 16 * mt + 4 * g4l);
+    }
+    // the wave's LN affine (L2-resident; per tile, so it is not live through block 2)
+    f32x4 gam[4], bet[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      gam[mt] = *reinterpret_cast<const f32x4*>(g1 + f1c * C1 + 16 * mt + 4 * g4l);
+      bet[mt] = *reinterpret_cast<const f32x4*>(be1 + f1c * C1 + 16 * mt + 4 * g4l);
+    }
+    f32x4 acc[RPW][4];
 #pragma unroll
     for (int i = 0; i < RPW; ++i) {
-      const int j = grp + RG * i;
-      f32x2 sn = {0.f, 0.f};
+      // rows j = carry + grp + 4 i: 16 rows of a continuing tile (4 per
+      // group), else 17 (group 0 takes the fifth); a wave without a fifth
+      // row branches over it (uniform)
+      const int j = carry + grp + RG * i;
+      if (i == RPW - 1 && j >= NJ) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc[i][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        continue;
+      }
+      const float* r = xs + (j * 3) * Fin;
+      const s16x4 xb4 = __builtin_bit_cast(
+          s16x4, uint2{pack2(f32x2{flo(r[goff[0]]), flo(r[goff[1]])}), pack2(f32x2{flo(r[goff[2]]), flo(r[goff[3]])})});
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[i][mt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wa[mt], xb4, bias4[mt], 0, 0, 0);
+    }
+    // LayerNorm statistics of each row over its F1 x C1 values in one pass:
+    // the tile waves' sums and sums of squares combine through LDS behind one
+    // barrier (var = E[y^2] - mean^2 in fp32: a row's |mean| / std stays far
+    // below the 2^12 where that loses bf16 precision; the second pass over
+    // the registers and its barrier cost ~8 % of the kernel)
+    float mean[RPW], rstd[RPW];
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int j = carry + grp + RG * i;
+      if (i == RPW - 1 && j >= NJ) continue;
+      f32x2 sn = {0.f, 0.f}, sq = {0.f, 0.f};
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
-        f32x2 a0 = f32x2{acc[i][mt][0], acc[i][mt][1]}, a1 = f32x2{acc[i][mt][2], acc[i][mt][3]};
-        if (pass) {
-          a0 -= f32x2{mean[i], mean[i]};
-          a1 -= f32x2{mean[i], mean[i]};
-          sn += a0 * a0 + a1 * a1;
-        } else {
-          sn += a0 + a1;
-        }
+        const f32x2 a0 = f32x2{acc[i][mt][0], acc[i][mt][1]}, a1 = f32x2{acc[i][mt][2], acc[i][mt][3]};
+        sn += a0;
+        sn += a1;
+        sq = a0 * a0 + sq;
+        sq = a1 * a1 + sq;
       }
-      const float t = wave_sum_v((sn.x + sn.y) * colm);
-      if (j < NJ && lane == 0) lnred[pass][j][nt] = t;
+      const float t = wave_sum_v((sn.x + sn.y) * colm), u = wave_sum_v((sq.x + sq.y) * colm);
+      if (j < NJ && lane == 0) {
+        lnred[0][j][nt] = t;
+        lnred[1][j][nt] = u;
+      }
     }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < RPW; ++i) {
-      const int j = min(grp + RG * i, NJ - 1);
-      const float t = (lnred[pass][j][0] + lnred[pass][j][1]) + lnred[pass][j][2];
-      if (pass)
-        rstd[i] = 1.0f / sqrtf(t * inv_n1 + eps1);
-      else
-        mean[i] = t * inv_n1;
+      const int j = min(carry + grp + RG * i, NJ - 1);
+      const float t = (lnred[0][j][0] + lnred[0][j][1]) + lnred[0][j][2];
+      const float u = (lnred[1][j][0] + lnred[1][j][1]) + lnred[1][j][2];
+      mean[i] = t * inv_n1;
+      rstd[i] = 1.0f / sqrtf(fmaxf(u * inv_n1 - mean[i] * mean[i], 0.f) + eps1);
     }
-  }
-  FE_TL(2);
+    FE_TL(2);
 #pragma unroll
-  for (int i = 0; i < RPW; ++i) {
-    const int j = grp + RG * i;
-    if (j >= NJ || f1 >= F1) continue;
-    const f32x2 mv = {mean[i], mean[i]}, rv = {rstd[i], rstd[i]};
+    for (int i = 0; i < RPW; ++i) {
+      const int j = carry + grp + RG * i;
+      if (j >= NJ || f1 >= F1) continue;
+      // (x - mean) rstd as one packed FMA, x rstd + (-mean rstd)
+      const f32x2 rv = {rstd[i], rstd[i]}, nmr = {-mean[i] * rstd[i], -mean[i] * rstd[i]};
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const int c = 16 * mt + 4 * g4;
-      f32x2 y0 = (f32x2{acc[i][mt][0], acc[i][mt][1]} - mv) * rv * f32x2{gam[mt][0], gam[mt][1]} +
-                 f32x2{bet[mt][0], bet[mt][1]};
-      f32x2 y1 = (f32x2{acc[i][mt][2], acc[i][mt][3]} - mv) * rv * f32x2{gam[mt][2], gam[mt][3]} +
-                 f32x2{bet[mt][2], bet[mt][3]};
-      y0 = lrelu2<LMAX>(y0, slope1);
-      y1 = lrelu2<LMAX>(y1, slope1);
-      *reinterpret_cast<uint2*>(b1r + (j * F1 + f1) * C1P + c) = uint2{pack2(y0), pack2(y1)};
+      for (int mt = 0; mt < 4; ++mt) {
+        const int c = 16 * mt + 4 * g4l;
+        f32x2 y0 = (f32x2{acc[i][mt][0], acc[i][mt][1]} * rv + nmr) * f32x2{gam[mt][0], gam[mt][1]} +
+                   f32x2{bet[mt][0], bet[mt][1]};
+        f32x2 y1 = (f32x2{acc[i][mt][2], acc[i][mt][3]} * rv + nmr) * f32x2{gam[mt][2], gam[mt][3]} +
+                   f32x2{bet[mt][2], bet[mt][3]};
+        y0 = lrelu2<LMAX>(y0, slope1);
+        y1 = lrelu2<LMAX>(y1, slope1);
+        *reinterpret_cast<uint2*>(b1r + (j * F1 + f1) * C1P + c) = uint2{pack2(y0), pack2(y1)};
+      }
     }
-  }
-  FE_TL(3);
-  // block-2 weights (L2-resident: every workgroup reads the same 37 KB) into
-  // region 0 once every wave is done with the block-1 affine (loading them
-  // with the stage instead delays the stage's LDS stores more than it saves)
-  static_for<WV>([&](auto U) { wvin[U] = reinterpret_cast<const nu4*>(wp2)[min(tid + U * NT, nwv - 1)]; });
-  __syncthreads();
-  static_for<WV>([&](auto U) {
-    const int i = tid + U * NT;
-    if (i < nwv) {
-      const int co = (i * Tr::VEC) / K, kk = i * Tr::VEC - co * K;
-      *reinterpret_cast<nu4*>(wl + co * KP + kk) = wvin[U];
-    }
-  });
-  __syncthreads();
-  FE_TL(11);
+    FE_TL(3);
+    __syncthreads();  // b1r complete; xs free for yv
 
-  // block 2 as one implicit GEMM over the workgroup's output positions:
-  // rows m = t2_local * F2 + f2 (8 x 20 = 160 = 10 tiles of 16 at config 3, no
-  // padded rows), columns the C2 channels, K = (kt, kf, ci).  Wave w < nmw
-  // owns m-tiles TMW w .. TMW w + TMW - 1 against both channel tiles, so each
-  // K step issues 2 TMW MFMAs behind TMW + 2 fragment reads.  (One m-tile per
-  // wave — ten multiplying waves instead of five — measured equal, 74.4 vs
-  // 74.6 us: the phase is LDS-read bound, profiles/r05t_fe_tl.log.)
-  const int nrow = min(TT2, T2 - t20);  // valid output rows of this workgroup
-  const int Mv = nrow * F2, ntl = C2 / 16;
-  constexpr int TMW = 2;                // m-tiles per wave
-  const int nmw = (Mv + 16 * TMW - 1) / (16 * TMW);  // waves with MFMA work (<= NW: F1 <= 40, F2 <= 20, TT2 = 8)
-  const int fk = 8 * (lane >> 4);
-  // the epilogue's LN affine and bias, loaded ahead of the MFMA loop (their
-  // latency hides behind it)
-  const int nout = F2 * C2;  // multiple of 16 (C2 % 16 == 0)
-  const int nch = nout / 8;
-  constexpr int NCH = (32 * 32 / 8 + 63) / 64;  // chunks per lane (F2, C2 <= 32)
-  float4 g2v[NCH][2], b2v[NCH][2];
-  if (w < nrow) {
+    // block 2 as one implicit GEMM over the tile's output positions (8 x 20
+    // = 160 rows = 10 m-tiles at config 3, no padded rows): each K step
+    // issues 2 TMW MFMAs behind TMW + 2 fragment reads.  (One m-tile per
+    // wave — ten multiplying waves of 18 steps — measured equal to five
+    // waves of two, 74.4 vs 74.6 us, profiles/r05t_fe_tl.log.)
+    const int nrow = min(TT2, T2 - t20);  // valid output rows of this tile
+    const int Mv = nrow * F2;
+    const int nmw = (Mv + 16 * TMW - 1) / (16 * TMW);  // waves with MFMA work (<= NW: F1 <= 40, F2 <= 20, TT2 = 8)
+    f32x4 acc2[TMW][2];
+#pragma unroll
+    for (int tm = 0; tm < TMW; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn) acc2[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float cb[2] = {0.f, 0.f};
+    if (w < nmw) {
+      int aoff[TMW][3];  // A-row (m = 16 TMW w + 16 tm + frl) offsets into b1r per kf, kt = 0
+#pragma unroll
+      for (int tm = 0; tm < TMW; ++tm) {
+        const int m = 16 * TMW * w + 16 * tm + frl;
+        const int mc = m < Mv ? m : 0;
+        const int tl = (int)(((float)mc + 0.5f) * inv_f2), fo = mc - tl * F2;  // mc / F2 (mc < 160)
+#pragma unroll
+        for (int kf = 0; kf < 3; ++kf) aoff[tm][kf] = (2 * tl * F1 + reflect_idx(2 * fo - 1 + kf, F1)) * C1P + fk;
+      }
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn) cb[tn] = b2 && tn < ntl ? b2[tn * 16 + frl] : 0.f;
+      // unconditional fragment reads (rows past Mv / channel tiles past C2 read
+      // valid LDS and are discarded at the store), fully unrolled so the reads
+      // of later K steps issue ahead of the MFMAs
+      const int wo = frl * KP + fk;
+      const T* wrow[2] = {wl + wo, wl + wo + (ntl > 1 ? 16 : 0) * KP};
+      // software-pipelined: step st + 1's fragments are read before step
+      // st's MFMAs issue (otherwise every step waits out a full LDS latency)
+      typename Tr::frag fa[2][TMW], fbw[2][2];
+      auto ld = [&](auto S, int buf) __attribute__((always_inline)) {
+        constexpr int st = decltype(S)::value;
+        constexpr int kt = st / 6, kf = (st / 2) % 3, c0 = 32 * (st % 2);
+        constexpr int k = (kt * 3 + kf) * C1 + c0;
+#pragma unroll
+        for (int tm = 0; tm < TMW; ++tm) fa[buf][tm] = Tr::load(b1r + kt * F1 * C1P + aoff[tm][kf] + c0);
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) fbw[buf][tn] = Tr::load(wrow[tn] + k);
+      };
+      ld(std::integral_constant<int, 0>{}, 0);
+      static_for<18>([&](auto S) {
+        constexpr int st = decltype(S)::value;
+        if constexpr (st + 1 < 18) ld(std::integral_constant<int, st + 1>{}, (st + 1) & 1);
+#pragma unroll
+        for (int tm = 0; tm < TMW; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < 2; ++tn) Tr::mma(acc2[tm][tn], fa[st & 1][tm], fbw[st & 1][tn]);
+      });
+      // D rows m = 16 TMW w + 16 tm + 4 (lane >> 4) + r -> yv[m][co] (rows of
+      // one output time step are contiguous: yv[t2_local][f2][co])
+#pragma unroll
+      for (int tm = 0; tm < TMW; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) {
+          if (tn >= ntl) continue;
+          const int co = tn * 16 + frl;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = 16 * TMW * w + 16 * tm + 4 * g4l + r;
+            if (m < Mv) yv[m * C2 + co] = acc2[tm][tn][r] + cb[tn];
+          }
+        }
+    }
+    // the epilogue's LN affine (its latency hides behind the barrier wait)
+    // (unconditional: values left undefined on some waves become loop-carried
+    // registers)
+    float4 g2v[NCH][2], b2v[NCH][2];
 #pragma unroll
     for (int u = 0; u < NCH; ++u) {
-      const int c = min(lane + 64 * u, nch - 1);
+      const int c = min(ln + 64 * u, nch - 1);
       const float4* gp = reinterpret_cast<const float4*>(g2 + 8 * c);
       const float4* bp = reinterpret_cast<const float4*>(be2 + 8 * c);
       g2v[u][0] = gp[0];
@@ -760,121 +852,79 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
       b2v[u][0] = bp[0];
       b2v[u][1] = bp[1];
     }
-  }
-  if (w < nmw) {
-    int aoff[TMW][3];  // A-row (m = 16 TMW w + 16 tm + fr) offsets into b1r per kf, kt = 0
-    bool arow[TMW];
-#pragma unroll
-    for (int tm = 0; tm < TMW; ++tm) {
-      const int m = 16 * TMW * w + 16 * tm + fr;
-      arow[tm] = m < Mv;
-      const int mc = arow[tm] ? m : 0;
-      const int tl = mc / F2, fo = mc - tl * F2;
-#pragma unroll
-      for (int kf = 0; kf < 3; ++kf) aoff[tm][kf] = (2 * tl * F1 + reflect_idx(2 * fo - 1 + kf, F1)) * C1P;
+    // the next tile's inputs, in flight through the epilogue (issued before
+    // block 2 they were spilled: its fragments need the registers)
+    if (tile + 1 < tend) fetch(tile + 1, tdl);
+    FE_TL(12);
+    __syncthreads();  // yv complete; block 2 done with b1r
+    if (w >= TT2) {
+      // waves idle in the epilogue carry block-1 row 16 into row 0 for a
+      // continuing next tile (its row 0 is this tile's row 16)
+      const int nv = F1 * C1P * (int)sizeof(T) / 16;
+      for (int v = tdl - 64 * TT2; v < nv; v += NT - 64 * TT2)
+        reinterpret_cast<nu4*>(b1r)[v] = reinterpret_cast<const nu4*>(b1r + (NJ - 1) * F1 * C1P)[v];
     }
-    float cb[2];
+    if (w < nrow) {
+      const int t2 = t20 + w;
+      const float* yw = yv + w * F2 * C2;
+      // the wave's own LDS row: LN over F2*C2 (wave-local), LeakyReLU, store.
+      // Lane l owns elements 8c .. 8c+7 for chunks c = l, l + 64, ... (16-B LDS
+      // reads, 2 x 16-B affine loads, one 16-B bf16 store per chunk)
+      float yv8[NCH][8];
+      float s2 = 0.f;
 #pragma unroll
-    for (int tn = 0; tn < 2; ++tn) cb[tn] = b2 && tn < ntl ? b2[tn * 16 + fr] : 0.f;
-    f32x4 acc[TMW][2];
+      for (int u = 0; u < NCH; ++u) {
+        const int c = ln + 64 * u;
+        const int cc = min(c, nch - 1);
+        const float4 a0 = *reinterpret_cast<const float4*>(yw + 8 * cc);
+        const float4 a1 = *reinterpret_cast<const float4*>(yw + 8 * cc + 4);
+        const float t8[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
 #pragma unroll
-    for (int tm = 0; tm < TMW; ++tm)
-#pragma unroll
-      for (int tn = 0; tn < 2; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // unconditional fragment reads (rows past Mv / channel tiles past C2 read
-    // valid LDS and are discarded at the store), fully unrolled so the reads
-    // of later K steps issue ahead of the MFMAs
-    const T* wrow[2] = {wl + fr * KP + fk, wl + ((ntl > 1 ? 16 : 0) + fr) * KP + fk};
-#pragma unroll
-    for (int kt = 0; kt < 3; ++kt) {
-      const T* brow = b1r + kt * F1 * C1P + fk;
-#pragma unroll
-      for (int kf = 0; kf < 3; ++kf)
-#pragma unroll
-        for (int c0 = 0; c0 < C1; c0 += 32) {
-          const int k = (kt * 3 + kf) * C1 + c0;
-          typename Tr::frag fa[TMW], fbw[2];
-#pragma unroll
-          for (int tm = 0; tm < TMW; ++tm) fa[tm] = Tr::load(brow + aoff[tm][kf] + c0);
-#pragma unroll
-          for (int tn = 0; tn < 2; ++tn) fbw[tn] = Tr::load(wrow[tn] + k);
-#pragma unroll
-          for (int tm = 0; tm < TMW; ++tm)
-#pragma unroll
-            for (int tn = 0; tn < 2; ++tn) Tr::mma(acc[tm][tn], fa[tm], fbw[tn]);
-        }
-    }
-    // D rows m = 16 TMW w + 16 tm + 4 (lane >> 4) + r -> yv[m][co] (rows of
-    // one output time step are contiguous: yv[t2_local][f2][co])
-#pragma unroll
-    for (int tm = 0; tm < TMW; ++tm)
-#pragma unroll
-      for (int tn = 0; tn < 2; ++tn) {
-        if (tn >= ntl) continue;
-        const int co = tn * 16 + fr;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = 16 * TMW * w + 16 * tm + 4 * (lane >> 4) + r;
-          if (m < Mv) yv[m * C2 + co] = acc[tm][tn][r] + cb[tn];
+        for (int e = 0; e < 8; ++e) {
+          yv8[u][e] = c < nch ? t8[e] : 0.f;
+          s2 += yv8[u][e];
         }
       }
+      const float m2 = wave_sum_v(s2) * inv_nout;
+      float q2 = 0.f;
+#pragma unroll
+      for (int u = 0; u < NCH; ++u)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float dv = ln + 64 * u < nch ? yv8[u][e] - m2 : 0.f;
+          q2 += dv * dv;
+        }
+      const float r2 = 1.0f / sqrtf(wave_sum_v(q2) * inv_nout + eps2);
+      const long long ob = ((long long)b * T2 + t2) * nout;
+#pragma unroll
+      for (int u = 0; u < NCH; ++u) {
+        const int c = ln + 64 * u;
+        if (c >= nch) continue;
+        const float4 ga = g2v[u][0], gb = g2v[u][1], ba = b2v[u][0], bb = b2v[u][1];
+        const float gg[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
+        const float bt[8] = {ba.x, ba.y, ba.z, ba.w, bb.x, bb.y, bb.z, bb.w};
+        float y[8];
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          const f32x2 t = (f32x2{yv8[u][e], yv8[u][e + 1]} * f32x2{r2, r2} + f32x2{-m2 * r2, -m2 * r2}) *
+                              f32x2{gg[e], gg[e + 1]} + f32x2{bt[e], bt[e + 1]};
+          const f32x2 l = lrelu2<LMAX>(t, slope2);
+          y[e] = l[0];
+          y[e + 1] = l[1];
+        }
+        if (out_bf16) {
+          *reinterpret_cast<typename MT<bf16_t>::frag*>(reinterpret_cast<bf16_t*>(out) + ob + 8 * c) = MT<bf16_t>::from8(y);
+        } else {
+          float* o = reinterpret_cast<float*>(out) + ob + 8 * c;
+          *reinterpret_cast<float4*>(o) = make_float4(y[0], y[1], y[2], y[3]);
+          *reinterpret_cast<float4*>(o + 4) = make_float4(y[4], y[5], y[6], y[7]);
+        }
+      }
+    }
+    FE_TL(13);
+    __syncthreads();  // yv read before the next tile's xs stores
   }
-  FE_TL(12);
-  __syncthreads();
-  if (w >= nrow) return;  // no barrier below
-  const int t2 = t20 + w;
-  const float* yw = yv + w * F2 * C2;
-  // the wave's own LDS row: LN over F2*C2 (wave-local), LeakyReLU, store.
-  // Lane l owns elements 8c .. 8c+7 for chunks c = l, l + 64, ... (16-B LDS
-  // reads, 2 x 16-B affine loads, one 16-B bf16 store per chunk)
-  float yv8[NCH][8];
-  float s2 = 0.f;
-#pragma unroll
-  for (int u = 0; u < NCH; ++u) {
-    const int c = lane + 64 * u;
-    const int cc = min(c, nch - 1);
-    const float4 a0 = *reinterpret_cast<const float4*>(yw + 8 * cc);
-    const float4 a1 = *reinterpret_cast<const float4*>(yw + 8 * cc + 4);
-    const float t8[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      yv8[u][e] = c < nch ? t8[e] : 0.f;
-      s2 += yv8[u][e];
-    }
-  }
-  const float m2 = wave_sum_v(s2) / nout;
-  float q2 = 0.f;
-#pragma unroll
-  for (int u = 0; u < NCH; ++u)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float dv = lane + 64 * u < nch ? yv8[u][e] - m2 : 0.f;
-      q2 += dv * dv;
-    }
-  const float r2 = 1.0f / sqrtf(wave_sum_v(q2) / nout + eps2);
-  const long long ob = ((long long)b * T2 + t2) * nout;
-#pragma unroll
-  for (int u = 0; u < NCH; ++u) {
-    const int c = lane + 64 * u;
-    if (c >= nch) continue;
-    const float4 ga = g2v[u][0], gb = g2v[u][1], ba = b2v[u][0], bb = b2v[u][1];
-    const float gg[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
-    const float bt[8] = {ba.x, ba.y, ba.z, ba.w, bb.x, bb.y, bb.z, bb.w};
-    float y[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float t = (yv8[u][e] - m2) * r2 * gg[e] + bt[e];
-      y[e] = t >= 0.f ? t : t * slope2;
-    }
-    if (out_bf16) {
-      *reinterpret_cast<typename MT<bf16_t>::frag*>(reinterpret_cast<bf16_t*>(out) + ob + 8 * c) = MT<bf16_t>::from8(y);
-    } else {
-      float* o = reinterpret_cast<float*>(out) + ob + 8 * c;
-      *reinterpret_cast<float4*>(o) = make_float4(y[0], y[1], y[2], y[3]);
-      *reinterpret_cast<float4*>(o + 4) = make_float4(y[4], y[5], y[6], y[7]);
-    }
-  }
-  FE_TL(13);
+  FE_TL(15);
 }
 
 // key padding mask from relative lengths (TransformerASR.py:295-301):
@@ -1042,11 +1092,21 @@ SBK_API int sbk_conv_frontend2(int dtype_bf16, const float* x, int B, int Tin, i
     return SBK_ERR_ARG;
   constexpr int TT2 = FE_TT2, NJ = 2 * TT2 + 1;
   const size_t esz = dtype_bf16 ? 2 : 4;
-  const size_t lds = ((std::max((size_t)C2 * (9 * C1 + 8) * esz, (size_t)2 * F1 * C1 * 4) + 15) & ~(size_t)15) +
+  const size_t lds = (((size_t)C2 * (9 * C1 + 8) * esz + 15) & ~(size_t)15) +
                      (size_t)std::max(TT2 * F2 * C2, (NJ * 3 * Fin + 3) & ~3) * 4 + (size_t)NJ * F1 * (C1 + 8) * esz +
-                     (size_t)C1 * 10 * 4;  // block-1 taps + bias
+                     4 * 64 * 8 + C1 * 4;  // block-1 A fragments + bias
   if (dtype_bf16 && lds > 160 * 1024 - 1024) return SBK_ERR_ARG;
-  const dim3 grid(B * ((T2 + TT2 - 1) / TT2));
+  // persistent: one workgroup per CU (the LDS allows no second), each
+  // walking tiles blockIdx.x + k gridDim.x
+  const int ntile = B * ((T2 + TT2 - 1) / TT2);
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  const dim3 grid(std::min(ntile, ncu));
   hipStream_t s = (hipStream_t)stream;
   if (!dtype_bf16) return SBK_ERR_ARG;  // fp32 path: the per-block kernels (LDS would not fit)
   auto launch = [&](auto kern, bool& attr) -> int {
@@ -1056,13 +1116,13 @@ SBK_API int sbk_conv_frontend2(int dtype_bf16, const float* x, int B, int Tin, i
       if (e != hipSuccess) return (int)e;
       attr = true;
     }
-    hipLaunchKernelGGL(kern, grid, dim3(FE_NT), lds, s, x, Tin, Fin, T1, F1, T2, F2, w1, b1, g1, be1, eps1, slope1,
+    hipLaunchKernelGGL(kern, grid, dim3(FE_NT), lds, s, x, ntile, Tin, Fin, T1, F1, T2, F2, w1, b1, g1, be1, eps1, slope1,
                        reinterpret_cast<const bf16_t*>(wp2), C2, b2, g2, be2, eps2, slope2, out, out_bf16, slot_max,
                        nslot, top_db);
     return 0;
   };
   static bool attr_max = false, attr_sel = false;
-  const int rc = slope1 <= 1.f ? launch(&frontend2_kernel<bf16_t, 64, true>, attr_max)
+  const int rc = slope1 <= 1.f && slope2 <= 1.f ? launch(&frontend2_kernel<bf16_t, 64, true>, attr_max)
                                : launch(&frontend2_kernel<bf16_t, 64, false>, attr_sel);
   if (rc) return rc;
   SBK_CHECK_LAUNCH();
