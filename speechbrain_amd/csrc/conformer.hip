@@ -747,9 +747,11 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
       const float t = (lnred[0][j][0] + lnred[0][j][1]) + lnred[0][j][2];
       const float u = (lnred[1][j][0] + lnred[1][j][1]) + lnred[1][j][2];
       mean[i] = t * inv_n1;
-      rstd[i] = 1.0f / sqrtf(fmaxf(u * inv_n1 - mean[i] * mean[i], 0.f) + eps1);
+      rstd[i] = rsqrtf(fmaxf(u * inv_n1 - mean[i] * mean[i], 0.f) + eps1);
     }
     FE_TL(2);
+    // this lane's b1r slot in row 0; rows are F1 * C1P apart (a scalar offset)
+    T* const b1w = b1r + f1 * C1P + 4 * g4l;
 #pragma unroll
     for (int i = 0; i < RPW; ++i) {
       const int j = carry + grp + RG * i;
@@ -758,14 +760,13 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
       const f32x2 rv = {rstd[i], rstd[i]}, nmr = {-mean[i] * rstd[i], -mean[i] * rstd[i]};
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
-        const int c = 16 * mt + 4 * g4l;
         f32x2 y0 = (f32x2{acc[i][mt][0], acc[i][mt][1]} * rv + nmr) * f32x2{gam[mt][0], gam[mt][1]} +
                    f32x2{bet[mt][0], bet[mt][1]};
         f32x2 y1 = (f32x2{acc[i][mt][2], acc[i][mt][3]} * rv + nmr) * f32x2{gam[mt][2], gam[mt][3]} +
                    f32x2{bet[mt][2], bet[mt][3]};
         y0 = lrelu2<LMAX>(y0, slope1);
         y1 = lrelu2<LMAX>(y1, slope1);
-        *reinterpret_cast<uint2*>(b1r + (j * F1 + f1) * C1P + c) = uint2{pack2(y0), pack2(y1)};
+        *reinterpret_cast<uint2*>(b1w + j * (F1 * C1P) + 16 * mt) = uint2{pack2(y0), pack2(y1)};
       }
     }
     FE_TL(3);
@@ -802,9 +803,9 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
       // of later K steps issue ahead of the MFMAs
       const int wo = frl * KP + fk;
       const T* wrow[2] = {wl + wo, wl + wo + (ntl > 1 ? 16 : 0) * KP};
-      // software-pipelined: step st + 1's fragments are read before step
-      // st's MFMAs issue (otherwise every step waits out a full LDS latency)
-      typename Tr::frag fa[2][TMW], fbw[2][2];
+      // (reading step st + 1's fragments ahead of step st's MFMAs measured
+      // 1-1.5 us slower: profiles/r05ac_fe_pipe_ab.log)
+      typename Tr::frag fa[1][TMW], fbw[1][2];
       auto ld = [&](auto S, int buf) __attribute__((always_inline)) {
         constexpr int st = decltype(S)::value;
         constexpr int kt = st / 6, kf = (st / 2) % 3, c0 = 32 * (st % 2);
@@ -814,28 +815,28 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
 #pragma unroll
         for (int tn = 0; tn < 2; ++tn) fbw[buf][tn] = Tr::load(wrow[tn] + k);
       };
-      ld(std::integral_constant<int, 0>{}, 0);
       static_for<18>([&](auto S) {
-        constexpr int st = decltype(S)::value;
-        if constexpr (st + 1 < 18) ld(std::integral_constant<int, st + 1>{}, (st + 1) & 1);
+        ld(S, 0);
 #pragma unroll
         for (int tm = 0; tm < TMW; ++tm)
 #pragma unroll
-          for (int tn = 0; tn < 2; ++tn) Tr::mma(acc2[tm][tn], fa[st & 1][tm], fbw[st & 1][tn]);
+          for (int tn = 0; tn < 2; ++tn) Tr::mma(acc2[tm][tn], fa[0][tm], fbw[0][tn]);
       });
       // D rows m = 16 TMW w + 16 tm + 4 (lane >> 4) + r -> yv[m][co] (rows of
-      // one output time step are contiguous: yv[t2_local][f2][co])
+      // one output time step are contiguous: yv[t2_local][f2][co]); row
+      // offsets beyond the lane base are scalar, and a full tile stores
+      // without row guards
+      const int mb = 16 * TMW * w + 4 * g4l;
+      float* const yw0 = yv + mb * C2 + frl;
+      const bool full = Mv == TT2 * F2 && 16 * TMW * nmw <= Mv;
 #pragma unroll
       for (int tm = 0; tm < TMW; ++tm)
 #pragma unroll
         for (int tn = 0; tn < 2; ++tn) {
           if (tn >= ntl) continue;
-          const int co = tn * 16 + frl;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int m = 16 * TMW * w + 16 * tm + 4 * g4l + r;
-            if (m < Mv) yv[m * C2 + co] = acc2[tm][tn][r] + cb[tn];
-          }
+          for (int r = 0; r < 4; ++r)
+            if (full || mb + 16 * tm + r < Mv) yw0[(16 * tm + r) * C2 + 16 * tn] = acc2[tm][tn][r] + cb[tn];
         }
     }
     // the epilogue's LN affine (its latency hides behind the barrier wait)
@@ -894,7 +895,7 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
           const float dv = ln + 64 * u < nch ? yv8[u][e] - m2 : 0.f;
           q2 += dv * dv;
         }
-      const float r2 = 1.0f / sqrtf(wave_sum_v(q2) * inv_nout + eps2);
+      const float r2 = rsqrtf(wave_sum_v(q2) * inv_nout + eps2);
       const long long ob = ((long long)b * T2 + t2) * nout;
 #pragma unroll
       for (int u = 0; u < NCH; ++u) {
