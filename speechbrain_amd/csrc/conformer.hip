@@ -514,11 +514,15 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
   T* wl = reinterpret_cast<T*>(smem);                                   // C2 x KP block-2 weights
   const int r0 = (C2 * KP * (int)sizeof(T) + 15) & ~15;
   float* yv = reinterpret_cast<float*>(smem + r0);                      // TT2 x F2*C2 (block 2)
-  float* xs = yv;                                                       // NJ x 3 x Fin (block 1, same space)
-  const int xsz = max(TT2 * F2 * C2, (NJ * 3 * Fin + 3) & ~3);
-  T* b1r = reinterpret_cast<T*>(yv + xsz);                              // NJ x F1 x C1P
+  T* b1r = reinterpret_cast<T*>(yv + TT2 * F2 * C2);                    // NJ x F1 x C1P
+  // the block-1 input rows (NJ x 3 x Fin fp32, <= 16.3 KB) live in b1r rows
+  // 1 .. 3: staged during the previous tile's epilogue (block 2 is done
+  // with b1r), gathered before the block-1 statistics barrier, overwritten
+  // by block 1's own rows only after it (host-checked to fit rows 1 .. 15)
+  float* xs = reinterpret_cast<float*>(b1r + F1 * C1P);
   uint2* wal = reinterpret_cast<uint2*>(b1r + NJ * F1 * C1P);           // 4 x 64 block-1 A fragments (bf16 taps)
-  float* b1s = reinterpret_cast<float*>(wal + 4 * 64);                  // C1 block-1 bias
+  float* g2s = reinterpret_cast<float*>(wal + 4 * 64);                  // F2*C2 block-2 LN gamma
+  float* be2s = g2s + F2 * C2;                                          // F2*C2 block-2 LN beta
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nblk = (T2 + TT2 - 1) / TT2;
@@ -529,39 +533,59 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
   int tile = tbeg;
   FE_TL(14);
 
-  // Persistent workgroups (round 5): one per CU, each walks the tiles
-  // blockIdx.x, + gridDim.x, ...  The per-tile constants — block-2 weights
-  // (37 KB, LDS), block-1 taps / bias / LN affine (VGPRs) — load once per
-  // workgroup instead of once per tile (57 KB of L2 reads and a staging
-  // barrier pair per tile before), and the next tile's input rows and
-  // top_db partial maxima are fetched into registers during this tile's
-  // block 2 and epilogue.  Block-1 row j is t1 = reflect(2*t20 - 1 + j) and
-  // reads x rows reflect(2*t1 - 1 + kt).
-  constexpr int XV = (NJ * 3 * 20 + NT - 1) / NT, WV = (32 * 9 * 64 / 8 + NT - 1) / NT;  // vectors per thread (Fin <= 80, C2 <= 32)
+  // Persistent workgroups (round 5): one per CU, each walks a contiguous run
+  // of tiles.  The per-tile constants — block-2 weights (37 KB) and LN
+  // affine, block-1 taps — load into LDS once per workgroup, and the next
+  // tile's input rows and top_db floor are staged by the four waves that
+  // have no epilogue row, while waves 0-7 run the epilogue.  Block-1 row j
+  // is t1 = reflect(2*t20 - 1 + j) and reads x rows reflect(2*t1 - 1 + kt).
+  constexpr int WV = (32 * 9 * 64 / 8 + NT - 1) / NT;  // weight vectors per thread (C2 <= 32)
+  constexpr int SNT = NT - 64 * TT2;                  // stager threads (waves TT2 ..)
+  constexpr int SXV = (NJ * 3 * 20 + SNT - 1) / SNT;  // x vectors per stager thread (Fin <= 80)
   const int fq4 = Fin / 4;        // Fin % 4 == 0, Fin <= 80 (host-checked)
   const float inv_fq4 = 1.0f / (float)fq4;
   // native vectors: the HIP float4 / uint4 structs (a union inside) held in
   // a register array are not always split into registers
   typedef float nf4 __attribute__((ext_vector_type(4)));
   typedef uint32_t nu4 __attribute__((ext_vector_type(4)));
-  nf4 xin[XV];
-  float smx = -INFINITY;  // this thread's top_db partial maximum (slot tid) of the tile's utterance
-  auto fetch = [&](int tl, int tid) __attribute__((always_inline)) {
+  __shared__ float redm[FE_NT / 64];  // top_db: the stager waves' partial maxima
+  // stager thread t (0 .. SNT-1): tile tl's input rows into xs (all loads in
+  // flight before the first store) and, for a tile that opens an utterance,
+  // the floor's partial maxima into redm
+  auto stage = [&](int tl, int t) __attribute__((always_inline)) {
     const int b = tl / nblk, t20 = (tl - b * nblk) * TT2;
     const float* xb = x + (long long)b * Tin * Fin;
+    nf4 v[SXV];
 #pragma unroll
-    for (int u = 0; u < XV; ++u) {
-      const int i = tid + u * NT;
+    for (int u = 0; u < SXV; ++u) {
+      const int i = min(t + u * SNT, NJ * 3 * fq4 - 1);
       const int q = (int)(((float)i + 0.5f) * inv_fq4);  // i / fq4 (exact: i < 2^11, fq4 <= 20)
-      const int jk = min(q, NJ * 3 - 1), f4 = i - q * fq4;
-      const int j = jk / 3, kt = jk - 3 * j;
+      const int f4 = i - q * fq4;
+      const int j = q / 3, kt = q - 3 * j;
       const int t1 = reflect_idx(2 * t20 - 1 + j, T1);
-      xin[u] = *reinterpret_cast<const nf4*>(xb + (long long)reflect_idx(2 * t1 - 1 + kt, Tin) * Fin + 4 * f4);
+      v[u] = *reinterpret_cast<const nf4*>(xb + (long long)reflect_idx(2 * t1 - 1 + kt, Tin) * Fin + 4 * f4);
     }
-    smx = -INFINITY;
-    if (slot_max && tid < nslot) smx = slot_max[(long long)b * nslot + tid];
+    if (slot_max && t20 == 0) {
+      float m = -INFINITY;
+      for (int i = t; i < nslot; i += SNT) m = fmaxf(m, slot_max[(long long)b * nslot + i]);
+      m = wave_max(m);
+      if (lane == 0) redm[w - TT2] = m;
+    }
+#pragma unroll
+    for (int u = 0; u < SXV; ++u)
+      if (t + u * SNT < NJ * 3 * fq4) *reinterpret_cast<nf4*>(xs + 4 * (t + u * SNT)) = v[u];
   };
-  fetch(tile, tid);
+  if (w >= TT2) {
+    stage(tile, tid - 64 * TT2);
+    // (a run's first tile may continue an utterance: its floor is needed too)
+    const int b0 = tile / nblk;
+    if (slot_max && tile != b0 * nblk) {
+      float m = -INFINITY;
+      for (int i = tid - 64 * TT2; i < nslot; i += SNT) m = fmaxf(m, slot_max[(long long)b0 * nslot + i]);
+      m = wave_max(m);
+      if (lane == 0) redm[w - TT2] = m;
+    }
+  }
   const int nwv = C2 * K / Tr::VEC;
   {
     nu4 wvin[WV];
@@ -590,9 +614,11 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
     return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));
   };
   const int fr = lane & 15, g4 = lane >> 4;
-  // A fragments (W^T rows c = 16 mt + fr, taps 4 g4 .. 4 g4 + 3, k >= 9
-  // zero) packed once by wave 0 into LDS with the bias; each tile re-reads
-  // them (held in VGPRs across the tile loop they pushed block 2 into spills)
+  // A fragments (W^T rows c = 16 mt + fr, taps 4 g4 .. 4 g4 + 3) packed once
+  // by wave 0 into LDS; each tile re-reads them (held in VGPRs across the
+  // tile loop they pushed block 2 into spills).  Tap 9 carries the bias
+  // against a B entry of 1.0, so the MFMA adds it (in bf16, as autocast's
+  // conv2d does) and no bias registers are needed; taps 10-15 are zero.
   if (w == 0) {
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
@@ -600,12 +626,14 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int k = 4 * g4 + e;
-        t4[e] = k < 9 ? w1[(16 * mt + fr) * 9 + min(k, 8)] : 0.f;
+        t4[e] = k < 9 ? w1[(16 * mt + fr) * 9 + min(k, 8)] : (k == 9 && b1 ? b1[16 * mt + fr] : 0.f);
       }
       wal[mt * 64 + lane] = uint2{pack2(f32x2{t4[0], t4[1]}), pack2(f32x2{t4[2], t4[3]})};
     }
-    b1s[lane] = b1 ? b1[lane] : 0.f;
   }
+  for (int i = tid; i < 2 * F2 * C2 / 4; i += NT)
+    reinterpret_cast<nf4*>(g2s)[i] = i < F2 * C2 / 4 ? reinterpret_cast<const nf4*>(g2)[i]
+                                                     : reinterpret_cast<const nf4*>(be2)[i - F2 * C2 / 4];
   // Block 1, work split: wave w takes frequency tile nt = w % 3 of the rows
   // j = w / 3 + 4 i (12 waves: 4 row groups x 3 tiles), all four channel
   // tiles, which share each gathered B fragment.  The LN affine of the
@@ -615,7 +643,6 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
   static_assert(NW == 12, "block 1: 4 row groups x 3 frequency tiles");
   constexpr int RG = 4, RPW = (NJ + RG - 1) / RG;  // rows per wave (5)
   __shared__ float lnred[2][NJ][4];                 // [pass][row][tile] partial sums
-  __shared__ float redm[FE_NT / 64];                // top_db: per-wave maxima
   const int nt = w % 3, grp = w / 3;
   const float inv_n1 = 1.0f / (float)(F1 * C1);
   // block 2 (tile-invariant part): rows m = t2_local * F2 + f2, columns the C2
@@ -627,6 +654,7 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
   const int nch = nout / 8;
   constexpr int NCH = (32 * 32 / 8 + 63) / 64;  // epilogue chunks per lane (F2, C2 <= 32)
 
+  __syncthreads();  // wl, wal, LN affine, the first tile's xs and floor staged
   float floor_db = -INFINITY;
   for (; tile < tend; ++tile) {
     const int b = tile / nblk, t20 = (tile - b * nblk) * TT2;
@@ -652,28 +680,17 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
       goff[e] = (k % 3) * Fin + reflect_idx(2 * f1c + k / 3 - 1, Fin);
     }
     const int fk = 8 * g4l;
+    const bool one9 = g4l == 2;  // this lane's B entry e = 1 is tap 9: the bias's 1.0
 
-    // the Fbank's top_db floor (features.py:706-711), max over the
-    // utterance's spectrum-kernel partial maxima - top_db, applied at the
-    // block-1 gathers (the separate clamp pass over the features is gone)
-    // (once per utterance: the floor stays in a register across its tiles)
+    // the Fbank's top_db floor (features.py:706-711): max over the
+    // utterance's spectrum-kernel partial maxima - top_db, reduced by the
+    // stager waves when the utterance's first tile of this run was staged;
+    // applied at the block-1 gathers (the separate clamp pass is gone)
     const bool newutt = tile == tbeg || t20 == 0;
-    if (slot_max && newutt) {
-      float m = smx;
-      for (int i = tdl + NT; i < nslot; i += NT) m = fmaxf(m, slot_max[(long long)b * nslot + i]);
-      m = wave_max(m);
-      if (lane == 0) redm[w] = m;
-    }
-#pragma unroll
-    for (int u = 0; u < XV; ++u) {
-      const int i = tdl + u * NT;
-      if (i < NJ * 3 * fq4) *reinterpret_cast<nf4*>(xs + 4 * i) = xin[u];
-    }
-    __syncthreads();  // xs, redm (and, first tile, wl) staged
     if (slot_max && newutt) {
       float m = redm[0];
 #pragma unroll
-      for (int i = 1; i < FE_NT / 64; ++i) m = fmaxf(m, redm[i]);
+      for (int i = 1; i < FE_NT / 64 - TT2; ++i) m = fmaxf(m, redm[i]);
       floor_db = m - top_db;
     }
     FE_TL(1);
@@ -684,11 +701,9 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
       return r;
     };
     s16x4 wa[4];  // (after the barrier: wave 0 staged them before the first tile)
-    f32x4 bias4[4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       wa[mt] = __builtin_bit_cast(s16x4, wal[mt * 64 + ln]);
-      bias4[mt] = *reinterpret_cast<const f32x4*>(b1s + 16 * mt + 4 * g4l);
     }
     // the wave's LN affine (L2-resident; per tile, so it is not live through block 2)
     f32x4 gam[4], bet[4];
@@ -711,9 +726,10 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
       }
       const float* r = xs + (j * 3) * Fin;
       const s16x4 xb4 = __builtin_bit_cast(
-          s16x4, uint2{pack2(f32x2{flo(r[goff[0]]), flo(r[goff[1]])}), pack2(f32x2{flo(r[goff[2]]), flo(r[goff[3]])})});
+          s16x4, uint2{pack2(f32x2{flo(r[goff[0]]), one9 ? 1.f : flo(r[goff[1]])}),
+                       pack2(f32x2{flo(r[goff[2]]), flo(r[goff[3]])})});
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) acc[i][mt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wa[mt], xb4, bias4[mt], 0, 0, 0);
+      for (int mt = 0; mt < 4; ++mt) acc[i][mt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wa[mt], xb4, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     }
     // LayerNorm statistics of each row over its F1 x C1 values in one pass:
     // the tile waves' sums and sums of squares combine through LDS behind one
@@ -839,31 +855,16 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
             if (full || mb + 16 * tm + r < Mv) yw0[(16 * tm + r) * C2 + 16 * tn] = acc2[tm][tn][r] + cb[tn];
         }
     }
-    // the epilogue's LN affine (its latency hides behind the barrier wait)
-    // (unconditional: values left undefined on some waves become loop-carried
-    // registers)
-    float4 g2v[NCH][2], b2v[NCH][2];
-#pragma unroll
-    for (int u = 0; u < NCH; ++u) {
-      const int c = min(ln + 64 * u, nch - 1);
-      const float4* gp = reinterpret_cast<const float4*>(g2 + 8 * c);
-      const float4* bp = reinterpret_cast<const float4*>(be2 + 8 * c);
-      g2v[u][0] = gp[0];
-      g2v[u][1] = gp[1];
-      b2v[u][0] = bp[0];
-      b2v[u][1] = bp[1];
-    }
-    // the next tile's inputs, in flight through the epilogue (issued before
-    // block 2 they were spilled: its fragments need the registers)
-    if (tile + 1 < tend) fetch(tile + 1, tdl);
     FE_TL(12);
     __syncthreads();  // yv complete; block 2 done with b1r
     if (w >= TT2) {
-      // waves idle in the epilogue carry block-1 row 16 into row 0 for a
-      // continuing next tile (its row 0 is this tile's row 16)
+      // the waves without an epilogue row: carry block-1 row 16 into row 0
+      // for a continuing next tile (its row 0 is this tile's row 16), and
+      // stage the next tile's input rows (b1r rows 1 .. 3) and floor
       const int nv = F1 * C1P * (int)sizeof(T) / 16;
-      for (int v = tdl - 64 * TT2; v < nv; v += NT - 64 * TT2)
+      for (int v = tdl - 64 * TT2; v < nv; v += SNT)
         reinterpret_cast<nu4*>(b1r)[v] = reinterpret_cast<const nu4*>(b1r + (NJ - 1) * F1 * C1P)[v];
+      if (tile + 1 < tend) stage(tile + 1, tdl - 64 * TT2);
     }
     if (w < nrow) {
       const int t2 = t20 + w;
@@ -901,7 +902,12 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
       for (int u = 0; u < NCH; ++u) {
         const int c = ln + 64 * u;
         if (c >= nch) continue;
-        const float4 ga = g2v[u][0], gb = g2v[u][1], ba = b2v[u][0], bb = b2v[u][1];
+        // the LN affine from LDS (staged once; in registers it pushed the
+        // prefetched rows into scratch)
+        const float4 ga = *reinterpret_cast<const float4*>(g2s + 8 * c);
+        const float4 gb = *reinterpret_cast<const float4*>(g2s + 8 * c + 4);
+        const float4 ba = *reinterpret_cast<const float4*>(be2s + 8 * c);
+        const float4 bb = *reinterpret_cast<const float4*>(be2s + 8 * c + 4);
         const float gg[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
         const float bt[8] = {ba.x, ba.y, ba.z, ba.w, bb.x, bb.y, bb.z, bb.w};
         float y[8];
@@ -923,7 +929,7 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
       }
     }
     FE_TL(13);
-    __syncthreads();  // yv read before the next tile's xs stores
+    __syncthreads();  // yv read; the next tile's xs, row 0 and floor staged
   }
   FE_TL(15);
 }
@@ -1094,9 +1100,11 @@ SBK_API int sbk_conv_frontend2(int dtype_bf16, const float* x, int B, int Tin, i
   constexpr int TT2 = FE_TT2, NJ = 2 * TT2 + 1;
   const size_t esz = dtype_bf16 ? 2 : 4;
   const size_t lds = (((size_t)C2 * (9 * C1 + 8) * esz + 15) & ~(size_t)15) +
-                     (size_t)std::max(TT2 * F2 * C2, (NJ * 3 * Fin + 3) & ~3) * 4 + (size_t)NJ * F1 * (C1 + 8) * esz +
-                     4 * 64 * 8 + C1 * 4;  // block-1 A fragments + bias
-  if (dtype_bf16 && lds > 160 * 1024 - 1024) return SBK_ERR_ARG;
+                     (size_t)TT2 * F2 * C2 * 4 + (size_t)NJ * F1 * (C1 + 8) * esz +
+                     4 * 64 * 8 + (size_t)2 * F2 * C2 * 4;  // block-1 A fragments, block-2 LN affine
+  if (dtype_bf16 && lds > 160 * 1024 - 640) return SBK_ERR_ARG;  // + 592 B of static LDS
+  // the block-1 input rows live in b1r rows 1 .. 15 (kernel)
+  if ((size_t)NJ * 3 * Fin * 4 > (size_t)(NJ - 2) * F1 * (C1 + 8) * esz) return SBK_ERR_ARG;
   // persistent: one workgroup per CU (the LDS allows no second), each
   // walking tiles blockIdx.x + k gridDim.x
   const int ntile = B * ((T2 + TT2 - 1) / TT2);
