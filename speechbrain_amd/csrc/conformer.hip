@@ -458,7 +458,9 @@ __global__ void __launch_bounds__(256) conv_block_mfma_kernel(const T* __restric
 // and VALU FMAs: 188 us; one row per wave on VALU FMAs: 130 us; one
 // workgroup per tile with per-tile weight staging: 74.6 us; block 2 with its
 // K loop split over wave pairs: +1k cycles per tile; a chunk-pair swizzle of
-// the block-1 rows: more LDS bank conflicts, not fewer.)
+// the block-1 rows: more LDS bank conflicts, not fewer; block 2 on four
+// waves beside the previous tile's epilogue on the other eight, yv in bf16
+// and double-buffered: 57.5 vs 56.3 us, profiles/r05ah_fe_overlap_ab_rejected.log.)
 // s_memtime marks of the waves of workgroup 100, its last tile (probe builds only)
 #define FE_TL(i) SBK_PROBE(if (blockIdx.x == 100 && lane == 0) g_fe_tl[w][i] = __builtin_amdgcn_s_memtime();)
 
