@@ -2,6 +2,7 @@
 conv front-end) and the drop-in modules vs the golden fixtures / CPU oracle.
 fp32 path: within 1e-4 of the reference; bf16 path: sanity bounds."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -206,6 +207,55 @@ def test_fused_frontend_vs_blockwise(dev, T, F):
             y16 = cnn.run(x, torch.bfloat16)
             r16 = b2.run(b1.run(x, torch.bfloat16), torch.bfloat16)
     assert_close(y16.float(), r16.float(), rtol=2e-2, name="frontend bf16")
+
+
+@pytest.mark.parametrize("B", [11, 32])
+def test_fused_frontend_tile_runs(dev, B):
+    """The persistent front-end kernel at batch sizes where a workgroup walks
+    a run of several tiles (B = 32: 1504 tiles on <= 256 workgroups; B = 11:
+    517, runs of 2-3 crossing utterance boundaries): the carried block-1 row,
+    the staged next-tile rows and the per-utterance top_db floor.  The floor
+    binds in every utterance (a near-silent stretch far below max - 80 dB;
+    one utterance 20 dB louder, so the floors differ): applying it on load
+    must equal running on the clamped features, bit for bit.  Against the
+    fp32 oracle (oracle/conformer.py conv_frontend) the error is bounded by
+    the oracle's own deviation under CPU bf16 autocast (every conv operand
+    rounded to bf16, as the reference runs under autocast), as in
+    test_gpu_bench_parity.py."""
+    import oracle.conformer as OC
+    from speechbrain_amd import ops
+    from speechbrain_amd.lobes.features import Fbank
+    from speechbrain_amd.lobes.models.convolution import ConvolutionFrontEnd
+    g = torch.Generator().manual_seed(B)
+    wav = 0.1 * torch.randn(B, 240000, generator=g)
+    wav[:, 40000:56000] *= 1e-6
+    wav[B // 2, :] *= 10.0
+    wav = wav.to(dev)
+    fb = Fbank(n_mels=80).to(dev)
+    raw, topdb = fb.forward_deferred(wav)
+    clamped = ops.topdb_clamp(raw, *topdb)
+    assert (raw < clamped).any()
+    torch.manual_seed(1)
+    cnn = ConvolutionFrontEnd(input_shape=(8, 10, 80), num_blocks=2, num_layers_per_block=1, out_channels=(64, 32),
+                              kernel_sizes=(3, 3), strides=(2, 2), residuals=(False, False)).to(dev).eval()
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        y = cnn.run(raw, torch.bfloat16, topdb=topdb)
+        y2 = cnn.run(clamped, torch.bfloat16)
+    assert torch.equal(y, y2), "the floor on load must equal the clamped input"
+    sd = {k: v.cpu() for k, v in cnn.state_dict().items()}
+    xin = clamped.float().cpu()
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    with torch.no_grad():
+        ref = OC.conv_frontend(xin, sd)
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            emu = OC.conv_frontend(xin, sd).float()
+    out = y.float().cpu()
+    assert out.shape == ref.shape
+    e_hip, e_emu = (out - ref).abs(), (emu - ref).abs()
+    print(f"\nfrontend B={B}: HIP vs fp32 oracle max {e_hip.max():.4e} mean {e_hip.mean():.4e}; "
+          f"bf16-operand oracle max {e_emu.max():.4e} mean {e_emu.mean():.4e}")
+    assert float(e_hip.max()) <= float(e_emu.max())
+    assert float(e_hip.mean()) <= float(e_emu.mean())
 
 
 # ----------------------------------------------------------------------------- modules vs golden
