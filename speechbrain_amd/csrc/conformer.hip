@@ -554,10 +554,9 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
   // stager thread t (0 .. SNT-1): tile tl's input rows into xs (all loads in
   // flight before the first store) and, for a tile that opens an utterance,
   // the floor's partial maxima into redm
-  auto stage = [&](int tl, int t) __attribute__((always_inline)) {
+  auto stage_load = [&](int tl, int t, nf4 (&v)[SXV]) __attribute__((always_inline)) {
     const int b = tl / nblk, t20 = (tl - b * nblk) * TT2;
     const float* xb = x + (long long)b * Tin * Fin;
-    nf4 v[SXV];
 #pragma unroll
     for (int u = 0; u < SXV; ++u) {
       const int i = min(t + u * SNT, NJ * 3 * fq4 - 1);
@@ -567,39 +566,63 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
       const int t1 = reflect_idx(2 * t20 - 1 + j, T1);
       v[u] = *reinterpret_cast<const nf4*>(xb + (long long)reflect_idx(2 * t1 - 1 + kt, Tin) * Fin + 4 * f4);
     }
-    if (slot_max && t20 == 0) {
-      float m = -INFINITY;
-      for (int i = t; i < nslot; i += SNT) m = fmaxf(m, slot_max[(long long)b * nslot + i]);
-      m = wave_max(m);
-      if (lane == 0) redm[w - TT2] = m;
-    }
+  };
+  // the floor's partial maxima of utterance b (stager thread t) into redm
+  auto floor_part = [&](int b, int t) __attribute__((always_inline)) {
+    float m = -INFINITY;
+    for (int i = t; i < nslot; i += SNT) m = fmaxf(m, slot_max[(long long)b * nslot + i]);
+    m = wave_max(m);
+    if (lane == 0) redm[w - TT2] = m;
+  };
+  auto stage_store = [&](int t, const nf4 (&v)[SXV]) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < SXV; ++u)
       if (t + u * SNT < NJ * 3 * fq4) *reinterpret_cast<nf4*>(xs + 4 * (t + u * SNT)) = v[u];
   };
-  if (w >= TT2) {
-    stage(tile, tid - 64 * TT2);
-    // (a run's first tile may continue an utterance: its floor is needed too)
-    const int b0 = tile / nblk;
-    if (slot_max && tile != b0 * nblk) {
-      float m = -INFINITY;
-      for (int i = tid - 64 * TT2; i < nslot; i += SNT) m = fmaxf(m, slot_max[(long long)b0 * nslot + i]);
-      m = wave_max(m);
-      if (lane == 0) redm[w - TT2] = m;
-    }
-  }
+  // the next tile's rows and, if it opens an utterance, its floor
+  auto stage = [&](int tl, int t) __attribute__((always_inline)) {
+    nf4 v[SXV];
+    stage_load(tl, t, v);
+    const int b = tl / nblk;
+    if (slot_max && tl == b * nblk) floor_part(b, t);
+    stage_store(t, v);
+  };
+  // prologue: every global load is issued before the first LDS store (one
+  // memory latency at the launch's start, not four in a row)
   const int nwv = C2 * K / Tr::VEC;
-  {
-    nu4 wvin[WV];
-    static_for<WV>([&](auto U) { wvin[U] = reinterpret_cast<const nu4*>(wp2)[min(tid + U * NT, nwv - 1)]; });
-    static_for<WV>([&](auto U) {
-      const int i = tid + U * NT;
-      if (i < nwv) {
-        const int co = (i * Tr::VEC) / K, kk = i * Tr::VEC - co * K;
-        *reinterpret_cast<nu4*>(wl + co * KP + kk) = wvin[U];
+  nu4 wvin[WV];
+  static_for<WV>([&](auto U) { wvin[U] = reinterpret_cast<const nu4*>(wp2)[min(tid + U * NT, nwv - 1)]; });
+  const int ngv = 2 * F2 * C2 / 4;  // block-2 LN affine vectors (<= 320 <= NT)
+  const nf4 gin = tid < ngv ? (tid < ngv / 2 ? reinterpret_cast<const nf4*>(g2)[tid]
+                                             : reinterpret_cast<const nf4*>(be2)[tid - ngv / 2])
+                            : nf4{0.f, 0.f, 0.f, 0.f};
+  // block-1 A fragments (W^T rows c = 16 mt + fr, taps 4 g4 .. 4 g4 + 3),
+  // packed and stored by wave 0 below
+  float tw[4][4];
+  if (w == 0) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = 4 * (lane >> 4) + e, c = 16 * mt + (lane & 15);
+        tw[mt][e] = k < 9 ? w1[c * 9 + min(k, 8)] : (k == 9 && b1 ? b1[c] : 0.f);
       }
-    });
   }
+  nf4 xv0[SXV];
+  if (w >= TT2) {
+    stage_load(tile, tid - 64 * TT2, xv0);
+    // the run's first tile's floor (it may continue an utterance)
+    if (slot_max) floor_part(tile / nblk, tid - 64 * TT2);
+  }
+  static_for<WV>([&](auto U) {
+    const int i = tid + U * NT;
+    if (i < nwv) {
+      const int co = (i * Tr::VEC) / K, kk = i * Tr::VEC - co * K;
+      *reinterpret_cast<nu4*>(wl + co * KP + kk) = wvin[U];
+    }
+  });
+  if (tid < ngv) reinterpret_cast<nf4*>(g2s)[tid] = gin;
+  if (w >= TT2) stage_store(tid - 64 * TT2, xv0);
   // block 1 on MFMA: the 3x3 / stride-2 convolution of a row is
   // C^T[c][f1] = W^T[c][tap] · X^T[tap][f1] with the 9 taps zero-padded to
   // one 16-deep bf16 step (v_mfma_f32_16x16x16_bf16; conv inputs and taps in
@@ -623,19 +646,9 @@ __global__ void __launch_bounds__(FE_NT) frontend2_kernel(const float* __restric
   // conv2d does) and no bias registers are needed; taps 10-15 are zero.
   if (w == 0) {
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      float t4[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int k = 4 * g4 + e;
-        t4[e] = k < 9 ? w1[(16 * mt + fr) * 9 + min(k, 8)] : (k == 9 && b1 ? b1[16 * mt + fr] : 0.f);
-      }
-      wal[mt * 64 + lane] = uint2{pack2(f32x2{t4[0], t4[1]}), pack2(f32x2{t4[2], t4[3]})};
-    }
+    for (int mt = 0; mt < 4; ++mt)
+      wal[mt * 64 + lane] = uint2{pack2(f32x2{tw[mt][0], tw[mt][1]}), pack2(f32x2{tw[mt][2], tw[mt][3]})};
   }
-  for (int i = tid; i < 2 * F2 * C2 / 4; i += NT)
-    reinterpret_cast<nf4*>(g2s)[i] = i < F2 * C2 / 4 ? reinterpret_cast<const nf4*>(g2)[i]
-                                                     : reinterpret_cast<const nf4*>(be2)[i - F2 * C2 / 4];
   // Block 1, work split: wave w takes frequency tile nt = w % 3 of the rows
   // j = w / 3 + 4 i (12 waves: 4 row groups x 3 tiles), all four channel
   // tiles, which share each gathered B fragment.  The LN affine of the
