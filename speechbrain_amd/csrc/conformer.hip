@@ -460,7 +460,11 @@ __global__ void __launch_bounds__(256) conv_block_mfma_kernel(const T* __restric
 // K loop split over wave pairs: +1k cycles per tile; a chunk-pair swizzle of
 // the block-1 rows: more LDS bank conflicts, not fewer; block 2 on four
 // waves beside the previous tile's epilogue on the other eight, yv in bf16
-// and double-buffered: 57.5 vs 56.3 us, profiles/r05ah_fe_overlap_ab_rejected.log.)
+// and double-buffered: 57.5 vs 56.3 us, profiles/r05ah_fe_overlap_ab_rejected.log;
+// frequency tile 2 packed two rows per MFMA (its 8 live frequencies of 16,
+// 3 row steps instead of 5, segmented 8-lane statistics): 57.5 vs 55.3 us,
+// profiles/r05al_fe_pack_ab_rejected.log — the per-lane row indexing costs
+// every wave more than the masked columns did.)
 // s_memtime marks of the waves of workgroup 100, its last tile (probe builds only)
 #define FE_TL(i) SBK_PROBE(if (blockIdx.x == 100 && lane == 0) g_fe_tl[w][i] = __builtin_amdgcn_s_memtime();)
 
