@@ -451,7 +451,8 @@ __global__ void __launch_bounds__(256) conv_block_mfma_kernel(const T* __restric
 // Persistent (round 5): one 768-thread workgroup per CU walks a contiguous
 // run of tiles with the block-2 weights resident in LDS; a tile continuing
 // the previous one reuses its last block-1 row as row 0 (16 rows computed,
-// not 17), and the next tile's input rows are fetched during the epilogue.
+// not 17), and the next tile's input rows are staged into block-1 rows 1-3
+// by the four waves that have no epilogue row.
 //   x (B, Tin, Fin) fp32; w1 (C1, 3, 3) fp32 in conv_block_c1's tap order;
 //   wp2 (C2, 3 time, 3 freq, C1) T; out (B, T2, F2*C2).
 // (Tried: two rows per pass over all 10 waves with cross-wave LN reductions
