@@ -209,11 +209,13 @@ def test_fused_frontend_vs_blockwise(dev, T, F):
     assert_close(y16.float(), r16.float(), rtol=2e-2, name="frontend bf16")
 
 
-@pytest.mark.parametrize("B", [11, 32])
-def test_fused_frontend_tile_runs(dev, B):
+@pytest.mark.parametrize("B,S", [(11, 240000), (32, 240000), (16, 224000)])
+def test_fused_frontend_tile_runs(dev, B, S):
     """The persistent front-end kernel at batch sizes where a workgroup walks
     a run of several tiles (B = 32: 1504 tiles on <= 256 workgroups; B = 11:
-    517, runs of 2-3 crossing utterance boundaries): the carried block-1 row,
+    517, runs of 2-3 crossing utterance boundaries; B = 16 at 14 s: 351
+    output rows per utterance, so every utterance ends in a 7-row tile inside
+    a run): the carried block-1 row,
     the staged next-tile rows and the per-utterance top_db floor.  The floor
     binds in every utterance (a near-silent stretch far below max - 80 dB;
     one utterance 20 dB louder, so the floors differ): applying it on load
@@ -227,7 +229,7 @@ def test_fused_frontend_tile_runs(dev, B):
     from speechbrain_amd.lobes.features import Fbank
     from speechbrain_amd.lobes.models.convolution import ConvolutionFrontEnd
     g = torch.Generator().manual_seed(B)
-    wav = 0.1 * torch.randn(B, 240000, generator=g)
+    wav = 0.1 * torch.randn(B, S, generator=g)
     wav[:, 40000:56000] *= 1e-6
     wav[B // 2, :] *= 10.0
     wav = wav.to(dev)
