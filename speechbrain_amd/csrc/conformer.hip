@@ -465,7 +465,10 @@ __global__ void __launch_bounds__(256) conv_block_mfma_kernel(const T* __restric
 // frequency tile 2 packed two rows per MFMA (its 8 live frequencies of 16,
 // 3 row steps instead of 5, segmented 8-lane statistics): 57.5 vs 55.3 us,
 // profiles/r05al_fe_pack_ab_rejected.log — the per-lane row indexing costs
-// every wave more than the masked columns did.)
+// every wave more than the masked columns did; an XOR bank swizzle of the
+// block-2 output rows (its stores are 4-way conflicted): 57.2 vs 55.6 us,
+// profiles/r05at_fe_yv_swizzle_ab_rejected.log — the extra index math and
+// two spilled VGPRs cost more than the conflicts.)
 // s_memtime marks of the waves of workgroup 100, its last tile (probe builds only)
 #define FE_TL(i) SBK_PROBE(if (blockIdx.x == 100 && lane == 0) g_fe_tl[w][i] = __builtin_amdgcn_s_memtime();)
 
