@@ -117,6 +117,18 @@ struct IntC {
 constexpr int FFN_BM = 48;
 constexpr int FFN_PAD = 16;  // LDS row pad (elements): conflict-free b128 reads (8 measured slower)
 constexpr int FFN_NW = 8, FFN_NT = FFN_NW * 64;  // 8 waves: LN'd rows fit in VGPRs (2 waves/SIMD)
+// Xn / Hs rows: element (row, col) at row * stride + (col ^ ffn_sw(row)), the
+// 16-B chunks of rows with bit 2 set swapped in pairs.  The 8-B column stores
+// (16 rows fr of one column per ds_write_b64 lane group: MI355X_MICROARCH
+// §LDS) were 4-way conflicted at the 544-B pitch — rows fr, fr + 4, fr + 8,
+// fr + 12 on one bank pair — and are 2-way with it, the floor for 16-B-aligned
+// rows; the b128 fragment reads stay conflict-free.  Counted: 720 of the 942
+// conflict cycles per wave (SQ_LDS_BANK_CONFLICT, profiles/r04t_chain_sq_counters.txt).
+__device__ __forceinline__ constexpr int ffn_sw(int row) { return ((row >> 2) & 1) << 3; }
+// row-reduction scratch stride (floats): 16-B-aligned rows whose partial
+// stores (16 lanes, rows fr) are 2-way and whose b128 reads are conflict-free
+// (a stride of NW = 8 made them 4-way and 2-way: 66 conflict cycles per LayerNorm)
+constexpr int FFN_RS = 12;
 
 #define FFN_MFMA(A, B, C) __builtin_amdgcn_mfma_f32_16x16x32_bf16((A), (B), (C), 0, 0, 0)
 
@@ -196,7 +208,7 @@ __device__ __forceinline__ void vm_wait(int n) {
 
 // Full-row LayerNorm of the epilogue values z (in place).  Lane (w, g, fr)
 // holds rows mt*16 + fr, units (w*T2 + j)*16 + 4g + e; row statistics are
-// reduced over g by shuffles and over the NW waves through red[BM][NW]; gam /
+// reduced over g by shuffles and over the NW waves through red[BM][FFN_RS]; gam /
 // bet are LDS copies.  Every LDS access is explicit (asm) and the barriers
 // wait on LDS only, so the weight tiles and stores in flight stay in flight.
 // (One barrier per pass with a buffer per pass measured 1.5 us slower per
@@ -224,14 +236,14 @@ __device__ __forceinline__ void row_ln(float (&z)[T2][MT][4], float* red, const 
     lds_barrier();  // the previous readers of red are done
     if (g == 0) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) lds_st1(red + (mt * 16 + fr) * NW + w, part[mt]);
+      for (int mt = 0; mt < MT; ++mt) lds_st1(red + (mt * 16 + fr) * FFN_RS + w, part[mt]);
     }
     lds_barrier();
     f32x4 rv[MT][2];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      rv[mt][0] = lds_f4(red + (mt * 16 + fr) * NW);
-      rv[mt][1] = lds_f4(red + (mt * 16 + fr) * NW + 4);
+      rv[mt][0] = lds_f4(red + (mt * 16 + fr) * FFN_RS);
+      rv[mt][1] = lds_f4(red + (mt * 16 + fr) * FFN_RS + 4);
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -310,15 +322,15 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
   bf16_t* Xn = ring + NB * TROWS * BK;                      // BM x XS
   bf16_t* Hs = Xn + BM * XS;                                // 2 x BM x HS
   float* b1s = reinterpret_cast<float*>(Hs + 2 * BM * HS);  // H (CHAIN: 2 H, block A then B)
-  float* red = b1s + (CHAIN ? 2 : 1) * a.H;                 // BM x NW row partials
+  float* red = b1s + (CHAIN ? 2 : 1) * a.H;                 // BM x FFN_RS row partials
   // epilogue vectors, copied to LDS in the prologue so that no global load
   // (and its in-order vmcnt wait behind the weight tiles) sits between blocks
-  float* prm = red + BM * NW;                               // P_* x D
+  float* prm = red + BM * FFN_RS;                           // P_* x D
   enum { P_B2 = 0, P_GP, P_BP, P_G0B, P_B0B, P_B2B, P_GN, P_BN, P_N };
   static_assert(P_N == NW, "one parameter row per wave");
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int fr = lane & 15, g = lane >> 4, fk = 8 * g;
+  const int fr = lane & 15, g = lane >> 4, fk = (8 * g) ^ ffn_sw(fr);  // chunk g of the swizzled rows mt*16 + fr
   const int m0 = blockIdx.x * BM;
   const int NCH = a.H / HC;
   const int S = NCH * SPC;                              // K-steps of one FFN block
@@ -409,7 +421,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     uint2 pk;
     pk.x = pack_bf16x2((v[0] - mean) * rstd * g04[0] + b04[0], (v[1] - mean) * rstd * g04[1] + b04[1]);
     pk.y = pack_bf16x2((v[2] - mean) * rstd * g04[2] + b04[2], (v[3] - mean) * rstd * g04[3] + b04[3]);
-    lds_st2(Xn + rr * XS + lane * PER, pk);
+    lds_st2(Xn + rr * XS + ((lane * PER) ^ ffn_sw(w)), pk);  // rr = w + i * NW, NW % 8 == 0
   }
   static_assert(2048 <= NT * 4, "b1 in one float4 per thread");
   if (psrc) lds_st4(prm + w * D + lane * PER, pv);
@@ -504,7 +516,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
         pk.x = pack_bf16x2(act_fn<ACT>(v[0] + bb[0], a.slope), act_fn<ACT>(v[1] + bb[1], a.slope));
         pk.y = pack_bf16x2(act_fn<ACT>(v[2] + bb[2], a.slope), act_fn<ACT>(v[3] + bb[3], a.slope));
         const unsigned long long pv = (unsigned long long)pk.x | ((unsigned long long)pk.y << 32);
-        asm volatile("ds_write_b64 %0, %1" ::"v"(lds_addr(Hn + (mt * 16 + fr) * HS + n)), "v"(pv) : "memory");
+        asm volatile("ds_write_b64 %0, %1" ::"v"(lds_addr(Hn + (mt * 16 + fr) * HS + (n ^ ffn_sw(fr)))), "v"(pv) : "memory");
         acc1[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
@@ -549,7 +561,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
         uint2 pk;
         pk.x = pack_bf16x2(z[j][mt][0], z[j][mt][1]);
         pk.y = pack_bf16x2(z[j][mt][2], z[j][mt][3]);
-        lds_st2(Xn + (mt * 16 + fr) * XS + d, pk);
+        lds_st2(Xn + (mt * 16 + fr) * XS + (d ^ ffn_sw(fr)), pk);
       }
     }
     lds_barrier();
@@ -620,7 +632,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
         uint2 pk;
         pk.x = pack_bf16x2(z[j][mt][0], z[j][mt][1]);
         pk.y = pack_bf16x2(z[j][mt][2], z[j][mt][3]);
-        lds_st2(Xn + (mt * 16 + fr) * XS + d, pk);
+        lds_st2(Xn + (mt * 16 + fr) * XS + (d ^ ffn_sw(fr)), pk);
       }
     }
     lds_barrier();
@@ -778,15 +790,17 @@ size_t ffn_lds(int H, bool chain) {
   // the epilogue parameter rows
   return ((size_t)2 * 256 * 64 + (size_t)FFN_BM * (D + FFN_PAD) + (size_t)2 * FFN_BM * (256 + FFN_PAD)) *
              sizeof(bf16_t) +
-         (size_t)(chain ? 2 : 1) * H * 4 + (size_t)FFN_NW * FFN_BM * 4 + (size_t)FFN_NW * D * 4;
+         (size_t)(chain ? 2 : 1) * H * 4 + (size_t)FFN_RS * FFN_BM * 4 + (size_t)FFN_NW * D * 4;
 }
 
 template <int D, int ACT, bool PROJ, bool CHAIN>
 int launch_ffn_act(const FfnArgs& a, size_t lds, hipStream_t s) {
-  static bool attr = false;  // > 64 KB dynamic LDS: opt in once per kernel
+  // > 64 KB dynamic LDS: opt in once per kernel, to the whole 160 KB (the
+  // first call's size would not cover a later launch with a larger H)
+  static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ffn_kernel<D, ACT, PROJ, CHAIN>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
