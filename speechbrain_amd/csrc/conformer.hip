@@ -1143,8 +1143,11 @@ SBK_API int sbk_conv_frontend2(int dtype_bf16, const float* x, int B, int Tin, i
   if (!dtype_bf16) return SBK_ERR_ARG;  // fp32 path: the per-block kernels (LDS would not fit)
   auto launch = [&](auto kern, bool& attr) -> int {
     if (!attr) {
+      // the host-checked maximum once (160 KB less the static lnred / redm):
+      // lds depends on the shapes (F1, F2, C2), and the first call's size
+      // would not cover a later, larger one
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 640);
       if (e != hipSuccess) return (int)e;
       attr = true;
     }
