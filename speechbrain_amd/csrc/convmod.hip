@@ -66,6 +66,7 @@ constexpr int CM_S = CM_D + 16;    // LDS row stride (elements): conflict-free b
 // bank pair) and are 2-way with it — 2-way is the floor for 16-B-aligned
 // rows; the fragment reads stay conflict-free.
 __device__ __forceinline__ constexpr int cm_sw(int row) { return ((row >> 2) & 1) << 3; }
+static_assert(CM_NW % 8 == 0, "rows w + CM_NW * i share bit 2 with w (their swizzle is cm_sw(w))");
 
 struct ConvModArgs {
   const float* x;  // (B*T, D) fp32 residual stream

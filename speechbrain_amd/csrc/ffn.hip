@@ -125,6 +125,7 @@ constexpr int FFN_NW = 8, FFN_NT = FFN_NW * 64;  // 8 waves: LN'd rows fit in VG
 // rows; the b128 fragment reads stay conflict-free.  Counted: 720 of the 942
 // conflict cycles per wave (SQ_LDS_BANK_CONFLICT, profiles/r04t_chain_sq_counters.txt).
 __device__ __forceinline__ constexpr int ffn_sw(int row) { return ((row >> 2) & 1) << 3; }
+static_assert(FFN_NW % 8 == 0, "rows w + FFN_NW * i share bit 2 with w (their swizzle is ffn_sw(w))");
 // row-reduction scratch stride (floats): 16-B-aligned rows whose partial
 // stores (16 lanes, rows fr) are 2-way and whose b128 reads are conflict-free
 // (a stride of NW = 8 made them 4-way and 2-way: 66 conflict cycles per LayerNorm)
