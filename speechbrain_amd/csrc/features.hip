@@ -1156,7 +1156,8 @@ __global__ void __launch_bounds__(RF_NT, SBK_RF_MINW) spec_reg_kernel(SpecArgs a
   int* mstart = reinterpret_cast<int*>(wd + (MODE == MODE_FBANK ? a.M * RF_LW : 0));  // that aligned bin
   int* mlen_s = mstart + (MODE == MODE_FBANK ? a.M : 0);  // table stage only: mel_len, mel_off
   int* moff_s = mlen_s + (MODE == MODE_FBANK ? a.M : 0);
-  __shared__ int lmax_s;
+  __shared__ float lmax_w[RF_NW];  // table stage: per-wave max of (start & 3) + len
+  __shared__ int trip_s[8];        // 16-B chunks per mel trip (16 filters; M <= 128)
   const int tid = threadIdx.x, lane = tid & 63;
   SBK_PROBE(int tl_row = blockIdx.x * RF_NW + (tid >> 6); unsigned long long tl0 = __builtin_amdgcn_s_memtime();)
   const int w = tid >> 6;
@@ -1195,36 +1196,52 @@ __global__ void __launch_bounds__(RF_NT, SBK_RF_MINW) spec_reg_kernel(SpecArgs a
   for (int i = tid; i <= NC; i += RF_NT) t2[i] = a.tw2[i];
   int lw = 0;  // dense mel width (multiple of 4, <= RF_LW); 0 = a filter is wider (CSR loop from global)
   if constexpr (MODE == MODE_FBANK) {
-    if (tid == 0) lmax_s = 0;
-    __syncthreads();
-    // the CSR index arrays go to LDS on the way (the dense rows then need
-    // one dependent global round trip, not two)
-    for (int i = tid; i < a.M; i += RF_NT) {
-      const int st = a.mel_start[i], ln = a.mel_len[i];
-      atomicMax(&lmax_s, (st & 3) + ln);
-      mstart[i] = st;
-      mlen_s[i] = ln;
-      moff_s[i] = a.mel_off[i];
+    // Two global round trips, every load of each issued before its first use
+    // (the loops that did this one dependent load at a time — the dense rows,
+    // then 16 mel_start / mel_len pairs per trip from global — kept the first
+    // block of every workgroup in the table stage for ~20k cycles,
+    // profiles/r05am_fbank_timeline.log): the CSR arrays -> LDS with the
+    // dense width as per-wave maxima (M <= 128 < RF_NT: one filter per
+    // thread), then the dense rows' weights.
+    static_assert(RF_NT >= 128, "one CSR entry per thread");
+    {
+      const int i0 = min(tid, a.M - 1);
+      const int st = a.mel_start[i0], ln = a.mel_len[i0], of = a.mel_off[i0];
+      if (tid < a.M) {
+        mstart[tid] = st;
+        mlen_s[tid] = ln;
+        moff_s[tid] = of;
+      }
+      const float wm = wave_max(tid < a.M ? (float)((st & 3) + ln) : 0.f);
+      if (lane == 0) lmax_w[tid >> 6] = wm;
     }
     __syncthreads();
-    const int lm = lmax_s;
+    float lmf = lmax_w[0];
+#pragma unroll
+    for (int i = 1; i < RF_NW; ++i) lmf = fmaxf(lmf, lmax_w[i]);
+    const int lm = (int)lmf;
     lw = lm <= RF_LW ? (lm + 3) & ~3 : 0;
     if (lw) {
-      for (int i = tid; i < a.M * RF_LW; i += RF_NT) {
-        const int jm = i / RF_LW, c = i - jm * RF_LW, L = mlen_s[jm];
-        const int sh = mstart[jm] & 3;
-        wd[i] = c >= sh && c - sh < L ? a.mel_w[moff_s[jm] + c - sh] : 0.f;
+      constexpr int UW = (128 * RF_LW + RF_NT - 1) / RF_NT;  // dense-row elements per thread (M <= 128)
+      float wv[UW];
+#pragma unroll
+      for (int u = 0; u < UW; ++u) {  // unconditional loads (clamped index), selected after
+        const int i = min(tid + u * RF_NT, a.M * RF_LW - 1);
+        const int jm = i / RF_LW, c = i - jm * RF_LW, sh = mstart[jm] & 3;
+        const bool in = c >= sh && c - sh < mlen_s[jm];
+        const float v = a.mel_w[in ? moff_s[jm] + c - sh : 0];
+        wv[u] = in ? v : 0.f;
       }
-      __syncthreads();  // every read of mstart above is done
-      for (int i = tid; i < a.M; i += RF_NT) mstart[i] &= ~3;
+#pragma unroll
+      for (int u = 0; u < UW; ++u)
+        if (tid + u * RF_NT < a.M * RF_LW) wd[tid + u * RF_NT] = wv[u];
       // 16-B chunks per mel trip (filters 16 t .. 16 t + 15): the largest of
       // its filters' own counts, so a trip skips the trailing all-zero chunks
-      // of the dense rows (wave-uniform; mel_off's table slots are free now)
-      for (int t = tid; 16 * t < a.M; t += RF_NT) {
+      // of the dense rows (wave-uniform), from the LDS copies
+      if (tid < 8 && 16 * tid < a.M) {
         int c = 0;
-        for (int jm = 16 * t; jm < min(16 * t + 16, a.M); ++jm)
-          c = max(c, ((a.mel_start[jm] & 3) + a.mel_len[jm] + 3) >> 2);
-        moff_s[t] = c;
+        for (int jm = 16 * tid; jm < min(16 * tid + 16, a.M); ++jm) c = max(c, ((mstart[jm] & 3) + mlen_s[jm] + 3) >> 2);
+        trip_s[tid] = c;
       }
     }
   }
@@ -1378,7 +1395,7 @@ __global__ void __launch_bounds__(RF_NT, SBK_RF_MINW) spec_reg_kernel(SpecArgs a
       if (lw) {
         // dense rows from the filter's 16-B aligned first bin, zero weights
         // outside it: 16-B reads of P and weights, lw / 4 of each
-        const rf4* pf = reinterpret_cast<const rf4*>(P0 + f * (2 * RF_FS) + mstart[jm]);
+        const rf4* pf = reinterpret_cast<const rf4*>(P0 + f * (2 * RF_FS) + (mstart[jm] & ~3));
         const rf4* wq = reinterpret_cast<const rf4*>(wd + jm * RF_LW);
 #pragma unroll
         for (int c = 0; c < RF_LW / 4; ++c) {
@@ -1410,7 +1427,7 @@ __global__ void __launch_bounds__(RF_NT, SBK_RF_MINW) spec_reg_kernel(SpecArgs a
     // two filters per trip: their LDS round trips overlap
     // (chunk count per trip from the table stage)
     auto trip_ch = [&](int t) __attribute__((always_inline)) {
-      return lw ? __builtin_amdgcn_readfirstlane(moff_s[t]) : 0;
+      return lw ? __builtin_amdgcn_readfirstlane(trip_s[t]) : 0;
     };
     int jm = lane >> 3;
     for (; jm + 8 < a.M; jm += 16) {
