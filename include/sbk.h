@@ -111,7 +111,7 @@ int sbk_context_window(const float* x, float* y, int N, int T, int F, int left, 
  * scratch of max(2*N*ceil(T/4), 3*N*(F/4)) + 4 floats, 16-B aligned;
  * n_fcells = number of frequency-masked cells, or < 0 to count them on the
  * device from the mask table).  F % 4 == 0, F <= 1024 with 16-B aligned x,
- * |c - w| <= 253 and <= 32 masks of each kind runs in place with no copy (x read once, the
+ * |c - w| <= 381 and <= 32 masks of each kind runs in place with no copy (x read once, the
  * unmasked cells written once, the masked cells written after the means);
  * otherwise the warp goes through `tmp` (a copy of x) —
  * sbk_specaugment_needs_scratch says which. */

@@ -351,7 +351,19 @@ __global__ void __launch_bounds__(256) warp4_kernel(const float* __restrict__ x,
 #ifndef SBK_RL_JMAX
 #define SBK_RL_JMAX 2  // (probe builds vary the slab width: 2 measured 39.2-39.7 us, 4 41.3-41.4, 1 48.6-49.2 per call)
 #endif
-constexpr int RL_RING = 1024, RL_WR = 512, RL_HMAX = (RL_RING - RL_WR) / 2, RL_MAXM = 32, RL_JMAX = SBK_RL_JMAX;
+// Windows of 256 output rows in a 1024-row ring: 34.5-34.7 us per call at
+// config 2 against 36.1-36.3 for 512 / 1024 (shorter first-window exposure,
+// more windows to overlap; profiles/r05bh_sa_window_ab.log), with a halo of
+// (1024 - 256) / 2 = 384 rows, up from 256
+#ifndef SBK_RL_WR
+#define SBK_RL_WR 256
+#endif
+#ifndef SBK_RL_RING
+#define SBK_RL_RING 1024
+#endif
+constexpr int RL_WR = SBK_RL_WR, RL_RING = SBK_RL_RING, RL_HMAX = (RL_RING - RL_WR) / 2, RL_MAXM = 32,
+              RL_JMAX = SBK_RL_JMAX;
+static_assert((RL_RING & (RL_RING - 1)) == 0 && RL_WR < RL_RING && RL_WR * RL_JMAX % 256 == 0, "ring geometry");
 template <bool CUBIC, bool WARP, bool MEAN>
 __global__ void __launch_bounds__(256) roll4_kernel(float* __restrict__ x, int N, int T, int F, int J, int c, int w,
                                                     const int* __restrict__ fmask, int n_fmask,
@@ -413,7 +425,9 @@ __global__ void __launch_bounds__(256) roll4_kernel(float* __restrict__ x, int N
   RL_STASH(0, have);
   __syncthreads();
   for (int t0 = 0; t0 < T;) {
-    const int t1 = have >= T ? T : have - H;
+    // (max: with H > RL_WR the first windows stage rows but complete none —
+    // t1 must not fall below t0)
+    const int t1 = have >= T ? T : max(t0, have - H);
     const int nlo = have, nhi = min(T, have + RL_WR);
     RL_FETCH(nlo);  // in flight under this window's compute
     if (act) {
