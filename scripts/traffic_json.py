@@ -1,7 +1,10 @@
 """Turn a FETCH_SIZE/WRITE_SIZE counter CSV into profiles/pmc_traffic.json:
 HBM bytes per launch per kernel (FETCH_SIZE x 2: on gfx950 it reports half
 the bytes of wide streaming reads, MI355X_MICROARCH.md §HBM; both in KB).
+An existing <out.json> is updated, not replaced: one config's passes must not
+drop the other configs' kernels (the bench lines look them up by name).
     python scripts/traffic_json.py <fetch.csv> <write.csv> <out.json>"""
+import os
 import collections
 import csv
 import json
@@ -21,4 +24,9 @@ for k, d in acc.items():
         w = sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"]) * 1024
         out[k] = int(f + w)
         print(f"{k:60s} read {f / 1e6:9.2f} MB  write {w / 1e6:9.2f} MB")
-json.dump(out, open(sys.argv[3], "w"), indent=1, sort_keys=True)
+merged = {}
+if os.path.exists(sys.argv[3]):
+    with open(sys.argv[3]) as f:
+        merged = json.load(f)
+merged.update(out)
+json.dump(merged, open(sys.argv[3], "w"), indent=1, sort_keys=True)
