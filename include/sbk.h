@@ -377,7 +377,10 @@ long long sbk_relpos_attention_lds(int dtype_bf16, int T, int dh);
  * am[b*am_sb + h*am_sh + i*Lk + j].  out (B*Lq, ldo) in the input dtype;
  * probs (B, H, Lq, Lk) fp32, the softmax; with p_drop > 0 attn receives the
  * dropped probabilities (the reference's returned weights) and out = attn·V.
- * dh <= 256; Lk, Lq, P within one workgroup's LDS. */
+ * dh <= 256; Lk, Lq, P within one workgroup's LDS.  pk == NULL: plain scaled
+ * dot-product attention (the MultiheadAttention drop-in, attention.py:642-778;
+ * torch.nn.MultiheadAttention's core) — no positional term, pbu / pbv and
+ * ldp ignored, P only range-checked (>= Lk). */
 int sbk_relpos_xattn_fwd(int dtype_bf16, const void* q, int ldq, const void* k, int ldk, const void* v, int ldv,
                          const void* pk, int ldp, int P, const float* pbu, const float* pbv, const unsigned char* kpm,
                          const float* am, long long am_sb, long long am_sh, int B, int Lq, int Lk, int H, int dh,
@@ -387,7 +390,9 @@ int sbk_relpos_xattn_fwd(int dtype_bf16, const void* q, int ldq, const void* k, 
  * probs / seed: dq (B*Lq, H*dh), dk, dv (B*Lk, H*dh), dpk (P, H*dh) fp32;
  * workspace G (B*H*Lq*Lk) fp32 (score gradients), dqu / dqv (B*Lq, H*dh)
  * fp32 — the content and positional parts of dq, whose column sums are the
- * pos_bias_u / pos_bias_v gradients. */
+ * pos_bias_u / pos_bias_v gradients.  pk == NULL (the forward's no-position
+ * mode): the band passes are skipped, dq is written directly, and dqu / dqv /
+ * dpk / pbu / pbv may be NULL. */
 int sbk_relpos_xattn_bwd(int dtype_bf16, const void* q, int ldq, const void* k, int ldk, const void* v, int ldv,
                          const void* pk, int ldp, int P, const float* pbu, const float* pbv, const float* probs,
                          const void* dO, int lddo, int B, int Lq, int Lk, int H, int dh, float scale,

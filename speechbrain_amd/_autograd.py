@@ -415,18 +415,26 @@ class RelPosCrossAttnFn(Function):
     """RelPosMHAXL core with query != key/value and q_len != k_len
     (attention.py:554-639, rel_shift :468-483) on csrc/xattn.hip: q (B*Lq, d),
     k / v (B*Lk, d), pk (P, d) in the compute dtype; pbu / pbv the (dh, H)
-    parameters.  Returns (out (B*Lq, d), attention weights after dropout, no
-    grad).  Backward: sbk_relpos_xattn_bwd (score, query, key / value and band
-    passes) and the pos-bias column sums on sbk_rowsum."""
+    parameters.  pk = pbu = pbv = None: plain scaled dot-product attention
+    (the MultiheadAttention drop-in; no positional term computed or
+    differentiated).  Returns (out (B*Lq, d), attention weights after dropout,
+    no grad).  Backward: sbk_relpos_xattn_bwd (score, query, key / value and,
+    with a band, the band passes) and the pos-bias column sums on sbk_rowsum."""
 
     @staticmethod
     def forward(ctx, q, k, v, pk, pbu, pbv, kpm, am, B, Lq, Lk, H, dh, scale, mpf, p):
-        q, k, v, pk = _cont(q), _cont(k), _cont(v), _cont(pk)
+        q, k, v = _cont(q), _cont(k), _cont(v)
         seed = new_seed() if p > 0 else 0
-        u, vb = _cont(pbu.detach().float()), _cont(pbv.detach().float())
+        nopos = pk is None
+        if nopos:
+            u = vb = None
+        else:
+            pk = _cont(pk)
+            u, vb = _cont(pbu.detach().float()), _cont(pbv.detach().float())
         o, probs, attn = _enc.relpos_xattn(q, k, v, pk, u, vb, kpm, B, Lq, Lk, H, dh, scale, mpf, am, p, seed)
         ctx.save_for_backward(q, k, v, pk, u, vb, probs)
-        ctx.dims = (B, Lq, Lk, H, dh, scale, mpf, p, seed, tuple(pbu.shape), tuple(pbv.shape))
+        ctx.dims = (B, Lq, Lk, H, dh, scale, mpf, p, seed, None if nopos else tuple(pbu.shape),
+                    None if nopos else tuple(pbv.shape))
         ctx.mark_non_differentiable(attn)
         return o, attn
 
@@ -435,18 +443,23 @@ class RelPosCrossAttnFn(Function):
         q, k, v, pk, u, vb, probs = ctx.saved_tensors
         B, Lq, Lk, H, dh, scale, mpf, p, seed, ushape, vshape = ctx.dims
         d = H * dh
-        P = pk.shape[0]
+        nopos = pk is None
+        P = 2 * Lk - 1 if nopos else pk.shape[0]
         dt = q.dtype
         dev = q.device
         f32 = lambda *shape: torch.empty(*shape, device=dev, dtype=_f32)  # noqa: E731
-        G, dqu, dqv, dq = f32(B * H * Lq * Lk), f32(B * Lq, d), f32(B * Lq, d), f32(B * Lq, d)
-        dk, dv, dpk = f32(B * Lk, d), f32(B * Lk, d), f32(P, d)
+        G, dq, dk, dv = f32(B * H * Lq * Lk), f32(B * Lq, d), f32(B * Lk, d), f32(B * Lk, d)
+        dqu = dqv = dpk = None
+        if not nopos:
+            dqu, dqv, dpk = f32(B * Lq, d), f32(B * Lq, d), f32(P, d)
         do_c = _as(do, dt)
         check(lib().sbk_relpos_xattn_bwd(_bf(q), ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0),
-                                         ptr(pk), pk.stride(0), P, ptr(u), ptr(vb), ptr(probs), ptr(do_c),
-                                         do_c.stride(0), B, Lq, Lk, H, dh, float(scale), int(mpf), float(p), int(seed),
-                                         ptr(G), ptr(dqu), ptr(dqv), ptr(dq), ptr(dk), ptr(dv), ptr(dpk),
-                                         stream_of(q)), "sbk_relpos_xattn_bwd")
+                                         ptr(pk), 0 if nopos else pk.stride(0), P, ptr(u), ptr(vb), ptr(probs),
+                                         ptr(do_c), do_c.stride(0), B, Lq, Lk, H, dh, float(scale), int(mpf),
+                                         float(p), int(seed), ptr(G), ptr(dqu), ptr(dqv), ptr(dq), ptr(dk), ptr(dv),
+                                         ptr(dpk), stream_of(q)), "sbk_relpos_xattn_bwd")
+        if nopos:
+            return (_as(dq, dt), _as(dk, dt), _as(dv, dt), None, None, None) + (None,) * 10
         dpbu = rowsum(dqu).view(ushape)
         dpbv = rowsum(dqv).view(vshape)
         return (_as(dq, dt), _as(dk, dt), _as(dv, dt), _as(dpk, dt), dpbu, dpbv) + (None,) * 10

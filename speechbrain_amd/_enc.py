@@ -674,18 +674,19 @@ def relpos_attention(qkv, pk, pbu, pbv, kpm, B, T, H, dh, scale, need_probs=Fals
 
 
 @custom_op("sbk::relpos_xattn", mutates_args=())
-def _relpos_xattn_op(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, pk: torch.Tensor, pbu: torch.Tensor,
-                     pbv: torch.Tensor, kpm: Optional[torch.Tensor], am: Optional[torch.Tensor], am_sb: int,
-                     am_sh: int, B: int, Lq: int, Lk: int, H: int, dh: int, scale: float, mpf: bool, p: float,
-                     seed: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+def _relpos_xattn_op(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, pk: Optional[torch.Tensor],
+                     pbu: Optional[torch.Tensor], pbv: Optional[torch.Tensor], kpm: Optional[torch.Tensor],
+                     am: Optional[torch.Tensor], am_sb: int, am_sh: int, B: int, Lq: int, Lk: int, H: int, dh: int,
+                     scale: float, mpf: bool, p: float, seed: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     out = torch.empty(B * Lq, H * dh, device=q.device, dtype=q.dtype)
     probs = torch.empty(B, H, Lq, Lk, device=q.device, dtype=_f32)
     attn = torch.empty_like(probs) if p > 0 else probs.new_empty(0)
+    P = pk.shape[0] if pk is not None else 2 * Lk - 1
     rc = lib().sbk_relpos_xattn_fwd(int(_is_bf16(q)), ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0),
-                                    ptr(pk), pk.stride(0), pk.shape[0], ptr(pbu), ptr(pbv), ptr(kpm), ptr(am),
-                                    int(am_sb), int(am_sh), B, Lq, Lk, H, dh, float(scale), int(mpf), float(p),
-                                    int(seed), ptr(out), out.stride(0), ptr(probs), ptr(attn) if p > 0 else None,
-                                    stream_of(q))
+                                    ptr(pk), pk.stride(0) if pk is not None else 0, P, ptr(pbu), ptr(pbv), ptr(kpm),
+                                    ptr(am), int(am_sb), int(am_sh), B, Lq, Lk, H, dh, float(scale), int(mpf),
+                                    float(p), int(seed), ptr(out), out.stride(0), ptr(probs),
+                                    ptr(attn) if p > 0 else None, stream_of(q))
     check(rc, "sbk_relpos_xattn_fwd")
     return out, probs, attn
 
@@ -702,12 +703,13 @@ def relpos_xattn(q, k, v, pk, pbu, pbv, kpm, B, Lq, Lk, H, dh, scale, mask_pos_f
     """RelPosMHAXL core for query != key/value (sbk_relpos_xattn_fwd): q
     (B*Lq, d), k / v (B*Lk, d), pk (P, d) with P // 2 + 1 == Lk, unit
     column stride, bf16 or fp32 alike; pbu / pbv fp32 (H*dh); am:
-    attn_mask_arg(..., Lk=Lk) or None.  Returns (out (B*Lq, d) in q.dtype,
-    probs (B, H, Lq, Lk) fp32, attention weights after dropout)."""
-    for t in (q, k, v, pk):
+    attn_mask_arg(..., Lk=Lk) or None.  pk = pbu = pbv = None: plain scaled
+    dot-product attention (no positional term).  Returns (out (B*Lq, d) in
+    q.dtype, probs (B, H, Lq, Lk) fp32, attention weights after dropout)."""
+    for t in (q, k, v) + ((pk,) if pk is not None else ()):
         if t.stride(-1) != 1 or t.shape[-1] != H * dh or t.dtype != q.dtype:
             raise ValueError("relpos_xattn: q / k / v / pk must be (rows, H*dh), unit column stride, one dtype")
-    if pk.shape[0] // 2 + 1 != Lk:
+    if pk is not None and pk.shape[0] // 2 + 1 != Lk:
         raise ValueError(f"pos_embs has {pk.shape[0]} rows: rel_shift keeps {pk.shape[0] // 2 + 1} != k_len {Lk}")
     m, sb, sh = am if am is not None else (None, 0, 0)
     out, probs, attn = OPS.relpos_xattn(q, k, v, pk, pbu, pbv, kpm, m, int(sb), int(sh), int(B), int(Lq), int(Lk),

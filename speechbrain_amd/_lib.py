@@ -214,8 +214,10 @@ class _FastOp:
     eager steps such as config 2's feature ops and SpecAugment — while a
     traced call goes through the registered op, so the launch is recorded as
     a graph node, and so does a call of an op with a registered backward on
-    inputs that require grad (its autograd edge).  Attribute access
-    (register_fake, register_autograd, ...) reaches the op."""
+    inputs that require grad (its autograd edge).  An op with no registered
+    backward called on inputs that require grad (grad mode on, not traced)
+    raises at the call.  Attribute access (register_fake, register_autograd,
+    ...) reaches the op."""
 
     def __init__(self, opdef, mutates_args=()):
         import inspect
@@ -228,17 +230,20 @@ class _FastOp:
         self._mut = tuple((names.index(m), m) for m in mutates_args)
 
     def __call__(self, *args, **kw):
+        diff = (torch.is_grad_enabled()
+                and any(isinstance(t, torch.Tensor) and t.requires_grad for t in (*args, *kw.values())))
+        if diff and self._def._backward_fn is None and not torch.jit.is_tracing():
+            # no registered backward: fail here, naming the op, rather than
+            # at a later backward() far from the call
+            raise RuntimeError(f"sbk::{self._def._name} has no backward; an input requires grad — call it under "
+                               "torch.no_grad() or on detached tensors (the differentiable path is _autograd)")
         if (torch.compiler.is_compiling() or torch.jit.is_tracing()
                 or torch._C._get_dispatch_mode(torch._C._TorchDispatchModeKey.FAKE) is not None
                 or torch._C._len_torch_dispatch_stack() > 0 or torch._C._are_functorch_transforms_active()
-                or (torch.is_grad_enabled()
-                    and any(isinstance(t, torch.Tensor) and t.requires_grad for t in (*args, *kw.values())))):
-            # traced, under a dispatch mode / functorch transform, or a call
-            # on inputs that require grad: through the dispatcher (graph
-            # node, fake / mode handling, and the autograd edge — or, for an
-            # op with no registered backward, the dispatcher's "autograd not
-            # implemented" error instead of a silently non-differentiable
-            # result)
+                or diff):
+            # traced, under a dispatch mode / functorch transform, or a
+            # differentiable call: through the dispatcher (graph node, fake /
+            # mode handling, the autograd edge)
             if self._op is None:
                 self._op = getattr(torch.ops.sbk, self._def._name)
             return self._op(*args, **kw)

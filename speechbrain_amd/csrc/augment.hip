@@ -735,19 +735,11 @@ SBK_API int sbk_specaugment(float* x, int N, int T, int F, int c, int w, int war
     float* pp = use_mean ? partial : nullptr;
 #define SBK_ROLL(CU, WA, ME)                                                                                        \
   do {                                                                                                              \
-    /* > 64 KB of LDS with the static arrays: opt in once per device, for  */                                      \
-    /* the widest slab any call can take (RL_JMAX), so a later call with a */                                      \
-    /* wider J than the first one is covered                               */                                      \
-    static unsigned attr_devs = 0;                                                                                  \
-    int dev_ = 0;                                                                                                   \
-    if (hipGetDevice(&dev_) != hipSuccess) return SBK_ERR_ARG;                                                      \
-    if (dev_ >= 32 || !(attr_devs & (1u << dev_))) {                                                                \
-      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&roll4_kernel<CU, WA, ME>),           \
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,                          \
-                                               (int)((size_t)RL_RING * RL_JMAX * 16));                              \
-      if (e != hipSuccess) return (int)e;                                                                           \
-      if (dev_ < 32) attr_devs |= 1u << dev_;                                                                       \
-    }                                                                                                               \
+    /* > 64 KB of LDS with the static arrays: opted in per device, for the */                                      \
+    /* widest slab any call can take (RL_JMAX)                             */                                      \
+    if (hipError_t e = sbk::lds_optin(reinterpret_cast<const void*>(&roll4_kernel<CU, WA, ME>),                    \
+                                      (size_t)RL_RING * RL_JMAX * 16))                                              \
+      return (int)e;                                                                                                \
     hipLaunchKernelGGL((roll4_kernel<CU, WA, ME>), dim3(nblk), dim3(256), lds, s4, x, N, T, F, J, c, w, fmask,      \
                        n_fmask, tmask, n_tmask, pp);                                                                \
   } while (0)

@@ -1064,13 +1064,7 @@ SBK_API int sbk_layernorm_bwd(const float* x, const void* dy, int dy_bf16, int M
   const int grid = sbk_layernorm_bwd_blocks(M);
   if (D > 2560) {  // workgroup per row; dgamma / dbeta partials in LDS
     const size_t lds = (size_t)2 * D * sizeof(float);
-    static bool attr = false;
-    if (!attr) {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ln_bwd_row_kernel),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 16384 * (int)sizeof(float));
-      if (e != hipSuccess) return (int)e;
-      attr = true;
-    }
+    if (hipError_t e = sbk::lds_optin(reinterpret_cast<const void*>(&ln_bwd_row_kernel), lds)) return (int)e;
     ln_bwd_row_kernel<<<grid, 256, lds, s>>>(x, dy, dy_bf16, M, D, g, eps, dres, dx, part);
     SBK_CHECK_LAUNCH();
     return 0;

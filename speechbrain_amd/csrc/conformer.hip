@@ -1141,24 +1141,16 @@ SBK_API int sbk_conv_frontend2(int dtype_bf16, const float* x, int B, int Tin, i
   const dim3 grid(std::min(ntile, ncu));
   hipStream_t s = (hipStream_t)stream;
   if (!dtype_bf16) return SBK_ERR_ARG;  // fp32 path: the per-block kernels (LDS would not fit)
-  auto launch = [&](auto kern, bool& attr) -> int {
-    if (!attr) {
-      // the host-checked maximum once (160 KB less the static lnred / redm):
-      // lds depends on the shapes (F1, F2, C2), and the first call's size
-      // would not cover a later, larger one
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 640);
-      if (e != hipSuccess) return (int)e;
-      attr = true;
-    }
+  auto launch = [&](auto kern) -> int {
+    // lds depends on the shapes (F1, F2, C2): lds_optin raises the opt-in when a launch needs more
+    if (hipError_t e = sbk::lds_optin(reinterpret_cast<const void*>(kern), lds)) return (int)e;
     hipLaunchKernelGGL(kern, grid, dim3(FE_NT), lds, s, x, ntile, Tin, Fin, T1, F1, T2, F2, w1, b1, g1, be1, eps1, slope1,
                        reinterpret_cast<const bf16_t*>(wp2), C2, b2, g2, be2, eps2, slope2, out, out_bf16, slot_max,
                        nslot, top_db);
     return 0;
   };
-  static bool attr_max = false, attr_sel = false;
-  const int rc = slope1 <= 1.f && slope2 <= 1.f ? launch(&frontend2_kernel<bf16_t, 64, true>, attr_max)
-                               : launch(&frontend2_kernel<bf16_t, 64, false>, attr_sel);
+  const int rc = slope1 <= 1.f && slope2 <= 1.f ? launch(&frontend2_kernel<bf16_t, 64, true>)
+                               : launch(&frontend2_kernel<bf16_t, 64, false>);
   if (rc) return rc;
   SBK_CHECK_LAUNCH();
   return 0;

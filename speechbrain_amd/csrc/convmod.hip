@@ -674,15 +674,9 @@ SBK_API int sbk_conv_module_pre(const float* x, const void* o, const void* wo, c
   if (grid > 0x7fffffffLL) return SBK_ERR_ARG;
   constexpr size_t lds = conv_module_lds();
   static_assert(lds <= 160 * 1024, "LDS budget");
-  static bool attr = false;
-  if (!attr) {
-    for (const void* k : {reinterpret_cast<const void*>(&conv_module_kernel<false>),
-                          reinterpret_cast<const void*>(&conv_module_kernel<true>)}) {
-      hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (e != hipSuccess) return (int)e;
-    }
-    attr = true;
-  }
+  for (const void* k : {reinterpret_cast<const void*>(&conv_module_kernel<false>),
+                        reinterpret_cast<const void*>(&conv_module_kernel<true>)})
+    if (hipError_t e = sbk::lds_optin(k, lds)) return (int)e;
   if (o)
     hipLaunchKernelGGL(conv_module_kernel<true>, dim3((unsigned)grid), dim3(CM_NT), lds, (hipStream_t)stream, a);
   else

@@ -1509,7 +1509,7 @@ void launch_static_m(int nc, int rows, hipStream_t s, const SpecArgs& a) {
   }
 }
 
-void launch_spec(int mode, int nc, int rows, size_t lds, hipStream_t s, const SpecArgs& a, const FftPlan& plan) {
+int launch_spec(int mode, int nc, int rows, size_t lds, hipStream_t s, const SpecArgs& a, const FftPlan& plan) {
   if (use_reg(nc, mode, a.C, a.M)) {
     const int nwb = (a.T + 7) / 8;
     static int ncu = 0;
@@ -1521,15 +1521,11 @@ void launch_spec(int mode, int nc, int rows, size_t lds, hipStream_t s, const Sp
     }
     const dim3 grid(std::min(rows * ((nwb + RF_NW - 1) / RF_NW), SBK_RF_WGS_PER_CU * ncu));
     const size_t rl = reg_lds(mode, a.M);
-    static bool attr = false;  // > 64 KB of dynamic LDS: opt in once
-    if (!attr) {
-      for (const void* k : {reinterpret_cast<const void*>(&spec_reg_kernel<MODE_POWER, true>),
-                            reinterpret_cast<const void*>(&spec_reg_kernel<MODE_POWER, false>),
-                            reinterpret_cast<const void*>(&spec_reg_kernel<MODE_FBANK, true>),
-                            reinterpret_cast<const void*>(&spec_reg_kernel<MODE_FBANK, false>)})
-        (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024);
-      attr = true;
-    }
+    for (const void* k : {reinterpret_cast<const void*>(&spec_reg_kernel<MODE_POWER, true>),
+                          reinterpret_cast<const void*>(&spec_reg_kernel<MODE_POWER, false>),
+                          reinterpret_cast<const void*>(&spec_reg_kernel<MODE_FBANK, true>),
+                          reinterpret_cast<const void*>(&spec_reg_kernel<MODE_FBANK, false>)})
+      if (hipError_t e = sbk::lds_optin(k, rl)) return (int)e;  // > 64 KB of dynamic LDS
     const bool gp = a.power != 1.0f || (mode == MODE_POWER && a.log_mag);
     if (mode == MODE_POWER) {
       if (gp) hipLaunchKernelGGL((spec_reg_kernel<MODE_POWER, true>), grid, dim3(RF_NT), rl, s, a);
@@ -1538,19 +1534,20 @@ void launch_spec(int mode, int nc, int rows, size_t lds, hipStream_t s, const Sp
       if (gp) hipLaunchKernelGGL((spec_reg_kernel<MODE_FBANK, true>), grid, dim3(RF_NT), rl, s, a);
       else hipLaunchKernelGGL((spec_reg_kernel<MODE_FBANK, false>), grid, dim3(RF_NT), rl, s, a);
     }
-    return;
+    return 0;
   }
   const int snc = static_nc(nc, mode, a.onesided);
   if (snc) {
     if (mode == MODE_STFT) launch_static_m<MODE_STFT>(snc, rows, s, a);
     else if (mode == MODE_POWER) launch_static_m<MODE_POWER>(snc, rows, s, a);
     else launch_static_m<MODE_FBANK>(snc, rows, s, a);
-    return;
+    return 0;
   }
   const dim3 grid(rows * ((a.T + a.fpb - 1) / a.fpb));
   if (mode == MODE_STFT) hipLaunchKernelGGL(spec_kernel<MODE_STFT>, grid, dim3(256), lds, s, a, plan);
   else if (mode == MODE_POWER) hipLaunchKernelGGL(spec_kernel<MODE_POWER>, grid, dim3(256), lds, s, a, plan);
   else hipLaunchKernelGGL(spec_kernel<MODE_FBANK>, grid, dim3(256), lds, s, a, plan);
+  return 0;
 }
 
 inline int grid_for(long long n, int block) {
@@ -1648,7 +1645,9 @@ SBK_API int sbk_spectrum(int mode, const float* wav, int Bo, int S, int C, int n
   if (!fpb) return SBK_ERR_ARG;
   if (snc && static_lds_for(snc, mode, a.M, a.n_melw) > 64 * 1024) return SBK_ERR_ARG;
   a.fpb = fpb;
-  launch_spec(mode, n_fft / 2, a.Bfold, spec_lds(n_fft, a.M, a.n_melw, fpb), (hipStream_t)stream, a, plan);
+  if (int rc = launch_spec(mode, n_fft / 2, a.Bfold, spec_lds(n_fft, a.M, a.n_melw, fpb), (hipStream_t)stream, a,
+                           plan))
+    return rc;
   SBK_CHECK_LAUNCH();
   return 0;
 }

@@ -796,15 +796,9 @@ size_t ffn_lds(int H, bool chain) {
 
 template <int D, int ACT, bool PROJ, bool CHAIN>
 int launch_ffn_act(const FfnArgs& a, size_t lds, hipStream_t s) {
-  // > 64 KB dynamic LDS: opt in once per kernel, to the whole 160 KB (the
-  // first call's size would not cover a later launch with a larger H)
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ffn_kernel<D, ACT, PROJ, CHAIN>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return (int)e;
-    attr = true;
-  }
+  // > 64 KB dynamic LDS: opted in per device, raised when a launch (a larger H) needs more
+  if (hipError_t e = sbk::lds_optin(reinterpret_cast<const void*>(&ffn_kernel<D, ACT, PROJ, CHAIN>), lds))
+    return (int)e;
   hipLaunchKernelGGL((ffn_kernel<D, ACT, PROJ, CHAIN>), dim3((a.M + FFN_BM - 1) / FFN_BM), dim3(FFN_NT), lds, s, a);
   return 0;
 }

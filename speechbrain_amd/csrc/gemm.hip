@@ -428,15 +428,9 @@ int launch(const void* A, int lda, const void* W, int ldw, int M, int N, int K, 
   size_t lds = (size_t)NBUF * (BM + BN) * LDSR * sizeof(T);
   const size_t cbytes = (size_t)BM * (BN + 4) * 4;  // epilogue C tile
   if (cbytes > lds) lds = cbytes;
-  if (lds > 64 * 1024) {  // opt in once per instantiation
-    static bool attr = false;
-    if (!attr) {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_kernel<T, BM, BN, BK, NBUF>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (e != hipSuccess) return (int)e;
-      attr = true;
-    }
-  }
+  if (lds > 64 * 1024)
+    if (hipError_t e = sbk::lds_optin(reinterpret_cast<const void*>(&gemm_kernel<T, BM, BN, BK, NBUF>), lds))
+      return (int)e;
   const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   hipLaunchKernelGGL((gemm_kernel<T, BM, BN, BK, NBUF>), dim3(grid, 1, batch), dim3(256), lds, s,
                      reinterpret_cast<const T*>(A), lda, reinterpret_cast<const T*>(W), ldw, M, N, K, ep);
@@ -560,13 +554,7 @@ int launch_ring(const void* A, int lda, const void* W, int ldw, int M, int N, in
   size_t lds = (size_t)4 * (BM + BN) * 64 * sizeof(bf16_t);
   const size_t cbytes = (size_t)BM * (BN + 4) * 4;
   if (cbytes > lds) lds = cbytes;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_ring_kernel<BM, BN>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
-    attr = true;
-  }
+  if (hipError_t e = sbk::lds_optin(reinterpret_cast<const void*>(&gemm_ring_kernel<BM, BN>), lds)) return (int)e;
   const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   hipLaunchKernelGGL((gemm_ring_kernel<BM, BN>), dim3(grid), dim3(256), lds, s, reinterpret_cast<const bf16_t*>(A),
                      lda, reinterpret_cast<const bf16_t*>(W), ldw, M, N, K, ep);

@@ -441,13 +441,9 @@ __global__ void __launch_bounds__(NT, 1) gemm256_kernel(G256 p) {
 
 template <bool MX, int ACT, int OUT>
 int launch_t(const G256& p, hipStream_t s) {
-  static bool attr = false;  // > 64 KB of dynamic LDS: opt in once
-  if (!attr) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm256_kernel<MX, ACT, OUT>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<MX>());
-    if (e != hipSuccess) return (int)e;
-    attr = true;
-  }
+  // > 64 KB of dynamic LDS: opted in per device
+  if (hipError_t e = sbk::lds_optin(reinterpret_cast<const void*>(&gemm256_kernel<MX, ACT, OUT>), lds_bytes<MX>()))
+    return (int)e;
   const int grid = (p.N >> 8) * ((p.M + 255) >> 8);
   hipLaunchKernelGGL((gemm256_kernel<MX, ACT, OUT>), dim3(grid), dim3(NT), lds_bytes<MX>(), s, p);
   SBK_CHECK_LAUNCH();

@@ -5,6 +5,8 @@
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #define SBK_API extern "C" __attribute__((visibility("default")))
 
 #define SBK_CHECK_LAUNCH()                          \
@@ -34,6 +36,31 @@
 namespace sbk {
 
 constexpr int kWave = 64;
+
+// Opt a kernel into `bytes` of dynamic LDS (> 64 KB needs it) on the current
+// device.  hipFuncSetAttribute is per device, so the record is per (kernel,
+// device), and it keeps the largest size set so far: a later launch asking
+// for more sets the attribute again.  Thread-safe; host only.
+inline hipError_t lds_optin(const void* kern, size_t bytes) {
+  struct Entry {
+    const void* kern;
+    int dev;
+    size_t bytes;
+  };
+  static std::mutex mu;
+  static Entry table[512];
+  static int n = 0;
+  int dev = 0;
+  if (hipError_t e = hipGetDevice(&dev)) return e;
+  std::lock_guard<std::mutex> lock(mu);
+  int i = 0;
+  while (i < n && !(table[i].kern == kern && table[i].dev == dev)) ++i;
+  if (i < n && table[i].bytes >= bytes) return hipSuccess;
+  if (hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes)) return e;
+  if (i < n) table[i].bytes = bytes;
+  else if (n < 512) table[n++] = Entry{kern, dev, bytes};
+  return hipSuccess;
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

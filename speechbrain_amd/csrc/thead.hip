@@ -409,13 +409,7 @@ size_t thead_lds(int mode) {
 template <int MODE, int JK>
 int launch_thead_j(const TheadArgs& a, hipStream_t s) {
   const size_t lds = thead_lds(MODE);
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&thead_kernel<MODE, JK>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
-    attr = true;
-  }
+  if (hipError_t e = sbk::lds_optin(reinterpret_cast<const void*>(&thead_kernel<MODE, JK>), lds)) return (int)e;
   hipLaunchKernelGGL((thead_kernel<MODE, JK>), dim3((a.M + TH_BM - 1) / TH_BM), dim3(TH_NT), lds, s, a);
   SBK_CHECK_LAUNCH();
   return 0;
@@ -493,13 +487,7 @@ SBK_API int sbk_thead_wgrad(const void* ds, const float* tn, const float* pn, co
     return SBK_ERR_ARG;
   const size_t lds = (size_t)2 * WG_BK * WG_LD * 2 + (size_t)U1 * WG_BJ * 4;
   if (lds > 160 * 1024) return SBK_ERR_ARG;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&thead_wgrad_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return (int)e;
-    attr = true;
-  }
+  if (hipError_t e = sbk::lds_optin(reinterpret_cast<const void*>(&thead_wgrad_kernel), lds)) return (int)e;
   const int Vp = sbk_thead_vpad(V);
   hipLaunchKernelGGL(thead_wgrad_kernel, dim3(Vp / WG_BV, J / WG_BJ, B), dim3(256), lds, (hipStream_t)stream,
                      reinterpret_cast<const bf16_t*>(ds), Vp, tn, pn, Tl, T, U1, J, V, act, act_slope(act, slope), dw);

@@ -20,6 +20,11 @@
 // at columns [h*dh, (h+1)*dh), fp32 or bf16; pbu / pbv (H*dh) fp32 (the
 // (dh, H) parameters read as (H, dh), attention.py:586-592); probabilities
 // (B, H, Lq, Lk) fp32.
+//
+// pk == nullptr selects plain scaled dot-product attention (the
+// MultiheadAttention drop-in's general path, attention.py:642-778): no
+// positional term, no u / v biases (pbu / pbv may be null), and the backward
+// skips the band passes — dq comes straight out of the row pass.
 #include "sbk_common.h"
 
 #include <math.h>
@@ -99,7 +104,7 @@ __global__ __launch_bounds__(kThreads) void xattn_fwd_kernel(
   float* part = red + 64;    // 256
   const int i = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const TI* qrow = q + (long long)(b * Lq + i) * ldq + h * dh;
-  for (int d = threadIdx.x; d < dh; d += kThreads) qu[d] = ld(qrow, d) + pbu[h * dh + d];
+  for (int d = threadIdx.x; d < dh; d += kThreads) qu[d] = ld(qrow, d) + (pbu ? pbu[h * dh + d] : 0.f);
   __syncthreads();
   const float* am_row = am ? am + b * am_sb + h * am_sh + (long long)i * Lk : nullptr;
   float mx = -INFINITY;
@@ -107,9 +112,9 @@ __global__ __launch_bounds__(kThreads) void xattn_fwd_kernel(
     const TI* krow = k + (long long)(b * Lk + j) * ldk + h * dh;
     float ac = 0.f;
     for (int d = 0; d < dh; ++d) ac += qu[d] * ld(krow, d);
-    int r, c;
-    shift_src(i, j, Lq, P, mpf, r, c);
     float bd = 0.f;
+    int r = 0, c = -1;
+    if (pk) shift_src(i, j, Lq, P, mpf, r, c);
     if (c >= 0) {
       const TI* qr = q + (long long)(b * Lq + r) * ldq + h * dh;
       const TI* pr = pk + (long long)c * ldp + h * dh;
@@ -243,7 +248,7 @@ __global__ __launch_bounds__(kThreads) void xattn_bwd_kv_kernel(
   const long long o = (long long)(b * Lk + j) * H * dh + h * dh;
   // Σ_i G[i][j] (q_i + u) = Σ_i G[i][j] q_i + u Σ_i G[i][j]
   weighted_rows(gc, q + (long long)b * Lq * ldq + h * dh, ldq, Lq, dh, part,
-                [&](int d, float y) { dk[o + d] = y + pbu[h * dh + d] * gsum; });
+                [&](int d, float y) { dk[o + d] = y + (pbu ? pbu[h * dh + d] * gsum : 0.f); });
   weighted_rows(pc, dO + (long long)b * Lq * lddo + h * dh, lddo, Lq, dh, part,
                 [&](int d, float y) { dv[o + d] = y; });
 }
@@ -301,8 +306,7 @@ unsigned drop_thresh(float p) {
 template <typename K>
 int prep_lds(K kern, size_t lds) {
   if (lds > 160 * 1024) return SBK_ERR_ARG;
-  if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return SBK_ERR_ARG;
+  if (sbk::lds_optin((const void*)kern, lds) != hipSuccess) return SBK_ERR_ARG;
   return 0;
 }
 
@@ -342,10 +346,11 @@ int xattn_bwd(const void* q, int ldq, const void* k, int ldk, const void* v, int
     auto kern = xattn_bwd_rows_kernel<TI>;
     if (int rc = prep_lds(kern, lds)) return rc;
     hipLaunchKernelGGL(kern, dim3(Lq, H, B), dim3(kThreads), lds, st, (const TI*)k, ldk, (const TI*)v, ldv,
-                       (const TI*)dO, lddo, probs, Lq, Lk, H, dh, scale, thresh, inv_keep, seed, use_drop, G, dqu);
+                       (const TI*)dO, lddo, probs, Lq, Lk, H, dh, scale, thresh, inv_keep, seed, use_drop, G,
+                       pk ? dqu : dq);
     SBK_CHECK_LAUNCH();
   }
-  {
+  if (pk) {
     const size_t lds = (size_t)(P + 256) * sizeof(float);
     auto kern = xattn_bwd_qv_kernel<TI>;
     if (int rc = prep_lds(kern, lds)) return rc;
@@ -361,7 +366,7 @@ int xattn_bwd(const void* q, int ldq, const void* k, int ldk, const void* v, int
                        probs, G, Lq, Lk, H, dh, thresh, inv_keep, seed, use_drop, dk, dv);
     SBK_CHECK_LAUNCH();
   }
-  {
+  if (pk) {
     const size_t lds = (size_t)(Lq + 256 + 64) * sizeof(float);
     auto kern = xattn_bwd_pk_kernel<TI>;
     if (int rc = prep_lds(kern, lds)) return rc;
@@ -380,8 +385,8 @@ SBK_API int sbk_relpos_xattn_fwd(int dtype_bf16, const void* q, int ldq, const v
                                  int Lq, int Lk, int H, int dh, float scale, int mask_pos_future, float p_drop,
                                  unsigned long long seed, void* out, int ldo, float* probs, float* attn,
                                  void* stream) {
-  if (!q || !k || !v || !pk || !pbu || !pbv || !out || !probs || bad_dims(B, Lq, Lk, H, dh, P) || p_drop < 0.f ||
-      p_drop >= 1.f || ldq < H * dh || ldk < H * dh || ldv < H * dh || ldp < H * dh || ldo < H * dh)
+  if (!q || !k || !v || (pk && (!pbu || !pbv || ldp < H * dh)) || !out || !probs || bad_dims(B, Lq, Lk, H, dh, P) ||
+      p_drop < 0.f || p_drop >= 1.f || ldq < H * dh || ldk < H * dh || ldv < H * dh || ldo < H * dh)
     return SBK_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   return dtype_bf16 ? xattn_fwd<uint16_t>(q, ldq, k, ldk, v, ldv, pk, ldp, P, pbu, pbv, kpm, am, am_sb, am_sh, B, Lq,
@@ -395,9 +400,9 @@ SBK_API int sbk_relpos_xattn_bwd(int dtype_bf16, const void* q, int ldq, const v
                                  const float* probs, const void* dO, int lddo, int B, int Lq, int Lk, int H, int dh,
                                  float scale, int mask_pos_future, float p_drop, unsigned long long seed, float* G,
                                  float* dqu, float* dqv, float* dq, float* dk, float* dv, float* dpk, void* stream) {
-  if (!q || !k || !v || !pk || !pbu || !pbv || !probs || !dO || !G || !dqu || !dqv || !dq || !dk || !dv || !dpk ||
-      bad_dims(B, Lq, Lk, H, dh, P) || p_drop < 0.f || p_drop >= 1.f || ldq < H * dh || ldk < H * dh ||
-      ldv < H * dh || ldp < H * dh || lddo < H * dh)
+  if (!q || !k || !v || !probs || !dO || !G || !dq || !dk || !dv ||
+      (pk && (!pbu || !pbv || !dqu || !dqv || !dpk || ldp < H * dh)) || bad_dims(B, Lq, Lk, H, dh, P) ||
+      p_drop < 0.f || p_drop >= 1.f || ldq < H * dh || ldk < H * dh || ldv < H * dh || lddo < H * dh)
     return SBK_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   return dtype_bf16 ? xattn_bwd<uint16_t>(q, ldq, k, ldk, v, ldv, pk, ldp, P, pbu, pbv, probs, dO, lddo, B, Lq, Lk, H,

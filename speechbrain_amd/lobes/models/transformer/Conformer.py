@@ -30,7 +30,7 @@ import torch.nn as nn
 from .... import _autograd as A
 from .... import _enc
 from ....nnet.activations import Swish
-from ....nnet.attention import PositionalwiseFeedForward, RelPosMHAXL
+from ....nnet.attention import FUSED_DH_MAX, MultiheadAttention, PositionalwiseFeedForward, RelPosMHAXL
 from ....nnet.normalization import LayerNorm
 
 __all__ = ["ConvolutionModule", "ConformerEncoderLayer", "ConformerEncoder"]
@@ -173,9 +173,16 @@ class ConformerEncoderLayer(nn.Module):
     def __init__(self, d_model, d_ffn, nhead, kernel_size=31, kdim=None, vdim=None, activation=Swish, bias=True,
                  dropout=0.0, causal=False, attention_type="RelPosMHAXL"):
         super().__init__()
-        if attention_type != "RelPosMHAXL":
-            raise NotImplementedError("only RelPosMHAXL attention is on the accelerated Conformer path")
-        self.mha_layer = RelPosMHAXL(num_heads=nhead, embed_dim=d_model, dropout=dropout, mask_pos_future=causal)
+        if attention_type == "regularMHA":  # Conformer.py:173-180
+            self.mha_layer = MultiheadAttention(nhead=nhead, d_model=d_model, dropout=dropout, kdim=kdim, vdim=vdim)
+        elif attention_type == "RelPosMHAXL":  # :181-188
+            self.mha_layer = RelPosMHAXL(num_heads=nhead, embed_dim=d_model, dropout=dropout,
+                                         mask_pos_future=causal)
+        else:
+            raise ValueError(f"attention_type {attention_type!r}: 'regularMHA' or 'RelPosMHAXL'")
+        self.attention_type = attention_type
+        # the per-module layer (mha_layer_forward): regularMHA, or heads wider than the fused kernels take
+        self.module_layer = attention_type == "regularMHA" or d_model // nhead > FUSED_DH_MAX
         self.convolution_module = ConvolutionModule(d_model, kernel_size, bias, activation, dropout, causal=causal)
         self.ffn_module1 = nn.Sequential(
             nn.LayerNorm(d_model),
@@ -194,7 +201,7 @@ class ConformerEncoderLayer(nn.Module):
 
     def chainable(self, dtype, d):
         """Every block of this layer has its fused kernel (the chained stack)."""
-        if self.training and self.drop.p > 0:
+        if self.training and self.drop.p > 0 or self.module_layer:
             return False
         f1, f2 = self.ffn_module1, self.ffn_module2
         mha = self.mha_layer
@@ -280,6 +287,29 @@ class ConformerEncoderLayer(nn.Module):
         z = f2[1].train_run(u, dtype, residual=x, alpha=0.5, out_p=f2[2].p if tr else 0.0)
         return A.layer_norm(z, self.norm2.norm, out_dtype=_f32), attn
 
+    def mha_layer_forward(self, x, B, T, kpm_u8, src_mask, pos_embs, dtype):
+        """Conformer.py:239-260 block by block on the drop-in modules, for the
+        regularMHA attention (:173-180) and for heads wider than the fused
+        kernels take: x (B*T, d) fp32 → (x_out, attention).  The FFN,
+        LayerNorm and convolution-module blocks are the training path's HIP
+        autograd Functions (they run as plain kernels under no_grad); the
+        attention is the mha_layer drop-in on norm1's output —
+        MultiheadAttention's fused kernels at inference and its general path
+        (src_mask, pos_embs added to the mask as attention.py:756-761,
+        dropout, gradients) otherwise; RelPosMHAXL's xattn core."""
+        f1, f2 = self.ffn_module1, self.ffn_module2
+        tr = self.training
+        d = x.shape[1]
+        u = A.layer_norm(x, f1[0], out_dtype=dtype)
+        x = f1[1].train_run(u, dtype, residual=x, alpha=0.5, out_p=f1[2].p if tr else 0.0)
+        u = A.layer_norm(x, self.norm1.norm, out_dtype=_f32).view(B, T, d)
+        o, attn = self.mha_layer(u, u, u, attn_mask=src_mask, key_padding_mask=kpm_u8, pos_embs=pos_embs)
+        x = A.DropAddFn.apply(o.reshape(B * T, d).float(), x, 1.0, None, 0.0, _f32)
+        x = self.convolution_module.train_run(x, B, T, dtype, kpm_u8, residual=x)
+        u = A.layer_norm(x, f2[0], out_dtype=dtype)
+        z = f2[1].train_run(u, dtype, residual=x, alpha=0.5, out_p=f2[2].p if tr else 0.0)
+        return A.layer_norm(z, self.norm2.norm, out_dtype=_f32), attn
+
     def wants_train_path(self, x):
         return A.needs_grad(self, x) or (self.training and self.ffn_module1[2].p > 0)
 
@@ -288,6 +318,10 @@ class ConformerEncoderLayer(nn.Module):
         B, T, d = x.shape
         dtype = _enc.compute_dtype()
         kpm = src_key_padding_mask.to(torch.uint8).contiguous() if src_key_padding_mask is not None else None
+        if self.module_layer:
+            y, attn = self.mha_layer_forward(x.float().reshape(B * T, d).contiguous(), B, T, kpm, src_mask,
+                                             pos_embs, dtype)
+            return y.view(B, T, d), attn
         am = _enc.attn_mask_arg(src_mask, B, T, self.mha_layer.num_heads, x.device)
         x2d = x.float().reshape(B * T, d).contiguous()
         if self.wants_train_path(x):
@@ -409,6 +443,15 @@ class ConformerEncoder(nn.Module):
                              "the positional embeddings are mandatory")
         B, T, d = src.shape
         kpm = src_key_padding_mask.to(torch.uint8).contiguous() if src_key_padding_mask is not None else None
+        if self.layers[0].module_layer:
+            # Conformer.py:371-383 on the per-module layers (regularMHA: pos_embs
+            # reach the attention mask as in the reference, None from TransformerASR)
+            x = src.float().reshape(B * T, d).contiguous()
+            attns = []
+            for layer in self.layers:
+                x, a = layer.mha_layer_forward(x, B, T, kpm, src_mask, pos_embs, _enc.compute_dtype())
+                attns.append(a)
+            return A.layer_norm(x, self.norm.norm, out_dtype=_f32).view(B, T, d), attns
         am = _enc.attn_mask_arg(src_mask, B, T, self.layers[0].mha_layer.num_heads, src.device)
         y, attns = self.run(src.float().reshape(B * T, d).contiguous(), B, T, pos_embs, kpm,
                             _enc.compute_dtype(), True, am=am)

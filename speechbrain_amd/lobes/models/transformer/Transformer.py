@@ -28,7 +28,7 @@ import torch.nn as nn
 
 from .... import _enc
 from .... import _autograd as A
-from ....nnet.attention import MultiheadAttention, PositionalwiseFeedForward, RelPosMHAXL, _mode_weight
+from ....nnet.attention import FUSED_DH_MAX, MultiheadAttention, PositionalwiseFeedForward, RelPosMHAXL, _mode_weight
 from ....nnet.normalization import LayerNorm
 
 __all__ = ["PositionalEncoding", "TransformerEncoderLayer", "TransformerEncoder", "TransformerDecoderLayer",
@@ -168,8 +168,10 @@ class TransformerEncoderLayer(nn.Module):
     def module_forward(self, src, src_mask=None, src_key_padding_mask=None, pos_embs=None):
         """Transformer.py:343-376 step by step on the drop-in submodules — the
         attention's differentiable path (masks, pos_embs, dropout,
-        gradients), the HIP LayerNorm / FFN autograd Functions — for
-        everything the fused inference step does not take."""
+        gradients), the HIP LayerNorm / FFN autograd Functions, the residual
+        adds with their dropout as one HIP launch each — for everything the
+        fused inference step does not take (RelPosMHAXL self-attention,
+        Transformer.py:307-310, runs its own fused kernel inside)."""
         src1 = self.norm1(src) if self.normalize_before else src
         if self.attention_type == "RelPosMHAXL":
             output, self_attn = self.self_att(src1, src1, src1, pos_embs, key_padding_mask=src_key_padding_mask,
@@ -177,27 +179,51 @@ class TransformerEncoderLayer(nn.Module):
         else:
             output, self_attn = self.self_att(src1, src1, src1, attn_mask=src_mask,
                                               key_padding_mask=src_key_padding_mask, pos_embs=pos_embs)
-        src = src + self.dropout1(output)
+        tr = self.training
+        src = _add_drop(src, output, self.dropout1.p if tr else 0.0)
         if not self.normalize_before:
             src = self.norm1(src)
         src1 = self.norm2(src) if self.normalize_before else src
-        output = src + self.dropout2(self.pos_ffn(src1))
+        output = _add_drop(src, self.pos_ffn(src1), self.dropout2.p if tr else 0.0)
         if not self.normalize_before:
             output = self.norm2(output)
         return output, self_attn
 
-    def _fused_ok(self, src, src_mask, pos_embs):
-        return (src_mask is None and pos_embs is None and self.attention_type == "regularMHA"
-                and not A.needs_grad(self, src) and not (self.training and self.dropout1.p > 0))
+    def _fused_ok(self, src, src_mask, pos_embs, kpm=None):
+        """The fused inference step takes: regularMHA self-attention in the
+        default projection layout, no src_mask / pos_embs, a bool / byte key
+        padding mask (an additive float one goes to the module path, as in
+        MultiheadAttention), a GELU / ReLU FFN, no gradients, no dropout."""
+        if not (src_mask is None and pos_embs is None and self.attention_type == "regularMHA"
+                and (kpm is None or kpm.dtype in (torch.bool, torch.uint8))
+                and not A.needs_grad(self, src) and not (self.training and self.dropout1.p > 0)):
+            return False
+        a = self.self_att.att
+        if (not a._qkv_same_embed_dim or a.bias_k is not None or a.add_zero_attn or a.in_proj_bias is None
+                or a.head_dim > FUSED_DH_MAX):
+            return False
+        try:
+            name, slope = self.pos_ffn.act_name()
+        except NotImplementedError:
+            return False
+        return name == "gelu" or (name in ("relu", "leaky_relu") and slope == 0.0)
 
     def forward(self, src, src_mask: Optional[torch.Tensor] = None,
                 src_key_padding_mask: Optional[torch.Tensor] = None, pos_embs: Optional[torch.Tensor] = None):
-        if not self._fused_ok(src, src_mask, pos_embs):
+        if not self._fused_ok(src, src_mask, pos_embs, src_key_padding_mask):
             return self.module_forward(src, src_mask, src_key_padding_mask, pos_embs)
         B, T, d = src.shape
         kpm = src_key_padding_mask.to(torch.uint8).contiguous() if src_key_padding_mask is not None else None
         y, attn = self.run(src.float().reshape(B * T, d).contiguous(), B, T, kpm, _mode(), True)
         return y.view(B, T, d), attn
+
+
+def _add_drop(res, y, p):
+    """res + Dropout(p)(y) (Transformer.py:359,370) as one HIP launch, differentiable."""
+    shp = res.shape
+    d = shp[-1]
+    r = res.float().reshape(-1, d).contiguous()
+    return A.DropAddFn.apply(y.float().reshape(-1, d).contiguous(), r, 1.0, None, float(p), _f32).view(shp)
 
 
 class TransformerEncoder(nn.Module):
@@ -227,7 +253,7 @@ class TransformerEncoder(nn.Module):
 
     def forward(self, src, src_mask: Optional[torch.Tensor] = None,
                 src_key_padding_mask: Optional[torch.Tensor] = None, pos_embs: Optional[torch.Tensor] = None):
-        if not all(l._fused_ok(src, src_mask, pos_embs) for l in self.layers):
+        if not all(l._fused_ok(src, src_mask, pos_embs, src_key_padding_mask) for l in self.layers):
             # Transformer.py:448-486 with the layers' module path
             keep = self.rng.random(len(self.layers)) if self.layerdrop_prob > 0.0 else None
             out, attns = src, []

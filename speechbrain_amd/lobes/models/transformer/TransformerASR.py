@@ -1,18 +1,25 @@
 """Drop-in for speechbrain.lobes.models.transformer.TransformerASR
-(TransformerASR.py:87-141 constructor, :143-211 forward, :213-247
-make_masks, :249-300 decode, :279-316 encode).
+(TransformerASR.py:87-141 constructor over TransformerInterface,
+Transformer.py:83-192; :143-211 forward, :213-247 make_masks, :236-277
+decode, :279-316 encode).
 
-Accelerated configuration (the LibriSpeech Conformer recipes,
-conformer_small.yaml:132-146): encoder_module="conformer",
-attention_type="RelPosMHAXL"; encode() runs on the HIP kernels.  The module
-tree mirrors the reference (positional_encoding, positional_encoding_decoder,
-encoder.*, decoder.* when num_decoder_layers > 0,
-custom_src_module.layers.0.w.*, custom_tgt_module.layers.0.emb.Embedding.weight),
-so a recipe checkpoint — decoder included — loads with strict=True.  The
-attention decoder (forward / decode) keeps the reference's semantics with its
-LayerNorms and FFNs on the HIP drop-ins and its masked attentions on the
-wrapped torch.nn.MultiheadAttention (outside the accelerated path).
-EncoderWrapper (:325-356) makes encode() the forward of a DDP-wrappable module.
+Every constructor variant of the reference builds the reference's module
+tree, so a recipe checkpoint — decoder included — loads with strict=True:
+  encoder_module "conformer" | "transformer" (Transformer.py:141-175),
+  attention_type "RelPosMHAXL" | "regularMHA" (:131-135; the rel-pos table
+  overrides the absolute one, and the decoder then takes
+  positional_encoding_decoder), positional_encoding "fixed_abs_sine" | None.
+The metric configuration (the LibriSpeech Conformer recipes,
+conformer_small.yaml:132-146: conformer + RelPosMHAXL) runs encode() as the
+fused HIP schedule of ConformerEncoder.run; the other combinations run the
+drop-in encoder modules (TransformerEncoder's fused step for the
+transformer.yaml recipe's regularMHA pre-norm GELU stack,
+recipes/LibriSpeech/ASR/transformer/hparams/transformer.yaml:133-150; the
+module path with RelPosMHAXL or regularMHA in the Conformer layers).  The
+attention decoder (forward / decode) runs the reference's semantics on the
+HIP drop-ins (LayerNorm, PositionalwiseFeedForward, MultiheadAttention's
+general path).  EncoderWrapper (:324-356) makes encode() the forward of a
+DDP-wrappable module.
 """
 import math
 from typing import Optional
@@ -26,36 +33,23 @@ from ....nnet.activations import Swish
 from ....nnet.attention import RelPosEncXL
 from ....nnet.linear import Linear
 from .Conformer import ConformerEncoder
-from .Transformer import NormalizedEmbedding, TransformerDecoder, get_key_padding_mask, get_lookahead_mask
+from .Transformer import (NormalizedEmbedding, PositionalEncoding, TransformerDecoder, TransformerEncoder,
+                          get_key_padding_mask, get_lookahead_mask)
 
 _f32 = torch.float32
 
 
-class PositionalEncoding(nn.Module):
-    """Transformer.py:199-243 absolute sine table (buffer `pe`, kept for
-    state_dict parity; used only by the decoder)."""
-
-    def __init__(self, input_size, max_len=2500):
-        super().__init__()
-        self.max_len = max_len
-        pe = torch.zeros(self.max_len, input_size, requires_grad=False)
-        positions = torch.arange(0, self.max_len).unsqueeze(1).float()
-        denominator = torch.exp(torch.arange(0, input_size, 2).float() * -(math.log(10000.0) / input_size))
-        pe[:, 0::2] = torch.sin(positions * denominator)
-        pe[:, 1::2] = torch.cos(positions * denominator)
-        pe = pe.unsqueeze(0)
-        self.register_buffer("pe", pe)
-
-    def forward(self, x):
-        return self.pe[:, : x.size(1)].clone().detach()
-
-
 class _ModuleList(nn.Module):
-    """nnet/containers.py ModuleList: children under `.layers`."""
+    """nnet/containers.py ModuleList: children under `.layers`, applied in order."""
 
     def __init__(self, *modules):
         super().__init__()
         self.layers = nn.ModuleList(modules)
+
+    def forward(self, x):
+        for layer in self.layers:
+            x = layer(x)
+        return x
 
 
 class TransformerASR(nn.Module):
@@ -66,20 +60,35 @@ class TransformerASR(nn.Module):
                  attention_type: Optional[str] = "regularMHA", max_length: Optional[int] = 2500,
                  causal: Optional[bool] = True):
         super().__init__()
-        if encoder_module != "conformer" or attention_type != "RelPosMHAXL":
-            raise NotImplementedError("accelerated TransformerASR: encoder_module='conformer', "
-                                      "attention_type='RelPosMHAXL'")
-        assert num_encoder_layers > 0
-        assert normalize_before, "normalize_before must be True for Conformer"
+        # TransformerInterface.__init__ (Transformer.py:108-192)
         self.causal = causal
         self.attention_type = attention_type
         self.positional_encoding_type = positional_encoding
-        self.positional_encoding = RelPosEncXL(d_model)
-        self.positional_encoding_decoder = PositionalEncoding(d_model, max_length)
-        self.encoder = ConformerEncoder(nhead=nhead, num_layers=num_encoder_layers, d_ffn=d_ffn, d_model=d_model,
-                                        dropout=dropout, activation=conformer_activation, kernel_size=kernel_size,
-                                        bias=bias, causal=self.causal, attention_type=self.attention_type)
-        if num_decoder_layers > 0:  # Transformer.py:177-192 (always regularMHA, causal)
+        self.encoder_kdim = self.encoder_vdim = self.decoder_kdim = self.decoder_vdim = None
+        assert attention_type in ["regularMHA", "RelPosMHAXL"]
+        assert positional_encoding in ["fixed_abs_sine", None]
+        assert num_encoder_layers + num_decoder_layers > 0, \
+            "number of encoder layers and number of decoder layers cannot both be 0!"
+        if positional_encoding == "fixed_abs_sine":
+            self.positional_encoding = PositionalEncoding(d_model, max_length)
+        if attention_type == "RelPosMHAXL":  # overrides any other pos_embedding (:130-135)
+            self.positional_encoding = RelPosEncXL(d_model)
+            self.positional_encoding_decoder = PositionalEncoding(d_model, max_length)
+        self.encoder_module = encoder_module
+        if num_encoder_layers > 0:
+            if encoder_module == "transformer":
+                self.encoder = TransformerEncoder(nhead=nhead, num_layers=num_encoder_layers, d_ffn=d_ffn,
+                                                  d_model=d_model, dropout=dropout, activation=activation,
+                                                  normalize_before=normalize_before, causal=self.causal,
+                                                  attention_type=self.attention_type)
+            elif encoder_module == "conformer":
+                self.encoder = ConformerEncoder(nhead=nhead, num_layers=num_encoder_layers, d_ffn=d_ffn,
+                                                d_model=d_model, dropout=dropout, activation=conformer_activation,
+                                                kernel_size=kernel_size, bias=bias, causal=self.causal,
+                                                attention_type=self.attention_type)
+                assert normalize_before, "normalize_before must be True for Conformer"
+                assert conformer_activation is not None, "conformer_activation must not be None"
+        if num_decoder_layers > 0:  # always regularMHA, causal (:177-192)
             self.decoder = TransformerDecoder(num_layers=num_decoder_layers, nhead=nhead, d_ffn=d_ffn, d_model=d_model,
                                               dropout=dropout, activation=activation,
                                               normalize_before=normalize_before, causal=True,
@@ -94,11 +103,26 @@ class TransformerASR(nn.Module):
             if p.dim() > 1:
                 torch.nn.init.xavier_normal_(p)
 
+    def _fast_encoder(self):
+        """The fused Conformer schedule (ConformerEncoder.run) applies."""
+        return (self.encoder_module == "conformer" and self.attention_type == "RelPosMHAXL"
+                and not self.encoder.layers[0].module_layer)
+
+    def _abs_pe(self, x):
+        """x + the absolute sine table (TransformerASR.py:173-174, 307-308).
+        With positional_encoding=None and regularMHA the reference never sets
+        its positional term and fails (UnboundLocalError at :177-182 /
+        :311-315); the drop-in raises a ValueError there."""
+        if self.positional_encoding_type == "fixed_abs_sine":
+            return x + self.positional_encoding(x)
+        raise ValueError("TransformerASR(positional_encoding=None, attention_type='regularMHA'): the reference "
+                         "leaves the positional embeddings unset here (TransformerASR.py:304-315)")
+
     def forward(self, src, tgt, wav_len=None, pad_idx=0):
-        """TransformerASR.py:143-211 → (encoder_out, decoder_out).  The encoder
-        runs on HIP with make_masks' src key padding mask (positions ≥
-        round(wav_len·T), unlike encode()'s > floor(wav_len·T)); the decoder
-        with the reference's lookahead and target padding masks."""
+        """TransformerASR.py:143-211 → (encoder_out, decoder_out).  The src key
+        padding mask is make_masks' (positions ≥ round(wav_len·T), unlike
+        encode()'s > floor(wav_len·T)); the decoder takes the reference's
+        lookahead and target padding masks."""
         if not hasattr(self, "decoder"):
             raise ValueError("TransformerASR.forward needs num_decoder_layers > 0 (use encode())")
         if src.dim() == 4:
@@ -106,19 +130,25 @@ class TransformerASR(nn.Module):
             src = src.reshape(bz, t, ch1 * ch2)
         src_kpm, tgt_kpm, src_mask, tgt_mask = self.make_masks(src, tgt, wav_len, pad_idx=pad_idx)
         if src_kpm is not None and src_kpm.shape[1] != src.shape[1]:
-            # the reference's rel-pos attention cannot view a narrower mask as (B, 1, 1, T) either
+            # neither the reference's rel-pos attention nor torch's MHA takes a narrower mask
             raise ValueError(f"src key padding mask width {src_kpm.shape[1]} != T = {src.shape[1]} "
                              "(no utterance fills the batch: max(wav_len) < 1)")
-        encoder_out = self._encode(src, None if src_kpm is None else src_kpm.to(torch.uint8))
-        tgt = self.custom_tgt_module.layers[0](tgt)
-        tgt = tgt + self.positional_encoding_decoder(tgt)
-        encoder_out = encoder_out + self.positional_encoding_decoder(encoder_out)
+        if self._fast_encoder():
+            encoder_out = self._encode(src, None if src_kpm is None else src_kpm.to(torch.uint8))
+        else:
+            encoder_out = self._module_encode(src, src_kpm, src_mask)
+        tgt = self.custom_tgt_module(tgt)
+        if self.attention_type == "RelPosMHAXL":
+            tgt = tgt + self.positional_encoding_decoder(tgt)
+            encoder_out = encoder_out + self.positional_encoding_decoder(encoder_out)
+        else:
+            tgt = self._abs_pe(tgt)
         decoder_out, _, _ = self.decoder(tgt=tgt, memory=encoder_out, memory_mask=src_mask, tgt_mask=tgt_mask,
                                          tgt_key_padding_mask=tgt_kpm, memory_key_padding_mask=src_kpm)
         return encoder_out, decoder_out
 
     def make_masks(self, src, tgt, wav_len=None, pad_idx=0):
-        """TransformerASR.py:213-247."""
+        """TransformerASR.py:213-234."""
         src_key_padding_mask = None
         if wav_len is not None:
             abs_len = torch.round(wav_len * src.shape[1])
@@ -135,7 +165,7 @@ class TransformerASR(nn.Module):
 
     @torch.no_grad()
     def decode(self, tgt, encoder_out, enc_len=None):
-        """TransformerASR.py:249-300 → (prediction, last cross-attention map)."""
+        """TransformerASR.py:236-277 → (prediction, last cross-attention map)."""
         if not hasattr(self, "decoder"):
             raise ValueError("TransformerASR.decode needs num_decoder_layers > 0")
         tgt_mask = get_lookahead_mask(tgt)
@@ -144,9 +174,12 @@ class TransformerASR(nn.Module):
             el = enc_len.to(encoder_out.device)
             src_key_padding_mask = ~(torch.arange(int(el.max().long().item()), device=el.device,
                                                   dtype=el.dtype)[None, :] < el[:, None])
-        tgt = self.custom_tgt_module.layers[0](tgt)
-        tgt = tgt + self.positional_encoding_decoder(tgt)
-        encoder_out = encoder_out + self.positional_encoding_decoder(encoder_out)
+        tgt = self.custom_tgt_module(tgt)
+        if self.attention_type == "RelPosMHAXL":
+            tgt = tgt + self.positional_encoding_decoder(tgt)
+            encoder_out = encoder_out + self.positional_encoding_decoder(encoder_out)
+        else:
+            tgt = self._abs_pe(tgt)
         prediction, self_attns, multihead_attns = self.decoder(tgt, encoder_out, tgt_mask=tgt_mask,
                                                                memory_key_padding_mask=src_key_padding_mask)
         return prediction, multihead_attns[-1]
@@ -162,10 +195,33 @@ class TransformerASR(nn.Module):
         if src.dim() == 4:
             bz, t, ch1, ch2 = src.shape
             src = src.reshape(bz, t, ch1 * ch2)
-        return self._encode(src, self.key_padding_mask(src.shape[1], wav_len, src.device))
+        kpm = self.key_padding_mask(src.shape[1], wav_len, src.device)
+        if self._fast_encoder():
+            return self._encode(src, kpm)
+        return self._module_encode(src, None if kpm is None else kpm.bool())
+
+    def _module_encode(self, src, kpm, src_mask=None):
+        """TransformerASR.py:303-316 (and :169-182) on the drop-in modules, for
+        every encoder / attention combination but the fused Conformer one: the
+        src Linear (MFMA GEMM) + dropout, the rel-pos table or the absolute
+        sine term, then the encoder module (TransformerEncoder's fused step or
+        its module path; the Conformer's regularMHA layers)."""
+        B, T, Fin = src.shape
+        dtype = _enc.compute_dtype()
+        lin = self.custom_src_module.layers[0]
+        drop = self.custom_src_module.layers[1]
+        x = A.linear(src.reshape(B * T, Fin), lin.w.weight, lin.w.bias, dtype, lin._wc, "t_w", out_dtype=_f32)
+        x = A.dropout(x, drop.p, self.training).view(B, T, -1)
+        pos = None
+        if self.attention_type == "RelPosMHAXL":
+            pos = self.positional_encoding(x)
+        else:
+            x = self._abs_pe(x)
+        y, _ = self.encoder(src=x, src_mask=src_mask, src_key_padding_mask=kpm, pos_embs=pos)
+        return y
 
     def _encode(self, src, kpm):
-        """src (B, T, F) and a uint8 key padding mask (B, T) or None → encoder output."""
+        """Fused Conformer path: src (B, T, F) and a uint8 key padding mask (B, T) or None → encoder output."""
         B, T, Fin = src.shape
         dtype = _enc.compute_dtype()
         if kpm is not None:

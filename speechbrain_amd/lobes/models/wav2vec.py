@@ -266,6 +266,8 @@ class EncoderWrapper(nn.Module):
 
     def forward(self, latents, wav_lens=None, padding_mask=None, mask=None):
         if (mask is not None or A.needs_grad(self, latents)
+                or not isinstance(self.latent_encoder, TransformerEncoder)
+                or not all(layer._fused_ok(latents, None, None, padding_mask) for layer in self.latent_encoder.layers)
                 or (self.training and (self.dropout_encoder_input.p > 0
                                        or any(isinstance(m, nn.Dropout) and m.p > 0
                                               for m in self.latent_encoder.modules())))):

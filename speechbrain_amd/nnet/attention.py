@@ -19,6 +19,10 @@ from .activations import Swish
 
 __all__ = ["RelPosEncXL", "RelPosMHAXL", "PositionalwiseFeedForward", "MultiheadAttention"]
 
+# head size limit of the fused self-attention kernels (csrc/attention.hip);
+# wider heads take the xattn core (dh <= 256), as any cross-attention does
+FUSED_DH_MAX = 128
+
 
 class RelPosEncXL(nn.Module):
     """attention.py:312-359.  The (1, 2T-1, d) table depends only on T and d;
@@ -216,19 +220,22 @@ class RelPosMHAXL(nn.Module):
         o, attn = A.RelPosCrossAttnFn.apply(q, k, v, pk, self.pos_bias_u, self.pos_bias_v, kpm, am, B, Lq, Lk, H, dh,
                                             self.scale, bool(self.mask_pos_future), float(p))
         out = A.linear(o, self.out_proj.weight, self.out_proj.bias, dtype, self._wc, "x_out")
+        if p == 0:
+            attn = attn.clone()  # without dropout the weights are the softmax saved for backward: the caller's copy
         return out.view(B, Lq, E), attn
 
     def forward(self, query, key, value, pos_embs, key_padding_mask=None, attn_mask=None,
                 return_attn_weights=True):
         """attention.py:485-639.  Self-attention (query, key and value
         identical, every Conformer call site) runs the fused kernels;
-        anything else — key or value != query, q_len != k_len — takes
-        cross_forward.  attn_mask: (Lq, Lk) or (B*H, Lq, Lk), bool (True =
+        anything else — key or value != query, q_len != k_len, or heads
+        wider than FUSED_DH_MAX — takes cross_forward.  attn_mask: (Lq, Lk) or (B*H, Lq, Lk), bool (True =
         masked) or additive float (:598-611)."""
         if not self._qkv_same_embed_dim:
             raise NotImplementedError  # the reference raises too (attention.py:566)
-        if not ((query is key or (query.shape == key.shape and torch.equal(query, key)))
-                and (key is value or (key.shape == value.shape and torch.equal(key, value)))):
+        if (self.head_dim > FUSED_DH_MAX
+                or not ((query is key or (query.shape == key.shape and torch.equal(query, key)))
+                        and (key is value or (key.shape == value.shape and torch.equal(key, value))))):
             out, attn = self.cross_forward(query, key, value, pos_embs, key_padding_mask, attn_mask)
             return (out, attn) if return_attn_weights else out
         B, T, d = query.shape
@@ -442,9 +449,8 @@ class MultiheadAttention(nn.Module):
         q = A.linear(query.reshape(B * L, -1), wq, bq, dtype, self._wc, "g_q", out_dtype=dtype)
         k = A.linear(key.reshape(B * S, -1), wk, bk, dtype, self._wc, "g_k", out_dtype=dtype)
         v = A.linear(value.reshape(B * S, -1), wv, bv, dtype, self._wc, "g_v", out_dtype=dtype)
-        # attn_mask (+ pos_embs, the reference's in-place add without the
-        # mutation of the caller's tensor) and a float key padding mask as one
-        # additive fp32 mask; bool / byte masks: True (non-zero) = masked
+        # attn_mask (+ pos_embs) and a float key padding mask as one additive
+        # fp32 mask; bool / byte masks: True (non-zero) = masked
         if pos_embs is not None:
             # attention.py:756-761, in place on the caller's mask as there (a
             # mask shared by a stack of layers accumulates every layer's add;
@@ -472,22 +478,12 @@ class MultiheadAttention(nn.Module):
                     mf = mf.view(1, 1, L, S) if mf.dim() == 2 else mf.view(-1, H, L, S)
                     m = (mf + add).reshape(B * H, L, S)
         am = _enc.attn_mask_arg(m, B, L, H, query.device, Lk=S)
-        z = self._zero_core(S, E, H, dh, query.device, dtype)
         p = a.dropout if self.training else 0.0
-        o, attn = A.RelPosCrossAttnFn.apply(q, k, v, z[0], z[1], z[1], kpm, am, B, L, S, H, dh, 1.0 / math.sqrt(dh),
+        # the xattn core without a positional band: plain scaled dot-product attention
+        o, attn = A.RelPosCrossAttnFn.apply(q, k, v, None, None, None, kpm, am, B, L, S, H, dh, 1.0 / math.sqrt(dh),
                                             False, float(p))
         out = A.linear(o, a.out_proj.weight, a.out_proj.bias, dtype, self._wc, "g_out")
         return out.view(B, L, E), attn.mean(dim=1)
-
-    def _zero_core(self, S, E, H, dh, dev, dtype):
-        """A zero (2S-1, E) positional band and zero (dh, H) biases: the
-        xattn core is then plain scaled dot-product attention."""
-        key = ("core", S, str(dev), dtype)
-        z = self._zeros.get(key)
-        if z is None:
-            z = (torch.zeros(2 * S - 1, E, device=dev, dtype=dtype), torch.zeros(dh, H, device=dev))
-            self._zeros = {key: z}
-        return z
 
     def forward(self, query, key, value, attn_mask=None, key_padding_mask=None, return_attn_weights=True,
                 pos_embs=None):
@@ -495,7 +491,7 @@ class MultiheadAttention(nn.Module):
                 and (key_padding_mask is None or key_padding_mask.dtype in (torch.bool, torch.uint8))
                 and not A.needs_grad(self, query) and not (self.training and self.att.dropout > 0)
                 and self.att._qkv_same_embed_dim and self.att.bias_k is None and not self.att.add_zero_attn
-                and self.att.in_proj_bias is not None)
+                and self.att.in_proj_bias is not None and self.d_model // self.nhead <= FUSED_DH_MAX)
         if not fast:
             out, w = self.general_forward(query, key, value, attn_mask, key_padding_mask, pos_embs)
             return (out, w) if return_attn_weights else out

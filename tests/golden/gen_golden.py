@@ -763,7 +763,156 @@ def gen_xattn():
     np.savez_compressed(os.path.join(OUT, "xattn.npz"), **out)
 
 
+def _doctest_ns():
+    """The reference's classes under the names doctest_cases.py uses."""
+    from types import SimpleNamespace
+    from speechbrain.processing import features as PF
+    from speechbrain.lobes import features as LFe
+    from speechbrain.lobes.models.transformer import Conformer as RC, Transformer as RT, TransformerASR as RA
+    from speechbrain.lobes.models import convolution as RCV, wav2vec as RW
+    from speechbrain.nnet import attention as RAT, CNN as RCNN, linear as RL, normalization as RN, activations as RACT
+    from speechbrain.nnet.transducer import transducer_joint as RJ
+    return SimpleNamespace(
+        STFT=PF.STFT, spectral_magnitude=PF.spectral_magnitude, Filterbank=PF.Filterbank, DCT=PF.DCT,
+        Deltas=PF.Deltas, ContextWindow=PF.ContextWindow, InputNormalization=PF.InputNormalization,
+        Fbank=LFe.Fbank, MFCC=LFe.MFCC, SpecAugment=SpecAugment, ConvolutionFrontEnd=RCV.ConvolutionFrontEnd,
+        ConvBlock=RCV.ConvBlock, Conv2d=RCNN.Conv2d, Linear=RL.Linear, LayerNorm=RN.LayerNorm, Swish=RACT.Swish,
+        RelPosMHAXL=RAT.RelPosMHAXL, MultiheadAttention=RAT.MultiheadAttention,
+        PositionalwiseFeedForward=RAT.PositionalwiseFeedForward, ConvolutionModule=RC.ConvolutionModule,
+        ConformerEncoderLayer=RC.ConformerEncoderLayer, ConformerEncoder=RC.ConformerEncoder,
+        PositionalEncoding=RT.PositionalEncoding, TransformerEncoderLayer=RT.TransformerEncoderLayer,
+        TransformerEncoder=RT.TransformerEncoder, TransformerDecoderLayer=RT.TransformerDecoderLayer,
+        TransformerDecoder=RT.TransformerDecoder, NormalizedEmbedding=RT.NormalizedEmbedding,
+        TransformerASR=RA.TransformerASR, EncoderWrapper=RA.EncoderWrapper, GELU=torch.nn.GELU,
+        Transducer_joint=RJ.Transducer_joint, W2VLatentExtractor=RW.W2VLatentExtractor,
+        W2VEncoderWrapper=RW.EncoderWrapper)
+
+
+def gen_doctests():
+    """doctests.npz: the reference's doctest examples (tests/golden/doctest_cases.py)
+    run on the reference modules with detinit weights and inputs: the output
+    shape (asserted equal to the doctest's printed shape) and the kept slice
+    of the output."""
+    sys.path.insert(0, OUT)
+    from detinit import det_state
+    from doctest_cases import cases
+    ns = _doctest_ns()
+    out = {}
+    for c in cases():
+        m = c.build(ns) if c.build is not None else None
+        if m is not None:
+            if c.det:
+                m.load_state_dict(det_state(m, c.seed), strict=True)
+            m.train(not c.eval_mode)
+        xs = c.make_inputs(torch)
+        torch.manual_seed(c.seed)
+        with torch.no_grad():
+            y = c.call(ns, m, *xs)
+        assert tuple(y.shape) == c.shape, (c.name, tuple(y.shape), c.shape)
+        out[c.name + ".shape"] = np.array(y.shape, np.int64)
+        out[c.name + ".out"] = t2n(c.keep(y))
+        print(c.name, tuple(y.shape))
+    np.savez_compressed(os.path.join(OUT, "doctests.npz"), **out)
+
+
+def _variant_model(ctor):
+    from speechbrain.nnet.activations import Swish
+    sys.path.insert(0, OUT)
+    kw = dict(ctor)
+    act = kw.pop("act", None)
+    if act is not None:
+        kw["activation"] = {"gelu": torch.nn.GELU, "relu": torch.nn.ReLU, "swish": Swish}[act]
+    return TransformerASR(**kw)
+
+
+def _recipe_cnn():
+    """transformer.yaml:122-130."""
+    return ConvolutionFrontEnd(input_shape=(8, 10, 80), num_blocks=3, num_layers_per_block=1,
+                               out_channels=(64, 64, 64), kernel_sizes=(5, 5, 1), strides=(2, 2, 1),
+                               residuals=(False, False, True))
+
+
+def gen_variants():
+    """variants.npz: TransformerASR / encoder constructor variants beyond the
+    Conformer + RelPosMHAXL recipe (TransformerASR.py:87-316,
+    Transformer.py:83-192,246-486, Conformer.py:118-383), weights from
+    detinit.  Per case: forward (with and without wav_len), encode, decode,
+    and (grads=True) the gradients of sum(R * encode(src, wav_len)) w.r.t.
+    the encoder-side parameters and the input.  Plus a regularMHA
+    ConformerEncoder called directly with a bool src_mask and key padding."""
+    sys.path.insert(0, OUT)
+    from detinit import det_state, det_input
+    from variant_cases import VARIANTS
+    out = {}
+    for i, (tag, c) in enumerate(VARIANTS.items()):
+        model = _variant_model(c["ctor"])
+        model.load_state_dict(det_state(model, 50 + i), strict=True)
+        model.eval()
+        B, T, Fd, U = c["B"], c["T"], c["F"], c["U"]
+        cnn = None
+        if c.get("cnn"):
+            cnn = _recipe_cnn()
+            cnn.load_state_dict(det_state(cnn, 150 + i), strict=True)
+            cnn.eval()
+        x = torch.from_numpy(det_input((B, T, Fd), 200 + i))
+        rng = np.random.default_rng(300 + i)
+        tgt = torch.from_numpy(rng.integers(1, c["ctor"]["tgt_vocab"], size=(B, U))).long()
+        tgt[1, U - 2:] = 0
+        if B > 2:
+            tgt[2, U - 4:] = 0
+        wav_len = torch.tensor([1.0, 0.8, 0.55][:B])
+        with torch.no_grad():
+            src = cnn(x) if cnn is not None else x
+            Te = src.shape[1]
+            e1, d1 = model(src, tgt, wav_len)
+            e0, d0 = model(src, tgt)
+            out[f"{tag}.fwd_enc"], out[f"{tag}.fwd_dec"] = t2n(e1), t2n(d1)
+            out[f"{tag}.fwd0_enc"], out[f"{tag}.fwd0_dec"] = t2n(e0), t2n(d0)
+            enc = model.encode(src, wav_len)
+            out[f"{tag}.enc"] = t2n(enc)
+            out[f"{tag}.enc0"] = t2n(model.encode(src))
+            enc_len = torch.round(wav_len * Te).long()
+            pred, att = model.decode(tgt, enc, enc_len)
+            out[f"{tag}.dec_pred"], out[f"{tag}.dec_att"] = t2n(pred), t2n(att)
+        out[f"{tag}.x"], out[f"{tag}.tgt"], out[f"{tag}.wav_len"] = t2n(x), tgt.numpy(), t2n(wav_len)
+        out[f"{tag}.enc_len"] = enc_len.numpy()
+        if c["grads"]:
+            xg = x.clone().requires_grad_(True)
+            y = model.encode(cnn(xg) if cnn is not None else xg, wav_len)
+            R = torch.from_numpy(det_input(tuple(y.shape), 400 + i))
+            (y * R).sum().backward()
+            out[f"{tag}.grad_x"] = t2n(xg.grad)
+            for k, p in model.named_parameters():
+                if p.grad is not None:
+                    out[f"{tag}.grad.{k}"] = t2n(p.grad)
+        print(tag, tuple(enc.shape))
+    # ConformerEncoder(regularMHA) directly: src_mask (bool, True = masked), key padding, attention maps
+    enc = ConformerEncoder(2, 64, 128, 4, kernel_size=7, attention_type="regularMHA")
+    enc.load_state_dict(det_state(enc, 90), strict=True)
+    enc.eval()
+    x = torch.from_numpy(det_input((2, 17, 64), 91)).requires_grad_(True)
+    kpm = torch.arange(17)[None, :] >= torch.tensor([17, 12])[:, None]
+    am = torch.triu(torch.ones(17, 17), diagonal=3).bool()
+    y, attns = enc(x, src_mask=am, src_key_padding_mask=kpm)
+    R = torch.from_numpy(det_input(tuple(y.shape), 92))
+    (y * R).sum().backward()
+    out["cenc.x"], out["cenc.kpm"], out["cenc.am"] = t2n(x), kpm.numpy(), am.numpy()
+    out["cenc.y"] = t2n(y)
+    for j, a in enumerate(attns):
+        out[f"cenc.attn{j}"] = t2n(a)
+    out["cenc.grad_x"] = t2n(x.grad)
+    for k, p in enc.named_parameters():
+        out[f"cenc.grad.{k}"] = t2n(p.grad)
+    np.savez_compressed(os.path.join(OUT, "variants.npz"), **out)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["variants"]:
+        gen_variants()
+        sys.exit(0)
+    if sys.argv[1:] == ["doctests"]:
+        gen_doctests()
+        sys.exit(0)
     if sys.argv[1:] == ["xattn"]:
         gen_xattn()
         sys.exit(0)
@@ -796,6 +945,8 @@ if __name__ == "__main__":
     gen_dropin()
     gen_recipe()
     gen_xattn()
+    gen_variants()
+    gen_doctests()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

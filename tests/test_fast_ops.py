@@ -47,3 +47,21 @@ def test_traced_call_is_recorded_as_the_op():
     tr = torch.jit.trace(lambda t: _double(t), torch.ones(2))
     assert "sbk::_test_double" in str(tr.graph)
     assert torch.equal(tr(torch.full((2,), 5.0)), torch.full((2,), 10.0))
+
+
+@custom_op("sbk::_test_nograd", mutates_args=())
+def _nograd(x: torch.Tensor) -> torch.Tensor:
+    return x + 1
+
+
+_nograd.register_fake(lambda x: torch.empty_like(x))
+
+
+def test_op_without_backward_raises_at_the_call():
+    import pytest
+    x = torch.ones(3, requires_grad=True)
+    with pytest.raises(RuntimeError, match="_test_nograd has no backward"):
+        _nograd(x)
+    with torch.no_grad():
+        assert torch.equal(_nograd(x), torch.full((3,), 2.0))
+    assert torch.equal(_nograd(x.detach()), torch.full((3,), 2.0))
