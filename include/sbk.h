@@ -257,8 +257,13 @@ int sbk_ffn_image(const void* w1, const void* w2, const void* w1b, const void* w
  * bias); act as sbk_gemm (not GLU).  img_elems: the image's size in bf16
  * elements, which must equal sbk_ffn_image_elems(D, H, np, chain) of this
  * call (SBK_ERR_ARG otherwise: an image built for another shape or for one
- * block instead of a chain is refused, never read out of bounds). */
-int sbk_ffn(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0, const void* img,
+ * block instead of a chain is refused, never read out of bounds).
+ * d_eff (1..D): the LayerNorms' statistics run over the first d_eff columns;
+ * columns d_eff..D-1 must be zero-padded channels (zero in x, in the LN
+ * gains / biases and in every weight row or column that reaches them), so a
+ * d_model < 256 model (conformer_small.yaml: 144) runs these kernels at
+ * D = 256 with results equal to the unpadded arithmetic.  d_eff = D: plain. */
+int sbk_ffn(const float* x, int M, int D, int d_eff, int H, const float* g0, const float* b0, float eps0, const void* img,
             long long img_elems, const float* b1, int act, float slope, const float* b2, float alpha, const float* gp, const float* bp,
             float epsp, float* out, const float* gn, const float* bn, float epsn, void* u, int u_bf16, void* stream);
 
@@ -268,7 +273,7 @@ int sbk_ffn(const float* x, int M, int D, int H, const float* g0, const float* b
  * LNn(out) wp^T — the following MHSA's in_proj (attention.py:549-553,
  * Conformer.py:186-197), replacing its QKV GEMM launch.  np == 0 behaves as
  * sbk_ffn. */
-int sbk_ffn_proj(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0, const void* img,
+int sbk_ffn_proj(const float* x, int M, int D, int d_eff, int H, const float* g0, const float* b0, float eps0, const void* img,
                  long long img_elems, const float* b1, int act, float slope, const float* b2, float alpha, const float* gp,
                  const float* bp, float epsp, float* out, const float* gn, const float* bn, float epsn, void* u,
                  int u_bf16, int np, void* yp, void* stream);
@@ -280,7 +285,8 @@ int sbk_ffn_proj(const float* x, int M, int D, int H, const float* g0, const flo
  * sbk_ffn_image(w1, w2, w1b, w2b, wp).  The Conformer's FFN2 + norm2 of
  * layer i with FFN1 + norm1 + in_proj of layer i+1 (Conformer.py:239-260,
  * attention.py:549-553); H is common to both. */
-int sbk_ffn_chain(const float* x, int M, int D, int H, int act, float slope, const float* g0, const float* b0,
+int sbk_ffn_chain(const float* x, int M, int D, int d_eff, int H, int act, float slope, const float* g0,
+                  const float* b0,
                   float eps0, const float* b1, const float* b2, float alpha, const float* gp, const float* bp,
                   float epsp, const float* g0b, const float* b0b, float eps0b, const float* b1b, const float* b2b,
                   float alphab, float* out, const float* gn, const float* bn, float epsn, void* u, int u_bf16,
@@ -404,9 +410,11 @@ int sbk_relpos_xattn_bwd(int dtype_bf16, const void* q, int ldq, const void* k, 
  * x, out (B*T, 256) fp32, out must not alias x; w1p (512, 256) bf16 rows GLU-permuted in
  * [value16 | gate16] groups (sbk_gemm_glu_group), b1p permuted alike; wc (K, 256) fp32 taps
  * (tap-major: the transpose of Conv1d.weight (256, 1, K)),
- * bc (256) or null; w2 (256, 256) bf16, b2 or null; kpm (B*T) uint8 or null.  K <= 31. */
+ * bc (256) or null; w2 (256, 256) bf16, b2 or null; kpm (B*T) uint8 or null.  K <= 31.
+ * d_eff: the LayerNorms' statistics over the first d_eff channels, the rest
+ * zero-padded (as sbk_ffn). */
 int sbk_conv_module_supported(int D, int K);
-int sbk_conv_module(const float* x, float* out, int B, int T, int D, const float* ln0_w, const float* ln0_b,
+int sbk_conv_module(const float* x, float* out, int B, int T, int D, int d_eff, const float* ln0_w, const float* ln0_b,
                     float eps0, const void* w1p, const float* b1p, const float* wc, const float* bc, int K, int causal,
                     const float* ln1_w, const float* ln1_b, float eps1, const void* w2, const float* b2,
                     const unsigned char* kpm, void* stream);
@@ -417,7 +425,7 @@ int sbk_conv_module(const float* x, float* out, int B, int T, int D, const float
  * o (B*T, 256) bf16 (the attention heads concatenated), wo (256, 256) bf16,
  * bo (256) fp32 or null; o == null behaves as sbk_conv_module. */
 int sbk_conv_module_pre(const float* x, const void* o, const void* wo, const float* bo, float* out, int B, int T,
-                        int D, const float* ln0_w, const float* ln0_b, float eps0, const void* w1p, const float* b1p,
+                        int D, int d_eff, const float* ln0_w, const float* ln0_b, float eps0, const void* w1p, const float* b1p,
                         const float* wc, const float* bc, int K, int causal, const float* ln1_w, const float* ln1_b,
                         float eps1, const void* w2, const float* b2, const unsigned char* kpm, void* stream);
 

@@ -348,13 +348,13 @@ def ffn_image(w1, w2, w1b=None, w2b=None, wp=None):
 def _ffn_op(x: torch.Tensor, g0: torch.Tensor, b0: torch.Tensor, e0: float, w1: torch.Tensor, b1: torch.Tensor,
             act: int, slope: float, w2: torch.Tensor, b2: torch.Tensor, alpha: float, gp: Optional[torch.Tensor],
             bp: Optional[torch.Tensor], ep: float, gn: Optional[torch.Tensor], bn: Optional[torch.Tensor], en: float,
-            next_bf16: bool) -> tuple[torch.Tensor, torch.Tensor]:
+            next_bf16: bool, deff: int) -> tuple[torch.Tensor, torch.Tensor]:
     M, D = x.shape
     H = w1.shape[0]
     img = ffn_image(w1, w2)
     out = torch.empty_like(x)
     u = torch.empty(M, D, device=x.device, dtype=_bf16 if next_bf16 else _f32) if gn is not None else None
-    rc = lib().sbk_ffn(ptr(x), M, D, H, ptr(g0), ptr(b0), float(e0), ptr(img), img.numel(), ptr(b1), act,
+    rc = lib().sbk_ffn(ptr(x), M, D, deff, H, ptr(g0), ptr(b0), float(e0), ptr(img), img.numel(), ptr(b1), act,
                        float(slope), ptr(b2), float(alpha), ptr(gp), ptr(bp), float(ep), ptr(out), ptr(gn), ptr(bn), float(en),
                        ptr(u), int(next_bf16), stream_of(x))
     check(rc, "sbk_ffn")
@@ -362,7 +362,7 @@ def _ffn_op(x: torch.Tensor, g0: torch.Tensor, b0: torch.Tensor, e0: float, w1: 
 
 
 @_ffn_op.register_fake
-def _(x, g0, b0, e0, w1, b1, act, slope, w2, b2, alpha, gp, bp, ep, gn, bn, en, next_bf16):
+def _(x, g0, b0, e0, w1, b1, act, slope, w2, b2, alpha, gp, bp, ep, gn, bn, en, next_bf16, deff):
     return (torch.empty_like(x),
             x.new_empty(x.shape, dtype=_bf16 if next_bf16 else _f32) if gn is not None else x.new_empty(0))
 
@@ -371,13 +371,13 @@ def _(x, g0, b0, e0, w1, b1, act, slope, w2, b2, alpha, gp, bp, ep, gn, bn, en, 
 def _ffn_proj_op(x: torch.Tensor, g0: torch.Tensor, b0: torch.Tensor, e0: float, w1: torch.Tensor,
                  b1: torch.Tensor, act: int, slope: float, w2: torch.Tensor, b2: torch.Tensor, alpha: float,
                  gp: Optional[torch.Tensor], bp: Optional[torch.Tensor], ep: float, gn: torch.Tensor,
-                 bn: torch.Tensor, en: float, wp: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+                 bn: torch.Tensor, en: float, wp: torch.Tensor, deff: int) -> tuple[torch.Tensor, torch.Tensor]:
     M, D = x.shape
     H, NP = w1.shape[0], wp.shape[0]
     img = ffn_image(w1, w2, wp=wp)
     out = torch.empty_like(x)
     y = torch.empty(M, NP, device=x.device, dtype=_bf16)
-    rc = lib().sbk_ffn_proj(ptr(x), M, D, H, ptr(g0), ptr(b0), float(e0), ptr(img), img.numel(), ptr(b1), act,
+    rc = lib().sbk_ffn_proj(ptr(x), M, D, deff, H, ptr(g0), ptr(b0), float(e0), ptr(img), img.numel(), ptr(b1), act,
                             float(slope), ptr(b2), float(alpha), ptr(gp), ptr(bp), float(ep), ptr(out), ptr(gn), ptr(bn),
                             float(en), None, 1, NP, ptr(y), stream_of(x))
     check(rc, "sbk_ffn_proj")
@@ -385,7 +385,7 @@ def _ffn_proj_op(x: torch.Tensor, g0: torch.Tensor, b0: torch.Tensor, e0: float,
 
 
 @_ffn_proj_op.register_fake
-def _(x, g0, b0, e0, w1, b1, act, slope, w2, b2, alpha, gp, bp, ep, gn, bn, en, wp):
+def _(x, g0, b0, e0, w1, b1, act, slope, w2, b2, alpha, gp, bp, ep, gn, bn, en, wp, deff):
     return torch.empty_like(x), x.new_empty((x.shape[0], wp.shape[0]), dtype=_bf16)
 
 
@@ -393,14 +393,16 @@ def ffn_proj_supported(D, H, NP):
     return ffn_supported(D, H) and NP > 0 and NP % 256 == 0
 
 
-def ffn_proj(x, ln0, w1, b1, act, slope, w2, b2, alpha, next_ln, wp, post_ln=None):
+def ffn_proj(x, ln0, w1, b1, act, slope, w2, b2, alpha, next_ln, wp, post_ln=None, deff=None):
     """sbk_ffn with the following block's input projection fused on chip:
     returns (out fp32, next_ln(out) · wp^T in bf16).  wp: (NP, D) bf16, no
-    bias (RelPosMHAXL's in_proj)."""
+    bias (RelPosMHAXL's in_proj).  deff: LayerNorm statistics over the first
+    deff columns (the rest zero-padded channels; default all)."""
     require_device(x, w1, w2, wp)
     gp, bp, ep = post_ln if post_ln is not None else (None, None, 0.0)
     return OPS.ffn_proj(x, ln0[0], ln0[1], float(ln0[2]), w1, b1, ACT[act], float(slope), w2, b2,
-                                  float(alpha), gp, bp, float(ep), next_ln[0], next_ln[1], float(next_ln[2]), wp)
+                                  float(alpha), gp, bp, float(ep), next_ln[0], next_ln[1], float(next_ln[2]), wp,
+                       int(deff or x.shape[1]))
 
 
 @custom_op("sbk::ffn_chain", mutates_args=())
@@ -409,13 +411,13 @@ def _ffn_chain_op(x: torch.Tensor, act: int, slope: float, g0: torch.Tensor, b0:
                   gp: Optional[torch.Tensor], bp: Optional[torch.Tensor], ep: float, g0b: torch.Tensor,
                   b0b: torch.Tensor, e0b: float, w1b: torch.Tensor, b1b: torch.Tensor, w2b: torch.Tensor,
                   b2b: torch.Tensor, alphab: float, gn: torch.Tensor, bn: torch.Tensor, en: float,
-                  wp: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+                  wp: torch.Tensor, deff: int) -> tuple[torch.Tensor, torch.Tensor]:
     M, D = x.shape
     H, NP = w1.shape[0], wp.shape[0]
     img = ffn_image(w1, w2, w1b, w2b, wp)
     out = torch.empty_like(x)
     y = torch.empty(M, NP, device=x.device, dtype=_bf16)
-    rc = lib().sbk_ffn_chain(ptr(x), M, D, H, act, float(slope), ptr(g0), ptr(b0), float(e0), ptr(b1), ptr(b2),
+    rc = lib().sbk_ffn_chain(ptr(x), M, D, deff, H, act, float(slope), ptr(g0), ptr(b0), float(e0), ptr(b1), ptr(b2),
                              float(alpha), ptr(gp), ptr(bp), float(ep), ptr(g0b), ptr(b0b), float(e0b), ptr(b1b),
                              ptr(b2b), float(alphab), ptr(out), ptr(gn), ptr(bn), float(en), None, 1, ptr(img), img.numel(), NP,
                              ptr(y), stream_of(x))
@@ -425,11 +427,11 @@ def _ffn_chain_op(x: torch.Tensor, act: int, slope: float, g0: torch.Tensor, b0:
 
 @_ffn_chain_op.register_fake
 def _(x, act, slope, g0, b0, e0, w1, b1, w2, b2, alpha, gp, bp, ep, g0b, b0b, e0b, w1b, b1b, w2b, b2b, alphab, gn,
-      bn, en, wp):
+      bn, en, wp, deff):
     return torch.empty_like(x), x.new_empty((x.shape[0], wp.shape[0]), dtype=_bf16)
 
 
-def ffn_chain(x, a, b, act, slope, next_ln, wp):
+def ffn_chain(x, a, b, act, slope, next_ln, wp, deff=None):
     """Two FFN blocks in one launch — a = (ln0, w1, b1, w2, b2, alpha,
     post_ln) then b = (ln0, w1, b1, w2, b2, alpha) on a's output, which stays
     on chip — followed by next_ln and the projection wp (bf16, no bias):
@@ -443,10 +445,11 @@ def ffn_chain(x, a, b, act, slope, next_ln, wp):
     gp, bp, ep = a[6] if a[6] is not None else (None, None, 0.0)
     return OPS.ffn_chain(x, ACT[act], float(slope), a[0][0], a[0][1], float(a[0][2]), a[1], a[2], a[3],
                                    a[4], float(a[5]), gp, bp, float(ep), b[0][0], b[0][1], float(b[0][2]), b[1], b[2],
-                                   b[3], b[4], float(b[5]), next_ln[0], next_ln[1], float(next_ln[2]), wp)
+                                   b[3], b[4], float(b[5]), next_ln[0], next_ln[1], float(next_ln[2]), wp,
+                         int(deff or x.shape[1]))
 
 
-def ffn(x, ln0, w1, b1, act, slope, w2, b2, alpha, post_ln=None, next_ln=None, next_dtype=_bf16, out=None):
+def ffn(x, ln0, w1, b1, act, slope, w2, b2, alpha, post_ln=None, next_ln=None, next_dtype=_bf16, out=None, deff=None):
     """Fused macaron FFN block (bf16 MFMA): z = x + alpha * FFN(LN0(x));
     out = post_ln(z) if given; u = next_ln(out) (returned) if given.
     x: (M, D) fp32; ln*: (weight, bias, eps); w1 (H, D), w2 (D, H) bf16.
@@ -456,7 +459,7 @@ def ffn(x, ln0, w1, b1, act, slope, w2, b2, alpha, post_ln=None, next_ln=None, n
     gp, bp, ep = post_ln if post_ln is not None else (None, None, 0.0)
     gn, bn, en = next_ln if next_ln is not None else (None, None, 0.0)
     y, u = OPS.ffn(x, ln0[0], ln0[1], float(ln0[2]), w1, b1, ACT[act], float(slope), w2, b2, float(alpha),
-                             gp, bp, float(ep), gn, bn, float(en), next_dtype == _bf16)
+                             gp, bp, float(ep), gn, bn, float(en), next_dtype == _bf16, int(deff or x.shape[1]))
     return y, (u if next_ln is not None else None)
 
 
@@ -492,10 +495,11 @@ def _conv_module_op(x: torch.Tensor, B: int, T: int, g0: torch.Tensor, b0: torch
                     w1p: torch.Tensor, b1p: torch.Tensor, wc: torch.Tensor, bc: Optional[torch.Tensor], causal: bool,
                     g1: torch.Tensor, b1: torch.Tensor, e1: float, w2: torch.Tensor, b2: Optional[torch.Tensor],
                     kpm: Optional[torch.Tensor], o: Optional[torch.Tensor], wo: Optional[torch.Tensor],
-                    bo: Optional[torch.Tensor]) -> torch.Tensor:
+                    bo: Optional[torch.Tensor], deff: int) -> torch.Tensor:
     K = wc.shape[0]  # wc: (K, d) tap-major
     out = torch.empty_like(x)
-    rc = lib().sbk_conv_module_pre(ptr(x), ptr(o), ptr(wo), ptr(bo), ptr(out), B, T, x.shape[1], ptr(g0), ptr(b0),
+    rc = lib().sbk_conv_module_pre(ptr(x), ptr(o), ptr(wo), ptr(bo), ptr(out), B, T, x.shape[1], deff, ptr(g0),
+                                   ptr(b0),
                                    float(e0), ptr(w1p), ptr(b1p), ptr(wc), ptr(bc), K, int(causal), ptr(g1), ptr(b1),
                                    float(e1), ptr(w2), ptr(b2), ptr(kpm), stream_of(x))
     check(rc, "sbk_conv_module_pre")
@@ -503,11 +507,11 @@ def _conv_module_op(x: torch.Tensor, B: int, T: int, g0: torch.Tensor, b0: torch
 
 
 @_conv_module_op.register_fake
-def _(x, B, T, g0, b0, e0, w1p, b1p, wc, bc, causal, g1, b1, e1, w2, b2, kpm, o, wo, bo):
+def _(x, B, T, g0, b0, e0, w1p, b1p, wc, bc, causal, g1, b1, e1, w2, b2, kpm, o, wo, bo, deff):
     return torch.empty_like(x)
 
 
-def conv_module(x, B, T, ln0, w1p, b1p, wc, bc, causal, ln1, w2, b2, kpm=None, pre=None):
+def conv_module(x, B, T, ln0, w1p, b1p, wc, bc, causal, ln1, w2, b2, kpm=None, pre=None, deff=None):
     """Fused Conformer convolution module (bf16 MFMA, one launch):
     x + rowmask0(after_conv(dwconv(GLU(pointwise(LN0(x)))))).  x: (B*T, 256) fp32.
     pre = (o, wo, bo): the module runs on x + o wo^T + bo (the MHSA output
@@ -515,7 +519,8 @@ def conv_module(x, B, T, ln0, w1p, b1p, wc, bc, causal, ln1, w2, b2, kpm=None, p
     require_device(x, w1p, w2)
     o, wo, bo = pre if pre is not None else (None, None, None)
     return OPS.conv_module(x, int(B), int(T), ln0[0], ln0[1], float(ln0[2]), w1p, b1p, wc, bc,
-                                     bool(causal), ln1[0], ln1[1], float(ln1[2]), w2, b2, kpm, o, wo, bo)
+                                     bool(causal), ln1[0], ln1[1], float(ln1[2]), w2, b2, kpm, o, wo, bo,
+                            int(deff or x.shape[1]))
 
 
 @custom_op("sbk::conv_block_c1", mutates_args=())

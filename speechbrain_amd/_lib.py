@@ -65,11 +65,11 @@ SIGNATURES = {
                                    _vp],
     # ffn.hip
     "sbk_ffn_supported": [_i, _i],
-    "sbk_ffn": [_vp, _i, _i, _i, _vp, _vp, _f, _vp, _ll, _vp, _i, _f, _vp, _f, _vp, _vp, _f, _vp, _vp, _vp, _f, _vp,
+    "sbk_ffn": [_vp, _i, _i, _i, _i, _vp, _vp, _f, _vp, _ll, _vp, _i, _f, _vp, _f, _vp, _vp, _f, _vp, _vp, _vp, _f, _vp,
                 _i, _vp],
-    "sbk_ffn_chain": [_vp, _i, _i, _i, _i, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _f,
+    "sbk_ffn_chain": [_vp, _i, _i, _i, _i, _i, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _f, _vp, _vp, _f,
                       _vp, _vp, _vp, _f, _vp, _i, _vp, _ll, _i, _vp, _vp],
-    "sbk_ffn_proj": [_vp, _i, _i, _i, _vp, _vp, _f, _vp, _ll, _vp, _i, _f, _vp, _f, _vp, _vp, _f, _vp, _vp, _vp, _f,
+    "sbk_ffn_proj": [_vp, _i, _i, _i, _i, _vp, _vp, _f, _vp, _ll, _vp, _i, _f, _vp, _f, _vp, _vp, _f, _vp, _vp, _vp, _f,
                      _vp, _i, _i, _vp, _vp],
     "sbk_ffn_image_elems": [_i, _i, _i, _i],
     "sbk_ffn_image": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp],
@@ -120,9 +120,9 @@ SIGNATURES = {
     "sbk_inorm_apply": [_vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp],
     # convmod.hip
     "sbk_conv_module_supported": [_i, _i],
-    "sbk_conv_module_pre": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _vp, _vp, _i, _i, _vp,
+    "sbk_conv_module_pre": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _vp, _vp, _i, _i, _vp,
                             _vp, _f, _vp, _vp, _vp, _vp],
-    "sbk_conv_module": [_vp, _vp, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _f, _vp, _vp, _vp,
+    "sbk_conv_module": [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _f, _vp, _vp, _vp,
                         _vp],
     # backward.hip (training path)
     "sbk_layernorm_bwd_blocks": [_i],

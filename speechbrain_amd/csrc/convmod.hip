@@ -89,6 +89,9 @@ struct ConvModArgs {
   const bf16_t* o;   // (B*T, D) attention output (heads concatenated)
   const bf16_t* wo;  // (D, D) out_proj weight
   const float* bo;   // (D) or null
+  // LayerNorm statistics over the first d_eff channels (the rest zero-padded,
+  // as in ffn.hip): inv_n = 1 / d_eff, npad = D - d_eff
+  float inv_n, npad;
 };
 
 // s_memtime phase marks of the waves of workgroup 100 (probe builds only)
@@ -345,9 +348,9 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
         t2 += q4.z;
         t2 += q4.w;
       }
-      const float mu = t * (1.0f / CM_D);
+      const float mu = t * a.inv_n;  // padded channels are zero: they add nothing to t or t2
       stat[row] = mu;
-      stat[CM_ROWS + row] = 1.0f / sqrtf(fmaxf(t2 * (1.0f / CM_D) - mu * mu, 0.f) + a.eps0);
+      stat[CM_ROWS + row] = 1.0f / sqrtf(fmaxf(t2 * a.inv_n - mu * mu, 0.f) + a.eps0);
     }
     lds_barrier();
     const float4 g04 = *reinterpret_cast<const float4*>(gb0s + u0);
@@ -383,11 +386,11 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       const int r = w + i * CM_NW, f = f0 + r;
       const bool live = r < nrows && f >= 0 && f < a.T;
       const float v[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
-      const float mean = wave_sum_v(v[0] + v[1] + v[2] + v[3]) * (1.0f / CM_D);
+      const float mean = wave_sum_v(v[0] + v[1] + v[2] + v[3]) * a.inv_n;
       float q = 0.f;
 #pragma unroll
       for (int e = 0; e < 4; ++e) q += (v[e] - mean) * (v[e] - mean);
-      const float rstd = 1.0f / sqrtf(wave_sum_v(q) * (1.0f / CM_D) + a.eps0);
+      const float rstd = 1.0f / sqrtf((wave_sum_v(q) - a.npad * mean * mean) * a.inv_n + a.eps0);
       uint2 pk = make_uint2(0u, 0u);
       if (live) {
         pk.x = pack_bf16x2((v[0] - mean) * rstd * g04.x + b04.x, (v[1] - mean) * rstd * g04.y + b04.y);
@@ -565,7 +568,7 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       v[u][0] = v4.x; v[u][1] = v4.y; v[u][2] = v4.z; v[u][3] = v4.w;
     }
 #pragma unroll
-    for (int u = 0; u < FPW; ++u) mean[u] = wave_sum_v((v[u][0] + v[u][1]) + (v[u][2] + v[u][3])) * (1.0f / CM_D);
+    for (int u = 0; u < FPW; ++u) mean[u] = wave_sum_v((v[u][0] + v[u][1]) + (v[u][2] + v[u][3])) * a.inv_n;
 #pragma unroll
     for (int u = 0; u < FPW; ++u) {
       float q = 0.f;
@@ -574,7 +577,8 @@ __global__ void __launch_bounds__(CM_NT) conv_module_kernel(ConvModArgs a) {
       rstd[u] = q;
     }
 #pragma unroll
-    for (int u = 0; u < FPW; ++u) rstd[u] = 1.0f / sqrtf(wave_sum_v(rstd[u]) * (1.0f / CM_D) + a.eps1);
+    for (int u = 0; u < FPW; ++u)
+      rstd[u] = 1.0f / sqrtf((wave_sum_v(rstd[u]) - a.npad * mean[u] * mean[u]) * a.inv_n + a.eps1);
 #pragma unroll
     for (int u = 0; u < FPW; ++u) {
 #pragma unroll
@@ -646,11 +650,12 @@ SBK_PROBE_EXPORT(sbk_probe_cm_tl, g_cm_tl)
 SBK_API int sbk_conv_module_supported(int D, int K) { return D == CM_D && K >= 1 && K <= CM_KMAX; }
 
 SBK_API int sbk_conv_module_pre(const float* x, const void* o, const void* wo, const float* bo, float* out, int B,
-                                int T, int D, const float* ln0_w, const float* ln0_b, float eps0, const void* w1p,
+                                int T, int D, int d_eff, const float* ln0_w, const float* ln0_b, float eps0, const void* w1p,
                                 const float* b1p, const float* wc, const float* bc, int K, int causal,
                                 const float* ln1_w, const float* ln1_b, float eps1, const void* w2, const float* b2,
                                 const unsigned char* kpm, void* stream) {
-  if (B <= 0 || T <= 0 || !sbk_conv_module_supported(D, K) || !x || !out || x == out) return SBK_ERR_ARG;
+  if (B <= 0 || T <= 0 || !sbk_conv_module_supported(D, K) || !x || !out || x == out || d_eff <= 0 || d_eff > D)
+    return SBK_ERR_ARG;
   if (o && (causal ? K - 1 : (K - 1) / 2) > 31) return SBK_ERR_ARG;  // phase -1 lane map: padL < 32
   if (!ln0_w || !ln0_b || !w1p || !b1p || !wc || !ln1_w || !ln1_b || !w2) return SBK_ERR_ARG;
   const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
@@ -670,6 +675,7 @@ SBK_API int sbk_conv_module_pre(const float* x, const void* o, const void* wo, c
   a.w2 = reinterpret_cast<const bf16_t*>(w2); a.b2 = b2;
   a.kpm = reinterpret_cast<const uint8_t*>(kpm);
   a.o = reinterpret_cast<const bf16_t*>(o); a.wo = reinterpret_cast<const bf16_t*>(wo); a.bo = bo;
+  a.inv_n = 1.0f / (float)d_eff; a.npad = (float)(D - d_eff);
   const long long grid = (long long)B * ((T + CM_BM - 1) / CM_BM);
   if (grid > 0x7fffffffLL) return SBK_ERR_ARG;
   constexpr size_t lds = conv_module_lds();
@@ -685,10 +691,11 @@ SBK_API int sbk_conv_module_pre(const float* x, const void* o, const void* wo, c
   return 0;
 }
 
-SBK_API int sbk_conv_module(const float* x, float* out, int B, int T, int D, const float* ln0_w, const float* ln0_b,
+SBK_API int sbk_conv_module(const float* x, float* out, int B, int T, int D, int d_eff, const float* ln0_w,
+                            const float* ln0_b,
                             float eps0, const void* w1p, const float* b1p, const float* wc, const float* bc, int K,
                             int causal, const float* ln1_w, const float* ln1_b, float eps1, const void* w2,
                             const float* b2, const unsigned char* kpm, void* stream) {
-  return sbk_conv_module_pre(x, nullptr, nullptr, nullptr, out, B, T, D, ln0_w, ln0_b, eps0, w1p, b1p, wc, bc, K,
+  return sbk_conv_module_pre(x, nullptr, nullptr, nullptr, out, B, T, D, d_eff, ln0_w, ln0_b, eps0, w1p, b1p, wc, bc, K,
                              causal, ln1_w, ln1_b, eps1, w2, b2, kpm, stream);
 }

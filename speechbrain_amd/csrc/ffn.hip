@@ -105,6 +105,11 @@ struct FfnArgs {
   float eps0b;
   const float *b1b, *b2b;
   float alphab;
+  // LayerNorm statistics over the first d_eff of the D columns (the others
+  // are zero-padded channels: D = 256 carrying a d_model < 256 model whose
+  // LN gains / biases and weight rows are zero there): inv_n = 1 / d_eff,
+  // npad = D - d_eff (each padded zero adds mean^2 to the centred sum)
+  float inv_n, npad;
 };
 
 __device__ __forceinline__ bf16x8 ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
@@ -216,7 +221,7 @@ __device__ __forceinline__ void vm_wait(int n) {
 // chain launch than two barriers over one buffer.)
 template <int D, int T2, int MT, int NW>
 __device__ __forceinline__ void row_ln(float (&z)[T2][MT][4], float* red, const float* gam, const float* bet, float eps,
-                                       int w, int g, int fr) {
+                                       int w, int g, int fr, float inv_n, float npad) {
   static_assert(NW == 8, "two b128 reads per row");
   float mean[MT], rstd[MT];
 #pragma unroll
@@ -253,9 +258,9 @@ __device__ __forceinline__ void row_ln(float (&z)[T2][MT][4], float* red, const 
       const float t = (rv[mt][0][0] + rv[mt][0][1]) + (rv[mt][0][2] + rv[mt][0][3]) + (rv[mt][1][0] + rv[mt][1][1]) +
                       (rv[mt][1][2] + rv[mt][1][3]);
       if (pass)
-        rstd[mt] = 1.0f / sqrtf(t / D + eps);
+        rstd[mt] = 1.0f / sqrtf((t - npad * mean[mt] * mean[mt]) * inv_n + eps);
       else
-        mean[mt] = t / D;
+        mean[mt] = t * inv_n;
     }
   }
   f32x4 gv[T2], bv[T2];
@@ -414,11 +419,11 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     if (rr >= BM) break;
     const bool live = m0 + rr < a.M;
     const float v[4] = {live ? xv[i][0] : 0.f, live ? xv[i][1] : 0.f, live ? xv[i][2] : 0.f, live ? xv[i][3] : 0.f};
-    const float mean = wave_sum_v(v[0] + v[1] + v[2] + v[3]) / D;
+    const float mean = wave_sum_v(v[0] + v[1] + v[2] + v[3]) * a.inv_n;
     float q = 0.f;
 #pragma unroll
     for (int e = 0; e < 4; ++e) q += (v[e] - mean) * (v[e] - mean);
-    const float rstd = 1.0f / sqrtf(wave_sum_v(q) / D + a.eps0);
+    const float rstd = 1.0f / sqrtf((wave_sum_v(q) - a.npad * mean * mean) * a.inv_n + a.eps0);
     uint2 pk;
     pk.x = pack_bf16x2((v[0] - mean) * rstd * g04[0] + b04[0], (v[1] - mean) * rstd * g04[1] + b04[1]);
     pk.y = pack_bf16x2((v[2] - mean) * rstd * g04[2] + b04[2], (v[3] - mean) * rstd * g04[3] + b04[3]);
@@ -546,13 +551,13 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
       }
     }
     FFN_TL(200);
-    if (a.gp) row_ln<D, T, MT, NW>(z, red, prm + P_GP * D, prm + P_BP * D, a.epsp, w, g, fr);
+    if (a.gp) row_ln<D, T, MT, NW>(z, red, prm + P_GP * D, prm + P_BP * D, a.epsp, w, g, fr, a.inv_n, a.npad);
     FFN_TL(201);
 #pragma unroll
     for (int j = 0; j < T; ++j)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) xres[j][mt] = f32x4{z[j][mt][0], z[j][mt][1], z[j][mt][2], z[j][mt][3]};
-    row_ln<D, T, MT, NW>(z, red, prm + P_G0B * D, prm + P_B0B * D, a.eps0b, w, g, fr);
+    row_ln<D, T, MT, NW>(z, red, prm + P_G0B * D, prm + P_B0B * D, a.eps0b, w, g, fr, a.inv_n, a.npad);
     FFN_TL(202);
 #pragma unroll
     for (int j = 0; j < T; ++j) {
@@ -608,7 +613,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     }
   }
   FFN_TL(195);
-  if (postln) row_ln<D, T, MT, NW>(z, red, prm + P_GP * D, prm + P_BP * D, a.epsp, w, g, fr);
+  if (postln) row_ln<D, T, MT, NW>(z, red, prm + P_GP * D, prm + P_BP * D, a.epsp, w, g, fr, a.inv_n, a.npad);
   if (PROJ) {
     // the out rows wait in LDS (over the hidden-chunk buffers, free once the
     // row_ln barriers have passed) until the last weight tile has landed: a
@@ -622,7 +627,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) xres[j][mt] = f32x4{z[j][mt][0], z[j][mt][1], z[j][mt][2], z[j][mt][3]};
     // u = next-LN(out) -> Xn (bf16) -> VGPR fragments, the A operand of the projection
-    row_ln<D, T, MT, NW>(z, red, prm + P_GN * D, prm + P_BN * D, a.epsn, w, g, fr);
+    row_ln<D, T, MT, NW>(z, red, prm + P_GN * D, prm + P_BN * D, a.epsn, w, g, fr, a.inv_n, a.npad);
     FFN_TL(204);
 #pragma unroll
     for (int j = 0; j < T; ++j) {
@@ -762,7 +767,7 @@ __global__ void __launch_bounds__(FFN_NT) ffn_kernel(FfnArgs a) {
     }
   }
   if (a.gn) {
-    row_ln<D, T, MT, NW>(z, red, prm + P_GN * D, prm + P_BN * D, a.epsn, w, g, fr);
+    row_ln<D, T, MT, NW>(z, red, prm + P_GN * D, prm + P_BN * D, a.epsn, w, g, fr, a.inv_n, a.npad);
 #pragma unroll
     for (int j = 0; j < T; ++j) {
       const int d = (w * T + j) * 16 + 4 * g;
@@ -926,13 +931,15 @@ int ffn_check(const float* x, int M, int D, int H, const float* g0, const float*
 }
 }  // namespace
 
-SBK_API int sbk_ffn_proj(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0,
+SBK_API int sbk_ffn_proj(const float* x, int M, int D, int d_eff, int H, const float* g0, const float* b0, float eps0,
                          const void* img, long long img_elems, const float* b1, int act, float slope, const float* b2,
                          float alpha, const float* gp, const float* bp, float epsp, float* out, const float* gn,
                          const float* bn, float epsn, void* u, int u_bf16, int np, void* yp, void* stream) {
-  if (ffn_check(x, M, D, H, g0, b0, img, img_elems, 0, b1, act, b2, gp, bp, out, gn, bn, u, np, yp))
+  if (ffn_check(x, M, D, H, g0, b0, img, img_elems, 0, b1, act, b2, gp, bp, out, gn, bn, u, np, yp) || d_eff <= 0 ||
+      d_eff > D)
     return SBK_ERR_ARG;
   FfnArgs a;
+  a.inv_n = 1.0f / (float)d_eff; a.npad = (float)(D - d_eff);
   a.x = x; a.M = M; a.H = H;
   a.g0 = g0; a.b0 = b0; a.eps0 = eps0;
   a.img = reinterpret_cast<const bf16_t*>(img); a.b1 = b1; a.act = act; a.slope = slope;
@@ -953,7 +960,8 @@ SBK_API int sbk_ffn_proj(const float* x, int M, int D, int H, const float* g0, c
 // Conformer layer i) then block B (g0b .. alphab: FFN1 of layer i+1, no
 // post-LN), then next-LN / projection tail as sbk_ffn_proj.  out receives
 // block B's output only.  img: sbk_ffn_image of (w1, w2, w1b, w2b, wp).
-SBK_API int sbk_ffn_chain(const float* x, int M, int D, int H, int act, float slope, const float* g0, const float* b0,
+SBK_API int sbk_ffn_chain(const float* x, int M, int D, int d_eff, int H, int act, float slope, const float* g0,
+                          const float* b0,
                           float eps0, const float* b1, const float* b2, float alpha, const float* gp, const float* bp,
                           float epsp, const float* g0b, const float* b0b, float eps0b, const float* b1b,
                           const float* b2b, float alphab, float* out, const float* gn, const float* bn, float epsn,
@@ -963,9 +971,11 @@ SBK_API int sbk_ffn_chain(const float* x, int M, int D, int H, int act, float sl
   if ((reinterpret_cast<uintptr_t>(g0b) | reinterpret_cast<uintptr_t>(b0b) | reinterpret_cast<uintptr_t>(b1b) |
        reinterpret_cast<uintptr_t>(b2b)) & 15)
     return SBK_ERR_ARG;
-  if (ffn_check(x, M, D, H, g0, b0, img, img_elems, 1, b1, act, b2, gp, bp, out, gn, bn, u, np, yp))
+  if (ffn_check(x, M, D, H, g0, b0, img, img_elems, 1, b1, act, b2, gp, bp, out, gn, bn, u, np, yp) || d_eff <= 0 ||
+      d_eff > D)
     return SBK_ERR_ARG;
   FfnArgs a;
+  a.inv_n = 1.0f / (float)d_eff; a.npad = (float)(D - d_eff);
   a.x = x; a.M = M; a.H = H;
   a.g0 = g0; a.b0 = b0; a.eps0 = eps0;
   a.img = reinterpret_cast<const bf16_t*>(img); a.b1 = b1; a.act = act; a.slope = slope;
@@ -982,10 +992,10 @@ SBK_API int sbk_ffn_chain(const float* x, int M, int D, int H, int act, float sl
   return 0;
 }
 
-SBK_API int sbk_ffn(const float* x, int M, int D, int H, const float* g0, const float* b0, float eps0,
+SBK_API int sbk_ffn(const float* x, int M, int D, int d_eff, int H, const float* g0, const float* b0, float eps0,
                     const void* img, long long img_elems, const float* b1, int act, float slope, const float* b2,
                     float alpha, const float* gp, const float* bp, float epsp, float* out, const float* gn,
                     const float* bn, float epsn, void* u, int u_bf16, void* stream) {
-  return sbk_ffn_proj(x, M, D, H, g0, b0, eps0, img, img_elems, b1, act, slope, b2, alpha, gp, bp, epsp, out, gn, bn,
+  return sbk_ffn_proj(x, M, D, d_eff, H, g0, b0, eps0, img, img_elems, b1, act, slope, b2, alpha, gp, bp, epsp, out, gn, bn,
                       epsn, u, u_bf16, 0, nullptr, stream);
 }

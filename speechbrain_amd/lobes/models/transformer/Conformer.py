@@ -44,6 +44,10 @@ USE_CONV_MODULE_KERNEL = True
 # FFN2 (+ norm2) of layer i and FFN1 (+ norm1 + in_proj) of layer i+1 in one
 # launch (sbk_ffn_chain), the out_proj in the conv module's prologue
 USE_LAYER_CHAIN = True
+# bf16 stacks with d_model < 256 (conformer_small.yaml: 144) on a zero-padded
+# D = 256 copy, so they take the fused kernels (_PaddedEncoder)
+USE_PADDED_SHADOW = True
+PAD_D = 256
 
 
 def _check_swish(act_module):
@@ -55,6 +59,8 @@ def _check_swish(act_module):
 
 class ConvolutionModule(nn.Module):
     """Conformer.py:24-115."""
+
+    _deff = None  # zero-padded shadow copies (_PaddedEncoder): LN statistics over this many channels
 
     def __init__(self, input_size, kernel_size=31, bias=True, activation=Swish, dropout=0.0, causal=False,
                  dilation=1):
@@ -137,7 +143,8 @@ class ConvolutionModule(nn.Module):
         return _enc.conv_module(x2d, B, T, self.ln_params(), w1p, b1p, wc,
                                 self.conv.bias.detach() if self.conv.bias is not None else None, self.causal,
                                 (ln.weight.detach(), ln.bias.detach(), ln.eps), w2,
-                                lin.bias.detach() if lin.bias is not None else None, pad_mask_u8, pre=pre)
+                                lin.bias.detach() if lin.bias is not None else None, pad_mask_u8, pre=pre,
+                                deff=self._deff)
 
     def train_run(self, x2d, B, T, dtype, pad_mask_u8=None, residual=None):
         """Differentiable chain (training path, _autograd): residual +
@@ -373,10 +380,16 @@ class ConformerEncoder(nn.Module):
 
     def run(self, src2d, B, T, pos_embs, kpm_u8, dtype, need_attn, am=None):
         """Fused stack on (B*T, d) fp32 → ((B*T, d) fp32, [attn]); am: the
-        src_mask as _enc.attn_mask_arg (takes the per-layer path)."""
+        src_mask as _enc.attn_mask_arg (takes the per-layer path).  A bf16
+        stack with d_model < 256 runs on its zero-padded D = 256 shadow
+        (_PaddedEncoder) when that shadow takes the layer chain."""
         if self.wants_train_path(src2d):
             return self.train_run(src2d, B, T, pos_embs, kpm_u8, dtype, am=am)
         d = src2d.shape[1]
+        if USE_PADDED_SHADOW and am is None and dtype == _bf16 and d < PAD_D:
+            sh = _PaddedEncoder.of(self)
+            if sh is not None:
+                return sh.run(src2d, B, T, pos_embs, kpm_u8, dtype, need_attn)
         pos = _enc.to_compute(pos_embs.reshape(-1, d), dtype)
         pk_all = _enc.gemm(pos, self.stacked_pos_weight(dtype), out_dtype=dtype)  # (2T-1, L*d)
         x = src2d
@@ -429,7 +442,8 @@ class ConformerEncoder(nn.Module):
                 a = f2[1].chain_block(ln(layer, f2[0]), 0.5, post_ln=ln(layer, layer.norm2.norm))
                 b = nl.ffn_module1[1].chain_block(ln(nl, nl.ffn_module1[0]), 0.5)
                 act, slope = f2[1].act_name()
-                x, qkv = _enc.ffn_chain(x, a, b, act, slope, ln(nl, nl.norm1.norm), nl.mha_layer.fused_in_proj(dtype))
+                x, qkv = _enc.ffn_chain(x, a, b, act, slope, ln(nl, nl.norm1.norm), nl.mha_layer.fused_in_proj(dtype),
+                                        deff=f2[1]._deff)
             else:
                 fn = self.norm.norm
                 _, y = f2[1].run_fused(x, ln(layer, f2[0]), 0.5, post_ln=ln(layer, layer.norm2.norm),
@@ -456,3 +470,140 @@ class ConformerEncoder(nn.Module):
         y, attns = self.run(src.float().reshape(B * T, d).contiguous(), B, T, pos_embs, kpm,
                             _enc.compute_dtype(), True, am=am)
         return y.view(B, T, d), attns
+
+
+class _PaddedEncoder:
+    """A ConformerEncoder with d_model < 256 (conformer_small.yaml:96-100:
+    144) as a zero-padded D = 256 shadow, so its bf16 inference runs the
+    fused layer chain, rel-pos attention and convolution-module kernels,
+    which are built for 256 channels and 64-dim heads.
+
+    Residual-stream channels d..255 are zero and stay zero: every LayerNorm
+    gain / bias, weight row that writes them and weight column that reads
+    them is zero, so GEMM sums, the GLU, the depthwise taps and Swish see
+    exact zeros there; the kernels take d_eff = d for their LayerNorm
+    statistics (sbk_ffn / sbk_conv_module: mean over d, the centred sum less
+    the (256 - d) mean^2 the padded zeros add).  Attention heads are padded
+    from d / H to 64 dims (q, k, v, the positional rows, pos_bias_u / v), with
+    the reference's scale 1 / sqrt(d) kept — identical scores and
+    probabilities.  Results equal the unpadded bf16 arithmetic up to MFMA
+    summation order.  Built once per parameter version (weights are copied,
+    not shared) and cached on the encoder."""
+
+    def __init__(self, enc, dev):
+        d = enc.norm.norm.weight.shape[0]
+        l0 = enc.layers[0]
+        H = l0.mha_layer.num_heads
+        K = l0.convolution_module.conv.weight.shape[-1]
+        F = l0.ffn_module1[1].ffn[0].out_features
+        act = type(l0.ffn_module1[1].ffn[1])
+        self.d = d
+        with torch.random.fork_rng(devices=[]):  # the shadow's own init must not move the global RNG
+            sh = ConformerEncoder(len(enc.layers), PAD_D, F, H, kernel_size=K, activation=act,
+                                  bias=l0.convolution_module.conv.bias is not None,
+                                  causal=l0.convolution_module.causal)
+        sh = sh.to(dev).eval()
+        dh, dp = d // H, PAD_D // H
+        hmap = torch.tensor([h * dp + i for h in range(H) for i in range(dh)], device=dev)
+        qmap = torch.tensor([h * 3 * dp + p * dp + i for h in range(H) for p in range(3) for i in range(dh)],
+                            device=dev)
+        gmap = torch.cat([torch.arange(d, device=dev), PAD_D + torch.arange(d, device=dev)])
+
+        def put(dst, src, rows=None, cols=None):
+            """zero dst, then dst[rows][:, cols] = src (None: the leading range)."""
+            src = src.detach().to(dev, torch.float32)
+            dst.zero_()
+            r = rows if rows is not None else torch.arange(src.shape[0], device=dev)
+            if dst.dim() == 1:
+                dst[r] = src
+                return
+            tmp = torch.zeros(src.shape[0], *dst.shape[1:], device=dev)
+            if cols is None:
+                tmp[:, :src.shape[1]] = src
+            else:
+                tmp[:, cols] = src
+            dst[r] = tmp
+
+        with torch.no_grad():
+            for lr, ls in zip(enc.layers, sh.layers):
+                for fr_, fs in ((lr.ffn_module1, ls.ffn_module1), (lr.ffn_module2, ls.ffn_module2)):
+                    put(fs[0].weight, fr_[0].weight)
+                    put(fs[0].bias, fr_[0].bias)
+                    put(fs[1].ffn[0].weight, fr_[1].ffn[0].weight, rows=torch.arange(F, device=dev))
+                    put(fs[1].ffn[0].bias, fr_[1].ffn[0].bias, rows=torch.arange(F, device=dev))
+                    put(fs[1].ffn[3].weight, fr_[1].ffn[3].weight)
+                    put(fs[1].ffn[3].bias, fr_[1].ffn[3].bias)
+                    fs[1]._deff = d
+                mr, ms = lr.mha_layer, ls.mha_layer
+                put(ms.in_proj_weight, mr.in_proj_weight, rows=qmap)
+                # the (dh, H) biases are read as (H, dh) (attention.py:586-592): flat h * dh + i -> h * 64 + i
+                put(ms.pos_bias_u.view(-1), mr.pos_bias_u.reshape(-1), rows=hmap)
+                put(ms.pos_bias_v.view(-1), mr.pos_bias_v.reshape(-1), rows=hmap)
+                put(ms.linear_pos.weight, mr.linear_pos.weight, rows=hmap)
+                put(ms.out_proj.weight, mr.out_proj.weight, cols=hmap)
+                put(ms.out_proj.bias, mr.out_proj.bias)
+                ms.scale = mr.scale
+                cr, cs = lr.convolution_module, ls.convolution_module
+                put(cs.layer_norm.weight, cr.layer_norm.weight)
+                put(cs.layer_norm.bias, cr.layer_norm.bias)
+                put(cs.bottleneck[0].weight.view(2 * PAD_D, PAD_D), cr.bottleneck[0].weight.view(2 * d, d), rows=gmap)
+                if cr.bottleneck[0].bias is not None:
+                    put(cs.bottleneck[0].bias, cr.bottleneck[0].bias, rows=gmap)
+                put(cs.conv.weight.view(PAD_D, K), cr.conv.weight.view(d, K))
+                if cr.conv.bias is not None:
+                    put(cs.conv.bias, cr.conv.bias)
+                put(cs.after_conv[0].weight, cr.after_conv[0].weight)
+                put(cs.after_conv[0].bias, cr.after_conv[0].bias)
+                put(cs.after_conv[2].weight, cr.after_conv[2].weight)
+                if cr.after_conv[2].bias is not None:
+                    put(cs.after_conv[2].bias, cr.after_conv[2].bias)
+                cs._deff = d
+                for nr, ns in ((lr.norm1.norm, ls.norm1.norm), (lr.norm2.norm, ls.norm2.norm)):
+                    put(ns.weight, nr.weight)
+                    put(ns.bias, nr.bias)
+                    ns.eps = nr.eps
+                for a, b in ((lr.ffn_module1[0], ls.ffn_module1[0]), (lr.ffn_module2[0], ls.ffn_module2[0]),
+                             (cr.layer_norm, cs.layer_norm), (cr.after_conv[0], cs.after_conv[0])):
+                    b.eps = a.eps
+            put(sh.norm.norm.weight, enc.norm.norm.weight)
+            put(sh.norm.norm.bias, enc.norm.norm.bias)
+            sh.norm.norm.eps = enc.norm.norm.eps
+        self.sh = sh
+        self._pos = {}
+
+    @staticmethod
+    def of(enc):
+        """The encoder's shadow for its current parameters (None when the
+        padded stack would not take the layer chain)."""
+        ps = list(enc.parameters())
+        dev = ps[0].device
+        sig = (str(dev),) + tuple((p.data_ptr(), p._version) for p in ps)
+        hit = getattr(enc, "_padded_shadow", None)
+        if hit is not None and hit[0] == sig:
+            return hit[1]
+        l0 = enc.layers[0]
+        d = enc.norm.norm.weight.shape[0]
+        ok = (l0.attention_type == "RelPosMHAXL" and not l0.module_layer and d % l0.mha_layer.num_heads == 0
+              and PAD_D % l0.mha_layer.num_heads == 0 and l0.mha_layer.vbias is None
+              and l0.mha_layer._qkv_same_embed_dim and enc._uniform_ffns())
+        shadow = None
+        if ok:
+            shadow = _PaddedEncoder(enc, dev)
+            if not (all(layer.chainable(_bf16, PAD_D) for layer in shadow.sh.layers) and shadow.sh._uniform_ffns()):
+                shadow = None
+        enc._padded_shadow = (sig, shadow)
+        return shadow
+
+    def run(self, src2d, B, T, pos_embs, kpm_u8, dtype, need_attn):
+        d = self.d
+        x = torch.zeros(src2d.shape[0], PAD_D, device=src2d.device, dtype=torch.float32)
+        x[:, :d] = src2d
+        key = (pos_embs.data_ptr(), tuple(pos_embs.shape), dtype)
+        pos = self._pos.get(key)
+        if pos is None:  # the positional table (a per-T constant) padded to 256 columns once
+            p = pos_embs.reshape(-1, d)
+            pos = torch.zeros(p.shape[0], PAD_D, device=p.device, dtype=dtype)
+            pos[:, :d] = p.to(dtype)
+            self._pos = {key: pos}
+        y, attns = self.sh.run(x, B, T, pos, kpm_u8, dtype, need_attn)
+        return y[:, :d].contiguous(), attns

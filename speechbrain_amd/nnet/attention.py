@@ -194,24 +194,42 @@ class RelPosMHAXL(nn.Module):
         out = A.linear(o, self.out_proj.weight, self.out_proj.bias, dtype, self._wc, "t_out", res=residual)
         return out, attn
 
-    def cross_forward(self, query, key, value, pos_embs, key_padding_mask=None, attn_mask=None):
+    def cross_forward(self, query, key, value, pos_embs, key_padding_mask=None, attn_mask=None, self_att=False):
         """attention.py:554-639 for query != key / value: separate q / k / v
         projections on the MFMA GEMM (the row chunks of in_proj_weight,
         :555-564; vbias as the v projection's bias, :576-579), linear_pos, the
         cross-length rel-pos core (csrc/xattn.hip: rel_shift of the
         (q_len, 2*k_len-1) band incl. mask_pos_future) and out_proj, each
-        differentiable.  Returns (out (B, Lq, E), attention weights)."""
+        differentiable.  self_att: the self-attention projection layout
+        instead (:546-553: in_proj rows per head [q_h | k_h | v_h]), for
+        heads wider than the fused kernels take.  Returns (out (B, Lq, E),
+        attention weights)."""
         B, Lq, E = query.shape
         Lk = key.shape[1]
         if value.shape[:2] != key.shape[:2]:
             raise ValueError(f"key {tuple(key.shape)} and value {tuple(value.shape)} lengths differ")
         dtype = _enc.compute_dtype()
         H, dh = self.num_heads, self.head_dim
-        wq, wk, wv = self.in_proj_weight.chunk(3, dim=0)
+        if self_att:
+            w3 = self.in_proj_weight.view(H, 3, dh, E)
+            wq, wk, wv = (w3[:, i].reshape(H * dh, E) for i in range(3))
+        else:
+            wq, wk, wv = self.in_proj_weight.chunk(3, dim=0)
         vb = self.value_bias_weight if self.vbias is not None else None
-        q = A.linear(query.reshape(B * Lq, E), wq, None, dtype, self._wc, "x_q", out_dtype=dtype)
-        k = A.linear(key.reshape(B * Lk, E), wk, None, dtype, self._wc, "x_k", out_dtype=dtype)
-        v = A.linear(value.reshape(B * Lk, E), wv, vb, dtype, self._wc, "x_v", out_dtype=dtype)
+        if self_att:
+            # kernel copies of the per-head slices, cached against in_proj_weight
+            # itself (the slices are fresh tensors every call)
+            def lin(x, i, w, b):
+                wk_ = self._wc.get(("s", i, dtype), [self.in_proj_weight],
+                                   lambda: A.kernel_weight(w.detach().contiguous(), dtype, _enc.WeightCache(), "k"))
+                return A.LinearFn.apply(A.to_dtype(x, dtype), w, b, wk_, dtype, None, 1.0, None)
+            q = lin(query.reshape(B * Lq, E), 0, wq, None)
+            k = lin(key.reshape(B * Lk, E), 1, wk, None)
+            v = lin(value.reshape(B * Lk, E), 2, wv, vb)
+        else:
+            q = A.linear(query.reshape(B * Lq, E), wq, None, dtype, self._wc, "x_q", out_dtype=dtype)
+            k = A.linear(key.reshape(B * Lk, E), wk, None, dtype, self._wc, "x_k", out_dtype=dtype)
+            v = A.linear(value.reshape(B * Lk, E), wv, vb, dtype, self._wc, "x_v", out_dtype=dtype)
         pk = A.linear(pos_embs.reshape(-1, E), self.linear_pos.weight, None, dtype, self._wc, "x_pos",
                       out_dtype=dtype)
         kpm = key_padding_mask.to(query.device, torch.uint8).contiguous() if key_padding_mask is not None else None
@@ -233,10 +251,10 @@ class RelPosMHAXL(nn.Module):
         masked) or additive float (:598-611)."""
         if not self._qkv_same_embed_dim:
             raise NotImplementedError  # the reference raises too (attention.py:566)
-        if (self.head_dim > FUSED_DH_MAX
-                or not ((query is key or (query.shape == key.shape and torch.equal(query, key)))
-                        and (key is value or (key.shape == value.shape and torch.equal(key, value))))):
-            out, attn = self.cross_forward(query, key, value, pos_embs, key_padding_mask, attn_mask)
+        same = ((query is key or (query.shape == key.shape and torch.equal(query, key)))
+                and (key is value or (key.shape == value.shape and torch.equal(key, value))))
+        if not same or self.head_dim > FUSED_DH_MAX:
+            out, attn = self.cross_forward(query, key, value, pos_embs, key_padding_mask, attn_mask, self_att=same)
             return (out, attn) if return_attn_weights else out
         B, T, d = query.shape
         dtype = _enc.compute_dtype()
@@ -257,6 +275,8 @@ class RelPosMHAXL(nn.Module):
 class PositionalwiseFeedForward(nn.Module):
     """attention.py:781-839: Linear → activation → Dropout → Linear, the
     activation fused into the first GEMM's epilogue."""
+
+    _deff = None  # zero-padded shadow copies (Conformer._PaddedEncoder): LN statistics over this many columns
 
     def __init__(self, d_ffn, input_shape=None, input_size=None, dropout=0.0, activation=nn.ReLU):
         super().__init__()
@@ -324,7 +344,7 @@ class PositionalwiseFeedForward(nn.Module):
         b1, b2 = (lin.bias.detach() if lin.bias is not None else torch.zeros(lin.out_features, device=x.device)
                   for lin in (self.ffn[0], self.ffn[3]))
         return _enc.ffn(x, ln0, w1, b1, act, slope, w2, b2, alpha,
-                        post_ln=post_ln, next_ln=next_ln, next_dtype=next_dtype, out=out)
+                        post_ln=post_ln, next_ln=next_ln, next_dtype=next_dtype, out=out, deff=self._deff)
 
     def chain_block(self, ln0, alpha, post_ln=None):
         """This block's parameters for _enc.ffn_chain: (ln0, w1, b1, w2, b2,
@@ -341,7 +361,8 @@ class PositionalwiseFeedForward(nn.Module):
         act, slope = self.act_name()
         b1, b2 = (lin.bias.detach() if lin.bias is not None else torch.zeros(lin.out_features, device=x.device)
                   for lin in (self.ffn[0], self.ffn[3]))
-        return _enc.ffn_proj(x, ln0, w1, b1, act, slope, w2, b2, alpha, next_ln, wp, post_ln=post_ln)
+        return _enc.ffn_proj(x, ln0, w1, b1, act, slope, w2, b2, alpha, next_ln, wp, post_ln=post_ln,
+                             deff=self._deff)
 
     def forward(self, x):
         shp = x.shape

@@ -33,16 +33,20 @@ def _oracle(wav, wav_len, sd_cnn, sd_tr, bf16):
         return OC.fbank_to_encoder(wav, sd_cnn, sd_tr, 12, 4, n_mels=80, wav_len=wav_len)
 
 
-@pytest.mark.parametrize("lens", [(1.0, 1.0), (1.0, 0.73)])
-def test_bench_step_vs_fp32_oracle(dev, lens):
+@pytest.mark.parametrize("d_model,lens", [(256, (1.0, 1.0)), (256, (1.0, 0.73)), (144, (1.0, 0.73))])
+def test_bench_step_vs_fp32_oracle(dev, d_model, lens):
+    """d_model 144 (conformer_small.yaml:96-100) runs on the zero-padded
+    D = 256 shadow (Conformer.py _PaddedEncoder), same derived bound."""
     import bench
-    fbank, cnn, tr = bench.build_model(256, dev)
+    fbank, cnn, tr = bench.build_model(d_model, dev)
     g = torch.Generator().manual_seed(1234)
     wav = 0.1 * torch.randn(2, int(bench.SR * bench.SECONDS), generator=g)
     wav_len = torch.tensor(lens)
     wd, ld = wav.to(dev), wav_len.to(dev)
     step = bench.make_step(fbank, cnn, tr, wd, ld)
     out = step().float()
+    if d_model < 256:
+        assert tr.encoder._padded_shadow[1] is not None, "the padded shadow must carry the d < 256 stack"
     # graph replay (what the bench times) gives the same bits as eager
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -61,11 +65,11 @@ def test_bench_step_vs_fp32_oracle(dev, lens):
     sd_tr = {k: v.cpu() for k, v in tr.state_dict().items()}
     ref = _oracle(wav, wav_len, sd_cnn, sd_tr, False)
     emu = _oracle(wav, wav_len, sd_cnn, sd_tr, True)
-    assert out.shape == ref.shape == (2, 376, 256)
+    assert out.shape == ref.shape == (2, 376, d_model)
     # every frame is compared, padded ones included (they are still encoded)
     e_hip = (out - ref).abs()
     e_emu = (emu - ref).abs()
-    print(f"\nbench-path parity lens={lens}: HIP bf16 vs fp32 oracle max {e_hip.max():.4e} mean {e_hip.mean():.4e}; "
+    print(f"\nbench-path parity d={d_model} lens={lens}: HIP bf16 vs fp32 oracle max {e_hip.max():.4e} mean {e_hip.mean():.4e}; "
           f"bf16-operand oracle vs fp32 oracle max {e_emu.max():.4e} mean {e_emu.mean():.4e}")
     assert torch.isfinite(out).all()
     assert float(e_hip.max()) <= FACTOR * float(e_emu.max())
