@@ -378,6 +378,11 @@ class ConformerEncoder(nn.Module):
     def wants_train_path(self, x):
         return any(layer.wants_train_path(x) for layer in self.layers) or A.needs_grad(self.norm, x)
 
+    def _shadow(self, d, dtype, am=None):
+        if USE_PADDED_SHADOW and am is None and dtype == _bf16 and d < PAD_D:
+            return _PaddedEncoder.of(self)
+        return None
+
     def run(self, src2d, B, T, pos_embs, kpm_u8, dtype, need_attn, am=None):
         """Fused stack on (B*T, d) fp32 → ((B*T, d) fp32, [attn]); am: the
         src_mask as _enc.attn_mask_arg (takes the per-layer path).  A bf16
@@ -386,10 +391,9 @@ class ConformerEncoder(nn.Module):
         if self.wants_train_path(src2d):
             return self.train_run(src2d, B, T, pos_embs, kpm_u8, dtype, am=am)
         d = src2d.shape[1]
-        if USE_PADDED_SHADOW and am is None and dtype == _bf16 and d < PAD_D:
-            sh = _PaddedEncoder.of(self)
-            if sh is not None:
-                return sh.run(src2d, B, T, pos_embs, kpm_u8, dtype, need_attn)
+        sh = self._shadow(d, dtype, am)
+        if sh is not None:
+            return sh.run(src2d, B, T, pos_embs, kpm_u8, dtype, need_attn)
         pos = _enc.to_compute(pos_embs.reshape(-1, d), dtype)
         pk_all = _enc.gemm(pos, self.stacked_pos_weight(dtype), out_dtype=dtype)  # (2T-1, L*d)
         x = src2d
@@ -594,16 +598,24 @@ class _PaddedEncoder:
         enc._padded_shadow = (sig, shadow)
         return shadow
 
-    def run(self, src2d, B, T, pos_embs, kpm_u8, dtype, need_attn):
+    def padded_pos(self, pos_embs, dtype):
+        """The positional table (a per-T constant) padded to 256 columns, once."""
         d = self.d
-        x = torch.zeros(src2d.shape[0], PAD_D, device=src2d.device, dtype=torch.float32)
-        x[:, :d] = src2d
         key = (pos_embs.data_ptr(), tuple(pos_embs.shape), dtype)
         pos = self._pos.get(key)
-        if pos is None:  # the positional table (a per-T constant) padded to 256 columns once
+        if pos is None:
             p = pos_embs.reshape(-1, d)
             pos = torch.zeros(p.shape[0], PAD_D, device=p.device, dtype=dtype)
             pos[:, :d] = p.to(dtype)
             self._pos = {key: pos}
-        y, attns = self.sh.run(x, B, T, pos, kpm_u8, dtype, need_attn)
+        return pos
+
+    def run(self, src2d, B, T, pos_embs, kpm_u8, dtype, need_attn):
+        d = self.d
+        if src2d.shape[1] == PAD_D:  # already padded by the producer (TransformerASR's padded src Linear)
+            x = src2d
+        else:
+            x = torch.zeros(src2d.shape[0], PAD_D, device=src2d.device, dtype=torch.float32)
+            x[:, :d] = src2d
+        y, attns = self.sh.run(x, B, T, self.padded_pos(pos_embs, dtype), kpm_u8, dtype, need_attn)
         return y[:, :d].contiguous(), attns

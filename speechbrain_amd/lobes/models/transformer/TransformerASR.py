@@ -32,11 +32,12 @@ from .... import _enc
 from ....nnet.activations import Swish
 from ....nnet.attention import RelPosEncXL
 from ....nnet.linear import Linear
-from .Conformer import ConformerEncoder
+from .Conformer import PAD_D, ConformerEncoder
 from .Transformer import (NormalizedEmbedding, PositionalEncoding, TransformerDecoder, TransformerEncoder,
                           get_key_padding_mask, get_lookahead_mask)
 
 _f32 = torch.float32
+_bf16 = torch.bfloat16
 
 
 class _ModuleList(nn.Module):
@@ -134,7 +135,7 @@ class TransformerASR(nn.Module):
             raise ValueError(f"src key padding mask width {src_kpm.shape[1]} != T = {src.shape[1]} "
                              "(no utterance fills the batch: max(wav_len) < 1)")
         if self._fast_encoder():
-            encoder_out = self._encode(src, None if src_kpm is None else src_kpm.to(torch.uint8))
+            encoder_out = self._encode(src, kpm=src_kpm)
         else:
             encoder_out = self._module_encode(src, src_kpm, src_mask)
         tgt = self.custom_tgt_module(tgt)
@@ -195,9 +196,9 @@ class TransformerASR(nn.Module):
         if src.dim() == 4:
             bz, t, ch1, ch2 = src.shape
             src = src.reshape(bz, t, ch1 * ch2)
-        kpm = self.key_padding_mask(src.shape[1], wav_len, src.device)
         if self._fast_encoder():
-            return self._encode(src, kpm)
+            return self._encode(src, wav_len)
+        kpm = self.key_padding_mask(src.shape[1], wav_len, src.device)
         return self._module_encode(src, None if kpm is None else kpm.bool())
 
     def _module_encode(self, src, kpm, src_mask=None):
@@ -220,26 +221,59 @@ class TransformerASR(nn.Module):
         y, _ = self.encoder(src=x, src_mask=src_mask, src_key_padding_mask=kpm, pos_embs=pos)
         return y
 
-    def _encode(self, src, kpm):
-        """Fused Conformer path: src (B, T, F) and a uint8 key padding mask (B, T) or None → encoder output."""
+    def _encode(self, src, wav_len=None, kpm=None):
+        """Fused Conformer path: src (B, T, F) and the relative lengths (or
+        None) or a ready key padding mask (forward's make_masks) → encoder
+        output.  (Running the key padding mask and the linear_pos GEMM on a
+        side stream beside the src Linear measured 20-30 us slower per
+        step: profiles/r06o_preamble_side_stream_ab_rejected.log.)"""
         B, T, Fin = src.shape
         dtype = _enc.compute_dtype()
-        if kpm is not None:
-            kpm = kpm.to(device=src.device, dtype=torch.uint8).contiguous()
         lin = self.custom_src_module.layers[0]
         drop = self.custom_src_module.layers[1]
         if A.needs_grad(self, src) or (self.training and (drop.p > 0 or self.encoder.wants_train_path(src))):
             # training path: differentiable HIP chain (_autograd)
+            kpm = self._kpm(T, wav_len, kpm, src.device)
             x = A.linear(src.reshape(B * T, Fin), lin.w.weight, lin.w.bias, dtype, lin._wc, "t_w", out_dtype=_f32)
             x = A.dropout(x, drop.p, self.training)
             pos = self.positional_encoding.table(T, src.device, _f32)
             y, _ = self.encoder.train_run(x, B, T, pos, kpm, dtype)
             return y.view(B, T, -1)
-        a = _enc.to_compute(src.reshape(B * T, Fin), dtype)
-        x = _enc.gemm(a, lin.kernel_weight(dtype), bias=lin.w.bias.detach(), out_dtype=_f32)
+        kpm = self._kpm(T, wav_len, kpm, src.device)
         pos = self.positional_encoding.table(T, src.device, dtype)  # a constant table: cached in the compute dtype
-        y, _ = self.encoder.run(x, B, T, pos, kpm, dtype, False)
+        a = _enc.to_compute(src.reshape(B * T, Fin), dtype)
+        sh = self.encoder._shadow(lin.w.weight.shape[0], dtype)
+        if sh is not None:
+            # d_model < 256 on the padded shadow: the src Linear writes the
+            # 256-wide zero-padded input itself (no fill + copy launches)
+            w, b = self._padded_src(dtype)
+            y, _ = sh.run(_enc.gemm(a, w, bias=b, out_dtype=_f32), B, T, pos, kpm, dtype, False)
+        else:
+            x = _enc.gemm(a, lin.kernel_weight(dtype), bias=lin.w.bias.detach(), out_dtype=_f32)
+            y, _ = self.encoder.run(x, B, T, pos, kpm, dtype, False)
         return y.view(B, T, -1)
+
+    def _kpm(self, T, wav_len, kpm, device):
+        """uint8 (B, T) key padding mask: the given one, or from wav_len."""
+        if kpm is not None:
+            return kpm.to(device=device, dtype=torch.uint8).contiguous()
+        return self.key_padding_mask(T, wav_len, device)
+
+    def _padded_src(self, dtype):
+        """The src Linear with its output rows zero-padded to the encoder
+        shadow's 256 channels (weight in the compute dtype, fp32 bias)."""
+        lin = self.custom_src_module.layers[0]
+        ps = [lin.w.weight] + ([lin.w.bias] if lin.w.bias is not None else [])
+
+        def make():
+            wt = lin.w.weight.detach()
+            w = torch.zeros(PAD_D, wt.shape[1], device=wt.device, dtype=torch.float32)
+            w[:wt.shape[0]] = wt
+            b = torch.zeros(PAD_D, device=wt.device, dtype=torch.float32)
+            if lin.w.bias is not None:
+                b[:wt.shape[0]] = lin.w.bias.detach()
+            return (_enc.cast_bf16(w) if dtype == _bf16 else w), b
+        return lin._wc.get(("pad", dtype), ps, make)
 
 
 class EncoderWrapper(nn.Module):
