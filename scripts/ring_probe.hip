@@ -32,7 +32,11 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int TKB, int NB, int NMFMA>
+// XR: extra ds_read_b128 per wave and 32-KB step from a shared 6-KB region
+// (the chain's phase-2 A fragments: every wave reads the same hidden chunk):
+// XR > 0 after the weight reads' wait (a second LDS round trip), XR < 0
+// issued with the weight reads under one wait, as the chain's step does
+template <int TKB, int NB, int NMFMA, int XR = 0>
 __global__ void __launch_bounds__(NT) ring_kernel(const bf16_t* __restrict__ img, float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int TB = TKB * 1024, WB = TB / 8, PPT = WB / 1024;  // tile, wave share, 1-KB pieces per wave
@@ -63,6 +67,14 @@ __global__ void __launch_bounds__(NT) ring_kernel(const bf16_t* __restrict__ img
     f32x4 r[4];
 #pragma unroll
     for (int i = 0; i < PPT; ++i) r[i] = lds_f4(slot + i * 1024);
+    // XR2: the extra reads issued with the weight reads, one wait for all
+    constexpr int XR2 = XR < 0 ? -XR : 0;
+    f32x4 h2[XR2 > 0 ? XR2 : 1];
+    if constexpr (XR2 > 0) {
+      const unsigned char* hs = smem + NB * TB + (lane & 15) * 16 + (w & 1) * 256;
+#pragma unroll
+      for (int i = 0; i < XR2; ++i) h2[i] = lds_f4(hs + i * 1024);
+    }
     if constexpr (PPT == 4)
       asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3])::"memory");
     else if constexpr (PPT == 2)
@@ -71,6 +83,25 @@ __global__ void __launch_bounds__(NT) ring_kernel(const bf16_t* __restrict__ img
       asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0])::"memory");
 #pragma unroll
     for (int i = 0; i < PPT; ++i) acc += r[i];
+    if constexpr (XR2 > 0) {  // landed with the weight reads (the wait above is lgkmcnt(0))
+#pragma unroll
+      for (int i = 0; i < XR2; ++i) {
+        asm volatile("" : "+v"(h2[i]));
+        acc += h2[i];
+      }
+    }
+    if constexpr (XR > 0) {  // the shared region sits past the ring (NB * TB <= 96 KB - 6 KB)
+      const unsigned char* hs = smem + NB * TB + (lane & 15) * 16 + (w & 1) * 256;
+      f32x4 h[XR];
+#pragma unroll
+      for (int i = 0; i < XR; ++i) h[i] = lds_f4(hs + i * 1024);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < XR; ++i) {
+        asm volatile("" : "+v"(h[i]));
+        acc += h[i];
+      }
+    }
     const bf16x8 fa = *reinterpret_cast<bf16x8*>(&r[0]);
     const bf16x8 fb = *reinterpret_cast<bf16x8*>(&r[PPT - 1]);
 #pragma unroll
@@ -81,9 +112,9 @@ __global__ void __launch_bounds__(NT) ring_kernel(const bf16_t* __restrict__ img
   out[blockIdx.x * NT + threadIdx.x] = s[0] + s[1] + s[2] + s[3];
 }
 
-template <int TKB, int NB, int NMFMA>
+template <int TKB, int NB, int NMFMA, int XR = 0>
 static void run(const bf16_t* img, float* out, int grid, int reps) {
-  auto k = ring_kernel<TKB, NB, NMFMA>;
+  auto k = ring_kernel<TKB, NB, NMFMA, XR>;
   const size_t lds = 96 * 1024;  // >= every ring here; > 80 KB: one workgroup per CU
   hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(k, dim3(grid), dim3(NT), lds, 0, img, out);
@@ -106,9 +137,9 @@ static void run(const bf16_t* img, float* out, int grid, int reps) {
   double cs = 0.0;
   for (float v : h) cs += v;
   const double us = ms * 1e3 / reps;
-  printf("tile %2d KB x %d slots (%d in flight, %3d KB ring), %2d MFMA per 32 KB: %7.2f us, %6.1f GB/s per CU, "
-         "%5.1f B/clk at 2.4 GHz, checksum %.6e\n",
-         TKB, NB, NB - 1, TKB * NB, NMFMA, us, IMG_BYTES / us * 1e-3, IMG_BYTES / (us * 2400.0), cs);
+  printf("tile %2d KB x %d slots (%d in flight, %3d KB ring), %2d MFMA + %d extra b128 reads per 32 KB: %7.2f us, "
+         "%6.1f GB/s per CU, %5.1f B/clk at 2.4 GHz, checksum %.6e\n",
+         TKB, NB, NB - 1, TKB * NB, NMFMA, XR, us, IMG_BYTES / us * 1e-3, IMG_BYTES / (us * 2400.0), cs);
 }
 
 int main() {
@@ -121,6 +152,17 @@ int main() {
   (void)hipMalloc(&img, IMG_BYTES);
   (void)hipMalloc(&out, (size_t)grid * NT * 4);
   (void)hipMemcpy(img, h.data(), IMG_BYTES, hipMemcpyHostToDevice);
+  if (getenv("RING_PROBE_XR")) {  // the chain's phase-2 LDS reads beside the stream
+    for (int rep = 0; rep < 2; ++rep) {
+      run<32, 2, 12, 0>(img, out, grid, 50);
+      run<32, 2, 12, 6>(img, out, grid, 50);
+      run<32, 2, 12, -6>(img, out, grid, 50);
+      run<32, 2, 12, -12>(img, out, grid, 50);
+    }
+    (void)hipFree(img);
+    (void)hipFree(out);
+    return 0;
+  }
   for (int rep = 0; rep < 2; ++rep) {
     run<32, 2, 0>(img, out, grid, 50);
     run<32, 3, 0>(img, out, grid, 50);
