@@ -29,6 +29,8 @@
 
 #include <math.h>
 
+#include <initializer_list>
+
 namespace {
 
 using sbk::bf16_to_f32;
@@ -152,6 +154,151 @@ __global__ __launch_bounds__(kThreads) void xattn_fwd_kernel(
                 [&](int d, float y) { st(orow, d, y); });
 }
 
+// No-position forward (pk == nullptr), query-blocked: one workgroup per
+// (QB query rows, head, batch).  The per-row kernel above gives every
+// score its own thread and walks a key row dimension by dimension, so a
+// wave reads 64 different rows element-wise and every query row re-reads
+// all of K and V (decoder cross-attention over 376 keys: 1.2-2x torch's
+// GEMM-based MHA, profiles/r06u_mha_decoder_timing.log).  Here K and V pass
+// through LDS in chunks of XQ_KC rows, read once per QB query rows with
+// coalesced loads, the scores of the block stay in LDS (QB x Lk) for the
+// softmax, and P·V accumulates per (row, 8 output dims); the LDS rows are
+// padded to dh + 4 floats so the dot products read 16 B at a time, the 16
+// key rows of a lane group 4 banks apart.  fp32 VALU as above (exact fp32
+// operands for the parity path).
+constexpr int XQ_QB = 16, XQ_KC = 64, XQ_DMAX = 128, XQ_LKMAX = 1024;
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 ld4(const uint16_t* p) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                     __uint_as_float(u.y & 0xffff0000u));
+}
+// ROWS x dh of src (row stride ld_src elements, 4-element aligned) -> dst
+// (row stride ld_dst floats); rows >= rmax -> 0.  Every load of the thread
+// is issued before the first LDS store (a load -> store loop per element
+// paid the global latency once per element: the first version of these
+// kernels spent most of its time there).
+template <int ROWS, typename TI>
+__device__ __forceinline__ void xq_stage(float* dst, int ld_dst, const TI* src, long long ld_src, int rmax, int dh) {
+  constexpr int PT = (ROWS * (XQ_DMAX / 4) + kThreads - 1) / kThreads;  // float4 per thread at dh = XQ_DMAX
+  const int q4 = dh >> 2, total = ROWS * q4;
+  float4 v[PT];
+#pragma unroll
+  for (int u = 0; u < PT; ++u) {
+    const int e = threadIdx.x + u * kThreads;
+    v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < total) {
+      const int r = e / q4, c = (e - r * q4) * 4;
+      if (r < rmax) v[u] = ld4(src + (long long)r * ld_src + c);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < PT; ++u) {
+    const int e = threadIdx.x + u * kThreads;
+    if (e < total) {
+      const int r = e / q4, c = (e - r * q4) * 4;
+      *reinterpret_cast<float4*>(dst + r * ld_dst + c) = v[u];
+    }
+  }
+}
+
+template <typename TI>
+__global__ __launch_bounds__(kThreads) void xattn_fwd_qb_kernel(
+    const TI* __restrict__ q, int ldq, const TI* __restrict__ k, int ldk, const TI* __restrict__ v, int ldv,
+    const unsigned char* __restrict__ kpm, const float* __restrict__ am, long long am_sb, long long am_sh, int Lq,
+    int Lk, int H, int dh, float scale, unsigned thresh, float inv_keep, unsigned long long seed, int use_drop,
+    TI* __restrict__ out, int ldo, float* __restrict__ probs, float* __restrict__ attn) {
+  extern __shared__ float sm[];
+  const int DP = dh + 4;                   // padded LDS row (floats): 16-B aligned, rows 4 banks apart
+  float* qs = sm;                          // XQ_QB x DP
+  float* kv = qs + XQ_QB * DP;             // XQ_KC x DP (K chunk, then V chunk)
+  float* s = kv + XQ_KC * DP;              // XQ_QB x Lk scores -> probabilities (dropped)
+  const int i0 = blockIdx.x * XQ_QB, h = blockIdx.y, b = blockIdx.z;
+  const int nq = min(XQ_QB, Lq - i0);
+  const int tid = threadIdx.x, ri = tid >> 4, sub = tid & 15;  // row ri, 16 threads per row
+  xq_stage<XQ_QB>(qs, DP, q + (long long)(b * Lq + i0) * ldq + h * dh, ldq, nq, dh);
+  // scores: thread (ri, sub) takes keys j0 + sub + 16 m of each chunk
+  for (int j0 = 0; j0 < Lk; j0 += XQ_KC) {
+    const int nk = min(XQ_KC, Lk - j0);
+    __syncthreads();  // the previous chunk's readers are done (and qs is staged)
+    xq_stage<XQ_KC>(kv, DP, k + (long long)(b * Lk + j0) * ldk + h * dh, ldk, nk, dh);
+    __syncthreads();
+    float ac[XQ_KC / 16] = {};
+    const float* qr = qs + ri * DP;
+    for (int d = 0; d < dh; d += 4) {
+      const float4 qd = *reinterpret_cast<const float4*>(qr + d);
+#pragma unroll
+      for (int m = 0; m < XQ_KC / 16; ++m) {
+        const float4 kd = *reinterpret_cast<const float4*>(kv + (sub + 16 * m) * DP + d);
+        ac[m] += qd.x * kd.x + qd.y * kd.y + qd.z * kd.z + qd.w * kd.w;
+      }
+    }
+    const int i = i0 + ri;
+    const float* am_row = (am && ri < nq) ? am + b * am_sb + h * am_sh + (long long)i * Lk : nullptr;
+#pragma unroll
+    for (int m = 0; m < XQ_KC / 16; ++m) {
+      const int j = j0 + sub + 16 * m;
+      if (j >= Lk) continue;
+      float sc = ac[m] * scale;
+      if (am_row) sc += am_row[j];
+      if (kpm && kpm[(long long)b * Lk + j]) sc = -INFINITY;
+      s[ri * Lk + j] = sc;
+    }
+  }
+  __syncthreads();
+  // softmax per row: 16 threads per row (lanes 16 ri' .. of one wave), xor shuffles within the 16
+  float mx = -INFINITY;
+  for (int j = sub; j < Lk; j += 16) mx = fmaxf(mx, s[ri * Lk + j]);
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 16));
+  float sum = 0.f;
+  for (int j = sub; j < Lk; j += 16) {
+    const float e = expf(s[ri * Lk + j] - mx);  // all -inf: NaN, as the reference's softmax
+    s[ri * Lk + j] = e;
+    sum += e;
+  }
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 16);
+  const float inv = 1.f / sum;
+  const long long prow = (((long long)b * H + h) * Lq + i0 + ri) * Lk;
+  for (int j = sub; j < Lk; j += 16) {
+    const float pv = s[ri * Lk + j] * inv;
+    float pd = pv;
+    if (ri < nq) {
+      probs[prow + j] = pv;
+      if (use_drop) {
+        pd = keep_elem(seed, prow + j, thresh) ? pv * inv_keep : 0.f;
+        attn[prow + j] = pd;
+      }
+    }
+    s[ri * Lk + j] = pd;
+  }
+  // out[ri][8 sub .. 8 sub + 7] (+ 128 per extra pass for dh > 128: not taken, dh <= XQ_DMAX)
+  float acc[8] = {};
+  const int d0 = 8 * sub;
+  for (int j0 = 0; j0 < Lk; j0 += XQ_KC) {
+    const int nk = min(XQ_KC, Lk - j0);
+    __syncthreads();
+    xq_stage<XQ_KC>(kv, DP, v + (long long)(b * Lk + j0) * ldv + h * dh, ldv, nk, dh);
+    __syncthreads();
+    if (d0 < dh)
+      for (int jj = 0; jj < nk; ++jj) {
+        const float pj = s[ri * Lk + j0 + jj];
+        const float4 va = *reinterpret_cast<const float4*>(kv + jj * DP + d0);
+        const float4 vb = *reinterpret_cast<const float4*>(kv + jj * DP + d0 + 4);
+        acc[0] += pj * va.x; acc[1] += pj * va.y; acc[2] += pj * va.z; acc[3] += pj * va.w;
+        acc[4] += pj * vb.x; acc[5] += pj * vb.y; acc[6] += pj * vb.z; acc[7] += pj * vb.w;
+      }
+  }
+  if (ri < nq && d0 < dh) {
+    TI* orow = out + (long long)(b * Lq + i0 + ri) * ldo + h * dh;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (d0 + e < dh) st(orow, d0 + e, acc[e]);
+  }
+}
+
 // Backward, row pass: per query row i, dP = dO·Vᵀ (through the dropout
 // mask), G = P ⊙ (dP - Σ P dP) · scale (the gradient of the pre-scale
 // score (ac + bd)), and dq_ac = G·K.
@@ -188,6 +335,86 @@ __global__ __launch_bounds__(kThreads) void xattn_bwd_rows_kernel(
   __syncthreads();
   float* dq = dqu + (long long)(b * Lq + i) * H * dh + h * dh;
   weighted_rows(g, k + (long long)b * Lk * ldk + h * dh, ldk, Lk, dh, part, [&](int d, float y) { dq[d] = y; });
+}
+
+// No-position backward row pass, query-blocked like xattn_fwd_qb_kernel:
+// dP = dO·Vᵀ over V chunks in LDS, G = P ⊙ (dP - Σ P dP) · scale (written
+// to global for the key-row pass), dq = G·K over K chunks in LDS.
+template <typename TI>
+__global__ __launch_bounds__(kThreads) void xattn_bwd_rows_qb_kernel(
+    const TI* __restrict__ k, int ldk, const TI* __restrict__ v, int ldv, const TI* __restrict__ dO, int lddo,
+    const float* __restrict__ probs, int Lq, int Lk, int H, int dh, float scale, unsigned thresh, float inv_keep,
+    unsigned long long seed, int use_drop, float* __restrict__ G, float* __restrict__ dq) {
+  extern __shared__ float sm[];
+  const int DP = dh + 4;
+  float* ds = sm;                          // XQ_QB x DP: dO rows
+  float* kv = ds + XQ_QB * DP;             // XQ_KC x DP: V chunk, then K chunk
+  float* g = kv + XQ_KC * DP;              // XQ_QB x Lk: dP, then G
+  const int i0 = blockIdx.x * XQ_QB, h = blockIdx.y, b = blockIdx.z;
+  const int nq = min(XQ_QB, Lq - i0);
+  const int tid = threadIdx.x, ri = tid >> 4, sub = tid & 15;
+  xq_stage<XQ_QB>(ds, DP, dO + (long long)(b * Lq + i0) * lddo + h * dh, lddo, nq, dh);
+  const long long prow = (((long long)b * H + h) * Lq + i0 + ri) * Lk;
+  for (int j0 = 0; j0 < Lk; j0 += XQ_KC) {
+    const int nk = min(XQ_KC, Lk - j0);
+    __syncthreads();
+    xq_stage<XQ_KC>(kv, DP, v + (long long)(b * Lk + j0) * ldv + h * dh, ldv, nk, dh);
+    __syncthreads();
+    float dp[XQ_KC / 16] = {};
+    const float* dr = ds + ri * DP;
+    for (int d = 0; d < dh; d += 4) {
+      const float4 od = *reinterpret_cast<const float4*>(dr + d);
+#pragma unroll
+      for (int m = 0; m < XQ_KC / 16; ++m) {
+        const float4 vd = *reinterpret_cast<const float4*>(kv + (sub + 16 * m) * DP + d);
+        dp[m] += od.x * vd.x + od.y * vd.y + od.z * vd.z + od.w * vd.w;
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < XQ_KC / 16; ++m) {
+      const int j = j0 + sub + 16 * m;
+      if (j >= Lk) continue;
+      float x = dp[m];
+      if (use_drop && ri < nq) x = keep_elem(seed, prow + j, thresh) ? x * inv_keep : 0.f;
+      g[ri * Lk + j] = x;
+    }
+  }
+  __syncthreads();
+  float dot = 0.f;
+  if (ri < nq)
+    for (int j = sub; j < Lk; j += 16) dot += probs[prow + j] * g[ri * Lk + j];
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) dot += __shfl_xor(dot, o, 16);
+  for (int j = sub; j < Lk; j += 16) {
+    float gv = 0.f;
+    if (ri < nq) {
+      gv = probs[prow + j] * (g[ri * Lk + j] - dot) * scale;
+      G[prow + j] = gv;
+    }
+    g[ri * Lk + j] = gv;
+  }
+  float acc[8] = {};
+  const int d0 = 8 * sub;
+  for (int j0 = 0; j0 < Lk; j0 += XQ_KC) {
+    const int nk = min(XQ_KC, Lk - j0);
+    __syncthreads();
+    xq_stage<XQ_KC>(kv, DP, k + (long long)(b * Lk + j0) * ldk + h * dh, ldk, nk, dh);
+    __syncthreads();
+    if (d0 < dh)
+      for (int jj = 0; jj < nk; ++jj) {
+        const float gj = g[ri * Lk + j0 + jj];
+        const float4 ka = *reinterpret_cast<const float4*>(kv + jj * DP + d0);
+        const float4 kb = *reinterpret_cast<const float4*>(kv + jj * DP + d0 + 4);
+        acc[0] += gj * ka.x; acc[1] += gj * ka.y; acc[2] += gj * ka.z; acc[3] += gj * ka.w;
+        acc[4] += gj * kb.x; acc[5] += gj * kb.y; acc[6] += gj * kb.z; acc[7] += gj * kb.w;
+      }
+  }
+  if (ri < nq && d0 < dh) {
+    float* dqr = dq + (long long)(b * Lq + i0 + ri) * H * dh + h * dh;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (d0 + e < dh) dqr[d0 + e] = acc[e];
+  }
 }
 
 // the band gradient dBD[r][c] of row r of batch b / head h: the G element
@@ -253,6 +480,72 @@ __global__ __launch_bounds__(kThreads) void xattn_bwd_kv_kernel(
                 [&](int d, float y) { dv[o + d] = y; });
 }
 
+// Key-row pass, key-blocked (dh <= XQ_DMAX): one workgroup per (XQ_QB key
+// rows, head, batch) walks the query rows in chunks of XQ_KC: the G / P
+// column slices of its keys (16 consecutive floats of each row) and the q /
+// dO rows of the chunk go through LDS, thread (key row, 8 dims) accumulates
+// dk and dv.  (The per-key kernel above read each G / P column element by
+// element at a stride of Lk: 25 % of a decoder cross-attention's backward.)
+template <typename TI>
+__global__ __launch_bounds__(kThreads) void xattn_bwd_kv_qb_kernel(
+    const TI* __restrict__ q, int ldq, const TI* __restrict__ dO, int lddo, const float* __restrict__ pbu,
+    const float* __restrict__ probs, const float* __restrict__ G, int Lq, int Lk, int H, int dh, unsigned thresh,
+    float inv_keep, unsigned long long seed, int use_drop, float* __restrict__ dk, float* __restrict__ dv) {
+  extern __shared__ float sm[];
+  const int DP = dh + 4;
+  float* gs = sm;                    // XQ_KC x XQ_QB: G[i][j0 + jj]
+  float* ps = gs + XQ_KC * XQ_QB;    // XQ_KC x XQ_QB: Pd
+  float* qs = ps + XQ_KC * XQ_QB;    // XQ_KC x DP: q rows
+  float* os = qs + XQ_KC * DP;       // XQ_KC x DP: dO rows
+  const int j0 = blockIdx.x * XQ_QB, h = blockIdx.y, b = blockIdx.z;
+  const int nj = min(XQ_QB, Lk - j0);
+  const int tid = threadIdx.x, rj = tid >> 4, sub = tid & 15, d0 = 8 * sub;
+  const long long gbase = ((long long)b * H + h) * Lq * Lk + j0;
+  float adk[8] = {}, adv[8] = {};
+  float gsum = 0.f;
+  for (int i0 = 0; i0 < Lq; i0 += XQ_KC) {
+    const int ni = min(XQ_KC, Lq - i0);
+    __syncthreads();
+    for (int e = tid; e < XQ_KC * XQ_QB; e += kThreads) {
+      const int ii = e / XQ_QB, jj = e - ii * XQ_QB;
+      float gv = 0.f, pv = 0.f;
+      if (ii < ni && jj < nj) {
+        const long long x = gbase + (long long)(i0 + ii) * Lk + jj;
+        gv = G[x];
+        pv = probs[x];
+        if (use_drop) pv = keep_elem(seed, x, thresh) ? pv * inv_keep : 0.f;
+      }
+      gs[e] = gv;
+      ps[e] = pv;
+    }
+    xq_stage<XQ_KC>(qs, DP, q + (long long)(b * Lq + i0) * ldq + h * dh, ldq, ni, dh);
+    xq_stage<XQ_KC>(os, DP, dO + (long long)(b * Lq + i0) * lddo + h * dh, lddo, ni, dh);
+    __syncthreads();
+    if (d0 < dh)
+      for (int ii = 0; ii < ni; ++ii) {
+        const float gj = gs[ii * XQ_QB + rj], pj = ps[ii * XQ_QB + rj];
+        gsum += gj;
+        const float4 qa = *reinterpret_cast<const float4*>(qs + ii * DP + d0);
+        const float4 qb = *reinterpret_cast<const float4*>(qs + ii * DP + d0 + 4);
+        const float4 oa = *reinterpret_cast<const float4*>(os + ii * DP + d0);
+        const float4 ob = *reinterpret_cast<const float4*>(os + ii * DP + d0 + 4);
+        adk[0] += gj * qa.x; adk[1] += gj * qa.y; adk[2] += gj * qa.z; adk[3] += gj * qa.w;
+        adk[4] += gj * qb.x; adk[5] += gj * qb.y; adk[6] += gj * qb.z; adk[7] += gj * qb.w;
+        adv[0] += pj * oa.x; adv[1] += pj * oa.y; adv[2] += pj * oa.z; adv[3] += pj * oa.w;
+        adv[4] += pj * ob.x; adv[5] += pj * ob.y; adv[6] += pj * ob.z; adv[7] += pj * ob.w;
+      }
+  }
+  if (rj < nj && d0 < dh) {
+    const long long o = (long long)(b * Lk + j0 + rj) * H * dh + h * dh;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (d0 + e < dh) {
+        dk[o + d0 + e] = adk[e] + (pbu ? pbu[h * dh + d0 + e] * gsum : 0.f);
+        dv[o + d0 + e] = adv[e];
+      }
+  }
+}
+
 // Backward, band-column pass: dpk[c] = Σ_b Σ_r dBD[b][r][c] (q_r + v).
 template <typename TI>
 __global__ __launch_bounds__(kThreads) void xattn_bwd_pk_kernel(
@@ -298,6 +591,17 @@ __global__ __launch_bounds__(kThreads) void xattn_bwd_pk_kernel(
   }
 }
 
+// operands the query-blocked kernels can stage 4 elements at a time
+template <typename TI>
+bool qb_aligned(std::initializer_list<const void*> ps, std::initializer_list<int> lds, int dh) {
+  if (dh > XQ_DMAX || dh % 4) return false;
+  for (const void* p : ps)
+    if (reinterpret_cast<uintptr_t>(p) % (4 * sizeof(TI))) return false;
+  for (int l : lds)
+    if (l % 4) return false;
+  return true;
+}
+
 unsigned drop_thresh(float p) {
   const double keep = 1.0 - (double)p;
   return (unsigned)fmin(keep * 16777216.0, 16777216.0);
@@ -320,11 +624,21 @@ int xattn_fwd(const void* q, int ldq, const void* k, int ldk, const void* v, int
               const float* pbu, const float* pbv, const unsigned char* kpm, const float* am, long long am_sb,
               long long am_sh, int B, int Lq, int Lk, int H, int dh, float scale, int mpf, float p,
               unsigned long long seed, void* out, int ldo, float* probs, float* attn, hipStream_t st) {
+  const int use_drop = p > 0.f;
+  if (use_drop && !attn) return SBK_ERR_ARG;
+  if (!pk && Lk <= XQ_LKMAX && qb_aligned<TI>({q, k, v}, {ldq, ldk, ldv}, dh)) {
+    const size_t lq = (size_t)((XQ_QB + XQ_KC) * (dh + 4) + XQ_QB * Lk) * sizeof(float);
+    auto kq = xattn_fwd_qb_kernel<TI>;
+    if (int rc = prep_lds(kq, lq)) return rc;
+    hipLaunchKernelGGL(kq, dim3((Lq + XQ_QB - 1) / XQ_QB, H, B), dim3(kThreads), lq, st, (const TI*)q, ldq,
+                       (const TI*)k, ldk, (const TI*)v, ldv, kpm, am, am_sb, am_sh, Lq, Lk, H, dh, scale,
+                       drop_thresh(p), (float)(1.0 / (1.0 - (double)p)), seed, use_drop, (TI*)out, ldo, probs, attn);
+    SBK_CHECK_LAUNCH();
+    return 0;
+  }
   const size_t lds = (size_t)(Lk + dh + 64 + 256) * sizeof(float);
   auto kern = xattn_fwd_kernel<TI>;
   if (int rc = prep_lds(kern, lds)) return rc;
-  const int use_drop = p > 0.f;
-  if (use_drop && !attn) return SBK_ERR_ARG;
   hipLaunchKernelGGL(kern, dim3(Lq, H, B), dim3(kThreads), lds, st, (const TI*)q, ldq, (const TI*)k, ldk,
                      (const TI*)v, ldv, (const TI*)pk, ldp, P, pbu, pbv, kpm, am, am_sb, am_sh, Lq, Lk, H, dh, scale,
                      mpf, drop_thresh(p), (float)(1.0 / (1.0 - (double)p)), seed, use_drop, (TI*)out, ldo, probs,
@@ -341,7 +655,15 @@ int xattn_bwd(const void* q, int ldq, const void* k, int ldk, const void* v, int
   const unsigned thresh = drop_thresh(p);
   const float inv_keep = (float)(1.0 / (1.0 - (double)p));
   const int use_drop = p > 0.f;
-  {
+  if (!pk && Lk <= XQ_LKMAX && qb_aligned<TI>({k, v, dO}, {ldk, ldv, lddo}, dh)) {
+    const size_t lq = (size_t)((XQ_QB + XQ_KC) * (dh + 4) + XQ_QB * Lk) * sizeof(float);
+    auto kq = xattn_bwd_rows_qb_kernel<TI>;
+    if (int rc = prep_lds(kq, lq)) return rc;
+    hipLaunchKernelGGL(kq, dim3((Lq + XQ_QB - 1) / XQ_QB, H, B), dim3(kThreads), lq, st, (const TI*)k, ldk,
+                       (const TI*)v, ldv, (const TI*)dO, lddo, probs, Lq, Lk, H, dh, scale, thresh, inv_keep, seed,
+                       use_drop, G, dq);
+    SBK_CHECK_LAUNCH();
+  } else {
     const size_t lds = (size_t)(Lk + dh + 64 + 256) * sizeof(float);
     auto kern = xattn_bwd_rows_kernel<TI>;
     if (int rc = prep_lds(kern, lds)) return rc;
@@ -358,7 +680,14 @@ int xattn_bwd(const void* q, int ldq, const void* k, int ldk, const void* v, int
                        mpf, dqv, dq);
     SBK_CHECK_LAUNCH();
   }
-  {
+  if (qb_aligned<TI>({q, dO}, {ldq, lddo}, dh)) {
+    const size_t lq = (size_t)(2 * XQ_KC * XQ_QB + 2 * XQ_KC * (dh + 4)) * sizeof(float);
+    auto kq = xattn_bwd_kv_qb_kernel<TI>;
+    if (int rc = prep_lds(kq, lq)) return rc;
+    hipLaunchKernelGGL(kq, dim3((Lk + XQ_QB - 1) / XQ_QB, H, B), dim3(kThreads), lq, st, (const TI*)q, ldq,
+                       (const TI*)dO, lddo, pbu, probs, G, Lq, Lk, H, dh, thresh, inv_keep, seed, use_drop, dk, dv);
+    SBK_CHECK_LAUNCH();
+  } else {
     const size_t lds = (size_t)(2 * Lq + 256) * sizeof(float);
     auto kern = xattn_bwd_kv_kernel<TI>;
     if (int rc = prep_lds(kern, lds)) return rc;
