@@ -38,6 +38,10 @@ CASES = {
     "cross_float_kpm": dict(L=5, S=13, kpm="float", am="float2"),
     "byte_mask": dict(L=6, S=8, am="byte2", kpm="bool"),
     "kdim_vdim": dict(L=7, S=10, kdim=20, vdim=24),
+    # several 16-row query blocks and 64-key chunks, 128-dim heads (the
+    # query-blocked xattn kernels' loop structure and their dh bound)
+    "cross_multi_chunk": dict(L=37, S=150, E=256, H=2, kpm="bool", am="float2"),
+    "self_multi_chunk": dict(L=70, S=70, E=64, H=4, am="bool2", self_attn=True),
 }
 
 
@@ -45,7 +49,7 @@ CASES = {
 def test_mha_general_vs_torch(dev, name):
     from speechbrain_amd.nnet.attention import MultiheadAttention
     c = CASES[name]
-    B, E, H, L, S = 2, 32, 4, c["L"], c["S"]
+    B, E, H, L, S = 2, c.get("E", 32), c.get("H", 4), c["L"], c["S"]
     torch.manual_seed(len(name))
     mha = MultiheadAttention(nhead=H, d_model=E, kdim=c.get("kdim"), vdim=c.get("vdim")).eval()
     att = copy.deepcopy(mha.att)  # the CPU reference keeps its own parameters (and grads)
@@ -67,6 +71,7 @@ def test_mha_general_vs_torch(dev, name):
     if c.get("kpm") == "bool":
         kpm = torch.zeros(B, S, dtype=torch.bool)
         kpm[1, -3:] = True
+        kpm[0, S // 2:] = S > 64  # a padded tail longer than a key chunk
     elif c.get("kpm") == "float":
         kpm = torch.randn(B, S)
     pos = torch.randn(L, S) if c.get("pos") else None
@@ -142,3 +147,46 @@ def test_transformer_encoder_masks_and_grads(dev, pre):
     ref.backward(g)
     y.backward(g.to(dev))
     _close(xd.grad, xr.grad, 5e-5, "dx")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_nopos_core_dropout_vs_autograd(dev, dtype):
+    """The no-position xattn core (the MultiheadAttention general path) in
+    training with attention dropout, over several query blocks and key chunks:
+    the returned weights are the kept probabilities / (1 - p), out = attn · V,
+    and dq / dk / dv equal autograd of that composition under the same keep
+    mask (recovered from the weights).  fp32 1e-5 of the largest value; bf16
+    operands: the fp32 reference is fed the same rounded operands."""
+    from speechbrain_amd import _autograd as A
+    from speechbrain_amd import _enc
+    torch.manual_seed(9)
+    B, H, dh, Lq, Lk, p = 2, 2, 64, 37, 150, 0.25
+    q = torch.randn(B * Lq, H * dh, device=dev).to(dtype).requires_grad_(True)
+    k = torch.randn(B * Lk, H * dh, device=dev).to(dtype).requires_grad_(True)
+    v = torch.randn(B * Lk, H * dh, device=dev).to(dtype).requires_grad_(True)
+    kpm = torch.zeros(B, Lk, dtype=torch.uint8, device=dev)
+    kpm[1, 100:] = 1
+    am = torch.randn(Lq, Lk, device=dev)
+    scale = dh ** -0.5
+    o, attn = A.RelPosCrossAttnFn.apply(q, k, v, None, None, None, kpm, _enc.attn_mask_arg(am, B, Lq, H, dev, Lk=Lk),
+                                        B, Lq, Lk, H, dh, scale, False, p)
+    R = torch.randn_like(o.float())
+    (o.float() * R).sum().backward()
+    q2, k2, v2 = (t.detach().float().cpu().double().requires_grad_(True) for t in (q, k, v))
+    qh = q2.view(B, Lq, H, dh).transpose(1, 2)
+    kh = k2.view(B, Lk, H, dh).transpose(1, 2)
+    vh = v2.view(B, Lk, H, dh).transpose(1, 2)
+    sc = qh @ kh.transpose(-1, -2) * scale + am.cpu().double()
+    sc = sc.masked_fill(kpm.cpu().bool()[:, None, None, :], float("-inf"))
+    P = sc.softmax(-1)
+    keep = (attn.detach().cpu() != 0).double()
+    Pd = P * keep / (1 - p)
+    tol = 1e-5 if dtype == torch.float32 else 1e-4
+    _close(attn, Pd, tol, "dropped weights")
+    o2 = (Pd @ vh).transpose(1, 2).reshape(B * Lq, H * dh)
+    otol = 1e-5 if dtype == torch.float32 else 1e-2  # bf16 output rounding
+    _close(o, o2, otol, "out")
+    (o2 * R.cpu().double()).sum().backward()
+    _close(q.grad, q2.grad, 2e-5 if dtype == torch.float32 else 2e-2, "dq")
+    _close(k.grad, k2.grad, 2e-5 if dtype == torch.float32 else 2e-2, "dk")
+    _close(v.grad, v2.grad, 2e-5 if dtype == torch.float32 else 2e-2, "dv")
