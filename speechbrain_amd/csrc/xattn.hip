@@ -203,44 +203,126 @@ __device__ __forceinline__ void xq_stage(float* dst, int ld_dst, const TI* src, 
   }
 }
 
-template <typename TI>
+// POS: the rel-pos band term as well.  Output (i, j) takes band element
+// (r, c) = shift_src(i, j); for the common r == i it is (q_i + v)·pk_c with
+// c = j - i + Lq - 1, so the (QB + KC - 1) band rows a block-chunk needs are
+// staged beside the K chunk (XQ_BR rows from c_base); the wrap rows of the
+// reference's rel_shift (r > i: q_len > k_len) read global memory.
+constexpr int XQ_BR = XQ_QB + XQ_KC;  // staged band rows per chunk (79 used)
+
+template <int ROWS, typename TI>
+__device__ __forceinline__ void xq_stage_rows(float* dst, int ld_dst, const TI* src, long long ld_src, int row0,
+                                              int rows_total, int dh) {
+  // rows row0 .. row0 + ROWS - 1 of src (rows outside [0, rows_total) -> 0)
+  constexpr int PT = (ROWS * (XQ_DMAX / 4) + kThreads - 1) / kThreads;
+  const int q4 = dh >> 2, total = ROWS * q4;
+  float4 v[PT];
+#pragma unroll
+  for (int u = 0; u < PT; ++u) {
+    const int e = threadIdx.x + u * kThreads;
+    v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < total) {
+      const int r = e / q4, c = (e - r * q4) * 4, gr = row0 + r;
+      if (gr >= 0 && gr < rows_total) v[u] = ld4(src + (long long)gr * ld_src + c);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < PT; ++u) {
+    const int e = threadIdx.x + u * kThreads;
+    if (e < total) {
+      const int r = e / q4, c = (e - r * q4) * 4;
+      *reinterpret_cast<float4*>(dst + r * ld_dst + c) = v[u];
+    }
+  }
+}
+
+template <typename TI, bool POS>
 __global__ __launch_bounds__(kThreads) void xattn_fwd_qb_kernel(
     const TI* __restrict__ q, int ldq, const TI* __restrict__ k, int ldk, const TI* __restrict__ v, int ldv,
+    const TI* __restrict__ pk, int ldp, int P, const float* __restrict__ pbu, const float* __restrict__ pbv, int mpf,
     const unsigned char* __restrict__ kpm, const float* __restrict__ am, long long am_sb, long long am_sh, int Lq,
     int Lk, int H, int dh, float scale, unsigned thresh, float inv_keep, unsigned long long seed, int use_drop,
     TI* __restrict__ out, int ldo, float* __restrict__ probs, float* __restrict__ attn) {
   extern __shared__ float sm[];
   const int DP = dh + 4;                   // padded LDS row (floats): 16-B aligned, rows 4 banks apart
-  float* qs = sm;                          // XQ_QB x DP
+  float* qs = sm;                          // XQ_QB x DP (POS: q + u)
   float* kv = qs + XQ_QB * DP;             // XQ_KC x DP (K chunk, then V chunk)
-  float* s = kv + XQ_KC * DP;              // XQ_QB x Lk scores -> probabilities (dropped)
+  float* qv = kv + XQ_KC * DP;             // POS: XQ_QB x DP, q + v
+  float* band = qv + (POS ? XQ_QB * DP : 0);  // POS: XQ_BR x DP band rows from c_base
+  float* s = band + (POS ? XQ_BR * DP : 0);   // XQ_QB x Lk scores -> probabilities (dropped)
   const int i0 = blockIdx.x * XQ_QB, h = blockIdx.y, b = blockIdx.z;
   const int nq = min(XQ_QB, Lq - i0);
   const int tid = threadIdx.x, ri = tid >> 4, sub = tid & 15;  // row ri, 16 threads per row
-  xq_stage<XQ_QB>(qs, DP, q + (long long)(b * Lq + i0) * ldq + h * dh, ldq, nq, dh);
+  const TI* qblk = q + (long long)(b * Lq + i0) * ldq + h * dh;
+  xq_stage<XQ_QB>(qs, DP, qblk, ldq, nq, dh);
+  if constexpr (POS) {
+    xq_stage<XQ_QB>(qv, DP, qblk, ldq, nq, dh);
+    __syncthreads();
+    for (int e = tid; e < XQ_QB * dh; e += kThreads) {
+      const int r = e / dh, d = e - r * dh;
+      qs[r * DP + d] += pbu[h * dh + d];
+      qv[r * DP + d] += pbv[h * dh + d];
+    }
+  }
+  const int i = i0 + ri;
   // scores: thread (ri, sub) takes keys j0 + sub + 16 m of each chunk
   for (int j0 = 0; j0 < Lk; j0 += XQ_KC) {
     const int nk = min(XQ_KC, Lk - j0);
+    const int cb = j0 - i0 - (XQ_QB - 1) + Lq - 1;  // band row of (i0 + 15, j0) when r == i
     __syncthreads();  // the previous chunk's readers are done (and qs is staged)
     xq_stage<XQ_KC>(kv, DP, k + (long long)(b * Lk + j0) * ldk + h * dh, ldk, nk, dh);
+    if constexpr (POS) xq_stage_rows<XQ_BR>(band, DP, pk + h * dh, ldp, cb, P, dh);
     __syncthreads();
     float ac[XQ_KC / 16] = {};
+    float bd[XQ_KC / 16] = {};
+    int bro[XQ_KC / 16];  // POS: LDS band row of each key (-1: zero term; -2: wrap row, global)
+    int wr[XQ_KC / 16], wc[XQ_KC / 16];
+    if constexpr (POS) {
+#pragma unroll
+      for (int m = 0; m < XQ_KC / 16; ++m) {
+        const int j = j0 + sub + 16 * m;
+        int r = 0, c = -1;
+        if (j < Lk && ri < nq) shift_src(i, j, Lq, P, mpf, r, c);
+        wr[m] = r;
+        wc[m] = c;
+        bro[m] = c < 0 ? -1 : (r == i && c - cb >= 0 && c - cb < XQ_BR) ? c - cb : -2;
+      }
+    }
     const float* qr = qs + ri * DP;
+    const float* vr = qv + ri * DP;
     for (int d = 0; d < dh; d += 4) {
       const float4 qd = *reinterpret_cast<const float4*>(qr + d);
+      float4 vd;
+      if constexpr (POS) vd = *reinterpret_cast<const float4*>(vr + d);
 #pragma unroll
       for (int m = 0; m < XQ_KC / 16; ++m) {
         const float4 kd = *reinterpret_cast<const float4*>(kv + (sub + 16 * m) * DP + d);
         ac[m] += qd.x * kd.x + qd.y * kd.y + qd.z * kd.z + qd.w * kd.w;
+        if constexpr (POS) {
+          const float4 pd = *reinterpret_cast<const float4*>(band + max(bro[m], 0) * DP + d);
+          bd[m] += vd.x * pd.x + vd.y * pd.y + vd.z * pd.z + vd.w * pd.w;
+        }
       }
     }
-    const int i = i0 + ri;
+    if constexpr (POS) {
+#pragma unroll
+      for (int m = 0; m < XQ_KC / 16; ++m) {
+        if (bro[m] == -1) bd[m] = 0.f;
+        if (bro[m] == -2) {  // rel_shift wrap row (r > i): (q_r + v)·pk_c from global memory
+          const TI* qrow = q + (long long)(b * Lq + wr[m]) * ldq + h * dh;
+          const TI* prow = pk + (long long)wc[m] * ldp + h * dh;
+          float t = 0.f;
+          for (int d = 0; d < dh; ++d) t += (ld(qrow, d) + pbv[h * dh + d]) * ld(prow, d);
+          bd[m] = t;
+        }
+      }
+    }
     const float* am_row = (am && ri < nq) ? am + b * am_sb + h * am_sh + (long long)i * Lk : nullptr;
 #pragma unroll
     for (int m = 0; m < XQ_KC / 16; ++m) {
       const int j = j0 + sub + 16 * m;
       if (j >= Lk) continue;
-      float sc = ac[m] * scale;
+      float sc = (ac[m] + bd[m]) * scale;
       if (am_row) sc += am_row[j];
       if (kpm && kpm[(long long)b * Lk + j]) sc = -INFINITY;
       s[ri * Lk + j] = sc;
@@ -626,13 +708,25 @@ int xattn_fwd(const void* q, int ldq, const void* k, int ldk, const void* v, int
               unsigned long long seed, void* out, int ldo, float* probs, float* attn, hipStream_t st) {
   const int use_drop = p > 0.f;
   if (use_drop && !attn) return SBK_ERR_ARG;
-  if (!pk && Lk <= XQ_LKMAX && qb_aligned<TI>({q, k, v}, {ldq, ldk, ldv}, dh)) {
-    const size_t lq = (size_t)((XQ_QB + XQ_KC) * (dh + 4) + XQ_QB * Lk) * sizeof(float);
-    auto kq = xattn_fwd_qb_kernel<TI>;
-    if (int rc = prep_lds(kq, lq)) return rc;
-    hipLaunchKernelGGL(kq, dim3((Lq + XQ_QB - 1) / XQ_QB, H, B), dim3(kThreads), lq, st, (const TI*)q, ldq,
-                       (const TI*)k, ldk, (const TI*)v, ldv, kpm, am, am_sb, am_sh, Lq, Lk, H, dh, scale,
-                       drop_thresh(p), (float)(1.0 / (1.0 - (double)p)), seed, use_drop, (TI*)out, ldo, probs, attn);
+  const size_t lq = (size_t)((XQ_QB + XQ_KC + (pk ? XQ_QB + XQ_BR : 0)) * (dh + 4) + XQ_QB * Lk) * sizeof(float);
+  if (Lk <= XQ_LKMAX && lq <= 160 * 1024 &&
+      (pk ? qb_aligned<TI>({q, k, v, pk}, {ldq, ldk, ldv, ldp}, dh) : qb_aligned<TI>({q, k, v}, {ldq, ldk, ldv}, dh))) {
+    const dim3 grid((Lq + XQ_QB - 1) / XQ_QB, H, B);
+    const unsigned th = drop_thresh(p);
+    const float ik = (float)(1.0 / (1.0 - (double)p));
+    if (pk) {
+      auto kq = xattn_fwd_qb_kernel<TI, true>;
+      if (int rc = prep_lds(kq, lq)) return rc;
+      hipLaunchKernelGGL(kq, grid, dim3(kThreads), lq, st, (const TI*)q, ldq, (const TI*)k, ldk, (const TI*)v, ldv,
+                         (const TI*)pk, ldp, P, pbu, pbv, mpf, kpm, am, am_sb, am_sh, Lq, Lk, H, dh, scale, th, ik,
+                         seed, use_drop, (TI*)out, ldo, probs, attn);
+    } else {
+      auto kq = xattn_fwd_qb_kernel<TI, false>;
+      if (int rc = prep_lds(kq, lq)) return rc;
+      hipLaunchKernelGGL(kq, grid, dim3(kThreads), lq, st, (const TI*)q, ldq, (const TI*)k, ldk, (const TI*)v, ldv,
+                         (const TI*)nullptr, 0, 0, (const float*)nullptr, (const float*)nullptr, 0, kpm, am, am_sb,
+                         am_sh, Lq, Lk, H, dh, scale, th, ik, seed, use_drop, (TI*)out, ldo, probs, attn);
+    }
     SBK_CHECK_LAUNCH();
     return 0;
   }
@@ -655,13 +749,13 @@ int xattn_bwd(const void* q, int ldq, const void* k, int ldk, const void* v, int
   const unsigned thresh = drop_thresh(p);
   const float inv_keep = (float)(1.0 / (1.0 - (double)p));
   const int use_drop = p > 0.f;
-  if (!pk && Lk <= XQ_LKMAX && qb_aligned<TI>({k, v, dO}, {ldk, ldv, lddo}, dh)) {
+  if (Lk <= XQ_LKMAX && qb_aligned<TI>({k, v, dO}, {ldk, ldv, lddo}, dh)) {
     const size_t lq = (size_t)((XQ_QB + XQ_KC) * (dh + 4) + XQ_QB * Lk) * sizeof(float);
     auto kq = xattn_bwd_rows_qb_kernel<TI>;
     if (int rc = prep_lds(kq, lq)) return rc;
     hipLaunchKernelGGL(kq, dim3((Lq + XQ_QB - 1) / XQ_QB, H, B), dim3(kThreads), lq, st, (const TI*)k, ldk,
                        (const TI*)v, ldv, (const TI*)dO, lddo, probs, Lq, Lk, H, dh, scale, thresh, inv_keep, seed,
-                       use_drop, G, dq);
+                       use_drop, G, pk ? dqu : dq);
     SBK_CHECK_LAUNCH();
   } else {
     const size_t lds = (size_t)(Lk + dh + 64 + 256) * sizeof(float);
