@@ -1710,7 +1710,10 @@ SBK_API int sbk_deltas_floor(const float* x, float* y, int N, int T, int F, int 
   if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) return SBK_ERR_ARG;
   const int n = (window_length - 1) / 2;
   const float denom = (float)(n * (n + 1) * (2 * n + 1)) / 3.0f;
-  int ttile = 64;
+  // 32-row tiles: 15.1 vs 16.0 us at config 2 for 64 (26.3 for 128; storing
+  // each tile's output rows as one contiguous float4 run measured 20.8-22.8:
+  // profiles/r06ai_deltas_tile_ab.log)
+  int ttile = 32;
   auto lds = [&](int tt) { return (size_t)(tt + 4 * n) * F * 4 * 2; };
   while (ttile > 4 && lds(ttile) > 64 * 1024) ttile >>= 1;
   if (lds(ttile) > 160 * 1024) return SBK_ERR_ARG;
@@ -1726,7 +1729,7 @@ SBK_API int sbk_deltas(const float* x, float* y, int N, int T, int F, int window
   if (N <= 0 || T <= 0 || F <= 0 || window_length < 3) return SBK_ERR_ARG;
   const int n = (window_length - 1) / 2;
   const float denom = (float)(n * (n + 1) * (2 * n + 1)) / 3.0f;
-  int ttile = 64;
+  int ttile = 32;  // as sbk_deltas_floor
   const int halo = concat ? 2 * n : n;
   auto lds = [&](int tt) { return (size_t)(tt + 2 * halo) * F * 4 * (concat ? 2 : 1); };
   while (ttile > 4 && lds(ttile) > 64 * 1024) ttile >>= 1;
