@@ -3,7 +3,7 @@
 set -u
 cd /root/repo
 for i in 1 2; do
-  for v in A T32 T128 C C32; do
+  for v in A T16 T24; do
     cp ab/libsbk_$v.so speechbrain_amd/libsbk.so
     timeout -k 10 300 python -u bench.py --no-cpu-baseline --config c2 > gpurun_out/r06ai_${v}_$i.log 2>&1 || exit $?
     python - gpurun_out/r06ai_${v}_$i.log $v <<'PY'
