@@ -607,6 +607,20 @@ int sbk_mx_gemm(const uint8_t* A, const uint8_t* SA, long long lda, long long ld
                 int K, const float* bias, int act, float alpha, const float* res, long long ldr, void* out,
                 long long ldc, int out_mode, uint8_t* out_scales, long long ldso, void* stream);
 
+/* sbk_mx_gemm with an fp32 workspace (16-B aligned) for the 256-tile
+ * kernel's split-K tail: when the tiles past the last full round of
+ * workgroups fill at most half the CUs and K >= 2048, each of them runs as
+ * two K halves plus an epilogue pass (config 5's FFN down-projection, 376
+ * tiles on 256 CUs).  ws_floats >= sbk_mx_gemm_ws_floats(M, N, K, out_mode)
+ * enables it (fp32 out only; 0 = no split at this shape); results equal
+ * sbk_mx_gemm's up to the fp32 order of the two halves' sum. */
+long long sbk_mx_gemm_ws_floats(int M, int N, int K, int out_mode);
+int sbk_mx_gemm_ws(const uint8_t* A, const uint8_t* SA, long long lda, long long ldsa, long long rpb, long long a_bs,
+                   long long s_bs, const uint8_t* W, const uint8_t* SW, long long ldw, long long ldsw, int M, int N,
+                   int K, const float* bias, int act, float alpha, const float* res, long long ldr, void* out,
+                   long long ldc, int out_mode, uint8_t* out_scales, long long ldso, float* ws, long long ws_floats,
+                   void* stream);
+
 /* sbk_mx_gemm on the 256 x 256-tile multi-phase kernel (csrc/gemm256.hip):
  * same arguments; N % 256 == 0, K % 128 == 0 (SBK_ERR_ARG otherwise).
  * sbk_mx_gemm takes this kernel by itself when the shape allows and M is

@@ -90,6 +90,9 @@ SIGNATURES = {
     # mxgemm.hip (MXFP8 block-scaled MFMA GEMM)
     "sbk_mx_gemm": [_vp, _vp, _ll, _ll, _ll, _ll, _ll, _vp, _vp, _ll, _ll, _i, _i, _i, _vp, _i, _f, _vp, _ll, _vp,
                     _ll, _i, _vp, _ll, _vp],
+    "sbk_mx_gemm_ws": [_vp, _vp, _ll, _ll, _ll, _ll, _ll, _vp, _vp, _ll, _ll, _i, _i, _i, _vp, _i, _f, _vp, _ll, _vp,
+                       _ll, _i, _vp, _ll, _vp, _ll, _vp],
+    "sbk_mx_gemm_ws_floats": [_i, _i, _i, _i],
     "sbk_mx_gemm256": [_vp, _vp, _ll, _ll, _ll, _ll, _ll, _vp, _vp, _ll, _ll, _i, _i, _i, _vp, _i, _f, _vp, _ll,
                        _vp, _ll, _i, _vp, _ll, _vp],
     "sbk_mx_quant": [_vp, _i, _ll, _i, _i, _vp, _ll, _vp, _ll, _vp],
@@ -146,7 +149,7 @@ SIGNATURES = {
     "sbk_joint_bwd": [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp],
     "sbk_joint_bwd_workspace_floats": [_i, _i, _i, _i],
 }
-RESTYPES = {"sbk_relpos_attention_lds": ctypes.c_longlong, "sbk_ffn_image_elems": ctypes.c_longlong, "sbk_joint_bwd_workspace_floats": ctypes.c_longlong, "sbk_rnnt_workspace_floats": ctypes.c_longlong}
+RESTYPES = {"sbk_relpos_attention_lds": ctypes.c_longlong, "sbk_mx_gemm_ws_floats": ctypes.c_longlong, "sbk_ffn_image_elems": ctypes.c_longlong, "sbk_joint_bwd_workspace_floats": ctypes.c_longlong, "sbk_rnnt_workspace_floats": ctypes.c_longlong}
 
 _lib = None
 _load_error = None

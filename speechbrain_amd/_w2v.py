@@ -5,6 +5,7 @@ LayerNorm / activation / MXFP8 quantisation kernel and the MXFP8 GEMM.
 MXFP8 tensors travel as two tensors: e4m3 bytes (uint8, (M, K)) and one
 E8M0 scale byte per 32 consecutive K elements (uint8, (M, K/32)).  `MX`
 bundles them for the module code.  No op has a CPU path."""
+import functools
 from typing import NamedTuple, Optional
 
 import torch
@@ -140,12 +141,21 @@ def _mx_gemm_op(aq: torch.Tensor, asc: torch.Tensor, M: int, K: int, lda: int, l
                 res: Optional[torch.Tensor], out_mode: int) -> tuple[torch.Tensor, torch.Tensor]:
     N = wq.shape[0]
     out, sc = _empty_out(M, N, out_mode, aq.device)
-    check(lib().sbk_mx_gemm(ptr(aq), ptr(asc), lda, ldsa, rpb, a_bs, s_bs, ptr(wq), ptr(wsc), wq.stride(0),
-                            wsc.stride(0), M, N, K, ptr(bias), act, float(alpha), ptr(res),
-                            res.stride(0) if res is not None else 0, ptr(out), out.stride(0), out_mode,
-                            ptr(sc) if out_mode == 2 else None, sc.stride(0) if out_mode == 2 else 0,
-                            stream_of(aq)), "sbk_mx_gemm")
+    # the 256-tile kernel's split-K tail workspace (config 5's FFN
+    # down-projection); 0 floats at shapes that do not split
+    nws = _ws_floats(M, N, K, out_mode)
+    ws = torch.empty(nws, device=aq.device, dtype=_f32) if nws else None
+    check(lib().sbk_mx_gemm_ws(ptr(aq), ptr(asc), lda, ldsa, rpb, a_bs, s_bs, ptr(wq), ptr(wsc), wq.stride(0),
+                               wsc.stride(0), M, N, K, ptr(bias), act, float(alpha), ptr(res),
+                               res.stride(0) if res is not None else 0, ptr(out), out.stride(0), out_mode,
+                               ptr(sc) if out_mode == 2 else None, sc.stride(0) if out_mode == 2 else 0, ptr(ws), nws,
+                               stream_of(aq)), "sbk_mx_gemm_ws")
     return out, sc
+
+
+@functools.lru_cache(maxsize=None)
+def _ws_floats(M, N, K, out_mode):
+    return int(lib().sbk_mx_gemm_ws_floats(M, N, K, out_mode))
 
 
 @_mx_gemm_op.register_fake

@@ -32,4 +32,8 @@ bool mx256_supported(int M, int N, int K, long long lda, long long ldsa, long lo
                      const void* SW, const Gemm256Epi& ep, int out_mode, const void* out_scales);
 int mx256_launch(const void* A, const void* SA, long long lda, long long ldsa, long long rpb, long long a_bs,
                  long long s_bs, const void* W, const void* SW, long long ldw, long long ldsw, int M, int N, int K,
-                 const Gemm256Epi& ep, int out_mode, void* out_scales, long long ldso, hipStream_t s);
+                 const Gemm256Epi& ep, int out_mode, void* out_scales, long long ldso, hipStream_t s,
+                 float* ws = nullptr, long long ws_floats = 0);
+// fp32 workspace (floats) mx256_launch uses for its split-K tail at this
+// shape (0: none; the launch runs whole tiles when ws is absent or smaller)
+long long mx256_split_floats(int M, int N, int K, int out_mode);

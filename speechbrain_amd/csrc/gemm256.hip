@@ -128,7 +128,25 @@ struct G256 {
   int out_mode;               // 0 fp32, 1 bf16, 2 MXFP8 (MX only)
   uint8_t* out_scales;
   long long ldso;
+  // split-K tail (launch_t): ksplit 2 = workgroups 2s and 2s + 1 take the two
+  // K halves of tile tile_base + s and store raw fp32 partials to part
+  // (tile-local 256 x 256, one per workgroup); 0 = whole tiles
+  int ksplit, tile_base;
+  float* part;
 };
+
+// tile index (the launch order) -> (row tile, column tile): bijective XCD
+// remap (workgroup i runs on XCD i % 8; each XCD walks a contiguous range),
+// then row panels in groups of 8 walked column by column
+__device__ __forceinline__ void tile_of(int orig, int ntn, int ntm, int& tm, int& tn) {
+  const int nwg = ntn * ntm, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  constexpr int GM = 8;  // row panels per group; a group is walked column by column
+  const int gsz = GM * ntn, grp = wg / gsz, first = grp * GM, gm = min(GM, ntm - first);
+  const int in = wg - grp * gsz;
+  tm = first + in % gm;
+  tn = in / gm;
+}
 
 template <bool MX, int ACT, int OUT>
 __global__ void __launch_bounds__(NT, 1) gemm256_kernel(G256 p) {
@@ -137,16 +155,15 @@ __global__ void __launch_bounds__(NT, 1) gemm256_kernel(G256 p) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 2, wn = w & 3;
 
-  // ---- tile of this workgroup
-  const int ntn = p.N >> 8, ntm = (p.M + 255) >> 8, nwg = ntn * ntm;
-  const int orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  constexpr int GM = 8;  // row panels per group; a group is walked column by column
-  const int gsz = GM * ntn, grp = wg / gsz, first = grp * GM, gm = min(GM, ntm - first);
-  const int in = wg - grp * gsz;
-  const int tm = first + in % gm, tn = in / gm;
+  // ---- tile of this workgroup (and, split, its K half)
+  const bool split = OUT == 0 && p.ksplit == 2;
+  const int half = split ? (int)(blockIdx.x & 1) : 0;
+  int tm, tn;
+  tile_of(split ? p.tile_base + (int)(blockIdx.x >> 1) : (int)blockIdx.x, p.N >> 8, (p.M + 255) >> 8, tm, tn);
   const int m0 = tm << 8, n0 = tn << 8;
-  const int nk = MX ? p.K >> 7 : p.K >> 6;
+  int nk = MX ? p.K >> 7 : p.K >> 6;
+  const int kt0 = half ? nk >> 1 : 0;  // first K-tile (every K-tile is 128 B of a row)
+  if (split) nk = half ? nk - (nk >> 1) : nk >> 1;
 
   // ---- DMA sources: half-tile piece j = 2w + i covers rows 8j .. 8j+7 of the
   // half; lane -> row 8j + (lane >> 3), physical chunk lane & 7 holding logical
@@ -160,8 +177,8 @@ __global__ void __launch_bounds__(NT, 1) gemm256_kernel(G256 p) {
       const int r = h * 128 + (2 * w + i) * 8 + (lane >> 3);
       const int pch = (lane & 7) ^ ((r >> 1) & 7);
       const long long m = min(m0 + r, p.M - 1), b = m / p.rpb;
-      asrc[h][i] = p.A + b * p.a_bs + (m - b * p.rpb) * p.lda + pch * 16;
-      wsrc[h][i] = p.W + (long long)(n0 + r) * p.ldw + pch * 16;
+      asrc[h][i] = p.A + b * p.a_bs + (m - b * p.rpb) * p.lda + pch * 16 + kt0 * 128;
+      wsrc[h][i] = p.W + (long long)(n0 + r) * p.ldw + pch * 16 + kt0 * 128;
     }
   // MXFP8 scale pieces: the 512 scale dwords of a K-tile (A rows 0-255, W
   // rows 0-255) are 8 pieces of 64 rows, one per wave: wave w moves A rows
@@ -175,6 +192,7 @@ __global__ void __launch_bounds__(NT, 1) gemm256_kernel(G256 p) {
     } else {
       ssrc = p.SW + (long long)(n0 + r) * p.ldsw;
     }
+    ssrc += kt0 * 4;
   }
   const uint32_t lds0 = lds_u32(smem);
   auto issue_a1 = [&](int kt, int buf, int h) __attribute__((always_inline)) {
@@ -428,6 +446,9 @@ __global__ void __launch_bounds__(NT, 1) gemm256_kernel(G256 p) {
             pk.x = pack_bf16x2(v0, v1);
             pk.y = pack_bf16x2(v2, v3);
             *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.ep.out) + (long long)row * p.ep.ldc + gcol) = pk;
+          } else if (split) {  // the partial, tile-local (the launch passes no bias / residual / mask, alpha 1)
+            *reinterpret_cast<float4*>(p.part + (long long)blockIdx.x * 65536 + (row - m0) * 256 + (gcol - n0)) =
+                make_float4(v0, v1, v2, v3);
           } else {
             *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.ep.out) + (long long)row * p.ep.ldc + gcol) =
                 make_float4(v0, v1, v2, v3);
@@ -439,26 +460,127 @@ __global__ void __launch_bounds__(NT, 1) gemm256_kernel(G256 p) {
   }
 }
 
+// Split-K tail, second step: out = epilogue(P0 + P1) for tile tile_base + s,
+// P0 / P1 the two K halves' fp32 partials (one add, so the sum does not
+// depend on which half finished first).  One workgroup per (tile, 16-row
+// band), a float4 column quad per thread; the epilogue is gemm256_kernel's
+// (bias, activation, row mask, alpha, fp32 residual, fp32 out).
+template <int ACT>
+__global__ void __launch_bounds__(256) splitk_epi_kernel(G256 p) {
+  const int s = blockIdx.x >> 4, band = blockIdx.x & 15;
+  int tm, tn;
+  tile_of(p.tile_base + s, p.N >> 8, (p.M + 255) >> 8, tm, tn);
+  const int m0 = tm << 8, n0 = tn << 8;
+  const int c = 4 * (threadIdx.x & 63), gcol = n0 + c;
+  float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (p.ep.bias) bv = *reinterpret_cast<const float4*>(p.ep.bias + gcol);
+  const float* p0 = p.part + (long long)(2 * s) * 65536;
+  const float* p1 = p0 + 65536;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rl = band * 16 + 4 * i + (threadIdx.x >> 6), row = m0 + rl;
+    if (row >= p.M) continue;  // (not stored by the partial launch either)
+    const float4 x0 = *reinterpret_cast<const float4*>(p0 + rl * 256 + c);
+    const float4 x1 = *reinterpret_cast<const float4*>(p1 + rl * 256 + c);
+    const float4 a = make_float4(x0.x + x1.x, x0.y + x1.y, x0.z + x1.z, x0.w + x1.w);
+    const float sc = (p.ep.rowmask && p.ep.rowmask[row]) ? 0.f : p.ep.alpha;
+    float v0, v1, v2, v3;
+    if constexpr (ACT == G_GELU) {
+      const f2v g0 = gelu_fast2(f2v{a.x + bv.x, a.y + bv.y}) * sc, g1 = gelu_fast2(f2v{a.z + bv.z, a.w + bv.w}) * sc;
+      v0 = g0[0]; v1 = g0[1]; v2 = g1[0]; v3 = g1[1];
+    } else {
+      v0 = act_f<ACT>(a.x + bv.x, p.ep.slope) * sc; v1 = act_f<ACT>(a.y + bv.y, p.ep.slope) * sc;
+      v2 = act_f<ACT>(a.z + bv.z, p.ep.slope) * sc; v3 = act_f<ACT>(a.w + bv.w, p.ep.slope) * sc;
+    }
+    if (p.ep.res) {
+      const float4 r = *reinterpret_cast<const float4*>(p.ep.res + (long long)row * p.ep.ldr + gcol);
+      v0 += r.x;
+      v1 += r.y;
+      v2 += r.z;
+      v3 += r.w;
+    }
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.ep.out) + (long long)row * p.ep.ldc + gcol) =
+        make_float4(v0, v1, v2, v3);
+  }
+}
+
+// compute units of the current device (cached; the split-K tail rule)
+int cu_count() {
+  static int n = 0;
+  if (n <= 0) {
+    int d = 0, c = 0;
+    if (hipGetDevice(&d) == hipSuccess && hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess &&
+        c > 0)
+      n = c;
+    else
+      return 256;
+  }
+  return n;
+}
+
+// Split-K tail (MXFP8, fp32 out): with one 256 x 256 workgroup per CU, the
+// tiles past the last full round run as a partial round (config 5's N =
+// 1024 projections: 376 tiles on 256 CUs, 120 in the second round).  When
+// that tail fills at most half the CUs and K has >= 16 K-tiles, each tail
+// tile runs as two workgroups over the K halves (a full round of half-length
+// tiles) plus splitk_epi_kernel.  Returns the tail tile count, 0 = no split.
+int split_tail(int M, int N, int K) {
+  if (M <= 0 || N <= 0 || (N & 255) || (K & 127)) return 0;
+  const int nt = (N >> 8) * ((M + 255) >> 8), cus = cu_count(), tail = nt % cus;
+  return (nt > cus && tail > 0 && 2 * tail <= cus && (K >> 7) >= 16) ? tail : 0;
+}
+
 template <bool MX, int ACT, int OUT>
-int launch_t(const G256& p, hipStream_t s) {
+int launch_t(const G256& p, hipStream_t s, float* ws, long long ws_floats) {
   // > 64 KB of dynamic LDS: opted in per device
   if (hipError_t e = sbk::lds_optin(reinterpret_cast<const void*>(&gemm256_kernel<MX, ACT, OUT>), lds_bytes<MX>()))
     return (int)e;
   const int grid = (p.N >> 8) * ((p.M + 255) >> 8);
-  hipLaunchKernelGGL((gemm256_kernel<MX, ACT, OUT>), dim3(grid), dim3(NT), lds_bytes<MX>(), s, p);
+  if constexpr (MX && OUT == 0) {
+    const int tail = ws ? split_tail(p.M, p.N, p.K) : 0;
+    if (tail && ws_floats >= 2LL * tail * 65536) {
+      if (hipError_t e = sbk::lds_optin(reinterpret_cast<const void*>(&gemm256_kernel<true, G_NONE, 0>),
+                                        lds_bytes<true>()))
+        return (int)e;
+      G256 q = p;  // whole tiles: the first grid - tail of the launch order
+      q.ksplit = 0;
+      hipLaunchKernelGGL((gemm256_kernel<MX, ACT, OUT>), dim3(grid - tail), dim3(NT), lds_bytes<MX>(), s, q);
+      SBK_CHECK_LAUNCH();
+      G256 h = p;  // the tail's K halves: raw partials
+      h.ep.bias = nullptr;
+      h.ep.res = nullptr;
+      h.ep.rowmask = nullptr;
+      h.ep.alpha = 1.f;
+      h.ep.act = G_NONE;
+      h.ksplit = 2;
+      h.tile_base = grid - tail;
+      h.part = ws;
+      hipLaunchKernelGGL((gemm256_kernel<true, G_NONE, 0>), dim3(2 * tail), dim3(NT), lds_bytes<true>(), s, h);
+      SBK_CHECK_LAUNCH();
+      G256 f = p;  // the tail's epilogue
+      f.tile_base = grid - tail;
+      f.part = ws;
+      hipLaunchKernelGGL((splitk_epi_kernel<ACT>), dim3(16 * tail), dim3(256), 0, s, f);
+      SBK_CHECK_LAUNCH();
+      return 0;
+    }
+  }
+  G256 q = p;
+  q.ksplit = 0;
+  hipLaunchKernelGGL((gemm256_kernel<MX, ACT, OUT>), dim3(grid), dim3(NT), lds_bytes<MX>(), s, q);
   SBK_CHECK_LAUNCH();
   return 0;
 }
 
 template <bool MX, int OUT>
-int launch_o(const G256& p, hipStream_t s) {
+int launch_o(const G256& p, hipStream_t s, float* ws = nullptr, long long ws_floats = 0) {
   switch (p.ep.act) {
-    case G_NONE: return launch_t<MX, G_NONE, OUT>(p, s);
+    case G_NONE: return launch_t<MX, G_NONE, OUT>(p, s, ws, ws_floats);
     case G_SWISH:
       if constexpr (MX) return SBK_ERR_ARG;
-      else return launch_t<MX, G_SWISH, OUT>(p, s);
-    case G_LRELU: return launch_t<MX, G_LRELU, OUT>(p, s);
-    case G_GELU: return launch_t<MX, G_GELU, OUT>(p, s);
+      else return launch_t<MX, G_SWISH, OUT>(p, s, ws, ws_floats);
+    case G_LRELU: return launch_t<MX, G_LRELU, OUT>(p, s, ws, ws_floats);
+    case G_GELU: return launch_t<MX, G_GELU, OUT>(p, s, ws, ws_floats);
     default: return SBK_ERR_ARG;
   }
 }
@@ -500,16 +622,21 @@ bool mx256_supported(int M, int N, int K, long long lda, long long ldsa, long lo
   return epi_ok(ep);
 }
 
+long long mx256_split_floats(int M, int N, int K, int out_mode) {
+  return out_mode == 0 ? 2LL * split_tail(M, N, K) * 65536 : 0;
+}
+
 int mx256_launch(const void* A, const void* SA, long long lda, long long ldsa, long long rpb, long long a_bs,
                  long long s_bs, const void* W, const void* SW, long long ldw, long long ldsw, int M, int N, int K,
-                 const Gemm256Epi& ep, int out_mode, void* out_scales, long long ldso, hipStream_t s) {
+                 const Gemm256Epi& ep, int out_mode, void* out_scales, long long ldso, hipStream_t s, float* ws,
+                 long long ws_floats) {
   if (!mx256_supported(M, N, K, lda, ldsa, rpb, a_bs, s_bs, ldw, ldsw, A, SA, W, SW, ep, out_mode, out_scales))
     return SBK_ERR_ARG;
   G256 p{reinterpret_cast<const uint8_t*>(A), reinterpret_cast<const uint8_t*>(SA), lda, ldsa, rpb, a_bs, s_bs,
          reinterpret_cast<const uint8_t*>(W), reinterpret_cast<const uint8_t*>(SW), ldw, ldsw, M, N, K, ep,
          out_mode, reinterpret_cast<uint8_t*>(out_scales), ldso};
   switch (out_mode) {
-    case 0: return launch_o<true, 0>(p, s);
+    case 0: return launch_o<true, 0>(p, s, ws, ws_floats);
     case 1: return launch_o<true, 1>(p, s);
     default: return launch_o<true, 2>(p, s);
   }

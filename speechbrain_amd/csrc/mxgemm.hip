@@ -473,11 +473,11 @@ int launch_act(const MxArgs& p, hipStream_t s) {
 // aligned scale rows (ldsa, s_bs, ldsw % 4 == 0).  rpb = rows per batch for
 // the conv addressing (rpb >= M for a plain GEMM).  Row m < M only: rows of
 // the last tile beyond M are loaded from row M-1 and not stored.
-SBK_API int sbk_mx_gemm(const uint8_t* A, const uint8_t* SA, long long lda, long long ldsa, long long rpb,
+static int mx_gemm_impl(const uint8_t* A, const uint8_t* SA, long long lda, long long ldsa, long long rpb,
                         long long a_bs, long long s_bs, const uint8_t* W, const uint8_t* SW, long long ldw,
                         long long ldsw, int M, int N, int K, const float* bias, int act, float alpha, const float* res,
                         long long ldr, void* out, long long ldc, int out_mode, uint8_t* out_scales, long long ldso,
-                        void* stream) {
+                        float* ws, long long ws_floats, void* stream) {
   if (M <= 0 || N <= 0 || K <= 0 || (K % BK) || (N % BN) || rpb <= 0) return SBK_ERR_ARG;
   if ((lda | a_bs | ldw) & 15) return SBK_ERR_ARG;
   if ((ldsa | s_bs | ldsw) & 3) return SBK_ERR_ARG;
@@ -496,11 +496,38 @@ SBK_API int sbk_mx_gemm(const uint8_t* A, const uint8_t* SA, long long lda, long
     const Gemm256Epi ep{bias, act, 0.f, res, (int)ldr, alpha, nullptr, out, (int)ldc, out_mode == 1};
     if (mx256_supported(M, N, K, lda, ldsa, rpb, a_bs, s_bs, ldw, ldsw, A, SA, W, SW, ep, out_mode, out_scales))
       return mx256_launch(A, SA, lda, ldsa, rpb, a_bs, s_bs, W, SW, ldw, ldsw, M, N, K, ep, out_mode, out_scales, ldso,
-                          s);
+                          s, ws, ws_floats);
   }
   if (act == 4) return launch_act<4>(p, s);
   if (act == 3) return launch_act<3>(p, s);
   return launch_act<0>(p, s);
+}
+
+SBK_API int sbk_mx_gemm(const uint8_t* A, const uint8_t* SA, long long lda, long long ldsa, long long rpb,
+                        long long a_bs, long long s_bs, const uint8_t* W, const uint8_t* SW, long long ldw,
+                        long long ldsw, int M, int N, int K, const float* bias, int act, float alpha, const float* res,
+                        long long ldr, void* out, long long ldc, int out_mode, uint8_t* out_scales, long long ldso,
+                        void* stream) {
+  return mx_gemm_impl(A, SA, lda, ldsa, rpb, a_bs, s_bs, W, SW, ldw, ldsw, M, N, K, bias, act, alpha, res, ldr, out,
+                      ldc, out_mode, out_scales, ldso, nullptr, 0, stream);
+}
+
+// sbk_mx_gemm with an fp32 workspace for the 256-tile kernel's split-K tail
+// (gemm256.hip split_tail): ws_floats >= sbk_mx_gemm_ws_floats(M, N, K,
+// out_mode) enables it, a smaller or null ws runs whole tiles
+SBK_API long long sbk_mx_gemm_ws_floats(int M, int N, int K, int out_mode) {
+  if ((long long)((M + 255) / 256) * (N / 256) < 180) return 0;  // sbk_mx_gemm's 256-tile threshold
+  return mx256_split_floats(M, N, K, out_mode);
+}
+
+SBK_API int sbk_mx_gemm_ws(const uint8_t* A, const uint8_t* SA, long long lda, long long ldsa, long long rpb,
+                           long long a_bs, long long s_bs, const uint8_t* W, const uint8_t* SW, long long ldw,
+                           long long ldsw, int M, int N, int K, const float* bias, int act, float alpha,
+                           const float* res, long long ldr, void* out, long long ldc, int out_mode,
+                           uint8_t* out_scales, long long ldso, float* ws, long long ws_floats, void* stream) {
+  if (ws_floats < 0 || (ws_floats > 0 && (!ws || (reinterpret_cast<uintptr_t>(ws) & 15)))) return SBK_ERR_ARG;
+  return mx_gemm_impl(A, SA, lda, ldsa, rpb, a_bs, s_bs, W, SW, ldw, ldsw, M, N, K, bias, act, alpha, res, ldr, out,
+                      ldc, out_mode, out_scales, ldso, ws, ws_floats, stream);
 }
 
 // MXFP8 quantisation of a row-major fp32 / bf16 matrix (M, K), K % 32 == 0:

@@ -97,3 +97,48 @@ def test_mx256_vs_dequantised_and_small_tile(dev, M, N, K):
             assert float(((d0 - d1).abs() / d0.abs().clamp(min=1.0)).max()) <= tol, mode
         else:
             assert torch.equal(o0, o1) and torch.equal(s0, s1), mode
+
+
+@pytest.mark.parametrize("act,with_res", [(0, True), (4, False)])
+def test_mx256_split_k_tail(dev, act, with_res):
+    """sbk_mx_gemm_ws: the tiles past the last full round of 256-tile
+    workgroups run as two K halves + an epilogue pass (gemm256.hip
+    split_tail).  At (M, N, K) = (17820, 1024, 2048) — 70 row tiles x 4 = 280
+    tiles, a ragged last row tile — the result equals the unsplit launch's up
+    to the fp32 order of the halves' sum, and the workspace size is the rule's
+    (2 x tail x 256 x 256 floats, fp32 out only)."""
+    from speechbrain_amd import _w2v
+    from speechbrain_amd._lib import lib, ptr, stream_of
+    L = lib()
+    M, N, K = 17820, 1024, 2048
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    nt = ((M + 255) // 256) * (N // 256)
+    tail = nt % cus
+    if not (nt > cus and 0 < tail and 2 * tail <= cus):
+        pytest.skip(f"{cus} CUs: no split tail at this shape")
+    nws = int(L.sbk_mx_gemm_ws_floats(M, N, K, 0))
+    assert nws == 2 * tail * 65536, (nws, tail)
+    assert int(L.sbk_mx_gemm_ws_floats(M, N, K, 1)) == 0 and int(L.sbk_mx_gemm_ws_floats(M, N, 1024, 0)) == 0
+    torch.manual_seed(act + 7)
+    a = _w2v.mx_quant(_rnd(dev, M, K))
+    w = _w2v.mx_quant(_rnd(dev, N, K))
+    bias = _rnd(dev, N)
+    res = _rnd(dev, M, N) if with_res else None
+    o0, _ = _mx_call(L.sbk_mx_gemm, a, w, M, N, K, 0, bias, act, res)
+    ws = torch.full((nws,), float("nan"), device=dev)
+    o1 = torch.full((M, N), float("nan"), device=dev)
+    rc = L.sbk_mx_gemm_ws(ptr(a.q), ptr(a.s), a.q.stride(0), a.s.stride(0), M, 0, 0, ptr(w.q), ptr(w.s),
+                          w.q.stride(0), w.s.stride(0), M, N, K, ptr(bias), act, 1.0, ptr(res),
+                          res.stride(0) if res is not None else 0, ptr(o1), o1.stride(0), 0, None, 0, ptr(ws), nws,
+                          stream_of(a.q))
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(o1).all())
+    err = float(((o1 - o0).abs() / o0.abs().clamp(min=1.0)).max())
+    assert err < 1e-5, err
+    # whole tiles are the unsplit kernel's bit for bit: at most the tail's
+    # tiles (tail x 65536 values) differ
+    assert int((o1 != o0).sum()) <= tail * 65536
+    # the op path (_w2v.mx_gemm's custom op) takes the workspace entry
+    o2, _ = _w2v._mx_gemm_op(a.q, a.s, M, K, a.q.stride(0), a.s.stride(0), M, 0, 0, w.q, w.s, bias, act, 1.0, res, 0)
+    assert torch.equal(o2, o1)
