@@ -142,3 +142,34 @@ def test_mx256_split_k_tail(dev, act, with_res):
     # the op path (_w2v.mx_gemm's custom op) takes the workspace entry
     o2, _ = _w2v._mx_gemm_op(a.q, a.s, M, K, a.q.stride(0), a.s.stride(0), M, 0, 0, w.q, w.s, bias, act, 1.0, res, 0)
     assert torch.equal(o2, o1)
+
+
+def test_mx256_split_k_tail_graph_replay(dev):
+    """The split-K tail inside a captured HIP graph (the C5 bench's mode):
+    the workspace comes from the graph's pool at capture, and a replay on new
+    inputs equals the eager call on them bit for bit."""
+    from speechbrain_amd import _w2v
+    from speechbrain_amd._lib import lib
+    M, N, K = 17820, 1024, 2048
+    if not int(lib().sbk_mx_gemm_ws_floats(M, N, K, 0)):
+        pytest.skip("no split tail at this shape on this device")
+    torch.manual_seed(11)
+    x = _rnd(dev, M, K)
+    w = _w2v.mx_quant(_rnd(dev, N, K))
+    bias, res = _rnd(dev, N), _rnd(dev, M, N)
+
+    def step():
+        return _w2v.mx_gemm(_w2v.mx_quant(x), w, bias=bias, res=res)
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step()  # warm-up outside the capture
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = step()
+    x.copy_(_rnd(dev, M, K))
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, step())
