@@ -99,18 +99,19 @@ def test_mx256_vs_dequantised_and_small_tile(dev, M, N, K):
             assert torch.equal(o0, o1) and torch.equal(s0, s1), mode
 
 
-@pytest.mark.parametrize("act,with_res", [(0, True), (4, False)])
-def test_mx256_split_k_tail(dev, act, with_res):
+@pytest.mark.parametrize("act,with_res,K", [(0, True, 2048), (4, False, 2048), (3, True, 2176)])
+def test_mx256_split_k_tail(dev, act, with_res, K):
     """sbk_mx_gemm_ws: the tiles past the last full round of 256-tile
     workgroups run as two K halves + an epilogue pass (gemm256.hip
-    split_tail).  At (M, N, K) = (17820, 1024, 2048) — 70 row tiles x 4 = 280
-    tiles, a ragged last row tile — the result equals the unsplit launch's up
-    to the fp32 order of the halves' sum, and the workspace size is the rule's
+    split_tail).  At (M, N) = (17820, 1024) — 70 row tiles x 4 = 280
+    tiles, a ragged last row tile; K = 2176 splits 17 K-tiles as 8 + 9; no
+    activation, GELU, ReLU — the result equals the unsplit launch's up to the
+    fp32 order of the halves' sum, and the workspace size is the rule's
     (2 x tail x 256 x 256 floats, fp32 out only)."""
     from speechbrain_amd import _w2v
     from speechbrain_amd._lib import lib, ptr, stream_of
     L = lib()
-    M, N, K = 17820, 1024, 2048
+    M, N = 17820, 1024
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
     nt = ((M + 255) // 256) * (N // 256)
     tail = nt % cus
